@@ -1,0 +1,229 @@
+/*
+ * wgraph.h — C ABI of the MI355X commit-graph render-prep engine.
+ *
+ * This is the drop-in boundary for whisper-git's `GraphLayout`
+ * (/root/reference/src/commit_graph.rs:240-472) and the per-row paint
+ * emission behind it (`graph_cell`, commit_graph.rs:803-908).  Each entry
+ * point names the reference item it replaces.  Plain C: pointers + sizes,
+ * int status codes (0 = OK, negative = error), no exceptions across the ABI.
+ *
+ * Threading: one wg_ctx per calling thread; a context is not re-entrant.
+ * Every call is synchronous with respect to the host unless the caller has
+ * installed its own stream with wg_set_stream(), in which case device-resident
+ * outputs are ordered on that stream and host copies synchronise it.
+ *
+ * Ownership: the library owns every device output buffer.  Device pointers
+ * returned by wg_device_views() stay valid until the next wg_layout_build(),
+ * wg_row_geometry(), wg_emit_vertices() or wg_destroy() on the same context.
+ */
+#ifndef WGRAPH_H
+#define WGRAPH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WGRAPH_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define WG_OK             0
+#define WG_E_INVALID     -1  /* bad argument (null pointer, size mismatch)        */
+#define WG_E_HIP         -2  /* HIP runtime error; see wg_last_error()             */
+#define WG_E_NOMEM       -3  /* device allocation failed                           */
+#define WG_E_STATE       -4  /* call order: e.g. geometry before a layout build    */
+#define WG_E_UNSUPPORTED -5  /* input outside the engine's limits (see message)    */
+#define WG_E_NODEVICE    -6  /* no gfx950 device / HIP code object not loadable    */
+
+/* Opaque engine context (one per calling thread). */
+typedef struct wg_ctx wg_ctx;
+
+/* ---- residency of caller buffers --------------------------------------- */
+#define WG_HOST   0
+#define WG_DEVICE 1
+
+/* ---- frozen constants (commit_graph.rs:30-54, 106, 775-780) ------------- */
+#define WG_ROW_HEIGHT          28.0f   /* ROW_HEIGHT          :30  */
+#define WG_LANE_W              24.0f   /* LANE_W              :33  */
+#define WG_LANE_COUNT_VISUAL   6       /* LANE_COUNT_VISUAL   :37  */
+#define WG_NODE_Y              14.0f   /* NODE_Y              :43  */
+#define WG_MAX_EXTRA_HEIGHT    28.0f   /* MAX_EXTRA_HEIGHT    :47  */
+#define WG_TIME_BASE_SECONDS   7200.0  /* TIME_BASE_SECONDS   :51  */
+#define WG_TIME_MAX_DELTA      2592000.0 /* TIME_MAX_DELTA_SECONDS :54 */
+#define WG_PILLS_BAND_HEIGHT   30.0f   /* PILLS_BAND_HEIGHT   :106 */
+#define WG_LINE_WIDTH          2.0f    /* LINE_WIDTH          :775 */
+#define WG_NODE_RADIUS         5.0f    /* NODE_RADIUS         :778 */
+#define WG_SELECTED_RING_WIDTH 2.5f    /* SELECTED_RING_WIDTH :780 */
+
+/* Colour indices.  The reference carries aetna theme tokens; the engine
+ * carries the palette index and resolves RGBA from a caller palette at
+ * vertex-emission time.  0..5 = LANE_COLORS[lane % 6] (:59-66),
+ * 6 = ORPHAN_COLOR (:70), 7 = tokens::FOREGROUND (selected ring, :898). */
+#define WG_COLOR_ORPHAN     6
+#define WG_COLOR_FOREGROUND 7
+#define WG_PALETTE_SIZE     8
+
+/* commit flags (CommitInfo::is_orphaned / is_synthetic, git/mod.rs:256-269) */
+#define WG_FLAG_ORPHAN    0x1u
+#define WG_FLAG_SYNTHETIC 0x2u
+
+/* ---- input: the commit list as structure-of-arrays ---------------------
+ * Replaces `&[CommitInfo]` (git/mod.rs:246-270) as consumed by
+ * GraphLayout::build.  Row order is the caller's (libgit2 revwalk
+ * TOPOLOGICAL|TIME, newest first; git/mod.rs:570-596, 761-775).        */
+typedef struct wg_commits {
+    uint64_t        n_commits;    /* N rows                                   */
+    uint64_t        n_parents;    /* E = parent_off[N]                        */
+    const uint8_t  *oid;          /* [N][20] commit ids (CommitInfo::id)      */
+    const int64_t  *time;         /* [N] seconds (CommitInfo::time)           */
+    const uint32_t *parent_off;   /* [N+1] CSR offsets into parent_oid        */
+    const uint8_t  *parent_oid;   /* [E][20] parent ids, in parent order      */
+    const uint8_t  *flags;        /* [N] WG_FLAG_*; may be NULL (all zero)    */
+    int32_t         residency;    /* WG_HOST or WG_DEVICE for all arrays      */
+    int32_t         reserved;
+} wg_commits;
+
+/* GraphEdge (commit_graph.rs:173-180); colour = palette index */
+typedef struct wg_edge {
+    uint32_t child_row;
+    uint32_t child_lane;
+    uint32_t parent_row;
+    uint32_t parent_lane;
+    uint32_t color;
+} wg_edge;
+
+/* Summary of the last wg_layout_build (pub fields of GraphLayout, :244-257) */
+typedef struct wg_layout_summary {
+    uint64_t n_rows;
+    uint64_t n_edges;
+    uint32_t max_lane;        /* GraphLayout::max_lane                        */
+    uint32_t n_slots;         /* length reached by active_lanes (diagnostic)  */
+    float    graph_width;     /* GraphLayout::graph_width                     */
+    uint32_t lane_path;       /* 0 = event-compressed fast path, 1 = general  */
+} wg_layout_summary;
+
+/* ---- row geometry layout (RowGeometry, commit_graph.rs:208-233) --------
+ * Per-row CSR.  vert[] holds, per row and in this order, the
+ * full_verticals, top_half_verticals and bottom_half_verticals entries
+ * (the z-order graph_cell paints them in, :827-838); each entry packs
+ *   bits  0..23 lane, bits 24..25 kind (WG_VERT_*), bits 28..31 colour.
+ * curve[] holds CurveSegment records (:186-193) as 8 floats
+ *   {p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y}, x in lane units,
+ *   y row-local pixels; curve_color[] the matching palette indices.    */
+#define WG_VERT_FULL   0u
+#define WG_VERT_TOP    1u
+#define WG_VERT_BOTTOM 2u
+#define WG_VERT_LANE(v)  ((v) & 0xFFFFFFu)
+#define WG_VERT_KIND(v)  (((v) >> 24) & 0x3u)
+#define WG_VERT_COLOR(v) (((v) >> 28) & 0xFu)
+
+typedef struct wg_curve { float p[8]; } wg_curve;
+
+typedef struct wg_geometry_summary {
+    uint64_t n_rows;
+    uint64_t n_vert;          /* total vertical entries                       */
+    uint64_t n_curve;         /* total curve segments                         */
+    float    total_height;    /* row_top_y[N] (content height)                */
+    uint32_t scan_path;       /* 0 = transducer scan, 1 = serial fallback     */
+} wg_geometry_summary;
+
+/* Host-side destination for wg_copy_geometry (any pointer may be NULL). */
+typedef struct wg_geometry_host {
+    float    *height;         /* [N]   RowGeometry::height                    */
+    float    *node_y;         /* [N]   RowGeometry::node_y                    */
+    float    *row_top;        /* [N+1] row_top_y (:329-335 / :374-381)        */
+    uint32_t *vert_off;       /* [N+1]                                        */
+    uint32_t *vert;           /* [n_vert]                                     */
+    uint32_t *curve_off;      /* [N+1]                                        */
+    wg_curve *curve;          /* [n_curve]                                    */
+    uint8_t  *curve_color;    /* [n_curve]                                    */
+} wg_geometry_host;
+
+/* ---- vertex emission (frozen spec WG-TESS-1) -------------
+ * SplineVertex (docs/render_engine.md:165-170): 24 bytes.                */
+typedef struct wg_vertex { float x, y, r, g, b, a; } wg_vertex;
+
+#define WG_TESS_CURVE_SEGMENTS 16   /* docs/render_engine.md:157          */
+#define WG_TESS_NODE_SEGMENTS  24   /* README.md:22                       */
+#define WG_VTX_PER_VERTICAL    6
+#define WG_VTX_PER_CURVE       (6 * WG_TESS_CURVE_SEGMENTS)   /* 96  */
+#define WG_VTX_PER_NODE        (3 * WG_TESS_NODE_SEGMENTS)    /* 72  */
+#define WG_VTX_PER_RING        (6 * WG_TESS_NODE_SEGMENTS)    /* 144 */
+
+typedef struct wg_vertex_summary {
+    uint64_t row_begin, row_end;
+    uint64_t n_vertices;
+    uint64_t checksum;        /* order-sensitive 64-bit hash of the buffer   */
+} wg_vertex_summary;
+
+/* Device-resident views (valid until the next producing call). */
+typedef struct wg_device_views {
+    const uint32_t *lane;       /* [N] lane per row (layouts.get(id).lane)    */
+    const uint8_t  *color;      /* [N] palette index per row                  */
+    const wg_edge  *edges;      /* [n_edges]                                  */
+    const float    *height;     /* [N]                                        */
+    const float    *node_y;     /* [N]                                        */
+    const float    *row_top;    /* [N+1]                                      */
+    const uint32_t *vert_off;   /* [N+1]                                      */
+    const uint32_t *vert;
+    const uint32_t *curve_off;  /* [N+1]                                      */
+    const wg_curve *curve;
+    const uint8_t  *curve_color;
+    const uint64_t *vtx_off;    /* [row_end-row_begin+1] vertex offsets       */
+    const wg_vertex *vertices;
+} wg_device_views;
+
+/* ---- lifecycle ----------------------------------------------------------- */
+/* GraphLayout::new (:261).  device_ordinal < 0 selects the current device. */
+wg_ctx     *wg_create(int device_ordinal);
+void        wg_destroy(wg_ctx *ctx);
+const char *wg_last_error(const wg_ctx *ctx);
+int         wg_abi_version(void);
+/* Install a caller-owned hipStream_t (NULL = library-owned stream). */
+int         wg_set_stream(wg_ctx *ctx, void *hip_stream);
+int         wg_synchronize(wg_ctx *ctx);
+
+/* ---- layout (GraphLayout::build, :265-355) -------------------------------
+ * Lane assignment, colours, edge list, default row geometry (bands = 0).  */
+int wg_layout_build(wg_ctx *ctx, const wg_commits *commits);
+int wg_layout_summary_get(wg_ctx *ctx, wg_layout_summary *out);
+/* layouts: lane/colour per row = GraphLayout::get(&commits[row].id) (:357) */
+int wg_copy_lanes(wg_ctx *ctx, uint32_t *lane, uint8_t *color);
+/* GraphLayout::edges (:248) */
+int wg_copy_edges(wg_ctx *ctx, wg_edge *edges);
+
+/* compute_row_heights (:486-507) on the commits of the last build. */
+int wg_copy_row_heights(wg_ctx *ctx, float *heights);
+
+/* ---- per-frame geometry (row_geometry_with_bands, :367-399) --------------
+ * band == NULL reproduces GraphLayout::row_geometry from build (:322-346);
+ * otherwise band[N] (residency as given) is the per-row pills band.      */
+int wg_row_geometry(wg_ctx *ctx, const float *band, int32_t band_residency);
+int wg_geometry_summary_get(wg_ctx *ctx, wg_geometry_summary *out);
+int wg_copy_geometry(wg_ctx *ctx, const wg_geometry_host *dst);
+
+/* ---- vertex emission (graph_cell, :803-908 + WG-TESS-1) -----------------
+ * Rows [row_begin, row_end) of the current geometry; selected_row < 0 for
+ * none.  palette = WG_PALETTE_SIZE RGBA float quadruples (host memory).  */
+int wg_emit_vertices(wg_ctx *ctx, uint64_t row_begin, uint64_t row_end,
+                     int64_t selected_row, const float *palette);
+int wg_vertex_summary_get(wg_ctx *ctx, wg_vertex_summary *out);
+/* Copy vertices [first, first+count) of the last emission to host memory. */
+int wg_copy_vertices(wg_ctx *ctx, uint64_t first, uint64_t count, wg_vertex *dst);
+/* Per-row vertex offsets (row_end-row_begin+1 entries) to host memory. */
+int wg_copy_vertex_offsets(wg_ctx *ctx, uint64_t *dst);
+
+int wg_device_views_get(wg_ctx *ctx, wg_device_views *out);
+
+/* ---- timing (HIP events on the context's stream) ------------------------ */
+#define WG_STAGE_MAX 32
+int wg_enable_timing(wg_ctx *ctx, int on);
+/* Per-stage milliseconds of the last producing calls; names[i] static. */
+int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WGRAPH_H */

@@ -1,0 +1,163 @@
+"""ctypes binding of the C oracle (oracle/liboracle.so).  TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / CPU baseline — never as the engine.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(_HERE), "whisper-git_amd"))
+from wgraph import abi  # noqa: E402  (types only)
+
+
+class _Geom(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("n_vert", ctypes.c_uint64), ("n_curve", ctypes.c_uint64),
+                ("height", ctypes.c_void_p), ("node_y", ctypes.c_void_p), ("row_top", ctypes.c_void_p),
+                ("vert_off", ctypes.c_void_p), ("vert", ctypes.c_void_p), ("curve_off", ctypes.c_void_p),
+                ("curve", ctypes.c_void_p), ("curve_color", ctypes.c_void_p)]
+
+
+class _Layout(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("n_edges", ctypes.c_uint64), ("max_lane", ctypes.c_uint32),
+                ("n_slots", ctypes.c_uint32), ("graph_width", ctypes.c_float),
+                ("lane", ctypes.c_void_p), ("color", ctypes.c_void_p), ("edges", ctypes.c_void_p),
+                ("heights", ctypes.c_void_p), ("geom", _Geom)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make oracle`")
+        L = ctypes.CDLL(path)
+        L.wgo_layout_build.argtypes = [ctypes.POINTER(abi.Commits), ctypes.POINTER(_Layout)]
+        L.wgo_row_geometry.argtypes = [ctypes.POINTER(_Layout), ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(_Geom)]
+        L.wgo_layout_free.argtypes = [ctypes.POINTER(_Layout)]
+        L.wgo_geometry_free.argtypes = [ctypes.POINTER(_Geom)]
+        L.wgo_compute_row_heights.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        L.wgo_emit_vertices.argtypes = [ctypes.POINTER(_Layout), ctypes.POINTER(_Geom), ctypes.c_uint64,
+                                        ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_uint64)]
+        L.wgo_free.argtypes = [ctypes.c_void_p]
+        L.wgo_vertex_checksum.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.wgo_vertex_checksum.restype = ctypes.c_uint64
+        for f in ("wgo_cubic_y_at", "wgo_cubic_t_at_y"):
+            getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_float]
+            getattr(L, f).restype = ctypes.c_float
+        L.wgo_cubic_subcurve.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _arr(ptr, dtype, count):
+    if count == 0:
+        return np.zeros(0, dtype)
+    buf = (ctypes.c_char * (np.dtype(dtype).itemsize * count)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype, count=count).copy()
+
+
+def _geom_to_dict(g: _Geom) -> dict:
+    n = g.n
+    return dict(height=_arr(g.height, np.float32, n), node_y=_arr(g.node_y, np.float32, n),
+                row_top=_arr(g.row_top, np.float32, n + 1), vert_off=_arr(g.vert_off, np.uint32, n + 1),
+                vert=_arr(g.vert, np.uint32, g.n_vert), curve_off=_arr(g.curve_off, np.uint32, n + 1),
+                curve=_arr(g.curve, np.float32, g.n_curve * 8).reshape(-1, 8),
+                curve_color=_arr(g.curve_color, np.uint8, g.n_curve))
+
+
+class OracleLayout:
+    """GraphLayout::build + row_geometry_with_bands + graph_cell emission."""
+
+    def __init__(self, dag):
+        self.dag = dag
+        self._c = abi.commits_struct(dag)
+        self._L = _Layout()
+        if lib().wgo_layout_build(ctypes.byref(self._c), ctypes.byref(self._L)) != 0:
+            raise MemoryError("wgo_layout_build failed")
+        L = self._L
+        self.n = L.n
+        self.max_lane = L.max_lane
+        self.n_slots = L.n_slots
+        self.graph_width = np.float32(L.graph_width)
+        self.lane = _arr(L.lane, np.uint32, L.n)
+        self.color = _arr(L.color, np.uint8, L.n)
+        self.edges = _arr(L.edges, abi.EDGE_DTYPE, L.n_edges)
+        self.heights = _arr(L.heights, np.float32, L.n)
+        self.geometry = _geom_to_dict(L.geom)   # build()'s row_geometry
+        self._g = None
+
+    def row_geometry(self, band=None) -> dict:
+        """row_geometry_with_bands(commits, band) (None -> zero bands)."""
+        if self._g is not None:
+            lib().wgo_geometry_free(ctypes.byref(self._g))
+        self._g = _Geom()
+        b = None if band is None else np.ascontiguousarray(band, np.float32)
+        self._band = b
+        rc = lib().wgo_row_geometry(ctypes.byref(self._L), self.dag.time.ctypes.data,
+                                    None if b is None else b.ctypes.data, ctypes.byref(self._g))
+        if rc != 0:
+            raise MemoryError("wgo_row_geometry failed")
+        return _geom_to_dict(self._g)
+
+    def emit_vertices(self, row_begin, row_end, selected=-1, palette=None, use_build_geometry=False):
+        """Vertices of rows [row_begin,row_end) from the last row_geometry()."""
+        pal = np.ascontiguousarray(abi.DEFAULT_PALETTE if palette is None else palette, np.float32)
+        g = self._L.geom if (use_build_geometry or self._g is None) else self._g
+        pv, po, pn = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        rc = lib().wgo_emit_vertices(ctypes.byref(self._L), ctypes.byref(g), row_begin, row_end, selected,
+                                     pal.ctypes.data, ctypes.byref(pv), ctypes.byref(po), ctypes.byref(pn))
+        if rc != 0:
+            raise ValueError("wgo_emit_vertices failed")
+        n = pn.value
+        v = _arr(pv.value, abi.VERTEX_DTYPE, n) if n else np.zeros(0, abi.VERTEX_DTYPE)
+        off = _arr(po.value, np.uint64, row_end - row_begin + 1)
+        lib().wgo_free(pv.value)
+        lib().wgo_free(po.value)
+        return v, off
+
+    def close(self):
+        if self._g is not None:
+            lib().wgo_geometry_free(ctypes.byref(self._g))
+            self._g = None
+        if self._L is not None:
+            lib().wgo_layout_free(ctypes.byref(self._L))
+            self._L = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def vertex_checksum(v: np.ndarray) -> int:
+    v = np.ascontiguousarray(v)
+    return int(lib().wgo_vertex_checksum(v.ctypes.data, v.shape[0]))
+
+
+def cubic_y_at(p8, t):
+    a = np.ascontiguousarray(p8, np.float32)
+    return np.float32(lib().wgo_cubic_y_at(a.ctypes.data, t))
+
+
+def cubic_t_at_y(p8, y):
+    a = np.ascontiguousarray(p8, np.float32)
+    return np.float32(lib().wgo_cubic_t_at_y(a.ctypes.data, y))
+
+
+def cubic_subcurve(p8, a, b):
+    x = np.ascontiguousarray(p8, np.float32)
+    out = np.zeros(8, np.float32)
+    lib().wgo_cubic_subcurve(x.ctypes.data, a, b, out.ctypes.data)
+    return out

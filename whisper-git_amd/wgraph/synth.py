@@ -1,0 +1,116 @@
+"""Seeded synthetic commit DAGs (workload generator, ctypes over libwgsynth.so).
+
+The generator itself is C (whisper-git_amd/synth/wg_synth.c).  Presets follow
+SURVEY.md §8(d): LINEAR (C1), RANDOM13 (C3), LINUX (C4), WIDE16 (C5) and
+ANOMALY (the edge cases GraphLayout::build tolerates).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+LINEAR, RANDOM13, LINUX, WIDE16, ANOMALY = 0, 1, 2, 3, 4
+PRESETS = {"linear": LINEAR, "random13": RANDOM13, "linux": LINUX, "wide16": WIDE16, "anomaly": ANOMALY}
+SEED_BASE = 0x5EED  # seed = 0x5EED + config id
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("max_lines", ctypes.c_int32),
+                ("n", ctypes.c_uint64), ("seed", ctypes.c_uint64),
+                ("p_merge", ctypes.c_double), ("p_octopus", ctypes.c_double),
+                ("p_newtip", ctypes.c_double), ("p_fork", ctypes.c_double),
+                ("main_weight", ctypes.c_double), ("p_dup_oid", ctypes.c_double),
+                ("p_skew", ctypes.c_double), ("p_external", ctypes.c_double),
+                ("p_self", ctypes.c_double), ("p_dup_parent", ctypes.c_double),
+                ("p_orphan_flag", ctypes.c_double), ("band_frac", ctypes.c_double),
+                ("truncated", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libwgsynth.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make synth` (or __graft_entry__.build())")
+        lib = ctypes.CDLL(path)
+        lib.wgs_preset.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(Params)]
+        lib.wgs_generate.argtypes = [ctypes.POINTER(Params)]
+        lib.wgs_generate.restype = ctypes.c_void_p
+        lib.wgs_sizes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        lib.wgs_copy.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
+        lib.wgs_free.argtypes = [ctypes.c_void_p]
+        _lib = lib
+    return _lib
+
+
+@dataclass
+class Dag:
+    """wg_commits as numpy arrays (+ the per-row pills band)."""
+    oid: np.ndarray          # uint8 [N, 20]
+    time: np.ndarray         # int64 [N]
+    parent_off: np.ndarray   # uint32 [N+1]
+    parent_oid: np.ndarray   # uint8 [E, 20]
+    flags: np.ndarray        # uint8 [N]
+    band: np.ndarray         # float32 [N]
+
+    @property
+    def n(self) -> int:
+        return int(self.time.shape[0])
+
+    @property
+    def e(self) -> int:
+        return int(self.parent_oid.shape[0])
+
+    def slice_rows(self, n: int) -> "Dag":
+        """First n rows (parents beyond the cut become out-of-list ids, as
+        with the reference's COMMIT_LIMIT truncation, repo_tab.rs:105)."""
+        e = int(self.parent_off[n])
+        return Dag(self.oid[:n].copy(), self.time[:n].copy(), self.parent_off[:n + 1].copy(),
+                   self.parent_oid[:e].copy(), self.flags[:n].copy(), self.band[:n].copy())
+
+
+def params(kind: int, n: int, seed: int | None = None) -> Params:
+    p = Params()
+    rc = _load().wgs_preset(kind, n, SEED_BASE + kind if seed is None else seed, ctypes.byref(p))
+    if rc != 0:
+        raise ValueError(f"unknown preset {kind}")
+    return p
+
+
+def generate(kind: int | str, n: int, seed: int | None = None, **overrides) -> Dag:
+    if isinstance(kind, str):
+        kind = PRESETS[kind]
+    p = params(kind, n, seed)
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    lib = _load()
+    h = lib.wgs_generate(ctypes.byref(p))
+    if not h:
+        raise MemoryError("wgs_generate failed")
+    try:
+        nn, ee = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.wgs_sizes(h, ctypes.byref(nn), ctypes.byref(ee))
+        N, E = nn.value, ee.value
+        d = Dag(np.empty((N, 20), np.uint8), np.empty(N, np.int64), np.empty(N + 1, np.uint32),
+                np.empty((E, 20), np.uint8), np.empty(N, np.uint8), np.empty(N, np.float32))
+        lib.wgs_copy(h, d.oid.ctypes.data, d.time.ctypes.data, d.parent_off.ctypes.data,
+                     d.parent_oid.ctypes.data, d.flags.ctypes.data, d.band.ctypes.data)
+        return d
+    finally:
+        lib.wgs_free(h)
+
+
+def save(d: Dag, path: str) -> None:
+    np.savez_compressed(path, oid=d.oid, time=d.time, parent_off=d.parent_off,
+                        parent_oid=d.parent_oid, flags=d.flags, band=d.band)
+
+
+def load(path: str) -> Dag:
+    z = np.load(path, allow_pickle=False)
+    return Dag(z["oid"], z["time"], z["parent_off"], z["parent_oid"], z["flags"], z["band"])
