@@ -1,0 +1,193 @@
+"""Benchmark: commit-rows/s to vertex buffers (BASELINE.json metric).
+
+One step = the whole hot path over one batch of device-resident commits:
+GraphLayout::build (hash join, lane assignment, edges, heights, default
+row geometry) -> row_geometry_with_bands (pills bands) -> graph_cell vertex
+emission for every row of this rank's shard (WG-TESS-1 SplineVertex buffers
+written to HBM).  Workload: the WIDE16 synthetic DAG (C5 shape, <= 16
+lanes), 1M commit-rows per GPU (weak scaling: N GPUs = an N-million-row
+DAG, each rank emits its contiguous 1M-row shard).
+
+Round-1 multi-GPU scheme: the sequential layout stages run
+replicated on every rank over the whole DAG; vertex emission (the
+HBM-bound stage) is sharded by contiguous row range; ranks meet only at the
+timing barrier.  Launched per the driver contract:
+  python bench.py --gpus 1 --steps K --warmup W
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--kind", default="wide16")
+    ap.add_argument("--cpu-rows", type=int, default=1_000_000, help="rows of the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(dag, rows, log):
+    """The CPU oracle (faithful single-thread restatement of commit_graph.rs)
+    timed on this host over the first `rows` rows of the same workload."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle_c   # checker / baseline only
+    d = dag.slice_rows(min(rows, dag.n))
+    t0 = time.perf_counter()
+    o = oracle_c.OracleLayout(d)
+    o.row_geometry(d.band)
+    step = 50_000
+    nv = 0
+    for r0 in range(0, d.n, step):
+        v, _ = o.emit_vertices(r0, min(d.n, r0 + step), selected=7 if r0 == 0 else -1)
+        nv += len(v)
+    dt = time.perf_counter() - t0
+    o.close()
+    log(f"cpu baseline: {d.n} rows in {dt:.2f}s ({nv} vertices)")
+    return {"value": d.n / dt, "unit": "commit-rows/s", "cores": 1, "kind": "port",
+            "sample": f"first {d.n} rows of the same {d.n}-row-prefix workload: oracle build + "
+                      f"row_geometry_with_bands + vertex emission, 1 thread, {dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    log = (lambda *a: print(*a, file=sys.stderr, flush=True)) if (args.verbose or rank == 0) else (lambda *a: None)
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local_rank))
+
+    import wgraph
+    from wgraph import abi, synth
+
+    rows_total = args.rows_per_gpu * world
+    t0 = time.perf_counter()
+    dag = synth.generate(args.kind, rows_total)
+    log(f"generated {args.kind} DAG: {dag.n} rows, {dag.e} parent refs in {time.perf_counter() - t0:.1f}s")
+    shard0 = rank * args.rows_per_gpu
+    shard1 = min(rows_total, shard0 + args.rows_per_gpu)
+
+    # device-resident inputs (the timed region starts from HBM)
+    dev = torch.device("cuda", local_rank)
+    t_oid = torch.from_numpy(dag.oid.reshape(-1)).to(dev)
+    t_time = torch.from_numpy(dag.time).to(dev)
+    t_poff = torch.from_numpy(dag.parent_off.view(np.int32)).to(dev)
+    t_poid = torch.from_numpy(dag.parent_oid.reshape(-1)).to(dev)
+    t_flags = torch.from_numpy(dag.flags).to(dev)
+    t_band = torch.from_numpy(dag.band).to(dev)
+    commits = abi.Commits()
+    commits.n_commits, commits.n_parents = dag.n, dag.e
+    commits.oid, commits.time = t_oid.data_ptr(), t_time.data_ptr()
+    commits.parent_off, commits.parent_oid = t_poff.data_ptr(), t_poid.data_ptr()
+    commits.flags, commits.residency = t_flags.data_ptr(), abi.WG_DEVICE
+
+    eng = wgraph.Engine(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    eng.set_stream(stream.cuda_stream)
+    pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
+    selected = shard0 + 7
+
+    def step():
+        eng.build(commits=commits)
+        eng.row_geometry(device_ptr=t_band.data_ptr())
+        eng.emit_vertices(shard0, shard1, selected=selected, palette=pal)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # timed region: barrier + sync on both sides, exactly K steps
+    stage_ms = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.enable_timing(True)
+        step()
+        for name, ms in eng.timings():
+            stage_ms.setdefault(name, []).append(ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    eng.enable_timing(False)
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    rows_done = rows_total  # all ranks together emit every row once per step
+    value = rows_done * args.steps / elapsed
+
+    # roofline of the dominant kernel (vertex emission), from live HIP events
+    vs = eng.vertex_summary()
+    gs = eng.geometry_summary()
+    n_rows_shard = shard1 - shard0
+    vtx_ms = float(np.mean(stage_ms.get("vtx_emit", [float("nan")])))
+    views = eng.device_views()
+    voff = np.empty(n_rows_shard + 1, np.uint32)
+    coff = np.empty(n_rows_shard + 1, np.uint32)
+    g = eng.geometry()
+    nvert_shard = int(g["vert_off"][shard1]) - int(g["vert_off"][shard0])
+    ncurve_shard = int(g["curve_off"][shard1]) - int(g["curve_off"][shard0])
+    # algorithmic bytes of one vtx_emit launch: vertices written + geometry read
+    bytes_w = 24 * vs.n_vertices
+    bytes_r = 4 * nvert_shard + 33 * ncurve_shard + n_rows_shard * (8 + 4 + 4 + 4 + 4 + 4 + 1)
+    achieved = (bytes_w + bytes_r) / (vtx_ms * 1e-3) / 1e9
+    roofline = {"kernel": "k_vtx_tiles (vtx_emit)", "bound": "hbm", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None, "algorithmic_bytes_per_launch": int(bytes_w + bytes_r),
+                "avg_launch_ms": round(vtx_ms, 4)}
+
+    stages = {k: round(float(np.mean(v)), 4) for k, v in stage_ms.items()}
+    log("stage ms (mean over timed steps):", json.dumps(stages))
+    log(f"rows {rows_total}, shard {n_rows_shard}, vertices {vs.n_vertices}, vert {gs.n_vert}, curves {gs.n_curve}, "
+        f"max_lane {eng.layout_summary().max_lane}, lane_path {eng.layout_summary().lane_path}")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(dag, args.cpu_rows, log)
+
+    if rank == 0:
+        out = {"metric": "commit-rows/sec to vertex buffers, 1M-commit synthetic DAG per GPU",
+               "value": round(value, 1), "unit": "commit-rows/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+               "config": {"workload": f"{args.kind} synthetic DAG (C5 shape), {args.rows_per_gpu} commit-rows per GPU, "
+                                      f"full path: layout build + banded geometry + SplineVertex emission",
+                          "rows_total": rows_total, "rows_per_gpu": args.rows_per_gpu,
+                          "vertices_per_gpu": int(vs.n_vertices), "parallelism": f"row-shard x{world}"},
+               "stages_ms": stages, "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,180 @@
+"""GPU parity: the HIP engine through the C ABI against the oracle.
+
+Bar: bit-exact for lanes, colours, max_lane, edges, heights, per-row list
+contents and order, row_top_y, and every f32 of the curve records and the
+vertex buffers (the north star allows 1 ulp on fp32 vertex positions; the
+engine is held to 0 ulp and the test reports the ulp distance if it ever
+differs).  Small cases compare against the committed goldens; larger ones
+against the C oracle run in-process; the full-size configuration through
+size-independent checks (checksums, monotone row_top, count identities).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+from wgraph import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def ulp_diff(a, b):
+    ai = a.view(np.int32).astype(np.int64)
+    bi = b.view(np.int32).astype(np.int64)
+    ai = np.where(ai < 0, -(ai & 0x7FFFFFFF), ai)
+    bi = np.where(bi < 0, -(bi & 0x7FFFFFFF), bi)
+    return np.abs(ai - bi)
+
+
+def assert_bits(name, got, want):
+    got = np.ascontiguousarray(got)
+    want = np.ascontiguousarray(want)
+    assert got.shape == want.shape, (name, got.shape, want.shape)
+    if got.tobytes() != want.tobytes():
+        if got.dtype == np.float32:
+            d = ulp_diff(got.reshape(-1), want.reshape(-1))
+            idx = np.nonzero(d)[0]
+            raise AssertionError(f"{name}: {idx.size} f32 mismatches, max {d.max()} ulp, first at {idx[:5]}: "
+                                 f"{got.reshape(-1)[idx[:5]]} vs {want.reshape(-1)[idx[:5]]}")
+        idx = np.nonzero(got.reshape(-1) != want.reshape(-1))[0]
+        raise AssertionError(f"{name}: {idx.size} mismatches, first at {idx[:5]}: "
+                             f"{got.reshape(-1)[idx[:5]]} vs {want.reshape(-1)[idx[:5]]}")
+
+
+def check_layout(engine, g):
+    s = engine.layout_summary()
+    assert s.max_lane == int(g["max_lane"])
+    assert np.float32(s.graph_width) == np.float32(g["graph_width"])
+    lane, color = engine.lanes()
+    assert_bits("lane", lane, g["lane"])
+    assert_bits("color", color, g["color"])
+    e = engine.edges()
+    assert_bits("edges", e.view(np.uint32).reshape(-1, 5) if len(e) else np.zeros((0, 5), np.uint32), g["edges"])
+    assert_bits("heights", engine.row_heights(), g["heights"])
+
+
+def check_geometry(engine, g, prefix):
+    got = engine.geometry()
+    for k in ("height", "node_y", "row_top", "vert_off", "vert", "curve_off", "curve", "curve_color"):
+        assert_bits(prefix + k, got[k], g[prefix + k])
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_full_pipeline(engine, name):
+    d, g = load_golden(name)
+    engine.build(d)
+    check_layout(engine, g)
+    check_geometry(engine, g, "build_")          # GraphLayout::build's row_geometry
+    engine.row_geometry(g["band"])               # row_geometry_with_bands
+    check_geometry(engine, g, "band_")
+    engine.emit_vertices(0, d.n, selected=int(g["selected"]))
+    s = engine.vertex_summary()
+    assert s.n_vertices == int(g["vtx_off"][-1])
+    assert_bits("vtx_off", engine.vertex_offsets(), g["vtx_off"])
+    head = int(g["vertices_head_rows"])
+    nh = int(g["vtx_off"][head])
+    v = engine.vertices(0, nh).view(np.float32).reshape(-1, 6)
+    assert_bits("vertices", v, g["vertices"])
+    assert s.checksum == int(g["vertex_checksum"])
+
+
+@pytest.mark.parametrize("kind,n", [("random13", 20000), ("linux", 30000), ("wide16", 50000), ("anomaly", 5000),
+                                    ("linear", 10000)])
+def test_against_oracle_midsize(engine, kind, n):
+    from oracle import oracle_c
+    d = synth.generate(kind, n, seed=1234 + n)
+    o = oracle_c.OracleLayout(d)
+    engine.build(d)
+    s = engine.layout_summary()
+    assert s.max_lane == o.max_lane
+    lane, color = engine.lanes()
+    assert_bits("lane", lane, o.lane)
+    assert_bits("color", color, o.color)
+    assert_bits("edges", engine.edges(), o.edges)
+    got = engine.geometry()
+    for k, v in o.geometry.items():
+        assert_bits("build_" + k, got[k], v)
+    engine.row_geometry(d.band)
+    og = o.row_geometry(d.band)
+    got = engine.geometry()
+    for k, v in og.items():
+        assert_bits("band_" + k, got[k], v)
+    sel = n // 3
+    engine.emit_vertices(0, n, selected=sel)
+    ov, ooff = o.emit_vertices(0, n, selected=sel)
+    assert_bits("vtx_off", engine.vertex_offsets(), ooff)
+    sv = engine.vertex_summary()
+    assert sv.checksum == __import__("oracle").oracle_c.vertex_checksum(ov)
+    # a window of rows bit-for-bit
+    a, b = int(ooff[sel - 5]), int(ooff[sel + 5])
+    assert_bits("vertices", engine.vertices(a, b - a).view(np.float32), ov[a:b].view(np.float32))
+
+
+def test_partial_row_range(engine):
+    from oracle import oracle_c
+    d = synth.generate("random13", 5000, seed=77)
+    o = oracle_c.OracleLayout(d)
+    engine.build(d)
+    engine.row_geometry(d.band)
+    o.row_geometry(d.band)
+    for rb, re_, sel in ((100, 700, 400), (4999, 5000, 4999), (0, 1, -1), (2500, 2500, -1)):
+        engine.emit_vertices(rb, re_, selected=sel)
+        ov, ooff = o.emit_vertices(rb, re_, selected=sel)
+        assert_bits("vtx_off", engine.vertex_offsets(), ooff)
+        if len(ov):
+            assert_bits("vertices", engine.vertices().view(np.float32), ov.view(np.float32))
+
+
+def test_row_top_exact_beyond_2_24(engine):
+    """1.3M rows: row_top crosses 2^24 and 2^25 px; the transducer scan must
+    reproduce the sequential f32 accumulation bit for bit (:329-335)."""
+    from oracle import oracle_c
+    d = synth.generate("linux", 1_300_000)
+    o = oracle_c.OracleLayout(d)
+    engine.build(d)
+    got = engine.geometry()
+    assert got["row_top"][-1] > 2 ** 25
+    assert_bits("row_top", got["row_top"], o.geometry["row_top"])
+    assert_bits("vert_off", got["vert_off"], o.geometry["vert_off"])
+    assert_bits("curve", got["curve"], o.geometry["curve"])
+    assert engine.geometry_summary().scan_path == 0
+
+
+def test_bands_with_fractional_and_negative_values(engine):
+    """Non-integer bands keep the transducer path exact; a negative band forces
+    the serial path, which must also be exact."""
+    from oracle import oracle_c
+    d = synth.generate("wide16", 40000, seed=5)
+    o = oracle_c.OracleLayout(d)
+    engine.build(d)
+    rng = np.random.default_rng(0)
+    for band in (rng.uniform(0, 40, d.n).astype(np.float32),
+                 np.where(rng.random(d.n) < 0.01, -3.0, 30.0).astype(np.float32)):
+        engine.row_geometry(band)
+        og = o.row_geometry(band)
+        got = engine.geometry()
+        for k in ("row_top", "height", "node_y", "vert", "curve"):
+            assert_bits(k, got[k], og[k])
+
+
+def test_empty_and_single(engine):
+    d = synth.generate("linear", 1)
+    engine.build(d)
+    assert engine.layout_summary().max_lane == 0
+    engine.emit_vertices(0, 1, selected=0)
+    assert engine.vertex_summary().n_vertices == abi.VTX_PER_NODE + abi.VTX_PER_RING
+
+
+def test_full_size_properties(engine):
+    """BASELINE config size (1M rows): size-independent identities."""
+    d = synth.generate("wide16", 1_000_000)
+    engine.build(d)
+    engine.row_geometry(d.band)
+    g = engine.geometry()
+    assert np.all(np.diff(g["row_top"]) >= 28.0)
+    nv = np.diff(g["vert_off"].astype(np.int64))
+    nc = np.diff(g["curve_off"].astype(np.int64))
+    engine.emit_vertices(0, d.n, selected=7)
+    off = engine.vertex_offsets()
+    want = 6 * nv + 96 * nc + 72
+    want[7] += 144
+    assert (np.diff(off.astype(np.int64)) == want).all()

@@ -1,0 +1,364 @@
+// wg_api.hip — C ABI entry points (include/wgraph.h) and stage orchestration.
+//
+// Each exported function names the GraphLayout item it replaces
+// (/root/reference/src/commit_graph.rs).  No C++ exception crosses the ABI;
+// every failure returns a negative status with a message in wg_last_error().
+#include <cstdarg>
+#include <cstring>
+#include <new>
+
+#include "wg_internal.h"
+
+int wg_fail(wg_ctx *c, int code, const char *fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+void wg_stage_begin(wg_ctx *c, const char *name) {
+    if (!c->timing || c->n_stages >= WG_STAGE_MAX) return;
+    StageTimer &t = c->stages[c->n_stages];
+    t.name = name;
+    (void)hipEventRecord(t.a, c->stream);
+}
+void wg_stage_end(wg_ctx *c) {
+    if (!c->timing || c->n_stages >= WG_STAGE_MAX) return;
+    (void)hipEventRecord(c->stages[c->n_stages].b, c->stream);
+    c->n_stages++;
+}
+
+extern "C" {
+
+int wg_abi_version(void) { return WGRAPH_ABI_VERSION; }
+
+wg_ctx *wg_create(int device_ordinal) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return nullptr;
+    int dev = device_ordinal;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (dev >= ndev || hipSetDevice(dev) != hipSuccess) return nullptr;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return nullptr;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return nullptr;   // CDNA4 only
+    wg_ctx *c = new (std::nothrow) wg_ctx();
+    if (!c) return nullptr;
+    c->device = dev;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return nullptr; }
+    c->own_stream = true;
+    for (int i = 0; i < WG_STAGE_MAX; i++) {
+        (void)hipEventCreate(&c->stages[i].a);
+        (void)hipEventCreate(&c->stages[i].b);
+    }
+    wg_init_height_thresholds(c->h_thresh);
+    return c;
+}
+
+void wg_destroy(wg_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    DevBuf *bufs[] = {&c->in_oid, &c->in_time, &c->in_poff, &c->in_poid, &c->in_flags, &c->hash, &c->canon,
+                      &c->prow, &c->lane_asg, &c->lane_out, &c->color_out, &c->lane_scalars, &c->edge_cnt,
+                      &c->edges, &c->heights, &c->band, &c->g_height, &c->g_node_y, &c->g_row_top,
+                      &c->rt_chunk, &c->rt_tables, &c->rt_flags, &c->cntF, &c->cntT, &c->cntB, &c->cntC,
+                      &c->cntCend, &c->vert_off, &c->curve_off, &c->vert, &c->curve, &c->curve_color,
+                      &c->curve_ref, &c->curve_row, &c->top_fill, &c->carry_cnt, &c->carry_off, &c->carry,
+                      &c->scan_tmp, &c->scal, &c->rowflags, &c->carry_fill, &c->sweep_err, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
+    for (DevBuf *b : bufs) b->release();
+    for (int i = 0; i < WG_STAGE_MAX; i++) {
+        (void)hipEventDestroy(c->stages[i].a);
+        (void)hipEventDestroy(c->stages[i].b);
+    }
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *wg_last_error(const wg_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int wg_set_stream(wg_ctx *c, void *s) {
+    if (!c) return WG_E_INVALID;
+    (void)hipSetDevice(c->device);
+    if (c->own_stream && c->stream) {
+        WG_HIP(c, hipStreamSynchronize(c->stream));
+        WG_HIP(c, hipStreamDestroy(c->stream));
+    }
+    if (s) { c->stream = (hipStream_t)s; c->own_stream = false; }
+    else {
+        WG_HIP(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    return WG_OK;
+}
+
+int wg_synchronize(wg_ctx *c) {
+    if (!c) return WG_E_INVALID;
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// GraphLayout::build (:265-355)
+// ---------------------------------------------------------------------------
+int wg_layout_build(wg_ctx *c, const wg_commits *in) {
+    if (!c || !in) return WG_E_INVALID;
+    (void)hipSetDevice(c->device);
+    c->have_layout = c->have_geom = c->have_vtx = false;
+    const uint64_t n = in->n_commits;
+    if (n >= 0xFFFFFFF0ull) return wg_fail(c, WG_E_UNSUPPORTED, "n_commits %llu exceeds 2^32-16", (unsigned long long)n);
+    if (n > 0 && (!in->oid || !in->time || !in->parent_off)) return wg_fail(c, WG_E_INVALID, "null input array");
+    uint64_t e = 0;
+    if (n > 0) {
+        if (in->residency == WG_HOST) e = in->parent_off[n];
+        else e = in->n_parents;
+        if (e != in->n_parents) return wg_fail(c, WG_E_INVALID, "n_parents %llu != parent_off[N] %llu",
+                                               (unsigned long long)in->n_parents, (unsigned long long)e);
+        if (e > 0 && !in->parent_oid) return wg_fail(c, WG_E_INVALID, "null parent_oid");
+    }
+    c->n = n;
+    c->e_refs = e;
+    if (in->residency == WG_HOST) {
+        wg_stage_begin(c, "h2d");
+        WG_ALLOC(c, c->in_oid, n * 20 + 4);
+        WG_ALLOC(c, c->in_time, n * 8 + 8);
+        WG_ALLOC(c, c->in_poff, (n + 1) * 4);
+        WG_ALLOC(c, c->in_poid, e * 20 + 4);
+        WG_ALLOC(c, c->in_flags, n + 4);
+        if (n) {
+            WG_HIP(c, hipMemcpyAsync(c->in_oid.p, in->oid, n * 20, hipMemcpyHostToDevice, c->stream));
+            WG_HIP(c, hipMemcpyAsync(c->in_time.p, in->time, n * 8, hipMemcpyHostToDevice, c->stream));
+            if (in->flags) WG_HIP(c, hipMemcpyAsync(c->in_flags.p, in->flags, n, hipMemcpyHostToDevice, c->stream));
+            else WG_HIP(c, hipMemsetAsync(c->in_flags.p, 0, n, c->stream));
+        }
+        WG_HIP(c, hipMemcpyAsync(c->in_poff.p, in->parent_off, (n + 1) * 4, hipMemcpyHostToDevice, c->stream));
+        if (e) WG_HIP(c, hipMemcpyAsync(c->in_poid.p, in->parent_oid, e * 20, hipMemcpyHostToDevice, c->stream));
+        c->d_oid = c->in_oid.as<uint8_t>();
+        c->d_time = c->in_time.as<int64_t>();
+        c->d_poff = c->in_poff.as<uint32_t>();
+        c->d_poid = c->in_poid.as<uint8_t>();
+        c->d_flags = c->in_flags.as<uint8_t>();
+        wg_stage_end(c);
+    } else if (in->residency == WG_DEVICE) {
+        c->d_oid = in->oid;
+        c->d_time = in->time;
+        c->d_poff = in->parent_off;
+        c->d_poid = in->parent_oid;
+        if (in->flags) c->d_flags = in->flags;
+        else {
+            WG_ALLOC(c, c->in_flags, n + 4);
+            WG_HIP(c, hipMemsetAsync(c->in_flags.p, 0, n + 4, c->stream));
+            c->d_flags = c->in_flags.as<uint8_t>();
+        }
+    } else {
+        return wg_fail(c, WG_E_INVALID, "bad residency %d", in->residency);
+    }
+    int rc;
+    if ((rc = wg_stage_hash_join(c)) != WG_OK) return rc;
+    if ((rc = wg_stage_lanes(c)) != WG_OK) return rc;
+    if ((rc = wg_stage_edges(c)) != WG_OK) return rc;
+    if ((rc = wg_stage_heights(c)) != WG_OK) return rc;
+    c->have_layout = true;
+    // self.row_geometry with the default node_y / zero bands (:322-346)
+    if ((rc = wg_stage_rowtop(c, nullptr)) != WG_OK) return rc;
+    if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
+    c->have_geom = true;
+    return WG_OK;
+}
+
+int wg_layout_summary_get(wg_ctx *c, wg_layout_summary *out) {
+    if (!c || !out) return WG_E_INVALID;
+    if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
+    out->n_rows = c->n;
+    out->n_edges = c->n_edges;
+    out->max_lane = c->max_lane;
+    out->n_slots = c->n_slots;
+    out->graph_width = c->graph_width;
+    out->lane_path = c->lane_path;
+    return WG_OK;
+}
+
+int wg_copy_lanes(wg_ctx *c, uint32_t *lane, uint8_t *color) {
+    if (!c) return WG_E_INVALID;
+    if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
+    if (lane && c->n) WG_HIP(c, hipMemcpyAsync(lane, c->lane_out.p, c->n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (color && c->n) WG_HIP(c, hipMemcpyAsync(color, c->color_out.p, c->n, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+int wg_copy_edges(wg_ctx *c, wg_edge *edges) {
+    if (!c || !edges) return WG_E_INVALID;
+    if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
+    if (c->n_edges)
+        WG_HIP(c, hipMemcpyAsync(edges, c->edges.p, c->n_edges * sizeof(wg_edge), hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+int wg_copy_row_heights(wg_ctx *c, float *h) {
+    if (!c || !h) return WG_E_INVALID;
+    if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
+    if (c->n) WG_HIP(c, hipMemcpyAsync(h, c->heights.p, c->n * 4, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// row_geometry_with_bands (:367-399)
+// ---------------------------------------------------------------------------
+int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
+    if (!c) return WG_E_INVALID;
+    if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
+    (void)hipSetDevice(c->device);
+    c->have_geom = c->have_vtx = false;
+    const float *d_band = nullptr;
+    if (band) {
+        if (residency == WG_HOST) {
+            WG_ALLOC(c, c->band, c->n * 4 + 4);
+            if (c->n) WG_HIP(c, hipMemcpyAsync(c->band.p, band, c->n * 4, hipMemcpyHostToDevice, c->stream));
+            d_band = c->band.as<float>();
+        } else if (residency == WG_DEVICE) {
+            d_band = band;
+        } else {
+            return wg_fail(c, WG_E_INVALID, "bad residency %d", residency);
+        }
+    }
+    int rc;
+    if ((rc = wg_stage_rowtop(c, d_band)) != WG_OK) return rc;
+    if ((rc = wg_stage_geometry(c, d_band)) != WG_OK) return rc;
+    c->have_geom = true;
+    return WG_OK;
+}
+
+int wg_geometry_summary_get(wg_ctx *c, wg_geometry_summary *out) {
+    if (!c || !out) return WG_E_INVALID;
+    if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
+    out->n_rows = c->n;
+    out->n_vert = c->n_vert;
+    out->n_curve = c->n_curve;
+    out->total_height = c->total_height;
+    out->scan_path = c->scan_path;
+    return WG_OK;
+}
+
+int wg_copy_geometry(wg_ctx *c, const wg_geometry_host *d) {
+    if (!c || !d) return WG_E_INVALID;
+    if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
+    const uint64_t n = c->n;
+    hipStream_t s = c->stream;
+    if (d->height && n) WG_HIP(c, hipMemcpyAsync(d->height, c->g_height.p, n * 4, hipMemcpyDeviceToHost, s));
+    if (d->node_y && n) WG_HIP(c, hipMemcpyAsync(d->node_y, c->g_node_y.p, n * 4, hipMemcpyDeviceToHost, s));
+    if (d->row_top) WG_HIP(c, hipMemcpyAsync(d->row_top, c->g_row_top.p, (n + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (d->vert_off) WG_HIP(c, hipMemcpyAsync(d->vert_off, c->vert_off.p, (n + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (d->curve_off) WG_HIP(c, hipMemcpyAsync(d->curve_off, c->curve_off.p, (n + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (d->vert && c->n_vert) WG_HIP(c, hipMemcpyAsync(d->vert, c->vert.p, c->n_vert * 4, hipMemcpyDeviceToHost, s));
+    if (d->curve && c->n_curve)
+        WG_HIP(c, hipMemcpyAsync(d->curve, c->curve.p, c->n_curve * sizeof(wg_curve), hipMemcpyDeviceToHost, s));
+    if (d->curve_color && c->n_curve)
+        WG_HIP(c, hipMemcpyAsync(d->curve_color, c->curve_color.p, c->n_curve, hipMemcpyDeviceToHost, s));
+    WG_HIP(c, hipStreamSynchronize(s));
+    return WG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// graph_cell (:803-908) tessellated per WG-TESS-1
+// ---------------------------------------------------------------------------
+int wg_emit_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel, const float *palette) {
+    if (!c || !palette) return WG_E_INVALID;
+    if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
+    if (rb > re || re > c->n) return wg_fail(c, WG_E_INVALID, "row range [%llu,%llu) outside [0,%llu)",
+                                             (unsigned long long)rb, (unsigned long long)re, (unsigned long long)c->n);
+    (void)hipSetDevice(c->device);
+    c->have_vtx = false;
+    WG_ALLOC(c, c->palette, WG_PALETTE_SIZE * 4 * sizeof(float));
+    WG_HIP(c, hipMemcpyAsync(c->palette.p, palette, WG_PALETTE_SIZE * 4 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    int rc = wg_stage_vertices(c, rb, re, sel);
+    if (rc != WG_OK) return rc;
+    c->have_vtx = true;
+    return WG_OK;
+}
+
+int wg_vertex_summary_get(wg_ctx *c, wg_vertex_summary *out) {
+    if (!c || !out) return WG_E_INVALID;
+    if (!c->have_vtx) return wg_fail(c, WG_E_STATE, "no vertices emitted");
+    out->row_begin = c->vrow_begin;
+    out->row_end = c->vrow_end;
+    out->n_vertices = c->n_vtx;
+    uint64_t chk = 0;
+    int rc = wg_vertex_checksum_run(c, &chk);
+    if (rc != WG_OK) return rc;
+    out->checksum = chk;
+    return WG_OK;
+}
+
+int wg_copy_vertices(wg_ctx *c, uint64_t first, uint64_t count, wg_vertex *dst) {
+    if (!c || (!dst && count)) return WG_E_INVALID;
+    if (!c->have_vtx) return wg_fail(c, WG_E_STATE, "no vertices emitted");
+    if (first > c->n_vtx || count > c->n_vtx - first) return wg_fail(c, WG_E_INVALID, "vertex range out of bounds");
+    if (count)
+        WG_HIP(c, hipMemcpyAsync(dst, c->vtx.as<wg_vertex>() + first, count * sizeof(wg_vertex), hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+int wg_copy_vertex_offsets(wg_ctx *c, uint64_t *dst) {
+    if (!c || !dst) return WG_E_INVALID;
+    if (!c->have_vtx) return wg_fail(c, WG_E_STATE, "no vertices emitted");
+    WG_HIP(c, hipMemcpyAsync(dst, c->vtx_off.p, (c->vrow_end - c->vrow_begin + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+int wg_device_views_get(wg_ctx *c, wg_device_views *o) {
+    if (!c || !o) return WG_E_INVALID;
+    std::memset(o, 0, sizeof(*o));
+    if (c->have_layout) {
+        o->lane = c->lane_out.as<uint32_t>();
+        o->color = c->color_out.as<uint8_t>();
+        o->edges = c->edges.as<wg_edge>();
+    }
+    if (c->have_geom) {
+        o->height = c->g_height.as<float>();
+        o->node_y = c->g_node_y.as<float>();
+        o->row_top = c->g_row_top.as<float>();
+        o->vert_off = c->vert_off.as<uint32_t>();
+        o->vert = c->vert.as<uint32_t>();
+        o->curve_off = c->curve_off.as<uint32_t>();
+        o->curve = c->curve.as<wg_curve>();
+        o->curve_color = c->curve_color.as<uint8_t>();
+    }
+    if (c->have_vtx) {
+        o->vtx_off = c->vtx_off.as<uint64_t>();
+        o->vertices = c->vtx.as<wg_vertex>();
+    }
+    return WG_OK;
+}
+
+int wg_enable_timing(wg_ctx *c, int on) {
+    if (!c) return WG_E_INVALID;
+    c->timing = on != 0;
+    c->n_stages = 0;
+    return WG_OK;
+}
+
+int wg_stage_timings(wg_ctx *c, int *n_stages, const char **names, float *ms) {
+    if (!c || !n_stages) return WG_E_INVALID;
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    *n_stages = c->n_stages;
+    for (int i = 0; i < c->n_stages; i++) {
+        if (names) names[i] = c->stages[i].name;
+        if (ms) {
+            float t = 0.0f;
+            WG_HIP(c, hipEventElapsedTime(&t, c->stages[i].a, c->stages[i].b));
+            ms[i] = t;
+        }
+    }
+    return WG_OK;
+}
+
+}  // extern "C"

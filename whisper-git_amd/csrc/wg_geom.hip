@@ -1,0 +1,444 @@
+// wg_geom.hip — edge -> per-row geometry.
+//
+// Reference: RowGeometry init (commit_graph.rs:337-343, :383-394),
+// decompose_edge_into_rows (:525-608) and Cubic (:614-695).  Each row's four
+// lists are filled in edge order (child_row asc, then parent order), which
+// graph_cell paints as z-order (:827-866); the engine reproduces that order
+// exactly:
+//   bottom_half  row r = same-lane edges of child r, in parent order
+//   top_half     row r = same-lane edges into parent r, sorted by edge id
+//   full         row r = same-lane edges with c < r < p, edge order
+//   curves       row r = cross-lane edges with c <= r <= p whose strip is
+//                non-empty (:577), edge order
+// Counts come from difference arrays + scans; `full` and `curves` are
+// ordered by a chunked sweep: one wave owns 64 rows and carries the ordered
+// list of edges alive across its first row (registered per chunk, then
+// rank-sorted), appends edges as their child rows are reached and compacts
+// out edges that ended.  The per-segment Bezier clipping (two 40-step
+// bisections + two de Casteljau splits) then runs one thread per segment.
+//
+// Bit-exact f32: built with -ffp-contract=off and the exact operation order
+// of Cubic::y_at (:623-629), split's lerp (:657) and `dy * 0.4` (:557-562).
+#include "wg_internal.h"
+
+namespace {
+
+constexpr int T = 256;
+constexpr uint32_t RF_ZERO = 1u, RF_CHILD = 2u, RF_PARENT = 4u;
+
+__device__ __forceinline__ uint32_t pack_vert(uint32_t lane, uint32_t kind, uint32_t color) {
+    return (lane & 0xFFFFFFu) | (kind << 24) | (color << 28);
+}
+
+// RowGeometry {height, node_y} + per-row strip flags
+__global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
+                            const float *__restrict__ row_top, float *__restrict__ height, float *__restrict__ node_y,
+                            uint8_t *__restrict__ rowflags) {
+    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    float ht, ny;
+    if (band) {
+        const float b = band[r];
+        ht = roundf(h[r] + b);        // (h + band).round()  (:389)
+        ny = roundf(b + WG_NODE_Y);   // (band + NODE_Y).round() (:390)
+    } else {
+        ht = h[r];                    // build(): height = h, node_y = NODE_Y (:339-341)
+        ny = WG_NODE_Y;
+    }
+    height[r] = ht;
+    node_y[r] = ny;
+    const float top = row_top[r], bot = row_top[r + 1];
+    const float node_abs = top + ny;          // child_y / parent_y of edges at this row (:554-555)
+    uint8_t f = 0;
+    if (bot - top < 1e-4f) f |= RF_ZERO;        // intermediate strip (:577)
+    if (bot - node_abs < 1e-4f) f |= RF_CHILD;  // strip [child_y, row_bot]
+    if (node_abs - top < 1e-4f) f |= RF_PARENT; // strip [row_top, parent_y]
+    rowflags[r] = f;
+}
+
+__global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
+                              uint32_t *cntB, uint32_t *cntT, uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ne) return;
+    const wg_edge e = edges[k];
+    const uint32_t c = e.child_row, p = e.parent_row;
+    if (c >= p) return;                                   // (:526-528)
+    if (e.child_lane == e.parent_lane) {
+        atomicAdd(&cntB[c], 1u);
+        atomicAdd(&cntT[p], 1u);
+        if (c + 1 < p) { atomicAdd(&diffF[c + 1], 1u); atomicAdd(&diffF[p], 0xFFFFFFFFu); }
+    } else {
+        if (c + 1 < p) { atomicAdd(&diffC[c + 1], 1u); atomicAdd(&diffC[p], 0xFFFFFFFFu); }
+        if (!(rowflags[c] & RF_CHILD)) atomicAdd(&cntCend[c], 1u);
+        if (!(rowflags[p] & RF_PARENT)) atomicAdd(&cntCend[p], 1u);
+    }
+}
+
+// per-row totals: nV = nF + nT + nB -> vert_off, nC -> curve_off (scanned after)
+__global__ void k_row_counts(uint64_t n, const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ scanC,
+                             const uint32_t *__restrict__ cntT, const uint32_t *__restrict__ cntB,
+                             const uint32_t *__restrict__ cntCend, const uint8_t *__restrict__ rowflags,
+                             uint32_t *__restrict__ nV, uint32_t *__restrict__ nC) {
+    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t nf = scanF[r + 1];
+    const uint32_t ic = scanC[r + 1];
+    nV[r] = nf + cntT[r] + cntB[r];
+    nC[r] = ((rowflags[r] & RF_ZERO) ? 0u : ic) + cntCend[r];
+}
+
+__global__ void k_bottom(uint64_t n, const uint32_t *__restrict__ edge_off, const wg_edge *__restrict__ edges,
+                         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ scanF,
+                         const uint32_t *__restrict__ cntT, uint32_t *__restrict__ vert) {
+    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    uint32_t o = vert_off[r] + scanF[r + 1] + cntT[r];
+    for (uint32_t k = edge_off[r]; k < edge_off[r + 1]; k++) {
+        const wg_edge e = edges[k];
+        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane)
+            vert[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
+    }
+}
+
+__global__ void k_top_collect(uint64_t ne, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
+                              const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ne) return;
+    const wg_edge e = edges[k];
+    if (!(e.child_row < e.parent_row && e.child_lane == e.parent_lane)) return;
+    const uint32_t p = e.parent_row;
+    const uint32_t pos = atomicAdd(&top_fill[p], 1u);
+    vert[vert_off[p] + scanF[p + 1] + pos] = (uint32_t)k;   // edge id, packed below
+}
+
+__global__ void k_top_finish(uint64_t n, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
+                             const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT, uint32_t *vert) {
+    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t nt = cntT[r];
+    if (nt == 0) return;
+    uint32_t *v = vert + vert_off[r] + scanF[r + 1];
+    for (uint32_t i = 1; i < nt; i++) {   // insertion sort by edge id (in-degree is small)
+        uint32_t x = v[i];
+        uint32_t j = i;
+        while (j > 0 && v[j - 1] > x) { v[j] = v[j - 1]; j--; }
+        v[j] = x;
+    }
+    for (uint32_t i = 0; i < nt; i++) {
+        const wg_edge e = edges[v[i]];
+        v[i] = pack_vert(e.child_lane, WG_VERT_TOP, e.color);
+    }
+}
+
+// ---- carry-in registration for the sweep -------------------------------------
+__global__ void k_carry_diff(uint64_t ne, const wg_edge *__restrict__ edges, uint32_t *diff) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ne) return;
+    const wg_edge e = edges[k];
+    if (e.child_row >= e.parent_row) return;
+    const uint32_t k0 = e.child_row / WG_SWEEP_CH + 1, k1 = e.parent_row / WG_SWEEP_CH;
+    if (k0 <= k1) { atomicAdd(&diff[k0], 1u); atomicAdd(&diff[k1 + 1], 0xFFFFFFFFu); }
+}
+__global__ void k_carry_counts(uint64_t nch, const uint32_t *__restrict__ scan, uint32_t *__restrict__ cnt) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nch) return;
+    cnt[k] = scan[k + 1];
+}
+__global__ void k_carry_fill(uint64_t ne, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ carry_off,
+                             uint32_t *fill, uint32_t *carry) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ne) return;
+    const wg_edge e = edges[k];
+    if (e.child_row >= e.parent_row) return;
+    const uint32_t k0 = e.child_row / WG_SWEEP_CH + 1, k1 = e.parent_row / WG_SWEEP_CH;
+    for (uint32_t q = k0; q <= k1; q++) {
+        const uint32_t pos = atomicAdd(&fill[q], 1u);
+        carry[carry_off[q] + pos] = (uint32_t)k;
+    }
+}
+// rank sort of each chunk's carry list (one wave per chunk; lists are short)
+__global__ void __launch_bounds__(64) k_carry_sort(uint64_t nch, const uint32_t *__restrict__ carry_off,
+                                                    const uint32_t *__restrict__ carry, uint32_t *__restrict__ sorted) {
+    const uint64_t q = blockIdx.x;
+    if (q >= nch) return;
+    const uint32_t a = carry_off[q], b = carry_off[q + 1], len = b - a;
+    for (uint32_t i = threadIdx.x; i < len; i += 64) {
+        const uint32_t x = carry[a + i];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < len; j++) rank += carry[a + j] < x;
+        sorted[a + rank] = x;
+    }
+}
+
+// ---- the sweep ---------------------------------------------------------------------
+constexpr int SW_WAVES = 4;
+constexpr int SW_CAP = 512;
+
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nch, const wg_edge *__restrict__ edges,
+        const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
+        const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
+        const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
+        uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
+        uint32_t *__restrict__ err) {
+    __shared__ uint32_t s_eid[SW_WAVES][SW_CAP];
+    __shared__ uint32_t s_c[SW_WAVES][SW_CAP];
+    __shared__ uint32_t s_p[SW_WAVES][SW_CAP];
+    __shared__ uint32_t s_info[SW_WAVES][SW_CAP];
+    const int w = threadIdx.x >> 6;
+    const uint32_t lid = threadIdx.x & 63;
+    const uint64_t q = (uint64_t)blockIdx.x * SW_WAVES + w;
+    if (q >= nch) return;
+    uint32_t *E = s_eid[w], *C = s_c[w], *P = s_p[w], *I = s_info[w];
+    const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
+    // carry-in edges (alive across R0), sorted by edge id
+    uint32_t cnt = 0;
+    {
+        const uint32_t a = q > 0 ? carry_off[q] : 0u, b = q > 0 ? carry_off[q + 1] : 0u;
+        if (b - a > (uint32_t)SW_CAP) { if (lid == 0) atomicOr(&err[0], 1u); return; }
+        for (uint32_t i = lid; i < b - a; i += 64) {
+            const uint32_t k = carry_sorted[a + i];
+            const wg_edge e = edges[k];
+            E[i] = k; C[i] = e.child_row; P[i] = e.parent_row;
+            I[i] = (e.child_lane & 0xFFFFFFu) | (e.color << 24) | ((e.child_lane == e.parent_lane) ? 0x10000000u : 0u);
+        }
+        cnt = b - a;
+    }
+    for (uint64_t r = R0; r < R1; r++) {
+        // append edges whose child is row r (edge order)
+        const uint32_t e0 = edge_off[r], e1 = edge_off[r + 1];
+        for (uint32_t base = e0; base < e1; base += 64) {
+            const uint32_t k = base + lid;
+            bool take = false;
+            wg_edge e;
+            if (k < e1) { e = edges[k]; take = e.child_row < e.parent_row; }
+            const uint64_t m = __ballot(take);
+            if (cnt + __builtin_popcountll(m) > (uint32_t)SW_CAP) { if (lid == 0) atomicOr(&err[0], 1u); return; }
+            if (take) {
+                const uint32_t pos = cnt + mbcnt(m);
+                E[pos] = k; C[pos] = e.child_row; P[pos] = e.parent_row;
+                I[pos] = (e.child_lane & 0xFFFFFFu) | (e.color << 24) | ((e.child_lane == e.parent_lane) ? 0x10000000u : 0u);
+            }
+            cnt += __builtin_popcountll(m);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint8_t rf = rowflags[r];
+        uint32_t fbase = vert_off[r], cbase = curve_off[r], kept = 0;
+        for (uint32_t base = 0; base < cnt; base += 64) {
+            const uint32_t idx = base + lid;
+            const bool act = idx < cnt;
+            uint32_t eid = 0, c = 0, p = 0, info = 0;
+            if (act) { eid = E[idx]; c = C[idx]; p = P[idx]; info = I[idx]; }
+            __builtin_amdgcn_wave_barrier();
+            const bool same = (info & 0x10000000u) != 0;
+            const bool full = act && same && c < r && r < p;
+            bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
+            const bool curv = act && !same && c <= r && r <= p && !skip;
+            const bool keep = act && p > r;
+            const uint64_t mf = __ballot(full), mc = __ballot(curv), mk = __ballot(keep);
+            if (full) vert[fbase + mbcnt(mf)] = pack_vert(info & 0xFFFFFFu, WG_VERT_FULL, (info >> 24) & 0xFu);
+            if (curv) { const uint32_t o = cbase + mbcnt(mc); curve_ref[o] = eid; curve_row[o] = (uint32_t)r; }
+            if (keep) {
+                const uint32_t o = kept + mbcnt(mk);
+                E[o] = eid; C[o] = c; P[o] = p; I[o] = info;
+            }
+            fbase += __builtin_popcountll(mf);
+            cbase += __builtin_popcountll(mc);
+            kept += __builtin_popcountll(mk);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+        }
+        cnt = kept;
+    }
+}
+
+// ---- Cubic (:614-695), exact f32 operation order ---------------------------------
+struct Pt { float x, y; };
+struct Cubic { Pt p0, p1, p2, p3; };
+
+__device__ __forceinline__ float y_at(const Cubic &c, float t) {   // :623-629
+    const float s = 1.0f - t;
+    return s * s * s * c.p0.y + 3.0f * s * s * t * c.p1.y + 3.0f * s * t * t * c.p2.y + t * t * t * c.p3.y;
+}
+__device__ __forceinline__ float t_at_y(const Cubic &c, float target) {   // :635-654
+    if (target <= c.p0.y) return 0.0f;
+    if (target >= c.p3.y) return 1.0f;
+    float lo = 0.0f, hi = 1.0f;
+    for (int i = 0; i < 40; i++) {
+        const float mid = (lo + hi) * 0.5f;
+        const float y = y_at(c, mid);
+        if (y < target) lo = mid; else hi = mid;
+    }
+    return (lo + hi) * 0.5f;
+}
+__device__ __forceinline__ Pt lerp(Pt a, Pt b, float t) { return Pt{a.x + (b.x - a.x) * t, a.y + (b.y - a.y) * t}; }
+__device__ __forceinline__ void split(const Cubic &c, float t, Cubic *left, Cubic *right) {   // :656-678
+    const Pt q01 = lerp(c.p0, c.p1, t), q12 = lerp(c.p1, c.p2, t), q23 = lerp(c.p2, c.p3, t);
+    const Pt r012 = lerp(q01, q12, t), r123 = lerp(q12, q23, t);
+    const Pt s = lerp(r012, r123, t);
+    if (left) *left = Cubic{c.p0, q01, r012, s};
+    if (right) *right = Cubic{s, r123, q23, c.p3};
+}
+__device__ __forceinline__ float clamp_rs(float x, float lo, float hi) {
+    if (x < lo) x = lo;
+    if (x > hi) x = hi;
+    return x;
+}
+__device__ __forceinline__ Cubic subcurve(const Cubic &c, float a, float b) {   // :683-694
+    if (a <= 0.0f && b >= 1.0f) return c;
+    Cubic right, left;
+    split(c, clamp_rs(a, 0.0f, 1.0f), nullptr, &right);
+    if (b >= 1.0f) return right;
+    const float new_t = clamp_rs((b - a) / (1.0f - a), 0.0f, 1.0f);
+    split(right, new_t, &left, nullptr);
+    return left;
+}
+
+__global__ void k_curves(uint64_t nc, const uint32_t *__restrict__ curve_ref, const uint32_t *__restrict__ curve_row,
+                         const wg_edge *__restrict__ edges, const float *__restrict__ row_top,
+                         const float *__restrict__ node_y, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nc) return;
+    const wg_edge e = edges[curve_ref[k]];
+    const uint32_t row = curve_row[k];
+    const float child_y = row_top[e.child_row] + node_y[e.child_row];     // :554
+    const float parent_y = row_top[e.parent_row] + node_y[e.parent_row];  // :555
+    const float dy = parent_y - child_y;
+    Cubic cv;
+    cv.p0 = Pt{(float)e.child_lane, child_y};
+    cv.p1 = Pt{(float)e.child_lane, child_y + dy * 0.4f};
+    cv.p2 = Pt{(float)e.parent_lane, parent_y - dy * 0.4f};
+    cv.p3 = Pt{(float)e.parent_lane, parent_y};
+    const float rtop = row_top[row], rbot = row_top[row + 1];
+    const float strip_top = (row == e.child_row) ? child_y : rtop;
+    const float strip_bot = (row == e.parent_row) ? parent_y : rbot;
+    const float t_a = (row == e.child_row) ? 0.0f : t_at_y(cv, strip_top);
+    const float t_b = (row == e.parent_row) ? 1.0f : t_at_y(cv, strip_bot);
+    const Cubic s = subcurve(cv, t_a, t_b);
+    float4 *o = reinterpret_cast<float4 *>(out + k);
+    o[0] = make_float4(s.p0.x, s.p0.y - rtop, s.p1.x, s.p1.y - rtop);
+    o[1] = make_float4(s.p2.x, s.p2.y - rtop, s.p3.x, s.p3.y - rtop);
+    out_color[k] = (uint8_t)e.color;
+}
+
+inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
+
+}  // namespace
+
+int wg_stage_geometry(wg_ctx *c, const float *d_band) {
+    const uint64_t n = c->n, ne = c->n_edges;
+    hipStream_t s = c->stream;
+    WG_ALLOC(c, c->g_height, n * 4 + 4);
+    WG_ALLOC(c, c->g_node_y, n * 4 + 4);
+    WG_ALLOC(c, c->rowflags, n + 4);
+    WG_ALLOC(c, c->cntF, (n + 2) * 4);
+    WG_ALLOC(c, c->cntT, (n + 2) * 4);
+    WG_ALLOC(c, c->cntB, (n + 2) * 4);
+    WG_ALLOC(c, c->cntC, (n + 2) * 4);
+    WG_ALLOC(c, c->cntCend, (n + 2) * 4);
+    WG_ALLOC(c, c->vert_off, (n + 2) * 4);
+    WG_ALLOC(c, c->curve_off, (n + 2) * 4);
+    WG_ALLOC(c, c->top_fill, (n + 2) * 4);
+    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(n + 2));
+    WG_ALLOC(c, c->sweep_err, 64);
+    c->n_vert = c->n_curve = 0;
+    if (n == 0) {
+        WG_HIP(c, hipMemsetAsync(c->vert_off.p, 0, 4, s));
+        WG_HIP(c, hipMemsetAsync(c->curve_off.p, 0, 4, s));
+        return WG_OK;
+    }
+    const float *h = c->heights.as<const float>();
+    const float *rt = c->g_row_top.as<const float>();
+    const wg_edge *E = c->edges.as<const wg_edge>();
+    const uint32_t *edge_off = c->edge_cnt.as<const uint32_t>();
+    uint32_t *cntF = c->cntF.as<uint32_t>(), *cntT = c->cntT.as<uint32_t>(), *cntB = c->cntB.as<uint32_t>();
+    uint32_t *cntC = c->cntC.as<uint32_t>(), *cntCend = c->cntCend.as<uint32_t>();
+    uint32_t *voff = c->vert_off.as<uint32_t>(), *coff = c->curve_off.as<uint32_t>();
+
+    wg_stage_begin(c, "geom_counts");
+    WG_HIP(c, hipMemsetAsync(cntF, 0, (n + 2) * 4, s));
+    WG_HIP(c, hipMemsetAsync(cntT, 0, (n + 2) * 4, s));
+    WG_HIP(c, hipMemsetAsync(cntB, 0, (n + 2) * 4, s));
+    WG_HIP(c, hipMemsetAsync(cntC, 0, (n + 2) * 4, s));
+    WG_HIP(c, hipMemsetAsync(cntCend, 0, (n + 2) * 4, s));
+    WG_HIP(c, hipMemsetAsync(c->top_fill.p, 0, (n + 2) * 4, s));
+    WG_HIP(c, hipMemsetAsync(c->sweep_err.p, 0, 64, s));
+    hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
+                       c->g_node_y.as<float>(), c->rowflags.as<uint8_t>());
+    if (ne)
+        hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, c->rowflags.as<const uint8_t>(), cntB,
+                           cntT, cntF, cntC, cntCend);
+    WG_HIP(c, wg_exclusive_scan_u32(cntF, cntF, n + 1, c->scan_tmp.p, s));
+    WG_HIP(c, wg_exclusive_scan_u32(cntC, cntC, n + 1, c->scan_tmp.p, s));
+    hipLaunchKernelGGL(k_row_counts, dim3(blocks(n)), dim3(T), 0, s, n, cntF, cntC, cntT, cntB, cntCend,
+                       c->rowflags.as<const uint8_t>(), voff, coff);
+    WG_HIP(c, wg_exclusive_scan_u32(voff, voff, n, c->scan_tmp.p, s));
+    WG_HIP(c, wg_exclusive_scan_u32(coff, coff, n, c->scan_tmp.p, s));
+    // carry-in registration
+    const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
+    WG_ALLOC(c, c->carry_cnt, (nch + 2) * 4);
+    WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
+    WG_ALLOC(c, c->carry_fill, (nch + 2) * 4);
+    WG_HIP(c, hipMemsetAsync(c->carry_cnt.p, 0, (nch + 2) * 4, s));
+    WG_HIP(c, hipMemsetAsync(c->carry_fill.p, 0, (nch + 2) * 4, s));
+    if (ne) hipLaunchKernelGGL(k_carry_diff, dim3(blocks(ne)), dim3(T), 0, s, ne, E, c->carry_cnt.as<uint32_t>());
+    WG_HIP(c, wg_exclusive_scan_u32(c->carry_cnt.as<uint32_t>(), c->carry_cnt.as<uint32_t>(), nch + 1, c->scan_tmp.p, s));
+    hipLaunchKernelGGL(k_carry_counts, dim3(blocks(nch)), dim3(T), 0, s, nch, c->carry_cnt.as<const uint32_t>(),
+                       c->carry_off.as<uint32_t>());
+    WG_HIP(c, wg_exclusive_scan_u32(c->carry_off.as<uint32_t>(), c->carry_off.as<uint32_t>(), nch, c->scan_tmp.p, s));
+    uint32_t tot[3] = {0, 0, 0};
+    WG_HIP(c, hipMemcpyAsync(&tot[0], voff + n, 4, hipMemcpyDeviceToHost, s));
+    WG_HIP(c, hipMemcpyAsync(&tot[1], coff + n, 4, hipMemcpyDeviceToHost, s));
+    WG_HIP(c, hipMemcpyAsync(&tot[2], c->carry_off.as<uint32_t>() + nch, 4, hipMemcpyDeviceToHost, s));
+    WG_HIP(c, hipStreamSynchronize(s));
+    wg_stage_end(c);
+    c->n_vert = tot[0];
+    c->n_curve = tot[1];
+    const uint64_t ncarry = tot[2];
+    WG_ALLOC(c, c->vert, c->n_vert * 4 + 16);
+    WG_ALLOC(c, c->curve, c->n_curve * sizeof(wg_curve) + 64);
+    WG_ALLOC(c, c->curve_color, c->n_curve + 16);
+    WG_ALLOC(c, c->curve_ref, c->n_curve * 4 + 16);
+    WG_ALLOC(c, c->curve_row, c->n_curve * 4 + 16);
+    WG_ALLOC(c, c->carry, ncarry * 8 + 16);
+
+    wg_stage_begin(c, "geom_lists");
+    uint32_t *vert = c->vert.as<uint32_t>();
+    hipLaunchKernelGGL(k_bottom, dim3(blocks(n)), dim3(T), 0, s, n, edge_off, E, voff, cntF, cntT, vert);
+    if (ne) {
+        hipLaunchKernelGGL(k_top_collect, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, c->top_fill.as<uint32_t>(), vert);
+        hipLaunchKernelGGL(k_carry_fill, dim3(blocks(ne)), dim3(T), 0, s, ne, E, c->carry_off.as<const uint32_t>(),
+                           c->carry_fill.as<uint32_t>(), c->carry.as<uint32_t>());
+    }
+    hipLaunchKernelGGL(k_top_finish, dim3(blocks(n)), dim3(T), 0, s, n, E, voff, cntF, cntT, vert);
+    uint32_t *carry_sorted = c->carry.as<uint32_t>() + ncarry + 2;
+    hipLaunchKernelGGL(k_carry_sort, dim3(nch), dim3(64), 0, s, nch, c->carry_off.as<const uint32_t>(),
+                       c->carry.as<const uint32_t>(), carry_sorted);
+    hipLaunchKernelGGL(k_sweep, dim3((nch + SW_WAVES - 1) / SW_WAVES), dim3(64 * SW_WAVES), 0, s, n, nch, E, edge_off,
+                       c->carry_off.as<const uint32_t>(), (const uint32_t *)carry_sorted, c->rowflags.as<const uint8_t>(),
+                       voff, coff, vert, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), c->sweep_err.as<uint32_t>());
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    wg_stage_begin(c, "geom_curves");
+    if (c->n_curve)
+        hipLaunchKernelGGL(k_curves, dim3(blocks(c->n_curve)), dim3(T), 0, s, c->n_curve, c->curve_ref.as<const uint32_t>(),
+                           c->curve_row.as<const uint32_t>(), E, rt, c->g_node_y.as<const float>(), c->curve.as<wg_curve>(),
+                           c->curve_color.as<uint8_t>());
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    uint32_t err = 0;
+    WG_HIP(c, hipMemcpyAsync(&err, c->sweep_err.p, 4, hipMemcpyDeviceToHost, s));
+    float total = 0.0f;
+    WG_HIP(c, hipMemcpyAsync(&total, rt + n, 4, hipMemcpyDeviceToHost, s));
+    uint32_t rtf[4] = {0, 0, 0, 0};
+    WG_HIP(c, hipMemcpyAsync(rtf, c->rt_flags.p, 16, hipMemcpyDeviceToHost, s));
+    WG_HIP(c, hipStreamSynchronize(s));
+    if (err) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP);
+    c->total_height = total;
+    c->scan_path = rtf[2] ? 1u : 0u;
+    return WG_OK;
+}

@@ -1,0 +1,113 @@
+// wg_hash.hip — oid -> row hash join on the GPU.
+//
+// Replaces `commit_set: HashMap<Oid, ()>` and `row_by_oid: HashMap<Oid, usize>`
+// (commit_graph.rs:272-274; looked up at :306-311, :441, :448).  One
+// open-addressing table in HBM, 8-byte entries {fingerprint:32 | row:32}.
+// `collect()` lets the LAST occurrence of a duplicate id win (:273-274),
+// reproduced with atomicMax on entries of the same key (same fingerprint,
+// full 20-byte compare).  Outputs:
+//   canon[i]  = last row whose id equals row i's id
+//   prow[k]   = canonical row of parent reference k, or -1 if not in the list
+#include "wg_internal.h"
+
+namespace {
+
+constexpr uint64_t HEMPTY = ~0ull;
+
+struct Key { uint32_t w[5]; };
+
+__device__ __forceinline__ Key load_key(const uint8_t *p) {
+    // ids are 20-byte records in hipMalloc'd arrays: 4-byte aligned
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+    Key k;
+#pragma unroll
+    for (int i = 0; i < 5; i++) k.w[i] = q[i];
+    return k;
+}
+__device__ __forceinline__ bool key_eq(const Key &a, const uint8_t *p) {
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p);
+    return a.w[0] == q[0] && a.w[1] == q[1] && a.w[2] == q[2] && a.w[3] == q[3] && a.w[4] == q[4];
+}
+__device__ __forceinline__ uint64_t key_hash(const Key &k) {
+    uint64_t h = ((uint64_t)k.w[1] << 32 | k.w[0]) ^ ((uint64_t)k.w[3] * 0x9E3779B97F4A7C15ull) ^ k.w[4];
+    h ^= h >> 31; h *= 0x7FB5D329728EA185ull; h ^= h >> 27; h *= 0x81DADEF4BC2DD44Dull; h ^= h >> 33;
+    return h;
+}
+__device__ __forceinline__ uint32_t key_fp(const Key &k) { return k.w[2] ^ (k.w[4] * 0x85EBCA6Bu); }
+
+__global__ void k_hash_insert(const uint8_t *__restrict__ oid, uint64_t n, unsigned long long *table, uint64_t mask) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Key k = load_key(oid + i * 20);
+    const uint32_t fp = key_fp(k);
+    const unsigned long long mine = ((unsigned long long)fp << 32) | (uint32_t)i;
+    uint64_t h = key_hash(k) & mask;
+    for (uint64_t probes = 0; probes <= mask; probes++) {
+        unsigned long long cur = table[h];
+        if (cur == HEMPTY) {
+            unsigned long long prev = atomicCAS(&table[h], HEMPTY, mine);
+            if (prev == HEMPTY) return;
+            cur = prev;
+        }
+        if ((uint32_t)(cur >> 32) == fp && key_eq(k, oid + (uint64_t)(uint32_t)cur * 20)) {
+            atomicMax(&table[h], mine);    // same key: the last row wins (:273-274)
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ int64_t hash_lookup(const Key &k, const uint8_t *__restrict__ oid,
+                                               const unsigned long long *__restrict__ table, uint64_t mask) {
+    const uint32_t fp = key_fp(k);
+    uint64_t h = key_hash(k) & mask;
+    for (uint64_t probes = 0; probes <= mask; probes++) {
+        unsigned long long cur = table[h];
+        if (cur == HEMPTY) return -1;
+        if ((uint32_t)(cur >> 32) == fp && key_eq(k, oid + (uint64_t)(uint32_t)cur * 20)) return (int64_t)(uint32_t)cur;
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+__global__ void k_canon(const uint8_t *__restrict__ oid, uint64_t n, const unsigned long long *__restrict__ table,
+                        uint64_t mask, uint32_t *__restrict__ canon) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t r = hash_lookup(load_key(oid + i * 20), oid, table, mask);
+    canon[i] = r < 0 ? (uint32_t)i : (uint32_t)r;
+}
+
+__global__ void k_probe_parents(const uint8_t *__restrict__ poid, uint64_t e, const uint8_t *__restrict__ oid,
+                                const unsigned long long *__restrict__ table, uint64_t mask, int32_t *__restrict__ prow) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= e) return;
+    prow[k] = (int32_t)hash_lookup(load_key(poid + k * 20), oid, table, mask);
+}
+
+}  // namespace
+
+int wg_stage_hash_join(wg_ctx *c) {
+    const uint64_t n = c->n, e = c->e_refs;
+    uint64_t cap = 1024;
+    while (cap < 2 * n) cap <<= 1;
+    c->hcap = cap;
+    WG_ALLOC(c, c->hash, cap * 8);
+    WG_ALLOC(c, c->canon, n * 4 + 4);
+    WG_ALLOC(c, c->prow, e * 4 + 4);
+    wg_stage_begin(c, "hash_join");
+    WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8, c->stream));
+    const int T = 256;
+    if (n) {
+        hipLaunchKernelGGL(k_hash_insert, dim3((n + T - 1) / T), dim3(T), 0, c->stream, c->d_oid, n,
+                           c->hash.as<unsigned long long>(), cap - 1);
+        hipLaunchKernelGGL(k_canon, dim3((n + T - 1) / T), dim3(T), 0, c->stream, c->d_oid, n,
+                           c->hash.as<const unsigned long long>(), cap - 1, c->canon.as<uint32_t>());
+    }
+    if (e)
+        hipLaunchKernelGGL(k_probe_parents, dim3((e + T - 1) / T), dim3(T), 0, c->stream, c->d_poid, e, c->d_oid,
+                           c->hash.as<const unsigned long long>(), cap - 1, c->prow.as<int32_t>());
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    return WG_OK;
+}

@@ -1,0 +1,157 @@
+// wg_internal.h — engine-internal declarations shared by the HIP sources.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "wgraph.h"
+
+#define WG_EMPTY 0xFFFFFFFFu   // "None" slot / empty hash entry / no row
+
+// ---------------------------------------------------------------------------
+// Device buffer that only grows (keeps HBM resident across frames).
+// ---------------------------------------------------------------------------
+struct DevBuf {
+    void  *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) { hipError_t e = hipFree(p); p = nullptr; cap = 0; if (e != hipSuccess) return e; }
+        size_t b = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&p, b);
+        if (e == hipSuccess) cap = b;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+struct StageTimer {
+    const char *name;
+    hipEvent_t  a, b;
+};
+
+// Row-top transducer scan geometry (wg_rowtop.hip)
+#define WG_RT_CHUNK   1024   // rows per chunk
+#define WG_RT_NBIN    4      // binades tabulated per chunk (guess-1 .. guess+2)
+
+// Sweep geometry (wg_geom.hip)
+#define WG_SWEEP_CH   64     // rows per sweep chunk (one wave)
+#define WG_SWEEP_CAP  2048   // active-edge capacity per wave (LDS)
+
+// Vertex tiles (wg_vertex.hip)
+#define WG_VTX_TILE   1536   // vertices per workgroup tile (36 KiB of LDS)
+
+struct wg_ctx {
+    int         device = 0;
+    hipStream_t stream = nullptr;
+    bool        own_stream = false;
+    std::string err;
+
+    // ---- last layout build -------------------------------------------------
+    uint64_t n = 0, e_refs = 0, n_edges = 0;
+    bool     have_layout = false;
+    uint32_t max_lane = 0, n_slots = 0, lane_path = 1;
+    float    graph_width = 24.0f;
+    // inputs (device copies when the caller passed host memory)
+    DevBuf in_oid, in_time, in_poff, in_poid, in_flags;
+    const uint8_t  *d_oid = nullptr;
+    const int64_t  *d_time = nullptr;
+    const uint32_t *d_poff = nullptr;
+    const uint8_t  *d_poid = nullptr;
+    const uint8_t  *d_flags = nullptr;
+    // hash join
+    DevBuf hash;            // uint64 [hcap]  (fingerprint<<32 | row)
+    uint64_t hcap = 0;
+    DevBuf canon;           // uint32 [N]  last row holding the same id
+    DevBuf prow;            // int32  [E]  canonical parent row or -1
+    // lanes
+    DevBuf lane_asg;        // uint32 [N]  lane assigned while processing row
+    DevBuf lane_out;        // uint32 [N]  layouts.get(id).lane per row
+    DevBuf color_out;       // uint8  [N]
+    DevBuf lane_scalars;    // uint32 [8]  max_lane, n_slots, overflow, ...
+    // edges
+    DevBuf edge_cnt;        // uint32 [N+1] -> edge_off after scan
+    DevBuf edges;           // wg_edge [n_edges]
+    // heights
+    DevBuf heights;         // float [N]
+    // ---- geometry ------------------------------------------------------------
+    bool     have_geom = false;
+    uint64_t n_vert = 0, n_curve = 0;
+    uint32_t scan_path = 0;
+    float    total_height = 0.0f;
+    DevBuf band;            // float [N] device copy of caller bands
+    DevBuf g_height, g_node_y, g_row_top;   // float [N], [N], [N+1]
+    DevBuf rt_chunk;        // per-chunk scan state
+    DevBuf rt_tables;       // per-chunk transducer tables
+    DevBuf rt_flags;        // uint32 [4]
+    DevBuf cntF, cntT, cntB, cntC, cntCend; // uint32 [N+1] per-row counts / diff arrays
+    DevBuf vert_off, curve_off;             // uint32 [N+1]
+    DevBuf vert, curve, curve_color;
+    DevBuf curve_ref;       // uint32 [n_curve] edge id per curve record
+    DevBuf curve_row;       // uint32 [n_curve] row per curve record
+    DevBuf top_fill;        // uint32 [N]
+    DevBuf carry_cnt, carry_off, carry;     // sweep carry-in lists
+    DevBuf scan_tmp;        // scan workspace
+    DevBuf scal;            // uint64 [16] device scalars (totals)
+    DevBuf rowflags;        // uint8 [N] bit0 zero-height strip, bit1 child strip empty, bit2 parent strip empty
+    DevBuf carry_fill;      // uint32 [nch]
+    DevBuf sweep_err;       // uint32 [4]
+    // ---- vertices -------------------------------------------------------------
+    bool     have_vtx = false;
+    uint64_t vrow_begin = 0, vrow_end = 0, n_vtx = 0;
+    int64_t  selected = -1;
+    DevBuf vtx_off;         // uint64 [rows+1]
+    DevBuf vtx;             // wg_vertex [n_vtx]
+    DevBuf palette;         // float [32]
+    DevBuf chk;             // uint64 [1]
+    // ---- host-side tables --------------------------------------------------------
+    uint32_t h_thresh[32];  // delta thresholds for heights 29..56
+    // ---- timing ----------------------------------------------------------------------
+    bool       timing = false;
+    StageTimer stages[WG_STAGE_MAX];
+    int        n_stages = 0;
+    uint64_t   scratch_host[16];
+};
+
+// error helpers -------------------------------------------------------------
+int wg_fail(wg_ctx *c, int code, const char *fmt, ...);
+#define WG_HIP(ctx, call)                                                          \
+    do {                                                                           \
+        hipError_t _e = (call);                                                    \
+        if (_e != hipSuccess)                                                      \
+            return wg_fail((ctx), WG_E_HIP, "%s:%d %s: %s", __FILE__, __LINE__,    \
+                           #call, hipGetErrorString(_e));                          \
+    } while (0)
+#define WG_ALLOC(ctx, buf, bytes)                                                  \
+    do {                                                                           \
+        hipError_t _e = (buf).ensure(bytes);                                       \
+        if (_e != hipSuccess)                                                      \
+            return wg_fail((ctx), WG_E_NOMEM, "hipMalloc(%zu) failed: %s",         \
+                           (size_t)(bytes), hipGetErrorString(_e));                \
+    } while (0)
+
+// stage timing
+void wg_stage_begin(wg_ctx *c, const char *name);
+void wg_stage_end(wg_ctx *c);
+
+// scans (wg_scan.hip) -----------------------------------------------------------
+// Exclusive scan of n uint32 in place into out[0..n] (out[n] = total).  The
+// input may alias out.  tmp must hold wg_scan_tmp_bytes(n).
+size_t wg_scan_tmp_bytes(uint64_t n);
+hipError_t wg_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, void *tmp, hipStream_t s);
+hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, hipStream_t s);
+
+// stages -------------------------------------------------------------------------
+int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
+int wg_stage_lanes(wg_ctx *c);                // wg_lanes.hip
+int wg_stage_edges(wg_ctx *c);                // wg_lanes.hip
+int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
+int wg_stage_rowtop(wg_ctx *c, const float *d_band);   // wg_rowtop.hip
+int wg_stage_geometry(wg_ctx *c, const float *d_band); // wg_geom.hip
+int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel);  // wg_vertex.hip
+int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out);  // wg_vertex.hip
+void wg_init_height_thresholds(uint32_t *th);  // wg_rowtop.hip

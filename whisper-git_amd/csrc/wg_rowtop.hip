@@ -1,0 +1,403 @@
+// wg_rowtop.hip — row heights and the sequential-f32 row_top_y prefix
+// (SURVEY.md §8a A6-A7).
+//
+// Heights: compute_row_heights (commit_graph.rs:486-507) maps each time gap
+// through an f64 log to round(28 + 28 * (f32)ratio).  The map is monotone in
+// the integer gap, so the host tabulates the 28 exact gap thresholds once
+// (same libm log, same f32 rounding) and the device counts thresholds
+// passed: bit-exact by construction, no transcendental on the GPU.
+//
+// row_top_y: `acc += h + band` in f32, strictly sequential (:329-335,
+// :374-381).  Past 2^24 px every add rounds, so a plain prefix sum is wrong.
+// Within one binade [2^k, 2^k+1) (ulp u) the rounding of acc + s depends on
+// acc only through the parity of acc/u (ties-to-even), so each row is a
+// 2-state transducer {parity -> (ulps added, new parity)}; transducers
+// compose associatively.  The scan runs in three parallel kernels plus one
+// single-wave walk:
+//   rt_sum     per 1024-row chunk: f64 sum of steps, validity flags
+//   rt_prefix  f64 prefix of chunk sums -> guessed binade per chunk
+//   rt_tables  per chunk, 4 candidate binades: composed chunk transducer
+//   rt_walk    one wave composes 64 chunk transducers per step (ordered
+//              shuffle scan) from the exact running f32 value; a chunk in
+//              which acc crosses a binade (a handful per run) is replayed
+//              serially by the wave
+//   rt_rows    per chunk: block scan of row transducers from the chunk's
+//              exact start -> row_top for every row
+// Steps that are negative / non-finite make the walk replay every chunk
+// serially (exact, slow; flagged in wg_geometry_summary.scan_path).
+#include <cmath>
+
+#include "wg_internal.h"
+
+namespace {
+
+constexpr int RT_T = 256;                 // threads per chunk block
+constexpr int RT_Q = WG_RT_CHUNK / RT_T;  // rows per thread (4)
+
+struct RtChunk {
+    double   sum;     // f64 sum of steps in the chunk
+    double   prefix;  // f64 exclusive prefix (guess only)
+    int32_t  kguess;  // binade of prefix
+    uint32_t mode;    // 0 = table path, 1 = replayed serially by the walk
+    float    start;   // exact f32 acc at chunk start (mode 0)
+    int32_t  kstart;  // binade of start (mode 0)
+};
+
+// 2-state transducer: parity p -> (d[p] ulps, o[p]); bit2 of f = valid
+struct Td {
+    uint32_t d0, d1, f;   // f: bit0 = o0, bit1 = o1, bit2 = valid
+};
+__device__ __forceinline__ Td td_identity() { return Td{0u, 0u, 0x2u | 0x4u}; }
+__device__ __forceinline__ Td td_invalid() { return Td{0u, 0u, 0x2u}; }
+// apply A then B
+__device__ __forceinline__ Td td_compose(const Td &A, const Td &B) {
+    const uint32_t a0 = A.f & 1u, a1 = (A.f >> 1) & 1u;
+    Td r;
+    r.d0 = A.d0 + (a0 ? B.d1 : B.d0);
+    r.d1 = A.d1 + (a1 ? B.d1 : B.d0);
+    const uint32_t o0 = (B.f >> a0) & 1u, o1 = (B.f >> a1) & 1u;
+    r.f = o0 | (o1 << 1) | (A.f & B.f & 4u);
+    return r;
+}
+__device__ __forceinline__ Td td_shfl_up(const Td &v, int d) {
+    return Td{(uint32_t)__shfl_up((int)v.d0, d, 64), (uint32_t)__shfl_up((int)v.d1, d, 64),
+              (uint32_t)__shfl_up((int)v.f, d, 64)};
+}
+__device__ __forceinline__ Td td_shfl_down(const Td &v, int d) {
+    return Td{(uint32_t)__shfl_down((int)v.d0, d, 64), (uint32_t)__shfl_down((int)v.d1, d, 64),
+              (uint32_t)__shfl_down((int)v.f, d, 64)};
+}
+
+// The step at binade k: acc = 2^k + p*u represents every acc of parity p.
+__device__ __forceinline__ Td row_td(float s, int k) {
+    if (k < -100 || k > 126) return td_invalid();
+    const float base = ldexpf(1.0f, k), u = ldexpf(1.0f, k - 23), top = ldexpf(1.0f, k + 1);
+    Td t;
+    t.f = 4u;
+    {
+        const float a = base, r = a + s;
+        if (!(r < top)) return td_invalid();
+        t.d0 = (uint32_t)((r - a) / u);
+        t.f |= ((uint32_t)((r - base) / u)) & 1u;
+    }
+    {
+        const float a = base + u, r = a + s;
+        if (!(r < top)) return td_invalid();
+        t.d1 = (uint32_t)((r - a) / u);
+        t.f |= (((uint32_t)((r - base) / u)) & 1u) << 1;
+    }
+    return t;
+}
+
+__device__ __forceinline__ float step_of(const float *__restrict__ h, const float *__restrict__ band, uint64_t i) {
+    return band ? h[i] + band[i] : h[i] + 0.0f;   // `h + band` (:379); build() adds 0
+}
+
+__device__ __forceinline__ int binade_of(float a) { return ilogbf(a); }
+
+// ---------------------------------------------------------------------------
+// heights
+// ---------------------------------------------------------------------------
+struct Thresh { uint32_t t[28]; };
+
+__global__ void k_heights(uint64_t n, const int64_t *__restrict__ time, Thresh th, float *__restrict__ h) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float out = WG_ROW_HEIGHT;
+    if (i + 1 < n) {
+        const uint64_t d = (uint64_t)time[i] - (uint64_t)time[i + 1];   // wrapping i64 sub
+        uint64_t ad = ((int64_t)d < 0) ? (0ull - d) : d;                // unsigned_abs
+        if (ad > 2592000ull) ad = 2592000ull;                             // .min(TIME_MAX_DELTA)
+        uint32_t hh = 28;
+#pragma unroll
+        for (int k = 0; k < 28; k++) hh += (uint32_t)(ad >= (uint64_t)th.t[k]);
+        out = (float)hh;
+    }
+    h[i] = out;
+}
+
+// ---------------------------------------------------------------------------
+// row_top scan
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(RT_T) k_rt_sum(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
+                                                 RtChunk *__restrict__ ch, uint32_t *__restrict__ flags) {
+    const uint64_t c = blockIdx.x;
+    const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
+    double sum = 0.0;
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < RT_Q; q++) {
+        const uint64_t i = r0 + q;
+        if (i < n) {
+            const float s = step_of(h, band, i);
+            bad |= !(s >= 0.0f) || !isfinite(s);
+            sum += (double)s;
+        }
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
+    __shared__ double ws[RT_T / 64];
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_down(sum, d, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < RT_T / 64; w++) t += ws[w];
+        ch[c].sum = t;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__restrict__ ch) {
+    __shared__ double ws[16];
+    __shared__ double carry;
+    if (threadIdx.x == 0) carry = 0.0;
+    __syncthreads();
+    for (uint64_t base = 0; base < nch; base += 1024) {
+        const uint64_t c = base + threadIdx.x;
+        const double v = c < nch ? ch[c].sum : 0.0;
+        double inc = v;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        for (int d = 1; d < 64; d <<= 1) {
+            double o = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += o;
+        }
+        if (lane == 63) ws[w] = inc;
+        __syncthreads();
+        double wb = 0.0, tot = 0.0;
+        for (int k = 0; k < 16; k++) { if (k < w) wb += ws[k]; tot += ws[k]; }
+        const double pre = carry + wb + inc - v;
+        if (c < nch) {
+            ch[c].prefix = pre;
+            ch[c].kguess = pre > 0.0 ? ilogb(pre) : -1000;
+            ch[c].mode = 1;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) carry += tot;
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(RT_T) k_rt_tables(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
+                                                    const RtChunk *__restrict__ ch, uint4 *__restrict__ tables) {
+    const uint64_t c = blockIdx.x;
+    const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
+    float s[RT_Q];
+#pragma unroll
+    for (int q = 0; q < RT_Q; q++) s[q] = (r0 + q < n) ? step_of(h, band, r0 + q) : -1.0f;
+    __shared__ Td wt[RT_T / 64];
+    const int kg = ch[c].kguess;
+    for (int b = 0; b < WG_RT_NBIN; b++) {
+        const int k = kg - 1 + b;
+        Td t = td_identity();
+#pragma unroll
+        for (int q = 0; q < RT_Q; q++)
+            if (r0 + q < n) t = td_compose(t, row_td(s[q], k));
+        // ordered wave reduction: lane i absorbs [i, i+2d)
+        for (int d = 1; d < 64; d <<= 1) {
+            Td o = td_shfl_down(t, d);
+            if (((threadIdx.x & 63) & (2 * d - 1)) == 0 && (threadIdx.x & 63) + d < 64) t = td_compose(t, o);
+        }
+        if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            Td a = wt[0];
+            for (int w = 1; w < RT_T / 64; w++) a = td_compose(a, wt[w]);
+            tables[c * WG_RT_NBIN + b] = make_uint4(a.d0, a.d1, a.f, 0u);
+        }
+        __syncthreads();
+    }
+}
+
+// Replay rows [r0, r1) serially from acc (one wave; steps prefetched 64 at a time).
+__device__ float serial_rows(uint64_t r0, uint64_t r1, float acc, const float *__restrict__ h,
+                             const float *__restrict__ band, float *__restrict__ row_top) {
+    const int lid = threadIdx.x & 63;
+    for (uint64_t base = r0; base < r1; base += 64) {
+        const uint64_t i = base + lid;
+        const float sv = i < r1 ? step_of(h, band, i) : 0.0f;
+        float mine = 0.0f;
+        const int cnt = (int)((r1 - base) < 64 ? (r1 - base) : 64);
+        for (int j = 0; j < cnt; j++) {
+            const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sv), j));
+            if (lid == j) mine = acc;
+            acc = acc + sj;
+        }
+        if (i < r1) row_top[i] = mine;
+    }
+    return acc;
+}
+
+__global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const float *__restrict__ h,
+                                                const float *__restrict__ band, RtChunk *__restrict__ ch,
+                                                const uint4 *__restrict__ tables, uint32_t *__restrict__ flags,
+                                                float *__restrict__ row_top) {
+    const int lid = threadIdx.x & 63;
+    const bool all_serial = flags[0] != 0;
+    float A = 0.0f;
+    uint64_t c = 0, serial_chunks = 0;
+    while (c < nch) {
+        bool do_serial = all_serial || !(A > 0.0f) || !isfinite(A);
+        if (!do_serial) {
+            const int k = binade_of(A);
+            const float u = ldexpf(1.0f, k - 23);
+            const double top = ldexp(1.0, k + 1);
+            const uint32_t p = ((uint32_t)(A / u)) & 1u;
+            const uint64_t cc = c + lid;
+            Td t = td_invalid();
+            if (cc < nch) {
+                const int b = k - ch[cc].kguess + 1;
+                if (b >= 0 && b < WG_RT_NBIN) {
+                    const uint4 q = tables[cc * WG_RT_NBIN + b];
+                    t = Td{q.x, q.y, q.z};
+                }
+            }
+            // ordered inclusive scan: P_j = T_c o ... o T_{c+j}
+            for (int d = 1; d < 64; d <<= 1) {
+                Td o = td_shfl_up(t, d);
+                if (lid >= d) t = td_compose(o, t);
+            }
+            const uint32_t D = p ? t.d1 : t.d0;
+            const bool ok = (t.f & 4u) && cc < nch && (double)A + (double)D * (double)u < top;
+            const uint64_t okm = __ballot(ok);
+            const int f = okm == ~0ull ? 64 : (int)__builtin_ctzll(~okm);   // leading run of valid lanes
+            const uint32_t Dprev = (uint32_t)__shfl_up((int)D, 1, 64);
+            if (lid < f) {
+                const uint32_t dp = lid == 0 ? 0u : Dprev;
+                ch[cc].start = A + (float)dp * u;
+                ch[cc].kstart = k;
+                ch[cc].mode = 0;
+            }
+            if (f > 0) {
+                const uint32_t Dl = (uint32_t)__shfl((int)D, f - 1, 64);
+                A = A + (float)Dl * u;
+                c += f;
+            }
+            do_serial = f < 64 && c < nch;
+        }
+        if (do_serial && c < nch) {
+            const uint64_t r0 = c * WG_RT_CHUNK, r1 = (r0 + WG_RT_CHUNK < n) ? r0 + WG_RT_CHUNK : n;
+            A = serial_rows(r0, r1, A, h, band, row_top);
+            if (lid == 0) ch[c].mode = 1;
+            c++;
+            serial_chunks++;
+        }
+    }
+    if (lid == 0) {
+        row_top[n] = A;
+        flags[1] = (uint32_t)serial_chunks;
+        flags[2] = all_serial ? 1u : 0u;
+    }
+}
+
+__global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
+                                                  const RtChunk *__restrict__ ch, float *__restrict__ row_top) {
+    const uint64_t c = blockIdx.x;
+    if (ch[c].mode != 0) return;
+    const int k = ch[c].kstart;
+    const float A = ch[c].start;
+    const float u = ldexpf(1.0f, k - 23);
+    const uint32_t p0 = ((uint32_t)(A / u)) & 1u;
+    const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
+    Td tr[RT_Q];
+    Td t = td_identity();
+#pragma unroll
+    for (int q = 0; q < RT_Q; q++) {
+        tr[q] = (r0 + q < n) ? row_td(step_of(h, band, r0 + q), k) : td_identity();
+        t = td_compose(t, tr[q]);
+    }
+    // ordered block exclusive scan
+    const int lid = threadIdx.x & 63, w = threadIdx.x >> 6;
+    Td inc = t;
+    for (int d = 1; d < 64; d <<= 1) {
+        Td o = td_shfl_up(inc, d);
+        if (lid >= d) inc = td_compose(o, inc);
+    }
+    __shared__ Td wt[RT_T / 64];
+    if (lid == 63) wt[w] = inc;
+    Td ex = td_shfl_up(inc, 1);
+    if (lid == 0) ex = td_identity();
+    __syncthreads();
+    Td wp = td_identity();
+    for (int k2 = 0; k2 < w; k2++) wp = td_compose(wp, wt[k2]);
+    ex = td_compose(wp, ex);
+    uint32_t D = p0 ? ex.d1 : ex.d0;
+    uint32_t p = p0 ? ((ex.f >> 1) & 1u) : (ex.f & 1u);
+#pragma unroll
+    for (int q = 0; q < RT_Q; q++) {
+        if (r0 + q < n) {
+            row_top[r0 + q] = A + (float)D * u;
+            D += p ? tr[q].d1 : tr[q].d0;
+            p = (tr[q].f >> p) & 1u;
+        }
+    }
+}
+
+}  // namespace
+
+// Host: exact gap thresholds of compute_row_heights (:486-507).
+static float height_of_gap(uint64_t d) {
+    const double log_max = std::log(1.0 + WG_TIME_MAX_DELTA / WG_TIME_BASE_SECONDS);
+    double delta = (double)d;
+    double clamped = delta < WG_TIME_MAX_DELTA ? delta : WG_TIME_MAX_DELTA;
+    double ratio = std::log(1.0 + clamped / WG_TIME_BASE_SECONDS) / log_max;
+    volatile float r32 = (float)ratio;
+    volatile float prod = WG_MAX_EXTRA_HEIGHT * r32;
+    volatile float h = WG_ROW_HEIGHT + prod;
+    return std::round((float)h);
+}
+
+void wg_init_height_thresholds(uint32_t *th) {
+    for (int k = 0; k < 28; k++) {
+        const float target = 29.0f + (float)k;
+        uint64_t lo = 0, hi = 2592001;   // first gap with height >= target, in [lo, hi]
+        while (lo < hi) {
+            uint64_t mid = (lo + hi) / 2;
+            if (height_of_gap(mid) >= target) hi = mid; else lo = mid + 1;
+        }
+        th[k] = (uint32_t)lo;   // 2592001 = never reached
+    }
+}
+
+extern "C" void wg_debug_height_thresholds(uint32_t *out28) { wg_init_height_thresholds(out28); }
+
+int wg_stage_heights(wg_ctx *c) {
+    const uint64_t n = c->n;
+    WG_ALLOC(c, c->heights, n * 4 + 4);
+    if (n == 0) return WG_OK;
+    Thresh th;
+    for (int k = 0; k < 28; k++) th.t[k] = c->h_thresh[k];
+    wg_stage_begin(c, "heights");
+    hipLaunchKernelGGL(k_heights, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_time, th, c->heights.as<float>());
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    return WG_OK;
+}
+
+int wg_stage_rowtop(wg_ctx *c, const float *d_band) {
+    const uint64_t n = c->n;
+    const uint64_t nch = (n + WG_RT_CHUNK - 1) / WG_RT_CHUNK;
+    WG_ALLOC(c, c->g_row_top, (n + 1) * 4);
+    WG_ALLOC(c, c->rt_chunk, (nch + 1) * sizeof(RtChunk));
+    WG_ALLOC(c, c->rt_tables, (nch + 1) * WG_RT_NBIN * sizeof(uint4));
+    WG_ALLOC(c, c->rt_flags, 64);
+    wg_stage_begin(c, "row_top");
+    WG_HIP(c, hipMemsetAsync(c->rt_flags.p, 0, 64, c->stream));
+    if (n == 0) {
+        WG_HIP(c, hipMemsetAsync(c->g_row_top.p, 0, 4, c->stream));
+        wg_stage_end(c);
+        return WG_OK;
+    }
+    const float *h = c->heights.as<const float>();
+    RtChunk *ch = c->rt_chunk.as<RtChunk>();
+    uint32_t *fl = c->rt_flags.as<uint32_t>();
+    hipLaunchKernelGGL(k_rt_sum, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, ch, fl);
+    hipLaunchKernelGGL(k_rt_prefix, dim3(1), dim3(1024), 0, c->stream, nch, ch);
+    hipLaunchKernelGGL(k_rt_tables, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch,
+                       c->rt_tables.as<uint4>());
+    hipLaunchKernelGGL(k_rt_walk, dim3(1), dim3(64), 0, c->stream, n, nch, h, d_band, ch,
+                       c->rt_tables.as<const uint4>(), fl, c->g_row_top.as<float>());
+    hipLaunchKernelGGL(k_rt_rows, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch,
+                       c->g_row_top.as<float>());
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    return WG_OK;
+}

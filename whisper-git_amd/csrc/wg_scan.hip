@@ -1,0 +1,113 @@
+// wg_scan.hip — exclusive prefix sums (CSR offsets of rows, edges, vertices).
+//
+// Reduce-then-scan over tiles of 2048 elements (256 threads x 8 items,
+// wave64 shuffles + one LDS exchange per block); tile sums are scanned
+// recursively.  Used for every CSR offset array of the engine.
+#include "wg_internal.h"
+
+namespace {
+
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr uint64_t SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+// returns the exclusive block prefix of v and the block total
+template <class T>
+__device__ __forceinline__ T block_excl_scan(T v, T &total) {
+    __shared__ T wsum[SCAN_THREADS / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    T inc = wave_incl_scan(v);
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    T base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_THREADS / 64; w++) {
+        T s = wsum[w];
+        if (w < wid) base += s;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return base + inc - v;
+}
+
+template <class TI, class TO>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(const TI *__restrict__ in, TO *__restrict__ bsum, uint64_t n) {
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    TO s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++)
+        if (base + k < n) s += (TO)in[base + k];
+    TO tot;
+    (void)block_excl_scan<TO>(s, tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+template <class TI, class TO>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_down(const TI *in, TO *out, const TO *__restrict__ boff, uint64_t n) {
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    TO v[SCAN_ITEMS];
+    TO s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        v[k] = (base + k < n) ? (TO)in[base + k] : (TO)0;
+        s += v[k];
+    }
+    TO tot;
+    TO run = block_excl_scan<TO>(s, tot) + (boff ? boff[blockIdx.x] : (TO)0);
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
+    }
+    // the thread holding the last element writes the grand total to out[n]
+    if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
+    if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
+}
+
+uint64_t nblocks(uint64_t n) { return n == 0 ? 1 : (n + SCAN_TILE - 1) / SCAN_TILE; }
+
+template <class TO>
+size_t tmp_bytes_rec(uint64_t n) {
+    uint64_t nb = nblocks(n);
+    if (nb <= 1) return 0;
+    return (nb + 1) * sizeof(TO) + 256 + tmp_bytes_rec<TO>(nb);
+}
+
+template <class TI, class TO>
+hipError_t scan_rec(const TI *in, TO *out, uint64_t n, char *tmp, hipStream_t s) {
+    uint64_t nb = nblocks(n);
+    if (nb <= 1) {
+        hipLaunchKernelGGL((k_scan_down<TI, TO>), dim3(1), dim3(SCAN_THREADS), 0, s, in, out, (const TO *)nullptr, n);
+        return hipGetLastError();
+    }
+    TO *bsum = reinterpret_cast<TO *>(tmp);
+    char *next = tmp + (((nb + 1) * sizeof(TO) + 255) & ~size_t(255));
+    hipLaunchKernelGGL((k_scan_reduce<TI, TO>), dim3(nb), dim3(SCAN_THREADS), 0, s, in, bsum, n);
+    hipError_t e = scan_rec<TO, TO>(bsum, bsum, nb, next, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_scan_down<TI, TO>), dim3(nb), dim3(SCAN_THREADS), 0, s, in, out, (const TO *)bsum, n);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t wg_scan_tmp_bytes(uint64_t n) { return tmp_bytes_rec<uint64_t>(n) + 1024; }
+
+hipError_t wg_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, void *tmp, hipStream_t s) {
+    return scan_rec<uint32_t, uint32_t>(in, out, n, (char *)tmp, s);
+}
+hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, hipStream_t s) {
+    return scan_rec<uint64_t, uint64_t>(in, out, n, (char *)tmp, s);
+}

@@ -1,1 +1,341 @@
-"""wgraph — MI355X commit-graph render-prep engine (host side)."""
+"""wgraph — MI355X commit-graph render-prep engine (host side).
+
+Python mirror of the reference's `GraphLayout` interface
+(/root/reference/src/commit_graph.rs:240-507) over the engine's C ABI
+(include/wgraph.h, libwgraph.so).  Every computation runs in the HIP engine;
+there is no CPU fallback: if the shared library or a gfx950 device is
+missing, constructing an Engine raises.
+
+    layout = GraphLayout()                      # GraphLayout::new   (:261)
+    layout.build(commits)                       # GraphLayout::build (:265)
+    layout.get(oid)                             # GraphLayout::get   (:357)
+    layout.max_lane, layout.edges, layout.row_geometry, layout.graph_width
+    layout.row_geometry_with_bands(commits, bands)     # (:367)
+    compute_row_heights(commits)                # (:486)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libwgraph.so")
+_lib = None
+
+
+class WgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{abi.ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libwgraph.so (fails loudly; there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: build it with `make engine` or __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u64, i64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32
+        sig = {
+            "wg_create": ([ctypes.c_int], vp), "wg_destroy": ([vp], None),
+            "wg_last_error": ([vp], ctypes.c_char_p), "wg_abi_version": ([], ctypes.c_int),
+            "wg_set_stream": ([vp, vp], ctypes.c_int), "wg_synchronize": ([vp], ctypes.c_int),
+            "wg_layout_build": ([vp, ctypes.POINTER(abi.Commits)], ctypes.c_int),
+            "wg_layout_summary_get": ([vp, ctypes.POINTER(abi.LayoutSummary)], ctypes.c_int),
+            "wg_copy_lanes": ([vp, vp, vp], ctypes.c_int),
+            "wg_copy_edges": ([vp, vp], ctypes.c_int),
+            "wg_copy_row_heights": ([vp, vp], ctypes.c_int),
+            "wg_row_geometry": ([vp, vp, i32], ctypes.c_int),
+            "wg_geometry_summary_get": ([vp, ctypes.POINTER(abi.GeometrySummary)], ctypes.c_int),
+            "wg_copy_geometry": ([vp, ctypes.POINTER(abi.GeometryHost)], ctypes.c_int),
+            "wg_emit_vertices": ([vp, u64, u64, i64, vp], ctypes.c_int),
+            "wg_vertex_summary_get": ([vp, ctypes.POINTER(abi.VertexSummary)], ctypes.c_int),
+            "wg_copy_vertices": ([vp, u64, u64, vp], ctypes.c_int),
+            "wg_copy_vertex_offsets": ([vp, vp], ctypes.c_int),
+            "wg_device_views_get": ([vp, ctypes.POINTER(abi.DeviceViews)], ctypes.c_int),
+            "wg_enable_timing": ([vp, ctypes.c_int], ctypes.c_int),
+            "wg_stage_timings": ([vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
+                                  ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = (
+    "wg_abi_version", "wg_create", "wg_destroy", "wg_last_error", "wg_set_stream", "wg_synchronize",
+    "wg_layout_build", "wg_layout_summary_get", "wg_copy_lanes", "wg_copy_edges", "wg_copy_row_heights",
+    "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
+    "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
+    "wg_enable_timing", "wg_stage_timings")
+
+
+class Engine:
+    """One wg_ctx (one per thread), bound to one GPU."""
+
+    def __init__(self, device: int = -1):
+        L = lib()
+        self._ctx = L.wg_create(device)
+        if not self._ctx:
+            raise RuntimeError("wg_create failed: no gfx950 (MI355X) device visible to HIP")
+        self._keep = []
+
+    # -- plumbing --------------------------------------------------------------
+    def _check(self, rc: int):
+        if rc != abi.WG_OK:
+            raise WgError(rc, lib().wg_last_error(self._ctx).decode(errors="replace"))
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib().wg_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, hip_stream_ptr: int | None):
+        self._check(lib().wg_set_stream(self._ctx, hip_stream_ptr))
+
+    def synchronize(self):
+        self._check(lib().wg_synchronize(self._ctx))
+
+    # -- layout ----------------------------------------------------------------------
+    def build(self, dag=None, commits: abi.Commits | None = None):
+        """GraphLayout::build on a wgraph.synth.Dag (host) or a prepared wg_commits."""
+        if commits is None:
+            commits = abi.commits_struct(dag)
+            self._keep = [dag]
+        self._commits = commits
+        self._check(lib().wg_layout_build(self._ctx, ctypes.byref(commits)))
+
+    def layout_summary(self) -> abi.LayoutSummary:
+        s = abi.LayoutSummary()
+        self._check(lib().wg_layout_summary_get(self._ctx, ctypes.byref(s)))
+        return s
+
+    def lanes(self):
+        s = self.layout_summary()
+        lane = np.empty(s.n_rows, np.uint32)
+        color = np.empty(s.n_rows, np.uint8)
+        self._check(lib().wg_copy_lanes(self._ctx, lane.ctypes.data, color.ctypes.data))
+        return lane, color
+
+    def edges(self) -> np.ndarray:
+        s = self.layout_summary()
+        e = np.empty(s.n_edges, abi.EDGE_DTYPE)
+        if s.n_edges:
+            self._check(lib().wg_copy_edges(self._ctx, e.ctypes.data))
+        return e
+
+    def row_heights(self) -> np.ndarray:
+        s = self.layout_summary()
+        h = np.empty(s.n_rows, np.float32)
+        self._check(lib().wg_copy_row_heights(self._ctx, h.ctypes.data))
+        return h
+
+    # -- geometry ---------------------------------------------------------------------
+    def row_geometry(self, band=None, device_ptr: int | None = None):
+        """row_geometry_with_bands; band None -> build()'s default geometry."""
+        if device_ptr is not None:
+            self._check(lib().wg_row_geometry(self._ctx, device_ptr, abi.WG_DEVICE))
+        elif band is None:
+            self._check(lib().wg_row_geometry(self._ctx, None, abi.WG_HOST))
+        else:
+            b = np.ascontiguousarray(band, np.float32)
+            self._band = b
+            self._check(lib().wg_row_geometry(self._ctx, b.ctypes.data, abi.WG_HOST))
+
+    def geometry_summary(self) -> abi.GeometrySummary:
+        s = abi.GeometrySummary()
+        self._check(lib().wg_geometry_summary_get(self._ctx, ctypes.byref(s)))
+        return s
+
+    def geometry(self) -> dict:
+        s = self.geometry_summary()
+        n = s.n_rows
+        g = dict(height=np.empty(n, np.float32), node_y=np.empty(n, np.float32),
+                 row_top=np.empty(n + 1, np.float32), vert_off=np.empty(n + 1, np.uint32),
+                 vert=np.empty(s.n_vert, np.uint32), curve_off=np.empty(n + 1, np.uint32),
+                 curve=np.empty((s.n_curve, 8), np.float32), curve_color=np.empty(s.n_curve, np.uint8))
+        d = abi.GeometryHost()
+        for k, a in g.items():
+            setattr(d, k, a.ctypes.data if a.size else None)
+        self._check(lib().wg_copy_geometry(self._ctx, ctypes.byref(d)))
+        return g
+
+    # -- vertices ------------------------------------------------------------------------
+    def emit_vertices(self, row_begin=0, row_end=None, selected=-1, palette=None):
+        if row_end is None:
+            row_end = self.layout_summary().n_rows
+        pal = np.ascontiguousarray(abi.DEFAULT_PALETTE if palette is None else palette, np.float32)
+        self._check(lib().wg_emit_vertices(self._ctx, row_begin, row_end, selected, pal.ctypes.data))
+
+    def vertex_summary(self) -> abi.VertexSummary:
+        s = abi.VertexSummary()
+        self._check(lib().wg_vertex_summary_get(self._ctx, ctypes.byref(s)))
+        return s
+
+    def vertices(self, first=0, count=None) -> np.ndarray:
+        s = self.vertex_summary()
+        if count is None:
+            count = s.n_vertices - first
+        v = np.empty(count, abi.VERTEX_DTYPE)
+        self._check(lib().wg_copy_vertices(self._ctx, first, count, v.ctypes.data if count else None))
+        return v
+
+    def vertex_offsets(self) -> np.ndarray:
+        s = self.vertex_summary()
+        o = np.empty(s.row_end - s.row_begin + 1, np.uint64)
+        self._check(lib().wg_copy_vertex_offsets(self._ctx, o.ctypes.data))
+        return o
+
+    def device_views(self) -> abi.DeviceViews:
+        v = abi.DeviceViews()
+        self._check(lib().wg_device_views_get(self._ctx, ctypes.byref(v)))
+        return v
+
+    # -- timing ----------------------------------------------------------------------------
+    def enable_timing(self, on=True):
+        self._check(lib().wg_enable_timing(self._ctx, 1 if on else 0))
+
+    def timings(self) -> list[tuple[str, float]]:
+        n = ctypes.c_int()
+        names = (ctypes.c_char_p * 32)()
+        ms = (ctypes.c_float * 32)()
+        self._check(lib().wg_stage_timings(self._ctx, ctypes.byref(n), names, ms))
+        return [(names[i].decode(), float(ms[i])) for i in range(n.value)]
+
+
+# ---------------------------------------------------------------------------
+# Reference-shaped API (commit_graph.rs:162-507)
+# ---------------------------------------------------------------------------
+@dataclass
+class CommitLayout:            # :162-166
+    lane: int
+    color: int                 # palette index (LANE_COLORS[lane % 6] or ORPHAN)
+
+
+@dataclass
+class GraphEdge:               # :173-180
+    child_row: int
+    child_lane: int
+    parent_row: int
+    parent_lane: int
+    color: int
+
+
+@dataclass
+class CurveSegment:            # :186-193
+    p0: tuple
+    p1: tuple
+    p2: tuple
+    p3: tuple
+    color: int
+
+
+@dataclass
+class RowGeometry:             # :208-233
+    height: float
+    full_verticals: list
+    top_half_verticals: list
+    bottom_half_verticals: list
+    curves: list
+    node_y: float
+
+
+def commits_to_soa(commits):
+    """[CommitInfo-like dicts: id(bytes20), time, parents(list[bytes20]), orphan] -> Dag."""
+    from .synth import Dag
+    n = len(commits)
+    oid = np.zeros((n, 20), np.uint8)
+    time = np.zeros(n, np.int64)
+    poff = np.zeros(n + 1, np.uint32)
+    flags = np.zeros(n, np.uint8)
+    pl = []
+    for i, c in enumerate(commits):
+        oid[i] = np.frombuffer(bytes(c["id"]), np.uint8)
+        time[i] = int(c["time"])
+        flags[i] = (1 if c.get("orphan") else 0) | (2 if c.get("synthetic") else 0)
+        pl.extend(bytes(p) for p in c["parents"])
+        poff[i + 1] = len(pl)
+    poid = np.frombuffer(b"".join(pl), np.uint8).reshape(-1, 20).copy() if pl else np.zeros((0, 20), np.uint8)
+    return Dag(oid, time, poff, poid, flags, np.zeros(n, np.float32))
+
+
+def geometry_rows(g: dict) -> list:
+    """CSR geometry (wgraph.h layout) -> list[RowGeometry]."""
+    rows = []
+    n = len(g["height"])
+    for r in range(n):
+        full, top, bottom = [], [], []
+        for v in g["vert"][g["vert_off"][r]:g["vert_off"][r + 1]]:
+            v = int(v)
+            entry = (v & 0xFFFFFF, (v >> 28) & 0xF)
+            (full, top, bottom)[(v >> 24) & 3].append(entry)
+        curves = []
+        for k in range(int(g["curve_off"][r]), int(g["curve_off"][r + 1])):
+            p = g["curve"][k]
+            curves.append(CurveSegment((p[0], p[1]), (p[2], p[3]), (p[4], p[5]), (p[6], p[7]), int(g["curve_color"][k])))
+        rows.append(RowGeometry(float(g["height"][r]), full, top, bottom, curves, float(g["node_y"][r])))
+    return rows
+
+
+class GraphLayout:
+    """Drop-in for whisper-git's GraphLayout, backed by the HIP engine."""
+
+    def __init__(self, engine: Engine | None = None):
+        self.engine = engine or Engine()
+        self._ids = {}
+        self.max_lane = 0
+        self.edges: list[GraphEdge] = []
+        self.row_geometry: list[RowGeometry] = []
+        self.graph_width = 0.0
+
+    @classmethod
+    def new(cls):
+        return cls()
+
+    def build(self, commits):
+        dag = commits if hasattr(commits, "parent_off") else commits_to_soa(commits)
+        self.engine.build(dag)
+        s = self.engine.layout_summary()
+        self.max_lane = int(s.max_lane)
+        self.graph_width = float(s.graph_width)
+        lane, color = self.engine.lanes()
+        self._ids = {bytes(dag.oid[i]): CommitLayout(int(lane[i]), int(color[i])) for i in range(dag.n)}
+        self.edges = [GraphEdge(*map(int, e)) for e in self.engine.edges()]
+        self.row_geometry = geometry_rows(self.engine.geometry())
+
+    def get(self, oid: bytes):
+        return self._ids.get(bytes(oid))
+
+    def row_geometry_with_bands(self, commits, band_heights):
+        n = len(commits) if not hasattr(commits, "parent_off") else commits.n
+        band = np.zeros(n, np.float32)
+        m = min(n, len(band_heights))
+        band[:m] = np.asarray(band_heights[:m], np.float32)
+        self.engine.row_geometry(band)
+        return geometry_rows(self.engine.geometry())
+
+
+def compute_row_heights(commits) -> np.ndarray:
+    """compute_row_heights (:486-507) on the engine."""
+    dag = commits if hasattr(commits, "parent_off") else commits_to_soa(commits)
+    e = Engine()
+    try:
+        e.build(dag)
+        return e.row_heights()
+    finally:
+        e.close()
