@@ -128,7 +128,10 @@ def main():
     for _ in range(args.steps):
         eng.enable_timing(True)
         step()
-        for name, ms in eng.timings():
+        per = {}
+        for name, ms in eng.timings():   # a stage may run twice per step (build + banded geometry)
+            per[name] = per.get(name, 0.0) + ms
+        for name, ms in per.items():
             stage_ms.setdefault(name, []).append(ms)
     torch.cuda.synchronize()
     if world > 1:

@@ -184,6 +184,14 @@ int         wg_abi_version(void);
 /* Install a caller-owned hipStream_t (NULL = library-owned stream). */
 int         wg_set_stream(wg_ctx *ctx, void *hip_stream);
 int         wg_synchronize(wg_ctx *ctx);
+/* Engine options.  WG_OPT_LANE_PATH: 0 = auto (event-compressed fast path
+ * when the commit list is well formed, general walk otherwise), 1 = always
+ * the general walk (for testing; results are identical). */
+#define WG_OPT_LANE_PATH 1
+/* WG_OPT_REPLAY_CHUNK: events per chunk of the parallel lane-event replay
+ * (multiple of 64; default 512).  Affects speed only, never results. */
+#define WG_OPT_REPLAY_CHUNK 2
+int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------
  * Lane assignment, colours, edge list, default row geometry (bands = 0).  */
@@ -222,6 +230,12 @@ int wg_device_views_get(wg_ctx *ctx, wg_device_views *out);
 int wg_enable_timing(wg_ctx *ctx, int on);
 /* Per-stage milliseconds of the last producing calls; names[i] static. */
 int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
+
+/* ---- diagnostics ------------------------------------------------------------
+ * Copies up to n (<= 16) 32-bit engine counters of the last layout build:
+ * [0] max_lane, [1] slots, [2] lane-table overflow, [3] fixed-point
+ * iterations of the lane-event replay, [4] lane events.                   */
+int wg_debug_counters(wg_ctx *ctx, uint32_t *out, int n);
 
 #ifdef __cplusplus
 }

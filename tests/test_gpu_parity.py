@@ -77,6 +77,43 @@ def test_golden_full_pipeline(engine, name):
     assert s.checksum == int(g["vertex_checksum"])
 
 
+WELL_FORMED = {"merge_basic", "octopus", "dup_first_parent", "secondary_reuses_slot", "wide_lanes", "single",
+               "repeated_parent", "random13_1000", "linux_1000", "wide16_1000", "linear_300"}
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_lanes_both_paths(engine, name):
+    """The event-compressed fast path and the general walk give identical layouts;
+    ill-formed inputs (duplicate ids, skewed or self parents) take the general walk."""
+    d, g = load_golden(name)
+    try:
+        for general in (True, False):
+            engine.set_lane_path(general)
+            engine.build(d)
+            check_layout(engine, g)
+            s = engine.layout_summary()
+            if d.n:
+                expect_path = 1 if (general or name not in WELL_FORMED) else 0
+                assert s.lane_path == expect_path, (name, general, s.lane_path)
+                assert s.n_slots == int(g["n_slots"])
+    finally:
+        engine.set_lane_path(False)
+
+
+@pytest.mark.parametrize("kind,n", [("random13", 200000), ("linux", 300000), ("wide16", 300000)])
+def test_fast_lanes_match_oracle_large(engine, kind, n):
+    from oracle import oracle_c
+    d = synth.generate(kind, n, seed=99)
+    o = oracle_c.OracleLayout(d)
+    engine.build(d)
+    s = engine.layout_summary()
+    assert s.lane_path == 0
+    assert s.max_lane == o.max_lane and s.n_slots == o.n_slots
+    lane, color = engine.lanes()
+    assert_bits("lane", lane, o.lane)
+    assert_bits("color", color, o.color)
+
+
 @pytest.mark.parametrize("kind,n", [("random13", 20000), ("linux", 30000), ("wide16", 50000), ("anomaly", 5000),
                                     ("linear", 10000)])
 def test_against_oracle_midsize(engine, kind, n):

@@ -21,16 +21,19 @@ int wg_fail(wg_ctx *c, int code, const char *fmt, ...) {
     return code;
 }
 
+// Stages nest: begin takes the next slot and pushes it, end closes the top.
 void wg_stage_begin(wg_ctx *c, const char *name) {
-    if (!c->timing || c->n_stages >= WG_STAGE_MAX) return;
+    if (!c->timing) return;
+    if (c->n_stages >= WG_STAGE_MAX || c->stage_depth >= 8) { c->stage_stack[c->stage_depth++ & 7] = -1; return; }
     StageTimer &t = c->stages[c->n_stages];
     t.name = name;
     (void)hipEventRecord(t.a, c->stream);
+    c->stage_stack[c->stage_depth++] = c->n_stages++;
 }
 void wg_stage_end(wg_ctx *c) {
-    if (!c->timing || c->n_stages >= WG_STAGE_MAX) return;
-    (void)hipEventRecord(c->stages[c->n_stages].b, c->stream);
-    c->n_stages++;
+    if (!c->timing || c->stage_depth <= 0) return;
+    const int idx = c->stage_stack[--c->stage_depth];
+    if (idx >= 0) (void)hipEventRecord(c->stages[idx].b, c->stream);
 }
 
 extern "C" {
@@ -71,6 +74,7 @@ void wg_destroy(wg_ctx *c) {
                       &c->curve_ref, &c->curve_row, &c->top_fill, &c->carry_cnt, &c->carry_off, &c->carry,
                       &c->scan_tmp, &c->scal, &c->rowflags, &c->carry_fill, &c->sweep_err, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
     for (DevBuf *b : bufs) b->release();
+    for (DevBuf &b : c->lf) b.release();
     for (int i = 0; i < WG_STAGE_MAX; i++) {
         (void)hipEventDestroy(c->stages[i].a);
         (void)hipEventDestroy(c->stages[i].b);
@@ -94,6 +98,18 @@ int wg_set_stream(wg_ctx *c, void *s) {
         c->own_stream = true;
     }
     return WG_OK;
+}
+
+int wg_set_option(wg_ctx *c, int option, int64_t value) {
+    if (!c) return WG_E_INVALID;
+    switch (option) {
+    case WG_OPT_LANE_PATH: c->force_general_lanes = value != 0; return WG_OK;
+    case WG_OPT_REPLAY_CHUNK:
+        if (value < 64 || value > (1 << 20) || (value & 63)) return wg_fail(c, WG_E_INVALID, "replay chunk must be a multiple of 64");
+        c->replay_chunk = (uint32_t)value;
+        return WG_OK;
+    default: return wg_fail(c, WG_E_INVALID, "unknown option %d", option);
+    }
 }
 
 int wg_synchronize(wg_ctx *c) {
@@ -339,10 +355,22 @@ int wg_device_views_get(wg_ctx *c, wg_device_views *o) {
     return WG_OK;
 }
 
+int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
+    if (!c || !out || n < 0) return WG_E_INVALID;
+    if (n > 16) n = 16;
+    if (!c->lane_scalars.p) return wg_fail(c, WG_E_STATE, "no layout built");
+    WG_HIP(c, hipMemcpyAsync(out, c->lane_scalars.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    if (n > 3) out[3] = c->replay_iters;
+    if (n > 4) out[4] = (uint32_t)c->n_events;
+    return WG_OK;
+}
+
 int wg_enable_timing(wg_ctx *c, int on) {
     if (!c) return WG_E_INVALID;
     c->timing = on != 0;
     c->n_stages = 0;
+    c->stage_depth = 0;
     return WG_OK;
 }
 

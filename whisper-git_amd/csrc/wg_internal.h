@@ -73,6 +73,11 @@ struct wg_ctx {
     DevBuf lane_out;        // uint32 [N]  layouts.get(id).lane per row
     DevBuf color_out;       // uint8  [N]
     DevBuf lane_scalars;    // uint32 [8]  max_lane, n_slots, overflow, ...
+    DevBuf lf[20];          // event-compressed lane path workspaces (wg_lanes.hip)
+    uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
+    uint32_t replay_iters = 0;     // iterations the last replay needed
+    uint64_t n_events = 0;  // events of the last fast-path lane build
+    bool force_general_lanes = false;   // WG_LANES=general (testing the general walk)
     // edges
     DevBuf edge_cnt;        // uint32 [N+1] -> edge_off after scan
     DevBuf edges;           // wg_edge [n_edges]
@@ -114,6 +119,8 @@ struct wg_ctx {
     bool       timing = false;
     StageTimer stages[WG_STAGE_MAX];
     int        n_stages = 0;
+    int        stage_stack[8] = {0};
+    int        stage_depth = 0;
     uint64_t   scratch_host[16];
 };
 
@@ -148,6 +155,12 @@ hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, 
 // stages -------------------------------------------------------------------------
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
 int wg_stage_lanes(wg_ctx *c);                // wg_lanes.hip
+int wg_lanes_fast(wg_ctx *c, bool *used);     // wg_lanes_fast.hip
+hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *ch_off,
+                          const uint32_t *ch, const uint32_t *sp, const uint32_t *secev, const uint32_t *winfo,
+                          uint8_t *slots_a, uint8_t *slots_b, unsigned long long *occ_a, unsigned long long *occ_b,
+                          uint32_t *stats, uint32_t *flags, uint32_t max_iters, uint32_t *scal, uint8_t **slot_out,
+                          uint32_t *iters);  // wg_lanes_replay.hip
 int wg_stage_edges(wg_ctx *c);                // wg_lanes.hip
 int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
 int wg_stage_rowtop(wg_ctx *c, const float *d_band);   // wg_rowtop.hip

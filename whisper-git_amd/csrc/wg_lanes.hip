@@ -203,6 +203,19 @@ int wg_stage_lanes(wg_ctx *c) {
     if (n == 0) return WG_OK;
     wg_stage_begin(c, "lanes");
     WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, c->stream));
+    if (!c->force_general_lanes) {
+        bool used = false;
+        int rc = wg_lanes_fast(c, &used);
+        if (rc != WG_OK) return rc;
+        if (used) {
+            wg_stage_end(c);
+            uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
+            float gw = (float)vis * WG_LANE_W;
+            c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
+            return WG_OK;
+        }
+        WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, c->stream));
+    }
     WG_HIP(c, launch_general<1>(c));
     uint32_t sc[4];
     WG_HIP(c, hipMemcpyAsync(sc, c->lane_scalars.p, 16, hipMemcpyDeviceToHost, c->stream));

@@ -1,0 +1,261 @@
+// wg_lanes_replay.hip — the sequential core of the event-compressed lane
+// assignment (wg_lanes_fast.hip): replay of the slot-occupancy events
+// (SURVEY.md §7 hard part 1: "speculate-and-verify ... fixed-point iteration
+// on shard entry states").
+//
+// The greedy's state between events is a 64-bit occupancy mask plus the
+// slots of the chains still alive.  The event stream is cut into chunks of
+// CH events (multiple of 64), one wave per chunk, all chunks replayed in
+// parallel:
+//   iteration i, chunk c:  entry occupancy = exit occupancy of chunk c-1
+//                          from iteration i-1; slots of tokens born in
+//                          earlier chunks read from iteration i-1's slots;
+//                          writes its own event slots + exit occupancy and
+//                          flags any difference from iteration i-1.
+// An iteration that changes nothing is a fixed point: every chunk's output
+// is its replay from its predecessors' outputs, which by induction from
+// chunk 0 (exact entry: empty) IS the sequential result.  Chunk c is exact
+// after at most c+1 iterations; in practice the state forgets a wrong guess
+// within a few dozen events, so 2-4 iterations suffice.  The driver launches
+// iterations in groups; an iteration whose predecessor changed nothing exits
+// at once.
+//
+// Inside a chunk one wave replays 64 events per batch.  Token slots are
+// resolved in parallel (previous batch by lane permute, older events from
+// HBM one batch ahead); MIN / FREE events whose tokens are known have a
+// fixed effect on the occupancy (clear the non-surviving token bits), folded
+// with a segmented AND-scan across lanes; allocations (lowest free slot =
+// ctz(~occ), :414-423), tokens born in the same batch and merges with more
+// than two waiters are replayed in order by the scalar unit.  max_lane is
+// the highest occupied slot after each occupying allocation (:462-471).
+#include "wg_internal.h"
+
+namespace {
+
+enum : uint32_t { F_A = 1u, F_O = 2u, F_C = 4u, F_M = 8u, F_IN0 = 1u << 14, F_IN1 = 1u << 22 };
+constexpr uint32_t EVF = 0x80000000u;
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
+    return ((uint64_t)rl((uint32_t)(v >> 32), lane) << 32) | rl((uint32_t)v, lane);
+}
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+struct ReplayArgs {
+    uint64_t nev;
+    uint32_t chunk;             // events per chunk (multiple of 64)
+    uint32_t iter;              // iteration index (>= 1)
+    const uint4 *ev;            // records, padded with >= 256 zero records
+    const uint32_t *ch_off, *ch, *sp, *secev, *winfo;
+    const uint8_t *slot_prev;   // iteration i-1
+    uint8_t *slot_next;         // iteration i
+    const unsigned long long *occ_prev;  // exit occupancy per chunk, iteration i-1
+    unsigned long long *occ_next;
+    uint32_t *chunk_stats;      // per chunk: max_lane, max_slot
+    uint32_t *changed;          // [iter] = 1 if iteration iter changed anything
+};
+
+__global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
+    const uint32_t lid = threadIdx.x & 63;
+    if (A.changed[A.iter - 1] == 0) return;          // previous iteration was a fixed point
+    const uint64_t c = blockIdx.x;
+    const uint64_t e0 = c * A.chunk;
+    if (e0 >= A.nev) return;
+    const uint64_t e1 = (e0 + A.chunk < A.nev) ? e0 + A.chunk : A.nev;
+    uint64_t occ = c == 0 ? 0ull : A.occ_prev[c - 1];
+    uint32_t max_lane = 0, max_s = 0;
+    bool diff = false;
+    uint32_t prev_v = 0;
+    const uint4 *ev = A.ev;
+    uint4 rec = ev[e0 + lid];
+    uint4 rec1 = ev[e0 + 64 + lid];
+    uint32_t q0_v = 0, q1_v = 0;
+    // old tokens of the first batch: all born before e0 -> iteration i-1
+    if ((rec.x & F_C) && (uint64_t)rec.y < e0) q0_v = A.slot_prev[rec.y];
+    if ((rec.x & F_C) && (uint64_t)rec.z < e0) q1_v = A.slot_prev[rec.z];
+    for (uint64_t base = e0; base < e1; base += 64) {
+        const uint32_t f_v = (base + lid < e1) ? rec.x : 0u;   // lanes past the chunk: no-op
+        const uint32_t t0_v = rec.y, t1_v = rec.z, row_v = rec.w;
+        const uint4 rec2 = ev[base + 128 + lid];
+        // old tokens of the next batch (born before `base`): earlier chunks from
+        // iteration i-1, this chunk's earlier batches from this iteration
+        uint32_t n0_v = 0, n1_v = 0;
+        if ((rec1.x & F_C) && (uint64_t)rec1.y < base)
+            n0_v = (uint64_t)rec1.y < e0 ? A.slot_prev[rec1.y] : A.slot_next[rec1.y];
+        if ((rec1.x & F_C) && (uint64_t)rec1.z < base)
+            n1_v = (uint64_t)rec1.z < e0 ? A.slot_prev[rec1.z] : A.slot_next[rec1.z];
+        // ---- parallel part: this lane's event ----------------------------------------
+        const bool have_prev = base > e0;    // previous batch of this chunk is in prev_v
+        const uint64_t pbase = base - 64;
+        const uint32_t g0 = (uint32_t)__shfl((int)prev_v, (int)(t0_v & 63u), 64);
+        const uint32_t g1 = (uint32_t)__shfl((int)prev_v, (int)(t1_v & 63u), 64);
+        const uint32_t s0 = (have_prev && (uint64_t)t0_v >= pbase) ? g0 : q0_v;
+        const uint32_t s1 = (have_prev && (uint64_t)t1_v >= pbase) ? g1 : q1_v;
+        const bool isC = f_v & F_C;
+        const bool special = (f_v & F_A) || (f_v & (F_IN0 | F_IN1 | F_M)) != 0;
+        const uint32_t smin = s0 < s1 ? s0 : s1;
+        uint64_t tokbits = (1ull << (s0 & 63u)) | (1ull << (s1 & 63u));
+        if (f_v & F_O) tokbits &= ~(1ull << (smin & 63u));   // MIN keep: the minimum stays occupied
+        const uint64_t amask = (isC && !special) ? ~tokbits : ~0ull;
+        uint32_t cur_v = (isC && !special) ? smin : 0u;
+        // segmented inclusive AND-scan: a segment starts right after each special lane
+        uint64_t q = amask;
+        uint32_t st = (lid == 0 || __shfl_up((int)special, 1, 64)) ? 1u : 0u;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t qo = shfl_up64(q, d);
+            const uint32_t so = (uint32_t)__shfl_up((int)st, d, 64);
+            if (lid >= (uint32_t)d && !st) { q &= qo; st |= so; }
+        }
+        // ---- sequential part: special events only ----------------------------------
+        const uint64_t sm = __ballot(special);
+        uint64_t smask = sm;
+        while (smask) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(smask);
+            smask &= smask - 1;
+            occ &= rl64(q, k);                                  // the folded run before event k
+            const uint32_t f = rl(f_v, k);
+            uint32_t s;
+            if (f & F_A) {
+                s = (uint32_t)__builtin_ctzll(~occ | (1ull << 63));
+                if (f & F_O) {
+                    occ |= 1ull << s;
+                    const uint32_t hb = 63u - (uint32_t)__builtin_clzll(occ);
+                    max_lane = hb > max_lane ? hb : max_lane;
+                }
+                max_s = s > max_s ? s : max_s;
+            } else {
+                // tokens born in this batch, or more than two waiters
+                uint32_t a = rl(s0, k), b = rl(s1, k);
+                if (f & F_IN0) a = rl(cur_v, (f >> 8) & 63u);
+                if (f & F_IN1) b = rl(cur_v, (f >> 16) & 63u);
+                uint64_t clr = (1ull << (a & 63u)) | (1ull << (b & 63u));
+                uint32_t m = a < b ? a : b;
+                if (f & F_M) {
+                    const uint32_t j = rl(row_v, k);
+                    const uint32_t lo = A.ch_off[j], hi = A.ch_off[j + 1];
+                    for (uint32_t x = lo; x <= hi; x++) {
+                        uint32_t t;
+                        if (x < hi) t = A.sp[A.ch[x]] & ~EVF;
+                        else if (A.winfo[j] & 0x80000000u) t = A.secev[j];
+                        else break;
+                        uint32_t ts;
+                        if (t >= base) ts = rl(cur_v, (uint32_t)(t - base));
+                        else if (have_prev && t >= pbase) ts = rl(prev_v, (uint32_t)(t - pbase));
+                        else ts = t < e0 ? A.slot_prev[t] : A.slot_next[t];
+                        clr |= 1ull << (ts & 63u);
+                        m = ts < m ? ts : m;
+                    }
+                }
+                occ &= ~clr;
+                if (f & F_O) occ |= 1ull << (m & 63u);
+                s = m;
+            }
+            cur_v = (lid == k) ? s : cur_v;
+        }
+        // the run after the last special event
+        occ &= (sm >> 63) ? ~0ull : rl64(q, 63);
+        if (base + lid < e1) {
+            const uint8_t nv = (uint8_t)cur_v;
+            diff |= A.slot_prev[base + lid] != nv;
+            A.slot_next[base + lid] = nv;
+        }
+        // same-wave vector memory ops to one address complete in order; only keep
+        // the compiler from moving the next batch's token loads above the store
+        asm volatile("" ::: "memory");
+        prev_v = cur_v;
+        rec = rec1;
+        rec1 = rec2;
+        q0_v = n0_v;
+        q1_v = n1_v;
+    }
+    if (lid == 0) {
+        A.occ_next[c] = occ;
+        A.chunk_stats[2 * c] = max_lane;
+        A.chunk_stats[2 * c + 1] = max_s;
+    }
+    if (__any(diff) || (lid == 0 && occ != A.occ_prev[c])) A.changed[A.iter] = 1u;
+}
+
+__global__ void k_lf_replay_init(uint64_t nchunks, unsigned long long *occ_prev, uint32_t *changed, uint32_t nflags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nchunks) occ_prev[i] = 0ull;    // initial guess (any guess is sound)
+    if (i < nflags) changed[i] = (i == 0) ? 1u : 0u;
+}
+
+// final: max_lane / slots / overflow over all chunks
+__global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats, uint32_t *__restrict__ scal) {
+    uint32_t ml = 0, ms = 0;
+    for (uint64_t c = threadIdx.x; c < nchunks; c += blockDim.x) {
+        ml = stats[2 * c] > ml ? stats[2 * c] : ml;
+        ms = stats[2 * c + 1] > ms ? stats[2 * c + 1] : ms;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t a = (uint32_t)__shfl_down((int)ml, d, 64), b = (uint32_t)__shfl_down((int)ms, d, 64);
+        ml = a > ml ? a : ml;
+        ms = b > ms ? b : ms;
+    }
+    if (threadIdx.x == 0) {
+        scal[0] = ml;
+        scal[1] = ms + 1;
+        scal[2] = ms >= 63 ? 1u : 0u;
+    }
+}
+
+}  // namespace
+
+// Replays nev events into slot_out (one byte per event).  ws_* are caller
+// workspaces: slots (2 x (nev + 64) bytes), occ (2 x nchunks x 8 bytes),
+// stats (2 x nchunks x 4 bytes), flags (max_iters + 1 words).
+// Returns the number of iterations used (0 on a HIP error) in *iters.
+hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *ch_off,
+                          const uint32_t *ch, const uint32_t *sp, const uint32_t *secev, const uint32_t *winfo,
+                          uint8_t *slots_a, uint8_t *slots_b, unsigned long long *occ_a, unsigned long long *occ_b,
+                          uint32_t *stats, uint32_t *flags, uint32_t max_iters, uint32_t *scal, uint8_t **slot_out,
+                          uint32_t *iters) {
+    const uint64_t nch = (nev + chunk - 1) / chunk;
+    *iters = 0;
+    if (nev == 0) {
+        hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, (uint64_t)0, stats, scal);
+        *slot_out = slots_a;
+        return hipGetLastError();
+    }
+    const uint64_t ninit = nch > max_iters + 1 ? nch : max_iters + 1;
+    hipLaunchKernelGGL(k_lf_replay_init, dim3((ninit + 255) / 256), dim3(256), 0, s, nch, occ_a, flags, max_iters + 1);
+    hipError_t e = hipMemsetAsync(slots_a, 0, nev, s);
+    if (e != hipSuccess) return e;
+    uint8_t *sp_prev = slots_a, *sp_next = slots_b;
+    unsigned long long *op = occ_a, *on = occ_b;
+    uint32_t done_check = 0, next_poll = 3;
+    // chunk c is exact after c + 1 iterations, so nch + 1 iterations always converge
+    if (max_iters > nch + 1) max_iters = (uint32_t)(nch + 1);
+    for (uint32_t it = 1; it <= max_iters; it++) {
+        ReplayArgs a{nev, chunk, it, ev, ch_off, ch, sp, secev, winfo, sp_prev, sp_next, op, on, stats, flags};
+        hipLaunchKernelGGL(k_lf_replay, dim3(nch), dim3(64), 0, s, a);
+        // after a fixed point later iterations do nothing; the converged slots are
+        // in both buffers, so either pointer is final
+        uint8_t *t = sp_prev; sp_prev = sp_next; sp_next = t;
+        unsigned long long *o = op; op = on; on = o;
+        // poll at iterations 3, 6, 12, 24, ... (launches after a fixed point exit at once)
+        if (it == next_poll || it == max_iters) {
+            next_poll *= 2;
+            uint32_t fl[2] = {1, 1};
+            e = hipMemcpyAsync(fl, flags + it - 1, 8, hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) return e;
+            e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            done_check = it;
+            if (fl[0] == 0 || fl[1] == 0) { *iters = it; break; }
+        }
+    }
+    (void)done_check;
+    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, nch, stats, scal);
+    *slot_out = sp_prev;   // the buffer written last (== the other one at convergence)
+    if (*iters == 0) *iters = max_iters + 1;   // did not converge within max_iters
+    return hipGetLastError();
+}

@@ -44,6 +44,7 @@ typedef struct wgs_params {
     double   band_frac;      /* rows with a 30 px pills band              */
     int32_t  truncated;      /* unresolved first parents point outside    */
     int32_t  reserved;
+    double   p_feature;      /* a merge's second parent starts a new line */
 } wgs_params;
 
 typedef struct wgs_dag {
@@ -72,12 +73,12 @@ int wgs_preset(int kind, uint64_t n, uint64_t seed, wgs_params *p) {
     p->band_frac = 0.02; p->main_weight = 4.0;
     switch (kind) {
     case WGS_LINEAR:   p->max_lines = 1;  break;
-    case WGS_RANDOM13: p->max_lines = 8;  p->p_merge = 0.30; p->p_newtip = 0.08; p->p_fork = 0.08; p->main_weight = 2.0; break;
-    case WGS_LINUX:    p->max_lines = 28; p->p_merge = 0.07; p->p_newtip = 0.03; p->p_fork = 0.03; p->p_octopus = 0.002; p->main_weight = 3.0; break;
-    case WGS_WIDE16:   p->max_lines = 10; p->p_merge = 0.10; p->p_newtip = 0.02; p->p_fork = 0.02; p->main_weight = 2.0; break;
+    case WGS_RANDOM13: p->max_lines = 8;  p->p_merge = 0.30; p->p_newtip = 0.06; p->p_fork = 0.10; p->main_weight = 2.0; p->p_feature = 0.3; break;
+    case WGS_LINUX:    p->max_lines = 28; p->p_merge = 0.07; p->p_newtip = 0.02; p->p_fork = 0.04; p->p_octopus = 0.002; p->main_weight = 3.0; p->p_feature = 0.5; break;
+    case WGS_WIDE16:   p->max_lines = 10; p->p_merge = 0.10; p->p_newtip = 0.01; p->p_fork = 0.03; p->main_weight = 2.0; p->p_feature = 0.3; break;
     case WGS_ANOMALY:  p->max_lines = 9;  p->p_merge = 0.25; p->p_newtip = 0.10; p->p_fork = 0.08; p->p_octopus = 0.05;
                        p->p_dup_oid = 0.03; p->p_skew = 0.04; p->p_external = 0.05; p->p_self = 0.01;
-                       p->p_dup_parent = 0.03; p->p_orphan_flag = 0.05; p->band_frac = 0.1; p->truncated = 1; break;
+                       p->p_dup_parent = 0.03; p->p_orphan_flag = 0.05; p->band_frac = 0.1; p->truncated = 1; p->p_feature = 0.3; break;
     default: return -1;
     }
     return 0;
@@ -180,11 +181,22 @@ wgs_dag *wgs_generate(const wgs_params *p) {
             }
         }
         /* merges: extra parents resolve to other lines' next commits */
-        if (nact >= 2 && p->p_merge > 0 && urand(&rs) < p->p_merge) {
+        if (nact >= 1 && p->p_merge > 0 && urand(&rs) < p->p_merge) {
             int extra = 1;
             if (p->p_octopus > 0 && urand(&rs) < p->p_octopus) extra += 1 + (int)urange(&rs, 6);
             for (int k = 0; k < extra; k++) {
-                int L3 = (int)urange(&rs, (uint64_t)nact);
+                int L3;
+                if (nact < maxl && p->p_feature > 0 && urand(&rs) < p->p_feature) {
+                    /* feature-branch merge: the merged tip starts a new line,
+                     * so this merge is the first reference to it */
+                    L3 = nact++;
+                    active[L3] = 1;
+                    line_last[L3] = -1;
+                    pend[L3].n = 0;
+                } else {
+                    if (nact < 2) continue;
+                    L3 = (int)urange(&rs, (uint64_t)nact);
+                }
                 if (L3 == L) continue;
                 if (vpush(&xrow, (int64_t)i) || vpush(&xval, UNRES) || vpush(&pend[L3], (int64_t)(xval.n - 1))) goto fail;
                 xcount[i]++;

@@ -46,6 +46,7 @@ def lib():
             "wg_create": ([ctypes.c_int], vp), "wg_destroy": ([vp], None),
             "wg_last_error": ([vp], ctypes.c_char_p), "wg_abi_version": ([], ctypes.c_int),
             "wg_set_stream": ([vp, vp], ctypes.c_int), "wg_synchronize": ([vp], ctypes.c_int),
+            "wg_set_option": ([vp, ctypes.c_int, i64], ctypes.c_int),
             "wg_layout_build": ([vp, ctypes.POINTER(abi.Commits)], ctypes.c_int),
             "wg_layout_summary_get": ([vp, ctypes.POINTER(abi.LayoutSummary)], ctypes.c_int),
             "wg_copy_lanes": ([vp, vp, vp], ctypes.c_int),
@@ -60,6 +61,7 @@ def lib():
             "wg_copy_vertex_offsets": ([vp, vp], ctypes.c_int),
             "wg_device_views_get": ([vp, ctypes.POINTER(abi.DeviceViews)], ctypes.c_int),
             "wg_enable_timing": ([vp, ctypes.c_int], ctypes.c_int),
+            "wg_debug_counters": ([vp, vp, ctypes.c_int], ctypes.c_int),
             "wg_stage_timings": ([vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
                                   ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         }
@@ -72,11 +74,11 @@ def lib():
 
 
 EXPORTED_SYMBOLS = (
-    "wg_abi_version", "wg_create", "wg_destroy", "wg_last_error", "wg_set_stream", "wg_synchronize",
+    "wg_abi_version", "wg_create", "wg_destroy", "wg_last_error", "wg_set_stream", "wg_synchronize", "wg_set_option",
     "wg_layout_build", "wg_layout_summary_get", "wg_copy_lanes", "wg_copy_edges", "wg_copy_row_heights",
     "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
-    "wg_enable_timing", "wg_stage_timings")
+    "wg_enable_timing", "wg_stage_timings", "wg_debug_counters")
 
 
 class Engine:
@@ -110,6 +112,10 @@ class Engine:
 
     def synchronize(self):
         self._check(lib().wg_synchronize(self._ctx))
+
+    def set_lane_path(self, general: bool):
+        """Force the general lane walk (True) or auto-select (False)."""
+        self._check(lib().wg_set_option(self._ctx, 1, 1 if general else 0))
 
     # -- layout ----------------------------------------------------------------------
     def build(self, dag=None, commits: abi.Commits | None = None):
@@ -207,6 +213,11 @@ class Engine:
         return v
 
     # -- timing ----------------------------------------------------------------------------
+    def debug_counters(self) -> np.ndarray:
+        out = np.zeros(16, np.uint32)
+        self._check(lib().wg_debug_counters(self._ctx, out.ctypes.data, 16))
+        return out
+
     def enable_timing(self, on=True):
         self._check(lib().wg_enable_timing(self._ctx, 1 if on else 0))
 

@@ -26,7 +26,8 @@ class Params(ctypes.Structure):
                 ("p_skew", ctypes.c_double), ("p_external", ctypes.c_double),
                 ("p_self", ctypes.c_double), ("p_dup_parent", ctypes.c_double),
                 ("p_orphan_flag", ctypes.c_double), ("band_frac", ctypes.c_double),
-                ("truncated", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("truncated", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("p_feature", ctypes.c_double)]
 
 
 _lib = None
