@@ -75,6 +75,7 @@ void wg_destroy(wg_ctx *c) {
                       &c->scan_tmp, &c->scal, &c->rowflags, &c->carry_fill, &c->sweep_err, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
     for (DevBuf *b : bufs) b->release();
     for (DevBuf &b : c->lf) b.release();
+    c->tile_first.release();
     for (int i = 0; i < WG_STAGE_MAX; i++) {
         (void)hipEventDestroy(c->stages[i].a);
         (void)hipEventDestroy(c->stages[i].b);

@@ -10,19 +10,30 @@
 // segment -> 16 strip quads = 96 vertices, node -> 24-triangle fan = 72
 // vertices, ring -> 24 quads = 144 vertices.
 //
-// HBM-write-bound.  The output is cut into fixed tiles of 1536 vertices
-// (36 KiB) so every workgroup writes the same number of bytes: the
-// workgroup locates the rows overlapping its tile, each thread computes
-// whole vertices into an LDS staging tile, and the tile leaves as
-// contiguous 16-byte stores (one 1 KiB wave-instruction per 64 lanes).
+// HBM-write-bound: 24 B per vertex out, a few bytes of geometry in.  A
+// workgroup owns a fixed tile of 2048 vertices (48 KiB out):
+//   1. rows overlapping the tile (tile -> first row precomputed) into LDS;
+//      pair -> row by a prefix-max of row starts (every primitive has an even
+//      vertex count, so vertex PAIRS never straddle a row or a primitive);
+//   2. the <= 23 curve segments overlapping the tile are tessellated once,
+//      all lanes together (17 strip points each: Bezier point, tangent,
+//      normal with one sqrt and two divisions), into LDS — the per-vertex
+//      work that remains is cheap and barely diverges across primitive kinds;
+//   3. each thread emits one pair (48 B) per round into a per-wave LDS
+//      stage; the wave then writes its 64 pairs as three fully contiguous
+//      1 KiB store instructions.
 #include "wg_internal.h"
 #include "wgraph_tess.h"
 
 namespace {
 
 constexpr int VT = 256;
-constexpr int TILE = WG_VTX_TILE;
-constexpr int MAXR = TILE / WG_VTX_PER_NODE + 3;
+constexpr int TILE = 2048;                  // vertices per workgroup
+constexpr int PAIRS = TILE / 2;             // 1024
+constexpr int ROUNDS = PAIRS / VT;          // 4
+constexpr int MAXR = TILE / WG_VTX_PER_NODE + 3;          // rows overlapping a tile
+constexpr int MAXC = TILE / WG_VTX_PER_CURVE + 3;         // curve segments overlapping a tile
+constexpr int NPTS = WG_TESS_CURVE_SEGMENTS + 1;          // 17 strip points per segment
 
 __constant__ float c_cos[25] = WG_UNIT_CIRCLE_COS_INIT;
 __constant__ float c_sin[25] = WG_UNIT_CIRCLE_SIN_INIT;
@@ -37,11 +48,22 @@ __global__ void k_vtx_counts(uint64_t rb, uint64_t re, int64_t sel, const uint32
     cnt[r - rb] = v;
 }
 
+// first row of every tile: the row whose vertex range contains the tile start
+__global__ void k_tile_first(uint64_t rows, const uint64_t *__restrict__ vtx_off, uint32_t *__restrict__ tile_first) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const uint64_t s = vtx_off[r], e = vtx_off[r + 1];
+    for (uint64_t t = (s + TILE - 1) / TILE; t * TILE < e; t++) tile_first[t] = (uint32_t)r;
+}
+
 struct RowInfo {
     uint64_t vstart;
     uint32_t voff, nv, coff, nc;
     float    h, ny, cx;
-    uint32_t ncol, sel;
+    uint32_t ncol;
+    uint32_t cbase;   // first LDS curve slot of this row's tile-overlapping curves
+    uint32_t clo;     // index (within the row) of the first such curve
+    uint32_t pad;
 };
 
 __device__ __forceinline__ float lane_x(uint32_t lane, uint32_t vis) {   // lane_center_x (:786-790)
@@ -54,36 +76,38 @@ __device__ __forceinline__ float clamp_rs(float x, float lo, float hi) {
     return x;
 }
 
-__global__ void __launch_bounds__(VT) k_vtx_tiles(uint64_t rb, uint64_t re, uint64_t total, int64_t sel, uint32_t vis,
+__global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint64_t total, uint32_t vis,
         const uint64_t *__restrict__ vtx_off, const uint32_t *__restrict__ voff, const uint32_t *__restrict__ vert,
         const uint32_t *__restrict__ coff, const wg_curve *__restrict__ curve, const uint8_t *__restrict__ curve_color,
         const float *__restrict__ height, const float *__restrict__ node_y, const uint32_t *__restrict__ lane_out,
-        const uint8_t *__restrict__ color_out, const float4 *__restrict__ palette, float *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float stage[TILE * 6];
+        const uint8_t *__restrict__ color_out, const float4 *__restrict__ palette,
+        const uint32_t *__restrict__ tile_first, float4 *__restrict__ out) {
     __shared__ RowInfo rows[MAXR];
-    __shared__ uint32_t s_first, s_nrows;
+    __shared__ uint32_t pair_row[PAIRS];
+    __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
+    __shared__ uint32_t slot_row[MAXC];
+    __shared__ uint32_t curve_col[MAXC];
+    __shared__ __attribute__((aligned(16))) float4 stage[VT / 64][64 * 3];
+    __shared__ uint32_t wmax[VT / 64];
+    __shared__ uint32_t s_ncurves;
     __shared__ float4 pal[WG_PALETTE_SIZE];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t v0 = (uint64_t)blockIdx.x * TILE;
     const uint64_t v1 = (v0 + TILE < total) ? v0 + TILE : total;
     const uint64_t nrows = re - rb;
-    if (threadIdx.x < WG_PALETTE_SIZE) pal[threadIdx.x] = palette[threadIdx.x];
-    if (threadIdx.x == 0) {
-        // last row with vtx_off[row] <= v0
-        uint64_t lo = 0, hi = nrows - 1;
-        while (lo < hi) {
-            uint64_t mid = (lo + hi + 1) / 2;
-            if (vtx_off[mid] <= v0) lo = mid; else hi = mid - 1;
-        }
-        s_first = (uint32_t)lo;
-        s_nrows = 0;
-    }
+    const float visf = (float)(vis - 1);
+    if (tid < WG_PALETTE_SIZE) pal[tid] = palette[tid];
+    for (uint32_t p = tid; p < PAIRS; p += VT) pair_row[p] = 0;
+    const uint64_t first = tile_first[blockIdx.x];
     __syncthreads();
-    const uint64_t first = s_first;
-    if (threadIdx.x < MAXR) {
-        const uint64_t j = first + threadIdx.x;
-        if (j < nrows && vtx_off[j] < v1) {
+    // ---- 1. rows overlapping the tile (wave 0) -------------------------------------
+    if (wid == 0) {
+        const uint64_t j = first + lane;
+        const bool in = lane < (uint32_t)MAXR && j < nrows && vtx_off[j < nrows ? j : 0] < v1;
+        RowInfo ri{};
+        uint32_t ncur = 0;
+        if (in) {
             const uint64_t r = rb + j;
-            RowInfo ri;
             ri.vstart = vtx_off[j];
             ri.voff = voff[r];
             ri.nv = voff[r + 1] - ri.voff;
@@ -93,46 +117,65 @@ __global__ void __launch_bounds__(VT) k_vtx_tiles(uint64_t rb, uint64_t re, uint
             ri.ny = node_y[r];
             ri.cx = lane_x(lane_out[r], vis);
             ri.ncol = color_out[r];
-            ri.sel = (sel >= 0 && (uint64_t)sel == r) ? 1u : 0u;
-            rows[threadIdx.x] = ri;
-            atomicMax(&s_nrows, threadIdx.x + 1);
+            // this row's curve segments whose 96 vertices intersect [v0, v1)
+            const uint64_t cv = ri.vstart + 6ull * ri.nv;   // first curve vertex
+            if (ri.nc) {
+                const uint64_t lo = v0 > cv ? (v0 - cv) / 96u : 0u;
+                const uint64_t hi_v = v1 - 1;
+                if (hi_v >= cv && lo < ri.nc) {
+                    uint64_t hi = (hi_v - cv) / 96u;
+                    if (hi > ri.nc - 1) hi = ri.nc - 1;
+                    if (hi >= lo) { ri.clo = (uint32_t)lo; ncur = (uint32_t)(hi - lo + 1); }
+                }
+            }
         }
+        // exclusive prefix of curve counts -> LDS curve slots
+        uint32_t inc = ncur;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= (uint32_t)d) inc += o;
+        }
+        ri.cbase = inc - ncur;
+        if (in) {
+            rows[lane] = ri;
+            const uint32_t sp = ri.vstart > v0 ? (uint32_t)((ri.vstart - v0) >> 1) : 0u;
+            pair_row[sp] = lane;   // distinct rows start at distinct pairs (>= 36 pairs per row)
+            for (uint32_t q = 0; q < ncur; q++) slot_row[ri.cbase + q] = lane;
+        }
+        if (lane == 63) s_ncurves = inc;
     }
     __syncthreads();
-    const uint32_t nr = s_nrows;
-    const float hw = WG_LINE_WIDTH * 0.5f;
-    const float visf = (float)(vis - 1);
-    for (uint64_t v = v0 + threadIdx.x; v < v1; v += VT) {
-        uint32_t j = 0;
-        while (j + 1 < nr && rows[j + 1].vstart <= v) j++;
-        const RowInfo &ri = rows[j];
-        uint32_t l = (uint32_t)(v - ri.vstart);
-        float x, y;
-        uint32_t col;
-        if (l < 6u * ri.nv) {
-            const uint32_t e = vert[ri.voff + l / 6u];
-            const uint32_t corner = l % 6u;
-            const float xc = lane_x(WG_VERT_LANE(e), vis);
-            const uint32_t kind = WG_VERT_KIND(e);
-            const float y0 = kind == WG_VERT_BOTTOM ? ri.ny : 0.0f;
-            const float y1 = kind == WG_VERT_TOP ? ri.ny : ri.h;
-            // (xl,y0) (xr,y0) (xl,y1) (xr,y0) (xr,y1) (xl,y1)
-            const bool right = corner == 1 || corner == 3 || corner == 4;
-            const bool low = corner == 2 || corner == 4 || corner == 5;
-            x = right ? xc + hw : xc - hw;
-            y = low ? y1 : y0;
-            col = WG_VERT_COLOR(e);
-        } else if ((l -= 6u * ri.nv) < 96u * ri.nc) {
-            const uint32_t k = ri.coff + l / 96u, m = l % 96u;
-            const uint32_t seg = m / 6u, corner = m % 6u;
-            // corners: L_j R_j L_j+1 R_j R_j+1 L_j+1
-            const uint32_t jj = seg + ((corner == 2 || corner == 4 || corner == 5) ? 1u : 0u);
-            const bool rside = corner == 1 || corner == 3 || corner == 4;
+    // ---- 2a. prefix-max over pair_row: each thread owns ROUNDS consecutive pairs ----------
+    {
+        uint32_t loc[ROUNDS], m = 0;
+#pragma unroll
+        for (int q = 0; q < ROUNDS; q++) { const uint32_t x = pair_row[tid * ROUNDS + q]; m = x > m ? x : m; loc[q] = m; }
+        uint32_t inc = m;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= (uint32_t)d) inc = o > inc ? o : inc;
+        }
+        if (lane == 63) wmax[wid] = inc;
+        uint32_t ex = (uint32_t)__shfl_up((int)inc, 1, 64);
+        if (lane == 0) ex = 0;
+        __syncthreads();
+        for (uint32_t w = 0; w < wid; w++) ex = wmax[w] > ex ? wmax[w] : ex;
+#pragma unroll
+        for (int q = 0; q < ROUNDS; q++) pair_row[tid * ROUNDS + q] = loc[q] > ex ? loc[q] : ex;
+    }
+    // ---- 2b. tessellate the tile's curve segments into LDS ----------------------------------
+    {
+        const uint32_t ncur = s_ncurves;
+        const float hw = WG_LINE_WIDTH * 0.5f;
+        for (uint32_t task = tid; task < ncur * NPTS; task += VT) {
+            const uint32_t slot = task / NPTS, jj = task % NPTS;
+            const RowInfo &ri = rows[slot_row[slot]];
+            const uint32_t k = ri.coff + ri.clo + (slot - ri.cbase);
             const float4 a = reinterpret_cast<const float4 *>(curve + k)[0];
             const float4 b = reinterpret_cast<const float4 *>(curve + k)[1];
             float X[4] = {a.x, a.z, b.x, b.z}, Y[4] = {a.y, a.w, b.y, b.w};
 #pragma unroll
-            for (int q = 0; q < 4; q++) X[q] = clamp_rs(X[q], 0.0f, visf) * WG_LANE_W + WG_LANE_W * 0.5f;   // to_x (:847-850)
+            for (int i = 0; i < 4; i++) X[i] = clamp_rs(X[i], 0.0f, visf) * WG_LANE_W + WG_LANE_W * 0.5f;  // to_x (:847-850)
             const float t = (float)jj * WG_TESS_DT;
             const float s = 1.0f - t;
             const float px = s * s * s * X[0] + 3.0f * s * s * t * X[1] + 3.0f * s * t * t * X[2] + t * t * t * X[3];
@@ -142,46 +185,88 @@ __global__ void __launch_bounds__(VT) k_vtx_tiles(uint64_t rb, uint64_t re, uint
             const float len = sqrtf(dx * dx + dy * dy);
             float nx, ny;
             if (len > 0.0f) { nx = -dy / len; ny = dx / len; } else { nx = 1.0f; ny = 0.0f; }
-            if (rside) { x = px - hw * nx; y = py - hw * ny; }
-            else       { x = px + hw * nx; y = py + hw * ny; }
-            col = curve_color[k];
-        } else if ((l -= 96u * ri.nc) < (uint32_t)WG_VTX_PER_NODE) {
-            const uint32_t tri = l / 3u, corner = l % 3u;
-            const float r = WG_NODE_RADIUS;
-            if (corner == 0) { x = ri.cx; y = ri.ny; }
-            else {
-                const uint32_t q = tri + corner - 1u;
-                x = ri.cx + r * c_cos[q];
-                y = ri.ny + r * c_sin[q];
-            }
-            col = ri.ncol;
-        } else {
-            l -= WG_VTX_PER_NODE;
-            const uint32_t q = l / 6u, corner = l % 6u;
-            const float ri_ = WG_NODE_RADIUS - WG_SELECTED_RING_WIDTH * 0.5f;
-            const float ro = WG_NODE_RADIUS + WG_SELECTED_RING_WIDTH * 0.5f;
-            // o0 i0 o1 i0 i1 o1
-            const bool inner = corner == 1 || corner == 3 || corner == 4;
-            const uint32_t qq = q + ((corner == 2 || corner == 4 || corner == 5) ? 1u : 0u);
-            const float rad = inner ? ri_ : ro;
-            x = ri.cx + rad * c_cos[qq];
-            y = ri.ny + rad * c_sin[qq];
-            col = WG_COLOR_FOREGROUND;
+            pts[task] = make_float4(px + hw * nx, py + hw * ny, px - hw * nx, py - hw * ny);
+            if (jj == 0) curve_col[slot] = curve_color[k];
         }
-        const float4 c4 = pal[col & 7u];
-        float *o = stage + (v - v0) * 6;
-        o[0] = x; o[1] = y; o[2] = c4.x; o[3] = c4.y; o[4] = c4.z; o[5] = c4.w;
     }
     __syncthreads();
-    // contiguous write-out: tile start is 16-byte aligned (TILE * 24 = 36864)
-    const uint64_t nfl = (v1 - v0) * 6;
-    const uint64_t n4 = nfl / 4;
-    float4 *dst = reinterpret_cast<float4 *>(out + v0 * 6);
-    const float4 *src = reinterpret_cast<const float4 *>(stage);
-    for (uint64_t i = threadIdx.x; i < n4; i += VT) dst[i] = src[i];
-    if (threadIdx.x == 0 && (nfl & 3)) {
-        float2 *d2 = reinterpret_cast<float2 *>(out + v0 * 6 + n4 * 4);
-        *d2 = make_float2(stage[n4 * 4], stage[n4 * 4 + 1]);
+    // ---- 3. emit pairs; per-wave LDS transpose -> contiguous stores --------------------------
+    const float hw = WG_LINE_WIDTH * 0.5f;
+    const uint32_t npairs = (uint32_t)((v1 - v0) >> 1);
+    float4 *st = stage[wid];
+#pragma unroll 1
+    for (int q = 0; q < ROUNDS; q++) {
+        const uint32_t wbase = q * VT + wid * 64;          // this wave's first pair in the round
+        if (wbase >= npairs) break;
+        const uint32_t p = wbase + lane;
+        if (p < npairs) {
+            const RowInfo &ri = rows[pair_row[p]];
+            uint32_t l = (uint32_t)(v0 + 2ull * p - ri.vstart);   // even
+            float xa, ya, xb, yb;
+            uint32_t col;
+            if (l < 6u * ri.nv) {
+                const uint32_t e = vert[ri.voff + l / 6u];
+                const uint32_t corner = l % 6u;   // 0, 2, 4
+                const float xc = lane_x(WG_VERT_LANE(e), vis);
+                const uint32_t kind = WG_VERT_KIND(e);
+                const float y0 = kind == WG_VERT_BOTTOM ? ri.ny : 0.0f;
+                const float y1 = kind == WG_VERT_TOP ? ri.ny : ri.h;
+                const float xl = xc - hw, xr = xc + hw;
+                // (xl,y0) (xr,y0) | (xl,y1) (xr,y0) | (xr,y1) (xl,y1)
+                xa = corner == 4 ? xr : xl;
+                ya = corner == 0 ? y0 : y1;
+                xb = corner == 4 ? xl : xr;
+                yb = corner == 4 ? y1 : y0;
+                col = WG_VERT_COLOR(e);
+            } else if ((l -= 6u * ri.nv) < 96u * ri.nc) {
+                const uint32_t slot = ri.cbase + (l / 96u - ri.clo), m = l % 96u;
+                const uint32_t seg = m / 6u, corner = m % 6u;   // 0, 2, 4
+                // L_j R_j | L_j+1 R_j | R_j+1 L_j+1
+                const float4 pa = pts[slot * NPTS + seg + (corner == 0 ? 0u : 1u)];
+                const float4 pb = pts[slot * NPTS + seg + (corner == 4 ? 1u : 0u)];
+                if (corner == 4) { xa = pa.z; ya = pa.w; xb = pb.x; yb = pb.y; }
+                else             { xa = pa.x; ya = pa.y; xb = pb.z; yb = pb.w; }
+                col = curve_col[slot];
+            } else if ((l -= 96u * ri.nc) < (uint32_t)WG_VTX_PER_NODE) {
+                const float r = WG_NODE_RADIUS;
+                // fan triangle t: (C, Q_t, Q_t+1); vertices l and l+1 may sit in two triangles
+                const uint32_t ta = l / 3u, ca = l % 3u, tb = (l + 1) / 3u, cb = (l + 1) % 3u;
+                const uint32_t qa = ta + ca - 1u, qb = tb + cb - 1u;
+                xa = ca == 0 ? ri.cx : ri.cx + r * c_cos[ca == 0 ? 0 : qa];
+                ya = ca == 0 ? ri.ny : ri.ny + r * c_sin[ca == 0 ? 0 : qa];
+                xb = cb == 0 ? ri.cx : ri.cx + r * c_cos[cb == 0 ? 0 : qb];
+                yb = cb == 0 ? ri.ny : ri.ny + r * c_sin[cb == 0 ? 0 : qb];
+                col = ri.ncol;
+            } else {
+                l -= WG_VTX_PER_NODE;
+                const uint32_t qd = l / 6u, corner = l % 6u;   // 0, 2, 4
+                const float rin = WG_NODE_RADIUS - WG_SELECTED_RING_WIDTH * 0.5f;
+                const float ro = WG_NODE_RADIUS + WG_SELECTED_RING_WIDTH * 0.5f;
+                // o_q i_q | o_q+1 i_q | i_q+1 o_q+1
+                const uint32_t ia = corner == 0 ? qd : qd + 1u, ib = corner == 4 ? qd + 1u : qd;
+                const float ra = corner == 4 ? rin : ro, rbr = corner == 4 ? ro : rin;
+                xa = ri.cx + ra * c_cos[ia]; ya = ri.ny + ra * c_sin[ia];
+                xb = ri.cx + rbr * c_cos[ib]; yb = ri.ny + rbr * c_sin[ib];
+                col = WG_COLOR_FOREGROUND;
+            }
+            const float4 c4 = pal[col & 7u];
+            st[lane * 3 + 0] = make_float4(xa, ya, c4.x, c4.y);
+            st[lane * 3 + 1] = make_float4(c4.z, c4.w, xb, yb);
+            st[lane * 3 + 2] = c4;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the wave's pairs [wbase, wbase + cnt) are 3 * cnt contiguous float4 in the output
+        const uint32_t cnt = (npairs - wbase) < 64u ? (npairs - wbase) : 64u;
+        float4 *dst = out + (v0 / 2 + wbase) * 3;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const uint32_t i = k * 64 + lane;
+            if (i < cnt * 3) dst[i] = st[i];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -220,19 +305,22 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     uint64_t total = 0;
     WG_HIP(c, hipMemcpyAsync(&total, off + rows, 8, hipMemcpyDeviceToHost, s));
     WG_HIP(c, hipStreamSynchronize(s));
-    wg_stage_end(c);
     c->n_vtx = total;
     WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
     float q = roundf(c->graph_width / WG_LANE_W);
     uint32_t vis = q <= 0.0f ? 0u : (uint32_t)q;
     if (vis < 1) vis = 1;
     const uint64_t ntiles = (total + TILE - 1) / TILE;
+    WG_ALLOC(c, c->tile_first, ntiles * 4 + 4);
+    hipLaunchKernelGGL(k_tile_first, dim3((rows + 255) / 256), dim3(256), 0, s, rows, (const uint64_t *)off,
+                       c->tile_first.as<uint32_t>());
+    wg_stage_end(c);
     wg_stage_begin(c, "vtx_emit");
-    hipLaunchKernelGGL(k_vtx_tiles, dim3(ntiles), dim3(VT), 0, s, rb, re, total, sel, vis, (const uint64_t *)off,
+    hipLaunchKernelGGL(k_vtx_tile, dim3(ntiles), dim3(VT), 0, s, rb, re, total, vis, (const uint64_t *)off,
                        c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
                        c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
                        c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
-                       c->palette.as<const float4>(), c->vtx.as<float>());
+                       c->palette.as<const float4>(), c->tile_first.as<const uint32_t>(), c->vtx.as<float4>());
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;
