@@ -8,23 +8,27 @@
 // passed: bit-exact by construction, no transcendental on the GPU.
 //
 // row_top_y: `acc += h + band` in f32, strictly sequential (:329-335,
-// :374-381).  Past 2^24 px every add rounds, so a plain prefix sum is wrong.
-// Within one binade [2^k, 2^k+1) (ulp u) the rounding of acc + s depends on
-// acc only through the parity of acc/u (ties-to-even), so each row is a
-// 2-state transducer {parity -> (ulps added, new parity)}; transducers
-// compose associatively.  The scan runs in three parallel kernels plus one
-// single-wave walk:
-//   rt_sum     per 1024-row chunk: f64 sum of steps, validity flags
-//   rt_prefix  f64 prefix of chunk sums -> guessed binade per chunk
-//   rt_tables  per chunk, 4 candidate binades: composed chunk transducer
-//   rt_walk    one wave composes 64 chunk transducers per step (ordered
-//              shuffle scan) from the exact running f32 value; a chunk in
-//              which acc crosses a binade (a handful per run) is replayed
-//              serially by the wave
-//   rt_rows    per chunk: block scan of row transducers from the chunk's
-//              exact start -> row_top for every row
-// Steps that are negative / non-finite make the walk replay every chunk
-// serially (exact, slow; flagged in wg_geometry_summary.scan_path).
+// :374-381).  Two regimes keep it parallel and still bit-exact:
+//   * exact regime — while every step is an integer and the running sum stays
+//     <= 2^24, every f32 add is exact: row_top is the plain integer prefix.
+//   * rounding regime — within one binade [2^k, 2^k+1) (ulp u) the rounding
+//     of acc + s depends on acc only through the parity of acc/u
+//     (ties-to-even), so each row is a 2-state transducer {parity -> (ulps
+//     added, new parity)}; transducers compose associatively.
+// Kernels (chunks of 1024 rows):
+//   rt_sum     f64 chunk sums, "all steps integral" and validity flags
+//   rt_prefix  exact f64 prefix of chunk sums; marks the exact-regime chunks
+//              and guesses every other chunk's binade
+//   rt_tables  per non-exact chunk, 4 candidate binades: composed transducer
+//   rt_walk    one wave, from the first non-exact chunk: composes 64 chunk
+//              transducers per step (ordered shuffle scan) from the exact
+//              running f32 value; a chunk in which acc crosses a binade is
+//              replayed by the wave 64 rows at a time with one transducer
+//              scan per crossing
+//   rt_rows    per chunk: exact prefix, or block scan of row transducers from
+//              the chunk's exact start
+// Negative or non-finite steps make the walk replay every row one by one
+// (exact, slow; flagged in wg_geometry_summary.scan_path).
 #include <cmath>
 
 #include "wg_internal.h"
@@ -33,14 +37,19 @@ namespace {
 
 constexpr int RT_T = 256;                 // threads per chunk block
 constexpr int RT_Q = WG_RT_CHUNK / RT_T;  // rows per thread (4)
+constexpr double TWO24 = 16777216.0;
+
+enum : uint32_t { MODE_TABLE = 0, MODE_REPLAYED = 1, MODE_EXACT = 2 };
 
 struct RtChunk {
-    double   sum;     // f64 sum of steps in the chunk
-    double   prefix;  // f64 exclusive prefix (guess only)
+    double   sum;     // f64 sum of steps in the chunk (exact for integral steps)
+    double   prefix;  // f64 exclusive prefix (exact in the exact regime, else a guess)
     int32_t  kguess;  // binade of prefix
-    uint32_t mode;    // 0 = table path, 1 = replayed serially by the walk
-    float    start;   // exact f32 acc at chunk start (mode 0)
-    int32_t  kstart;  // binade of start (mode 0)
+    uint32_t mode;    // MODE_*
+    float    start;   // exact f32 acc at chunk start (MODE_TABLE / MODE_EXACT)
+    int32_t  kstart;  // binade of start (MODE_TABLE)
+    uint32_t integral;// every step of the chunk is an integer < 2^24
+    uint32_t pad;
 };
 
 // 2-state transducer: parity p -> (d[p] ulps, o[p]); bit2 of f = valid
@@ -66,6 +75,10 @@ __device__ __forceinline__ Td td_shfl_up(const Td &v, int d) {
 __device__ __forceinline__ Td td_shfl_down(const Td &v, int d) {
     return Td{(uint32_t)__shfl_down((int)v.d0, d, 64), (uint32_t)__shfl_down((int)v.d1, d, 64),
               (uint32_t)__shfl_down((int)v.f, d, 64)};
+}
+__device__ __forceinline__ Td td_shfl(const Td &v, int lane) {
+    return Td{(uint32_t)__shfl((int)v.d0, lane, 64), (uint32_t)__shfl((int)v.d1, lane, 64),
+              (uint32_t)__shfl((int)v.f, lane, 64)};
 }
 
 // The step at binade k: acc = 2^k + p*u represents every acc of parity p.
@@ -124,54 +137,74 @@ __global__ void __launch_bounds__(RT_T) k_rt_sum(uint64_t n, const float *__rest
     const uint64_t c = blockIdx.x;
     const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
     double sum = 0.0;
-    bool bad = false;
+    bool bad = false, frac = false;
 #pragma unroll
     for (int q = 0; q < RT_Q; q++) {
         const uint64_t i = r0 + q;
         if (i < n) {
             const float s = step_of(h, band, i);
             bad |= !(s >= 0.0f) || !isfinite(s);
+            frac |= !(s == truncf(s) && s < 16777216.0f);
             sum += (double)s;
         }
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
     __shared__ double ws[RT_T / 64];
+    __shared__ uint32_t wf[RT_T / 64];
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_down(sum, d, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = sum;
+    const bool anyfrac = __any(frac);
+    if ((threadIdx.x & 63) == 0) { ws[threadIdx.x >> 6] = sum; wf[threadIdx.x >> 6] = anyfrac ? 1u : 0u; }
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
-        for (int w = 0; w < RT_T / 64; w++) t += ws[w];
+        uint32_t fr = 0;
+        for (int w = 0; w < RT_T / 64; w++) { t += ws[w]; fr |= wf[w]; }
         ch[c].sum = t;
+        ch[c].integral = fr ? 0u : 1u;
     }
 }
 
-__global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__restrict__ ch) {
+// exact f64 prefix over chunks; exact-regime marking; binade guesses
+__global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__restrict__ ch, uint32_t *__restrict__ flags) {
     __shared__ double ws[16];
+    __shared__ uint32_t wn[16];
     __shared__ double carry;
-    if (threadIdx.x == 0) carry = 0.0;
+    __shared__ uint32_t carry_int;   // all chunks so far integral
+    if (threadIdx.x == 0) { carry = 0.0; carry_int = 1u; }
     __syncthreads();
     for (uint64_t base = 0; base < nch; base += 1024) {
         const uint64_t c = base + threadIdx.x;
         const double v = c < nch ? ch[c].sum : 0.0;
+        const uint32_t nonint = (c < nch && !ch[c].integral) ? 1u : 0u;
         double inc = v;
+        uint32_t ninc = nonint;   // inclusive count of non-integral chunks
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         for (int d = 1; d < 64; d <<= 1) {
-            double o = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += o;
+            const double o = __shfl_up(inc, d, 64);
+            const uint32_t on = (uint32_t)__shfl_up((int)ninc, d, 64);
+            if (lane >= d) { inc += o; ninc += on; }
         }
-        if (lane == 63) ws[w] = inc;
+        if (lane == 63) { ws[w] = inc; wn[w] = ninc; }
         __syncthreads();
         double wb = 0.0, tot = 0.0;
-        for (int k = 0; k < 16; k++) { if (k < w) wb += ws[k]; tot += ws[k]; }
+        uint32_t nb = 0, ntot = 0;
+        for (int k = 0; k < 16; k++) {
+            if (k < w) { wb += ws[k]; nb += wn[k]; }
+            tot += ws[k];
+            ntot += wn[k];
+        }
         const double pre = carry + wb + inc - v;
+        const uint32_t nonint_incl = nb + ninc;   // non-integral chunks in [base, c]
         if (c < nch) {
             ch[c].prefix = pre;
             ch[c].kguess = pre > 0.0 ? ilogb(pre) : -1000;
-            ch[c].mode = 1;
+            // exact regime: every chunk up to c integral and the sum after c <= 2^24
+            const bool exact = carry_int && nonint_incl == 0 && pre + v <= TWO24 && !flags[0];
+            ch[c].mode = exact ? MODE_EXACT : MODE_REPLAYED;
+            ch[c].start = (float)pre;
         }
         __syncthreads();
-        if (threadIdx.x == 0) carry += tot;
+        if (threadIdx.x == 0) { carry += tot; if (ntot) carry_int = 0u; }
         __syncthreads();
     }
 }
@@ -179,6 +212,7 @@ __global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__res
 __global__ void __launch_bounds__(RT_T) k_rt_tables(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
                                                     const RtChunk *__restrict__ ch, uint4 *__restrict__ tables) {
     const uint64_t c = blockIdx.x;
+    if (ch[c].mode == MODE_EXACT) return;
     const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
     float s[RT_Q];
 #pragma unroll
@@ -207,7 +241,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_tables(uint64_t n, const float *__r
     }
 }
 
-// Replay rows [r0, r1) serially from acc (one wave; steps prefetched 64 at a time).
+// Replay rows [r0, r1) from acc one by one (negative / non-finite steps).
 __device__ float serial_rows(uint64_t r0, uint64_t r1, float acc, const float *__restrict__ h,
                              const float *__restrict__ band, float *__restrict__ row_top) {
     const int lid = threadIdx.x & 63;
@@ -226,17 +260,77 @@ __device__ float serial_rows(uint64_t r0, uint64_t r1, float acc, const float *_
     return acc;
 }
 
+// Replay rows [r0, r1) from acc (steps finite, >= 0) 64 rows at a time: one
+// ordered transducer scan per binade the running value passes through.
+__device__ float replay_rows(uint64_t r0, uint64_t r1, float acc, const float *__restrict__ h,
+                             const float *__restrict__ band, float *__restrict__ row_top) {
+    const uint32_t lid = threadIdx.x & 63;
+    for (uint64_t base = r0; base < r1; base += 64) {
+        const uint64_t i = base + lid;
+        const uint32_t cnt = (uint32_t)((r1 - base) < 64 ? (r1 - base) : 64);
+        const float sv = lid < cnt ? step_of(h, band, i) : 0.0f;
+        float mine = 0.0f;
+        uint32_t j = 0;   // first row of the piece not yet placed (uniform)
+        while (j < cnt) {
+            if (!(acc >= 1.0e-30f)) {   // acc == 0 (or tiny): one exact step
+                const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sv), (int)j));
+                if (lid == j) mine = acc;
+                acc = acc + sj;
+                j++;
+                continue;
+            }
+            const int k = binade_of(acc);
+            const float u = ldexpf(1.0f, k - 23);
+            const double top = ldexp(1.0, k + 1);
+            const uint32_t p = ((uint32_t)(acc / u)) & 1u;
+            Td t = (lid >= j && lid < cnt) ? row_td(sv, k) : td_identity();
+            for (int d = 1; d < 64; d <<= 1) {
+                const Td o = td_shfl_up(t, d);
+                if (lid >= (uint32_t)d) t = td_compose(o, t);
+            }
+            const uint32_t D = p ? t.d1 : t.d0;   // ulps added through this lane's row
+            const bool ok = (t.f & 4u) && (double)acc + (double)D * (double)u < top;
+            const uint64_t okm = __ballot(ok || lid < j) | (cnt < 64 ? (~0ull << cnt) : 0ull);
+            const uint32_t f = okm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);   // first row crossing the binade
+            const uint32_t Dprev = (uint32_t)__shfl_up((int)D, 1, 64);
+            if (lid >= j && lid < f) mine = acc + (float)(lid == j ? 0u : Dprev) * u;
+            if (f > j) acc = acc + (float)(uint32_t)__shfl((int)D, (int)(f - 1), 64) * u;
+            j = f;
+            if (j < cnt) {   // the crossing row itself: one ordinary f32 add
+                const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sv), (int)j));
+                if (lid == j) mine = acc;
+                acc = acc + sj;
+                j++;
+            }
+        }
+        if (lid < cnt) row_top[i] = mine;
+    }
+    return acc;
+}
+
 __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const float *__restrict__ h,
                                                 const float *__restrict__ band, RtChunk *__restrict__ ch,
                                                 const uint4 *__restrict__ tables, uint32_t *__restrict__ flags,
                                                 float *__restrict__ row_top) {
     const int lid = threadIdx.x & 63;
     const bool all_serial = flags[0] != 0;
-    float A = 0.0f;
-    uint64_t c = 0, serial_chunks = 0;
+    // skip the exact-regime prefix (its chunks are independent prefix sums)
+    uint64_t c = 0;
+    if (!all_serial) {
+        for (uint64_t b = 0; b < nch; b += 64) {
+            const uint64_t cc = b + lid;
+            const uint64_t m = __ballot(cc < nch && ch[cc].mode == MODE_EXACT);
+            if (m == ~0ull) { c = b + 64; continue; }
+            c = b + (uint64_t)__builtin_ctzll(~m);
+            break;
+        }
+        if (c > nch) c = nch;
+    }
+    float A = c == 0 ? 0.0f : (float)(ch[c - 1].prefix + ch[c - 1].sum);   // exact (<= 2^24, integral)
+    uint64_t replayed = 0;
     while (c < nch) {
-        bool do_serial = all_serial || !(A > 0.0f) || !isfinite(A);
-        if (!do_serial) {
+        bool do_replay = all_serial || !(A > 0.0f) || !isfinite(A);
+        if (!do_replay) {
             const int k = binade_of(A);
             const float u = ldexpf(1.0f, k - 23);
             const double top = ldexp(1.0, k + 1);
@@ -264,26 +358,26 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
                 const uint32_t dp = lid == 0 ? 0u : Dprev;
                 ch[cc].start = A + (float)dp * u;
                 ch[cc].kstart = k;
-                ch[cc].mode = 0;
+                ch[cc].mode = MODE_TABLE;
             }
             if (f > 0) {
                 const uint32_t Dl = (uint32_t)__shfl((int)D, f - 1, 64);
                 A = A + (float)Dl * u;
                 c += f;
             }
-            do_serial = f < 64 && c < nch;
+            do_replay = f < 64 && c < nch;
         }
-        if (do_serial && c < nch) {
+        if (do_replay && c < nch) {
             const uint64_t r0 = c * WG_RT_CHUNK, r1 = (r0 + WG_RT_CHUNK < n) ? r0 + WG_RT_CHUNK : n;
-            A = serial_rows(r0, r1, A, h, band, row_top);
-            if (lid == 0) ch[c].mode = 1;
+            A = all_serial ? serial_rows(r0, r1, A, h, band, row_top) : replay_rows(r0, r1, A, h, band, row_top);
+            if (lid == 0) ch[c].mode = MODE_REPLAYED;
             c++;
-            serial_chunks++;
+            replayed++;
         }
     }
     if (lid == 0) {
         row_top[n] = A;
-        flags[1] = (uint32_t)serial_chunks;
+        flags[1] = (uint32_t)replayed;
         flags[2] = all_serial ? 1u : 0u;
     }
 }
@@ -291,12 +385,37 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
 __global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
                                                   const RtChunk *__restrict__ ch, float *__restrict__ row_top) {
     const uint64_t c = blockIdx.x;
-    if (ch[c].mode != 0) return;
-    const int k = ch[c].kstart;
+    const uint32_t mode = ch[c].mode;
+    if (mode == MODE_REPLAYED) return;
+    const int lid = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
     const float A = ch[c].start;
+    if (mode == MODE_EXACT) {
+        // every partial sum is an integer <= 2^24: the f32 scan is exact
+        float s[RT_Q], t = 0.0f;
+#pragma unroll
+        for (int q = 0; q < RT_Q; q++) { s[q] = (r0 + q < n) ? step_of(h, band, r0 + q) : 0.0f; t += s[q]; }
+        float inc = t;
+        for (int d = 1; d < 64; d <<= 1) {
+            const float o = __shfl_up(inc, d, 64);
+            if (lid >= d) inc += o;
+        }
+        __shared__ float wsum[RT_T / 64];
+        if (lid == 63) wsum[w] = inc;
+        __syncthreads();
+        float run = A + (inc - t);
+        for (int k2 = 0; k2 < w; k2++) run += wsum[k2];
+        // every partial value is an exact integer, so the association order is irrelevant
+#pragma unroll
+        for (int q = 0; q < RT_Q; q++) {
+            if (r0 + q < n) row_top[r0 + q] = run;
+            run += s[q];
+        }
+        return;   // row_top[n] is written by the walk
+    }
+    const int k = ch[c].kstart;
     const float u = ldexpf(1.0f, k - 23);
     const uint32_t p0 = ((uint32_t)(A / u)) & 1u;
-    const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
     Td tr[RT_Q];
     Td t = td_identity();
 #pragma unroll
@@ -305,7 +424,6 @@ __global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, const float *__res
         t = td_compose(t, tr[q]);
     }
     // ordered block exclusive scan
-    const int lid = threadIdx.x & 63, w = threadIdx.x >> 6;
     Td inc = t;
     for (int d = 1; d < 64; d <<= 1) {
         Td o = td_shfl_up(inc, d);
@@ -390,7 +508,7 @@ int wg_stage_rowtop(wg_ctx *c, const float *d_band) {
     RtChunk *ch = c->rt_chunk.as<RtChunk>();
     uint32_t *fl = c->rt_flags.as<uint32_t>();
     hipLaunchKernelGGL(k_rt_sum, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, ch, fl);
-    hipLaunchKernelGGL(k_rt_prefix, dim3(1), dim3(1024), 0, c->stream, nch, ch);
+    hipLaunchKernelGGL(k_rt_prefix, dim3(1), dim3(1024), 0, c->stream, nch, ch, fl);
     hipLaunchKernelGGL(k_rt_tables, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch,
                        c->rt_tables.as<uint4>());
     hipLaunchKernelGGL(k_rt_walk, dim3(1), dim3(64), 0, c->stream, n, nch, h, d_band, ch,
