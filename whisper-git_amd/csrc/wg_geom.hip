@@ -172,7 +172,8 @@ __global__ void __launch_bounds__(64) k_carry_sort(uint64_t nch, const uint32_t 
 
 // ---- the sweep ---------------------------------------------------------------------
 constexpr int SW_WAVES = 4;
-constexpr int SW_CAP = 512;
+constexpr int SW_CAP = 384;   // edges alive across one row (per wave)
+constexpr int SW_NE = 192;    // edges starting inside the 64-row chunk, staged in LDS
 
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -184,20 +185,35 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         uint32_t *__restrict__ err) {
+    // active list (edges alive at the current row, edge order) + the chunk's own new edges
     __shared__ uint32_t s_eid[SW_WAVES][SW_CAP];
     __shared__ uint32_t s_c[SW_WAVES][SW_CAP];
     __shared__ uint32_t s_p[SW_WAVES][SW_CAP];
     __shared__ uint32_t s_info[SW_WAVES][SW_CAP];
+    __shared__ uint32_t n_c[SW_WAVES][SW_NE];
+    __shared__ uint32_t n_p[SW_WAVES][SW_NE];
+    __shared__ uint32_t n_info[SW_WAVES][SW_NE];
     const int w = threadIdx.x >> 6;
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t q = (uint64_t)blockIdx.x * SW_WAVES + w;
     if (q >= nch) return;
     uint32_t *E = s_eid[w], *C = s_c[w], *P = s_p[w], *I = s_info[w];
+    uint32_t *NC = n_c[w], *NP = n_p[w], *NI = n_info[w];
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
+    const uint32_t nr = (uint32_t)(R1 - R0);
+    // per-row scalars of the chunk, one row per lane
+    const uint64_t rr = R0 + lid;
+    const uint32_t eoff_v = lid < nr ? edge_off[rr] : 0u;
+    const uint32_t rf_v = lid < nr ? rowflags[rr] : 0u;
+    const uint32_t voff_v = lid < nr ? vert_off[rr] : 0u;
+    const uint32_t coff_v = lid < nr ? curve_off[rr] : 0u;
+    const uint32_t E1 = edge_off[R1];
+    const uint32_t E0 = (uint32_t)__builtin_amdgcn_readlane((int)eoff_v, 0);
+    const bool staged = E1 - E0 <= (uint32_t)SW_NE;
     // carry-in edges (alive across R0), sorted by edge id
     uint32_t cnt = 0;
     {
-        const uint32_t a = q > 0 ? carry_off[q] : 0u, b = q > 0 ? carry_off[q + 1] : 0u;
+        const uint32_t a = carry_off[q], b = carry_off[q + 1];
         if (b - a > (uint32_t)SW_CAP) { if (lid == 0) atomicOr(&err[0], 1u); return; }
         for (uint32_t i = lid; i < b - a; i += 64) {
             const uint32_t k = carry_sorted[a + i];
@@ -207,27 +223,49 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
         }
         cnt = b - a;
     }
-    for (uint64_t r = R0; r < R1; r++) {
+    // the chunk's own edges, staged once (coalesced)
+    if (staged) {
+        for (uint32_t i = lid; i < E1 - E0; i += 64) {
+            const wg_edge e = edges[E0 + i];
+            NC[i] = e.child_row; NP[i] = e.parent_row;
+            NI[i] = (e.child_lane & 0xFFFFFFu) | (e.color << 24) | ((e.child_lane == e.parent_lane) ? 0x10000000u : 0u);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t j = 0; j < nr; j++) {
+        const uint64_t r = R0 + j;
         // append edges whose child is row r (edge order)
-        const uint32_t e0 = edge_off[r], e1 = edge_off[r + 1];
+        const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)eoff_v, (int)j);
+        const uint32_t e1 = (j + 1 < nr) ? (uint32_t)__builtin_amdgcn_readlane((int)eoff_v, (int)(j + 1)) : E1;
         for (uint32_t base = e0; base < e1; base += 64) {
             const uint32_t k = base + lid;
             bool take = false;
-            wg_edge e;
-            if (k < e1) { e = edges[k]; take = e.child_row < e.parent_row; }
+            uint32_t c = 0, p = 0, info = 0;
+            if (k < e1) {
+                if (staged) { c = NC[k - E0]; p = NP[k - E0]; info = NI[k - E0]; }
+                else {
+                    const wg_edge e = edges[k];
+                    c = e.child_row; p = e.parent_row;
+                    info = (e.child_lane & 0xFFFFFFu) | (e.color << 24) | ((e.child_lane == e.parent_lane) ? 0x10000000u : 0u);
+                }
+                take = c < p;
+            }
             const uint64_t m = __ballot(take);
             if (cnt + __builtin_popcountll(m) > (uint32_t)SW_CAP) { if (lid == 0) atomicOr(&err[0], 1u); return; }
             if (take) {
                 const uint32_t pos = cnt + mbcnt(m);
-                E[pos] = k; C[pos] = e.child_row; P[pos] = e.parent_row;
-                I[pos] = (e.child_lane & 0xFFFFFFu) | (e.color << 24) | ((e.child_lane == e.parent_lane) ? 0x10000000u : 0u);
+                E[pos] = k; C[pos] = c; P[pos] = p; I[pos] = info;
             }
             cnt += __builtin_popcountll(m);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const uint8_t rf = rowflags[r];
-        uint32_t fbase = vert_off[r], cbase = curve_off[r], kept = 0;
+        const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)rf_v, (int)j);
+        uint32_t fbase = (uint32_t)__builtin_amdgcn_readlane((int)voff_v, (int)j);
+        uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
+        uint32_t kept = 0;
         for (uint32_t base = 0; base < cnt; base += 64) {
             const uint32_t idx = base + lid;
             const bool act = idx < cnt;
@@ -236,7 +274,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
             __builtin_amdgcn_wave_barrier();
             const bool same = (info & 0x10000000u) != 0;
             const bool full = act && same && c < r && r < p;
-            bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
+            const bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
             const bool curv = act && !same && c <= r && r <= p && !skip;
             const bool keep = act && p > r;
             const uint64_t mf = __ballot(full), mc = __ballot(curv), mk = __ballot(keep);
