@@ -113,7 +113,7 @@ struct wg_ctx {
     DevBuf vtx;             // wg_vertex [n_vtx]
     DevBuf palette;         // float [32]
     DevBuf chk;             // uint64 [1]
-    DevBuf tile_first;      // uint32 [tiles] first row of every vertex tile
+    DevBuf tile_first;      // uint4 [tiles+1] per-tile record (first row, first vertical, first curve, straddles)
     // ---- host-side tables --------------------------------------------------------
     uint32_t h_thresh[32];  // delta thresholds for heights 29..56
     // ---- timing ----------------------------------------------------------------------

@@ -12,10 +12,13 @@
 //
 // HBM-write-bound: 24 B per vertex out, a few bytes of geometry in.  A
 // workgroup owns a fixed tile of 2048 vertices (48 KiB out):
-//   1. rows overlapping the tile (tile -> first row precomputed) into LDS;
-//      pair -> row by a prefix-max of row starts (every primitive has an even
-//      vertex count, so vertex PAIRS never straddle a row or a primitive);
-//   2. the <= 23 curve segments overlapping the tile are tessellated once,
+//   1. one round of independent global loads, all addressed from a per-tile
+//      record (k_tile_info): the rows overlapping the tile, its vertical
+//      entries (one contiguous range of vert[]) and its curve segments (one
+//      contiguous range of curve[]); pair -> row by a prefix-max of row starts
+//      (every primitive has an even vertex count, so vertex PAIRS never
+//      straddle a row or a primitive);
+//   2. the <= 24 curve segments overlapping the tile are tessellated once,
 //      all lanes together (17 strip points each: Bezier point, tangent,
 //      normal with one sqrt and two divisions), into LDS — the per-vertex
 //      work that remains is cheap and barely diverges across primitive kinds;
@@ -34,6 +37,7 @@ constexpr int ROUNDS = PAIRS / VT;          // 4
 constexpr int MAXR = TILE / WG_VTX_PER_NODE + 3;          // rows overlapping a tile
 constexpr int MAXC = TILE / WG_VTX_PER_CURVE + 3;         // curve segments overlapping a tile
 constexpr int NPTS = WG_TESS_CURVE_SEGMENTS + 1;          // 17 strip points per segment
+constexpr int MAXV = TILE / WG_VTX_PER_VERTICAL + 2;      // vertical entries overlapping a tile
 
 __constant__ float c_cos[25] = WG_UNIT_CIRCLE_COS_INIT;
 __constant__ float c_sin[25] = WG_UNIT_CIRCLE_SIN_INIT;
@@ -48,12 +52,41 @@ __global__ void k_vtx_counts(uint64_t rb, uint64_t re, int64_t sel, const uint32
     cnt[r - rb] = v;
 }
 
-// first row of every tile: the row whose vertex range contains the tile start
-__global__ void k_tile_first(uint64_t rows, const uint64_t *__restrict__ vtx_off, uint32_t *__restrict__ tile_first) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= rows) return;
-    const uint64_t s = vtx_off[r], e = vtx_off[r + 1];
-    for (uint64_t t = (s + TILE - 1) / TILE; t * TILE < e; t++) tile_first[t] = (uint32_t)r;
+// Per-tile record, written by the row whose vertex range contains the tile
+// start: {first row, first vertical entry A, first curve K0, straddle bits}.
+// A tile's verticals are vert[A(t) .. A(t+1) + sV(t+1)) and its curves
+// curve[K0(t) .. K0(t+1) + sC(t+1)), because every row's entries are
+// contiguous and rows are consecutive; a sentinel record closes the range.
+__global__ void k_tile_info(uint64_t rb, uint64_t rows, const uint64_t *__restrict__ vtx_off,
+                            const uint32_t *__restrict__ voff, const uint32_t *__restrict__ coff,
+                            uint64_t ntiles, uint4 *__restrict__ info) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= rows) return;
+    const uint64_t r = rb + j;
+    const uint64_t s = vtx_off[j], e = vtx_off[j + 1];
+    const uint32_t vo = voff[r], nv = voff[r + 1] - vo, co = coff[r], nc = coff[r + 1] - co;
+    const uint64_t cv = s + (uint64_t)WG_VTX_PER_VERTICAL * nv;
+    for (uint64_t t = (s + TILE - 1) / TILE; t * TILE < e; t++) {
+        const uint64_t v0 = t * TILE;
+        uint32_t A, K0, fl = 0;
+        if (v0 < cv) {
+            const uint64_t d = v0 - s;
+            A = vo + (uint32_t)(d / WG_VTX_PER_VERTICAL);
+            fl |= (d % WG_VTX_PER_VERTICAL) ? 1u : 0u;
+            K0 = co;
+        } else {
+            A = vo + nv;
+            const uint64_t d = v0 - cv;
+            if (d < (uint64_t)WG_VTX_PER_CURVE * nc) {
+                K0 = co + (uint32_t)(d / WG_VTX_PER_CURVE);
+                fl |= (d % WG_VTX_PER_CURVE) ? 2u : 0u;
+            } else {
+                K0 = co + nc;
+            }
+        }
+        info[t] = make_uint4((uint32_t)j, A, K0, fl);
+    }
+    if (j == rows - 1) info[ntiles] = make_uint4((uint32_t)rows, voff[r + 1], coff[r + 1], 0u);
 }
 
 struct RowInfo {
@@ -61,9 +94,6 @@ struct RowInfo {
     uint32_t voff, nv, coff, nc;
     float    h, ny, cx;
     uint32_t ncol;
-    uint32_t cbase;   // first LDS curve slot of this row's tile-overlapping curves
-    uint32_t clo;     // index (within the row) of the first such curve
-    uint32_t pad;
 };
 
 __device__ __forceinline__ float lane_x(uint32_t lane, uint32_t vis) {   // lane_center_x (:786-790)
@@ -81,96 +111,63 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         const uint32_t *__restrict__ coff, const wg_curve *__restrict__ curve, const uint8_t *__restrict__ curve_color,
         const float *__restrict__ height, const float *__restrict__ node_y, const uint32_t *__restrict__ lane_out,
         const uint8_t *__restrict__ color_out, const float4 *__restrict__ palette,
-        const uint32_t *__restrict__ tile_first, float4 *__restrict__ out) {
+        const uint4 *__restrict__ tinfo, float4 *__restrict__ out) {
     __shared__ RowInfo rows[MAXR];
     __shared__ uint32_t pair_row[PAIRS];
     __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
-    __shared__ uint32_t slot_row[MAXC];
     __shared__ uint32_t curve_col[MAXC];
+    __shared__ uint32_t vents[MAXV];               // the tile's vertical entries
     __shared__ __attribute__((aligned(16))) float4 stage[VT / 64][64 * 3];
     __shared__ uint32_t wmax[VT / 64];
-    __shared__ uint32_t s_ncurves;
     __shared__ float4 pal[WG_PALETTE_SIZE];
+    __shared__ float2 circ[3][WG_TESS_NODE_SEGMENTS + 2];   // r*(cos, sin) for node, ring inner, ring outer radius
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t v0 = (uint64_t)blockIdx.x * TILE;
+    if (tid < 3 * (WG_TESS_NODE_SEGMENTS + 1)) {
+        const uint32_t w = tid / (WG_TESS_NODE_SEGMENTS + 1), q = tid % (WG_TESS_NODE_SEGMENTS + 1);
+        const float r = w == 0 ? WG_NODE_RADIUS
+                      : w == 1 ? WG_NODE_RADIUS - WG_SELECTED_RING_WIDTH * 0.5f
+                               : WG_NODE_RADIUS + WG_SELECTED_RING_WIDTH * 0.5f;
+        circ[w][q] = make_float2(r * c_cos[q], r * c_sin[q]);
+    }
     const uint64_t v1 = (v0 + TILE < total) ? v0 + TILE : total;
     const uint64_t nrows = re - rb;
     const float visf = (float)(vis - 1);
     if (tid < WG_PALETTE_SIZE) pal[tid] = palette[tid];
     for (uint32_t p = tid; p < PAIRS; p += VT) pair_row[p] = 0;
-    const uint64_t first = tile_first[blockIdx.x];
-    __syncthreads();
-    // ---- 1. rows overlapping the tile (wave 0) -------------------------------------
+    const uint4 ti = tinfo[blockIdx.x], tn = tinfo[blockIdx.x + 1];
+    const uint64_t first = ti.x;
+    const uint32_t A = ti.y, K0 = ti.z;
+    uint32_t nV = tn.y + (tn.w & 1u) - A, nC = tn.z + ((tn.w >> 1) & 1u) - K0;
+    nV = nV < (uint32_t)MAXV ? nV : (uint32_t)MAXV;   // bounds hold by construction; never overrun LDS
+    nC = nC < (uint32_t)MAXC ? nC : (uint32_t)MAXC;
+    // ---- 1. one round of independent global loads: rows, verticals, curves ---------
     if (wid == 0) {
-        const uint64_t j = first + lane;
-        const bool in = lane < (uint32_t)MAXR && j < nrows && vtx_off[j < nrows ? j : 0] < v1;
-        RowInfo ri{};
-        uint32_t ncur = 0;
-        if (in) {
-            const uint64_t r = rb + j;
-            ri.vstart = vtx_off[j];
-            ri.voff = voff[r];
-            ri.nv = voff[r + 1] - ri.voff;
-            ri.coff = coff[r];
-            ri.nc = coff[r + 1] - ri.coff;
-            ri.h = height[r];
-            ri.ny = node_y[r];
-            ri.cx = lane_x(lane_out[r], vis);
-            ri.ncol = color_out[r];
-            // this row's curve segments whose 96 vertices intersect [v0, v1)
-            const uint64_t cv = ri.vstart + 6ull * ri.nv;   // first curve vertex
-            if (ri.nc) {
-                const uint64_t lo = v0 > cv ? (v0 - cv) / 96u : 0u;
-                const uint64_t hi_v = v1 - 1;
-                if (hi_v >= cv && lo < ri.nc) {
-                    uint64_t hi = (hi_v - cv) / 96u;
-                    if (hi > ri.nc - 1) hi = ri.nc - 1;
-                    if (hi >= lo) { ri.clo = (uint32_t)lo; ncur = (uint32_t)(hi - lo + 1); }
-                }
-            }
-        }
-        // exclusive prefix of curve counts -> LDS curve slots
-        uint32_t inc = ncur;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
-            if (lane >= (uint32_t)d) inc += o;
-        }
-        ri.cbase = inc - ncur;
-        if (in) {
+        const uint64_t j0 = first + lane;
+        const uint64_t j = j0 < nrows ? j0 : nrows - 1;
+        const uint64_t r = rb + j;
+        RowInfo ri;
+        ri.vstart = vtx_off[j];
+        ri.voff = voff[r];
+        ri.nv = voff[r + 1] - ri.voff;
+        ri.coff = coff[r];
+        ri.nc = coff[r + 1] - ri.coff;
+        ri.h = height[r];
+        ri.ny = node_y[r];
+        ri.cx = lane_x(lane_out[r], vis);
+        ri.ncol = color_out[r];
+        if (lane < (uint32_t)MAXR && j0 < nrows && ri.vstart < v1) {
             rows[lane] = ri;
             const uint32_t sp = ri.vstart > v0 ? (uint32_t)((ri.vstart - v0) >> 1) : 0u;
             pair_row[sp] = lane;   // distinct rows start at distinct pairs (>= 36 pairs per row)
-            for (uint32_t q = 0; q < ncur; q++) slot_row[ri.cbase + q] = lane;
         }
-        if (lane == 63) s_ncurves = inc;
     }
-    __syncthreads();
-    // ---- 2a. prefix-max over pair_row: each thread owns ROUNDS consecutive pairs ----------
+    for (uint32_t i = tid; i < nV; i += VT) vents[i] = vert[A + i];
     {
-        uint32_t loc[ROUNDS], m = 0;
-#pragma unroll
-        for (int q = 0; q < ROUNDS; q++) { const uint32_t x = pair_row[tid * ROUNDS + q]; m = x > m ? x : m; loc[q] = m; }
-        uint32_t inc = m;
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
-            if (lane >= (uint32_t)d) inc = o > inc ? o : inc;
-        }
-        if (lane == 63) wmax[wid] = inc;
-        uint32_t ex = (uint32_t)__shfl_up((int)inc, 1, 64);
-        if (lane == 0) ex = 0;
-        __syncthreads();
-        for (uint32_t w = 0; w < wid; w++) ex = wmax[w] > ex ? wmax[w] : ex;
-#pragma unroll
-        for (int q = 0; q < ROUNDS; q++) pair_row[tid * ROUNDS + q] = loc[q] > ex ? loc[q] : ex;
-    }
-    // ---- 2b. tessellate the tile's curve segments into LDS ----------------------------------
-    {
-        const uint32_t ncur = s_ncurves;
         const float hw = WG_LINE_WIDTH * 0.5f;
-        for (uint32_t task = tid; task < ncur * NPTS; task += VT) {
+        for (uint32_t task = tid; task < nC * NPTS; task += VT) {
             const uint32_t slot = task / NPTS, jj = task % NPTS;
-            const RowInfo &ri = rows[slot_row[slot]];
-            const uint32_t k = ri.coff + ri.clo + (slot - ri.cbase);
+            const uint32_t k = K0 + slot;
             const float4 a = reinterpret_cast<const float4 *>(curve + k)[0];
             const float4 b = reinterpret_cast<const float4 *>(curve + k)[1];
             float X[4] = {a.x, a.z, b.x, b.z}, Y[4] = {a.y, a.w, b.y, b.w};
@@ -190,6 +187,25 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         }
     }
     __syncthreads();
+    // ---- 2. prefix-max over pair_row: each thread owns ROUNDS consecutive pairs ----------
+    {
+        uint32_t loc[ROUNDS], m = 0;
+#pragma unroll
+        for (int q = 0; q < ROUNDS; q++) { const uint32_t x = pair_row[tid * ROUNDS + q]; m = x > m ? x : m; loc[q] = m; }
+        uint32_t inc = m;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= (uint32_t)d) inc = o > inc ? o : inc;
+        }
+        if (lane == 63) wmax[wid] = inc;
+        uint32_t ex = (uint32_t)__shfl_up((int)inc, 1, 64);
+        if (lane == 0) ex = 0;
+        __syncthreads();
+        for (uint32_t w = 0; w < wid; w++) ex = wmax[w] > ex ? wmax[w] : ex;
+#pragma unroll
+        for (int q = 0; q < ROUNDS; q++) pair_row[tid * ROUNDS + q] = loc[q] > ex ? loc[q] : ex;
+    }
+    __syncthreads();
     // ---- 3. emit pairs; per-wave LDS transpose -> contiguous stores --------------------------
     const float hw = WG_LINE_WIDTH * 0.5f;
     const uint32_t npairs = (uint32_t)((v1 - v0) >> 1);
@@ -205,7 +221,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
             float xa, ya, xb, yb;
             uint32_t col;
             if (l < 6u * ri.nv) {
-                const uint32_t e = vert[ri.voff + l / 6u];
+                const uint32_t e = vents[ri.voff + l / 6u - A];
                 const uint32_t corner = l % 6u;   // 0, 2, 4
                 const float xc = lane_x(WG_VERT_LANE(e), vis);
                 const uint32_t kind = WG_VERT_KIND(e);
@@ -219,7 +235,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
                 yb = corner == 4 ? y1 : y0;
                 col = WG_VERT_COLOR(e);
             } else if ((l -= 6u * ri.nv) < 96u * ri.nc) {
-                const uint32_t slot = ri.cbase + (l / 96u - ri.clo), m = l % 96u;
+                const uint32_t slot = ri.coff + l / 96u - K0, m = l % 96u;
                 const uint32_t seg = m / 6u, corner = m % 6u;   // 0, 2, 4
                 // L_j R_j | L_j+1 R_j | R_j+1 L_j+1
                 const float4 pa = pts[slot * NPTS + seg + (corner == 0 ? 0u : 1u)];
@@ -228,25 +244,23 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
                 else             { xa = pa.x; ya = pa.y; xb = pb.z; yb = pb.w; }
                 col = curve_col[slot];
             } else if ((l -= 96u * ri.nc) < (uint32_t)WG_VTX_PER_NODE) {
-                const float r = WG_NODE_RADIUS;
                 // fan triangle t: (C, Q_t, Q_t+1); vertices l and l+1 may sit in two triangles
                 const uint32_t ta = l / 3u, ca = l % 3u, tb = (l + 1) / 3u, cb = (l + 1) % 3u;
-                const uint32_t qa = ta + ca - 1u, qb = tb + cb - 1u;
-                xa = ca == 0 ? ri.cx : ri.cx + r * c_cos[ca == 0 ? 0 : qa];
-                ya = ca == 0 ? ri.ny : ri.ny + r * c_sin[ca == 0 ? 0 : qa];
-                xb = cb == 0 ? ri.cx : ri.cx + r * c_cos[cb == 0 ? 0 : qb];
-                yb = cb == 0 ? ri.ny : ri.ny + r * c_sin[cb == 0 ? 0 : qb];
+                const float2 oa = circ[0][ca == 0 ? 0u : ta + ca - 1u], ob = circ[0][cb == 0 ? 0u : tb + cb - 1u];   // r*cos, r*sin
+                const float xa_ = ri.cx + oa.x, ya_ = ri.ny + oa.y, xb_ = ri.cx + ob.x, yb_ = ri.ny + ob.y;
+                xa = ca == 0 ? ri.cx : xa_;
+                ya = ca == 0 ? ri.ny : ya_;
+                xb = cb == 0 ? ri.cx : xb_;
+                yb = cb == 0 ? ri.ny : yb_;
                 col = ri.ncol;
             } else {
                 l -= WG_VTX_PER_NODE;
                 const uint32_t qd = l / 6u, corner = l % 6u;   // 0, 2, 4
-                const float rin = WG_NODE_RADIUS - WG_SELECTED_RING_WIDTH * 0.5f;
-                const float ro = WG_NODE_RADIUS + WG_SELECTED_RING_WIDTH * 0.5f;
-                // o_q i_q | o_q+1 i_q | i_q+1 o_q+1
+                // o_q i_q | o_q+1 i_q | i_q+1 o_q+1   (circ[1] inner radius, circ[2] outer)
                 const uint32_t ia = corner == 0 ? qd : qd + 1u, ib = corner == 4 ? qd + 1u : qd;
-                const float ra = corner == 4 ? rin : ro, rbr = corner == 4 ? ro : rin;
-                xa = ri.cx + ra * c_cos[ia]; ya = ri.ny + ra * c_sin[ia];
-                xb = ri.cx + rbr * c_cos[ib]; yb = ri.ny + rbr * c_sin[ib];
+                const float2 oa = circ[corner == 4 ? 1 : 2][ia], ob = circ[corner == 4 ? 2 : 1][ib];
+                xa = ri.cx + oa.x; ya = ri.ny + oa.y;
+                xb = ri.cx + ob.x; yb = ri.ny + ob.y;
                 col = WG_COLOR_FOREGROUND;
             }
             const float4 c4 = pal[col & 7u];
@@ -311,16 +325,17 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     uint32_t vis = q <= 0.0f ? 0u : (uint32_t)q;
     if (vis < 1) vis = 1;
     const uint64_t ntiles = (total + TILE - 1) / TILE;
-    WG_ALLOC(c, c->tile_first, ntiles * 4 + 4);
-    hipLaunchKernelGGL(k_tile_first, dim3((rows + 255) / 256), dim3(256), 0, s, rows, (const uint64_t *)off,
-                       c->tile_first.as<uint32_t>());
+    WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
+    hipLaunchKernelGGL(k_tile_info, dim3((rows + 255) / 256), dim3(256), 0, s, rb, rows, (const uint64_t *)off,
+                       c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), ntiles,
+                       c->tile_first.as<uint4>());
     wg_stage_end(c);
     wg_stage_begin(c, "vtx_emit");
     hipLaunchKernelGGL(k_vtx_tile, dim3(ntiles), dim3(VT), 0, s, rb, re, total, vis, (const uint64_t *)off,
                        c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
                        c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
                        c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
-                       c->palette.as<const float4>(), c->tile_first.as<const uint32_t>(), c->vtx.as<float4>());
+                       c->palette.as<const float4>(), c->tile_first.as<const uint4>(), c->vtx.as<float4>());
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;
