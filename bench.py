@@ -162,7 +162,7 @@ def main():
     bytes_w = 24 * vs.n_vertices
     bytes_r = 4 * nvert_shard + 33 * ncurve_shard + n_rows_shard * (8 + 4 + 4 + 4 + 4 + 4 + 1)
     achieved = (bytes_w + bytes_r) / (vtx_ms * 1e-3) / 1e9
-    roofline = {"kernel": "k_vtx_tiles (vtx_emit)", "bound": "hbm", "achieved": round(achieved, 1),
+    roofline = {"kernel": "k_vtx_tile (vtx_emit)", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None, "algorithmic_bytes_per_launch": int(bytes_w + bytes_r),
                 "avg_launch_ms": round(vtx_ms, 4)}

@@ -11,7 +11,7 @@
 // vertices, ring -> 24 quads = 144 vertices.
 //
 // HBM-write-bound: 24 B per vertex out, a few bytes of geometry in.  A
-// workgroup owns a fixed tile of 2048 vertices (48 KiB out):
+// workgroup owns a fixed tile of 4096 vertices (96 KiB out):
 //   1. one round of independent global loads, all addressed from a per-tile
 //      record (k_tile_info): the rows overlapping the tile, its vertical
 //      entries (one contiguous range of vert[]) and its curve segments (one
@@ -30,10 +30,17 @@
 
 namespace {
 
-constexpr int VT = 256;
-constexpr int TILE = 2048;                  // vertices per workgroup
-constexpr int PAIRS = TILE / 2;             // 1024
-constexpr int ROUNDS = PAIRS / VT;          // 4
+#ifndef WG_VTX_THREADS
+#define WG_VTX_THREADS 256
+#endif
+#ifndef WG_VTX_TILE_VERTS
+#define WG_VTX_TILE_VERTS 4096
+#endif
+constexpr int VT = WG_VTX_THREADS;
+constexpr int TILE = WG_VTX_TILE_VERTS;     // vertices per workgroup
+constexpr int PAIRS = TILE / 2;             // 2048
+constexpr int ROUNDS = PAIRS / VT;          // 8
+static_assert(TILE / WG_VTX_PER_NODE + 3 <= 64, "rows of a tile are loaded by one wave");
 constexpr int MAXR = TILE / WG_VTX_PER_NODE + 3;          // rows overlapping a tile
 constexpr int MAXC = TILE / WG_VTX_PER_CURVE + 3;         // curve segments overlapping a tile
 constexpr int NPTS = WG_TESS_CURVE_SEGMENTS + 1;          // 17 strip points per segment
@@ -113,7 +120,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         const uint8_t *__restrict__ color_out, const float4 *__restrict__ palette,
         const uint4 *__restrict__ tinfo, float4 *__restrict__ out) {
     __shared__ RowInfo rows[MAXR];
-    __shared__ uint32_t pair_row[PAIRS];
+    __shared__ uint8_t pair_row[PAIRS];            // row (within the tile) of every vertex pair
     __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
     __shared__ uint32_t curve_col[MAXC];
     __shared__ uint32_t vents[MAXV];               // the tile's vertical entries

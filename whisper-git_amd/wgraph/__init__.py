@@ -24,7 +24,8 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libwgraph.so")
+# WGRAPH_LIB selects an alternative in-tree build of the same engine (kernel variants)
+LIB_PATH = os.environ.get("WGRAPH_LIB") or os.path.join(_HERE, "libwgraph.so")
 _lib = None
 
 
