@@ -226,9 +226,13 @@ int wg_copy_vertex_offsets(wg_ctx *ctx, uint64_t *dst);
 int wg_device_views_get(wg_ctx *ctx, wg_device_views *out);
 
 /* ---- timing (HIP events on the context's stream) ------------------------ */
-#define WG_STAGE_MAX 32
+#define WG_STAGE_MAX 1024
+/* on = 0 disables; on > 0 enables and restarts the stage log (on > 1 also
+ * pre-creates that many stage event pairs, so none is created later).      */
 int wg_enable_timing(wg_ctx *ctx, int on);
-/* Per-stage milliseconds of the last producing calls; names[i] static. */
+/* Per-stage milliseconds of every stage logged since wg_enable_timing, in
+ * launch order (a multi-step run logs each step's stages); names[i] static;
+ * names/ms hold WG_STAGE_MAX entries.                                      */
 int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
 
 /* ---- diagnostics ------------------------------------------------------------

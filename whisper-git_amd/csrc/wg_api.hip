@@ -26,6 +26,7 @@ void wg_stage_begin(wg_ctx *c, const char *name) {
     if (!c->timing) return;
     if (c->n_stages >= WG_STAGE_MAX || c->stage_depth >= 8) { c->stage_stack[c->stage_depth++ & 7] = -1; return; }
     StageTimer &t = c->stages[c->n_stages];
+    if (!t.a) { (void)hipEventCreate(&t.a); (void)hipEventCreate(&t.b); }
     t.name = name;
     (void)hipEventRecord(t.a, c->stream);
     c->stage_stack[c->stage_depth++] = c->n_stages++;
@@ -54,10 +55,6 @@ wg_ctx *wg_create(int device_ordinal) {
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return nullptr; }
     c->own_stream = true;
-    for (int i = 0; i < WG_STAGE_MAX; i++) {
-        (void)hipEventCreate(&c->stages[i].a);
-        (void)hipEventCreate(&c->stages[i].b);
-    }
     wg_init_height_thresholds(c->h_thresh);
     return c;
 }
@@ -77,8 +74,8 @@ void wg_destroy(wg_ctx *c) {
     for (DevBuf &b : c->lf) b.release();
     c->tile_first.release();
     for (int i = 0; i < WG_STAGE_MAX; i++) {
-        (void)hipEventDestroy(c->stages[i].a);
-        (void)hipEventDestroy(c->stages[i].b);
+        if (c->stages[i].a) (void)hipEventDestroy(c->stages[i].a);
+        if (c->stages[i].b) (void)hipEventDestroy(c->stages[i].b);
     }
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -370,6 +367,8 @@ int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
 int wg_enable_timing(wg_ctx *c, int on) {
     if (!c) return WG_E_INVALID;
     c->timing = on != 0;
+    for (int i = 0; i < on && i < WG_STAGE_MAX; i++)
+        if (!c->stages[i].a) { WG_HIP(c, hipEventCreate(&c->stages[i].a)); WG_HIP(c, hipEventCreate(&c->stages[i].b)); }
     c->n_stages = 0;
     c->stage_depth = 0;
     return WG_OK;

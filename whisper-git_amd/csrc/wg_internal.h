@@ -30,8 +30,8 @@ struct DevBuf {
 };
 
 struct StageTimer {
-    const char *name;
-    hipEvent_t  a, b;
+    const char *name = nullptr;
+    hipEvent_t  a = nullptr, b = nullptr;   // created on first use
 };
 
 // Row-top transducer scan geometry (wg_rowtop.hip)

@@ -219,13 +219,15 @@ class Engine:
         self._check(lib().wg_debug_counters(self._ctx, out.ctypes.data, 16))
         return out
 
-    def enable_timing(self, on=True):
-        self._check(lib().wg_enable_timing(self._ctx, 1 if on else 0))
+    def enable_timing(self, on=True, reserve: int = 0):
+        """Start (or stop) the per-stage HIP-event log; `reserve` pre-creates
+        that many stage slots so none is created inside a timed region."""
+        self._check(lib().wg_enable_timing(self._ctx, max(int(reserve), 1) if on else 0))
 
     def timings(self) -> list[tuple[str, float]]:
         n = ctypes.c_int()
-        names = (ctypes.c_char_p * 32)()
-        ms = (ctypes.c_float * 32)()
+        names = (ctypes.c_char_p * abi.WG_STAGE_MAX)()
+        ms = (ctypes.c_float * abi.WG_STAGE_MAX)()
         self._check(lib().wg_stage_timings(self._ctx, ctypes.byref(n), names, ms))
         return [(names[i].decode(), float(ms[i])) for i in range(n.value)]
 

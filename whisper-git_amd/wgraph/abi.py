@@ -9,6 +9,7 @@ WG_OK, WG_E_INVALID, WG_E_HIP, WG_E_NOMEM, WG_E_STATE, WG_E_UNSUPPORTED, WG_E_NO
 WG_HOST, WG_DEVICE = 0, 1
 WG_VERT_FULL, WG_VERT_TOP, WG_VERT_BOTTOM = 0, 1, 2
 WG_COLOR_ORPHAN, WG_COLOR_FOREGROUND, WG_PALETTE_SIZE = 6, 7, 8
+WG_STAGE_MAX = 1024
 VTX_PER_VERTICAL, VTX_PER_CURVE, VTX_PER_NODE, VTX_PER_RING = 6, 96, 72, 144
 
 ERRORS = {WG_E_INVALID: "WG_E_INVALID", WG_E_HIP: "WG_E_HIP", WG_E_NOMEM: "WG_E_NOMEM",
