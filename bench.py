@@ -192,6 +192,26 @@ def main():
         roofline["traffic_bytes_per_launch"] = int(pmc["hbm_bytes_per_launch"])
         roofline["traffic_source"] = pmc["_file"]
 
+    # host-resident variant (reported beside `value`, never as it): the commit
+    # SoA and bands start in pinned-less host memory, so the step includes the
+    # PCIe H2D copies; vertex buffers still land in HBM
+    host_rate = None
+    if rank == 0 and world == 1:
+        host_commits = abi.commits_struct(dag)
+        band_host = np.ascontiguousarray(dag.band)
+
+        def host_step():
+            eng.build(commits=host_commits)
+            eng.row_geometry(band_host)
+            eng.emit_vertices(shard0, shard1, selected=selected, palette=pal)
+        host_step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            host_step()
+        torch.cuda.synchronize()
+        host_rate = rows_total * 3 / (time.perf_counter() - t1)
+
     stages = {k: round(float(v), 4) for k, v in stage_ms.items()}
     log("stage ms (mean over timed steps):", json.dumps(stages))
     log(f"rows {rows_total}, shard {n_rows_shard}, vertices {vs.n_vertices}, vert {gs.n_vert}, curves {gs.n_curve}, "
@@ -209,7 +229,8 @@ def main():
                "config": {"workload": workload,
                           "rows_total": rows_total, "rows_per_gpu": args.rows_per_gpu,
                           "vertices_per_gpu": int(vs.n_vertices), "parallelism": f"row-shard x{world}"},
-               "stages_ms": stages, "roofline": roofline, "cpu_baseline": cpu}
+               "stages_ms": stages, "host_input_rows_per_s": None if host_rate is None else round(host_rate, 1),
+               "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

@@ -22,10 +22,9 @@
 //   chain    every row's "source" event via pointer jumping along w = 1
 //            first-parent chains (log2 N rounds)
 //   events   16-byte event records in row order
-//   loop     ONE wave replays the events: 64-bit occupancy mask in SGPRs,
-//            lowest-free = ctz(~occ); event slots kept in VGPRs for the
-//            current and previous 64-event batch, older ones prefetched from
-//            HBM one batch ahead
+//   replay   the event stream cut into chunks replayed in parallel and
+//            iterated to a fixed point (wg_lanes_replay.hip): 64-bit
+//            occupancy mask, lowest-free = ctz(~occ)
 //   lanes    lane[j] = slot of source(j)   (parallel gather)
 // max_lane = max over occupying allocations of the highest occupied slot
 // (update_peak, :462-471, can only rise when a slot is taken).
@@ -184,107 +183,6 @@ __global__ void k_lf_events(uint64_t n, const uint32_t *__restrict__ poff, const
             ev[e] = make_uint4(F_A | F_O, 0u, 0u, (uint32_t)j);
             e++;
         }
-    }
-}
-
-// ---- the event replay: one wave --------------------------------------------------
-__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
-}
-
-// Straight-line replay (scalar branches cost more than the work): every
-// event computes both the lowest-free slot and the min token slot and
-// selects.  Tokens in the event's own 64-batch are read from the batch's
-// slot register (index packed in the record); all others were resolved into
-// per-lane registers when the batch started (from the previous batch's
-// register by lane permute, or from HBM one batch ahead).
-__global__ void __launch_bounds__(64) k_lf_loop(uint64_t nev, const uint4 *__restrict__ ev,
-                                                const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
-                                                const uint32_t *__restrict__ sp, const uint32_t *__restrict__ secev,
-                                                const uint32_t *__restrict__ winfo, uint8_t *slot_of,
-                                                uint32_t *__restrict__ scal) {
-    const uint32_t lid = threadIdx.x & 63;
-    uint64_t occ = 0;
-    uint32_t max_lane = 0, max_s1 = 0, overflow = 0;
-    uint32_t prev_v = 0;
-    const uint4 none = make_uint4(F_A, 0u, 0u, 0u);
-    uint4 rec = (lid < nev) ? ev[lid] : none;
-    uint4 rec1 = (64 + lid < nev) ? ev[64 + lid] : none;
-    uint32_t q0_v = 0, q1_v = 0;   // HBM-resolved old tokens of the current batch
-    for (uint64_t base = 0; base < nev; base += 64) {
-        const uint32_t f_v = rec.x, t0_v = rec.y, t1_v = rec.z, row_v = rec.w;
-        const uint64_t nb2 = base + 128 + lid;
-        const uint4 rec2 = (nb2 < nev) ? ev[nb2] : none;
-        // old tokens of the NEXT batch: events before `base` are stored already
-        uint32_t n0_v = 0, n1_v = 0;
-        if ((rec1.x & F_C) && (uint64_t)rec1.y < base) n0_v = slot_of[rec1.y];
-        if ((rec1.x & F_C) && (uint64_t)rec1.z < base) n1_v = slot_of[rec1.z];
-        // resolve this batch's out-of-batch tokens: previous batch by permute, older from HBM
-        const uint64_t pbase = base - 64;
-        const uint32_t g0 = (uint32_t)__shfl((int)prev_v, (int)(t0_v & 63u), 64);
-        const uint32_t g1 = (uint32_t)__shfl((int)prev_v, (int)(t1_v & 63u), 64);
-        const uint32_t pre0_v = (base >= 64 && (uint64_t)t0_v >= pbase) ? g0 : q0_v;
-        const uint32_t pre1_v = (base >= 64 && (uint64_t)t1_v >= pbase) ? g1 : q1_v;
-        // one packed word per event: flags | s0 << 8 | s1 << 16 (slots, or the
-        // local index of a token that lives in this same batch)
-        const uint32_t x_v = (f_v & 0xFFu) | (((f_v & F_IN0) ? ((f_v >> 8) & 63u) : (pre0_v & 0xFFu)) << 8) |
-                             (((f_v & F_IN1) ? ((f_v >> 16) & 63u) : (pre1_v & 0xFFu)) << 16) |
-                             ((f_v & F_IN0) ? X_IN0 : 0u) | ((f_v & F_IN1) ? X_IN1 : 0u);
-        uint32_t cur_v = 0;
-        const uint32_t cnt = (uint32_t)((nev - base) < 64 ? (nev - base) : 64);
-        for (uint32_t k = 0; k < cnt; k++) {
-            const uint32_t x = rl(x_v, k);
-            uint32_t s0 = (x >> 8) & 0xFFu, s1 = (x >> 16) & 0xFFu;
-            if (__builtin_expect((x & (X_IN0 | X_IN1)) != 0, 0)) {   // token allocated in this batch
-                if (x & X_IN0) s0 = rl(cur_v, s0);
-                if (x & X_IN1) s1 = rl(cur_v, s1);
-            }
-            uint32_t smin = s0 < s1 ? s0 : s1;
-            uint64_t clr = (1ull << s0) | (1ull << s1);
-            if (__builtin_expect((x & F_M) != 0, 0)) {   // more than two waiters: walk the child list
-                const uint32_t j = rl(row_v, k);
-                const uint32_t a = ch_off[j], b = ch_off[j + 1];
-                for (uint32_t q = a; q <= b; q++) {
-                    uint32_t t;
-                    if (q < b) t = sp[ch[q]] & ~EVF;
-                    else if (winfo[j] & 0x80000000u) t = secev[j];
-                    else break;
-                    uint32_t st;
-                    if (t >= base) st = rl(cur_v, (uint32_t)(t - base));
-                    else if (t + 64 >= base) st = rl(prev_v, (uint32_t)(t + 64 - base));
-                    else st = slot_of[t];
-                    clr |= 1ull << st;
-                    smin = st < smin ? st : smin;
-                }
-            }
-            // branch-free update with integer masks
-            const uint32_t mA = 0u - (x & F_A);                 // A: take the lowest free slot
-            const uint64_t mC = 0ull - (uint64_t)((x >> 2) & 1u); // C: clear token slots
-            const uint64_t mO = 0ull - (uint64_t)((x >> 1) & 1u); // O: occupy own slot
-            const uint64_t fr = ~occ;
-            overflow |= (fr == 0ull) & (x & F_A);
-            const uint32_t sa = (uint32_t)__builtin_ctzll(fr | (1ull << 63));
-            const uint32_t s = (sa & mA) | (smin & ~mA);
-            occ = (occ & ~(clr & mC)) | ((1ull << s) & mO);
-            const uint32_t hb = 63u - (uint32_t)__builtin_clzll(occ | 1ull);
-            const uint32_t mAO = mA & (uint32_t)mO;
-            max_lane = max_lane > (hb & mAO) ? max_lane : (hb & mAO);
-            max_s1 = max_s1 > ((s + 1) & mA) ? max_s1 : ((s + 1) & mA);
-            cur_v = (lid == k) ? s : cur_v;
-        }
-        if (base + lid < nev) slot_of[base + lid] = (uint8_t)cur_v;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        prev_v = cur_v;
-        rec = rec1;
-        rec1 = rec2;
-        q0_v = n0_v;
-        q1_v = n1_v;
-        if (overflow) break;
-    }
-    if (lid == 0) {
-        scal[0] = max_lane;
-        scal[1] = max_s1;
-        scal[2] = overflow;
     }
 }
 
