@@ -34,6 +34,33 @@ struct StageTimer {
     hipEvent_t  a = nullptr, b = nullptr;   // created on first use
 };
 
+// Crossing parent reference (row-sharded builds, wg_shard.hip): a reference
+// from row c to a row p that lies beyond the shard of c.  kf: bits 0..15 the
+// parent index within row c, bit 16 "first occurrence of p among row c's
+// in-list parents" (the greedy ignores repeated parents, :435-459).
+struct WgXEnt { uint32_t c, p, kf, pad; };
+#define WG_XF_FIRST_IN_ROW 0x10000u
+// chain tokens of the lane fast path: an event id, a crossing entry (resolved
+// once the other shards have reported), a row (pointer jumping) or nothing
+#define WG_TOK_EV   0x80000000u
+#define WG_TOK_X    0x40000000u
+#define WG_TOK_NONE 0xFFFFFFFFu
+
+// The rows one lane fast-path run owns: [s, e) of a list whose CSR and
+// resolved parent rows are indexed globally.  A single-GPU build is s = 0,
+// e = N with no crossing entries.
+struct LfRange {
+    uint64_t s = 0, nl = 0, e = 0;
+    const uint32_t *poff = nullptr;   // parent_off, by global row
+    const int32_t *prow = nullptr;    // parent row, by global ref index (own refs)
+    const uint32_t *canon = nullptr;  // by global row, or null (ids known distinct)
+    const WgXEnt *xall = nullptr;     // crossing entries of every shard, shard-major
+    uint64_t xin_end = 0;             // [0, xin_end): entries of earlier shards
+    uint64_t xown_begin = 0, xown_end = 0;   // this shard's own entries
+    uint8_t *isfb = nullptr;          // by global ref index: target beyond e and first reference to it
+    uint32_t *xsec = nullptr;         // by global ref index: SECALLOC token of such a secondary reference
+};
+
 // Row-top transducer scan geometry (wg_rowtop.hip)
 #define WG_RT_CHUNK   1024   // rows per chunk
 #define WG_RT_NBIN    4      // binades tabulated per chunk (guess-1 .. guess+2)
@@ -73,10 +100,12 @@ struct wg_ctx {
     DevBuf lane_out;        // uint32 [N]  layouts.get(id).lane per row
     DevBuf color_out;       // uint8  [N]
     DevBuf lane_scalars;    // uint32 [8]  max_lane, n_slots, overflow, ...
-    DevBuf lf[20];          // event-compressed lane path workspaces (wg_lanes.hip)
+    DevBuf lf[24];          // event-compressed lane path workspaces (wg_lanes_fast.hip)
     uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint64_t n_events = 0;  // events of the last fast-path lane build
+    uint64_t e_refs_own = 0;   // parent references of the rows this context owns
+    bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])
     bool force_general_lanes = false;   // WG_LANES=general (testing the general walk)
     // edges
     DevBuf edge_cnt;        // uint32 [N+1] -> edge_off after scan
@@ -157,12 +186,19 @@ hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, 
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
 int wg_stage_lanes(wg_ctx *c);                // wg_lanes.hip
 int wg_lanes_fast(wg_ctx *c, bool *used);     // wg_lanes_fast.hip
-hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *ch_off,
-                          const uint32_t *ch, const uint32_t *sp, const uint32_t *secev, const uint32_t *winfo,
+hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *aux,
                           uint8_t *slots_a, uint8_t *slots_b, unsigned long long *occ_a, unsigned long long *occ_b,
                           uint32_t *stats, uint32_t *flags, uint32_t max_iters, uint32_t *scal, uint8_t **slot_out,
                           uint32_t *iters);  // wg_lanes_replay.hip
 int wg_stage_edges(wg_ctx *c);                // wg_lanes.hip
+// event-compressed lane phases over a row range (wg_lanes_fast.hip)
+int wg_lf_refs(wg_ctx *c, const LfRange &R, uint32_t *viol, uint64_t *nev, uint64_t *naux);
+int wg_lf_chain(wg_ctx *c, const LfRange &R);
+int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok);
+int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint4 *ev_out, uint32_t *aux_out,
+                 uint32_t aux_base);
+int wg_lf_replay(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, const uint8_t **slots, bool *converged);
+int wg_lf_lanes(wg_ctx *c, const LfRange &R, const uint8_t *slots, uint32_t *lane);
 int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
 int wg_stage_rowtop(wg_ctx *c, const float *d_band);   // wg_rowtop.hip
 int wg_stage_geometry(wg_ctx *c, const float *d_band); // wg_geom.hip

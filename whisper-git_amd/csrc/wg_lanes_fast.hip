@@ -18,33 +18,38 @@
 // Only those events touch the slot-occupancy state, and they are a few
 // percent of rows.  The pipeline:
 //   refs     first reference + first-parent child count per row (atomics)
-//   rows     w(j), event counts -> scan -> event ids
-//   chain    every row's "source" event via pointer jumping along w = 1
+//   rows     w(j), event and merge-token counts -> scans -> event ids
+//   chain    every row's "source" token via pointer jumping along w = 1
 //            first-parent chains (log2 N rounds)
-//   events   16-byte event records in row order
+//   events   16-byte event records in row order; merges with more than two
+//            waiters list all their tokens in an aux array
 //   replay   the event stream cut into chunks replayed in parallel and
 //            iterated to a fixed point (wg_lanes_replay.hip): 64-bit
 //            occupancy mask, lowest-free = ctz(~occ)
 //   lanes    lane[j] = slot of source(j)   (parallel gather)
 // max_lane = max over occupying allocations of the highest occupied slot
 // (update_peak, :462-471, can only rise when a slot is taken).
+//
+// Every phase works on a row range [s, e) (LfRange): a single-GPU build is
+// the whole list; a row-sharded build (wg_shard.hip) runs the same phases on
+// its shard, with the references that cross shard boundaries supplied as
+// crossing entries.  A waiter created before s is a crossing token (WG_TOK_X)
+// until the other shards report which event started its chain.
 #include "wg_internal.h"
 
 namespace {
 
 constexpr int T = 256;
-constexpr uint32_t EVF = 0x80000000u;   // "is an event id" tag in the chain pointers
 constexpr uint64_t REF_NONE = ~0ull;
+constexpr uint32_t TAGS = WG_TOK_EV | WG_TOK_X;
 
 // event record flags (uint4.x): A = takes the lowest free slot, O = occupies
 // its slot afterwards, C = clears its token slots (MIN / FREE), M = more than
-// two waiters (tokens read from the child list); IN0/IN1 = token 0/1 lives in
-// the event's own 64-event batch at local index bits 8..13 / 16..21.
+// two waiters (all tokens listed in aux at record.w); IN0/IN1 = token 0/1
+// lives in the event's own 64-event batch at local index bits 8..13 / 16..21.
 enum : uint32_t { F_A = 1u, F_O = 2u, F_C = 4u, F_M = 8u, F_IN0 = 1u << 14, F_IN1 = 1u << 22 };
-// replay word (per lane, built at batch start): bits 0..3 flags, 8..15 / 16..23 token slots
-enum : uint32_t { X_IN0 = 1u << 4, X_IN1 = 1u << 5 };
 
-__device__ __forceinline__ uint32_t token_bits(uint32_t e, uint32_t t0, uint32_t t1) {
+__device__ __forceinline__ uint32_t token_bits(uint64_t e, uint32_t t0, uint32_t t1) {
     uint32_t b = ((t0 & 63u) << 8) | ((t1 & 63u) << 16);
     if ((t0 >> 6) == (e >> 6)) b |= F_IN0;
     if ((t1 >> 6) == (e >> 6)) b |= F_IN1;
@@ -53,243 +58,430 @@ __device__ __forceinline__ uint32_t token_bits(uint32_t e, uint32_t t0, uint32_t
 
 inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
 
-// is parent ref k of row i the first occurrence of that parent in the row's in-list refs?
+__device__ __forceinline__ unsigned long long ref_key(uint64_t row, uint32_t kidx) {
+    return ((unsigned long long)row << 16) | kidx;
+}
+
+// is parent ref k of a row (refs from pa) the first occurrence of that parent in the row's in-list refs?
 __device__ __forceinline__ bool first_in_row(const int32_t *__restrict__ prow, uint32_t pa, uint32_t k, int32_t p) {
     for (uint32_t q = pa; q < k; q++)
         if (prow[q] == p) return false;
     return true;
 }
 
-__global__ void k_lf_refs(uint64_t n, const uint32_t *__restrict__ canon, const uint32_t *__restrict__ poff,
-                          const int32_t *__restrict__ prow, unsigned long long *first_ref, uint32_t *fpc,
-                          uint32_t *viol) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    bool bad = canon[i] != (uint32_t)i;
-    const uint32_t pa = poff[i], pb = poff[i + 1];
+// is ref k (row gi, index kidx, target p) the first in-list reference to p?
+__device__ __forceinline__ bool is_first_ref(const LfRange &R, const unsigned long long *__restrict__ first_ref,
+                                             uint64_t gi, uint32_t k, uint32_t kidx, uint64_t p) {
+    if (p >= R.e) return R.isfb[k] != 0;
+    return first_ref[p - R.s] == ref_key(gi, kidx);
+}
+
+__global__ void k_lf_refs(LfRange R, unsigned long long *first_ref, uint32_t *fpc, uint32_t *viol) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R.nl) return;
+    const uint64_t gi = R.s + i;
+    bool bad = R.canon && R.canon[gi] != (uint32_t)gi;
+    const uint32_t pa = R.poff[gi], pb = R.poff[gi + 1];
     for (uint32_t k = pa; k < pb; k++) {
-        const int32_t p = prow[k];
+        const int32_t p = R.prow[k];
         if (p < 0) continue;
-        if ((uint64_t)p <= i) { bad = true; continue; }
+        if ((uint64_t)p <= gi) { bad = true; continue; }
         if (k - pa > 0xFFFFu) { bad = true; continue; }
-        if (!first_in_row(prow, pa, k, p)) continue;
-        atomicMin(&first_ref[p], ((unsigned long long)i << 16) | (k - pa));
-        if (k == pa) atomicAdd(&fpc[p], 1u);
+        if ((uint64_t)p >= R.e) continue;            // beyond the shard: crossing entry
+        if (!first_in_row(R.prow, pa, k, p)) continue;
+        atomicMin(&first_ref[p - R.s], ref_key(gi, k - pa));
+        if (k == pa) atomicAdd(&fpc[p - R.s], 1u);
     }
     if (bad) atomicOr(viol, 1u);
 }
 
-// per row: w, first-parent-in-list, event count
-__global__ void k_lf_rows(uint64_t n, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow,
-                          const unsigned long long *__restrict__ first_ref, const uint32_t *__restrict__ fpc,
-                          uint32_t *__restrict__ winfo, uint32_t *__restrict__ ev_cnt) {
-    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+// references from earlier shards into this one
+__global__ void k_lf_xin(LfRange R, unsigned long long *first_ref, uint32_t *fpc) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= R.xin_end) return;
+    const WgXEnt en = R.xall[x];
+    if (!(en.kf & WG_XF_FIRST_IN_ROW) || en.p < R.s || en.p >= R.e) return;
+    const uint32_t kidx = en.kf & 0xFFFFu;
+    atomicMin(&first_ref[en.p - R.s], ref_key(en.c, kidx));
+    if (kidx == 0) atomicAdd(&fpc[en.p - R.s], 1u);
+}
+
+// own references beyond the shard: first reference to their target?
+__global__ void k_lf_xfirst(LfRange R) {
+    const uint64_t x = R.xown_begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= R.xown_end) return;
+    const WgXEnt en = R.xall[x];
+    const uint32_t kidx = en.kf & 0xFFFFu;
+    const uint32_t k = R.poff[en.c] + kidx;
+    if (!(en.kf & WG_XF_FIRST_IN_ROW)) { R.isfb[k] = 0; return; }
+    const unsigned long long key = ref_key(en.c, kidx);
+    bool first = true;
+    for (uint64_t y = 0; y < R.xown_end && first; y++) {
+        const WgXEnt o = R.xall[y];
+        if (o.p == en.p && (o.kf & WG_XF_FIRST_IN_ROW) && ref_key(o.c, o.kf & 0xFFFFu) < key) first = false;
+    }
+    R.isfb[k] = first ? 1 : 0;
+}
+
+// per row: w, first-parent-in-list, event count, merge-token count
+__global__ void k_lf_rows(LfRange R, const unsigned long long *__restrict__ first_ref, const uint32_t *__restrict__ fpc,
+                          uint32_t *__restrict__ winfo, uint32_t *__restrict__ ev_cnt, uint32_t *__restrict__ aux_cnt) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= R.nl) return;
+    const uint64_t gj = R.s + j;
     const unsigned long long fr = first_ref[j];
     const uint32_t sec_first = (fr != REF_NONE && (fr & 0xFFFFu) != 0) ? 1u : 0u;
     const uint32_t w = fpc[j] + sec_first;
-    const uint32_t pa = poff[j], pb = poff[j + 1];
-    const bool fp_in = pb > pa && prow[pa] >= 0;
+    const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
+    const bool fp_in = pb > pa && R.prow[pa] >= 0;
     uint32_t nc = 0;
     for (uint32_t k = pa + 1; k < pb; k++) {
-        const int32_t p = prow[k];
-        if (p >= 0 && first_ref[p] == (((unsigned long long)j << 16) | (k - pa))) nc++;
+        const int32_t p = R.prow[k];
+        if (p >= 0 && is_first_ref(R, first_ref, gj, k, k - pa, (uint64_t)p)) nc++;
     }
     const uint32_t na = (w != 1) ? 1u : 0u;
     const uint32_t nb = (w == 1 && !fp_in) ? 1u : 0u;
     winfo[j] = (w < 0x3FFFFFFFu ? w : 0x3FFFFFFFu) | (fp_in ? 0x40000000u : 0u) | (sec_first ? 0x80000000u : 0u);
     ev_cnt[j] = na + nb + nc;
+    aux_cnt[j] = w > 2 ? w + 1 : 0u;
 }
 
-// SECALLOC event id of every parent whose first reference is secondary
-__global__ void k_lf_secev(uint64_t n, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow,
-                           const unsigned long long *__restrict__ first_ref, const uint32_t *__restrict__ winfo,
+// SECALLOC event of every first reference through a secondary parent
+__global__ void k_lf_secev(LfRange R, const unsigned long long *__restrict__ first_ref, const uint32_t *__restrict__ winfo,
                            const uint32_t *__restrict__ ev_off, uint32_t *__restrict__ secev) {
-    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= R.nl) return;
+    const uint64_t gj = R.s + j;
     const uint32_t wi = winfo[j], w = wi & 0x3FFFFFFFu;
     const bool fp_in = wi & 0x40000000u;
     uint32_t e = ev_off[j] + ((w != 1) ? 1u : 0u) + ((w == 1 && !fp_in) ? 1u : 0u);
-    const uint32_t pa = poff[j], pb = poff[j + 1];
+    const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
     for (uint32_t k = pa + 1; k < pb; k++) {
-        const int32_t p = prow[k];
-        if (p >= 0 && first_ref[p] == (((unsigned long long)j << 16) | (k - pa))) secev[p] = e++;
+        const int32_t p = R.prow[k];
+        if (p < 0 || !is_first_ref(R, first_ref, gj, k, k - pa, (uint64_t)p)) continue;
+        if ((uint64_t)p < R.e) secev[p - R.s] = WG_TOK_EV | e;
+        else R.xsec[k] = WG_TOK_EV | e;
+        e++;
     }
 }
 
-__global__ void k_lf_children(uint64_t n, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow,
-                              const uint32_t *__restrict__ ch_off, uint32_t *ch_fill, uint32_t *ch) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t pa = poff[i];
-    if (pa == poff[i + 1]) return;
-    const int32_t p = prow[pa];
-    if (p < 0) return;
-    ch[ch_off[p] + atomicAdd(&ch_fill[p], 1u)] = (uint32_t)i;
+// first references into this shard through a secondary parent of an earlier shard
+__global__ void k_lf_xin_secev(LfRange R, const unsigned long long *__restrict__ first_ref, uint32_t *__restrict__ secev) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= R.xin_end) return;
+    const WgXEnt en = R.xall[x];
+    const uint32_t kidx = en.kf & 0xFFFFu;
+    if (!(en.kf & WG_XF_FIRST_IN_ROW) || kidx == 0 || en.p < R.s || en.p >= R.e) return;
+    if (first_ref[en.p - R.s] == ref_key(en.c, kidx)) secev[en.p - R.s] = WG_TOK_X | (uint32_t)x;
 }
 
-__global__ void k_lf_sp_init(uint64_t n, const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
+__global__ void k_lf_children(LfRange R, const uint32_t *__restrict__ ch_off, uint32_t *ch_fill, uint32_t *ch) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R.nl) return;
+    const uint64_t gi = R.s + i;
+    const uint32_t pa = R.poff[gi];
+    if (pa == R.poff[gi + 1]) return;
+    const int32_t p = R.prow[pa];
+    if (p < 0 || (uint64_t)p >= R.e) return;
+    const uint64_t pl = (uint64_t)p - R.s;
+    ch[ch_off[pl] + atomicAdd(&ch_fill[pl], 1u)] = (uint32_t)i;
+}
+
+__global__ void k_lf_xin_children(LfRange R, const uint32_t *__restrict__ ch_off, uint32_t *ch_fill, uint32_t *ch) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= R.xin_end) return;
+    const WgXEnt en = R.xall[x];
+    if ((en.kf & 0xFFFFu) != 0 || en.p < R.s || en.p >= R.e) return;
+    const uint64_t pl = en.p - R.s;
+    ch[ch_off[pl] + atomicAdd(&ch_fill[pl], 1u)] = WG_TOK_X | (uint32_t)x;
+}
+
+__global__ void k_lf_sp_init(uint64_t nl, const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
                              const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
                              const uint32_t *__restrict__ secev, uint32_t *__restrict__ sp) {
-    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nl) return;
     const uint32_t wi = winfo[j], w = wi & 0x3FFFFFFFu;
-    if (w != 1) sp[j] = EVF | ev_off[j];                       // own ALLOC / MIN event
-    else if (wi & 0x80000000u) sp[j] = EVF | secev[j];          // waiter = secondary allocation
+    if (w != 1) sp[j] = WG_TOK_EV | ev_off[j];                  // own ALLOC / MIN event
+    else if (wi & 0x80000000u) sp[j] = secev[j];                // waiter = secondary allocation
     else sp[j] = ch[ch_off[j]];                                 // waiter = the only first-parent child
 }
 
-__global__ void k_lf_jump(uint64_t n, const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint32_t *changed) {
-    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+__global__ void k_lf_jump(uint64_t nl, const uint32_t *__restrict__ in, uint32_t *__restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nl) return;
     const uint32_t v = in[j];
-    uint32_t o = v;
-    if (!(v & EVF)) o = in[v];
-    out[j] = o;
-    if (!(o & EVF) && changed) *changed = 1u;
+    out[j] = (v & TAGS) ? v : in[v];
 }
 
-__global__ void k_lf_events(uint64_t n, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow,
+// token of every own crossing entry: the chain of its child row (first
+// parent) or its SECALLOC event (first reference through a secondary parent)
+__global__ void k_lf_export(LfRange R, const uint32_t *__restrict__ sp, uint32_t *__restrict__ tok) {
+    const uint64_t x = R.xown_begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= R.xown_end) return;
+    const WgXEnt en = R.xall[x];
+    const uint32_t kidx = en.kf & 0xFFFFu;
+    uint32_t t = WG_TOK_NONE;
+    if (kidx == 0) t = sp[en.c - R.s];
+    else if ((en.kf & WG_XF_FIRST_IN_ROW) && R.isfb[R.poff[en.c] + kidx]) t = R.xsec[R.poff[en.c] + kidx];
+    tok[x - R.xown_begin] = t;
+}
+
+__device__ __forceinline__ uint32_t globalize(uint32_t v, uint32_t ev_base, const uint32_t *__restrict__ xt) {
+    if (v & WG_TOK_EV) return WG_TOK_EV | ((v & ~WG_TOK_EV) + ev_base);
+    if (v & WG_TOK_X) return xt[v & ~WG_TOK_X];
+    return v;
+}
+
+__global__ void k_lf_globalize(uint64_t nl, uint32_t ev_base, const uint32_t *__restrict__ xt, uint32_t *sp,
+                               uint32_t *secev, const uint32_t *__restrict__ winfo) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nl) return;
+    sp[j] = globalize(sp[j], ev_base, xt);
+    if (winfo[j] & 0x80000000u) secev[j] = globalize(secev[j], ev_base, xt);
+}
+
+__global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, const uint32_t *__restrict__ xt,
                             const unsigned long long *__restrict__ first_ref, const uint32_t *__restrict__ winfo,
-                            const uint32_t *__restrict__ ev_off, const uint32_t *__restrict__ ch_off,
-                            const uint32_t *__restrict__ ch, const uint32_t *__restrict__ secev,
-                            const uint32_t *__restrict__ sp, uint4 *__restrict__ ev) {
-    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+                            const uint32_t *__restrict__ ev_off, const uint32_t *__restrict__ aux_off,
+                            const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
+                            const uint32_t *__restrict__ secev, const uint32_t *__restrict__ sp,
+                            uint4 *__restrict__ ev, uint32_t *__restrict__ aux) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= R.nl) return;
+    const uint64_t gj = R.s + j;
     const uint32_t wi = winfo[j], w = wi & 0x3FFFFFFFu;
     const bool fp_in = wi & 0x40000000u, sec_first = wi & 0x80000000u;
-    uint32_t e = ev_off[j];
+    uint32_t e = ev_off[j];                  // shard-local event index; global id = ev_base + e
     if (w == 0) {
-        ev[e] = make_uint4(fp_in ? (F_A | F_O) : F_A, 0u, 0u, (uint32_t)j);
+        ev[e] = make_uint4(fp_in ? (F_A | F_O) : F_A, 0u, 0u, (uint32_t)gj);
         e++;
     } else if (w >= 2) {
         // tokens: sources of the first-parent children, plus the secondary allocation
         uint32_t t[2] = {0u, 0u};
         uint32_t nt = 0;
-        for (uint32_t k = ch_off[j]; k < ch_off[j + 1] && nt < 2; k++) t[nt++] = sp[ch[k]] & ~EVF;
-        if (sec_first && nt < 2) t[nt++] = secev[j];
+        uint32_t *list = (w > 2) ? aux + aux_off[j] : nullptr;
+        if (list) list[0] = w;
+        for (uint32_t k = ch_off[j]; k < ch_off[j + 1]; k++) {
+            const uint32_t v = ch[k];
+            const uint32_t tk = ((v & WG_TOK_X) ? xt[v & ~WG_TOK_X] : sp[v]) & ~WG_TOK_EV;
+            if (nt < 2) t[nt] = tk;
+            if (list) list[1 + nt] = tk;
+            nt++;
+        }
+        if (sec_first) {
+            const uint32_t tk = secev[j] & ~WG_TOK_EV;
+            if (nt < 2) t[nt] = tk;
+            if (list) list[1 + nt] = tk;
+            nt++;
+        }
         const uint32_t f = F_C | (fp_in ? F_O : 0u) | ((w > 2) ? F_M : 0u);
-        ev[e] = make_uint4(f | token_bits(e, t[0], t[1]), t[0], t[1], (uint32_t)j);
+        ev[e] = make_uint4(f | token_bits(ev_base + e, t[0], t[1]), t[0], t[1], (w > 2) ? aux_base + aux_off[j] : (uint32_t)gj);
         e++;
     } else if (!fp_in) {
-        const uint32_t t0 = sp[j] & ~EVF;
-        ev[e] = make_uint4(F_C | token_bits(e, t0, t0), t0, t0, (uint32_t)j);
+        const uint32_t t0 = sp[j] & ~WG_TOK_EV;
+        ev[e] = make_uint4(F_C | token_bits(ev_base + e, t0, t0), t0, t0, (uint32_t)gj);
         e++;
     }
-    const uint32_t pa = poff[j], pb = poff[j + 1];
+    const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
     for (uint32_t k = pa + 1; k < pb; k++) {
-        const int32_t p = prow[k];
-        if (p >= 0 && first_ref[p] == (((unsigned long long)j << 16) | (k - pa))) {
-            ev[e] = make_uint4(F_A | F_O, 0u, 0u, (uint32_t)j);
+        const int32_t p = R.prow[k];
+        if (p >= 0 && is_first_ref(R, first_ref, gj, k, k - pa, (uint64_t)p)) {
+            ev[e] = make_uint4(F_A | F_O, 0u, 0u, (uint32_t)gj);
             e++;
         }
     }
 }
 
-__global__ void k_lf_lanes(uint64_t n, const uint32_t *__restrict__ sp, const uint8_t *__restrict__ slot_of,
+__global__ void k_lf_lanes(uint64_t nl, const uint32_t *__restrict__ sp, const uint8_t *__restrict__ slot_of,
                            uint32_t *__restrict__ lane) {
-    uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    lane[j] = slot_of[sp[j] & ~EVF];
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nl) return;
+    lane[j] = slot_of[sp[j] & ~WG_TOK_EV];
 }
 
 }  // namespace
 
-// Returns WG_OK with *used = false when the input needs the general walk.
-int wg_lanes_fast(wg_ctx *c, bool *used) {
-    *used = false;
-    const uint64_t n = c->n, e = c->e_refs;
+// workspace slots in c->lf
+enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_CH, LF_SPA, LF_SPB, LF_EVREC,
+       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX };
+
+static const uint32_t *lf_sp(wg_ctx *c) { return c->lf_sp_b ? c->lf[LF_SPB].as<const uint32_t>() : c->lf[LF_SPA].as<const uint32_t>(); }
+
+int wg_lf_refs(wg_ctx *c, const LfRange &R, uint32_t *viol, uint64_t *nev, uint64_t *naux) {
+    const uint64_t n = R.nl;
     hipStream_t s = c->stream;
-    DevBuf &first_ref = c->lf[0], &fpc = c->lf[1], &winfo = c->lf[2], &ev_off = c->lf[3], &secev = c->lf[4];
-    DevBuf &ch_off = c->lf[5], &ch_fill = c->lf[6], &ch = c->lf[7], &spA = c->lf[8], &spB = c->lf[9];
-    DevBuf &evrec = c->lf[10], &slot_of = c->lf[11], &flags = c->lf[12];
+    DevBuf &first_ref = c->lf[LF_FIRST], &fpc = c->lf[LF_FPC], &winfo = c->lf[LF_WINFO], &ev_off = c->lf[LF_EVOFF];
+    DevBuf &flags = c->lf[LF_FLAGS], &aux_off = c->lf[LF_AUXOFF];
     WG_ALLOC(c, first_ref, n * 8 + 8);
     WG_ALLOC(c, fpc, (n + 2) * 4);
     WG_ALLOC(c, winfo, n * 4 + 4);
     WG_ALLOC(c, ev_off, (n + 2) * 4);
-    WG_ALLOC(c, secev, n * 4 + 4);
-    WG_ALLOC(c, ch_off, (n + 2) * 4);
-    WG_ALLOC(c, ch_fill, (n + 2) * 4);
-    WG_ALLOC(c, ch, e * 4 + 4);
-    WG_ALLOC(c, spA, n * 4 + 4);
-    WG_ALLOC(c, spB, n * 4 + 4);
+    WG_ALLOC(c, aux_off, (n + 2) * 4);
     WG_ALLOC(c, flags, 64);
     WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(n + 2));
-    const uint32_t *poff = c->d_poff;
-    const int32_t *prow = c->prow.as<const int32_t>();
-
     wg_stage_begin(c, "lf_refs");
     WG_HIP(c, hipMemsetAsync(first_ref.p, 0xFF, n * 8, s));
     WG_HIP(c, hipMemsetAsync(fpc.p, 0, (n + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(ch_fill.p, 0, (n + 2) * 4, s));
     WG_HIP(c, hipMemsetAsync(flags.p, 0, 64, s));
-    hipLaunchKernelGGL(k_lf_refs, dim3(blocks(n)), dim3(T), 0, s, n, c->canon.as<const uint32_t>(), poff, prow,
-                       first_ref.as<unsigned long long>(), fpc.as<uint32_t>(), flags.as<uint32_t>());
-    hipLaunchKernelGGL(k_lf_rows, dim3(blocks(n)), dim3(T), 0, s, n, poff, prow, first_ref.as<const unsigned long long>(),
-                       fpc.as<const uint32_t>(), winfo.as<uint32_t>(), ev_off.as<uint32_t>());
+    if (n) hipLaunchKernelGGL(k_lf_refs, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<unsigned long long>(),
+                              fpc.as<uint32_t>(), flags.as<uint32_t>());
+    if (R.xin_end)
+        hipLaunchKernelGGL(k_lf_xin, dim3(blocks(R.xin_end)), dim3(T), 0, s, R, first_ref.as<unsigned long long>(),
+                           fpc.as<uint32_t>());
+    if (R.xown_end > R.xown_begin)
+        hipLaunchKernelGGL(k_lf_xfirst, dim3(blocks(R.xown_end - R.xown_begin)), dim3(T), 0, s, R);
+    if (n) hipLaunchKernelGGL(k_lf_rows, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<const unsigned long long>(),
+                              fpc.as<const uint32_t>(), winfo.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(ev_off.as<uint32_t>(), ev_off.as<uint32_t>(), n, c->scan_tmp.p, s));
-    uint32_t hdr[2] = {0, 0};
+    WG_HIP(c, wg_exclusive_scan_u32(aux_off.as<uint32_t>(), aux_off.as<uint32_t>(), n, c->scan_tmp.p, s));
+    uint32_t hdr[3] = {0, 0, 0};
     WG_HIP(c, hipMemcpyAsync(&hdr[0], flags.p, 4, hipMemcpyDeviceToHost, s));
     WG_HIP(c, hipMemcpyAsync(&hdr[1], ev_off.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
+    WG_HIP(c, hipMemcpyAsync(&hdr[2], aux_off.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
     WG_HIP(c, hipStreamSynchronize(s));
     wg_stage_end(c);
-    if (hdr[0]) return WG_OK;                       // not well formed: general walk
-    const uint64_t nev = hdr[1];
-    c->n_events = nev;
-    WG_ALLOC(c, evrec, (nev + 256) * 16);
-    WG_HIP(c, hipMemsetAsync(evrec.as<uint4>() + nev, 0, 256 * 16, s));   // no-op padding for the replay prefetch
-    WG_ALLOC(c, slot_of, nev + 64);
+    *viol = hdr[0];
+    *nev = hdr[1];
+    *naux = hdr[2];
+    return WG_OK;
+}
+
+int wg_lf_chain(wg_ctx *c, const LfRange &R) {
+    const uint64_t n = R.nl;
+    hipStream_t s = c->stream;
+    DevBuf &first_ref = c->lf[LF_FIRST], &fpc = c->lf[LF_FPC], &winfo = c->lf[LF_WINFO], &ev_off = c->lf[LF_EVOFF];
+    DevBuf &secev = c->lf[LF_SECEV], &ch_off = c->lf[LF_CHOFF], &ch_fill = c->lf[LF_CHFILL], &ch = c->lf[LF_CH];
+    DevBuf &spA = c->lf[LF_SPA], &spB = c->lf[LF_SPB];
+    // children: own rows' first parents in range + earlier shards' first parents
+    const uint64_t nref = c->e_refs_own + R.xin_end;
+    WG_ALLOC(c, secev, n * 4 + 4);
+    WG_ALLOC(c, ch_off, (n + 2) * 4);
+    WG_ALLOC(c, ch_fill, (n + 2) * 4);
+    WG_ALLOC(c, ch, nref * 4 + 4);
+    WG_ALLOC(c, spA, n * 4 + 4);
+    WG_ALLOC(c, spB, n * 4 + 4);
     wg_stage_begin(c, "lf_chain");
-    hipLaunchKernelGGL(k_lf_secev, dim3(blocks(n)), dim3(T), 0, s, n, poff, prow, first_ref.as<const unsigned long long>(),
-                       winfo.as<const uint32_t>(), ev_off.as<const uint32_t>(), secev.as<uint32_t>());
-    // first-parent children CSR
+    WG_HIP(c, hipMemsetAsync(ch_fill.p, 0, (n + 2) * 4, s));
+    if (n) hipLaunchKernelGGL(k_lf_secev, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<const unsigned long long>(),
+                              winfo.as<const uint32_t>(), ev_off.as<const uint32_t>(), secev.as<uint32_t>());
+    if (R.xin_end)
+        hipLaunchKernelGGL(k_lf_xin_secev, dim3(blocks(R.xin_end)), dim3(T), 0, s, R,
+                           first_ref.as<const unsigned long long>(), secev.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(fpc.as<uint32_t>(), ch_off.as<uint32_t>(), n, c->scan_tmp.p, s));
-    hipLaunchKernelGGL(k_lf_children, dim3(blocks(n)), dim3(T), 0, s, n, poff, prow, ch_off.as<const uint32_t>(),
-                       ch_fill.as<uint32_t>(), ch.as<uint32_t>());
-    hipLaunchKernelGGL(k_lf_sp_init, dim3(blocks(n)), dim3(T), 0, s, n, winfo.as<const uint32_t>(),
-                       ev_off.as<const uint32_t>(), ch_off.as<const uint32_t>(), ch.as<const uint32_t>(),
-                       secev.as<const uint32_t>(), spA.as<uint32_t>());
+    if (n) hipLaunchKernelGGL(k_lf_children, dim3(blocks(n)), dim3(T), 0, s, R, ch_off.as<const uint32_t>(),
+                              ch_fill.as<uint32_t>(), ch.as<uint32_t>());
+    if (R.xin_end)
+        hipLaunchKernelGGL(k_lf_xin_children, dim3(blocks(R.xin_end)), dim3(T), 0, s, R, ch_off.as<const uint32_t>(),
+                           ch_fill.as<uint32_t>(), ch.as<uint32_t>());
+    if (n) hipLaunchKernelGGL(k_lf_sp_init, dim3(blocks(n)), dim3(T), 0, s, n, winfo.as<const uint32_t>(),
+                              ev_off.as<const uint32_t>(), ch_off.as<const uint32_t>(), ch.as<const uint32_t>(),
+                              secev.as<const uint32_t>(), spA.as<uint32_t>());
     // pointer jumping: after r rounds every pointer skips 2^r chain links
-    int rounds = 1;
+    int rounds = 0;
     while ((1ull << rounds) < n + 1) rounds++;
     DevBuf *in = &spA, *out = &spB;
     for (int r = 0; r < rounds; r++) {
-        hipLaunchKernelGGL(k_lf_jump, dim3(blocks(n)), dim3(T), 0, s, n, in->as<const uint32_t>(), out->as<uint32_t>(),
-                           (uint32_t *)nullptr);
+        hipLaunchKernelGGL(k_lf_jump, dim3(blocks(n)), dim3(T), 0, s, n, in->as<const uint32_t>(), out->as<uint32_t>());
         DevBuf *t = in; in = out; out = t;
     }
-    const uint32_t *sp = in->as<const uint32_t>();
+    c->lf_sp_b = (in == &spB);
+    WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
+    return WG_OK;
+}
+
+int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok) {
+    const uint64_t nx = R.xown_end - R.xown_begin;
+    if (nx) hipLaunchKernelGGL(k_lf_export, dim3(blocks(nx)), dim3(T), 0, c->stream, R, lf_sp(c), tok);
+    WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint4 *ev_out, uint32_t *aux_out,
+                 uint32_t aux_base) {
+    const uint64_t n = R.nl;
+    if (!n) return WG_OK;
+    hipStream_t s = c->stream;
+    uint32_t *sp = const_cast<uint32_t *>(lf_sp(c));
     wg_stage_begin(c, "lf_events");
-    hipLaunchKernelGGL(k_lf_events, dim3(blocks(n)), dim3(T), 0, s, n, poff, prow, first_ref.as<const unsigned long long>(),
-                       winfo.as<const uint32_t>(), ev_off.as<const uint32_t>(), ch_off.as<const uint32_t>(),
-                       ch.as<const uint32_t>(), secev.as<const uint32_t>(), sp, evrec.as<uint4>());
+    if (ev_base || xt)
+        hipLaunchKernelGGL(k_lf_globalize, dim3(blocks(n)), dim3(T), 0, s, n, ev_base, xt, sp, c->lf[LF_SECEV].as<uint32_t>(),
+                           c->lf[LF_WINFO].as<const uint32_t>());
+    hipLaunchKernelGGL(k_lf_events, dim3(blocks(n)), dim3(T), 0, s, R, ev_base, aux_base, xt,
+                       c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
+                       c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
+                       c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
+                       c->lf[LF_SECEV].as<const uint32_t>(), (const uint32_t *)sp, ev_out, aux_out);
+    WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
+    return WG_OK;
+}
+
+// Replays nev global events (records padded with 256 zero records) and
+// leaves the slot of every event in *slots; scalars in c->lane_scalars.
+int wg_lf_replay(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, const uint8_t **slots, bool *converged) {
+    hipStream_t s = c->stream;
     wg_stage_begin(c, "lf_loop");
     const uint32_t chunk = c->replay_chunk;
     const uint64_t nch = (nev + chunk - 1) / chunk + 1;
     const uint32_t max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
-    DevBuf &slot_b = c->lf[13], &occ = c->lf[14], &stats = c->lf[15], &rflags = c->lf[16];
+    DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
+    DevBuf &rflags = c->lf[LF_RFLAGS];
+    WG_ALLOC(c, slot_a, nev + 64);
     WG_ALLOC(c, slot_b, nev + 64);
     WG_ALLOC(c, occ, nch * 16 + 16);
     WG_ALLOC(c, stats, nch * 8 + 8);
     WG_ALLOC(c, rflags, (max_iters + 2) * 4);
-    uint8_t *slots = nullptr;
+    uint8_t *out = nullptr;
     uint32_t iters = 0;
-    WG_HIP(c, wg_lane_replay(s, nev, chunk, evrec.as<const uint4>(), ch_off.as<const uint32_t>(), ch.as<const uint32_t>(),
-                             sp, secev.as<const uint32_t>(), winfo.as<const uint32_t>(), slot_of.as<uint8_t>(),
-                             slot_b.as<uint8_t>(), occ.as<unsigned long long>(), occ.as<unsigned long long>() + nch,
-                             stats.as<uint32_t>(), rflags.as<uint32_t>(), max_iters, c->lane_scalars.as<uint32_t>(),
-                             &slots, &iters));
+    WG_HIP(c, wg_lane_replay(s, nev, chunk, ev, aux, slot_a.as<uint8_t>(), slot_b.as<uint8_t>(),
+                             occ.as<unsigned long long>(), occ.as<unsigned long long>() + nch, stats.as<uint32_t>(),
+                             rflags.as<uint32_t>(), max_iters, c->lane_scalars.as<uint32_t>(), &out, &iters));
     c->replay_iters = iters;
     wg_stage_end(c);
-    if (iters > max_iters) return WG_OK;            // no fixed point within budget: general walk
-    hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(n)), dim3(T), 0, s, n, sp, (const uint8_t *)slots,
-                       c->lane_asg.as<uint32_t>());
+    *slots = out;
+    *converged = iters <= max_iters;
+    return WG_OK;
+}
+
+int wg_lf_lanes(wg_ctx *c, const LfRange &R, const uint8_t *slots, uint32_t *lane) {
+    if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, c->stream, R.nl, lf_sp(c), slots, lane);
     WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+// Single-GPU build.  Returns WG_OK with *used = false when the input needs the general walk.
+int wg_lanes_fast(wg_ctx *c, bool *used) {
+    *used = false;
+    LfRange R;
+    R.s = 0;
+    R.nl = c->n;
+    R.e = c->n;
+    R.poff = c->d_poff;
+    R.prow = c->prow.as<const int32_t>();
+    R.canon = c->canon.as<const uint32_t>();
+    c->e_refs_own = c->e_refs;
+    uint32_t viol = 0;
+    uint64_t nev = 0, naux = 0;
+    int rc = wg_lf_refs(c, R, &viol, &nev, &naux);
+    if (rc != WG_OK) return rc;
+    if (viol) return WG_OK;                          // not well formed: general walk
+    c->n_events = nev;
+    if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
+    DevBuf &evrec = c->lf[LF_EVREC], &aux = c->lf[LF_AUX];
+    WG_ALLOC(c, evrec, (nev + 256) * 16);
+    WG_ALLOC(c, aux, naux * 4 + 4);
+    WG_HIP(c, hipMemsetAsync(evrec.as<uint4>() + nev, 0, 256 * 16, c->stream));   // no-op padding for the replay prefetch
+    if ((rc = wg_lf_events(c, R, 0, nullptr, evrec.as<uint4>(), aux.as<uint32_t>(), 0)) != WG_OK) return rc;
+    const uint8_t *slots = nullptr;
+    bool conv = false;
+    if ((rc = wg_lf_replay(c, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(), &slots, &conv)) != WG_OK) return rc;
+    if (!conv) return WG_OK;                         // no fixed point within budget: general walk
+    if ((rc = wg_lf_lanes(c, R, slots, c->lane_asg.as<uint32_t>())) != WG_OK) return rc;
     uint32_t sc[4];
-    WG_HIP(c, hipMemcpyAsync(sc, c->lane_scalars.p, 16, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipStreamSynchronize(s));
+    WG_HIP(c, hipMemcpyAsync(sc, c->lane_scalars.p, 16, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
     if (sc[2]) return WG_OK;                        // more than 63 slots: general walk
     c->max_lane = sc[0];
     c->n_slots = sc[1];

@@ -33,7 +33,6 @@
 namespace {
 
 enum : uint32_t { F_A = 1u, F_O = 2u, F_C = 4u, F_M = 8u, F_IN0 = 1u << 14, F_IN1 = 1u << 22 };
-constexpr uint32_t EVF = 0x80000000u;
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
@@ -52,7 +51,7 @@ struct ReplayArgs {
     uint32_t chunk;             // events per chunk (multiple of 64)
     uint32_t iter;              // iteration index (>= 1)
     const uint4 *ev;            // records, padded with >= 256 zero records
-    const uint32_t *ch_off, *ch, *sp, *secev, *winfo;
+    const uint32_t *aux;        // token lists of merges with more than two waiters
     const uint8_t *slot_prev;   // iteration i-1
     uint8_t *slot_next;         // iteration i
     const unsigned long long *occ_prev;  // exit occupancy per chunk, iteration i-1
@@ -137,13 +136,10 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
                 uint64_t clr = (1ull << (a & 63u)) | (1ull << (b & 63u));
                 uint32_t m = a < b ? a : b;
                 if (f & F_M) {
-                    const uint32_t j = rl(row_v, k);
-                    const uint32_t lo = A.ch_off[j], hi = A.ch_off[j + 1];
-                    for (uint32_t x = lo; x <= hi; x++) {
-                        uint32_t t;
-                        if (x < hi) t = A.sp[A.ch[x]] & ~EVF;
-                        else if (A.winfo[j] & 0x80000000u) t = A.secev[j];
-                        else break;
+                    const uint32_t off = rl(row_v, k);      // record.w = aux offset: {count, tokens...}
+                    const uint32_t cnt = A.aux[off];
+                    for (uint32_t x = 0; x < cnt; x++) {
+                        const uint32_t t = A.aux[off + 1 + x];
                         uint32_t ts;
                         if (t >= base) ts = rl(cur_v, (uint32_t)(t - base));
                         else if (have_prev && t >= pbase) ts = rl(prev_v, (uint32_t)(t - pbase));
@@ -213,8 +209,7 @@ __global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict_
 // workspaces: slots (2 x (nev + 64) bytes), occ (2 x nchunks x 8 bytes),
 // stats (2 x nchunks x 4 bytes), flags (max_iters + 1 words).
 // Returns the number of iterations used (0 on a HIP error) in *iters.
-hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *ch_off,
-                          const uint32_t *ch, const uint32_t *sp, const uint32_t *secev, const uint32_t *winfo,
+hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *aux,
                           uint8_t *slots_a, uint8_t *slots_b, unsigned long long *occ_a, unsigned long long *occ_b,
                           uint32_t *stats, uint32_t *flags, uint32_t max_iters, uint32_t *scal, uint8_t **slot_out,
                           uint32_t *iters) {
@@ -235,7 +230,7 @@ hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uin
     // chunk c is exact after c + 1 iterations, so nch + 1 iterations always converge
     if (max_iters > nch + 1) max_iters = (uint32_t)(nch + 1);
     for (uint32_t it = 1; it <= max_iters; it++) {
-        ReplayArgs a{nev, chunk, it, ev, ch_off, ch, sp, secev, winfo, sp_prev, sp_next, op, on, stats, flags};
+        ReplayArgs a{nev, chunk, it, ev, aux, sp_prev, sp_next, op, on, stats, flags};
         hipLaunchKernelGGL(k_lf_replay, dim3(nch), dim3(64), 0, s, a);
         // after a fixed point later iterations do nothing; the converged slots are
         // in both buffers, so either pointer is final
