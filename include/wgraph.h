@@ -102,6 +102,7 @@ typedef struct wg_layout_summary {
     uint32_t n_slots;         /* length reached by active_lanes (diagnostic)  */
     float    graph_width;     /* GraphLayout::graph_width                     */
     uint32_t lane_path;       /* 0 = event-compressed fast path, 1 = general  */
+    uint64_t row_begin;       /* first row of the rows reported (shard start)  */
 } wg_layout_summary;
 
 /* ---- row geometry layout (RowGeometry, commit_graph.rs:208-233) --------
@@ -225,6 +226,43 @@ int wg_copy_vertex_offsets(wg_ctx *ctx, uint64_t *dst);
 
 int wg_device_views_get(wg_ctx *ctx, wg_device_views *out);
 
+/* ---- row-sharded multi-GPU build --------------------------
+ * One process per GPU.  Every rank holds the WHOLE commit list in device
+ * memory; rank `rank` of `world` owns rows [row_begin, row_end) (contiguous
+ * shards in rank order covering the list).  The build runs to a few
+ * exchange points; at each one the engine exposes this rank's message
+ * (wg_shard_msg.bytes long, copied out with wg_shard_copy_msg to device or
+ * host memory), the caller all-gathers the messages of every rank — e.g.
+ * torch.distributed all_gather over RCCL, each message padded to the
+ * largest — and hands the gathered buffer (device memory, rank r's message
+ * at r * stride, sizes[r] its length) to wg_shard_exchange, until done = 1.
+ * Every rank must make the same sequence of calls.
+ *
+ * After a sharded build the per-row queries (wg_copy_lanes, _edges,
+ * _row_heights, wg_copy_geometry, wg_emit_vertices) cover the own rows
+ * only: lanes/heights/geometry have row_end-row_begin entries, edges are
+ * those whose child is an own row (global row numbers), vertex emission
+ * takes global rows inside the shard.  Results equal the single-GPU build of
+ * the whole list restricted to the shard.  Lists the sharded path does not
+ * take (duplicate ids, parents at earlier rows, > 63 lane slots) are built
+ * whole on every rank instead, with the same results.                     */
+typedef struct wg_shard_msg {
+    const void *send;         /* engine-owned device buffer (diagnostic)      */
+    uint64_t    bytes;        /* length of this rank's message                */
+    int32_t     done;         /* 1: the call is complete, nothing to exchange */
+    int32_t     step;         /* exchange index                               */
+} wg_shard_msg;
+/* GraphLayout::build (:265-355) of a row shard (+ zero-band geometry). */
+int wg_shard_build_begin(wg_ctx *ctx, const wg_commits *commits, int world, int rank,
+                         uint64_t row_begin, uint64_t row_end, wg_shard_msg *out);
+/* row_geometry_with_bands (:367-399) of the shard; band = the whole [N] array. */
+int wg_shard_geometry_begin(wg_ctx *ctx, const float *band, int32_t band_residency, wg_shard_msg *out);
+/* Copy this rank's current message (device or host destination). */
+int wg_shard_copy_msg(wg_ctx *ctx, void *dst);
+/* Deliver the all-gathered messages; runs to the next exchange or the end. */
+int wg_shard_exchange(wg_ctx *ctx, const void *gathered, uint64_t stride, const uint64_t *sizes,
+                      wg_shard_msg *out);
+
 /* ---- timing (HIP events on the context's stream) ------------------------ */
 #define WG_STAGE_MAX 1024
 /* on = 0 disables; on > 0 enables and restarts the stage log (on > 1 also
@@ -238,7 +276,8 @@ int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
 /* ---- diagnostics ------------------------------------------------------------
  * Copies up to n (<= 16) 32-bit engine counters of the last layout build:
  * [0] max_lane, [1] slots, [2] lane-table overflow, [3] fixed-point
- * iterations of the lane-event replay, [4] lane events.                   */
+ * iterations of the lane-event replay, [4] lane events, [5] build mode
+ * (0 single, 1 row-sharded, 2 row-sharded request built whole).           */
 int wg_debug_counters(wg_ctx *ctx, uint32_t *out, int n);
 
 #ifdef __cplusplus

@@ -1,0 +1,64 @@
+"""Host plumbing of the row-sharded build: the variable-length all-gather
+(wgraph.shard.ShardComm) over a world-size-2 gloo group on the CPU, and the
+shard partition.  The engine side runs in tests/test_gpu_shard.py."""
+import ctypes
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from wgraph.shard import ShardComm, shard_rows
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = ShardComm(torch.device("cpu"))
+        got = []
+        for step, length in enumerate([0, 5, 37 + 11 * rank, 4096 * (rank + 1)]):
+            payload = bytes((rank * 31 + step + i) & 0xFF for i in range(length))
+            out, stride, sizes = comm.allgather(length, lambda ptr: ctypes.memmove(ptr, payload, length))
+            got.append((stride, sizes, [bytes(out[r * stride:r * stride + sizes[r]].numpy()) for r in range(world)]))
+        q.put((rank, got, comm.exchanges))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allgather_world2_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, n)) for r, g, n in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for step, length_of in enumerate([lambda r: 0, lambda r: 5, lambda r: 37 + 11 * r, lambda r: 4096 * (r + 1)]):
+        for rank in range(world):
+            stride, sizes, msgs = res[rank][0][step]
+            assert sizes == [length_of(r) for r in range(world)]
+            assert stride % 16 == 0 and stride >= max(max(sizes), 16)
+            for r in range(world):
+                assert msgs[r] == bytes((r * 31 + step + i) & 0xFF for i in range(length_of(r)))
+        assert res[0][1] == 4
+
+
+@pytest.mark.parametrize("n,world", [(0, 2), (1, 2), (7, 3), (1_000_000, 8), (8_000_000, 8)])
+def test_shard_rows_partition(n, world):
+    bounds = [shard_rows(n, world, r) for r in range(world)]
+    assert bounds[0][0] == 0 and bounds[-1][1] == n
+    for (a, b), (c, d) in zip(bounds, bounds[1:]):
+        assert b == c and a <= b
+    assert max(b - a for a, b in bounds) - min(b - a for a, b in bounds) <= 1

@@ -72,6 +72,11 @@ void wg_destroy(wg_ctx *c) {
                       &c->scan_tmp, &c->scal, &c->rowflags, &c->carry_fill, &c->sweep_err, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
     for (DevBuf *b : bufs) b->release();
     for (DevBuf &b : c->lf) b.release();
+    ShardState &S = c->sh;
+    DevBuf *sb[] = {&S.msg, &S.ptable, &S.prow, &S.unres, &S.flags, &S.xcnt, &S.refx, &S.isfb, &S.xsec, &S.xall,
+                    &S.xtok, &S.xt, &S.dev_small, &S.h_g, &S.rt_g, &S.band_host, &S.xchild, &S.xpar, &S.in_scan,
+                    &S.edge_y, &S.own_edges};
+    for (DevBuf *b : sb) b->release();
     c->tile_first.release();
     for (int i = 0; i < WG_STAGE_MAX; i++) {
         if (c->stages[i].a) (void)hipEventDestroy(c->stages[i].a);
@@ -123,6 +128,9 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     if (!c || !in) return WG_E_INVALID;
     (void)hipSetDevice(c->device);
     c->have_layout = c->have_geom = c->have_vtx = false;
+    c->sh.on = false;
+    c->sh.step = 0;
+    c->edge_y = nullptr;
     const uint64_t n = in->n_commits;
     if (n >= 0xFFFFFFF0ull) return wg_fail(c, WG_E_UNSUPPORTED, "n_commits %llu exceeds 2^32-16", (unsigned long long)n);
     if (n > 0 && (!in->oid || !in->time || !in->parent_off)) return wg_fail(c, WG_E_INVALID, "null input array");
@@ -136,6 +144,10 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     }
     c->n = n;
     c->e_refs = e;
+    c->sh.N = n;
+    c->sh.s = 0;
+    c->sh.e = n;
+    c->sh.row_base = 0;
     if (in->residency == WG_HOST) {
         wg_stage_begin(c, "h2d");
         WG_ALLOC(c, c->in_oid, n * 20 + 4);
@@ -187,8 +199,18 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
 int wg_layout_summary_get(wg_ctx *c, wg_layout_summary *out) {
     if (!c || !out) return WG_E_INVALID;
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
-    out->n_rows = c->n;
+    const ShardState &S = c->sh;
+    out->n_rows = S.e - S.s;
+    out->row_begin = S.s;
     out->n_edges = c->n_edges;
+    if (S.on && !S.replicated) out->n_edges = S.n_own_edges;
+    else if (S.on) {
+        uint32_t eo[2] = {0, 0};
+        WG_HIP(c, hipMemcpyAsync(&eo[0], c->edge_cnt.as<uint32_t>() + S.s, 4, hipMemcpyDeviceToHost, c->stream));
+        WG_HIP(c, hipMemcpyAsync(&eo[1], c->edge_cnt.as<uint32_t>() + S.e, 4, hipMemcpyDeviceToHost, c->stream));
+        WG_HIP(c, hipStreamSynchronize(c->stream));
+        out->n_edges = eo[1] - eo[0];
+    }
     out->max_lane = c->max_lane;
     out->n_slots = c->n_slots;
     out->graph_width = c->graph_width;
@@ -199,8 +221,11 @@ int wg_layout_summary_get(wg_ctx *c, wg_layout_summary *out) {
 int wg_copy_lanes(wg_ctx *c, uint32_t *lane, uint8_t *color) {
     if (!c) return WG_E_INVALID;
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
-    if (lane && c->n) WG_HIP(c, hipMemcpyAsync(lane, c->lane_out.p, c->n * 4, hipMemcpyDeviceToHost, c->stream));
-    if (color && c->n) WG_HIP(c, hipMemcpyAsync(color, c->color_out.p, c->n, hipMemcpyDeviceToHost, c->stream));
+    const uint64_t rows = c->sh.e - c->sh.s, b = c->sh.row_base;
+    if (lane && rows)
+        WG_HIP(c, hipMemcpyAsync(lane, c->lane_out.as<uint32_t>() + b, rows * 4, hipMemcpyDeviceToHost, c->stream));
+    if (color && rows)
+        WG_HIP(c, hipMemcpyAsync(color, c->color_out.as<uint8_t>() + b, rows, hipMemcpyDeviceToHost, c->stream));
     WG_HIP(c, hipStreamSynchronize(c->stream));
     return WG_OK;
 }
@@ -208,8 +233,21 @@ int wg_copy_lanes(wg_ctx *c, uint32_t *lane, uint8_t *color) {
 int wg_copy_edges(wg_ctx *c, wg_edge *edges) {
     if (!c || !edges) return WG_E_INVALID;
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
-    if (c->n_edges)
+    const ShardState &S = c->sh;
+    if (S.on && !S.replicated) {
+        if (S.n_own_edges)
+            WG_HIP(c, hipMemcpyAsync(edges, S.own_edges.p, S.n_own_edges * sizeof(wg_edge), hipMemcpyDeviceToHost, c->stream));
+    } else if (S.on) {
+        uint32_t eo[2] = {0, 0};
+        WG_HIP(c, hipMemcpyAsync(&eo[0], c->edge_cnt.as<uint32_t>() + S.s, 4, hipMemcpyDeviceToHost, c->stream));
+        WG_HIP(c, hipMemcpyAsync(&eo[1], c->edge_cnt.as<uint32_t>() + S.e, 4, hipMemcpyDeviceToHost, c->stream));
+        WG_HIP(c, hipStreamSynchronize(c->stream));
+        if (eo[1] > eo[0])
+            WG_HIP(c, hipMemcpyAsync(edges, c->edges.as<wg_edge>() + eo[0], (eo[1] - eo[0]) * sizeof(wg_edge),
+                                     hipMemcpyDeviceToHost, c->stream));
+    } else if (c->n_edges) {
         WG_HIP(c, hipMemcpyAsync(edges, c->edges.p, c->n_edges * sizeof(wg_edge), hipMemcpyDeviceToHost, c->stream));
+    }
     WG_HIP(c, hipStreamSynchronize(c->stream));
     return WG_OK;
 }
@@ -217,7 +255,8 @@ int wg_copy_edges(wg_ctx *c, wg_edge *edges) {
 int wg_copy_row_heights(wg_ctx *c, float *h) {
     if (!c || !h) return WG_E_INVALID;
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
-    if (c->n) WG_HIP(c, hipMemcpyAsync(h, c->heights.p, c->n * 4, hipMemcpyDeviceToHost, c->stream));
+    const uint64_t rows = c->sh.e - c->sh.s;
+    if (rows) WG_HIP(c, hipMemcpyAsync(h, c->heights.as<float>() + c->sh.row_base, rows * 4, hipMemcpyDeviceToHost, c->stream));
     WG_HIP(c, hipStreamSynchronize(c->stream));
     return WG_OK;
 }
@@ -228,6 +267,7 @@ int wg_copy_row_heights(wg_ctx *c, float *h) {
 int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
     if (!c) return WG_E_INVALID;
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
+    if (c->sh.on && !c->sh.replicated) return wg_fail(c, WG_E_STATE, "sharded layout: use wg_shard_geometry_begin");
     (void)hipSetDevice(c->device);
     c->have_geom = c->have_vtx = false;
     const float *d_band = nullptr;
@@ -249,33 +289,69 @@ int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
     return WG_OK;
 }
 
+// the own rows' slice of the row arrays: [b, b + rows), CSR ranges from vert_off/curve_off[b]
+static int own_geometry_range(wg_ctx *c, uint64_t *v0, uint64_t *v1, uint64_t *c0, uint64_t *c1) {
+    const uint64_t b = c->sh.row_base, rows = c->sh.e - c->sh.s;
+    uint32_t o[4] = {0, 0, 0, 0};
+    WG_HIP(c, hipMemcpyAsync(&o[0], c->vert_off.as<uint32_t>() + b, 4, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipMemcpyAsync(&o[1], c->vert_off.as<uint32_t>() + b + rows, 4, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipMemcpyAsync(&o[2], c->curve_off.as<uint32_t>() + b, 4, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipMemcpyAsync(&o[3], c->curve_off.as<uint32_t>() + b + rows, 4, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    *v0 = o[0]; *v1 = o[1]; *c0 = o[2]; *c1 = o[3];
+    return WG_OK;
+}
+
 int wg_geometry_summary_get(wg_ctx *c, wg_geometry_summary *out) {
     if (!c || !out) return WG_E_INVALID;
     if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
-    out->n_rows = c->n;
+    out->n_rows = c->sh.e - c->sh.s;
     out->n_vert = c->n_vert;
     out->n_curve = c->n_curve;
     out->total_height = c->total_height;
     out->scan_path = c->scan_path;
+    if (c->sh.on) {
+        uint64_t v0, v1, c0, c1;
+        int rc = own_geometry_range(c, &v0, &v1, &c0, &c1);
+        if (rc != WG_OK) return rc;
+        out->n_vert = v1 - v0;
+        out->n_curve = c1 - c0;
+        float t = 0.0f;   // row_top at the end of the shard
+        WG_HIP(c, hipMemcpyAsync(&t, c->g_row_top.as<float>() + c->sh.row_base + (c->sh.e - c->sh.s), 4,
+                                 hipMemcpyDeviceToHost, c->stream));
+        WG_HIP(c, hipStreamSynchronize(c->stream));
+        out->total_height = t;
+    }
     return WG_OK;
 }
 
 int wg_copy_geometry(wg_ctx *c, const wg_geometry_host *d) {
     if (!c || !d) return WG_E_INVALID;
     if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
-    const uint64_t n = c->n;
+    const uint64_t n = c->sh.e - c->sh.s, b = c->sh.row_base;
+    uint64_t v0 = 0, v1 = c->n_vert, c0 = 0, c1 = c->n_curve;
+    if (c->sh.on) {
+        int rc = own_geometry_range(c, &v0, &v1, &c0, &c1);
+        if (rc != WG_OK) return rc;
+    }
     hipStream_t s = c->stream;
-    if (d->height && n) WG_HIP(c, hipMemcpyAsync(d->height, c->g_height.p, n * 4, hipMemcpyDeviceToHost, s));
-    if (d->node_y && n) WG_HIP(c, hipMemcpyAsync(d->node_y, c->g_node_y.p, n * 4, hipMemcpyDeviceToHost, s));
-    if (d->row_top) WG_HIP(c, hipMemcpyAsync(d->row_top, c->g_row_top.p, (n + 1) * 4, hipMemcpyDeviceToHost, s));
-    if (d->vert_off) WG_HIP(c, hipMemcpyAsync(d->vert_off, c->vert_off.p, (n + 1) * 4, hipMemcpyDeviceToHost, s));
-    if (d->curve_off) WG_HIP(c, hipMemcpyAsync(d->curve_off, c->curve_off.p, (n + 1) * 4, hipMemcpyDeviceToHost, s));
-    if (d->vert && c->n_vert) WG_HIP(c, hipMemcpyAsync(d->vert, c->vert.p, c->n_vert * 4, hipMemcpyDeviceToHost, s));
-    if (d->curve && c->n_curve)
-        WG_HIP(c, hipMemcpyAsync(d->curve, c->curve.p, c->n_curve * sizeof(wg_curve), hipMemcpyDeviceToHost, s));
-    if (d->curve_color && c->n_curve)
-        WG_HIP(c, hipMemcpyAsync(d->curve_color, c->curve_color.p, c->n_curve, hipMemcpyDeviceToHost, s));
+    if (d->height && n) WG_HIP(c, hipMemcpyAsync(d->height, c->g_height.as<float>() + b, n * 4, hipMemcpyDeviceToHost, s));
+    if (d->node_y && n) WG_HIP(c, hipMemcpyAsync(d->node_y, c->g_node_y.as<float>() + b, n * 4, hipMemcpyDeviceToHost, s));
+    if (d->row_top) WG_HIP(c, hipMemcpyAsync(d->row_top, c->g_row_top.as<float>() + b, (n + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (d->vert_off) WG_HIP(c, hipMemcpyAsync(d->vert_off, c->vert_off.as<uint32_t>() + b, (n + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (d->curve_off) WG_HIP(c, hipMemcpyAsync(d->curve_off, c->curve_off.as<uint32_t>() + b, (n + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (d->vert && v1 > v0)
+        WG_HIP(c, hipMemcpyAsync(d->vert, c->vert.as<uint32_t>() + v0, (v1 - v0) * 4, hipMemcpyDeviceToHost, s));
+    if (d->curve && c1 > c0)
+        WG_HIP(c, hipMemcpyAsync(d->curve, c->curve.as<wg_curve>() + c0, (c1 - c0) * sizeof(wg_curve), hipMemcpyDeviceToHost, s));
+    if (d->curve_color && c1 > c0)
+        WG_HIP(c, hipMemcpyAsync(d->curve_color, c->curve_color.as<uint8_t>() + c0, c1 - c0, hipMemcpyDeviceToHost, s));
     WG_HIP(c, hipStreamSynchronize(s));
+    // offsets relative to the copied slice
+    for (uint64_t i = 0; c->sh.on && i <= n; i++) {
+        if (d->vert_off) d->vert_off[i] -= (uint32_t)v0;
+        if (d->curve_off) d->curve_off[i] -= (uint32_t)c0;
+    }
     return WG_OK;
 }
 
@@ -285,14 +361,22 @@ int wg_copy_geometry(wg_ctx *c, const wg_geometry_host *d) {
 int wg_emit_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel, const float *palette) {
     if (!c || !palette) return WG_E_INVALID;
     if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
-    if (rb > re || re > c->n) return wg_fail(c, WG_E_INVALID, "row range [%llu,%llu) outside [0,%llu)",
-                                             (unsigned long long)rb, (unsigned long long)re, (unsigned long long)c->n);
+    const ShardState &S = c->sh;
+    if (rb > re || rb < S.s || re > S.e)
+        return wg_fail(c, WG_E_INVALID, "row range [%llu,%llu) outside [%llu,%llu)", (unsigned long long)rb,
+                       (unsigned long long)re, (unsigned long long)S.s, (unsigned long long)S.e);
     (void)hipSetDevice(c->device);
     c->have_vtx = false;
     WG_ALLOC(c, c->palette, WG_PALETTE_SIZE * 4 * sizeof(float));
     WG_HIP(c, hipMemcpyAsync(c->palette.p, palette, WG_PALETTE_SIZE * 4 * sizeof(float), hipMemcpyHostToDevice, c->stream));
-    int rc = wg_stage_vertices(c, rb, re, sel);
+    // global rows -> the context's row arrays (a shard's rows start at row_base)
+    const uint64_t b = S.row_base;
+    const int64_t sel_l = (sel >= 0 && (uint64_t)sel >= S.s && (uint64_t)sel < S.e) ? (int64_t)((uint64_t)sel - S.s + b) : -1;
+    int rc = wg_stage_vertices(c, rb - S.s + b, re - S.s + b, sel_l);
     if (rc != WG_OK) return rc;
+    c->vrow_begin = rb;
+    c->vrow_end = re;
+    c->selected = sel;
     c->have_vtx = true;
     return WG_OK;
 }
@@ -331,18 +415,19 @@ int wg_copy_vertex_offsets(wg_ctx *c, uint64_t *dst) {
 int wg_device_views_get(wg_ctx *c, wg_device_views *o) {
     if (!c || !o) return WG_E_INVALID;
     std::memset(o, 0, sizeof(*o));
+    const uint64_t b = c->sh.row_base;   // views start at the first own row
     if (c->have_layout) {
-        o->lane = c->lane_out.as<uint32_t>();
-        o->color = c->color_out.as<uint8_t>();
-        o->edges = c->edges.as<wg_edge>();
+        o->lane = c->lane_out.as<uint32_t>() + b;
+        o->color = c->color_out.as<uint8_t>() + b;
+        o->edges = (c->sh.on && !c->sh.replicated) ? c->sh.own_edges.as<wg_edge>() : c->edges.as<wg_edge>();
     }
     if (c->have_geom) {
-        o->height = c->g_height.as<float>();
-        o->node_y = c->g_node_y.as<float>();
-        o->row_top = c->g_row_top.as<float>();
-        o->vert_off = c->vert_off.as<uint32_t>();
+        o->height = c->g_height.as<float>() + b;
+        o->node_y = c->g_node_y.as<float>() + b;
+        o->row_top = c->g_row_top.as<float>() + b;
+        o->vert_off = c->vert_off.as<uint32_t>() + b;
         o->vert = c->vert.as<uint32_t>();
-        o->curve_off = c->curve_off.as<uint32_t>();
+        o->curve_off = c->curve_off.as<uint32_t>() + b;
         o->curve = c->curve.as<wg_curve>();
         o->curve_color = c->curve_color.as<uint8_t>();
     }
@@ -361,6 +446,7 @@ int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
     WG_HIP(c, hipStreamSynchronize(c->stream));
     if (n > 3) out[3] = c->replay_iters;
     if (n > 4) out[4] = (uint32_t)c->n_events;
+    if (n > 5) out[5] = c->sh.on ? (c->sh.replicated ? 2u : 1u) : 0u;
     return WG_OK;
 }
 

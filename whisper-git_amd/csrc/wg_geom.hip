@@ -338,13 +338,22 @@ __device__ __forceinline__ Cubic subcurve(const Cubic &c, float a, float b) {   
 
 __global__ void k_curves(uint64_t nc, const uint32_t *__restrict__ curve_ref, const uint32_t *__restrict__ curve_row,
                          const wg_edge *__restrict__ edges, const float *__restrict__ row_top,
-                         const float *__restrict__ node_y, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color) {
+                         const float *__restrict__ node_y, const float2 *__restrict__ edge_y,
+                         wg_curve *__restrict__ out, uint8_t *__restrict__ out_color) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nc) return;
-    const wg_edge e = edges[curve_ref[k]];
+    const uint32_t ref = curve_ref[k];
+    const wg_edge e = edges[ref];
     const uint32_t row = curve_row[k];
-    const float child_y = row_top[e.child_row] + node_y[e.child_row];     // :554
-    const float parent_y = row_top[e.parent_row] + node_y[e.parent_row];  // :555
+    float child_y, parent_y;
+    if (edge_y) {   // row-sharded geometry: endpoints may lie in other shards
+        const float2 ey = edge_y[ref];
+        child_y = ey.x;
+        parent_y = ey.y;
+    } else {
+        child_y = row_top[e.child_row] + node_y[e.child_row];     // :554
+        parent_y = row_top[e.parent_row] + node_y[e.parent_row];  // :555
+    }
     const float dy = parent_y - child_y;
     Cubic cv;
     cv.p0 = Pt{(float)e.child_lane, child_y};
@@ -464,7 +473,8 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     wg_stage_begin(c, "geom_curves");
     if (c->n_curve)
         hipLaunchKernelGGL(k_curves, dim3(blocks(c->n_curve)), dim3(T), 0, s, c->n_curve, c->curve_ref.as<const uint32_t>(),
-                           c->curve_row.as<const uint32_t>(), E, rt, c->g_node_y.as<const float>(), c->curve.as<wg_curve>(),
+                           c->curve_row.as<const uint32_t>(), E, rt, c->g_node_y.as<const float>(),
+                           reinterpret_cast<const float2 *>(c->edge_y), c->curve.as<wg_curve>(),
                            c->curve_color.as<uint8_t>());
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);

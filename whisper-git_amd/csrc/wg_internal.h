@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "wgraph.h"
 
@@ -72,6 +73,35 @@ struct LfRange {
 // Vertex tiles (wg_vertex.hip)
 #define WG_VTX_TILE   1536   // vertices per workgroup tile (36 KiB of LDS)
 
+// Row-sharded build state (wg_shard.hip)
+struct ShardState {
+    bool on = false;          // the last build was a wg_shard_build_* build
+    bool replicated = false;  // ... that fell back to the whole-list build on every rank
+    int world = 1, rank = 0, step = 0;
+    uint64_t N = 0, s = 0, e = 0, Etot = 0;
+    uint64_t E0 = 0, E1 = 0;  // own parent references [parent_off[s], parent_off[e])
+    uint64_t row_base = 0;    // index of row s in the context's row arrays
+    DevBuf msg;               // this rank's outgoing message
+    uint64_t msg_bytes = 0;
+    DevBuf ptable;            // id partition table (global duplicate check)
+    DevBuf prow;              // int32 [E1-E0] parent rows of own references
+    DevBuf unres;             // own references not found in the local table
+    uint64_t n_unres = 0, uoff_own = 0;
+    std::vector<uint64_t> ucnt;
+    DevBuf flags, xcnt, refx, isfb, xsec;
+    DevBuf xall;              // WgXEnt [nx]: crossing entries of every rank
+    std::vector<uint64_t> xoff, evoff, auxoff;   // per-rank prefixes (world + 1)
+    uint64_t nev_own = 0, naux_own = 0;
+    DevBuf xtok, xt;          // chain token per crossing entry: shard-local / global
+    DevBuf dev_small;
+    DevBuf h_g, rt_g;         // heights / row_top of rows [0, e)
+    DevBuf band_host;         // device copy of a host band array [N]
+    const float *band_g = nullptr;
+    DevBuf xchild, xpar;      // per crossing entry: child lane/colour, parent lane/y
+    DevBuf in_scan, edge_y, own_edges;
+    uint64_t n_own_edges = 0;
+};
+
 struct wg_ctx {
     int         device = 0;
     hipStream_t stream = nullptr;
@@ -134,6 +164,7 @@ struct wg_ctx {
     DevBuf rowflags;        // uint8 [N] bit0 zero-height strip, bit1 child strip empty, bit2 parent strip empty
     DevBuf carry_fill;      // uint32 [nch]
     DevBuf sweep_err;       // uint32 [4]
+    const float *edge_y = nullptr;   // per edge {child_y, parent_y} override (row-sharded geometry), or null
     // ---- vertices -------------------------------------------------------------
     bool     have_vtx = false;
     uint64_t vrow_begin = 0, vrow_end = 0, n_vtx = 0;
@@ -145,6 +176,7 @@ struct wg_ctx {
     DevBuf tile_first;      // uint4 [tiles+1] per-tile record (first row, first vertical, first curve, straddles)
     // ---- host-side tables --------------------------------------------------------
     uint32_t h_thresh[32];  // delta thresholds for heights 29..56
+    ShardState sh;
     // ---- timing ----------------------------------------------------------------------
     bool       timing = false;
     StageTimer stages[WG_STAGE_MAX];
@@ -200,6 +232,8 @@ int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *
 int wg_lf_replay(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, const uint8_t **slots, bool *converged);
 int wg_lf_lanes(wg_ctx *c, const LfRange &R, const uint8_t *slots, uint32_t *lane);
 int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
+int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out);             // rows [0,m) of an n-row list
+int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top);
 int wg_stage_rowtop(wg_ctx *c, const float *d_band);   // wg_rowtop.hip
 int wg_stage_geometry(wg_ctx *c, const float *d_band); // wg_geom.hip
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel);  // wg_vertex.hip

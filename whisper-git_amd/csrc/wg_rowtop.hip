@@ -113,9 +113,10 @@ __device__ __forceinline__ int binade_of(float a) { return ilogbf(a); }
 // ---------------------------------------------------------------------------
 struct Thresh { uint32_t t[28]; };
 
-__global__ void k_heights(uint64_t n, const int64_t *__restrict__ time, Thresh th, float *__restrict__ h) {
+// rows [0, m) of an n-row list (the last row of the LIST gets ROW_HEIGHT)
+__global__ void k_heights(uint64_t m, uint64_t n, const int64_t *__restrict__ time, Thresh th, float *__restrict__ h) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= m) return;
     float out = WG_ROW_HEIGHT;
     if (i + 1 < n) {
         const uint64_t d = (uint64_t)time[i] - (uint64_t)time[i + 1];   // wrapping i64 sub
@@ -477,34 +478,35 @@ void wg_init_height_thresholds(uint32_t *th) {
 
 extern "C" void wg_debug_height_thresholds(uint32_t *out28) { wg_init_height_thresholds(out28); }
 
-int wg_stage_heights(wg_ctx *c) {
-    const uint64_t n = c->n;
-    WG_ALLOC(c, c->heights, n * 4 + 4);
-    if (n == 0) return WG_OK;
+int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out) {
+    if (m == 0) return WG_OK;
     Thresh th;
     for (int k = 0; k < 28; k++) th.t[k] = c->h_thresh[k];
     wg_stage_begin(c, "heights");
-    hipLaunchKernelGGL(k_heights, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, c->d_time, th, c->heights.as<float>());
+    hipLaunchKernelGGL(k_heights, dim3((m + 255) / 256), dim3(256), 0, c->stream, m, n, c->d_time, th, out);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;
 }
 
-int wg_stage_rowtop(wg_ctx *c, const float *d_band) {
-    const uint64_t n = c->n;
+int wg_stage_heights(wg_ctx *c) {
+    WG_ALLOC(c, c->heights, c->n * 4 + 4);
+    return wg_heights_run(c, c->n, c->n, c->heights.as<float>());
+}
+
+// row_top[0..n] of n rows with heights h (+ band, may be null)
+int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top) {
     const uint64_t nch = (n + WG_RT_CHUNK - 1) / WG_RT_CHUNK;
-    WG_ALLOC(c, c->g_row_top, (n + 1) * 4);
     WG_ALLOC(c, c->rt_chunk, (nch + 1) * sizeof(RtChunk));
     WG_ALLOC(c, c->rt_tables, (nch + 1) * WG_RT_NBIN * sizeof(uint4));
     WG_ALLOC(c, c->rt_flags, 64);
     wg_stage_begin(c, "row_top");
     WG_HIP(c, hipMemsetAsync(c->rt_flags.p, 0, 64, c->stream));
     if (n == 0) {
-        WG_HIP(c, hipMemsetAsync(c->g_row_top.p, 0, 4, c->stream));
+        WG_HIP(c, hipMemsetAsync(row_top, 0, 4, c->stream));
         wg_stage_end(c);
         return WG_OK;
     }
-    const float *h = c->heights.as<const float>();
     RtChunk *ch = c->rt_chunk.as<RtChunk>();
     uint32_t *fl = c->rt_flags.as<uint32_t>();
     hipLaunchKernelGGL(k_rt_sum, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, ch, fl);
@@ -512,10 +514,14 @@ int wg_stage_rowtop(wg_ctx *c, const float *d_band) {
     hipLaunchKernelGGL(k_rt_tables, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch,
                        c->rt_tables.as<uint4>());
     hipLaunchKernelGGL(k_rt_walk, dim3(1), dim3(64), 0, c->stream, n, nch, h, d_band, ch,
-                       c->rt_tables.as<const uint4>(), fl, c->g_row_top.as<float>());
-    hipLaunchKernelGGL(k_rt_rows, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch,
-                       c->g_row_top.as<float>());
+                       c->rt_tables.as<const uint4>(), fl, row_top);
+    hipLaunchKernelGGL(k_rt_rows, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch, row_top);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;
+}
+
+int wg_stage_rowtop(wg_ctx *c, const float *d_band) {
+    WG_ALLOC(c, c->g_row_top, (c->n + 1) * 4);
+    return wg_rowtop_run(c, c->n, c->heights.as<const float>(), d_band, c->g_row_top.as<float>());
 }

@@ -1,0 +1,859 @@
+// wg_shard.hip — row-sharded GraphLayout::build and row_geometry_with_bands
+// (SURVEY.md §8e): one process per GPU, rank r owns the contiguous rows
+// [s, e) of a commit list every rank holds in HBM, and the ranks meet at a
+// few all-gather points (RCCL over xGMI through the caller's
+// torch.distributed group; the engine only packs and unpacks messages).
+//
+// The greedy lane walk (commit_graph.rs:276-295, 401-471) is sequential over
+// the whole list, but its state only changes at lane events (wg_lanes_fast.hip),
+// and the references that cross a shard boundary are few (one per chain alive
+// at the boundary plus the long merges).  The exchanges:
+//   X1  ids of parent references this shard could not resolve locally
+//   X2  rows found for them by the shards that own those ids
+//   X3  well-formedness + the crossing entries (references to rows beyond
+//       the shard), so every shard knows every waiter created before it
+//   X4  event counts and, per crossing entry, the token of its chain
+//       (shard-local event or an earlier crossing entry) -> global event ids
+//   X5  the event records of every shard; each rank replays the global event
+//       stream (latency-bound, ~the same cost at 8M rows as at 1M) and reads
+//       its own rows' lanes from it
+//   X6  per geometry pass: lanes, colours and endpoint y of crossing edges
+// Geometry then runs unchanged on a local problem: the shard's rows between a
+// zero-height head row (child of every edge coming from earlier shards) and a
+// zero-height tail row (parent of every edge leaving it), with the true
+// endpoint y of every edge supplied per edge.  row_top (sequential f32,
+// :329-335 / :374-381) is computed for rows [0, e) on every rank.
+//
+// Lists that are not well formed (duplicate ids anywhere, parents at earlier
+// rows), that need more than 63 lane slots or whose replay does not converge
+// fall back, on every rank alike, to the single-GPU build over the whole list.
+#include <cstring>
+#include <vector>
+
+#include "wg_internal.h"
+#include "wg_hashfn.h"
+
+namespace {
+
+constexpr int T = 256;
+constexpr uint32_t XT_PENDING = 0xFFFFFFFEu;
+inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
+
+// ---- X1 / X2: parent resolution ------------------------------------------------
+__global__ void k_sh_insert(const uint8_t *__restrict__ oid, uint64_t s, uint64_t nl, unsigned long long *table,
+                            uint64_t mask) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const uint64_t gi = s + i;
+    const Key k = load_key(oid + gi * 20);
+    const unsigned long long mine = ((unsigned long long)key_fp(k) << 32) | (uint32_t)gi;
+    uint64_t h = key_hash(k) & mask;
+    for (uint64_t probes = 0; probes <= mask; probes++) {
+        unsigned long long cur = table[h];
+        if (cur == HEMPTY) {
+            const unsigned long long prev = atomicCAS(&table[h], HEMPTY, mine);
+            if (prev == HEMPTY) return;
+            cur = prev;
+        }
+        if ((uint32_t)(cur >> 32) == key_fp(k) && key_eq(k, oid + (uint64_t)(uint32_t)cur * 20)) {
+            atomicMax(&table[h], mine);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+// every id whose partition (hash) is this rank: any id seen twice?
+__global__ void k_sh_dupscan(const uint8_t *__restrict__ oid, uint64_t n, uint32_t world, uint32_t rank,
+                             unsigned long long *table, uint64_t mask, uint32_t *flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Key k = load_key(oid + i * 20);
+    const uint64_t hk = key_hash(k);
+    if ((uint32_t)((hk >> 40) % world) != rank) return;
+    const unsigned long long mine = ((unsigned long long)key_fp(k) << 32) | (uint32_t)i;
+    uint64_t h = hk & mask;
+    for (uint64_t probes = 0; probes <= mask; probes++) {
+        unsigned long long cur = table[h];
+        if (cur == HEMPTY) {
+            const unsigned long long prev = atomicCAS(&table[h], HEMPTY, mine);
+            if (prev == HEMPTY) return;
+            cur = prev;
+        }
+        if ((uint32_t)(cur >> 32) == key_fp(k) && key_eq(k, oid + (uint64_t)(uint32_t)cur * 20)) {
+            atomicOr(&flags[1], 1u);
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+__global__ void k_sh_probe(const uint8_t *__restrict__ poid, uint64_t E0, uint64_t E1, const uint8_t *__restrict__ oid,
+                           const unsigned long long *__restrict__ table, uint64_t mask, int32_t *__restrict__ prow_l,
+                           uint32_t *__restrict__ unres, uint32_t *n_unres) {
+    const uint64_t k = E0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= E1) return;
+    const int64_t r = hash_find(load_key(poid + k * 20), oid, table, mask);
+    prow_l[k - E0] = (int32_t)r;
+    if (r < 0) unres[atomicAdd(n_unres, 1u)] = (uint32_t)k;
+}
+
+__global__ void k_sh_pack_ids(const uint8_t *__restrict__ poid, const uint32_t *__restrict__ unres, uint64_t n,
+                              uint32_t *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(poid + (uint64_t)unres[i] * 20);
+#pragma unroll
+    for (int w = 0; w < 5; w++) out[i * 5 + w] = src[w];
+}
+
+struct Sections {            // per-rank sections of a gathered buffer
+    const uint8_t *base;
+    uint64_t stride;
+    uint32_t world;
+    uint64_t off[17];        // prefix of entry counts, off[world] = total
+};
+
+__device__ __forceinline__ uint32_t section_of(const Sections &S, uint64_t g) {
+    uint32_t r = 0;
+    while (r + 1 < S.world && S.off[r + 1] <= g) r++;
+    return r;
+}
+
+__global__ void k_sh_probe_gathered(Sections S, uint64_t hdr, const uint8_t *__restrict__ oid,
+                                    const unsigned long long *__restrict__ table, uint64_t mask, int32_t *__restrict__ found) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= S.off[S.world]) return;
+    const uint32_t r = section_of(S, g);
+    const uint8_t *p = S.base + r * S.stride + hdr + (g - S.off[r]) * 20;
+    found[g] = (int32_t)hash_find(load_key(p), oid, table, mask);
+}
+
+__global__ void k_sh_combine(Sections S, uint64_t own_off, uint64_t n, const uint32_t *__restrict__ unres, uint64_t E0,
+                             int32_t *__restrict__ prow_l) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t best = -1;
+    for (uint32_t r = 0; r < S.world; r++) {
+        const int32_t v = reinterpret_cast<const int32_t *>(S.base + r * S.stride)[own_off + i];
+        best = v > best ? v : best;
+    }
+    prow_l[unres[i] - E0] = best;
+}
+
+// ---- X3: well-formedness + crossing entries ------------------------------------------
+__global__ void k_sh_rows(uint64_t s, uint64_t nl, uint64_t e, const uint32_t *__restrict__ poff,
+                          const int32_t *__restrict__ prow, uint32_t *__restrict__ xcnt, uint32_t *flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const uint64_t gi = s + i;
+    const uint32_t pa = poff[gi], pb = poff[gi + 1];
+    uint32_t cnt = 0;
+    bool bad = false;
+    for (uint32_t k = pa; k < pb; k++) {
+        const int32_t p = prow[k];
+        if (p < 0) continue;
+        if ((uint64_t)p <= gi || k - pa > 0xFFFFu) bad = true;
+        if ((uint64_t)p >= e) cnt++;
+    }
+    xcnt[i] = cnt;
+    if (bad) atomicOr(&flags[0], 1u);
+}
+
+__global__ void k_sh_xout(uint64_t s, uint64_t nl, uint64_t e, const uint32_t *__restrict__ poff,
+                          const int32_t *__restrict__ prow, const uint32_t *__restrict__ xoff, WgXEnt *__restrict__ out,
+                          uint32_t *__restrict__ refx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const uint64_t gi = s + i;
+    const uint32_t pa = poff[gi], pb = poff[gi + 1];
+    uint32_t o = xoff[i];
+    for (uint32_t k = pa; k < pb; k++) {
+        const int32_t p = prow[k];
+        if (p < 0 || (uint64_t)p < e) continue;
+        bool first = true;
+        for (uint32_t q = pa; q < k; q++) first &= prow[q] != p;
+        WgXEnt x;
+        x.c = (uint32_t)gi;
+        x.p = (uint32_t)p;
+        x.kf = (k - pa) | (first ? WG_XF_FIRST_IN_ROW : 0u);
+        x.pad = 0;
+        refx[k] = o;
+        out[o++] = x;
+    }
+}
+
+// ---- X4: chain tokens of crossing entries -> global event ids ---------------------------
+// entries of rank r are [xoff[r], xoff[r+1]); a token names either an event of
+// the entry's own rank or an entry of an earlier rank (depth < world)
+__global__ void k_sh_resolve(uint64_t nx, uint32_t world, const uint64_t *__restrict__ xoff,
+                             const uint64_t *__restrict__ evoff, const uint32_t *__restrict__ tok, uint32_t *xt) {
+    for (uint64_t x = threadIdx.x; x < nx; x += blockDim.x) xt[x] = XT_PENDING;
+    __syncthreads();
+    for (uint32_t round = 0; round <= world; round++) {
+        for (uint64_t x = threadIdx.x; x < nx; x += blockDim.x) {
+            if (xt[x] != XT_PENDING) continue;
+            const uint32_t v = tok[x];
+            if (v == WG_TOK_NONE) { xt[x] = WG_TOK_NONE; continue; }
+            if (v & WG_TOK_EV) {
+                uint32_t r = 0;
+                while (r + 1 < world && xoff[r + 1] <= x) r++;
+                xt[x] = WG_TOK_EV | ((v & ~WG_TOK_EV) + (uint32_t)evoff[r]);
+            } else {
+                const uint32_t y = xt[v & ~WG_TOK_X];
+                if (y != XT_PENDING) xt[x] = y;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- X6: crossing-edge endpoints -----------------------------------------------------------
+__device__ __forceinline__ float node_y_of(const float *__restrict__ band, uint64_t row) {
+    return band ? roundf(band[row] + WG_NODE_Y) : WG_NODE_Y;   // (:390) / build default (:341)
+}
+
+// child records for own crossing entries, parent records for earlier entries into this shard
+__global__ void k_sh_pack_ends(uint64_t s, uint64_t e, const WgXEnt *__restrict__ xall, uint64_t xown_begin,
+                               uint64_t nown, uint64_t xin_end, const uint32_t *__restrict__ lane_l,
+                               const uint8_t *__restrict__ color_l, const float *__restrict__ rt_g,
+                               const float *__restrict__ band, uint4 *__restrict__ out) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nown) {
+        const uint64_t x = xown_begin + q;
+        const uint64_t c = xall[x].c;
+        out[q] = make_uint4((uint32_t)x, lane_l[c - s + 1], color_l[c - s + 1], 1u);
+    } else if (q < nown + xin_end) {
+        const uint64_t x = q - nown;
+        const uint64_t p = xall[x].p;
+        if (p >= s && p < e) {
+            const float y = rt_g[p] + node_y_of(band, p);
+            out[q] = make_uint4((uint32_t)x, lane_l[p - s + 1], __float_as_uint(y), 1u);
+        } else {
+            out[q] = make_uint4((uint32_t)x, 0u, 0u, 0u);
+        }
+    }
+}
+
+// scatter every rank's endpoint records into per-entry tables
+__global__ void k_sh_unpack_ends(Sections S, const uint64_t *__restrict__ nown, uint4 *__restrict__ xchild,
+                                 uint4 *__restrict__ xpar) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= S.off[S.world]) return;
+    const uint32_t r = section_of(S, g);
+    const uint64_t q = g - S.off[r];
+    const uint4 v = reinterpret_cast<const uint4 *>(S.base + r * S.stride + 16)[q];
+    if (!v.w) return;
+    if (q < nown[r]) xchild[v.x] = v;
+    else xpar[v.x] = v;
+}
+
+// the local problem's rows: head (0), own rows (1..nl), tail (nl+1)
+__global__ void k_sh_local_rows(uint64_t s, uint64_t nl, const float *__restrict__ h_g, const float *__restrict__ band_g,
+                                const float *__restrict__ rt_g, float *__restrict__ h_l, float *__restrict__ band_l,
+                                float *__restrict__ rt_l) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > nl + 2) return;
+    // row_top: head and first own row share rt_g[s]; tail and end share rt_g[e]
+    const uint64_t g = r == 0 ? s : (r <= nl ? s + r - 1 : s + nl);
+    rt_l[r] = rt_g[g];
+    if (r < nl + 2) {
+        const bool own = r >= 1 && r <= nl;
+        h_l[r] = own ? h_g[s + r - 1] : 0.0f;
+        if (band_l) band_l[r] = own ? band_g[s + r - 1] : 0.0f;
+    }
+}
+
+__global__ void k_sh_in_flags(uint64_t s, const WgXEnt *__restrict__ xall, uint64_t xin_end, uint32_t *__restrict__ f) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= xin_end) return;
+    f[x] = xall[x].p >= s ? 1u : 0u;
+}
+
+__global__ void k_sh_own_counts(uint64_t s, uint64_t nl, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow,
+                                const uint32_t *__restrict__ in_scan, uint64_t xin_end, uint32_t *__restrict__ cnt) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nl + 2) return;
+    uint32_t v = 0;
+    if (r == 0) v = in_scan[xin_end];
+    else if (r <= nl) {
+        const uint64_t gi = s + r - 1;
+        for (uint32_t k = poff[gi]; k < poff[gi + 1]; k++) v += prow[k] >= 0;
+    }
+    cnt[r] = v;
+}
+
+struct LocalEdgeArgs {
+    uint64_t s, nl, e, xin_end, xown_begin;
+    const WgXEnt *xall;
+    const uint32_t *poff;
+    const int32_t *prow;        // by global ref index
+    const uint32_t *refx;       // by global ref index: own crossing entry (section-local)
+    const uint32_t *in_scan;    // position of incoming entries
+    const uint32_t *edge_off;   // local edge CSR
+    const uint32_t *lane_l;
+    const uint8_t *color_l;
+    const float *rt_g, *band;
+    const uint4 *xchild, *xpar;
+    wg_edge *edges;             // local
+    float2 *edge_y;
+    wg_edge *own_g;             // own edges, global numbering
+};
+
+__device__ __forceinline__ void far_parent(const LocalEdgeArgs &A, uint64_t p, uint64_t x, uint32_t *pl, uint32_t *plane,
+                                           float *py) {
+    if (p < A.e) {
+        *pl = (uint32_t)(p - A.s + 1);
+        *plane = A.lane_l[p - A.s + 1];
+        *py = A.rt_g[p] + node_y_of(A.band, p);
+    } else {
+        *pl = (uint32_t)(A.nl + 1);
+        *plane = A.xpar[x].y;
+        *py = __uint_as_float(A.xpar[x].z);
+    }
+}
+
+__global__ void k_sh_edges_in(LocalEdgeArgs A) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= A.xin_end) return;
+    const WgXEnt en = A.xall[x];
+    if (en.p < A.s) return;
+    const uint32_t o = A.in_scan[x];
+    uint32_t pl, plane;
+    float py;
+    far_parent(A, en.p, x, &pl, &plane, &py);
+    wg_edge ed;
+    ed.child_row = 0;
+    ed.child_lane = A.xchild[x].y;
+    ed.parent_row = pl;
+    ed.parent_lane = plane;
+    ed.color = A.xchild[x].z;
+    A.edges[o] = ed;
+    A.edge_y[o] = make_float2(A.rt_g[en.c] + node_y_of(A.band, en.c), py);
+}
+
+__global__ void k_sh_edges_own(LocalEdgeArgs A) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.nl) return;
+    const uint64_t gi = A.s + i;
+    uint32_t o = A.edge_off[i + 1];
+    const uint32_t n_in = A.edge_off[1];
+    const uint32_t cl = A.lane_l[i + 1], col = A.color_l[i + 1];
+    const float cy = A.rt_g[gi] + node_y_of(A.band, gi);
+    for (uint32_t k = A.poff[gi]; k < A.poff[gi + 1]; k++) {
+        const int32_t p = A.prow[k];
+        if (p < 0) continue;
+        uint32_t pl, plane;
+        float py;
+        far_parent(A, (uint64_t)p, (uint64_t)p >= A.e ? A.xown_begin + A.refx[k] : 0, &pl, &plane, &py);
+        wg_edge ed;
+        ed.child_row = (uint32_t)(i + 1);
+        ed.child_lane = cl;
+        ed.parent_row = pl;
+        ed.parent_lane = plane;
+        ed.color = col;
+        A.edges[o] = ed;
+        A.edge_y[o] = make_float2(cy, py);
+        ed.child_row = (uint32_t)gi;
+        ed.parent_row = (uint32_t)p;
+        A.own_g[o - n_in] = ed;
+        o++;
+    }
+}
+
+__global__ void k_sh_lane_out(uint64_t s, uint64_t nl, const uint32_t *__restrict__ lane_asg, const uint8_t *__restrict__ flags,
+                              uint32_t *__restrict__ lane_l, uint8_t *__restrict__ color_l) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nl + 2) return;
+    if (r == 0 || r > nl) { lane_l[r] = 0; color_l[r] = 0; return; }
+    const uint32_t l = lane_asg[r - 1];
+    lane_l[r] = l;
+    color_l[r] = (flags[s + r - 1] & WG_FLAG_ORPHAN) ? (uint8_t)WG_COLOR_ORPHAN : (uint8_t)(l % 6u);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+enum { SH_IDLE = 0, SH_X1, SH_X2, SH_X3, SH_X4, SH_X5, SH_X6 };
+
+static int sh_send(wg_ctx *c, uint64_t bytes, wg_shard_msg *out) {
+    WG_ALLOC(c, c->sh.msg, bytes + 64);
+    c->sh.msg_bytes = bytes;
+    out->send = c->sh.msg.p;
+    out->bytes = bytes;
+    out->done = 0;
+    out->step = c->sh.step;
+    return WG_OK;
+}
+static void sh_done(wg_ctx *c, wg_shard_msg *out) {
+    c->sh.step = SH_IDLE;
+    out->send = nullptr;
+    out->bytes = 0;
+    out->done = 1;
+    out->step = 0;
+}
+
+static Sections make_sections(const void *gathered, uint64_t stride, int world, const std::vector<uint64_t> &cnt) {
+    Sections S;
+    S.base = reinterpret_cast<const uint8_t *>(gathered);
+    S.stride = stride;
+    S.world = (uint32_t)world;
+    S.off[0] = 0;
+    for (int r = 0; r < world; r++) S.off[r + 1] = S.off[r] + cnt[r];
+    return S;
+}
+
+// per-rank 16-byte headers of a gathered buffer
+static int read_headers(wg_ctx *c, const void *gathered, uint64_t stride, std::vector<uint32_t> &hdr) {
+    const int W = c->sh.world;
+    hdr.assign((size_t)W * 4, 0);
+    WG_HIP(c, hipMemcpy2DAsync(hdr.data(), 16, gathered, stride, 16, W, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+static LfRange sh_range(wg_ctx *c) {
+    ShardState &S = c->sh;
+    LfRange R;
+    R.s = S.s;
+    R.nl = S.e - S.s;
+    R.e = S.e;
+    R.poff = c->d_poff;
+    R.prow = S.prow.as<const int32_t>() - S.E0;
+    R.canon = nullptr;
+    R.xall = S.xall.as<const WgXEnt>();
+    R.xin_end = S.xoff[S.rank];
+    R.xown_begin = S.xoff[S.rank];
+    R.xown_end = S.xoff[S.rank + 1];
+    R.isfb = S.isfb.as<uint8_t>() - S.E0;
+    R.xsec = S.xsec.as<uint32_t>() - S.E0;
+    return R;
+}
+
+// whole-list build on every rank (inputs that the sharded path does not take)
+static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
+    ShardState &S = c->sh;
+    S.replicated = true;
+    c->n = S.N;
+    c->e_refs = S.Etot;
+    c->edge_y = nullptr;
+    int rc;
+    if ((rc = wg_stage_hash_join(c)) != WG_OK) return rc;
+    if ((rc = wg_stage_lanes(c)) != WG_OK) return rc;
+    if ((rc = wg_stage_edges(c)) != WG_OK) return rc;
+    if ((rc = wg_stage_heights(c)) != WG_OK) return rc;
+    c->have_layout = true;
+    if ((rc = wg_stage_rowtop(c, nullptr)) != WG_OK) return rc;
+    if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
+    c->have_geom = true;
+    S.row_base = S.s;
+    sh_done(c, out);
+    return WG_OK;
+}
+
+// geometry pass, part 1: row_top for rows [0, e), endpoint records (X6)
+static int sh_geometry_begin(wg_ctx *c, const float *band_g, wg_shard_msg *out) {
+    ShardState &S = c->sh;
+    const uint64_t e = S.e;
+    WG_ALLOC(c, S.rt_g, (e + 1) * 4);
+    int rc = wg_rowtop_run(c, e, S.h_g.as<const float>(), band_g, S.rt_g.as<float>());
+    if (rc != WG_OK) return rc;
+    S.band_g = band_g;
+    const uint64_t nown = S.xoff[S.rank + 1] - S.xoff[S.rank], xin = S.xoff[S.rank];
+    S.step = SH_X6;
+    if ((rc = sh_send(c, 16 + (nown + xin) * 16, out)) != WG_OK) return rc;
+    uint32_t hdr[4] = {(uint32_t)nown, (uint32_t)xin, 0, 0};
+    WG_HIP(c, hipMemcpyAsync(S.msg.p, hdr, 16, hipMemcpyHostToDevice, c->stream));
+    if (nown + xin)
+        hipLaunchKernelGGL(k_sh_pack_ends, dim3(blocks(nown + xin)), dim3(T), 0, c->stream, S.s, S.e,
+                           S.xall.as<const WgXEnt>(), S.xoff[S.rank], nown, xin, c->lane_out.as<const uint32_t>(),
+                           c->color_out.as<const uint8_t>(), S.rt_g.as<const float>(), band_g,
+                           reinterpret_cast<uint4 *>(S.msg.as<uint8_t>() + 16));
+    WG_HIP(c, hipGetLastError());
+    WG_HIP(c, hipStreamSynchronize(c->stream));   // the caller copies the message on another stream
+    return WG_OK;
+}
+
+// geometry pass, part 2: the local problem and the unchanged geometry stages
+static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, wg_shard_msg *out) {
+    ShardState &S = c->sh;
+    const int W = S.world;
+    const uint64_t s = S.s, e = S.e, nl = e - s, nloc = nl + 2, nx = S.xoff[W];
+    hipStream_t st = c->stream;
+    std::vector<uint32_t> hdr;
+    int rc = read_headers(c, gathered, stride, hdr);
+    if (rc != WG_OK) return rc;
+    std::vector<uint64_t> cnt(W), nown(W);
+    for (int r = 0; r < W; r++) { nown[r] = hdr[4 * r]; cnt[r] = hdr[4 * r] + hdr[4 * r + 1]; }
+    WG_ALLOC(c, S.xchild, nx * 16 + 16);
+    WG_ALLOC(c, S.xpar, nx * 16 + 16);
+    WG_ALLOC(c, S.dev_small, 64 * 8);
+    WG_HIP(c, hipMemcpyAsync(S.dev_small.p, nown.data(), W * 8, hipMemcpyHostToDevice, st));
+    Sections SX = make_sections(gathered, stride, W, cnt);
+    if (SX.off[W])
+        hipLaunchKernelGGL(k_sh_unpack_ends, dim3(blocks(SX.off[W])), dim3(T), 0, st, SX, S.dev_small.as<const uint64_t>(),
+                           S.xchild.as<uint4>(), S.xpar.as<uint4>());
+    // local rows
+    const float *band_g = S.band_g;
+    WG_ALLOC(c, c->heights, nloc * 4 + 4);
+    WG_ALLOC(c, c->g_row_top, (nloc + 1) * 4);
+    if (band_g) WG_ALLOC(c, c->band, nloc * 4 + 4);
+    hipLaunchKernelGGL(k_sh_local_rows, dim3(blocks(nloc + 1)), dim3(T), 0, st, s, nl, S.h_g.as<const float>(), band_g,
+                       S.rt_g.as<const float>(), c->heights.as<float>(), band_g ? c->band.as<float>() : nullptr,
+                       c->g_row_top.as<float>());
+    // local edges: incoming (earlier shards, edge order) then own
+    const uint64_t xin = S.xoff[S.rank];
+    WG_ALLOC(c, S.in_scan, (xin + 2) * 4);
+    WG_ALLOC(c, c->edge_cnt, (nloc + 2) * 4);
+    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(nloc + xin + 2));
+    WG_HIP(c, hipMemsetAsync(S.in_scan.p, 0, 8, st));
+    if (xin) hipLaunchKernelGGL(k_sh_in_flags, dim3(blocks(xin)), dim3(T), 0, st, s, S.xall.as<const WgXEnt>(), xin,
+                                S.in_scan.as<uint32_t>());
+    WG_HIP(c, wg_exclusive_scan_u32(S.in_scan.as<uint32_t>(), S.in_scan.as<uint32_t>(), xin, c->scan_tmp.p, st));
+    const int32_t *prow = S.prow.as<const int32_t>() - S.E0;
+    hipLaunchKernelGGL(k_sh_own_counts, dim3(blocks(nloc)), dim3(T), 0, st, s, nl, c->d_poff, prow,
+                       S.in_scan.as<const uint32_t>(), xin, c->edge_cnt.as<uint32_t>());
+    WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), nloc, c->scan_tmp.p, st));
+    uint32_t tot[2] = {0, 0};
+    WG_HIP(c, hipMemcpyAsync(&tot[0], c->edge_cnt.as<uint32_t>() + nloc, 4, hipMemcpyDeviceToHost, st));
+    WG_HIP(c, hipMemcpyAsync(&tot[1], c->edge_cnt.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
+    WG_HIP(c, hipStreamSynchronize(st));
+    const uint64_t ne = tot[0], n_in = tot[1];
+    WG_ALLOC(c, c->edges, ne * sizeof(wg_edge) + 16);
+    WG_ALLOC(c, S.edge_y, ne * 8 + 16);
+    WG_ALLOC(c, S.own_edges, (ne - n_in) * sizeof(wg_edge) + 16);
+    LocalEdgeArgs A;
+    A.s = s; A.nl = nl; A.e = e; A.xin_end = xin; A.xown_begin = S.xoff[S.rank];
+    A.xall = S.xall.as<const WgXEnt>();
+    A.poff = c->d_poff;
+    A.prow = prow;
+    A.refx = S.refx.as<const uint32_t>() - S.E0;
+    A.in_scan = S.in_scan.as<const uint32_t>();
+    A.edge_off = c->edge_cnt.as<const uint32_t>();
+    A.lane_l = c->lane_out.as<const uint32_t>();
+    A.color_l = c->color_out.as<const uint8_t>();
+    A.rt_g = S.rt_g.as<const float>();
+    A.band = band_g;
+    A.xchild = S.xchild.as<const uint4>();
+    A.xpar = S.xpar.as<const uint4>();
+    A.edges = c->edges.as<wg_edge>();
+    A.edge_y = S.edge_y.as<float2>();
+    A.own_g = S.own_edges.as<wg_edge>();
+    if (xin) hipLaunchKernelGGL(k_sh_edges_in, dim3(blocks(xin)), dim3(T), 0, st, A);
+    if (nl) hipLaunchKernelGGL(k_sh_edges_own, dim3(blocks(nl)), dim3(T), 0, st, A);
+    WG_HIP(c, hipGetLastError());
+    c->n = nloc;
+    c->n_edges = ne;
+    c->edge_y = S.edge_y.as<const float>();
+    S.n_own_edges = ne - n_in;
+    rc = wg_stage_geometry(c, band_g ? c->band.as<const float>() : nullptr);
+    if (rc != WG_OK) return rc;
+    c->have_geom = true;
+    sh_done(c, out);
+    return WG_OK;
+}
+
+extern "C" {
+
+int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, uint64_t row_begin, uint64_t row_end,
+                         wg_shard_msg *out) {
+    if (!c || !in || !out) return WG_E_INVALID;
+    if (world < 1 || world > 16 || rank < 0 || rank >= world) return wg_fail(c, WG_E_INVALID, "bad world/rank %d/%d", world, rank);
+    if (in->residency != WG_DEVICE) return wg_fail(c, WG_E_INVALID, "sharded builds take device-resident commits");
+    const uint64_t N = in->n_commits;
+    if (row_begin > row_end || row_end > N) return wg_fail(c, WG_E_INVALID, "row range outside the list");
+    (void)hipSetDevice(c->device);
+    ShardState &S = c->sh;
+    S.on = true;
+    S.replicated = false;
+    S.world = world;
+    S.rank = rank;
+    S.N = N;
+    S.s = row_begin;
+    S.e = row_end;
+    S.Etot = in->n_parents;
+    S.row_base = 1;
+    c->have_layout = c->have_geom = c->have_vtx = false;
+    c->edge_y = nullptr;
+    c->d_oid = in->oid;
+    c->d_time = in->time;
+    c->d_poff = in->parent_off;
+    c->d_poid = in->parent_oid;
+    if (in->flags) c->d_flags = in->flags;
+    else {
+        WG_ALLOC(c, c->in_flags, N + 4);
+        WG_HIP(c, hipMemsetAsync(c->in_flags.p, 0, N + 4, c->stream));
+        c->d_flags = c->in_flags.as<uint8_t>();
+    }
+    c->n = N;
+    c->e_refs = S.Etot;
+    hipStream_t st = c->stream;
+    uint32_t eo[2] = {0, 0};
+    if (N) {
+        WG_HIP(c, hipMemcpyAsync(&eo[0], c->d_poff + row_begin, 4, hipMemcpyDeviceToHost, st));
+        WG_HIP(c, hipMemcpyAsync(&eo[1], c->d_poff + row_end, 4, hipMemcpyDeviceToHost, st));
+        WG_HIP(c, hipStreamSynchronize(st));
+    }
+    S.E0 = eo[0];
+    S.E1 = eo[1];
+    c->e_refs_own = S.E1 - S.E0;
+    if (world == 1) return sh_fallback(c, out);
+    const uint64_t nl = row_end - row_begin, El = S.E1 - S.E0;
+    // ---- local table, probes, global duplicate scan -------------------------------------
+    uint64_t cap = 1024;
+    while (cap < 2 * nl) cap <<= 1;
+    uint64_t pcap = 1024;
+    while (pcap < 2 * (N / world + 1) + 1024) pcap <<= 1;
+    WG_ALLOC(c, c->hash, cap * 8);
+    WG_ALLOC(c, S.ptable, pcap * 8);
+    WG_ALLOC(c, S.prow, El * 4 + 4);
+    WG_ALLOC(c, S.unres, El * 4 + 4);
+    WG_ALLOC(c, S.flags, 64);
+    wg_stage_begin(c, "hash_join");
+    WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8, st));
+    WG_HIP(c, hipMemsetAsync(S.ptable.p, 0xFF, pcap * 8, st));
+    WG_HIP(c, hipMemsetAsync(S.flags.p, 0, 64, st));
+    if (nl) hipLaunchKernelGGL(k_sh_insert, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
+                               c->hash.as<unsigned long long>(), cap - 1);
+    if (N) hipLaunchKernelGGL(k_sh_dupscan, dim3(blocks(N)), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
+                              S.ptable.as<unsigned long long>(), pcap - 1, S.flags.as<uint32_t>());
+    if (El) hipLaunchKernelGGL(k_sh_probe, dim3(blocks(El)), dim3(T), 0, st, c->d_poid, S.E0, S.E1, c->d_oid,
+                               c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>(), S.unres.as<uint32_t>(),
+                               S.flags.as<uint32_t>() + 2);
+    uint32_t nu = 0;
+    WG_HIP(c, hipMemcpyAsync(&nu, S.flags.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, st));
+    WG_HIP(c, hipStreamSynchronize(st));
+    c->hcap = cap;
+    S.n_unres = nu;
+    S.step = SH_X1;
+    int rc = sh_send(c, (uint64_t)nu * 20, out);
+    if (rc != WG_OK) return rc;
+    if (nu) hipLaunchKernelGGL(k_sh_pack_ids, dim3(blocks(nu)), dim3(T), 0, st, c->d_poid, S.unres.as<const uint32_t>(),
+                               (uint64_t)nu, S.msg.as<uint32_t>());
+    WG_HIP(c, hipGetLastError());
+    WG_HIP(c, hipStreamSynchronize(st));
+    wg_stage_end(c);
+    return WG_OK;
+}
+
+int wg_shard_copy_msg(wg_ctx *c, void *dst) {
+    if (!c || (!dst && c->sh.msg_bytes)) return WG_E_INVALID;
+    if (c->sh.msg_bytes) WG_HIP(c, hipMemcpyAsync(dst, c->sh.msg.p, c->sh.msg_bytes, hipMemcpyDefault, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const uint64_t *sizes, wg_shard_msg *out) {
+    if (!c || !out || !sizes) return WG_E_INVALID;
+    ShardState &S = c->sh;
+    const int W = S.world;
+    if (!S.on || S.step == SH_IDLE) return wg_fail(c, WG_E_STATE, "no sharded call in progress");
+    for (int r = 0; r < W; r++)
+        if (sizes[r] > stride) return wg_fail(c, WG_E_INVALID, "message %d longer than the stride", r);
+    if (!gathered && stride) return wg_fail(c, WG_E_INVALID, "null gathered buffer");
+    (void)hipSetDevice(c->device);
+    hipStream_t st = c->stream;
+    const uint64_t s = S.s, e = S.e, nl = e - s, El = S.E1 - S.E0;
+    int rc;
+    switch (S.step) {
+    case SH_X1: {   // everyone's unresolved ids -> rows found in this shard
+        S.ucnt.assign(W, 0);
+        for (int r = 0; r < W; r++) S.ucnt[r] = sizes[r] / 20;
+        Sections SU = make_sections(gathered, stride, W, S.ucnt);
+        const uint64_t L = SU.off[W];
+        S.uoff_own = SU.off[S.rank];
+        S.step = SH_X2;
+        if ((rc = sh_send(c, L * 4, out)) != WG_OK) return rc;
+        if (L) hipLaunchKernelGGL(k_sh_probe_gathered, dim3(blocks(L)), dim3(T), 0, st, SU, (uint64_t)0, c->d_oid,
+                                  c->hash.as<const unsigned long long>(), c->hcap - 1, S.msg.as<int32_t>());
+        WG_HIP(c, hipGetLastError());
+        WG_HIP(c, hipStreamSynchronize(st));
+        return WG_OK;
+    }
+    case SH_X2: {   // rows of our unresolved refs; well-formedness; crossing entries
+        std::vector<uint64_t> dummy(W, 0);
+        Sections SF = make_sections(gathered, stride, W, dummy);
+        if (S.n_unres)
+            hipLaunchKernelGGL(k_sh_combine, dim3(blocks(S.n_unres)), dim3(T), 0, st, SF, S.uoff_own, S.n_unres,
+                               S.unres.as<const uint32_t>(), S.E0, S.prow.as<int32_t>());
+        WG_ALLOC(c, S.xcnt, (nl + 2) * 4);
+        WG_ALLOC(c, S.refx, El * 4 + 4);
+        WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(nl + 2));
+        const int32_t *prow = S.prow.as<const int32_t>() - S.E0;
+        if (nl) hipLaunchKernelGGL(k_sh_rows, dim3(blocks(nl)), dim3(T), 0, st, s, nl, e, c->d_poff, prow,
+                                   S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
+        WG_HIP(c, wg_exclusive_scan_u32(S.xcnt.as<uint32_t>(), S.xcnt.as<uint32_t>(), nl, c->scan_tmp.p, st));
+        uint32_t fl[2] = {0, 0}, nxo = 0;
+        WG_HIP(c, hipMemcpyAsync(fl, S.flags.p, 8, hipMemcpyDeviceToHost, st));
+        WG_HIP(c, hipMemcpyAsync(&nxo, S.xcnt.as<uint32_t>() + nl, 4, hipMemcpyDeviceToHost, st));
+        WG_HIP(c, hipStreamSynchronize(st));
+        S.step = SH_X3;
+        if ((rc = sh_send(c, 16 + (uint64_t)nxo * sizeof(WgXEnt), out)) != WG_OK) return rc;
+        uint32_t hdr[4] = {fl[0] | fl[1], nxo, 0, 0};
+        WG_HIP(c, hipMemcpyAsync(S.msg.p, hdr, 16, hipMemcpyHostToDevice, st));
+        if (nl) hipLaunchKernelGGL(k_sh_xout, dim3(blocks(nl)), dim3(T), 0, st, s, nl, e, c->d_poff, prow,
+                                   S.xcnt.as<const uint32_t>(), reinterpret_cast<WgXEnt *>(S.msg.as<uint8_t>() + 16),
+                                   S.refx.as<uint32_t>() - S.E0);
+        WG_HIP(c, hipGetLastError());
+        WG_HIP(c, hipStreamSynchronize(st));
+        return WG_OK;
+    }
+    case SH_X3: {   // crossing table; lane phases up to the chain tokens
+        std::vector<uint32_t> hdr;
+        if ((rc = read_headers(c, gathered, stride, hdr)) != WG_OK) return rc;
+        bool bad = false;
+        S.xoff.assign(W + 1, 0);
+        for (int r = 0; r < W; r++) {
+            bad |= hdr[4 * r] != 0;
+            S.xoff[r + 1] = S.xoff[r] + hdr[4 * r + 1];
+        }
+        if (bad) return sh_fallback(c, out);
+        const uint64_t nx = S.xoff[W];
+        WG_ALLOC(c, S.xall, nx * sizeof(WgXEnt) + 16);
+        for (int r = 0; r < W; r++)
+            if (hdr[4 * r + 1])
+                WG_HIP(c, hipMemcpyAsync(S.xall.as<WgXEnt>() + S.xoff[r], (const uint8_t *)gathered + r * stride + 16,
+                                         hdr[4 * r + 1] * sizeof(WgXEnt), hipMemcpyDeviceToDevice, st));
+        WG_ALLOC(c, S.isfb, El + 16);
+        WG_ALLOC(c, S.xsec, El * 4 + 16);
+        WG_HIP(c, hipMemsetAsync(S.isfb.p, 0, El + 16, st));
+        WG_ALLOC(c, c->lane_scalars, 64);
+        WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, st));
+        LfRange R = sh_range(c);
+        wg_stage_begin(c, "lanes");
+        uint32_t viol = 0;
+        uint64_t nev = 0, naux = 0;
+        if ((rc = wg_lf_refs(c, R, &viol, &nev, &naux)) != WG_OK) return rc;
+        if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
+        wg_stage_end(c);
+        S.nev_own = nev;
+        S.naux_own = naux;
+        const uint64_t nown = R.xown_end - R.xown_begin;
+        S.step = SH_X4;
+        if ((rc = sh_send(c, 16 + nown * 4, out)) != WG_OK) return rc;
+        uint32_t h4[4] = {(uint32_t)nev, (uint32_t)naux, viol, 0};
+        WG_HIP(c, hipMemcpyAsync(S.msg.p, h4, 16, hipMemcpyHostToDevice, st));
+        if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(S.msg.as<uint8_t>() + 16))) != WG_OK) return rc;
+        WG_HIP(c, hipStreamSynchronize(st));
+        return WG_OK;
+    }
+    case SH_X4: {   // global event ids; this shard's event records
+        std::vector<uint32_t> hdr;
+        if ((rc = read_headers(c, gathered, stride, hdr)) != WG_OK) return rc;
+        S.evoff.assign(W + 1, 0);
+        S.auxoff.assign(W + 1, 0);
+        bool bad = false;
+        for (int r = 0; r < W; r++) {
+            S.evoff[r + 1] = S.evoff[r] + hdr[4 * r];
+            S.auxoff[r + 1] = S.auxoff[r] + hdr[4 * r + 1];
+            bad |= hdr[4 * r + 2] != 0;
+        }
+        if (bad || S.evoff[W] >= (1ull << 30)) return sh_fallback(c, out);
+        const uint64_t nx = S.xoff[W];
+        WG_ALLOC(c, S.xtok, nx * 4 + 16);
+        WG_ALLOC(c, S.xt, nx * 4 + 16);
+        for (int r = 0; r < W; r++) {
+            const uint64_t n = S.xoff[r + 1] - S.xoff[r];
+            if (n) WG_HIP(c, hipMemcpyAsync(S.xtok.as<uint32_t>() + S.xoff[r], (const uint8_t *)gathered + r * stride + 16,
+                                            n * 4, hipMemcpyDeviceToDevice, st));
+        }
+        WG_ALLOC(c, S.dev_small, 64 * 8);
+        WG_HIP(c, hipMemcpyAsync(S.dev_small.p, S.xoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
+        WG_HIP(c, hipMemcpyAsync(S.dev_small.as<uint64_t>() + 32, S.evoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
+        if (nx) hipLaunchKernelGGL(k_sh_resolve, dim3(1), dim3(1024), 0, st, nx, (uint32_t)W, S.dev_small.as<const uint64_t>(),
+                                   S.dev_small.as<const uint64_t>() + 32, S.xtok.as<const uint32_t>(), S.xt.as<uint32_t>());
+        S.step = SH_X5;
+        const uint64_t nev = S.nev_own, naux = S.naux_own;
+        if ((rc = sh_send(c, 16 + nev * 16 + naux * 4, out)) != WG_OK) return rc;
+        uint32_t h5[4] = {(uint32_t)nev, (uint32_t)naux, 0, 0};
+        WG_HIP(c, hipMemcpyAsync(S.msg.p, h5, 16, hipMemcpyHostToDevice, st));
+        LfRange R = sh_range(c);
+        uint8_t *m = S.msg.as<uint8_t>();
+        if ((rc = wg_lf_events(c, R, (uint32_t)S.evoff[S.rank], S.xt.as<const uint32_t>(), reinterpret_cast<uint4 *>(m + 16),
+                               reinterpret_cast<uint32_t *>(m + 16 + nev * 16), (uint32_t)S.auxoff[S.rank])) != WG_OK)
+            return rc;
+        WG_HIP(c, hipStreamSynchronize(st));
+        return WG_OK;
+    }
+    case SH_X5: {   // replay the global event stream; lanes of own rows; default geometry
+        const uint64_t nev = S.evoff[W], naux = S.auxoff[W];
+        DevBuf &evrec = c->lf[10], &aux = c->lf[18];
+        WG_ALLOC(c, evrec, (nev + 256) * 16);
+        WG_ALLOC(c, aux, naux * 4 + 4);
+        WG_HIP(c, hipMemsetAsync(evrec.as<uint4>() + nev, 0, 256 * 16, st));
+        for (int r = 0; r < W; r++) {
+            const uint64_t ne_r = S.evoff[r + 1] - S.evoff[r], na_r = S.auxoff[r + 1] - S.auxoff[r];
+            const uint8_t *src = (const uint8_t *)gathered + r * stride + 16;
+            if (ne_r) WG_HIP(c, hipMemcpyAsync(evrec.as<uint4>() + S.evoff[r], src, ne_r * 16, hipMemcpyDeviceToDevice, st));
+            if (na_r) WG_HIP(c, hipMemcpyAsync(aux.as<uint32_t>() + S.auxoff[r], src + ne_r * 16, na_r * 4,
+                                               hipMemcpyDeviceToDevice, st));
+        }
+        c->n_events = nev;
+        const uint8_t *slots = nullptr;
+        bool conv = false;
+        if ((rc = wg_lf_replay(c, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(), &slots, &conv)) != WG_OK) return rc;
+        if (!conv) return sh_fallback(c, out);
+        WG_ALLOC(c, c->lane_asg, nl * 4 + 4);
+        LfRange R = sh_range(c);
+        if ((rc = wg_lf_lanes(c, R, slots, c->lane_asg.as<uint32_t>())) != WG_OK) return rc;
+        uint32_t sc[4];
+        WG_HIP(c, hipMemcpyAsync(sc, c->lane_scalars.p, 16, hipMemcpyDeviceToHost, st));
+        WG_HIP(c, hipStreamSynchronize(st));
+        if (sc[2]) return sh_fallback(c, out);      // more than 63 slots: same decision on every rank
+        c->max_lane = sc[0];
+        c->n_slots = sc[1];
+        c->lane_path = 0;
+        const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
+        const float gw = (float)vis * WG_LANE_W;
+        c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
+        const uint64_t nloc = nl + 2;
+        WG_ALLOC(c, c->lane_out, nloc * 4 + 4);
+        WG_ALLOC(c, c->color_out, nloc + 4);
+        hipLaunchKernelGGL(k_sh_lane_out, dim3(blocks(nloc)), dim3(T), 0, st, s, nl, c->lane_asg.as<const uint32_t>(),
+                           c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>());
+        // heights of rows [0, e) (the last row of the LIST is ROW_HEIGHT)
+        WG_ALLOC(c, S.h_g, e * 4 + 4);
+        if ((rc = wg_heights_run(c, e, S.N, S.h_g.as<float>())) != WG_OK) return rc;
+        c->have_layout = true;
+        return sh_geometry_begin(c, nullptr, out);
+    }
+    case SH_X6:
+        return sh_geometry_finish(c, gathered, stride, out);
+    default:
+        return wg_fail(c, WG_E_STATE, "bad shard step %d", S.step);
+    }
+}
+
+int wg_shard_geometry_begin(wg_ctx *c, const float *band, int32_t residency, wg_shard_msg *out) {
+    if (!c || !out) return WG_E_INVALID;
+    ShardState &S = c->sh;
+    if (!S.on || !c->have_layout) return wg_fail(c, WG_E_STATE, "no sharded layout built");
+    if (S.step != SH_IDLE) return wg_fail(c, WG_E_STATE, "a sharded call is in progress");
+    (void)hipSetDevice(c->device);
+    c->have_vtx = false;
+    const float *d_band = nullptr;
+    if (band) {
+        if (residency == WG_HOST) {
+            WG_ALLOC(c, S.band_host, S.N * 4 + 4);
+            if (S.N) WG_HIP(c, hipMemcpyAsync(S.band_host.p, band, S.N * 4, hipMemcpyHostToDevice, c->stream));
+            d_band = S.band_host.as<float>();
+        } else if (residency == WG_DEVICE) {
+            d_band = band;
+        } else {
+            return wg_fail(c, WG_E_INVALID, "bad residency %d", residency);
+        }
+    }
+    if (S.replicated) {
+        c->have_geom = false;
+        int rc = wg_row_geometry(c, d_band, WG_DEVICE);
+        if (rc != WG_OK) return rc;
+        sh_done(c, out);
+        return WG_OK;
+    }
+    c->have_geom = false;
+    return sh_geometry_begin(c, d_band, out);
+}
+
+}  // extern "C"

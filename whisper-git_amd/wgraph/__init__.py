@@ -65,6 +65,12 @@ def lib():
             "wg_debug_counters": ([vp, vp, ctypes.c_int], ctypes.c_int),
             "wg_stage_timings": ([vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
                                   ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+            "wg_shard_build_begin": ([vp, ctypes.POINTER(abi.Commits), ctypes.c_int, ctypes.c_int, u64, u64,
+                                      ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
+            "wg_shard_geometry_begin": ([vp, vp, i32, ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
+            "wg_shard_copy_msg": ([vp, vp], ctypes.c_int),
+            "wg_shard_exchange": ([vp, vp, u64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(abi.ShardMsg)],
+                                  ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -79,7 +85,8 @@ EXPORTED_SYMBOLS = (
     "wg_layout_build", "wg_layout_summary_get", "wg_copy_lanes", "wg_copy_edges", "wg_copy_row_heights",
     "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
-    "wg_enable_timing", "wg_stage_timings", "wg_debug_counters")
+    "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
+    "wg_shard_copy_msg", "wg_shard_exchange")
 
 
 class Engine:
@@ -126,6 +133,37 @@ class Engine:
             self._keep = [dag]
         self._commits = commits
         self._check(lib().wg_layout_build(self._ctx, ctypes.byref(commits)))
+
+    # -- row-sharded build (one rank per GPU; see wgraph.shard.ShardComm) ------------------
+    def shard_build(self, commits: abi.Commits, world: int, rank: int, row_begin: int, row_end: int, comm):
+        """GraphLayout::build of rows [row_begin, row_end) of a device-resident
+        list every rank holds; `comm` all-gathers the engine's messages."""
+        self._commits = commits
+        msg = abi.ShardMsg()
+        self._check(lib().wg_shard_build_begin(self._ctx, ctypes.byref(commits), world, rank, row_begin, row_end,
+                                               ctypes.byref(msg)))
+        self._shard_loop(msg, comm)
+
+    def shard_geometry(self, comm, band=None, device_ptr: int | None = None):
+        """row_geometry_with_bands of this rank's shard (band = the whole list's)."""
+        msg = abi.ShardMsg()
+        if device_ptr is not None:
+            self._check(lib().wg_shard_geometry_begin(self._ctx, device_ptr, abi.WG_DEVICE, ctypes.byref(msg)))
+        elif band is None:
+            self._check(lib().wg_shard_geometry_begin(self._ctx, None, abi.WG_HOST, ctypes.byref(msg)))
+        else:
+            b = np.ascontiguousarray(band, np.float32)
+            self._band = b
+            self._check(lib().wg_shard_geometry_begin(self._ctx, b.ctypes.data, abi.WG_HOST, ctypes.byref(msg)))
+        self._shard_loop(msg, comm)
+
+    def _shard_loop(self, msg, comm):
+        while not msg.done:
+            gathered, stride, sizes = comm.allgather(
+                int(msg.bytes), lambda dst: self._check(lib().wg_shard_copy_msg(self._ctx, dst)))
+            sz = (ctypes.c_uint64 * len(sizes))(*sizes)
+            self._check(lib().wg_shard_exchange(self._ctx, gathered.data_ptr(), stride, sz, ctypes.byref(msg)))
+            del gathered
 
     def layout_summary(self) -> abi.LayoutSummary:
         s = abi.LayoutSummary()
@@ -185,7 +223,8 @@ class Engine:
     # -- vertices ------------------------------------------------------------------------
     def emit_vertices(self, row_begin=0, row_end=None, selected=-1, palette=None):
         if row_end is None:
-            row_end = self.layout_summary().n_rows
+            ls = self.layout_summary()
+            row_end = ls.row_begin + ls.n_rows
         pal = np.ascontiguousarray(abi.DEFAULT_PALETTE if palette is None else palette, np.float32)
         self._check(lib().wg_emit_vertices(self._ctx, row_begin, row_end, selected, pal.ctypes.data))
 

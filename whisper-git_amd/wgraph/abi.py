@@ -32,7 +32,13 @@ class Edge(ctypes.Structure):
 class LayoutSummary(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_uint64), ("n_edges", ctypes.c_uint64),
                 ("max_lane", ctypes.c_uint32), ("n_slots", ctypes.c_uint32),
-                ("graph_width", ctypes.c_float), ("lane_path", ctypes.c_uint32)]
+                ("graph_width", ctypes.c_float), ("lane_path", ctypes.c_uint32),
+                ("row_begin", ctypes.c_uint64)]
+
+
+class ShardMsg(ctypes.Structure):
+    _fields_ = [("send", ctypes.c_void_p), ("bytes", ctypes.c_uint64), ("done", ctypes.c_int32),
+                ("step", ctypes.c_int32)]
 
 
 class GeometrySummary(ctypes.Structure):
