@@ -8,10 +8,12 @@ written to HBM).  Workload: the WIDE16 synthetic DAG (C5 shape, <= 16
 lanes), 1M commit-rows per GPU (weak scaling: N GPUs = an N-million-row
 DAG, each rank emits its contiguous 1M-row shard).
 
-Round-1 multi-GPU scheme: the sequential layout stages run
-replicated on every rank over the whole DAG; vertex emission (the
-HBM-bound stage) is sharded by contiguous row range; ranks meet only at the
-timing barrier.  Launched per the driver contract:
+Multi-GPU: every rank holds the whole N-million-row DAG in
+HBM and builds only its contiguous 1M-row shard (wg_shard_* C ABI): parent
+ids, crossing references, chain tokens and the lane-event stream are
+all-gathered over RCCL (torch.distributed "nccl" group) at six exchange
+points per step, then each rank emits its own rows' vertex buffers.
+Launched per the driver contract:
   python bench.py --gpus 1 --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
@@ -42,6 +44,8 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=1_000_000, help="rows of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (host rehearsal)")
+    ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     return ap.parse_args()
 
 
@@ -95,9 +99,13 @@ def main():
 
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
+    dev_idx = 0 if args.same_device else local_rank
+    torch.cuda.set_device(dev_idx)
     if world > 1:
-        dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group(backend="nccl", init_method="env://", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(backend=args.dist_backend, init_method="env://")
 
     import wgraph
     from wgraph import abi, synth
@@ -112,7 +120,7 @@ def main():
     shard1 = min(rows_total, shard0 + args.rows_per_gpu)
 
     # device-resident inputs (the timed region starts from HBM)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", dev_idx)
     t_oid = torch.from_numpy(dag.oid.reshape(-1)).to(dev)
     t_time = torch.from_numpy(dag.time).to(dev)
     t_poff = torch.from_numpy(dag.parent_off.view(np.int32)).to(dev)
@@ -125,15 +133,23 @@ def main():
     commits.parent_off, commits.parent_oid = t_poff.data_ptr(), t_poid.data_ptr()
     commits.flags, commits.residency = t_flags.data_ptr(), abi.WG_DEVICE
 
-    eng = wgraph.Engine(local_rank)
+    eng = wgraph.Engine(dev_idx)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
     pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
     selected = shard0 + 7
+    comm = None
+    if world > 1:
+        from wgraph.shard import ShardComm
+        comm = ShardComm(dev)
 
     def step():
-        eng.build(commits=commits)
-        eng.row_geometry(device_ptr=t_band.data_ptr())
+        if comm is None:
+            eng.build(commits=commits)
+            eng.row_geometry(device_ptr=t_band.data_ptr())
+        else:
+            eng.shard_build(commits, world, rank, shard0, shard1, comm)
+            eng.shard_geometry(comm, device_ptr=t_band.data_ptr())
         eng.emit_vertices(shard0, shard1, selected=selected, palette=pal)
 
     for _ in range(args.warmup):
@@ -173,9 +189,10 @@ def main():
     gs = eng.geometry_summary()
     n_rows_shard = shard1 - shard0
     vtx_ms = float(np.mean(launches.get("vtx_emit", [float("nan")])))   # one launch per step
-    g = eng.geometry()
-    nvert_shard = int(g["vert_off"][shard1]) - int(g["vert_off"][shard0])
-    ncurve_shard = int(g["curve_off"][shard1]) - int(g["curve_off"][shard0])
+    g = eng.geometry()   # this rank's rows (the whole list at N=1)
+    r0, r1 = (shard0, shard1) if world == 1 else (0, shard1 - shard0)
+    nvert_shard = int(g["vert_off"][r1]) - int(g["vert_off"][r0])
+    ncurve_shard = int(g["curve_off"][r1]) - int(g["curve_off"][r0])
     # algorithmic bytes of one vtx_emit launch: vertices written + geometry read
     bytes_w = 24 * vs.n_vertices
     bytes_r = 4 * nvert_shard + 33 * ncurve_shard + n_rows_shard * (8 + 4 + 4 + 4 + 4 + 4 + 1)
@@ -215,7 +232,9 @@ def main():
     stages = {k: round(float(v), 4) for k, v in stage_ms.items()}
     log("stage ms (mean over timed steps):", json.dumps(stages))
     log(f"rows {rows_total}, shard {n_rows_shard}, vertices {vs.n_vertices}, vert {gs.n_vert}, curves {gs.n_curve}, "
-        f"max_lane {eng.layout_summary().max_lane}, lane_path {eng.layout_summary().lane_path}")
+        f"max_lane {eng.layout_summary().max_lane}, lane_path {eng.layout_summary().lane_path}, "
+        f"build mode {int(eng.debug_counters()[5])}" + (f", exchanges/step {comm.exchanges / (args.steps + args.warmup):.1f}"
+                                                         if comm else ""))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

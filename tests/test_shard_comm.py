@@ -23,13 +23,16 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        comm = ShardComm(torch.device("cpu"))
+        comm = ShardComm(torch.device("cpu"), initial_cap=64)
         got = []
-        for step, length in enumerate([0, 5, 37 + 11 * rank, 4096 * (rank + 1)]):
+        # lengths below, at and above the slot; the last two reuse step 3's grown slot
+        for step, length in enumerate([0, 5, 37 + 11 * rank, 4096 * (rank + 1), 10, 3000]):
             payload = bytes((rank * 31 + step + i) & 0xFF for i in range(length))
-            out, stride, sizes = comm.allgather(length, lambda ptr: ctypes.memmove(ptr, payload, length))
-            got.append((stride, sizes, [bytes(out[r * stride:r * stride + sizes[r]].numpy()) for r in range(world)]))
-        q.put((rank, got, comm.exchanges))
+            out, off, stride, sizes = comm.allgather(length, lambda ptr: ctypes.memmove(ptr, payload, length),
+                                                     step=min(step, 3))
+            got.append((stride, sizes, [bytes(out[off + r * stride:off + r * stride + sizes[r]].numpy())
+                                        for r in range(world)]))
+        q.put((rank, got, (comm.exchanges, comm.collectives)))
     finally:
         dist.destroy_process_group()
 
@@ -45,14 +48,17 @@ def test_allgather_world2_gloo():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for step, length_of in enumerate([lambda r: 0, lambda r: 5, lambda r: 37 + 11 * r, lambda r: 4096 * (r + 1)]):
+    lengths = [lambda r: 0, lambda r: 5, lambda r: 37 + 11 * r, lambda r: 4096 * (r + 1), lambda r: 10,
+               lambda r: 3000]
+    for step, length_of in enumerate(lengths):
         for rank in range(world):
             stride, sizes, msgs = res[rank][0][step]
             assert sizes == [length_of(r) for r in range(world)]
             assert stride % 16 == 0 and stride >= max(max(sizes), 16)
             for r in range(world):
                 assert msgs[r] == bytes((r * 31 + step + i) & 0xFF for i in range(length_of(r)))
-        assert res[0][1] == 4
+    # one collective per exchange, plus one retry where the 64-byte slot had to grow (step 3)
+    assert res[0][1] == (6, 7)
 
 
 @pytest.mark.parametrize("n,world", [(0, 2), (1, 2), (7, 3), (1_000_000, 8), (8_000_000, 8)])

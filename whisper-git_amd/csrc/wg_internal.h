@@ -85,9 +85,9 @@ struct ShardState {
     uint64_t msg_bytes = 0;
     DevBuf ptable;            // id partition table (global duplicate check)
     DevBuf prow;              // int32 [E1-E0] parent rows of own references
-    DevBuf unres;             // own references not found in the local table
-    uint64_t n_unres = 0, uoff_own = 0;
-    std::vector<uint64_t> ucnt;
+    DevBuf unres;             // unresolved-reference records of every rank (32 B each)
+    uint64_t n_unres = 0;
+    std::vector<uint64_t> uoffs;   // per-rank prefix of those records
     DevBuf flags, xcnt, refx, isfb, xsec;
     DevBuf xall;              // WgXEnt [nx]: crossing entries of every rank
     std::vector<uint64_t> xoff, evoff, auxoff;   // per-rank prefixes (world + 1)

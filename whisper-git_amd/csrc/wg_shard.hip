@@ -8,13 +8,14 @@
 // the whole list, but its state only changes at lane events (wg_lanes_fast.hip),
 // and the references that cross a shard boundary are few (one per chain alive
 // at the boundary plus the long merges).  The exchanges:
-//   X1  ids of parent references this shard could not resolve locally
-//   X2  rows found for them by the shards that own those ids
-//   X3  well-formedness + the crossing entries (references to rows beyond
-//       the shard), so every shard knows every waiter created before it
-//   X4  event counts and, per crossing entry, the token of its chain
+//   X1  well-formedness flags + the parent references this shard could not
+//       resolve locally (child row, parent index, id)
+//   X2  the rows the owning shards found for them: every rank derives the
+//       same table of crossing entries (references to rows beyond the
+//       child's shard), so every shard knows every waiter created before it
+//   X3  event counts and, per crossing entry, the token of its chain
 //       (shard-local event or an earlier crossing entry) -> global event ids
-//   X5  the event records of every shard; each rank replays the global event
+//   X4  the event records of every shard; each rank replays the global event
 //       stream (latency-bound, ~the same cost at 8M rows as at 1M) and reads
 //       its own rows' lanes from it
 //   X6  per geometry pass: lanes, colours and endpoint y of crossing edges
@@ -88,23 +89,47 @@ __global__ void k_sh_dupscan(const uint8_t *__restrict__ oid, uint64_t n, uint32
     }
 }
 
-__global__ void k_sh_probe(const uint8_t *__restrict__ poid, uint64_t E0, uint64_t E1, const uint8_t *__restrict__ oid,
-                           const unsigned long long *__restrict__ table, uint64_t mask, int32_t *__restrict__ prow_l,
-                           uint32_t *__restrict__ unres, uint32_t *n_unres) {
-    const uint64_t k = E0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= E1) return;
-    const int64_t r = hash_find(load_key(poid + k * 20), oid, table, mask);
-    prow_l[k - E0] = (int32_t)r;
-    if (r < 0) unres[atomicAdd(n_unres, 1u)] = (uint32_t)k;
+// own rows' references against the local table; per-row count of the unresolved
+__global__ void k_sh_probe(uint64_t s, uint64_t nl, const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
+                           uint64_t E0, const uint8_t *__restrict__ oid, const unsigned long long *__restrict__ table,
+                           uint64_t mask, int32_t *__restrict__ prow_l, uint32_t *__restrict__ ucnt, uint32_t *flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const uint64_t gi = s + i;
+    const uint32_t pa = poff[gi], pb = poff[gi + 1];
+    uint32_t nu = 0;
+    bool bad = false;
+    for (uint32_t k = pa; k < pb; k++) {
+        const int64_t r = hash_find(load_key(poid + (uint64_t)k * 20), oid, table, mask);
+        prow_l[k - E0] = (int32_t)r;
+        if (r < 0) nu++;
+        else if ((uint64_t)r <= gi) bad = true;       // parent at an earlier row (or itself)
+        if (k - pa > 0xFFFFu) bad = true;
+    }
+    ucnt[i] = nu;
+    if (bad) atomicOr(&flags[0], 1u);
 }
 
-__global__ void k_sh_pack_ids(const uint8_t *__restrict__ poid, const uint32_t *__restrict__ unres, uint64_t n,
-                              uint32_t *__restrict__ out) {
+// unresolved reference record: {child row, parent index, id[5], 0} (32 bytes), row order
+__global__ void k_sh_pack_unres(uint64_t s, uint64_t nl, const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
+                                uint64_t E0, const int32_t *__restrict__ prow_l, const uint32_t *__restrict__ uoff,
+                                uint32_t *__restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(poid + (uint64_t)unres[i] * 20);
+    if (i >= nl) return;
+    const uint64_t gi = s + i;
+    const uint32_t pa = poff[gi], pb = poff[gi + 1];
+    uint32_t o = uoff[i];
+    for (uint32_t k = pa; k < pb; k++) {
+        if (prow_l[k - E0] >= 0) continue;
+        uint32_t *r = out + (uint64_t)o * 8;
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(poid + (uint64_t)k * 20);
+        r[0] = (uint32_t)gi;
+        r[1] = k - pa;
 #pragma unroll
-    for (int w = 0; w < 5; w++) out[i * 5 + w] = src[w];
+        for (int w = 0; w < 5; w++) r[2 + w] = src[w];
+        r[7] = 0;
+        o++;
+    }
 }
 
 struct Sections {            // per-rank sections of a gathered buffer
@@ -120,66 +145,50 @@ __device__ __forceinline__ uint32_t section_of(const Sections &S, uint64_t g) {
     return r;
 }
 
-__global__ void k_sh_probe_gathered(Sections S, uint64_t hdr, const uint8_t *__restrict__ oid,
+__global__ void k_sh_probe_gathered(uint64_t L, const uint32_t *__restrict__ rec, const uint8_t *__restrict__ oid,
                                     const unsigned long long *__restrict__ table, uint64_t mask, int32_t *__restrict__ found) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= S.off[S.world]) return;
-    const uint32_t r = section_of(S, g);
-    const uint8_t *p = S.base + r * S.stride + hdr + (g - S.off[r]) * 20;
-    found[g] = (int32_t)hash_find(load_key(p), oid, table, mask);
+    if (g >= L) return;
+    found[g] = (int32_t)hash_find(load_key(reinterpret_cast<const uint8_t *>(rec + g * 8 + 2)), oid, table, mask);
 }
 
-__global__ void k_sh_combine(Sections S, uint64_t own_off, uint64_t n, const uint32_t *__restrict__ unres, uint64_t E0,
-                             int32_t *__restrict__ prow_l) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// row of every unresolved reference of every rank: the shard that owns the id found it
+__global__ void k_sh_combine(Sections F, uint64_t L, const uint32_t *__restrict__ rec, int32_t *__restrict__ row,
+                             uint32_t *__restrict__ xflag, uint32_t *flags) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= L) return;
     int32_t best = -1;
-    for (uint32_t r = 0; r < S.world; r++) {
-        const int32_t v = reinterpret_cast<const int32_t *>(S.base + r * S.stride)[own_off + i];
+    for (uint32_t r = 0; r < F.world; r++) {
+        const int32_t v = reinterpret_cast<const int32_t *>(F.base + r * F.stride)[g];
         best = v > best ? v : best;
     }
-    prow_l[unres[i] - E0] = best;
+    row[g] = best;
+    xflag[g] = best >= 0 ? 1u : 0u;
+    if (best >= 0 && (uint32_t)best <= rec[g * 8]) atomicOr(&flags[0], 1u);   // parent at an earlier row
 }
 
-// ---- X3: well-formedness + crossing entries ------------------------------------------
-__global__ void k_sh_rows(uint64_t s, uint64_t nl, uint64_t e, const uint32_t *__restrict__ poff,
-                          const int32_t *__restrict__ prow, uint32_t *__restrict__ xcnt, uint32_t *flags) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nl) return;
-    const uint64_t gi = s + i;
-    const uint32_t pa = poff[gi], pb = poff[gi + 1];
-    uint32_t cnt = 0;
-    bool bad = false;
-    for (uint32_t k = pa; k < pb; k++) {
-        const int32_t p = prow[k];
-        if (p < 0) continue;
-        if ((uint64_t)p <= gi || k - pa > 0xFFFFu) bad = true;
-        if ((uint64_t)p >= e) cnt++;
-    }
-    xcnt[i] = cnt;
-    if (bad) atomicOr(&flags[0], 1u);
-}
-
-__global__ void k_sh_xout(uint64_t s, uint64_t nl, uint64_t e, const uint32_t *__restrict__ poff,
-                          const int32_t *__restrict__ prow, const uint32_t *__restrict__ xoff, WgXEnt *__restrict__ out,
-                          uint32_t *__restrict__ refx) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nl) return;
-    const uint64_t gi = s + i;
-    const uint32_t pa = poff[gi], pb = poff[gi + 1];
-    uint32_t o = xoff[i];
-    for (uint32_t k = pa; k < pb; k++) {
-        const int32_t p = prow[k];
-        if (p < 0 || (uint64_t)p < e) continue;
-        bool first = true;
-        for (uint32_t q = pa; q < k; q++) first &= prow[q] != p;
-        WgXEnt x;
-        x.c = (uint32_t)gi;
-        x.p = (uint32_t)p;
-        x.kf = (k - pa) | (first ? WG_XF_FIRST_IN_ROW : 0u);
-        x.pad = 0;
-        refx[k] = o;
-        out[o++] = x;
+// crossing entries (every rank's resolved-elsewhere references, rank-major, row order)
+__global__ void k_sh_xbuild(uint64_t L, const uint32_t *__restrict__ rec, const int32_t *__restrict__ row,
+                            const uint32_t *__restrict__ xpos, uint64_t own_lo, uint64_t own_hi,
+                            const uint32_t *__restrict__ poff, uint64_t E0, WgXEnt *__restrict__ xall,
+                            int32_t *__restrict__ prow_l, uint32_t *__restrict__ refx) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= L || row[g] < 0) return;
+    const uint32_t c = rec[g * 8], kidx = rec[g * 8 + 1];
+    bool first = true;   // no earlier reference of the same row resolves to the same parent
+    for (uint64_t h = g; h > 0 && rec[(h - 1) * 8] == c; h--)
+        if (row[h - 1] == row[g]) first = false;
+    const uint32_t x = xpos[g];
+    WgXEnt en;
+    en.c = c;
+    en.p = (uint32_t)row[g];
+    en.kf = kidx | (first ? WG_XF_FIRST_IN_ROW : 0u);
+    en.pad = 0;
+    xall[x] = en;
+    if (g >= own_lo && g < own_hi) {
+        const uint64_t k = (uint64_t)poff[c] + kidx;
+        prow_l[k - E0] = row[g];
+        refx[k - E0] = x - xpos[own_lo];
     }
 }
 
@@ -376,7 +385,9 @@ __global__ void k_sh_lane_out(uint64_t s, uint64_t nl, const uint32_t *__restric
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-enum { SH_IDLE = 0, SH_X1, SH_X2, SH_X3, SH_X4, SH_X5, SH_X6 };
+// exchange points: X1 unresolved references, X2 their rows, X3 chain tokens,
+// X4 event records, X6 crossing-edge endpoints (per geometry pass)
+enum { SH_IDLE = 0, SH_X1, SH_X2, SH_X3, SH_X4, SH_X6 = 6 };
 
 static int sh_send(wg_ctx *c, uint64_t bytes, wg_shard_msg *out) {
     WG_ALLOC(c, c->sh.msg, bytes + 64);
@@ -609,8 +620,9 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     WG_ALLOC(c, c->hash, cap * 8);
     WG_ALLOC(c, S.ptable, pcap * 8);
     WG_ALLOC(c, S.prow, El * 4 + 4);
-    WG_ALLOC(c, S.unres, El * 4 + 4);
+    WG_ALLOC(c, S.xcnt, (nl + 2) * 4);
     WG_ALLOC(c, S.flags, 64);
+    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(nl + 2));
     wg_stage_begin(c, "hash_join");
     WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8, st));
     WG_HIP(c, hipMemsetAsync(S.ptable.p, 0xFF, pcap * 8, st));
@@ -619,19 +631,25 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
                                c->hash.as<unsigned long long>(), cap - 1);
     if (N) hipLaunchKernelGGL(k_sh_dupscan, dim3(blocks(N)), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
                               S.ptable.as<unsigned long long>(), pcap - 1, S.flags.as<uint32_t>());
-    if (El) hipLaunchKernelGGL(k_sh_probe, dim3(blocks(El)), dim3(T), 0, st, c->d_poid, S.E0, S.E1, c->d_oid,
-                               c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>(), S.unres.as<uint32_t>(),
-                               S.flags.as<uint32_t>() + 2);
-    uint32_t nu = 0;
-    WG_HIP(c, hipMemcpyAsync(&nu, S.flags.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, st));
+    if (nl) hipLaunchKernelGGL(k_sh_probe, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid, S.E0,
+                               c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>(),
+                               S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
+    WG_HIP(c, wg_exclusive_scan_u32(S.xcnt.as<uint32_t>(), S.xcnt.as<uint32_t>(), nl, c->scan_tmp.p, st));
+    uint32_t h[3] = {0, 0, 0};
+    WG_HIP(c, hipMemcpyAsync(h, S.flags.p, 8, hipMemcpyDeviceToHost, st));
+    WG_HIP(c, hipMemcpyAsync(&h[2], S.xcnt.as<uint32_t>() + nl, 4, hipMemcpyDeviceToHost, st));
     WG_HIP(c, hipStreamSynchronize(st));
     c->hcap = cap;
-    S.n_unres = nu;
+    S.n_unres = h[2];
     S.step = SH_X1;
-    int rc = sh_send(c, (uint64_t)nu * 20, out);
+    // X1: {violation | duplicate, n} + one 32-byte record per unresolved reference, row order
+    int rc = sh_send(c, 16 + (uint64_t)h[2] * 32, out);
     if (rc != WG_OK) return rc;
-    if (nu) hipLaunchKernelGGL(k_sh_pack_ids, dim3(blocks(nu)), dim3(T), 0, st, c->d_poid, S.unres.as<const uint32_t>(),
-                               (uint64_t)nu, S.msg.as<uint32_t>());
+    uint32_t hdr[4] = {h[0] | h[1], h[2], 0, 0};
+    WG_HIP(c, hipMemcpyAsync(S.msg.p, hdr, 16, hipMemcpyHostToDevice, st));
+    if (nl) hipLaunchKernelGGL(k_sh_pack_unres, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid, S.E0,
+                               S.prow.as<const int32_t>(), S.xcnt.as<const uint32_t>(),
+                               reinterpret_cast<uint32_t *>(S.msg.as<uint8_t>() + 16));
     WG_HIP(c, hipGetLastError());
     WG_HIP(c, hipStreamSynchronize(st));
     wg_stage_end(c);
@@ -658,64 +676,55 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
     const uint64_t s = S.s, e = S.e, nl = e - s, El = S.E1 - S.E0;
     int rc;
     switch (S.step) {
-    case SH_X1: {   // everyone's unresolved ids -> rows found in this shard
-        S.ucnt.assign(W, 0);
-        for (int r = 0; r < W; r++) S.ucnt[r] = sizes[r] / 20;
-        Sections SU = make_sections(gathered, stride, W, S.ucnt);
-        const uint64_t L = SU.off[W];
-        S.uoff_own = SU.off[S.rank];
-        S.step = SH_X2;
-        if ((rc = sh_send(c, L * 4, out)) != WG_OK) return rc;
-        if (L) hipLaunchKernelGGL(k_sh_probe_gathered, dim3(blocks(L)), dim3(T), 0, st, SU, (uint64_t)0, c->d_oid,
-                                  c->hash.as<const unsigned long long>(), c->hcap - 1, S.msg.as<int32_t>());
-        WG_HIP(c, hipGetLastError());
-        WG_HIP(c, hipStreamSynchronize(st));
-        return WG_OK;
-    }
-    case SH_X2: {   // rows of our unresolved refs; well-formedness; crossing entries
-        std::vector<uint64_t> dummy(W, 0);
-        Sections SF = make_sections(gathered, stride, W, dummy);
-        if (S.n_unres)
-            hipLaunchKernelGGL(k_sh_combine, dim3(blocks(S.n_unres)), dim3(T), 0, st, SF, S.uoff_own, S.n_unres,
-                               S.unres.as<const uint32_t>(), S.E0, S.prow.as<int32_t>());
-        WG_ALLOC(c, S.xcnt, (nl + 2) * 4);
-        WG_ALLOC(c, S.refx, El * 4 + 4);
-        WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(nl + 2));
-        const int32_t *prow = S.prow.as<const int32_t>() - S.E0;
-        if (nl) hipLaunchKernelGGL(k_sh_rows, dim3(blocks(nl)), dim3(T), 0, st, s, nl, e, c->d_poff, prow,
-                                   S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
-        WG_HIP(c, wg_exclusive_scan_u32(S.xcnt.as<uint32_t>(), S.xcnt.as<uint32_t>(), nl, c->scan_tmp.p, st));
-        uint32_t fl[2] = {0, 0}, nxo = 0;
-        WG_HIP(c, hipMemcpyAsync(fl, S.flags.p, 8, hipMemcpyDeviceToHost, st));
-        WG_HIP(c, hipMemcpyAsync(&nxo, S.xcnt.as<uint32_t>() + nl, 4, hipMemcpyDeviceToHost, st));
-        WG_HIP(c, hipStreamSynchronize(st));
-        S.step = SH_X3;
-        if ((rc = sh_send(c, 16 + (uint64_t)nxo * sizeof(WgXEnt), out)) != WG_OK) return rc;
-        uint32_t hdr[4] = {fl[0] | fl[1], nxo, 0, 0};
-        WG_HIP(c, hipMemcpyAsync(S.msg.p, hdr, 16, hipMemcpyHostToDevice, st));
-        if (nl) hipLaunchKernelGGL(k_sh_xout, dim3(blocks(nl)), dim3(T), 0, st, s, nl, e, c->d_poff, prow,
-                                   S.xcnt.as<const uint32_t>(), reinterpret_cast<WgXEnt *>(S.msg.as<uint8_t>() + 16),
-                                   S.refx.as<uint32_t>() - S.E0);
-        WG_HIP(c, hipGetLastError());
-        WG_HIP(c, hipStreamSynchronize(st));
-        return WG_OK;
-    }
-    case SH_X3: {   // crossing table; lane phases up to the chain tokens
+    case SH_X1: {   // everyone's unresolved references -> rows this shard owns
         std::vector<uint32_t> hdr;
         if ((rc = read_headers(c, gathered, stride, hdr)) != WG_OK) return rc;
+        S.uoffs.assign(W + 1, 0);
         bool bad = false;
-        S.xoff.assign(W + 1, 0);
         for (int r = 0; r < W; r++) {
             bad |= hdr[4 * r] != 0;
-            S.xoff[r + 1] = S.xoff[r] + hdr[4 * r + 1];
+            S.uoffs[r + 1] = S.uoffs[r] + hdr[4 * r + 1];
         }
         if (bad) return sh_fallback(c, out);
-        const uint64_t nx = S.xoff[W];
-        WG_ALLOC(c, S.xall, nx * sizeof(WgXEnt) + 16);
+        const uint64_t L = S.uoffs[W];
+        WG_ALLOC(c, S.unres, L * 32 + 32);      // every rank's records, compacted
         for (int r = 0; r < W; r++)
             if (hdr[4 * r + 1])
-                WG_HIP(c, hipMemcpyAsync(S.xall.as<WgXEnt>() + S.xoff[r], (const uint8_t *)gathered + r * stride + 16,
-                                         hdr[4 * r + 1] * sizeof(WgXEnt), hipMemcpyDeviceToDevice, st));
+                WG_HIP(c, hipMemcpyAsync(S.unres.as<uint8_t>() + S.uoffs[r] * 32, (const uint8_t *)gathered + r * stride + 16,
+                                         (uint64_t)hdr[4 * r + 1] * 32, hipMemcpyDeviceToDevice, st));
+        S.step = SH_X2;
+        if ((rc = sh_send(c, L * 4, out)) != WG_OK) return rc;
+        if (L) hipLaunchKernelGGL(k_sh_probe_gathered, dim3(blocks(L)), dim3(T), 0, st, L, S.unres.as<const uint32_t>(),
+                                  c->d_oid, c->hash.as<const unsigned long long>(), c->hcap - 1, S.msg.as<int32_t>());
+        WG_HIP(c, hipGetLastError());
+        WG_HIP(c, hipStreamSynchronize(st));
+        return WG_OK;
+    }
+    case SH_X2: {   // rows of every unresolved reference -> crossing table; lanes up to the chain tokens
+        const uint64_t L = S.uoffs[W];
+        std::vector<uint64_t> dummy(W, 0);
+        Sections SF = make_sections(gathered, stride, W, dummy);
+        WG_ALLOC(c, S.xt, L * 4 + 16);         // row per record
+        WG_ALLOC(c, S.xtok, (L + 2) * 4);      // crossing flag -> position
+        WG_ALLOC(c, S.refx, El * 4 + 4);
+        WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(L + 2));
+        WG_HIP(c, hipMemsetAsync(S.xtok.p, 0, 8, st));
+        if (L) hipLaunchKernelGGL(k_sh_combine, dim3(blocks(L)), dim3(T), 0, st, SF, L, S.unres.as<const uint32_t>(),
+                                  S.xt.as<int32_t>(), S.xtok.as<uint32_t>(), S.flags.as<uint32_t>() + 4);
+        WG_HIP(c, wg_exclusive_scan_u32(S.xtok.as<uint32_t>(), S.xtok.as<uint32_t>(), L, c->scan_tmp.p, st));
+        std::vector<uint32_t> xb(W + 2, 0);
+        for (int r = 0; r <= W; r++)
+            WG_HIP(c, hipMemcpyAsync(&xb[r], S.xtok.as<uint32_t>() + S.uoffs[r], 4, hipMemcpyDeviceToHost, st));
+        WG_HIP(c, hipMemcpyAsync(&xb[W + 1], S.flags.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, st));
+        WG_HIP(c, hipStreamSynchronize(st));
+        if (xb[W + 1]) return sh_fallback(c, out);   // a parent at an earlier row: every rank sees it
+        S.xoff.assign(W + 1, 0);
+        for (int r = 0; r <= W; r++) S.xoff[r] = xb[r];
+        const uint64_t nx = S.xoff[W];
+        WG_ALLOC(c, S.xall, nx * sizeof(WgXEnt) + 16);
+        if (L) hipLaunchKernelGGL(k_sh_xbuild, dim3(blocks(L)), dim3(T), 0, st, L, S.unres.as<const uint32_t>(),
+                                  S.xt.as<const int32_t>(), S.xtok.as<const uint32_t>(), S.uoffs[S.rank], S.uoffs[S.rank + 1],
+                                  c->d_poff, S.E0, S.xall.as<WgXEnt>(), S.prow.as<int32_t>(), S.refx.as<uint32_t>());
         WG_ALLOC(c, S.isfb, El + 16);
         WG_ALLOC(c, S.xsec, El * 4 + 16);
         WG_HIP(c, hipMemsetAsync(S.isfb.p, 0, El + 16, st));
@@ -731,7 +740,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         S.nev_own = nev;
         S.naux_own = naux;
         const uint64_t nown = R.xown_end - R.xown_begin;
-        S.step = SH_X4;
+        S.step = SH_X3;
         if ((rc = sh_send(c, 16 + nown * 4, out)) != WG_OK) return rc;
         uint32_t h4[4] = {(uint32_t)nev, (uint32_t)naux, viol, 0};
         WG_HIP(c, hipMemcpyAsync(S.msg.p, h4, 16, hipMemcpyHostToDevice, st));
@@ -739,7 +748,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_HIP(c, hipStreamSynchronize(st));
         return WG_OK;
     }
-    case SH_X4: {   // global event ids; this shard's event records
+    case SH_X3: {   // global event ids; this shard's event records
         std::vector<uint32_t> hdr;
         if ((rc = read_headers(c, gathered, stride, hdr)) != WG_OK) return rc;
         S.evoff.assign(W + 1, 0);
@@ -764,7 +773,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_HIP(c, hipMemcpyAsync(S.dev_small.as<uint64_t>() + 32, S.evoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
         if (nx) hipLaunchKernelGGL(k_sh_resolve, dim3(1), dim3(1024), 0, st, nx, (uint32_t)W, S.dev_small.as<const uint64_t>(),
                                    S.dev_small.as<const uint64_t>() + 32, S.xtok.as<const uint32_t>(), S.xt.as<uint32_t>());
-        S.step = SH_X5;
+        S.step = SH_X4;
         const uint64_t nev = S.nev_own, naux = S.naux_own;
         if ((rc = sh_send(c, 16 + nev * 16 + naux * 4, out)) != WG_OK) return rc;
         uint32_t h5[4] = {(uint32_t)nev, (uint32_t)naux, 0, 0};
@@ -777,7 +786,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_HIP(c, hipStreamSynchronize(st));
         return WG_OK;
     }
-    case SH_X5: {   // replay the global event stream; lanes of own rows; default geometry
+    case SH_X4: {   // replay the global event stream; lanes of own rows; default geometry
         const uint64_t nev = S.evoff[W], naux = S.auxoff[W];
         DevBuf &evrec = c->lf[10], &aux = c->lf[18];
         WG_ALLOC(c, evrec, (nev + 256) * 16);

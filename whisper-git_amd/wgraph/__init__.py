@@ -159,10 +159,10 @@ class Engine:
 
     def _shard_loop(self, msg, comm):
         while not msg.done:
-            gathered, stride, sizes = comm.allgather(
-                int(msg.bytes), lambda dst: self._check(lib().wg_shard_copy_msg(self._ctx, dst)))
+            gathered, off, stride, sizes = comm.allgather(
+                int(msg.bytes), lambda dst: self._check(lib().wg_shard_copy_msg(self._ctx, dst)), step=int(msg.step))
             sz = (ctypes.c_uint64 * len(sizes))(*sizes)
-            self._check(lib().wg_shard_exchange(self._ctx, gathered.data_ptr(), stride, sz, ctypes.byref(msg)))
+            self._check(lib().wg_shard_exchange(self._ctx, gathered.data_ptr() + off, stride, sz, ctypes.byref(msg)))
             del gathered
 
     def layout_summary(self) -> abi.LayoutSummary:

@@ -19,49 +19,67 @@ def shard_rows(n: int, world: int, rank: int) -> tuple[int, int]:
 
 
 class ShardComm:
-    """Variable-length byte all-gather.
+    """Variable-length byte all-gather, one collective per exchange.
 
     device: the CUDA (HIP) device the engine runs on; the gathered buffer is
     always returned there.  With a gloo group the exchange itself runs on host
     tensors (copied in and out), with nccl it stays in HBM.
+
+    Every message travels in a slot of `cap + 16` bytes: a 16-byte header
+    holding its length, then the payload.  `cap` is remembered per exchange
+    point (the engine numbers them), so steady-state steps move each
+    message with ONE all-gather; a message longer than the slot makes every
+    rank (they all see the same lengths) repeat that exchange with a larger
+    slot.
     """
 
-    def __init__(self, device: torch.device, group=None):
+    HDR = 16
+
+    def __init__(self, device: torch.device, group=None, initial_cap: int = 4096):
         self.device = device
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.on_device = dist.get_backend(group) == "nccl"
+        self.initial_cap = initial_cap
+        self.caps: dict[int, int] = {}
         self.exchanges = 0
+        self.collectives = 0
         self.bytes_sent = 0
 
     @staticmethod
-    def layout(sizes: list[int]) -> int:
-        """Stride of the gathered buffer: the largest message, 16-byte aligned (>= 16)."""
-        m = max(max(sizes), 16)
+    def round_cap(n: int) -> int:
+        """Slot payload capacity for an n-byte message: 16-byte aligned, >= 16."""
+        m = max(n, 16)
         return (m + 15) // 16 * 16
 
-    def allgather(self, nbytes: int, fill):
+    def allgather(self, nbytes: int, fill, step: int = 0):
         """fill(ptr) writes this rank's nbytes-long message to ptr (device or
-        host memory).  Returns (gathered device tensor, stride, sizes)."""
+        host memory).  Returns (gathered device tensor, payload offset, stride,
+        sizes): rank r's message starts at offset + r * stride."""
         dev = self.device if self.on_device else torch.device("cpu")
-        n = torch.tensor([nbytes], dtype=torch.int64, device=dev)
-        ns = [torch.empty_like(n) for _ in range(self.world)]
-        dist.all_gather(ns, n, group=self.group)
-        sizes = [int(x.item()) for x in ns]
-        stride = self.layout(sizes)
-        send = torch.zeros(stride, dtype=torch.uint8, device=dev)
-        if nbytes:
-            fill(send.data_ptr())
-        out = torch.empty(self.world * stride, dtype=torch.uint8, device=dev)
-        if self.on_device:
-            dist.all_gather_into_tensor(out, send, group=self.group)
+        cap = self.caps.get(step, self.initial_cap)
+        while True:
+            stride = cap + self.HDR
+            send = torch.zeros(stride, dtype=torch.uint8, device=dev)
+            send[:8].view(torch.int64)[0] = nbytes
+            if nbytes and nbytes <= cap:
+                fill(send.data_ptr() + self.HDR)
+            out = torch.empty(self.world * stride, dtype=torch.uint8, device=dev)
+            if self.on_device:
+                dist.all_gather_into_tensor(out, send, group=self.group)
+            else:
+                dist.all_gather(list(out.view(self.world, stride).unbind(0)), send, group=self.group)
+            self.collectives += 1
+            sizes = [int(x) for x in out.view(self.world, stride)[:, :8].contiguous().view(torch.int64).view(-1).cpu()]
+            if max(sizes) <= cap:
+                break
+            cap = self.round_cap(max(sizes))
+        self.caps[step] = cap
+        if not self.on_device and self.device.type != "cpu":
+            out = out.to(self.device)
+        if self.device.type != "cpu":
             torch.cuda.current_stream(self.device).synchronize()
-        else:
-            dist.all_gather(list(out.view(self.world, stride).unbind(0)), send, group=self.group)
-            if self.device.type != "cpu":
-                out = out.to(self.device)
-                torch.cuda.synchronize(self.device)
         self.exchanges += 1
         self.bytes_sent += nbytes
-        return out, stride, sizes
+        return out, self.HDR, stride, sizes
