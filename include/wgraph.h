@@ -263,6 +263,42 @@ int wg_shard_copy_msg(wg_ctx *ctx, void *dst);
 int wg_shard_exchange(wg_ctx *ctx, const void *gathered, uint64_t stride, const uint64_t *sizes,
                       wg_shard_msg *out);
 
+/* ---- SDF font atlas (legacy TextRenderer atlas, docs/render_engine.md:105-112;
+ * frozen spec WG-SDF-1) -------------------------------------
+ * A TrueType font's characters [first_char, last_char] are rasterised at
+ * em_px pixels per em (4x4 samples per pixel, non-zero winding), shelf-packed
+ * into a width x height atlas with `spread` pixels of padding, and turned
+ * into an R8 signed distance field by a two-pass separable EDT on the GPU.
+ * Two slots: 0 = regular, 1 = bold (the legacy renderer's two instances). */
+#define WG_FONT_SLOTS 2
+typedef struct wg_atlas_params {
+    uint32_t width, height;   /* atlas size (width <= 4096)                  */
+    float    em_px;           /* pixels per em at atlas resolution          */
+    uint32_t spread;          /* SDF range / cell padding in pixels (1..60) */
+    uint32_t first_char, last_char;   /* e.g. 32, 126                        */
+} wg_atlas_params;
+typedef struct wg_glyph {     /* per character, atlas pixels (y down)       */
+    uint32_t codepoint;
+    float    advance;         /* advanceWidth * em_px / unitsPerEm          */
+    int32_t  bearing_x;       /* bitmap left relative to the pen            */
+    int32_t  bearing_top;     /* bitmap top above the baseline              */
+    uint32_t w, h;            /* bitmap size (0 for blank glyphs)           */
+    uint32_t atlas_x, atlas_y;/* cell origin; cell = (w, h) + 2 * spread    */
+} wg_glyph;
+typedef struct wg_atlas_info {
+    uint32_t width, height, spread, n_glyphs, n_edges;
+    uint32_t far_d2;          /* squared distances >= far_d2 mean "farther than 4*spread" */
+    float    em_px, ascent, descent, line_gap;
+    uint32_t first_char;
+} wg_atlas_info;
+int wg_font_atlas_build(wg_ctx *ctx, int slot, const uint8_t *ttf, uint64_t ttf_len, const wg_atlas_params *params);
+int wg_font_atlas_info(wg_ctx *ctx, int slot, wg_atlas_info *out);
+/* Any destination may be NULL: sdf/coverage width*height bytes (coverage =
+ * inside samples 0..16), d2_in/d2_out width*height squared distances,
+ * glyphs n_glyphs entries. */
+int wg_copy_font_atlas(wg_ctx *ctx, int slot, uint8_t *sdf, uint8_t *coverage, uint16_t *d2_in, uint16_t *d2_out,
+                       wg_glyph *glyphs);
+
 /* ---- timing (HIP events on the context's stream) ------------------------ */
 #define WG_STAGE_MAX 1024
 /* on = 0 disables; on > 0 enables and restarts the stage log (on > 1 also

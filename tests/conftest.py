@@ -18,7 +18,9 @@ def pytest_configure(config):
 
 
 def golden_names():
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+    """DAG goldens (tests/golden/make_golden.py); font_*.npz are SDF atlases."""
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
+                  if not os.path.basename(p).startswith("font_"))
 
 
 def load_golden(name):

@@ -77,6 +77,10 @@ void wg_destroy(wg_ctx *c) {
                     &S.xtok, &S.xt, &S.dev_small, &S.h_g, &S.rt_g, &S.band_host, &S.xchild, &S.xpar, &S.in_scan,
                     &S.edge_y, &S.own_edges};
     for (DevBuf *b : sb) b->release();
+    for (FontSlot &f : c->fonts) {
+        DevBuf *fb[] = {&f.edges, &f.gdesc, &f.cov, &f.sdf, &f.gin, &f.gout, &f.d2in, &f.d2out, &f.gtab};
+        for (DevBuf *b : fb) b->release();
+    }
     c->tile_first.release();
     for (int i = 0; i < WG_STAGE_MAX; i++) {
         if (c->stages[i].a) (void)hipEventDestroy(c->stages[i].a);

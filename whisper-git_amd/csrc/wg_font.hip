@@ -1,0 +1,487 @@
+// wg_font.hip — SDF font atlas (frozen spec WG-SDF-1 in
+// DESIGN.md §5b).
+//
+// The reference's legacy text path (docs/render_engine.md:105-131: Roboto
+// Regular/Bold, ASCII 32-126 rasterised by fontdue at 2x oversampling, a
+// custom EDT turning coverage into an R8 SDF atlas with per-glyph advance,
+// bearing and UV) is absent from the snapshot, and fontdue is not vendored,
+// so the engine freezes its own pipeline:
+//   host     TrueType parse (head/hhea/maxp/cmap fmt 4/hmtx/loca/glyf incl.
+//            offset composites), quadratic contours flattened into 8 lines
+//            each, scaled to atlas pixels, glyph cells shelf-packed
+//   k_font_coverage   one workgroup per glyph, edges in LDS: every cell pixel
+//            counts which of its 4x4 sample points lie inside the outline
+//            (non-zero winding) -> coverage 0..16; inside = coverage >= 8
+//   k_edt_cols        pass 1, one thread per column (coalesced rows): squared
+//            vertical distance to the nearest pixel of the other class
+//   k_edt_rows        pass 2, one workgroup per row staged in LDS: squared
+//            distance = min over q of g(q) + (x-q)^2, scanned outward with an
+//            early exit; exact for distances <= R = 4 * spread, "far" beyond
+//            (the SDF saturates at `spread`)
+//            -> SDF byte: 127.5 - (d_out - d_in) * 127.5 / spread, clamped
+// All arithmetic is integer or exact f32 (dyadic sample offsets, correctly
+// rounded division/sqrt), so the oracle (oracle/font_oracle.py, fontTools +
+// numpy) reproduces every byte; its EDT is pinned against scipy's exact EDT.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "wg_internal.h"
+
+namespace {
+
+constexpr int QUAD_STEPS = 8;          // lines per quadratic segment
+constexpr int COV_T = 256;
+constexpr int MAX_GLYPH_EDGES = 2048;  // edges staged in LDS (32 KiB); larger glyphs read them from HBM
+
+struct GlyphDesc {          // per glyph, device
+    uint32_t edge_off, n_edges;
+    int32_t bx0, by1;       // bitmap box: left x, top y (y up), atlas pixels
+    uint32_t cw, ch;        // cell size (bitmap + 2 * spread)
+    uint32_t ax, ay;        // cell origin in the atlas
+};
+
+// ---- pass 0: coverage -----------------------------------------------------------
+__global__ void __launch_bounds__(COV_T) k_font_coverage(const GlyphDesc *__restrict__ gd, const float4 *__restrict__ edges,
+                                                         uint32_t spread, uint32_t W, uint8_t *__restrict__ cov) {
+    __shared__ float4 se[MAX_GLYPH_EDGES];
+    const GlyphDesc g = gd[blockIdx.x];
+    const float4 *E = edges + g.edge_off;
+    const bool staged = g.n_edges <= (uint32_t)MAX_GLYPH_EDGES;
+    if (staged)
+        for (uint32_t i = threadIdx.x; i < g.n_edges; i += COV_T) se[i] = E[i];
+    __syncthreads();
+    if (staged) E = se;
+    const float off[4] = {0.125f, 0.375f, 0.625f, 0.875f};
+    const uint32_t npx = g.cw * g.ch;
+    for (uint32_t p = threadIdx.x; p < npx; p += COV_T) {
+        const uint32_t ci = p % g.cw, cj = p / g.cw;
+        const int32_t i = (int32_t)ci - (int32_t)spread, j = (int32_t)cj - (int32_t)spread;
+        const float px = (float)(g.bx0 + i), py = (float)(g.by1 - j);
+        int wind[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) wind[q] = 0;
+        for (uint32_t k = 0; k < g.n_edges; k++) {
+            const float4 e = E[k];   // (x0, y0, x1, y1), y up
+            const bool up = e.y < e.w;
+            const float ylo = up ? e.y : e.w, yhi = up ? e.w : e.y;
+            if (py - 0.125f < ylo || py - 0.875f >= yhi) continue;   // no sample row of this pixel in [ylo, yhi)
+#pragma unroll
+            for (int sy = 0; sy < 4; sy++) {
+                const float y = py - off[sy];
+                if (!(ylo <= y && y < yhi)) continue;
+                const float t = (y - e.y) / (e.w - e.y);
+                const float xi = e.x + t * (e.z - e.x);
+#pragma unroll
+                for (int sx = 0; sx < 4; sx++) {
+                    const float x = px + off[sx];
+                    if (xi > x) wind[sy * 4 + sx] += up ? 1 : -1;
+                }
+            }
+        }
+        uint32_t k = 0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) k += wind[q] != 0;
+        cov[(uint64_t)(g.ay + cj) * W + g.ax + ci] = (uint8_t)k;
+    }
+}
+
+// ---- pass 1: columns ---------------------------------------------------------------
+// gin[y][x]  = (vertical distance from an inside pixel to the nearest outside pixel)^2
+// gout[y][x] = (vertical distance from an outside pixel to the nearest inside pixel)^2
+// 0 on the pixel's own class; capped at (R + 1)^2
+__global__ void k_edt_cols(const uint8_t *__restrict__ cov, uint32_t W, uint32_t H, uint32_t R,
+                           uint16_t *__restrict__ gin, uint16_t *__restrict__ gout) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= W) return;
+    const uint32_t far = R + 1;
+    uint32_t din = far, dout = far;   // distance to the last outside / inside pixel above
+    for (uint32_t y = 0; y < H; y++) {
+        const bool in = cov[(uint64_t)y * W + x] >= 8;
+        din = in ? (din < far ? din + 1 : far) : 0;
+        dout = in ? 0 : (dout < far ? dout + 1 : far);
+        gin[(uint64_t)y * W + x] = (uint16_t)din;
+        gout[(uint64_t)y * W + x] = (uint16_t)dout;
+    }
+    din = far;
+    dout = far;
+    for (uint32_t yy = H; yy-- > 0;) {
+        const uint64_t o = (uint64_t)yy * W + x;
+        const bool in = cov[o] >= 8;
+        din = in ? (din < far ? din + 1 : far) : 0;
+        dout = in ? 0 : (dout < far ? dout + 1 : far);
+        const uint32_t a = gin[o] < din ? gin[o] : din, b = gout[o] < dout ? gout[o] : dout;
+        gin[o] = (uint16_t)(a * a);
+        gout[o] = (uint16_t)(b * b);
+    }
+}
+
+// ---- pass 2: rows -> squared distances and the SDF byte -------------------------------
+constexpr int ROW_T = 256;
+constexpr int ROW_MAX = 4096;
+
+__device__ __forceinline__ uint32_t row_min(const uint16_t *g, int32_t x, int32_t W, uint32_t R) {
+    const uint32_t cap = (R + 1) * (R + 1);
+    uint32_t best = g[x];
+    for (uint32_t o = 1; o <= R && o * o < best; o++) {
+        const uint32_t oo = o * o;
+        if (x - (int32_t)o >= 0) { const uint32_t v = g[x - o] + oo; best = v < best ? v : best; }
+        if (x + (int32_t)o < W) { const uint32_t v = g[x + o] + oo; best = v < best ? v : best; }
+    }
+    return best < cap ? best : cap;
+}
+
+__global__ void __launch_bounds__(ROW_T) k_edt_rows(const uint16_t *__restrict__ gin, const uint16_t *__restrict__ gout,
+                                                    uint32_t W, uint32_t R, float spread, uint16_t *__restrict__ d2in,
+                                                    uint16_t *__restrict__ d2out, uint8_t *__restrict__ sdf) {
+    __shared__ uint16_t si[ROW_MAX], so[ROW_MAX];
+    const uint64_t y = blockIdx.x;
+    for (uint32_t x = threadIdx.x; x < W; x += ROW_T) {
+        si[x] = gin[y * W + x];
+        so[x] = gout[y * W + x];
+    }
+    __syncthreads();
+    const float k = 127.5f / spread;
+    for (uint32_t x = threadIdx.x; x < W; x += ROW_T) {
+        const uint32_t a = row_min(si, (int32_t)x, (int32_t)W, R), b = row_min(so, (int32_t)x, (int32_t)W, R);
+        if (d2in) d2in[y * W + x] = (uint16_t)a;
+        if (d2out) d2out[y * W + x] = (uint16_t)b;
+        const float signed_d = sqrtf((float)b) - sqrtf((float)a);   // > 0 outside
+        float v = 127.5f - signed_d * k;
+        v = v < 0.0f ? 0.0f : (v > 255.0f ? 255.0f : v);
+        sdf[y * W + x] = (uint8_t)floorf(v + 0.5f);
+    }
+}
+
+// ---- TrueType (host) ---------------------------------------------------------------------
+struct Reader {
+    const uint8_t *p;
+    uint64_t n;
+    bool ok = true;
+    uint32_t u8(uint64_t o) { if (o + 1 > n) { ok = false; return 0; } return p[o]; }
+    uint32_t u16(uint64_t o) { if (o + 2 > n) { ok = false; return 0; } return (uint32_t)p[o] << 8 | p[o + 1]; }
+    int32_t i16(uint64_t o) { return (int16_t)u16(o); }
+    uint32_t u32(uint64_t o) { if (o + 4 > n) { ok = false; return 0; } return (uint32_t)p[o] << 24 | (uint32_t)p[o + 1] << 16 | (uint32_t)p[o + 2] << 8 | p[o + 3]; }
+};
+
+struct Font {
+    Reader r;
+    uint64_t head = 0, hhea = 0, maxp = 0, cmap = 0, hmtx = 0, loca = 0, glyf = 0;
+    uint64_t loca_len = 0, glyf_len = 0;
+    uint32_t upem = 0, nglyphs = 0, nhm = 0;
+    int32_t loca_fmt = 0, ascent = 0, descent = 0, line_gap = 0;
+    uint64_t cmap4 = 0;
+
+    bool open(const uint8_t *p, uint64_t n) {
+        r = Reader{p, n};
+        const uint32_t nt = r.u16(4);
+        for (uint32_t i = 0; i < nt; i++) {
+            const uint64_t rec = 12 + 16ull * i;
+            const uint32_t tag = r.u32(rec), off = r.u32(rec + 8), len = r.u32(rec + 12);
+            if ((uint64_t)off + len > n) return false;
+            switch (tag) {
+            case 0x68656164: head = off; break;                 // head
+            case 0x68686561: hhea = off; break;                 // hhea
+            case 0x6D617870: maxp = off; break;                 // maxp
+            case 0x636D6170: cmap = off; break;                 // cmap
+            case 0x686D7478: hmtx = off; break;                 // hmtx
+            case 0x6C6F6361: loca = off; loca_len = len; break; // loca
+            case 0x676C7966: glyf = off; glyf_len = len; break; // glyf
+            default: break;
+            }
+        }
+        if (!head || !hhea || !maxp || !cmap || !hmtx || !loca || !glyf) return false;
+        upem = r.u16(head + 18);
+        loca_fmt = r.i16(head + 50);
+        nglyphs = r.u16(maxp + 4);
+        ascent = r.i16(hhea + 4);
+        descent = r.i16(hhea + 6);
+        line_gap = r.i16(hhea + 8);
+        nhm = r.u16(hhea + 34);
+        const uint32_t ns = r.u16(cmap + 2);
+        for (uint32_t i = 0; i < ns && !cmap4; i++) {
+            const uint32_t pid = r.u16(cmap + 4 + 8 * i), eid = r.u16(cmap + 6 + 8 * i), off = r.u32(cmap + 8 + 8 * i);
+            if (((pid == 3 && eid == 1) || pid == 0) && r.u16(cmap + off) == 4) cmap4 = cmap + off;
+        }
+        return r.ok && upem && cmap4 && nhm;
+    }
+    uint32_t glyph_index(uint32_t c) {
+        const uint32_t segx2 = r.u16(cmap4 + 6);
+        const uint64_t ends = cmap4 + 14, starts = ends + segx2 + 2, deltas = starts + segx2, ranges = deltas + segx2;
+        for (uint32_t s = 0; s < segx2 / 2; s++) {
+            if (r.u16(ends + 2 * s) < c) continue;
+            const uint32_t st = r.u16(starts + 2 * s);
+            if (st > c) return 0;
+            const uint32_t delta = r.u16(deltas + 2 * s), ro = r.u16(ranges + 2 * s);
+            if (ro == 0) return (c + delta) & 0xFFFF;
+            const uint32_t g = r.u16(ranges + 2 * s + ro + 2 * (c - st));
+            return g ? (g + delta) & 0xFFFF : 0;
+        }
+        return 0;
+    }
+    uint32_t advance(uint32_t g) { return r.u16(hmtx + 4ull * (g < nhm ? g : nhm - 1)); }
+    bool glyph_range(uint32_t g, uint64_t *off, uint64_t *len) {
+        if (g >= nglyphs) return false;
+        uint64_t a, b;
+        if (loca_fmt == 0) { a = 2ull * r.u16(loca + 2ull * g); b = 2ull * r.u16(loca + 2ull * g + 2); }
+        else { a = r.u32(loca + 4ull * g); b = r.u32(loca + 4ull * g + 4); }
+        if (b < a || b > glyf_len) return false;
+        *off = glyf + a;
+        *len = b - a;
+        return true;
+    }
+
+    struct Pt { float x, y; bool on; };
+    // contours of glyph g (font units), composites resolved with integer offsets
+    bool outline(uint32_t g, std::vector<std::vector<Pt>> &cs, int depth = 0) {
+        uint64_t o, len;
+        if (!glyph_range(g, &o, &len)) return false;
+        if (len == 0) return true;
+        const int32_t nc = r.i16(o);
+        if (nc >= 0) {
+            std::vector<uint32_t> endp(nc);
+            for (int32_t i = 0; i < nc; i++) endp[i] = r.u16(o + 10 + 2ull * i);
+            const uint32_t np = nc ? endp[nc - 1] + 1 : 0;
+            uint64_t q = o + 10 + 2ull * nc;
+            q += 2 + r.u16(q);   // instructions
+            std::vector<uint8_t> fl(np);
+            for (uint32_t i = 0; i < np;) {
+                const uint8_t f = (uint8_t)r.u8(q++);
+                fl[i++] = f;
+                if (f & 8) { uint32_t rep = r.u8(q++); while (rep-- && i < np) fl[i++] = f; }
+            }
+            std::vector<int32_t> xs(np), ys(np);
+            int32_t v = 0;
+            for (uint32_t i = 0; i < np; i++) {
+                const uint8_t f = fl[i];
+                if (f & 2) { const int32_t d = (int32_t)r.u8(q++); v += (f & 16) ? d : -d; }
+                else if (!(f & 16)) { v += r.i16(q); q += 2; }
+                xs[i] = v;
+            }
+            v = 0;
+            for (uint32_t i = 0; i < np; i++) {
+                const uint8_t f = fl[i];
+                if (f & 4) { const int32_t d = (int32_t)r.u8(q++); v += (f & 32) ? d : -d; }
+                else if (!(f & 32)) { v += r.i16(q); q += 2; }
+                ys[i] = v;
+            }
+            uint32_t a = 0;
+            for (int32_t cI = 0; cI < nc; cI++) {
+                std::vector<Pt> c;
+                for (uint32_t i = a; i <= endp[cI] && i < np; i++) c.push_back(Pt{(float)xs[i], (float)ys[i], (fl[i] & 1) != 0});
+                a = endp[cI] + 1;
+                if (!c.empty()) cs.push_back(c);
+            }
+            return r.ok;
+        }
+        if (depth > 4) return false;
+        uint64_t q = o + 10;
+        for (;;) {
+            const uint32_t f = r.u16(q), gi = r.u16(q + 2);
+            q += 4;
+            int32_t dx, dy;
+            if (f & 1) { dx = r.i16(q); dy = r.i16(q + 2); q += 4; }
+            else { dx = (int8_t)r.u8(q); dy = (int8_t)r.u8(q + 1); q += 2; }
+            if (!(f & 2)) return false;                          // point-matched components: unsupported
+            if (f & (0x8 | 0x40 | 0x80)) return false;           // scaled components: unsupported
+            std::vector<std::vector<Pt>> sub;
+            if (!outline(gi, sub, depth + 1)) return false;
+            for (auto &c : sub) {
+                for (auto &p : c) { p.x += (float)dx; p.y += (float)dy; }
+                cs.push_back(c);
+            }
+            if (!(f & 0x20)) break;
+        }
+        return r.ok;
+    }
+};
+
+// contour -> lines (WG-SDF-1): on/off points, implied midpoints, quadratics in 8 steps
+void flatten(const std::vector<Font::Pt> &c, float scale, std::vector<float4> &out) {
+    const size_t n = c.size();
+    if (n < 2) return;
+    size_t s = 0;
+    while (s < n && !c[s].on) s++;
+    Font::Pt start;
+    if (s == n) start = Font::Pt{(c[0].x + c[1].x) * 0.5f, (c[0].y + c[1].y) * 0.5f, true};   // all off-curve
+    else start = c[s];
+    std::vector<float2> pts;   // flattened, font units
+    pts.push_back(make_float2(start.x, start.y));
+    Font::Pt cur = start;
+    bool have_ctrl = false;
+    Font::Pt ctrl{};
+    auto quad = [&](Font::Pt p0, Font::Pt cc, Font::Pt p1) {
+        for (int k = 1; k <= QUAD_STEPS; k++) {
+            const float t = (float)k * (1.0f / QUAD_STEPS);
+            const float mt = 1.0f - t;
+            const float a = mt * mt, b = 2.0f * mt * t, d = t * t;
+            pts.push_back(make_float2(a * p0.x + b * cc.x + d * p1.x, a * p0.y + b * cc.y + d * p1.y));
+        }
+    };
+    const size_t first = (s == n) ? 1 : s + 1;
+    for (size_t m = 0; m < n; m++) {
+        const Font::Pt p = c[(first + m) % n];
+        if (s != n && (first + m) % n == s) {   // back at the start point: close below
+            break;
+        }
+        if (p.on) {
+            if (have_ctrl) { quad(cur, ctrl, p); have_ctrl = false; }
+            else pts.push_back(make_float2(p.x, p.y));
+            cur = p;
+        } else {
+            if (have_ctrl) {
+                const Font::Pt mid{(ctrl.x + p.x) * 0.5f, (ctrl.y + p.y) * 0.5f, true};
+                quad(cur, ctrl, mid);
+                cur = mid;
+            }
+            ctrl = p;
+            have_ctrl = true;
+        }
+    }
+    if (have_ctrl) quad(cur, ctrl, start);
+    else pts.push_back(make_float2(start.x, start.y));
+    for (size_t i = 0; i + 1 < pts.size(); i++) {
+        const float x0 = pts[i].x * scale, y0 = pts[i].y * scale, x1 = pts[i + 1].x * scale, y1 = pts[i + 1].y * scale;
+        if (y0 == y1) continue;    // horizontal lines never cross a sample row
+        out.push_back(make_float4(x0, y0, x1, y1));
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int wg_font_atlas_build(wg_ctx *c, int slot, const uint8_t *ttf, uint64_t len, const wg_atlas_params *prm) {
+    if (!c || !ttf || !prm || slot < 0 || slot >= WG_FONT_SLOTS) return WG_E_INVALID;
+    const uint32_t W = prm->width, H = prm->height, spread = prm->spread;
+    if (W == 0 || H == 0 || W > ROW_MAX || spread == 0 || spread > 60 || !(prm->em_px > 0.0f) ||
+        prm->first_char > prm->last_char || prm->last_char > 0xFFFF)
+        return wg_fail(c, WG_E_INVALID, "bad atlas parameters");
+    (void)hipSetDevice(c->device);
+    Font f;
+    if (!f.open(ttf, len)) return wg_fail(c, WG_E_INVALID, "not a TrueType font with cmap format 4");
+    FontSlot &S = c->fonts[slot];
+    S.built = false;
+    const float scale = prm->em_px / (float)f.upem;
+    std::vector<float4> edges;
+    std::vector<GlyphDesc> gd;
+    S.glyphs.clear();
+    uint32_t cx = 0, cy = 0, row_h = 0;
+    for (uint32_t ch = prm->first_char; ch <= prm->last_char; ch++) {
+        const uint32_t g = f.glyph_index(ch);
+        wg_glyph m{};
+        m.codepoint = ch;
+        m.advance = (float)f.advance(g) * scale;
+        std::vector<std::vector<Font::Pt>> cs;
+        if (!f.outline(g, cs)) return wg_fail(c, WG_E_UNSUPPORTED, "glyph %u (U+%04X) outline not supported", g, ch);
+        uint64_t go, gl;
+        f.glyph_range(g, &go, &gl);
+        if (gl > 0 && !cs.empty()) {
+            const float xmin = (float)f.r.i16(go + 2), ymin = (float)f.r.i16(go + 4);
+            const float xmax = (float)f.r.i16(go + 6), ymax = (float)f.r.i16(go + 8);
+            const int32_t bx0 = (int32_t)floorf(xmin * scale), bx1 = (int32_t)ceilf(xmax * scale);
+            const int32_t by0 = (int32_t)floorf(ymin * scale), by1 = (int32_t)ceilf(ymax * scale);
+            m.bearing_x = bx0;
+            m.bearing_top = by1;
+            m.w = (uint32_t)(bx1 - bx0);
+            m.h = (uint32_t)(by1 - by0);
+            const uint32_t cw = m.w + 2 * spread, chh = m.h + 2 * spread;
+            if (cx + cw > W) { cx = 0; cy += row_h; row_h = 0; }
+            if (cw > W || cy + chh > H) return wg_fail(c, WG_E_UNSUPPORTED, "atlas %ux%u too small at em %.1f px", W, H, prm->em_px);
+            m.atlas_x = cx;
+            m.atlas_y = cy;
+            GlyphDesc d;
+            d.edge_off = (uint32_t)edges.size();
+            for (auto &cc : cs) flatten(cc, scale, edges);
+            d.n_edges = (uint32_t)edges.size() - d.edge_off;
+            d.bx0 = bx0;
+            d.by1 = by1;
+            d.cw = cw;
+            d.ch = chh;
+            d.ax = cx;
+            d.ay = cy;
+            gd.push_back(d);
+            cx += cw;
+            row_h = chh > row_h ? chh : row_h;
+        }
+        S.glyphs.push_back(m);
+    }
+    S.W = W;
+    S.H = H;
+    S.spread = spread;
+    S.em_px = prm->em_px;
+    S.R = 4 * spread;
+    S.ascent = (float)f.ascent * scale;
+    S.descent = (float)f.descent * scale;
+    S.line_gap = (float)f.line_gap * scale;
+    S.n_edges = edges.size();
+    S.first_char = prm->first_char;
+    hipStream_t s = c->stream;
+    const uint64_t npx = (uint64_t)W * H;
+    WG_ALLOC(c, S.edges, edges.size() * sizeof(float4) + 16);
+    WG_ALLOC(c, S.gdesc, gd.size() * sizeof(GlyphDesc) + 16);
+    WG_ALLOC(c, S.cov, npx);
+    WG_ALLOC(c, S.sdf, npx);
+    WG_ALLOC(c, S.gin, npx * 2);
+    WG_ALLOC(c, S.gout, npx * 2);
+    WG_ALLOC(c, S.d2in, npx * 2);
+    WG_ALLOC(c, S.d2out, npx * 2);
+    WG_ALLOC(c, S.gtab, S.glyphs.size() * sizeof(wg_glyph) + 16);
+    if (!edges.empty()) WG_HIP(c, hipMemcpyAsync(S.edges.p, edges.data(), edges.size() * sizeof(float4), hipMemcpyHostToDevice, s));
+    if (!gd.empty()) WG_HIP(c, hipMemcpyAsync(S.gdesc.p, gd.data(), gd.size() * sizeof(GlyphDesc), hipMemcpyHostToDevice, s));
+    WG_HIP(c, hipMemcpyAsync(S.gtab.p, S.glyphs.data(), S.glyphs.size() * sizeof(wg_glyph), hipMemcpyHostToDevice, s));
+    wg_stage_begin(c, "font_atlas");
+    wg_stage_begin(c, "font_coverage");
+    WG_HIP(c, hipMemsetAsync(S.cov.p, 0, npx, s));
+    if (!gd.empty())
+        hipLaunchKernelGGL(k_font_coverage, dim3((uint32_t)gd.size()), dim3(COV_T), 0, s, S.gdesc.as<const GlyphDesc>(),
+                           S.edges.as<const float4>(), spread, W, S.cov.as<uint8_t>());
+    wg_stage_end(c);
+    wg_stage_begin(c, "font_edt");
+    hipLaunchKernelGGL(k_edt_cols, dim3((W + 255) / 256), dim3(256), 0, s, S.cov.as<const uint8_t>(), W, H, S.R,
+                       S.gin.as<uint16_t>(), S.gout.as<uint16_t>());
+    hipLaunchKernelGGL(k_edt_rows, dim3(H), dim3(ROW_T), 0, s, S.gin.as<const uint16_t>(), S.gout.as<const uint16_t>(), W,
+                       S.R, (float)spread, S.d2in.as<uint16_t>(), S.d2out.as<uint16_t>(), S.sdf.as<uint8_t>());
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    wg_stage_end(c);
+    WG_HIP(c, hipStreamSynchronize(s));
+    S.built = true;
+    return WG_OK;
+}
+
+int wg_font_atlas_info(wg_ctx *c, int slot, wg_atlas_info *out) {
+    if (!c || !out || slot < 0 || slot >= WG_FONT_SLOTS) return WG_E_INVALID;
+    const FontSlot &S = c->fonts[slot];
+    if (!S.built) return wg_fail(c, WG_E_STATE, "font slot %d not built", slot);
+    out->width = S.W;
+    out->height = S.H;
+    out->spread = S.spread;
+    out->n_glyphs = (uint32_t)S.glyphs.size();
+    out->n_edges = (uint32_t)S.n_edges;
+    out->far_d2 = (S.R + 1) * (S.R + 1);
+    out->em_px = S.em_px;
+    out->ascent = S.ascent;
+    out->descent = S.descent;
+    out->line_gap = S.line_gap;
+    out->first_char = S.first_char;
+    return WG_OK;
+}
+
+int wg_copy_font_atlas(wg_ctx *c, int slot, uint8_t *sdf, uint8_t *coverage, uint16_t *d2_in, uint16_t *d2_out,
+                       wg_glyph *glyphs) {
+    if (!c || slot < 0 || slot >= WG_FONT_SLOTS) return WG_E_INVALID;
+    FontSlot &S = c->fonts[slot];
+    if (!S.built) return wg_fail(c, WG_E_STATE, "font slot %d not built", slot);
+    const uint64_t npx = (uint64_t)S.W * S.H;
+    hipStream_t s = c->stream;
+    if (sdf) WG_HIP(c, hipMemcpyAsync(sdf, S.sdf.p, npx, hipMemcpyDeviceToHost, s));
+    if (coverage) WG_HIP(c, hipMemcpyAsync(coverage, S.cov.p, npx, hipMemcpyDeviceToHost, s));
+    if (d2_in) WG_HIP(c, hipMemcpyAsync(d2_in, S.d2in.p, npx * 2, hipMemcpyDeviceToHost, s));
+    if (d2_out) WG_HIP(c, hipMemcpyAsync(d2_out, S.d2out.p, npx * 2, hipMemcpyDeviceToHost, s));
+    WG_HIP(c, hipStreamSynchronize(s));
+    if (glyphs) std::memcpy(glyphs, S.glyphs.data(), S.glyphs.size() * sizeof(wg_glyph));
+    return WG_OK;
+}
+
+}  // extern "C"

@@ -102,6 +102,16 @@ struct ShardState {
     uint64_t n_own_edges = 0;
 };
 
+// SDF font atlas slot (wg_font.hip)
+struct FontSlot {
+    bool built = false;
+    uint32_t W = 0, H = 0, spread = 0, R = 0, first_char = 0;
+    uint64_t n_edges = 0;
+    float em_px = 0, ascent = 0, descent = 0, line_gap = 0;
+    std::vector<wg_glyph> glyphs;
+    DevBuf edges, gdesc, cov, sdf, gin, gout, d2in, d2out, gtab;
+};
+
 struct wg_ctx {
     int         device = 0;
     hipStream_t stream = nullptr;
@@ -177,6 +187,7 @@ struct wg_ctx {
     // ---- host-side tables --------------------------------------------------------
     uint32_t h_thresh[32];  // delta thresholds for heights 29..56
     ShardState sh;
+    FontSlot fonts[WG_FONT_SLOTS];
     // ---- timing ----------------------------------------------------------------------
     bool       timing = false;
     StageTimer stages[WG_STAGE_MAX];

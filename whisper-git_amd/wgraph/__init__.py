@@ -65,6 +65,9 @@ def lib():
             "wg_debug_counters": ([vp, vp, ctypes.c_int], ctypes.c_int),
             "wg_stage_timings": ([vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
                                   ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+            "wg_font_atlas_build": ([vp, ctypes.c_int, vp, u64, ctypes.POINTER(abi.AtlasParams)], ctypes.c_int),
+            "wg_font_atlas_info": ([vp, ctypes.c_int, ctypes.POINTER(abi.AtlasInfo)], ctypes.c_int),
+            "wg_copy_font_atlas": ([vp, ctypes.c_int, vp, vp, vp, vp, vp], ctypes.c_int),
             "wg_shard_build_begin": ([vp, ctypes.POINTER(abi.Commits), ctypes.c_int, ctypes.c_int, u64, u64,
                                       ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_geometry_begin": ([vp, vp, i32, ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
@@ -86,7 +89,10 @@ EXPORTED_SYMBOLS = (
     "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
-    "wg_shard_copy_msg", "wg_shard_exchange")
+    "wg_shard_copy_msg", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas")
+
+FONT_DIR = os.path.join(os.path.dirname(_HERE), "fonts")
+FONTS = {0: os.path.join(FONT_DIR, "Roboto-Regular.ttf"), 1: os.path.join(FONT_DIR, "Roboto-Bold.ttf")}
 
 
 class Engine:
@@ -251,6 +257,31 @@ class Engine:
         v = abi.DeviceViews()
         self._check(lib().wg_device_views_get(self._ctx, ctypes.byref(v)))
         return v
+
+    # -- SDF font atlas (WG-SDF-1) ----------------------------------------------------------
+    def build_font_atlas(self, slot: int, ttf=None, width=1024, height=1024, em_px=96.0, spread=8, first=32, last=126):
+        """Rasterise + EDT a TrueType font into atlas slot (0 regular, 1 bold)."""
+        if ttf is None:
+            ttf = FONTS[slot]
+        data = open(ttf, "rb").read() if isinstance(ttf, str) else bytes(ttf)
+        buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+        p = abi.AtlasParams(width, height, em_px, spread, first, last)
+        self._check(lib().wg_font_atlas_build(self._ctx, slot, buf, len(data), ctypes.byref(p)))
+
+    def atlas_info(self, slot: int) -> abi.AtlasInfo:
+        i = abi.AtlasInfo()
+        self._check(lib().wg_font_atlas_info(self._ctx, slot, ctypes.byref(i)))
+        return i
+
+    def atlas(self, slot: int) -> dict:
+        i = self.atlas_info(slot)
+        shape = (i.height, i.width)
+        out = dict(sdf=np.empty(shape, np.uint8), cov=np.empty(shape, np.uint8), d2in=np.empty(shape, np.uint16),
+                   d2out=np.empty(shape, np.uint16), glyphs=np.empty(i.n_glyphs, abi.GLYPH_DTYPE))
+        self._check(lib().wg_copy_font_atlas(self._ctx, slot, out["sdf"].ctypes.data, out["cov"].ctypes.data,
+                                             out["d2in"].ctypes.data, out["d2out"].ctypes.data,
+                                             out["glyphs"].ctypes.data))
+        return out
 
     # -- timing ----------------------------------------------------------------------------
     def debug_counters(self) -> np.ndarray:

@@ -36,6 +36,24 @@ class LayoutSummary(ctypes.Structure):
                 ("row_begin", ctypes.c_uint64)]
 
 
+class AtlasParams(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("em_px", ctypes.c_float),
+                ("spread", ctypes.c_uint32), ("first_char", ctypes.c_uint32), ("last_char", ctypes.c_uint32)]
+
+
+class AtlasInfo(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("spread", ctypes.c_uint32),
+                ("n_glyphs", ctypes.c_uint32), ("n_edges", ctypes.c_uint32), ("far_d2", ctypes.c_uint32),
+                ("em_px", ctypes.c_float), ("ascent", ctypes.c_float), ("descent", ctypes.c_float),
+                ("line_gap", ctypes.c_float), ("first_char", ctypes.c_uint32)]
+
+
+GLYPH_DTYPE = np.dtype([("codepoint", "<u4"), ("advance", "<f4"), ("bearing_x", "<i4"), ("bearing_top", "<i4"),
+                        ("w", "<u4"), ("h", "<u4"), ("atlas_x", "<u4"), ("atlas_y", "<u4")])
+# WG-SDF-1 defaults: Roboto at 96 px/em (48 px text at 2x oversampling), 8 px spread, ASCII 32..126
+ATLAS_DEFAULTS = dict(width=1024, height=1024, em_px=96.0, spread=8, first=32, last=126)
+
+
 class ShardMsg(ctypes.Structure):
     _fields_ = [("send", ctypes.c_void_p), ("bytes", ctypes.c_uint64), ("done", ctypes.c_int32),
                 ("step", ctypes.c_int32)]
