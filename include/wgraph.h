@@ -299,6 +299,38 @@ int wg_font_atlas_info(wg_ctx *ctx, int slot, wg_atlas_info *out);
 int wg_copy_font_atlas(wg_ctx *ctx, int slot, uint8_t *sdf, uint8_t *coverage, uint16_t *d2_in, uint16_t *d2_out,
                        wg_glyph *glyphs);
 
+/* ---- SDF glyph quads (legacy TextRenderer::layout_text, docs/render_engine.md:113-131;
+ * frozen spec WG-TEXT-1) ----------------------------------
+ * Per row of the current geometry, three runs on one baseline
+ * (node_y + baseline_dy, row-local y like the SplineVertex buffers):
+ *   short SHA (first 7 hex digits of the id, git/mod.rs:300; none for
+ *   synthetic rows) at sha_x; summary (bytes; "(no summary)" when empty,
+ *   commit_graph.rs:1003-1007) at summary_x, clipped at summary_max_x;
+ *   relative time (format_relative_time(now, time), git/mod.rs:34-49)
+ *   right-aligned at time_right_x.
+ * Each visible glyph is one quad = 6 TextVertex, pen advanced in f32 in
+ * reading order; bytes outside the atlas range draw as '?'.              */
+typedef struct wg_text_vertex { float x, y, u, v, r, g, b, a; } wg_text_vertex;
+typedef struct wg_text_params {
+    int32_t slot;             /* font atlas slot                            */
+    float   text_px;          /* font size in pixels                        */
+    float   sha_x, summary_x, summary_max_x, time_right_x, baseline_dy;
+    int64_t now;              /* unix seconds ("now" of the relative times) */
+    float   color_sha[4], color_summary[4], color_time[4];
+} wg_text_params;
+typedef struct wg_glyph_summary {
+    uint64_t row_begin, row_end, n_quads, n_vertices;
+    uint64_t checksum;        /* same definition as wg_vertex_summary      */
+} wg_glyph_summary;
+/* summary_off: [N+1] byte offsets of every row's summary (NULL: all empty);
+ * rows [row_begin, row_end) of the current geometry (global numbering).  */
+int wg_emit_glyphs(wg_ctx *ctx, uint64_t row_begin, uint64_t row_end, const uint8_t *summary,
+                   const uint64_t *summary_off, int32_t residency, const wg_text_params *params);
+int wg_glyph_summary_get(wg_ctx *ctx, wg_glyph_summary *out);
+int wg_copy_glyph_vertices(wg_ctx *ctx, uint64_t first, uint64_t count, wg_text_vertex *dst);
+/* per-row first quad (row_end-row_begin+1 entries) */
+int wg_copy_glyph_offsets(wg_ctx *ctx, uint64_t *dst);
+
 /* ---- timing (HIP events on the context's stream) ------------------------ */
 #define WG_STAGE_MAX 1024
 /* on = 0 disables; on > 0 enables and restarts the stage log (on > 1 also

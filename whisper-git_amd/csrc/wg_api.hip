@@ -77,6 +77,8 @@ void wg_destroy(wg_ctx *c) {
                     &S.xtok, &S.xt, &S.dev_small, &S.h_g, &S.rt_g, &S.band_host, &S.xchild, &S.xpar, &S.in_scan,
                     &S.edge_y, &S.own_edges};
     for (DevBuf *b : sb) b->release();
+    DevBuf *tb[] = {&c->text_sum, &c->text_sum_off, &c->text_off, &c->text_rec, &c->text_vtx};
+    for (DevBuf *b : tb) b->release();
     for (FontSlot &f : c->fonts) {
         DevBuf *fb[] = {&f.edges, &f.gdesc, &f.cov, &f.sdf, &f.gin, &f.gout, &f.d2in, &f.d2out, &f.gtab};
         for (DevBuf *b : fb) b->release();
@@ -131,7 +133,7 @@ int wg_synchronize(wg_ctx *c) {
 int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     if (!c || !in) return WG_E_INVALID;
     (void)hipSetDevice(c->device);
-    c->have_layout = c->have_geom = c->have_vtx = false;
+    c->have_layout = c->have_geom = c->have_vtx = c->have_text = false;
     c->sh.on = false;
     c->sh.step = 0;
     c->edge_y = nullptr;
@@ -273,7 +275,7 @@ int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
     if (c->sh.on && !c->sh.replicated) return wg_fail(c, WG_E_STATE, "sharded layout: use wg_shard_geometry_begin");
     (void)hipSetDevice(c->device);
-    c->have_geom = c->have_vtx = false;
+    c->have_geom = c->have_vtx = c->have_text = false;
     const float *d_band = nullptr;
     if (band) {
         if (residency == WG_HOST) {

@@ -188,6 +188,10 @@ struct wg_ctx {
     uint32_t h_thresh[32];  // delta thresholds for heights 29..56
     ShardState sh;
     FontSlot fonts[WG_FONT_SLOTS];
+    // ---- glyph quads (wg_text.hip) ------------------------------------------------
+    bool     have_text = false;
+    uint64_t text_rb = 0, text_re = 0, n_quads = 0;
+    DevBuf text_sum, text_sum_off, text_off, text_rec, text_vtx;
     // ---- timing ----------------------------------------------------------------------
     bool       timing = false;
     StageTimer stages[WG_STAGE_MAX];
@@ -249,4 +253,5 @@ int wg_stage_rowtop(wg_ctx *c, const float *d_band);   // wg_rowtop.hip
 int wg_stage_geometry(wg_ctx *c, const float *d_band); // wg_geom.hip
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel);  // wg_vertex.hip
 int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out);  // wg_vertex.hip
+int wg_words_checksum(wg_ctx *c, const uint32_t *w, uint64_t nwords, uint64_t *out);  // wg_vertex.hip
 void wg_init_height_thresholds(uint32_t *th);  // wg_rowtop.hip

@@ -586,7 +586,7 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     S.e = row_end;
     S.Etot = in->n_parents;
     S.row_base = 1;
-    c->have_layout = c->have_geom = c->have_vtx = false;
+    c->have_layout = c->have_geom = c->have_vtx = c->have_text = false;
     c->edge_y = nullptr;
     c->d_oid = in->oid;
     c->d_time = in->time;
@@ -841,7 +841,7 @@ int wg_shard_geometry_begin(wg_ctx *c, const float *band, int32_t residency, wg_
     if (!S.on || !c->have_layout) return wg_fail(c, WG_E_STATE, "no sharded layout built");
     if (S.step != SH_IDLE) return wg_fail(c, WG_E_STATE, "a sharded call is in progress");
     (void)hipSetDevice(c->device);
-    c->have_vtx = false;
+    c->have_vtx = c->have_text = false;
     const float *d_band = nullptr;
     if (band) {
         if (residency == WG_HOST) {

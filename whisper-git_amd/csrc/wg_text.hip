@@ -1,0 +1,325 @@
+// wg_text.hip — per-row SDF glyph quads (frozen spec
+// WG-TEXT-1 in DESIGN.md §5c).
+//
+// The reference lays a commit row out as short SHA (mono, muted), avatar,
+// summary ("(no summary)" when empty, ellipsised) and, right-aligned, the
+// relative time (commit_graph.rs:1002-1130; short_id = first 7 hex digits of
+// the id, git/mod.rs:300; format_relative_time, git/mod.rs:34-49, which reads
+// the clock — the engine takes `now` as an input).  The legacy TextRenderer
+// turned each character into one textured quad of 6 TextVertex
+// {position, tex_coord, color} (docs/render_engine.md:113-131), absent from
+// the snapshot.  WG-TEXT-1 freezes that layout on top of the WG-SDF-1 atlas.
+//
+// Two kernels:
+//   k_text_rows    one thread per row: builds the three runs (hex digits,
+//                  summary bytes, relative-time text), advances the pen
+//                  sequentially in f32 (the order a CPU layout loop uses),
+//                  clips the summary at summary_max_x and writes one 16-byte
+//                  record per visible glyph {pen x, baseline, glyph, run}
+//   k_text_quads   one thread per glyph record: 6 TextVertex (192 B) staged
+//                  per wave in LDS and written as contiguous 1 KiB stores
+// Rows are counted first (same walk, counts only) so every record has a
+// fixed slot.
+#include "wg_internal.h"
+
+namespace {
+
+constexpr int T = 256;
+inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
+
+struct TextArgs {
+    uint64_t rb, re;                 // rows
+    const uint8_t *oid;
+    const int64_t *time;
+    const uint8_t *flags;
+    const uint8_t *sum;              // summary bytes
+    const uint64_t *sum_off;         // [N + 1] (global rows)
+    const float *node_y;             // row arrays of the current geometry (context indexing)
+    uint64_t row_base;               // context index of global row `rb` minus rb
+    const wg_glyph *glyphs;
+    uint32_t first_char, n_glyphs;
+    float scale;                     // text_px / em_px
+    float sha_x, summary_x, summary_max_x, time_right_x, baseline_dy;
+    int64_t now;
+};
+
+// format_relative_time (git/mod.rs:34-49) into buf, returns the length
+__device__ __forceinline__ uint32_t relative_time(int64_t now, int64_t t, char *buf) {
+    int64_t d = now - t;
+    if (d < 0) d = 0;
+    if (d < 60) {
+        const char *s = "just now";
+        for (int i = 0; i < 8; i++) buf[i] = s[i];
+        return 8;
+    }
+    int64_t v;
+    const char *unit;
+    uint32_t ul;
+    if (d < 3600) { v = d / 60; unit = "m"; ul = 1; }
+    else if (d < 86400) { v = d / 3600; unit = "h"; ul = 1; }
+    else if (d < 604800) { v = d / 86400; unit = "d"; ul = 1; }
+    else if (d < 2592000) { v = d / 604800; unit = "w"; ul = 1; }
+    else if (d < 31536000) { v = d / 2592000; unit = "mo"; ul = 2; }
+    else { v = d / 31536000; unit = "y"; ul = 1; }
+    char tmp[20];
+    uint32_t n = 0;
+    do { tmp[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    uint32_t len = 0;
+    while (n) buf[len++] = tmp[--n];
+    for (uint32_t i = 0; i < ul; i++) buf[len++] = unit[i];
+    return len;
+}
+
+__device__ __forceinline__ uint32_t glyph_of(const TextArgs &A, uint32_t ch) {
+    uint32_t g = ch - A.first_char;
+    if (ch < A.first_char || g >= A.n_glyphs) g = '?' - A.first_char;   // outside the atlas: '?'
+    return g;
+}
+
+// one run: returns the number of visible glyphs; writes records when out != null
+__device__ __forceinline__ uint32_t run(const TextArgs &A, const uint8_t *s, uint32_t len, float x, float max_x,
+                                        float base, uint32_t run_id, uint4 *out, uint32_t o) {
+    uint32_t n = 0;
+    float pen = x;
+    for (uint32_t i = 0; i < len; i++) {
+        const uint32_t g = glyph_of(A, s[i]);
+        const wg_glyph gl = A.glyphs[g];
+        const float next = pen + gl.advance * A.scale;
+        if (next > max_x) break;                       // clipped (summary column)
+        if (gl.w) {
+            if (out) out[o + n] = make_uint4(__float_as_uint(pen), __float_as_uint(base), g, run_id);
+            n++;
+        }
+        pen = next;
+    }
+    return n;
+}
+
+__device__ __forceinline__ float run_width(const TextArgs &A, const uint8_t *s, uint32_t len) {
+    float w = 0.0f;
+    for (uint32_t i = 0; i < len; i++) w = w + A.glyphs[glyph_of(A, s[i])].advance * A.scale;
+    return w;
+}
+
+template <bool WRITE>
+__global__ void k_text_rows(TextArgs A, uint64_t *__restrict__ cnt, const uint64_t *__restrict__ off, uint4 *__restrict__ rec) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t r = A.rb + j;
+    if (r >= A.re) return;
+    const float base = A.node_y[A.row_base + r] + A.baseline_dy;
+    uint8_t sha[7];
+    uint32_t nsha = 0;
+    if (!(A.flags[r] & WG_FLAG_SYNTHETIC)) {
+        const char *hex = "0123456789abcdef";
+        for (int i = 0; i < 7; i++) {
+            const uint8_t b = A.oid[r * 20 + i / 2];
+            sha[i] = (uint8_t)hex[(i & 1) ? (b & 15) : (b >> 4)];
+        }
+        nsha = 7;
+    }
+    const uint8_t *sum = A.sum ? A.sum + A.sum_off[r] : nullptr;
+    uint32_t nsum = A.sum ? (uint32_t)(A.sum_off[r + 1] - A.sum_off[r]) : 0;
+    const uint8_t *none = reinterpret_cast<const uint8_t *>("(no summary)");
+    if (nsum == 0) { sum = none; nsum = 12; }
+    char tb[24];
+    const uint32_t nt = relative_time(A.now, A.time[r], tb);
+    const float tx = A.time_right_x - run_width(A, reinterpret_cast<const uint8_t *>(tb), nt);
+    uint4 *out = WRITE ? rec : nullptr;
+    uint32_t o = WRITE ? (uint32_t)(off[j]) : 0u;
+    uint32_t n = run(A, sha, nsha, A.sha_x, 3.0e38f, base, 0, out, o);
+    n += run(A, sum, nsum, A.summary_x, A.summary_max_x, base, 1, out, o + n);
+    n += run(A, reinterpret_cast<const uint8_t *>(tb), nt, tx, 3.0e38f, base, 2, out, o + n);
+    if (!WRITE) cnt[j] = n;
+}
+
+struct QuadArgs {
+    uint64_t nq;
+    const uint4 *rec;
+    const wg_glyph *glyphs;
+    float scale, spread, inv_w, inv_h;
+    float4 color[3];
+};
+
+constexpr int QT = 256;
+
+__global__ void __launch_bounds__(QT) k_text_quads(QuadArgs A, float4 *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float4 stage[QT / 64][64 * 12];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t q0 = (uint64_t)blockIdx.x * QT + w * 64;   // this wave's first quad
+    if (q0 >= A.nq) return;
+    const uint64_t q = q0 + lane;
+    float4 *st = stage[w];
+    if (q < A.nq) {
+        const uint4 r = A.rec[q];
+        const float pen = __uint_as_float(r.x), base = __uint_as_float(r.y);
+        const wg_glyph g = A.glyphs[r.z];
+        const float4 c = A.color[r.w];
+        const float cw = (float)(g.w + 2u * (uint32_t)A.spread), ch = (float)(g.h + 2u * (uint32_t)A.spread);
+        const float x0 = pen + ((float)g.bearing_x - A.spread) * A.scale;
+        const float y0 = base - ((float)g.bearing_top + A.spread) * A.scale;
+        const float x1 = x0 + cw * A.scale, y1 = y0 + ch * A.scale;
+        const float u0 = (float)g.atlas_x * A.inv_w, v0 = (float)g.atlas_y * A.inv_h;
+        const float u1 = ((float)g.atlas_x + cw) * A.inv_w, v1 = ((float)g.atlas_y + ch) * A.inv_h;
+        // (x0,y0) (x1,y0) (x0,y1) | (x1,y0) (x1,y1) (x0,y1); TextVertex = {x, y, u, v, r, g, b, a}
+        const float px[6] = {x0, x1, x0, x1, x1, x0}, py[6] = {y0, y0, y1, y0, y1, y1};
+        const float pu[6] = {u0, u1, u0, u1, u1, u0}, pv[6] = {v0, v0, v1, v0, v1, v1};
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            st[lane * 12 + 2 * k] = make_float4(px[k], py[k], pu[k], pv[k]);
+            st[lane * 12 + 2 * k + 1] = c;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t cnt = (A.nq - q0) < 64 ? (A.nq - q0) : 64;
+    float4 *dst = out + q0 * 12;
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const uint32_t i = k * 64 + lane;
+        if (i < cnt * 12) dst[i] = st[i];
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, const uint64_t *summary_off,
+                   int32_t residency, const wg_text_params *p) {
+    if (!c || !p) return WG_E_INVALID;
+    if (p->slot < 0 || p->slot >= WG_FONT_SLOTS || !c->fonts[p->slot].built)
+        return wg_fail(c, WG_E_STATE, "font atlas slot %d not built", p->slot);
+    if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
+    const ShardState &S = c->sh;
+    if (rb > re || rb < S.s || re > S.e) return wg_fail(c, WG_E_INVALID, "row range outside the built rows");
+    if (!(p->text_px > 0.0f)) return wg_fail(c, WG_E_INVALID, "text_px must be positive");
+    (void)hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    FontSlot &F = c->fonts[p->slot];
+    c->have_text = false;
+    const uint64_t rows = re - rb, N = S.N;
+    const uint8_t *d_sum = nullptr;
+    const uint64_t *d_off = nullptr;
+    if (summary_off) {
+        if (residency == WG_HOST) {
+            const uint64_t bytes = summary_off[N] - summary_off[0];
+            WG_ALLOC(c, c->text_sum, bytes + 16);
+            WG_ALLOC(c, c->text_sum_off, (N + 1) * 8);
+            if (bytes) WG_HIP(c, hipMemcpyAsync(c->text_sum.p, summary + summary_off[0], bytes, hipMemcpyHostToDevice, s));
+            // offsets relative to the copied bytes
+            std::vector<uint64_t> rel(N + 1);
+            for (uint64_t i = 0; i <= N; i++) rel[i] = summary_off[i] - summary_off[0];
+            WG_HIP(c, hipMemcpyAsync(c->text_sum_off.p, rel.data(), (N + 1) * 8, hipMemcpyHostToDevice, s));
+            WG_HIP(c, hipStreamSynchronize(s));
+            d_sum = c->text_sum.as<uint8_t>();
+            d_off = c->text_sum_off.as<uint64_t>();
+        } else if (residency == WG_DEVICE) {
+            d_sum = summary;
+            d_off = summary_off;
+        } else {
+            return wg_fail(c, WG_E_INVALID, "bad residency %d", residency);
+        }
+    }
+    TextArgs A;
+    A.rb = rb;
+    A.re = re;
+    A.oid = c->d_oid;
+    A.time = c->d_time;
+    A.flags = c->d_flags;
+    A.sum = d_sum;
+    A.sum_off = d_off;
+    A.node_y = c->g_node_y.as<const float>();
+    A.row_base = S.row_base - S.s;          // context index = global row + row_base - s
+    A.glyphs = F.gtab.as<const wg_glyph>();
+    A.first_char = F.first_char;
+    A.n_glyphs = (uint32_t)F.glyphs.size();
+    A.scale = p->text_px / F.em_px;
+    A.sha_x = p->sha_x;
+    A.summary_x = p->summary_x;
+    A.summary_max_x = p->summary_max_x;
+    A.time_right_x = p->time_right_x;
+    A.baseline_dy = p->baseline_dy;
+    A.now = p->now;
+    if ('?' < F.first_char || '?' - F.first_char >= F.glyphs.size())
+        return wg_fail(c, WG_E_UNSUPPORTED, "atlas lacks '?' (the substitute glyph)");
+    WG_ALLOC(c, c->text_off, (rows + 2) * 8);
+    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(rows + 2));
+    c->text_rb = rb;
+    c->text_re = re;
+    c->n_quads = 0;
+    wg_stage_begin(c, "text_rows");
+    uint64_t nq = 0;
+    if (rows) {
+        hipLaunchKernelGGL(k_text_rows<false>, dim3(blocks(rows)), dim3(T), 0, s, A, c->text_off.as<uint64_t>(),
+                           (const uint64_t *)nullptr, (uint4 *)nullptr);
+        WG_HIP(c, wg_exclusive_scan_u64(c->text_off.as<uint64_t>(), c->text_off.as<uint64_t>(), rows, c->scan_tmp.p, s));
+        WG_HIP(c, hipMemcpyAsync(&nq, c->text_off.as<uint64_t>() + rows, 8, hipMemcpyDeviceToHost, s));
+        WG_HIP(c, hipStreamSynchronize(s));
+        WG_ALLOC(c, c->text_rec, nq * 16 + 16);
+        hipLaunchKernelGGL(k_text_rows<true>, dim3(blocks(rows)), dim3(T), 0, s, A, (uint64_t *)nullptr,
+                           (const uint64_t *)c->text_off.as<uint64_t>(), c->text_rec.as<uint4>());
+    } else {
+        WG_HIP(c, hipMemsetAsync(c->text_off.p, 0, 8, s));
+    }
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    c->n_quads = nq;
+    WG_ALLOC(c, c->text_vtx, nq * 6 * sizeof(wg_text_vertex) + 64);
+    wg_stage_begin(c, "text_quads");
+    if (nq) {
+        QuadArgs Q;
+        Q.nq = nq;
+        Q.rec = c->text_rec.as<const uint4>();
+        Q.glyphs = F.gtab.as<const wg_glyph>();
+        Q.scale = A.scale;
+        Q.spread = (float)F.spread;
+        Q.inv_w = 1.0f / (float)F.W;
+        Q.inv_h = 1.0f / (float)F.H;
+        for (int k = 0; k < 3; k++) {
+            const float *col = k == 0 ? p->color_sha : (k == 1 ? p->color_summary : p->color_time);
+            Q.color[k] = make_float4(col[0], col[1], col[2], col[3]);
+        }
+        hipLaunchKernelGGL(k_text_quads, dim3((uint32_t)((nq + QT - 1) / QT)), dim3(QT), 0, s, Q, c->text_vtx.as<float4>());
+        WG_HIP(c, hipGetLastError());
+    }
+    wg_stage_end(c);
+    c->have_text = true;
+    return WG_OK;
+}
+
+int wg_glyph_summary_get(wg_ctx *c, wg_glyph_summary *out) {
+    if (!c || !out) return WG_E_INVALID;
+    if (!c->have_text) return wg_fail(c, WG_E_STATE, "no glyphs emitted");
+    out->row_begin = c->text_rb;
+    out->row_end = c->text_re;
+    out->n_quads = c->n_quads;
+    out->n_vertices = c->n_quads * 6;
+    uint64_t chk = 0;
+    int rc = wg_words_checksum(c, c->text_vtx.as<const uint32_t>(), c->n_quads * 6 * 8, &chk);
+    if (rc != WG_OK) return rc;
+    out->checksum = chk;
+    return WG_OK;
+}
+
+int wg_copy_glyph_vertices(wg_ctx *c, uint64_t first, uint64_t count, wg_text_vertex *dst) {
+    if (!c || (!dst && count)) return WG_E_INVALID;
+    if (!c->have_text) return wg_fail(c, WG_E_STATE, "no glyphs emitted");
+    const uint64_t nv = c->n_quads * 6;
+    if (first > nv || count > nv - first) return wg_fail(c, WG_E_INVALID, "vertex range out of bounds");
+    if (count)
+        WG_HIP(c, hipMemcpyAsync(dst, c->text_vtx.as<wg_text_vertex>() + first, count * sizeof(wg_text_vertex),
+                                 hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+int wg_copy_glyph_offsets(wg_ctx *c, uint64_t *dst) {
+    if (!c || !dst) return WG_E_INVALID;
+    if (!c->have_text) return wg_fail(c, WG_E_STATE, "no glyphs emitted");
+    WG_HIP(c, hipMemcpyAsync(dst, c->text_off.p, (c->text_re - c->text_rb + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+}  // extern "C"

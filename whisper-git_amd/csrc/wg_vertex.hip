@@ -348,15 +348,13 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     return WG_OK;
 }
 
-int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out) {
+int wg_words_checksum(wg_ctx *c, const uint32_t *w, uint64_t nw, uint64_t *out) {
     WG_ALLOC(c, c->chk, 64);
     WG_HIP(c, hipMemsetAsync(c->chk.p, 0, 8, c->stream));
-    const uint64_t nw = c->n_vtx * 6;
     if (nw) {
         uint64_t b = (nw + 255) / 256;
         if (b > 4096) b = 4096;
-        hipLaunchKernelGGL(k_checksum, dim3(b), dim3(256), 0, c->stream, c->vtx.as<const uint32_t>(), nw,
-                           c->chk.as<unsigned long long>());
+        hipLaunchKernelGGL(k_checksum, dim3(b), dim3(256), 0, c->stream, w, nw, c->chk.as<unsigned long long>());
         WG_HIP(c, hipGetLastError());
     }
     uint64_t v = 0;
@@ -364,4 +362,8 @@ int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out) {
     WG_HIP(c, hipStreamSynchronize(c->stream));
     *out = v;
     return WG_OK;
+}
+
+int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out) {
+    return wg_words_checksum(c, c->vtx.as<const uint32_t>(), c->n_vtx * 6, out);
 }

@@ -68,6 +68,10 @@ def lib():
             "wg_font_atlas_build": ([vp, ctypes.c_int, vp, u64, ctypes.POINTER(abi.AtlasParams)], ctypes.c_int),
             "wg_font_atlas_info": ([vp, ctypes.c_int, ctypes.POINTER(abi.AtlasInfo)], ctypes.c_int),
             "wg_copy_font_atlas": ([vp, ctypes.c_int, vp, vp, vp, vp, vp], ctypes.c_int),
+            "wg_emit_glyphs": ([vp, u64, u64, vp, vp, i32, ctypes.POINTER(abi.TextParams)], ctypes.c_int),
+            "wg_glyph_summary_get": ([vp, ctypes.POINTER(abi.GlyphSummary)], ctypes.c_int),
+            "wg_copy_glyph_vertices": ([vp, u64, u64, vp], ctypes.c_int),
+            "wg_copy_glyph_offsets": ([vp, vp], ctypes.c_int),
             "wg_shard_build_begin": ([vp, ctypes.POINTER(abi.Commits), ctypes.c_int, ctypes.c_int, u64, u64,
                                       ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_geometry_begin": ([vp, vp, i32, ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
@@ -89,7 +93,8 @@ EXPORTED_SYMBOLS = (
     "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
-    "wg_shard_copy_msg", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas")
+    "wg_shard_copy_msg", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
+    "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets")
 
 FONT_DIR = os.path.join(os.path.dirname(_HERE), "fonts")
 FONTS = {0: os.path.join(FONT_DIR, "Roboto-Regular.ttf"), 1: os.path.join(FONT_DIR, "Roboto-Bold.ttf")}
@@ -282,6 +287,45 @@ class Engine:
                                              out["d2in"].ctypes.data, out["d2out"].ctypes.data,
                                              out["glyphs"].ctypes.data))
         return out
+
+    # -- glyph quads (WG-TEXT-1) --------------------------------------------------------------
+    def emit_glyphs(self, row_begin=0, row_end=None, summaries=None, device=None, **params):
+        """Text quads of rows [row_begin, row_end).  summaries: (bytes uint8
+        array, offsets uint64 [N+1]) host arrays, or device=(ptr, off_ptr)."""
+        if row_end is None:
+            ls = self.layout_summary()
+            row_end = ls.row_begin + ls.n_rows
+        p = abi.text_params(**params)
+        if device is not None:
+            self._check(lib().wg_emit_glyphs(self._ctx, row_begin, row_end, device[0], device[1], abi.WG_DEVICE,
+                                             ctypes.byref(p)))
+        elif summaries is None:
+            self._check(lib().wg_emit_glyphs(self._ctx, row_begin, row_end, None, None, abi.WG_HOST, ctypes.byref(p)))
+        else:
+            b = np.ascontiguousarray(summaries[0], np.uint8)
+            o = np.ascontiguousarray(summaries[1], np.uint64)
+            self._text_keep = (b, o)
+            self._check(lib().wg_emit_glyphs(self._ctx, row_begin, row_end, b.ctypes.data if b.size else o.ctypes.data,
+                                             o.ctypes.data, abi.WG_HOST, ctypes.byref(p)))
+
+    def glyph_summary(self) -> abi.GlyphSummary:
+        s = abi.GlyphSummary()
+        self._check(lib().wg_glyph_summary_get(self._ctx, ctypes.byref(s)))
+        return s
+
+    def glyph_vertices(self, first=0, count=None) -> np.ndarray:
+        s = self.glyph_summary()
+        if count is None:
+            count = s.n_vertices - first
+        v = np.empty(count, abi.TEXT_VERTEX_DTYPE)
+        self._check(lib().wg_copy_glyph_vertices(self._ctx, first, count, v.ctypes.data if count else None))
+        return v
+
+    def glyph_offsets(self) -> np.ndarray:
+        s = self.glyph_summary()
+        o = np.empty(s.row_end - s.row_begin + 1, np.uint64)
+        self._check(lib().wg_copy_glyph_offsets(self._ctx, o.ctypes.data))
+        return o
 
     # -- timing ----------------------------------------------------------------------------
     def debug_counters(self) -> np.ndarray:

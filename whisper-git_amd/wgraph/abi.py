@@ -7,6 +7,7 @@ import numpy as np
 
 WG_OK, WG_E_INVALID, WG_E_HIP, WG_E_NOMEM, WG_E_STATE, WG_E_UNSUPPORTED, WG_E_NODEVICE = 0, -1, -2, -3, -4, -5, -6
 WG_HOST, WG_DEVICE = 0, 1
+WG_FLAG_ORPHAN, WG_FLAG_SYNTHETIC = 0x1, 0x2
 WG_VERT_FULL, WG_VERT_TOP, WG_VERT_BOTTOM = 0, 1, 2
 WG_COLOR_ORPHAN, WG_COLOR_FOREGROUND, WG_PALETTE_SIZE = 6, 7, 8
 WG_STAGE_MAX = 1024
@@ -52,6 +53,37 @@ GLYPH_DTYPE = np.dtype([("codepoint", "<u4"), ("advance", "<f4"), ("bearing_x", 
                         ("w", "<u4"), ("h", "<u4"), ("atlas_x", "<u4"), ("atlas_y", "<u4")])
 # WG-SDF-1 defaults: Roboto at 96 px/em (48 px text at 2x oversampling), 8 px spread, ASCII 32..126
 ATLAS_DEFAULTS = dict(width=1024, height=1024, em_px=96.0, spread=8, first=32, last=126)
+
+
+class TextParams(ctypes.Structure):
+    _fields_ = [("slot", ctypes.c_int32), ("text_px", ctypes.c_float), ("sha_x", ctypes.c_float),
+                ("summary_x", ctypes.c_float), ("summary_max_x", ctypes.c_float), ("time_right_x", ctypes.c_float),
+                ("baseline_dy", ctypes.c_float), ("now", ctypes.c_int64), ("color_sha", ctypes.c_float * 4),
+                ("color_summary", ctypes.c_float * 4), ("color_time", ctypes.c_float * 4)]
+
+
+class GlyphSummary(ctypes.Structure):
+    _fields_ = [("row_begin", ctypes.c_uint64), ("row_end", ctypes.c_uint64), ("n_quads", ctypes.c_uint64),
+                ("n_vertices", ctypes.c_uint64), ("checksum", ctypes.c_uint64)]
+
+
+TEXT_VERTEX_DTYPE = np.dtype([(k, "<f4") for k in ("x", "y", "u", "v", "r", "g", "b", "a")])
+# WG-TEXT-1 default columns (pixels, row-local; the graph column is 6 lanes x 24 px wide)
+TEXT_DEFAULTS = dict(slot=0, text_px=13.0, sha_x=152.0, summary_x=214.0, summary_max_x=900.0, time_right_x=980.0,
+                     baseline_dy=4.5, now=1_704_067_200,   # 2024-01-01T00:00:00Z, where synthetic histories start
+                     color_sha=(0.55, 0.58, 0.62, 1.0), color_summary=(0.9, 0.91, 0.93, 1.0),
+                     color_time=(0.55, 0.58, 0.62, 1.0))
+
+
+def text_params(**kw) -> TextParams:
+    d = dict(TEXT_DEFAULTS, **kw)
+    p = TextParams()
+    for k, v in d.items():
+        if k.startswith("color_"):
+            getattr(p, k)[:] = [float(x) for x in v]
+        else:
+            setattr(p, k, v)
+    return p
 
 
 class ShardMsg(ctypes.Structure):

@@ -115,3 +115,44 @@ def save(d: Dag, path: str) -> None:
 def load(path: str) -> Dag:
     z = np.load(path, allow_pickle=False)
     return Dag(z["oid"], z["time"], z["parent_off"], z["parent_oid"], z["flags"], z["band"])
+
+
+_WORDS = (b"fix add remove update refactor merge branch into main for the of in to a with and bug test docs build "
+          b"cache lane graph layout render atlas kernel shard commit parser stream buffer index config api client "
+          b"server handle error path memory leak race speed up cleanup bump version deps revert wip tweak rename "
+          b"move split support allow use make drop check ensure avoid guard") .split()
+
+
+def summaries(n: int, seed: int = 0, mean_words: float = 6.0, p_empty: float = 0.02):
+    """Synthetic commit summaries for n rows: (bytes uint8 array, offsets
+    uint64 [n+1]).  Lowercase words, a capitalised first word, ~2% empty rows
+    ("(no summary)") and ~1% non-ASCII bytes (drawn as '?')."""
+    rng = np.random.default_rng(0xC0FFEE + seed)
+    vocab = np.frombuffer(b"".join(_WORDS), np.uint8)
+    vlen = np.array([len(w) for w in _WORDS], np.int64)
+    vstart = np.concatenate([[0], np.cumsum(vlen)[:-1]])
+    counts = rng.poisson(mean_words, n).clip(1, 14)
+    counts[rng.random(n) < p_empty] = 0
+    ids = rng.integers(0, len(_WORDS), int(counts.sum()))
+    wl = vlen[ids] + 1                                  # word + separator
+    row_of = np.repeat(np.arange(n), counts)
+    row_bytes = np.zeros(n, np.int64)
+    np.add.at(row_bytes, row_of, wl)
+    row_bytes = np.maximum(row_bytes - (counts > 0), 0)  # no trailing space
+    off = np.concatenate([[0], np.cumsum(row_bytes)]).astype(np.uint64)
+    out = np.full(int(off[-1]) + int(counts.sum()) + 1, ord(" "), np.uint8)
+    # place words at running positions within each row
+    wstart_in_row = np.cumsum(wl) - wl
+    first_word = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    wstart_in_row = wstart_in_row - np.repeat(wstart_in_row[first_word[counts > 0]], counts[counts > 0])
+    pos = off[row_of].astype(np.int64) + wstart_in_row
+    total = int(vlen[ids].sum())
+    src = np.repeat(vstart[ids], vlen[ids]) + (np.arange(total) - np.repeat(np.cumsum(vlen[ids]) - vlen[ids], vlen[ids]))
+    dst = np.repeat(pos, vlen[ids]) + (np.arange(total) - np.repeat(np.cumsum(vlen[ids]) - vlen[ids], vlen[ids]))
+    out[dst] = vocab[src]
+    out = out[:int(off[-1])]
+    firsts = off[:-1][counts > 0].astype(np.int64)
+    out[firsts] = np.where((out[firsts] >= 97) & (out[firsts] <= 122), out[firsts] - 32, out[firsts])
+    odd = rng.random(out.size) < 0.01
+    out[odd & (out != ord(" "))] = 0xC3
+    return out, off
