@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=1_000_000, help="rows of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the glyph-quad and font-atlas side measurements")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (host rehearsal)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     return ap.parse_args()
@@ -73,6 +74,72 @@ def cpu_baseline(dag, rows, log, min_seconds=10.0, max_reps=4):
     return {"value": d.n * reps / total, "unit": "commit-rows/s", "cores": 1, "kind": "port",
             "sample": f"first {d.n} rows of the same workload, {reps} passes: oracle build + "
                       f"row_geometry_with_bands + vertex emission, 1 thread, {total:.1f}s total"}
+
+
+def extra_measurements(eng, dag, dev, torch, r0, r1, args, log):
+    """Side measurements beside the headline metric (never `value`):
+    glyph quads (A13) for the same rows with synthetic summaries, and the
+    Roboto Regular+Bold 1024^2 SDF atlas build (A14, BASELINE config C2) on
+    the GPU beside the CPU restatement."""
+    from wgraph import abi, synth
+    out = {}
+    b, o = synth.summaries(dag.n)
+    t_b = torch.from_numpy(b).to(dev)
+    t_o = torch.from_numpy(o.view(np.int64)).to(dev)
+    # atlas (C2): both fonts, GPU wall time incl. the host TrueType parse
+    eng.build_font_atlas(0)
+    eng.build_font_atlas(1)
+    torch.cuda.synchronize()
+    reps = 5
+    eng.enable_timing(True, reserve=64)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.build_font_atlas(0)
+        eng.build_font_atlas(1)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) * 1e3 / reps
+    ev = {}
+    for name, ms in eng.timings():
+        ev[name] = ev.get(name, 0.0) + ms / reps
+    atlas = {"config": "Roboto Regular+Bold, 1024x1024 R8 SDF, 96 px/em, spread 8, ASCII 32-126",
+             "gpu_ms": round(wall, 3), "gpu_kernel_ms": round(ev.get("font_atlas", 0.0), 4),
+             "edt_ms": round(ev.get("font_edt", 0.0), 4), "coverage_ms": round(ev.get("font_coverage", 0.0), 4)}
+    if not args.no_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import font_oracle   # checker / baseline only
+        from wgraph import FONTS
+        t0 = time.perf_counter()
+        for slot in (0, 1):
+            font_oracle.build_atlas(FONTS[slot], **{k: v for k, v in abi.ATLAS_DEFAULTS.items()
+                                                    if k in ("width", "height", "em_px", "spread")})
+        atlas["cpu_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        atlas["cpu_kind"] = "port (numpy restatement, 1 thread)"
+    out["font_atlas"] = atlas
+    # glyph quads over the rank's rows
+    eng.row_geometry(dag.band)
+    kw = dict(now=int(dag.time.max()) + 86400)
+    eng.emit_glyphs(r0, r1, device=(t_b.data_ptr(), t_o.data_ptr()), **kw)
+    torch.cuda.synchronize()
+    eng.enable_timing(True, reserve=64 * 6)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.emit_glyphs(r0, r1, device=(t_b.data_ptr(), t_o.data_ptr()), **kw)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    ev = {}
+    for name, ms in eng.timings():
+        ev.setdefault(name, []).append(ms)
+    eng.enable_timing(False)
+    gs = eng.glyph_summary()
+    quad_ms = float(np.mean(ev.get("text_quads", [float("nan")])))
+    rows_ms = float(np.mean(ev.get("text_rows", [float("nan")])))
+    out["glyph_quads"] = {"rows": int(r1 - r0), "quads": int(gs.n_quads), "ms_per_call": round(dt * 1e3, 4),
+                          "rows_per_s": round((r1 - r0) / dt, 1), "text_rows_ms": round(rows_ms, 4),
+                          "text_quads_ms": round(quad_ms, 4),
+                          "text_quads_GBps": round(gs.n_quads * (192 + 16) / (quad_ms * 1e-3) / 1e9, 1),
+                          "data": "synthetic summaries (wgraph.synth.summaries), relative times vs max(time)+1d"}
+    log("extras:", json.dumps(out))
+    return out
 
 
 def pmc_traffic(args, workload):
@@ -229,6 +296,10 @@ def main():
         torch.cuda.synchronize()
         host_rate = rows_total * 3 / (time.perf_counter() - t1)
 
+    extras = {}
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras = extra_measurements(eng, dag, dev, torch, shard0, shard1, args, log)
+
     stages = {k: round(float(v), 4) for k, v in stage_ms.items()}
     log("stage ms (mean over timed steps):", json.dumps(stages))
     log(f"rows {rows_total}, shard {n_rows_shard}, vertices {vs.n_vertices}, vert {gs.n_vert}, curves {gs.n_curve}, "
@@ -249,7 +320,7 @@ def main():
                           "rows_total": rows_total, "rows_per_gpu": args.rows_per_gpu,
                           "vertices_per_gpu": int(vs.n_vertices), "parallelism": f"row-shard x{world}"},
                "stages_ms": stages, "host_input_rows_per_s": None if host_rate is None else round(host_rate, 1),
-               "roofline": roofline, "cpu_baseline": cpu}
+               "roofline": roofline, "cpu_baseline": cpu, **extras}
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

@@ -9,11 +9,13 @@
 //   host     TrueType parse (head/hhea/maxp/cmap fmt 4/hmtx/loca/glyf incl.
 //            offset composites), quadratic contours flattened into 8 lines
 //            each, scaled to atlas pixels, glyph cells shelf-packed
-//   k_font_coverage   one workgroup per glyph, edges in LDS: every cell pixel
-//            counts which of its 4x4 sample points lie inside the outline
-//            (non-zero winding) -> coverage 0..16; inside = coverage >= 8
-//   k_edt_cols        pass 1, one thread per column (coalesced rows): squared
-//            vertical distance to the nearest pixel of the other class
+//   k_font_coverage   one workgroup per (glyph, 8-row band), the band's edges
+//            compacted into LDS: every cell pixel counts which of its 4x4
+//            sample points lie inside the outline (non-zero winding) ->
+//            coverage 0..16; inside = coverage >= 8
+//   k_edt_cols        pass 1, one thread per pixel scanning its column
+//            outward: squared vertical distance to the nearest pixel of the
+//            other class
 //   k_edt_rows        pass 2, one workgroup per row staged in LDS: squared
 //            distance = min over q of g(q) + (x-q)^2, scanned outward with an
 //            early exit; exact for distances <= R = 4 * spread, "far" beyond
@@ -32,7 +34,6 @@ namespace {
 
 constexpr int QUAD_STEPS = 8;          // lines per quadratic segment
 constexpr int COV_T = 256;
-constexpr int MAX_GLYPH_EDGES = 2048;  // edges staged in LDS (32 KiB); larger glyphs read them from HBM
 
 struct GlyphDesc {          // per glyph, device
     uint32_t edge_off, n_edges;
@@ -42,27 +43,50 @@ struct GlyphDesc {          // per glyph, device
 };
 
 // ---- pass 0: coverage -----------------------------------------------------------
+// grid = (glyph, band of BAND cell rows): the band's edges are compacted into
+// LDS first (winding sums are integer, so their order does not matter), then
+// every pixel of the band tests only those.
+constexpr int BAND = 8;
+constexpr int BAND_EDGES = 1024;
+
 __global__ void __launch_bounds__(COV_T) k_font_coverage(const GlyphDesc *__restrict__ gd, const float4 *__restrict__ edges,
                                                          uint32_t spread, uint32_t W, uint8_t *__restrict__ cov) {
-    __shared__ float4 se[MAX_GLYPH_EDGES];
+    __shared__ float4 se[BAND_EDGES];
+    __shared__ uint32_t s_n;
     const GlyphDesc g = gd[blockIdx.x];
-    const float4 *E = edges + g.edge_off;
-    const bool staged = g.n_edges <= (uint32_t)MAX_GLYPH_EDGES;
-    if (staged)
-        for (uint32_t i = threadIdx.x; i < g.n_edges; i += COV_T) se[i] = E[i];
+    const uint32_t cj0 = blockIdx.y * BAND;
+    if (cj0 >= g.ch) return;
+    const uint32_t cj1 = cj0 + BAND < g.ch ? cj0 + BAND : g.ch;
+    // sample rows of the band lie in (ybot, ytop)
+    const float ytop = (float)(g.by1 - ((int32_t)cj0 - (int32_t)spread));
+    const float ybot = (float)(g.by1 - ((int32_t)cj1 - (int32_t)spread));
+    if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
-    if (staged) E = se;
+    const float4 *E = edges + g.edge_off;
+    for (uint32_t i = threadIdx.x; i < g.n_edges; i += COV_T) {
+        const float4 e = E[i];
+        const float ylo = e.y < e.w ? e.y : e.w, yhi = e.y < e.w ? e.w : e.y;
+        if (yhi > ybot && ylo < ytop) {
+            const uint32_t k = atomicAdd(&s_n, 1u);
+            if (k < (uint32_t)BAND_EDGES) se[k] = e;
+        }
+    }
+    __syncthreads();
+    const uint32_t ne = s_n;
+    const float4 *B = se;
+    if (ne > (uint32_t)BAND_EDGES) { B = E; }   // too many for LDS: test every edge of the glyph
+    const uint32_t nb = ne > (uint32_t)BAND_EDGES ? g.n_edges : ne;
     const float off[4] = {0.125f, 0.375f, 0.625f, 0.875f};
-    const uint32_t npx = g.cw * g.ch;
+    const uint32_t npx = g.cw * (cj1 - cj0);
     for (uint32_t p = threadIdx.x; p < npx; p += COV_T) {
-        const uint32_t ci = p % g.cw, cj = p / g.cw;
+        const uint32_t ci = p % g.cw, cj = cj0 + p / g.cw;
         const int32_t i = (int32_t)ci - (int32_t)spread, j = (int32_t)cj - (int32_t)spread;
         const float px = (float)(g.bx0 + i), py = (float)(g.by1 - j);
         int wind[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) wind[q] = 0;
-        for (uint32_t k = 0; k < g.n_edges; k++) {
-            const float4 e = E[k];   // (x0, y0, x1, y1), y up
+        for (uint32_t k = 0; k < nb; k++) {
+            const float4 e = B[k];   // (x0, y0, x1, y1), y up
             const bool up = e.y < e.w;
             const float ylo = up ? e.y : e.w, yhi = up ? e.w : e.y;
             if (py - 0.125f < ylo || py - 0.875f >= yhi) continue;   // no sample row of this pixel in [ylo, yhi)
@@ -89,31 +113,23 @@ __global__ void __launch_bounds__(COV_T) k_font_coverage(const GlyphDesc *__rest
 // ---- pass 1: columns ---------------------------------------------------------------
 // gin[y][x]  = (vertical distance from an inside pixel to the nearest outside pixel)^2
 // gout[y][x] = (vertical distance from an outside pixel to the nearest inside pixel)^2
-// 0 on the pixel's own class; capped at (R + 1)^2
+// 0 on the pixel's own class; capped at (R + 1)^2.  One thread per pixel
+// scanning its column outward (coalesced across x), exit at the first hit.
 __global__ void k_edt_cols(const uint8_t *__restrict__ cov, uint32_t W, uint32_t H, uint32_t R,
                            uint16_t *__restrict__ gin, uint16_t *__restrict__ gout) {
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t y = blockIdx.y;
     if (x >= W) return;
-    const uint32_t far = R + 1;
-    uint32_t din = far, dout = far;   // distance to the last outside / inside pixel above
-    for (uint32_t y = 0; y < H; y++) {
-        const bool in = cov[(uint64_t)y * W + x] >= 8;
-        din = in ? (din < far ? din + 1 : far) : 0;
-        dout = in ? 0 : (dout < far ? dout + 1 : far);
-        gin[(uint64_t)y * W + x] = (uint16_t)din;
-        gout[(uint64_t)y * W + x] = (uint16_t)dout;
+    const uint64_t o = (uint64_t)y * W + x;
+    const bool in = cov[o] >= 8;
+    uint32_t d = R + 1;
+    for (uint32_t k = 1; k <= R; k++) {
+        const bool hit_up = y >= k && ((cov[o - (uint64_t)k * W] >= 8) != in);
+        const bool hit_dn = y + k < H && ((cov[o + (uint64_t)k * W] >= 8) != in);
+        if (hit_up || hit_dn) { d = k; break; }
     }
-    din = far;
-    dout = far;
-    for (uint32_t yy = H; yy-- > 0;) {
-        const uint64_t o = (uint64_t)yy * W + x;
-        const bool in = cov[o] >= 8;
-        din = in ? (din < far ? din + 1 : far) : 0;
-        dout = in ? 0 : (dout < far ? dout + 1 : far);
-        const uint32_t a = gin[o] < din ? gin[o] : din, b = gout[o] < dout ? gout[o] : dout;
-        gin[o] = (uint16_t)(a * a);
-        gout[o] = (uint16_t)(b * b);
-    }
+    gin[o] = (uint16_t)(in ? d * d : 0u);
+    gout[o] = (uint16_t)(in ? 0u : d * d);
 }
 
 // ---- pass 2: rows -> squared distances and the SDF byte -------------------------------
@@ -433,12 +449,14 @@ int wg_font_atlas_build(wg_ctx *c, int slot, const uint8_t *ttf, uint64_t len, c
     wg_stage_begin(c, "font_atlas");
     wg_stage_begin(c, "font_coverage");
     WG_HIP(c, hipMemsetAsync(S.cov.p, 0, npx, s));
+    uint32_t max_ch = 0;
+    for (const GlyphDesc &d : gd) max_ch = d.ch > max_ch ? d.ch : max_ch;
     if (!gd.empty())
-        hipLaunchKernelGGL(k_font_coverage, dim3((uint32_t)gd.size()), dim3(COV_T), 0, s, S.gdesc.as<const GlyphDesc>(),
-                           S.edges.as<const float4>(), spread, W, S.cov.as<uint8_t>());
+        hipLaunchKernelGGL(k_font_coverage, dim3((uint32_t)gd.size(), (max_ch + BAND - 1) / BAND), dim3(COV_T), 0, s,
+                           S.gdesc.as<const GlyphDesc>(), S.edges.as<const float4>(), spread, W, S.cov.as<uint8_t>());
     wg_stage_end(c);
     wg_stage_begin(c, "font_edt");
-    hipLaunchKernelGGL(k_edt_cols, dim3((W + 255) / 256), dim3(256), 0, s, S.cov.as<const uint8_t>(), W, H, S.R,
+    hipLaunchKernelGGL(k_edt_cols, dim3((W + 255) / 256, H), dim3(256), 0, s, S.cov.as<const uint8_t>(), W, H, S.R,
                        S.gin.as<uint16_t>(), S.gout.as<uint16_t>());
     hipLaunchKernelGGL(k_edt_rows, dim3(H), dim3(ROW_T), 0, s, S.gin.as<const uint16_t>(), S.gout.as<const uint16_t>(), W,
                        S.R, (float)spread, S.d2in.as<uint16_t>(), S.d2out.as<uint16_t>(), S.sdf.as<uint8_t>());
