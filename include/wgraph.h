@@ -192,6 +192,10 @@ int         wg_synchronize(wg_ctx *ctx);
 /* WG_OPT_REPLAY_CHUNK: events per chunk of the parallel lane-event replay
  * (multiple of 64; default 512).  Affects speed only, never results. */
 #define WG_OPT_REPLAY_CHUNK 2
+/* WG_OPT_SWEEP_REG: edges per 64-row chunk the geometry sweep keeps in
+ * registers (0..512, default 512); wider chunks use the LDS sweep.  Affects
+ * speed only, never results. */
+#define WG_OPT_SWEEP_REG 3
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------

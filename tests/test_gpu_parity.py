@@ -146,6 +146,19 @@ def test_against_oracle_midsize(engine, kind, n):
     assert_bits("vertices", engine.vertices(a, b - a).view(np.float32), ov[a:b].view(np.float32))
 
 
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_geometry_lds_sweep(engine, name):
+    """Every chunk through the LDS sweep (register capacity 0): same lists."""
+    from wgraph import lib
+    d, g = load_golden(name)
+    engine._check(lib().wg_set_option(engine._ctx, 3, 0))
+    try:
+        engine.build(d)
+        check_geometry(engine, g, "build_")
+    finally:
+        engine._check(lib().wg_set_option(engine._ctx, 3, 512))
+
+
 def test_partial_row_range(engine):
     from oracle import oracle_c
     d = synth.generate("random13", 5000, seed=77)

@@ -66,10 +66,10 @@ void wg_destroy(wg_ctx *c) {
     DevBuf *bufs[] = {&c->in_oid, &c->in_time, &c->in_poff, &c->in_poid, &c->in_flags, &c->hash, &c->canon,
                       &c->prow, &c->lane_asg, &c->lane_out, &c->color_out, &c->lane_scalars, &c->edge_cnt,
                       &c->edges, &c->heights, &c->band, &c->g_height, &c->g_node_y, &c->g_row_top,
-                      &c->rt_chunk, &c->rt_tables, &c->rt_flags, &c->cntF, &c->cntT, &c->cntB, &c->cntC,
+                      &c->rt_chunk, &c->rt_tables, &c->rt_sup, &c->rt_flags, &c->cntF, &c->cntT, &c->cntB, &c->cntC,
                       &c->cntCend, &c->vert_off, &c->curve_off, &c->vert, &c->curve, &c->curve_color,
                       &c->curve_ref, &c->curve_row, &c->top_fill, &c->carry_cnt, &c->carry_off, &c->carry,
-                      &c->scan_tmp, &c->scal, &c->rowflags, &c->carry_fill, &c->sweep_err, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
+                      &c->scan_tmp, &c->scal, &c->rowflags, &c->carry_fill, &c->sweep_err, &c->sweep_big, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
     for (DevBuf *b : bufs) b->release();
     for (DevBuf &b : c->lf) b.release();
     ShardState &S = c->sh;
@@ -116,6 +116,10 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
     case WG_OPT_REPLAY_CHUNK:
         if (value < 64 || value > (1 << 20) || (value & 63)) return wg_fail(c, WG_E_INVALID, "replay chunk must be a multiple of 64");
         c->replay_chunk = (uint32_t)value;
+        return WG_OK;
+    case WG_OPT_SWEEP_REG:
+        if (value < 0 || value > 512) return wg_fail(c, WG_E_INVALID, "sweep register capacity must be 0..512");
+        c->sweep_reg_cap = (uint32_t)value;
         return WG_OK;
     default: return wg_fail(c, WG_E_INVALID, "unknown option %d", option);
     }

@@ -179,26 +179,16 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nch, const wg_edge *__restrict__ edges,
+// Fallback sweep for chunks with more edges than the register sweep holds:
+// active list in LDS, appended / compacted row by row.
+__device__ void sweep_chunk_lds(uint64_t q, uint64_t n, const wg_edge *__restrict__ edges,
         const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
         const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
-        uint32_t *__restrict__ err) {
-    // active list (edges alive at the current row, edge order) + the chunk's own new edges
-    __shared__ uint32_t s_eid[SW_WAVES][SW_CAP];
-    __shared__ uint32_t s_c[SW_WAVES][SW_CAP];
-    __shared__ uint32_t s_p[SW_WAVES][SW_CAP];
-    __shared__ uint32_t s_info[SW_WAVES][SW_CAP];
-    __shared__ uint32_t n_c[SW_WAVES][SW_NE];
-    __shared__ uint32_t n_p[SW_WAVES][SW_NE];
-    __shared__ uint32_t n_info[SW_WAVES][SW_NE];
-    const int w = threadIdx.x >> 6;
+        uint32_t *__restrict__ err, uint32_t *E, uint32_t *C, uint32_t *P, uint32_t *I, uint32_t *NC, uint32_t *NP,
+        uint32_t *NI) {
     const uint32_t lid = threadIdx.x & 63;
-    const uint64_t q = (uint64_t)blockIdx.x * SW_WAVES + w;
-    if (q >= nch) return;
-    uint32_t *E = s_eid[w], *C = s_c[w], *P = s_p[w], *I = s_info[w];
-    uint32_t *NC = n_c[w], *NP = n_p[w], *NI = n_info[w];
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
     // per-row scalars of the chunk, one row per lane
@@ -291,6 +281,97 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
             __builtin_amdgcn_wave_barrier();
         }
         cnt = kept;
+    }
+}
+
+__global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const uint32_t *__restrict__ list,
+        const uint32_t *__restrict__ list_n, const wg_edge *__restrict__ edges,
+        const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
+        const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
+        const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
+        uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
+        uint32_t *__restrict__ err) {
+    __shared__ uint32_t s_eid[SW_WAVES][SW_CAP];
+    __shared__ uint32_t s_c[SW_WAVES][SW_CAP];
+    __shared__ uint32_t s_p[SW_WAVES][SW_CAP];
+    __shared__ uint32_t s_info[SW_WAVES][SW_CAP];
+    __shared__ uint32_t n_c[SW_WAVES][SW_NE];
+    __shared__ uint32_t n_p[SW_WAVES][SW_NE];
+    __shared__ uint32_t n_info[SW_WAVES][SW_NE];
+    const int w = threadIdx.x >> 6;
+    const uint32_t cnt = *list_n;
+    for (uint32_t i = blockIdx.x * SW_WAVES + w; i < cnt; i += gridDim.x * SW_WAVES)
+        sweep_chunk_lds(list[i], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off, curve_off, vert,
+                        curve_ref, curve_row, err, s_eid[w], s_c[w], s_p[w], s_info[w], n_c[w], n_p[w], n_info[w]);
+}
+
+// The sweep: one wave per 64-row chunk.  A chunk's edge set is fixed — the
+// edges alive across its first row (carry-in, edge order) followed by the
+// edges whose child row lies in the chunk (edge order) — so it is held in
+// registers (slot s of lane l = set entry 64 s + l) and every row's ordered
+// full / curve lists are ballots over "alive at this row": no LDS, no
+// per-row compaction.  Chunks with more than 64 * SW_SLOTS edges go to the
+// LDS sweep above.
+constexpr int SW_SLOTS = 8;
+
+__global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nch, const wg_edge *__restrict__ edges,
+        const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
+        const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
+        const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
+        uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
+        uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap) {
+    const uint32_t lid = threadIdx.x & 63;
+    const uint64_t q = (uint64_t)blockIdx.x * SW_WAVES + (threadIdx.x >> 6);
+    if (q >= nch) return;
+    const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
+    const uint32_t nr = (uint32_t)(R1 - R0);
+    const uint32_t a = carry_off[q], ncar = carry_off[q + 1] - a;
+    const uint32_t E0 = edge_off[R0], E1 = edge_off[R1];
+    const uint32_t total = ncar + (E1 - E0);
+    if (total > reg_cap) {
+        if (lid == 0) big[atomicAdd(big_n, 1u)] = (uint32_t)q;
+        return;
+    }
+    // per-row scalars of the chunk, one row per lane
+    const uint64_t rr = R0 + lid;
+    const uint32_t rf_v = lid < nr ? rowflags[rr] : 0u;
+    const uint32_t voff_v = lid < nr ? vert_off[rr] : 0u;
+    const uint32_t coff_v = lid < nr ? curve_off[rr] : 0u;
+    uint32_t ek[SW_SLOTS], ec[SW_SLOTS], ep[SW_SLOTS], ei[SW_SLOTS];
+    const uint32_t nslots = (total + 63) / 64;
+#pragma unroll
+    for (int sl = 0; sl < SW_SLOTS; sl++) {
+        const uint32_t idx = 64u * sl + lid;
+        ek[sl] = 0; ec[sl] = 1; ep[sl] = 0; ei[sl] = 0;   // dead: c >= p
+        if ((uint32_t)sl < nslots && idx < total) {
+            const uint32_t k = idx < ncar ? carry_sorted[a + idx] : E0 + (idx - ncar);
+            const wg_edge e = edges[k];
+            ek[sl] = k;
+            ec[sl] = e.child_row;
+            ep[sl] = e.parent_row;
+            ei[sl] = (e.child_lane & 0xFFFFFFu) | (e.color << 24) | ((e.child_lane == e.parent_lane) ? 0x10000000u : 0u);
+        }
+    }
+    for (uint32_t j = 0; j < nr; j++) {
+        const uint32_t r = (uint32_t)(R0 + j);
+        const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)rf_v, (int)j);
+        uint32_t fbase = (uint32_t)__builtin_amdgcn_readlane((int)voff_v, (int)j);
+        uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
+#pragma unroll
+        for (int sl = 0; sl < SW_SLOTS; sl++) {
+            if ((uint32_t)sl >= nslots) break;
+            const uint32_t c = ec[sl], p = ep[sl], info = ei[sl];
+            const bool live = c < p;
+            const bool same = (info & 0x10000000u) != 0;
+            const bool full = live && same && c < r && r < p;
+            const bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
+            const bool curv = live && !same && c <= r && r <= p && !skip;
+            const uint64_t mf = __ballot(full), mc = __ballot(curv);
+            if (full) vert[fbase + mbcnt(mf)] = pack_vert(info & 0xFFFFFFu, WG_VERT_FULL, (info >> 24) & 0xFu);
+            if (curv) { const uint32_t o = cbase + mbcnt(mc); curve_ref[o] = ek[sl]; curve_row[o] = r; }
+            fbase += __builtin_popcountll(mf);
+            cbase += __builtin_popcountll(mc);
+        }
     }
 }
 
@@ -465,9 +546,17 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     uint32_t *carry_sorted = c->carry.as<uint32_t>() + ncarry + 2;
     hipLaunchKernelGGL(k_carry_sort, dim3(nch), dim3(64), 0, s, nch, c->carry_off.as<const uint32_t>(),
                        c->carry.as<const uint32_t>(), carry_sorted);
+    // chunks too wide for the register sweep are listed in sweep_err[2..] and swept through LDS
+    uint32_t *big_n = c->sweep_err.as<uint32_t>() + 1;
+    WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
     hipLaunchKernelGGL(k_sweep, dim3((nch + SW_WAVES - 1) / SW_WAVES), dim3(64 * SW_WAVES), 0, s, n, nch, E, edge_off,
                        c->carry_off.as<const uint32_t>(), (const uint32_t *)carry_sorted, c->rowflags.as<const uint8_t>(),
-                       voff, coff, vert, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), c->sweep_err.as<uint32_t>());
+                       voff, coff, vert, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(),
+                       c->sweep_big.as<uint32_t>(), big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS);
+    hipLaunchKernelGGL(k_sweep_lds, dim3(64), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)c->sweep_big.as<uint32_t>(),
+                       (const uint32_t *)big_n, E, edge_off, c->carry_off.as<const uint32_t>(),
+                       (const uint32_t *)carry_sorted, c->rowflags.as<const uint8_t>(), voff, coff, vert,
+                       c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), c->sweep_err.as<uint32_t>());
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     wg_stage_begin(c, "geom_curves");

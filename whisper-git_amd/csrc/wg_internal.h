@@ -161,6 +161,7 @@ struct wg_ctx {
     DevBuf g_height, g_node_y, g_row_top;   // float [N], [N], [N+1]
     DevBuf rt_chunk;        // per-chunk scan state
     DevBuf rt_tables;       // per-chunk transducer tables
+    DevBuf rt_sup;          // super-chunk tables, binade bases and walk states
     DevBuf rt_flags;        // uint32 [4]
     DevBuf cntF, cntT, cntB, cntC, cntCend; // uint32 [N+1] per-row counts / diff arrays
     DevBuf vert_off, curve_off;             // uint32 [N+1]
@@ -173,7 +174,9 @@ struct wg_ctx {
     DevBuf scal;            // uint64 [16] device scalars (totals)
     DevBuf rowflags;        // uint8 [N] bit0 zero-height strip, bit1 child strip empty, bit2 parent strip empty
     DevBuf carry_fill;      // uint32 [nch]
-    DevBuf sweep_err;       // uint32 [4]
+    DevBuf sweep_err;       // uint32 [16]: [0] LDS sweep overflow, [1] chunks listed for the LDS sweep
+    DevBuf sweep_big;       // uint32 [nch] chunks too wide for the register sweep
+    uint32_t sweep_reg_cap = 512;   // edges per chunk the register sweep holds (WG_OPT_SWEEP_REG)
     const float *edge_y = nullptr;   // per edge {child_y, parent_y} override (row-sharded geometry), or null
     // ---- vertices -------------------------------------------------------------
     bool     have_vtx = false;

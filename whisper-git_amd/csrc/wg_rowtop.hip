@@ -242,6 +242,67 @@ __global__ void __launch_bounds__(RT_T) k_rt_tables(uint64_t n, const float *__r
     }
 }
 
+// ---- super-chunks: 64 chunks (64K rows) composed per candidate binade ----------------
+constexpr int RT_SUP = 64;
+struct SupState { float start; int32_t k; uint32_t mode; uint32_t pad; };   // mode 1: walked at super level
+
+__device__ __forceinline__ Td td_reduce64(Td t) {   // ordered: lane 0 gets T_0 o ... o T_63
+    const int lid = threadIdx.x & 63;
+    for (int d = 1; d < 64; d <<= 1) {
+        const Td o = td_shfl_down(t, d);
+        if ((lid & (2 * d - 1)) == 0 && lid + d < 64) t = td_compose(t, o);
+    }
+    return t;
+}
+
+__global__ void __launch_bounds__(64) k_rt_super(uint64_t nch, const RtChunk *__restrict__ ch, const uint4 *__restrict__ tables,
+                                                 uint4 *__restrict__ stab, int32_t *__restrict__ skbase) {
+    const uint64_t S = blockIdx.x, c0 = S * RT_SUP, cc = c0 + (threadIdx.x & 63);
+    const bool full = c0 + RT_SUP <= nch;
+    double sm = full ? ch[cc].sum : 0.0;
+    for (int d = 32; d >= 1; d >>= 1) sm += __shfl_down(sm, d, 64);
+    sm = __shfl(sm, 0, 64);
+    const int k0 = ch[c0 < nch ? c0 : 0].kguess - 1;
+    for (int j = 0; j < WG_RT_NBIN; j++) {
+        const int k = k0 + j;
+        Td t = td_invalid();
+        if (full && ch[cc].mode != MODE_EXACT) {
+            const int b = k - ch[cc].kguess + 1;
+            if (b >= 0 && b < WG_RT_NBIN) { const uint4 q = tables[cc * WG_RT_NBIN + b]; t = Td{q.x, q.y, q.z}; }
+        }
+        t = td_reduce64(t);
+        // ulp counts stay far below 2^32 only where the ulp is >= 2 (k >= 24) and the sum is bounded
+        const bool fits = full && k >= 24 && k < 120 && sm < ldexp(1.0, k - 23) * 2147483648.0;
+        if ((threadIdx.x & 63) == 0) stab[S * WG_RT_NBIN + j] = fits ? make_uint4(t.d0, t.d1, t.f, 0u) : make_uint4(0u, 0u, 2u, 0u);
+    }
+    if ((threadIdx.x & 63) == 0) skbase[S] = k0;
+}
+
+// chunk starts inside the super-chunks the walk consumed whole
+__global__ void __launch_bounds__(64) k_rt_fill(uint64_t nch, const SupState *__restrict__ sup, RtChunk *__restrict__ ch,
+                                                const uint4 *__restrict__ tables) {
+    const uint64_t S = blockIdx.x;
+    const SupState st = sup[S];
+    if (st.mode != 1u) return;
+    const int lid = threadIdx.x & 63;
+    const uint64_t cc = S * RT_SUP + lid;
+    const float u = ldexpf(1.0f, st.k - 23);
+    const uint32_t p0 = ((uint32_t)(st.start / u)) & 1u;
+    const int b = st.k - ch[cc].kguess + 1;
+    const uint4 q = tables[cc * WG_RT_NBIN + b];   // valid: the super table was composed from these
+    Td t = Td{q.x, q.y, q.z};
+    for (int d = 1; d < 64; d <<= 1) {
+        const Td o = td_shfl_up(t, d);
+        if (lid >= d) t = td_compose(o, t);
+    }
+    Td ex = td_shfl_up(t, 1);
+    if (lid == 0) ex = td_identity();
+    const uint32_t D = p0 ? ex.d1 : ex.d0;
+    ch[cc].start = st.start + (float)D * u;
+    ch[cc].kstart = st.k;
+    ch[cc].mode = MODE_TABLE;
+}
+
 // Replay rows [r0, r1) from acc one by one (negative / non-finite steps).
 __device__ float serial_rows(uint64_t r0, uint64_t r1, float acc, const float *__restrict__ h,
                              const float *__restrict__ band, float *__restrict__ row_top) {
@@ -312,7 +373,8 @@ __device__ float replay_rows(uint64_t r0, uint64_t r1, float acc, const float *_
 __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const float *__restrict__ h,
                                                 const float *__restrict__ band, RtChunk *__restrict__ ch,
                                                 const uint4 *__restrict__ tables, uint32_t *__restrict__ flags,
-                                                float *__restrict__ row_top) {
+                                                float *__restrict__ row_top, uint64_t nsup, const uint4 *__restrict__ stab,
+                                                const int32_t *__restrict__ skbase, SupState *__restrict__ sup) {
     const int lid = threadIdx.x & 63;
     const bool all_serial = flags[0] != 0;
     // skip the exact-regime prefix (its chunks are independent prefix sums)
@@ -331,6 +393,34 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
     uint64_t replayed = 0;
     while (c < nch) {
         bool do_replay = all_serial || !(A > 0.0f) || !isfinite(A);
+        if (!do_replay && (c % RT_SUP) == 0 && c / RT_SUP < nsup) {
+            // super level: up to 64 super-chunks (4M rows) per step
+            const int k = binade_of(A);
+            const float u = ldexpf(1.0f, k - 23);
+            const double top = ldexp(1.0, k + 1);
+            const uint32_t p = ((uint32_t)(A / u)) & 1u;
+            const uint64_t ss = c / RT_SUP + lid;
+            Td t = td_invalid();
+            if (ss < nsup) {
+                const int b = k - skbase[ss];
+                if (b >= 0 && b < WG_RT_NBIN) { const uint4 q = stab[ss * WG_RT_NBIN + b]; t = Td{q.x, q.y, q.z}; }
+            }
+            for (int d = 1; d < 64; d <<= 1) {
+                Td o = td_shfl_up(t, d);
+                if (lid >= d) t = td_compose(o, t);
+            }
+            const uint32_t D = p ? t.d1 : t.d0;
+            const bool ok = (t.f & 4u) && ss < nsup && (double)A + (double)D * (double)u < top;
+            const uint64_t okm = __ballot(ok);
+            const int f = okm == ~0ull ? 64 : (int)__builtin_ctzll(~okm);
+            const uint32_t Dprev = (uint32_t)__shfl_up((int)D, 1, 64);
+            if (lid < f) sup[ss] = SupState{A + (float)(lid == 0 ? 0u : Dprev) * u, k, 1u, 0u};
+            if (f > 0) {
+                A = A + (float)(uint32_t)__shfl((int)D, f - 1, 64) * u;
+                c += (uint64_t)f * RT_SUP;
+                continue;
+            }
+        }
         if (!do_replay) {
             const int k = binade_of(A);
             const float u = ldexpf(1.0f, k - 23);
@@ -351,7 +441,8 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
                 if (lid >= d) t = td_compose(o, t);
             }
             const uint32_t D = p ? t.d1 : t.d0;
-            const bool ok = (t.f & 4u) && cc < nch && (double)A + (double)D * (double)u < top;
+            const bool ok = (t.f & 4u) && cc < nch && cc / RT_SUP == c / RT_SUP &&   // stop at the super boundary
+                            (double)A + (double)D * (double)u < top;
             const uint64_t okm = __ballot(ok);
             const int f = okm == ~0ull ? 64 : (int)__builtin_ctzll(~okm);   // leading run of valid lanes
             const uint32_t Dprev = (uint32_t)__shfl_up((int)D, 1, 64);
@@ -366,7 +457,8 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
                 A = A + (float)Dl * u;
                 c += f;
             }
-            do_replay = f < 64 && c < nch;
+            // stopped before a chunk inside the super-chunk: that chunk crosses a binade
+            do_replay = f < 64 && c < nch && !(f > 0 && (c % RT_SUP) == 0);
         }
         if (do_replay && c < nch) {
             const uint64_t r0 = c * WG_RT_CHUNK, r1 = (r0 + WG_RT_CHUNK < n) ? r0 + WG_RT_CHUNK : n;
@@ -513,8 +605,21 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
     hipLaunchKernelGGL(k_rt_prefix, dim3(1), dim3(1024), 0, c->stream, nch, ch, fl);
     hipLaunchKernelGGL(k_rt_tables, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch,
                        c->rt_tables.as<uint4>());
+    const uint64_t nsup = nch / RT_SUP;   // full super-chunks only
+    WG_ALLOC(c, c->rt_sup, nsup * (WG_RT_NBIN * 16 + 4 + sizeof(SupState)) + 64);
+    uint4 *stab = c->rt_sup.as<uint4>();
+    int32_t *skb = reinterpret_cast<int32_t *>(stab + nsup * WG_RT_NBIN);
+    SupState *sup = reinterpret_cast<SupState *>(c->rt_sup.as<uint8_t>() + ((nsup * (WG_RT_NBIN * 16 + 4) + 15) / 16) * 16);
+    if (nsup) {
+        WG_HIP(c, hipMemsetAsync(sup, 0, nsup * sizeof(SupState), c->stream));
+        hipLaunchKernelGGL(k_rt_super, dim3(nsup), dim3(64), 0, c->stream, nch, (const RtChunk *)ch,
+                           c->rt_tables.as<const uint4>(), stab, skb);
+    }
     hipLaunchKernelGGL(k_rt_walk, dim3(1), dim3(64), 0, c->stream, n, nch, h, d_band, ch,
-                       c->rt_tables.as<const uint4>(), fl, row_top);
+                       c->rt_tables.as<const uint4>(), fl, row_top, nsup, (const uint4 *)stab, (const int32_t *)skb, sup);
+    if (nsup)
+        hipLaunchKernelGGL(k_rt_fill, dim3(nsup), dim3(64), 0, c->stream, nch, (const SupState *)sup, ch,
+                           c->rt_tables.as<const uint4>());
     hipLaunchKernelGGL(k_rt_rows, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch, row_top);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
