@@ -11,7 +11,7 @@
 // vertices, ring -> 24 quads = 144 vertices.
 //
 // HBM-write-bound: 24 B per vertex out, a few bytes of geometry in.  A
-// workgroup owns a fixed tile of 4096 vertices (96 KiB out):
+// workgroup owns a fixed tile of 2048 vertices (48 KiB out):
 //   1. one round of independent global loads, all addressed from a per-tile
 //      record (k_tile_info): the rows overlapping the tile, its vertical
 //      entries (one contiguous range of vert[]) and its curve segments (one
@@ -34,12 +34,13 @@ namespace {
 #define WG_VTX_THREADS 256
 #endif
 #ifndef WG_VTX_TILE_VERTS
-#define WG_VTX_TILE_VERTS 4096
+#define WG_VTX_TILE_VERTS 2048
 #endif
 constexpr int VT = WG_VTX_THREADS;
 constexpr int TILE = WG_VTX_TILE_VERTS;     // vertices per workgroup
-constexpr int PAIRS = TILE / 2;             // 2048
-constexpr int ROUNDS = PAIRS / VT;          // 8
+constexpr int PAIRS = TILE / 2;             // 1024
+constexpr int ROUNDS = PAIRS / VT;          // 4
+typedef float v4f __attribute__((ext_vector_type(4)));
 static_assert(TILE / WG_VTX_PER_NODE + 3 <= 64, "rows of a tile are loaded by one wave");
 constexpr int MAXR = TILE / WG_VTX_PER_NODE + 3;          // rows overlapping a tile
 constexpr int MAXC = TILE / WG_VTX_PER_CURVE + 3;         // curve segments overlapping a tile
@@ -284,7 +285,8 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             const uint32_t i = k * 64 + lane;
-            if (i < cnt * 3) dst[i] = st[i];
+            // streaming (non-temporal) stores: the buffer is not re-read by this pass
+            if (i < cnt * 3) __builtin_nontemporal_store(reinterpret_cast<const v4f *>(st)[i], reinterpret_cast<v4f *>(dst) + i);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
