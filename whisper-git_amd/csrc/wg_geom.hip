@@ -471,7 +471,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     WG_ALLOC(c, c->vert_off, (n + 2) * 4);
     WG_ALLOC(c, c->curve_off, (n + 2) * 4);
     WG_ALLOC(c, c->top_fill, (n + 2) * 4);
-    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(n + 2));
+    { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
     WG_ALLOC(c, c->sweep_err, 64);
     c->n_vert = c->n_curve = 0;
     if (n == 0) {

@@ -227,8 +227,9 @@ void wg_stage_end(wg_ctx *c);
 
 // scans (wg_scan.hip) -----------------------------------------------------------
 // Exclusive scan of n uint32 in place into out[0..n] (out[n] = total).  The
-// input may alias out.  tmp must hold wg_scan_tmp_bytes(n).
+// input may alias out.  tmp = c->scan_tmp after wg_scan_reserve(c, n).
 size_t wg_scan_tmp_bytes(uint64_t n);
+int wg_scan_reserve(wg_ctx *c, uint64_t n);   // grow c->scan_tmp for scans of up to n elements
 hipError_t wg_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, void *tmp, hipStream_t s);
 hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, hipStream_t s);
 

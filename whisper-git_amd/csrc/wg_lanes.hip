@@ -240,7 +240,7 @@ int wg_stage_edges(wg_ctx *c) {
     WG_ALLOC(c, c->lane_out, n * 4 + 4);
     WG_ALLOC(c, c->color_out, n + 4);
     WG_ALLOC(c, c->edge_cnt, (n + 1) * 4);
-    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(n + 1));
+    { const int _sr = wg_scan_reserve(c, n + 1); if (_sr != WG_OK) return _sr; }
     c->n_edges = 0;
     if (n == 0) {
         WG_HIP(c, hipMemsetAsync(c->edge_cnt.p, 0, 4, c->stream));

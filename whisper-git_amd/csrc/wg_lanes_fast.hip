@@ -319,7 +319,7 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, uint32_t *viol, uint64_t *nev, uint6
     WG_ALLOC(c, ev_off, (n + 2) * 4);
     WG_ALLOC(c, aux_off, (n + 2) * 4);
     WG_ALLOC(c, flags, 64);
-    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(n + 2));
+    { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "lf_refs");
     WG_HIP(c, hipMemsetAsync(first_ref.p, 0xFF, n * 8, s));
     WG_HIP(c, hipMemsetAsync(fpc.p, 0, (n + 2) * 4, s));

@@ -111,3 +111,8 @@ hipError_t wg_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, 
 hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, hipStream_t s) {
     return scan_rec<uint64_t, uint64_t>(in, out, n, (char *)tmp, s);
 }
+
+int wg_scan_reserve(wg_ctx *c, uint64_t n) {
+    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(n));
+    return WG_OK;
+}

@@ -518,7 +518,7 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     const uint64_t xin = S.xoff[S.rank];
     WG_ALLOC(c, S.in_scan, (xin + 2) * 4);
     WG_ALLOC(c, c->edge_cnt, (nloc + 2) * 4);
-    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(nloc + xin + 2));
+    { const int _sr = wg_scan_reserve(c, nloc + xin + 2); if (_sr != WG_OK) return _sr; }
     WG_HIP(c, hipMemsetAsync(S.in_scan.p, 0, 8, st));
     if (xin) hipLaunchKernelGGL(k_sh_in_flags, dim3(blocks(xin)), dim3(T), 0, st, s, S.xall.as<const WgXEnt>(), xin,
                                 S.in_scan.as<uint32_t>());
@@ -622,7 +622,7 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     WG_ALLOC(c, S.prow, El * 4 + 4);
     WG_ALLOC(c, S.xcnt, (nl + 2) * 4);
     WG_ALLOC(c, S.flags, 64);
-    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(nl + 2));
+    { const int _sr = wg_scan_reserve(c, nl + 2); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "hash_join");
     WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8, st));
     WG_HIP(c, hipMemsetAsync(S.ptable.p, 0xFF, pcap * 8, st));
@@ -707,7 +707,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_ALLOC(c, S.xt, L * 4 + 16);         // row per record
         WG_ALLOC(c, S.xtok, (L + 2) * 4);      // crossing flag -> position
         WG_ALLOC(c, S.refx, El * 4 + 4);
-        WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(L + 2));
+        { const int _sr = wg_scan_reserve(c, L + 2); if (_sr != WG_OK) return _sr; }
         WG_HIP(c, hipMemsetAsync(S.xtok.p, 0, 8, st));
         if (L) hipLaunchKernelGGL(k_sh_combine, dim3(blocks(L)), dim3(T), 0, st, SF, L, S.unres.as<const uint32_t>(),
                                   S.xt.as<int32_t>(), S.xtok.as<uint32_t>(), S.flags.as<uint32_t>() + 4);

@@ -245,7 +245,7 @@ int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, 
     if ('?' < F.first_char || '?' - F.first_char >= F.glyphs.size())
         return wg_fail(c, WG_E_UNSUPPORTED, "atlas lacks '?' (the substitute glyph)");
     WG_ALLOC(c, c->text_off, (rows + 2) * 8);
-    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(rows + 2));
+    { const int _sr = wg_scan_reserve(c, rows + 2); if (_sr != WG_OK) return _sr; }
     c->text_rb = rb;
     c->text_re = re;
     c->n_quads = 0;

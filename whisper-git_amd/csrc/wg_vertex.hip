@@ -311,7 +311,7 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const uint64_t rows = re - rb;
     hipStream_t s = c->stream;
     WG_ALLOC(c, c->vtx_off, (rows + 2) * 8);
-    WG_ALLOC(c, c->scan_tmp, wg_scan_tmp_bytes(rows + 2));
+    { const int _sr = wg_scan_reserve(c, rows + 2); if (_sr != WG_OK) return _sr; }
     c->vrow_begin = rb;
     c->vrow_end = re;
     c->selected = sel;
