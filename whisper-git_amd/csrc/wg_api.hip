@@ -37,6 +37,36 @@ void wg_stage_end(wg_ctx *c) {
     if (idx >= 0) (void)hipEventRecord(c->stages[idx].b, c->stream);
 }
 
+namespace {
+struct FetchArgs { const void *p[16]; uint32_t wide, n; };
+__global__ void k_fetch(FetchArgs a, unsigned long long *out) {
+    const uint32_t i = threadIdx.x;
+    if (i < a.n) out[i] = ((a.wide >> i) & 1u) ? *reinterpret_cast<const unsigned long long *>(a.p[i])
+                                               : (unsigned long long)*reinterpret_cast<const uint32_t *>(a.p[i]);
+    __threadfence_system();
+}
+}  // namespace
+
+int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out) {
+    if (items.size() > 16) return wg_fail(c, WG_E_INVALID, "wg_fetch: too many items");
+    if (!c->h_fetch) {
+        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, 16 * sizeof(uint64_t), hipHostMallocMapped));
+        WG_HIP(c, hipHostGetDevicePointer((void **)&c->d_fetch, c->h_fetch, 0));
+    }
+    FetchArgs a{};
+    a.n = 0;
+    for (const WgFetch &f : items) {
+        a.p[a.n] = f.p;
+        if (f.wide) a.wide |= 1u << a.n;
+        a.n++;
+    }
+    hipLaunchKernelGGL(k_fetch, dim3(1), dim3(64), 0, c->stream, a, (unsigned long long *)c->d_fetch);
+    WG_HIP(c, hipGetLastError());
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < a.n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[i];
+    return WG_OK;
+}
+
 extern "C" {
 
 int wg_abi_version(void) { return WGRAPH_ABI_VERSION; }
@@ -88,6 +118,7 @@ void wg_destroy(wg_ctx *c) {
         if (c->stages[i].a) (void)hipEventDestroy(c->stages[i].a);
         if (c->stages[i].b) (void)hipEventDestroy(c->stages[i].b);
     }
+    if (c->h_fetch) (void)hipHostFree(c->h_fetch);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -19,6 +19,8 @@
 //
 // Bit-exact f32: built with -ffp-contract=off and the exact operation order
 // of Cubic::y_at (:623-629), split's lerp (:657) and `dy * 0.4` (:557-562).
+#include <cstring>
+
 #include "wg_internal.h"
 
 namespace {
@@ -518,11 +520,11 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     hipLaunchKernelGGL(k_carry_counts, dim3(blocks(nch)), dim3(T), 0, s, nch, c->carry_cnt.as<const uint32_t>(),
                        c->carry_off.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(c->carry_off.as<uint32_t>(), c->carry_off.as<uint32_t>(), nch, c->scan_tmp.p, s));
-    uint32_t tot[3] = {0, 0, 0};
-    WG_HIP(c, hipMemcpyAsync(&tot[0], voff + n, 4, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipMemcpyAsync(&tot[1], coff + n, 4, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipMemcpyAsync(&tot[2], c->carry_off.as<uint32_t>() + nch, 4, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipStreamSynchronize(s));
+    uint64_t tot[3] = {0, 0, 0};
+    {
+        const int rc = wg_fetch(c, {{voff + n, false}, {coff + n, false}, {c->carry_off.as<uint32_t>() + nch, false}}, tot);
+        if (rc != WG_OK) return rc;
+    }
     wg_stage_end(c);
     c->n_vert = tot[0];
     c->n_curve = tot[1];
@@ -567,15 +569,14 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
                            c->curve_color.as<uint8_t>());
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
-    uint32_t err = 0;
-    WG_HIP(c, hipMemcpyAsync(&err, c->sweep_err.p, 4, hipMemcpyDeviceToHost, s));
-    float total = 0.0f;
-    WG_HIP(c, hipMemcpyAsync(&total, rt + n, 4, hipMemcpyDeviceToHost, s));
-    uint32_t rtf[4] = {0, 0, 0, 0};
-    WG_HIP(c, hipMemcpyAsync(rtf, c->rt_flags.p, 16, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipStreamSynchronize(s));
-    if (err) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP);
-    c->total_height = total;
-    c->scan_path = rtf[2] ? 1u : 0u;
+    uint64_t fin[3] = {0, 0, 0};
+    {
+        const int rc = wg_fetch(c, {{c->sweep_err.p, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false}}, fin);
+        if (rc != WG_OK) return rc;
+    }
+    if (fin[0]) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP);
+    const uint32_t tbits = (uint32_t)fin[1];
+    std::memcpy(&c->total_height, &tbits, 4);
+    c->scan_path = fin[2] ? 1u : 0u;
     return WG_OK;
 }

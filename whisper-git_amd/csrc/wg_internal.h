@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <string>
 #include <vector>
+#include <initializer_list>
 
 #include "wgraph.h"
 
@@ -202,7 +203,15 @@ struct wg_ctx {
     int        stage_stack[8] = {0};
     int        stage_depth = 0;
     uint64_t   scratch_host[16];
+    uint64_t  *h_fetch = nullptr;   // mapped pinned host memory for wg_fetch
+    uint64_t  *d_fetch = nullptr;
 };
+
+// small device -> host reads (wg_api.hip): one tiny kernel writes the values
+// into mapped pinned host memory, then the stream is synchronised — instead of
+// one blit per hipMemcpyAsync into pageable memory
+struct WgFetch { const void *p; bool wide; };   // wide: 8-byte value, else 4-byte
+int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out);
 
 // error helpers -------------------------------------------------------------
 int wg_fail(wg_ctx *c, int code, const char *fmt, ...);
@@ -237,7 +246,7 @@ hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, 
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
 int wg_stage_lanes(wg_ctx *c);                // wg_lanes.hip
 int wg_lanes_fast(wg_ctx *c, bool *used);     // wg_lanes_fast.hip
-hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *aux,
+hipError_t wg_lane_replay(wg_ctx *c, hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *aux,
                           uint8_t *slots_a, uint8_t *slots_b, unsigned long long *occ_a, unsigned long long *occ_b,
                           uint32_t *stats, uint32_t *flags, uint32_t max_iters, uint32_t *scal, uint8_t **slot_out,
                           uint32_t *iters);  // wg_lanes_replay.hip

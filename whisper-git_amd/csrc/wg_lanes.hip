@@ -217,18 +217,19 @@ int wg_stage_lanes(wg_ctx *c) {
         WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, c->stream));
     }
     WG_HIP(c, launch_general<1>(c));
-    uint32_t sc[4];
-    WG_HIP(c, hipMemcpyAsync(sc, c->lane_scalars.p, 16, hipMemcpyDeviceToHost, c->stream));
-    WG_HIP(c, hipStreamSynchronize(c->stream));
+    const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
+    uint64_t sc[3];
+    int frc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc);
+    if (frc != WG_OK) return frc;
     if (sc[2]) {   // more than 64 slots: rerun with the wide slot table
         WG_HIP(c, launch_general<LANE_NCH_MAX>(c));
-        WG_HIP(c, hipMemcpyAsync(sc, c->lane_scalars.p, 16, hipMemcpyDeviceToHost, c->stream));
-        WG_HIP(c, hipStreamSynchronize(c->stream));
+        frc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc);
+        if (frc != WG_OK) return frc;
         if (sc[2]) return wg_fail(c, WG_E_UNSUPPORTED, "lane table exceeds %d slots", LANE_NCH_MAX * 64);
     }
     wg_stage_end(c);
-    c->max_lane = sc[0];
-    c->n_slots = sc[1];
+    c->max_lane = (uint32_t)sc[0];
+    c->n_slots = (uint32_t)sc[1];
     uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
     float gw = (float)vis * WG_LANE_W;                 // graph_width (:353-354)
     c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
@@ -253,9 +254,11 @@ int wg_stage_edges(wg_ctx *c) {
                        c->edge_cnt.as<uint32_t>(), c->d_poff, c->prow.as<const int32_t>());
     WG_HIP(c, hipGetLastError());
     WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), n, c->scan_tmp.p, c->stream));
-    uint32_t ne = 0;
-    WG_HIP(c, hipMemcpyAsync(&ne, c->edge_cnt.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, c->stream));
-    WG_HIP(c, hipStreamSynchronize(c->stream));
+    uint64_t ne = 0;
+    {
+        const int rc = wg_fetch(c, {{c->edge_cnt.as<uint32_t>() + n, false}}, &ne);
+        if (rc != WG_OK) return rc;
+    }
     c->n_edges = ne;
     WG_ALLOC(c, c->edges, (uint64_t)ne * sizeof(wg_edge) + 16);
     hipLaunchKernelGGL(k_edges, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->edge_cnt.as<const uint32_t>(),

@@ -335,13 +335,14 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, uint32_t *viol, uint64_t *nev, uint6
                               fpc.as<const uint32_t>(), winfo.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(ev_off.as<uint32_t>(), ev_off.as<uint32_t>(), n, c->scan_tmp.p, s));
     WG_HIP(c, wg_exclusive_scan_u32(aux_off.as<uint32_t>(), aux_off.as<uint32_t>(), n, c->scan_tmp.p, s));
-    uint32_t hdr[3] = {0, 0, 0};
-    WG_HIP(c, hipMemcpyAsync(&hdr[0], flags.p, 4, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipMemcpyAsync(&hdr[1], ev_off.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipMemcpyAsync(&hdr[2], aux_off.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipStreamSynchronize(s));
+    uint64_t hdr[3] = {0, 0, 0};
+    {
+        const int rc = wg_fetch(c, {{flags.p, false}, {ev_off.as<uint32_t>() + n, false}, {aux_off.as<uint32_t>() + n, false}},
+                                hdr);
+        if (rc != WG_OK) return rc;
+    }
     wg_stage_end(c);
-    *viol = hdr[0];
+    *viol = (uint32_t)hdr[0];
     *nev = hdr[1];
     *naux = hdr[2];
     return WG_OK;
@@ -435,7 +436,7 @@ int wg_lf_replay(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, 
     WG_ALLOC(c, rflags, (max_iters + 2) * 4);
     uint8_t *out = nullptr;
     uint32_t iters = 0;
-    WG_HIP(c, wg_lane_replay(s, nev, chunk, ev, aux, slot_a.as<uint8_t>(), slot_b.as<uint8_t>(),
+    WG_HIP(c, wg_lane_replay(c, s, nev, chunk, ev, aux, slot_a.as<uint8_t>(), slot_b.as<uint8_t>(),
                              occ.as<unsigned long long>(), occ.as<unsigned long long>() + nch, stats.as<uint32_t>(),
                              rflags.as<uint32_t>(), max_iters, c->lane_scalars.as<uint32_t>(), &out, &iters));
     c->replay_iters = iters;
@@ -479,12 +480,12 @@ int wg_lanes_fast(wg_ctx *c, bool *used) {
     if ((rc = wg_lf_replay(c, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(), &slots, &conv)) != WG_OK) return rc;
     if (!conv) return WG_OK;                         // no fixed point within budget: general walk
     if ((rc = wg_lf_lanes(c, R, slots, c->lane_asg.as<uint32_t>())) != WG_OK) return rc;
-    uint32_t sc[4];
-    WG_HIP(c, hipMemcpyAsync(sc, c->lane_scalars.p, 16, hipMemcpyDeviceToHost, c->stream));
-    WG_HIP(c, hipStreamSynchronize(c->stream));
+    const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
+    uint64_t sc[3];
+    if ((rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc)) != WG_OK) return rc;
     if (sc[2]) return WG_OK;                        // more than 63 slots: general walk
-    c->max_lane = sc[0];
-    c->n_slots = sc[1];
+    c->max_lane = (uint32_t)sc[0];
+    c->n_slots = (uint32_t)sc[1];
     c->lane_path = 0;
     *used = true;
     return WG_OK;

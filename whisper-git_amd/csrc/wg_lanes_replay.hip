@@ -209,7 +209,7 @@ __global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict_
 // workspaces: slots (2 x (nev + 64) bytes), occ (2 x nchunks x 8 bytes),
 // stats (2 x nchunks x 4 bytes), flags (max_iters + 1 words).
 // Returns the number of iterations used (0 on a HIP error) in *iters.
-hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *aux,
+hipError_t wg_lane_replay(wg_ctx *c, hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *aux,
                           uint8_t *slots_a, uint8_t *slots_b, unsigned long long *occ_a, unsigned long long *occ_b,
                           uint32_t *stats, uint32_t *flags, uint32_t max_iters, uint32_t *scal, uint8_t **slot_out,
                           uint32_t *iters) {
@@ -239,11 +239,8 @@ hipError_t wg_lane_replay(hipStream_t s, uint64_t nev, uint32_t chunk, const uin
         // poll at iterations 3, 6, 12, 24, ... (launches after a fixed point exit at once)
         if (it == next_poll || it == max_iters) {
             next_poll *= 2;
-            uint32_t fl[2] = {1, 1};
-            e = hipMemcpyAsync(fl, flags + it - 1, 8, hipMemcpyDeviceToHost, s);
-            if (e != hipSuccess) return e;
-            e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return e;
+            uint64_t fl[2] = {1, 1};
+            if (wg_fetch(c, {{flags + it - 1, false}, {flags + it, false}}, fl) != WG_OK) return hipErrorUnknown;
             done_check = it;
             if (fl[0] == 0 || fl[1] == 0) { *iters = it; break; }
         }

@@ -255,8 +255,8 @@ int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, 
         hipLaunchKernelGGL(k_text_rows<false>, dim3(blocks(rows)), dim3(T), 0, s, A, c->text_off.as<uint64_t>(),
                            (const uint64_t *)nullptr, (uint4 *)nullptr);
         WG_HIP(c, wg_exclusive_scan_u64(c->text_off.as<uint64_t>(), c->text_off.as<uint64_t>(), rows, c->scan_tmp.p, s));
-        WG_HIP(c, hipMemcpyAsync(&nq, c->text_off.as<uint64_t>() + rows, 8, hipMemcpyDeviceToHost, s));
-        WG_HIP(c, hipStreamSynchronize(s));
+        const int frc = wg_fetch(c, {{c->text_off.as<uint64_t>() + rows, true}}, &nq);
+        if (frc != WG_OK) return frc;
         WG_ALLOC(c, c->text_rec, nq * 16 + 16);
         hipLaunchKernelGGL(k_text_rows<true>, dim3(blocks(rows)), dim3(T), 0, s, A, (uint64_t *)nullptr,
                            (const uint64_t *)c->text_off.as<uint64_t>(), c->text_rec.as<uint4>());

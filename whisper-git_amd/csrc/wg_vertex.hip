@@ -326,8 +326,10 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
                        c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off);
     WG_HIP(c, wg_exclusive_scan_u64(off, off, rows, c->scan_tmp.p, s));
     uint64_t total = 0;
-    WG_HIP(c, hipMemcpyAsync(&total, off + rows, 8, hipMemcpyDeviceToHost, s));
-    WG_HIP(c, hipStreamSynchronize(s));
+    {
+        const int rc = wg_fetch(c, {{off + rows, true}}, &total);
+        if (rc != WG_OK) return rc;
+    }
     c->n_vtx = total;
     WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
     float q = roundf(c->graph_width / WG_LANE_W);
@@ -359,11 +361,7 @@ int wg_words_checksum(wg_ctx *c, const uint32_t *w, uint64_t nw, uint64_t *out) 
         hipLaunchKernelGGL(k_checksum, dim3(b), dim3(256), 0, c->stream, w, nw, c->chk.as<unsigned long long>());
         WG_HIP(c, hipGetLastError());
     }
-    uint64_t v = 0;
-    WG_HIP(c, hipMemcpyAsync(&v, c->chk.p, 8, hipMemcpyDeviceToHost, c->stream));
-    WG_HIP(c, hipStreamSynchronize(c->stream));
-    *out = v;
-    return WG_OK;
+    return wg_fetch(c, {{c->chk.p, true}}, out);
 }
 
 int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out) {
