@@ -38,26 +38,31 @@ void wg_stage_end(wg_ctx *c) {
 }
 
 namespace {
-struct FetchArgs { const void *p[16]; uint32_t wide, n; };
+constexpr int FETCH_MAX = 64;
+struct FetchArgs { const void *p[FETCH_MAX]; unsigned long long wide; uint32_t n; };
 __global__ void k_fetch(FetchArgs a, unsigned long long *out) {
     const uint32_t i = threadIdx.x;
-    if (i < a.n) out[i] = ((a.wide >> i) & 1u) ? *reinterpret_cast<const unsigned long long *>(a.p[i])
-                                               : (unsigned long long)*reinterpret_cast<const uint32_t *>(a.p[i]);
+    if (i < a.n) out[i] = ((a.wide >> i) & 1ull) ? *reinterpret_cast<const unsigned long long *>(a.p[i])
+                                                 : (unsigned long long)*reinterpret_cast<const uint32_t *>(a.p[i]);
     __threadfence_system();
 }
 }  // namespace
 
 int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out) {
-    if (items.size() > 16) return wg_fail(c, WG_E_INVALID, "wg_fetch: too many items");
+    return wg_fetch_n(c, (int)items.size(), items.begin(), out);
+}
+
+int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out) {
+    if (n < 0 || n > FETCH_MAX) return wg_fail(c, WG_E_INVALID, "wg_fetch: too many items");
     if (!c->h_fetch) {
-        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, 16 * sizeof(uint64_t), hipHostMallocMapped));
+        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, FETCH_MAX * sizeof(uint64_t), hipHostMallocMapped));
         WG_HIP(c, hipHostGetDevicePointer((void **)&c->d_fetch, c->h_fetch, 0));
     }
     FetchArgs a{};
     a.n = 0;
-    for (const WgFetch &f : items) {
-        a.p[a.n] = f.p;
-        if (f.wide) a.wide |= 1u << a.n;
+    for (int i = 0; i < n; i++) {
+        a.p[a.n] = items[i].p;
+        if (items[i].wide) a.wide |= 1ull << a.n;
         a.n++;
     }
     hipLaunchKernelGGL(k_fetch, dim3(1), dim3(64), 0, c->stream, a, (unsigned long long *)c->d_fetch);

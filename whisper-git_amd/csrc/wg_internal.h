@@ -212,6 +212,7 @@ struct wg_ctx {
 // one blit per hipMemcpyAsync into pageable memory
 struct WgFetch { const void *p; bool wide; };   // wide: 8-byte value, else 4-byte
 int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out);
+int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out);   // n <= 64
 
 // error helpers -------------------------------------------------------------
 int wg_fail(wg_ctx *c, int code, const char *fmt, ...);

@@ -420,8 +420,14 @@ static Sections make_sections(const void *gathered, uint64_t stride, int world, 
 static int read_headers(wg_ctx *c, const void *gathered, uint64_t stride, std::vector<uint32_t> &hdr) {
     const int W = c->sh.world;
     hdr.assign((size_t)W * 4, 0);
-    WG_HIP(c, hipMemcpy2DAsync(hdr.data(), 16, gathered, stride, 16, W, hipMemcpyDeviceToHost, c->stream));
-    WG_HIP(c, hipStreamSynchronize(c->stream));
+    WgFetch it[64];
+    for (int r = 0; r < W; r++)
+        for (int k = 0; k < 3; k++) it[3 * r + k] = WgFetch{(const uint8_t *)gathered + r * stride + 4 * k, false};
+    uint64_t v[64];
+    const int rc = wg_fetch_n(c, 3 * W, it, v);
+    if (rc != WG_OK) return rc;
+    for (int r = 0; r < W; r++)
+        for (int k = 0; k < 3; k++) hdr[4 * r + k] = (uint32_t)v[3 * r + k];
     return WG_OK;
 }
 
@@ -527,10 +533,9 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     hipLaunchKernelGGL(k_sh_own_counts, dim3(blocks(nloc)), dim3(T), 0, st, s, nl, c->d_poff, prow,
                        S.in_scan.as<const uint32_t>(), xin, c->edge_cnt.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), nloc, c->scan_tmp.p, st));
-    uint32_t tot[2] = {0, 0};
-    WG_HIP(c, hipMemcpyAsync(&tot[0], c->edge_cnt.as<uint32_t>() + nloc, 4, hipMemcpyDeviceToHost, st));
-    WG_HIP(c, hipMemcpyAsync(&tot[1], c->edge_cnt.as<uint32_t>() + 1, 4, hipMemcpyDeviceToHost, st));
-    WG_HIP(c, hipStreamSynchronize(st));
+    uint64_t tot[2] = {0, 0};
+    if ((rc = wg_fetch(c, {{c->edge_cnt.as<uint32_t>() + nloc, false}, {c->edge_cnt.as<uint32_t>() + 1, false}}, tot)) != WG_OK)
+        return rc;
     const uint64_t ne = tot[0], n_in = tot[1];
     WG_ALLOC(c, c->edges, ne * sizeof(wg_edge) + 16);
     WG_ALLOC(c, S.edge_y, ne * 8 + 16);
@@ -601,11 +606,10 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     c->n = N;
     c->e_refs = S.Etot;
     hipStream_t st = c->stream;
-    uint32_t eo[2] = {0, 0};
+    uint64_t eo[2] = {0, 0};
     if (N) {
-        WG_HIP(c, hipMemcpyAsync(&eo[0], c->d_poff + row_begin, 4, hipMemcpyDeviceToHost, st));
-        WG_HIP(c, hipMemcpyAsync(&eo[1], c->d_poff + row_end, 4, hipMemcpyDeviceToHost, st));
-        WG_HIP(c, hipStreamSynchronize(st));
+        const int frc = wg_fetch(c, {{c->d_poff + row_begin, false}, {c->d_poff + row_end, false}}, eo);
+        if (frc != WG_OK) return frc;
     }
     S.E0 = eo[0];
     S.E1 = eo[1];
@@ -635,17 +639,19 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
                                c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>(),
                                S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(S.xcnt.as<uint32_t>(), S.xcnt.as<uint32_t>(), nl, c->scan_tmp.p, st));
-    uint32_t h[3] = {0, 0, 0};
-    WG_HIP(c, hipMemcpyAsync(h, S.flags.p, 8, hipMemcpyDeviceToHost, st));
-    WG_HIP(c, hipMemcpyAsync(&h[2], S.xcnt.as<uint32_t>() + nl, 4, hipMemcpyDeviceToHost, st));
-    WG_HIP(c, hipStreamSynchronize(st));
+    uint64_t h[3] = {0, 0, 0};
+    {
+        const int frc = wg_fetch(c, {{S.flags.as<uint32_t>(), false}, {S.flags.as<uint32_t>() + 1, false},
+                                     {S.xcnt.as<uint32_t>() + nl, false}}, h);
+        if (frc != WG_OK) return frc;
+    }
     c->hcap = cap;
     S.n_unres = h[2];
     S.step = SH_X1;
     // X1: {violation | duplicate, n} + one 32-byte record per unresolved reference, row order
     int rc = sh_send(c, 16 + (uint64_t)h[2] * 32, out);
     if (rc != WG_OK) return rc;
-    uint32_t hdr[4] = {h[0] | h[1], h[2], 0, 0};
+    uint32_t hdr[4] = {(uint32_t)(h[0] | h[1]), (uint32_t)h[2], 0, 0};
     WG_HIP(c, hipMemcpyAsync(S.msg.p, hdr, 16, hipMemcpyHostToDevice, st));
     if (nl) hipLaunchKernelGGL(k_sh_pack_unres, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid, S.E0,
                                S.prow.as<const int32_t>(), S.xcnt.as<const uint32_t>(),
@@ -712,11 +718,13 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         if (L) hipLaunchKernelGGL(k_sh_combine, dim3(blocks(L)), dim3(T), 0, st, SF, L, S.unres.as<const uint32_t>(),
                                   S.xt.as<int32_t>(), S.xtok.as<uint32_t>(), S.flags.as<uint32_t>() + 4);
         WG_HIP(c, wg_exclusive_scan_u32(S.xtok.as<uint32_t>(), S.xtok.as<uint32_t>(), L, c->scan_tmp.p, st));
-        std::vector<uint32_t> xb(W + 2, 0);
-        for (int r = 0; r <= W; r++)
-            WG_HIP(c, hipMemcpyAsync(&xb[r], S.xtok.as<uint32_t>() + S.uoffs[r], 4, hipMemcpyDeviceToHost, st));
-        WG_HIP(c, hipMemcpyAsync(&xb[W + 1], S.flags.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, st));
-        WG_HIP(c, hipStreamSynchronize(st));
+        uint64_t xb[20] = {0};
+        {
+            WgFetch it[20];
+            for (int r = 0; r <= W; r++) it[r] = WgFetch{S.xtok.as<uint32_t>() + S.uoffs[r], false};
+            it[W + 1] = WgFetch{S.flags.as<uint32_t>() + 4, false};
+            if ((rc = wg_fetch_n(c, W + 2, it, xb)) != WG_OK) return rc;
+        }
         if (xb[W + 1]) return sh_fallback(c, out);   // a parent at an earlier row: every rank sees it
         S.xoff.assign(W + 1, 0);
         for (int r = 0; r <= W; r++) S.xoff[r] = xb[r];
@@ -807,12 +815,12 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_ALLOC(c, c->lane_asg, nl * 4 + 4);
         LfRange R = sh_range(c);
         if ((rc = wg_lf_lanes(c, R, slots, c->lane_asg.as<uint32_t>())) != WG_OK) return rc;
-        uint32_t sc[4];
-        WG_HIP(c, hipMemcpyAsync(sc, c->lane_scalars.p, 16, hipMemcpyDeviceToHost, st));
-        WG_HIP(c, hipStreamSynchronize(st));
+        const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
+        uint64_t sc[3];
+        if ((rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc)) != WG_OK) return rc;
         if (sc[2]) return sh_fallback(c, out);      // more than 63 slots: same decision on every rank
-        c->max_lane = sc[0];
-        c->n_slots = sc[1];
+        c->max_lane = (uint32_t)sc[0];
+        c->n_slots = (uint32_t)sc[1];
         c->lane_path = 0;
         const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
         const float gw = (float)vis * WG_LANE_W;
