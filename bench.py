@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=1_000_000, help="rows of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the glyph-quad and font-atlas side measurements")
+    ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (host-input rate, glyph quads, font atlas)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (host rehearsal)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     return ap.parse_args()
@@ -280,7 +280,7 @@ def main():
     # SoA and bands start in pinned-less host memory, so the step includes the
     # PCIe H2D copies; vertex buffers still land in HBM
     host_rate = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_extras:
         host_commits = abi.commits_struct(dag)
         band_host = np.ascontiguousarray(dag.band)
 

@@ -79,7 +79,7 @@ def main():
     timed = windows[-5:] if len(windows) >= 5 else windows
 
     vtx = next((r for r in stats if short(r["Name"]) == KERNEL), None)
-    lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py --steps 5 --warmup 2 --no-cpu`", ""]
+    lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py --steps 5 --warmup 2 --no-cpu --no-extras`", ""]
     if bench:
         lines += [f"bench line under the profiler: value {bench['value']:.4g} {bench['unit']}, "
                   f"{bench['ms_per_step']} ms/step, workload: {bench['config']['workload']}", ""]
