@@ -101,10 +101,10 @@ void wg_destroy(wg_ctx *c) {
     DevBuf *bufs[] = {&c->in_oid, &c->in_time, &c->in_poff, &c->in_poid, &c->in_flags, &c->hash, &c->canon,
                       &c->prow, &c->lane_asg, &c->lane_out, &c->color_out, &c->lane_scalars, &c->edge_cnt,
                       &c->edges, &c->heights, &c->band, &c->g_height, &c->g_node_y, &c->g_row_top,
-                      &c->rt_chunk, &c->rt_tables, &c->rt_sup, &c->rt_flags, &c->cntF, &c->cntT, &c->cntB, &c->cntC,
-                      &c->cntCend, &c->vert_off, &c->curve_off, &c->vert, &c->curve, &c->curve_color,
-                      &c->curve_ref, &c->curve_row, &c->top_fill, &c->carry_cnt, &c->carry_off, &c->carry,
-                      &c->scan_tmp, &c->scal, &c->rowflags, &c->carry_fill, &c->sweep_err, &c->sweep_big, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
+                      &c->rt_chunk, &c->rt_tables, &c->rt_sup, &c->rt_flags, &c->geom_zero,
+                      &c->vert_off, &c->curve_off, &c->vert, &c->curve, &c->curve_color,
+                      &c->curve_ref, &c->curve_row, &c->carry_off, &c->carry,
+                      &c->scan_tmp, &c->scal, &c->rowflags, &c->sweep_big, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
     for (DevBuf *b : bufs) b->release();
     for (DevBuf &b : c->lf) b.release();
     ShardState &S = c->sh;
@@ -414,7 +414,12 @@ int wg_emit_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel, const flo
     (void)hipSetDevice(c->device);
     c->have_vtx = false;
     WG_ALLOC(c, c->palette, WG_PALETTE_SIZE * 4 * sizeof(float));
-    WG_HIP(c, hipMemcpyAsync(c->palette.p, palette, WG_PALETTE_SIZE * 4 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if (!c->palette_valid || std::memcmp(c->palette_host, palette, sizeof(c->palette_host)) != 0) {   // upload on change only
+        std::memcpy(c->palette_host, palette, sizeof(c->palette_host));
+        WG_HIP(c, hipMemcpyAsync(c->palette.p, c->palette_host, sizeof(c->palette_host), hipMemcpyHostToDevice, c->stream));
+        WG_HIP(c, hipStreamSynchronize(c->stream));   // palette_host may change before the copy ran
+        c->palette_valid = true;
+    }
     // global rows -> the context's row arrays (a shard's rows start at row_base)
     const uint64_t b = S.row_base;
     const int64_t sel_l = (sel >= 0 && (uint64_t)sel >= S.s && (uint64_t)sel < S.e) ? (int64_t)((uint64_t)sel - S.s + b) : -1;

@@ -465,16 +465,9 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     WG_ALLOC(c, c->g_height, n * 4 + 4);
     WG_ALLOC(c, c->g_node_y, n * 4 + 4);
     WG_ALLOC(c, c->rowflags, n + 4);
-    WG_ALLOC(c, c->cntF, (n + 2) * 4);
-    WG_ALLOC(c, c->cntT, (n + 2) * 4);
-    WG_ALLOC(c, c->cntB, (n + 2) * 4);
-    WG_ALLOC(c, c->cntC, (n + 2) * 4);
-    WG_ALLOC(c, c->cntCend, (n + 2) * 4);
     WG_ALLOC(c, c->vert_off, (n + 2) * 4);
     WG_ALLOC(c, c->curve_off, (n + 2) * 4);
-    WG_ALLOC(c, c->top_fill, (n + 2) * 4);
     { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
-    WG_ALLOC(c, c->sweep_err, 64);
     c->n_vert = c->n_curve = 0;
     if (n == 0) {
         WG_HIP(c, hipMemsetAsync(c->vert_off.p, 0, 4, s));
@@ -485,18 +478,17 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     const float *rt = c->g_row_top.as<const float>();
     const wg_edge *E = c->edges.as<const wg_edge>();
     const uint32_t *edge_off = c->edge_cnt.as<const uint32_t>();
-    uint32_t *cntF = c->cntF.as<uint32_t>(), *cntT = c->cntT.as<uint32_t>(), *cntB = c->cntB.as<uint32_t>();
-    uint32_t *cntC = c->cntC.as<uint32_t>(), *cntCend = c->cntCend.as<uint32_t>();
+    // every counter array that starts at zero lives in one workspace: one memset
+    const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
+    const uint64_t rowa = (n + 2 + 63) & ~63ull, cha = (nch + 2 + 63) & ~63ull;
+    WG_ALLOC(c, c->geom_zero, (6 * rowa + 2 * cha + 64) * 4);
+    uint32_t *cntF = c->geom_zero.as<uint32_t>(), *cntT = cntF + rowa, *cntB = cntT + rowa;
+    uint32_t *cntC = cntB + rowa, *cntCend = cntC + rowa, *top_fill = cntCend + rowa;
+    uint32_t *carry_cnt = top_fill + rowa, *carry_fill = carry_cnt + cha, *sweep_err = carry_fill + cha;
     uint32_t *voff = c->vert_off.as<uint32_t>(), *coff = c->curve_off.as<uint32_t>();
 
     wg_stage_begin(c, "geom_counts");
-    WG_HIP(c, hipMemsetAsync(cntF, 0, (n + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(cntT, 0, (n + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(cntB, 0, (n + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(cntC, 0, (n + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(cntCend, 0, (n + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(c->top_fill.p, 0, (n + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(c->sweep_err.p, 0, 64, s));
+    WG_HIP(c, hipMemsetAsync(c->geom_zero.p, 0, (6 * rowa + 2 * cha + 64) * 4, s));
     hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
                        c->g_node_y.as<float>(), c->rowflags.as<uint8_t>());
     if (ne)
@@ -509,15 +501,10 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     WG_HIP(c, wg_exclusive_scan_u32(voff, voff, n, c->scan_tmp.p, s));
     WG_HIP(c, wg_exclusive_scan_u32(coff, coff, n, c->scan_tmp.p, s));
     // carry-in registration
-    const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
-    WG_ALLOC(c, c->carry_cnt, (nch + 2) * 4);
     WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
-    WG_ALLOC(c, c->carry_fill, (nch + 2) * 4);
-    WG_HIP(c, hipMemsetAsync(c->carry_cnt.p, 0, (nch + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(c->carry_fill.p, 0, (nch + 2) * 4, s));
-    if (ne) hipLaunchKernelGGL(k_carry_diff, dim3(blocks(ne)), dim3(T), 0, s, ne, E, c->carry_cnt.as<uint32_t>());
-    WG_HIP(c, wg_exclusive_scan_u32(c->carry_cnt.as<uint32_t>(), c->carry_cnt.as<uint32_t>(), nch + 1, c->scan_tmp.p, s));
-    hipLaunchKernelGGL(k_carry_counts, dim3(blocks(nch)), dim3(T), 0, s, nch, c->carry_cnt.as<const uint32_t>(),
+    if (ne) hipLaunchKernelGGL(k_carry_diff, dim3(blocks(ne)), dim3(T), 0, s, ne, E, carry_cnt);
+    WG_HIP(c, wg_exclusive_scan_u32(carry_cnt, carry_cnt, nch + 1, c->scan_tmp.p, s));
+    hipLaunchKernelGGL(k_carry_counts, dim3(blocks(nch)), dim3(T), 0, s, nch, (const uint32_t *)carry_cnt,
                        c->carry_off.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(c->carry_off.as<uint32_t>(), c->carry_off.as<uint32_t>(), nch, c->scan_tmp.p, s));
     uint64_t tot[3] = {0, 0, 0};
@@ -540,16 +527,16 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     uint32_t *vert = c->vert.as<uint32_t>();
     hipLaunchKernelGGL(k_bottom, dim3(blocks(n)), dim3(T), 0, s, n, edge_off, E, voff, cntF, cntT, vert);
     if (ne) {
-        hipLaunchKernelGGL(k_top_collect, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, c->top_fill.as<uint32_t>(), vert);
+        hipLaunchKernelGGL(k_top_collect, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, vert);
         hipLaunchKernelGGL(k_carry_fill, dim3(blocks(ne)), dim3(T), 0, s, ne, E, c->carry_off.as<const uint32_t>(),
-                           c->carry_fill.as<uint32_t>(), c->carry.as<uint32_t>());
+                           carry_fill, c->carry.as<uint32_t>());
     }
     hipLaunchKernelGGL(k_top_finish, dim3(blocks(n)), dim3(T), 0, s, n, E, voff, cntF, cntT, vert);
     uint32_t *carry_sorted = c->carry.as<uint32_t>() + ncarry + 2;
     hipLaunchKernelGGL(k_carry_sort, dim3(nch), dim3(64), 0, s, nch, c->carry_off.as<const uint32_t>(),
                        c->carry.as<const uint32_t>(), carry_sorted);
     // chunks too wide for the register sweep are listed in sweep_err[2..] and swept through LDS
-    uint32_t *big_n = c->sweep_err.as<uint32_t>() + 1;
+    uint32_t *big_n = sweep_err + 1;
     WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
     hipLaunchKernelGGL(k_sweep, dim3((nch + SW_WAVES - 1) / SW_WAVES), dim3(64 * SW_WAVES), 0, s, n, nch, E, edge_off,
                        c->carry_off.as<const uint32_t>(), (const uint32_t *)carry_sorted, c->rowflags.as<const uint8_t>(),
@@ -558,7 +545,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     hipLaunchKernelGGL(k_sweep_lds, dim3(64), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)c->sweep_big.as<uint32_t>(),
                        (const uint32_t *)big_n, E, edge_off, c->carry_off.as<const uint32_t>(),
                        (const uint32_t *)carry_sorted, c->rowflags.as<const uint8_t>(), voff, coff, vert,
-                       c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), c->sweep_err.as<uint32_t>());
+                       c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), sweep_err);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     wg_stage_begin(c, "geom_curves");
@@ -571,7 +558,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     wg_stage_end(c);
     uint64_t fin[3] = {0, 0, 0};
     {
-        const int rc = wg_fetch(c, {{c->sweep_err.p, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false}}, fin);
+        const int rc = wg_fetch(c, {{sweep_err, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false}}, fin);
         if (rc != WG_OK) return rc;
     }
     if (fin[0]) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP);

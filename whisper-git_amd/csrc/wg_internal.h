@@ -164,18 +164,15 @@ struct wg_ctx {
     DevBuf rt_tables;       // per-chunk transducer tables
     DevBuf rt_sup;          // super-chunk tables, binade bases and walk states
     DevBuf rt_flags;        // uint32 [4]
-    DevBuf cntF, cntT, cntB, cntC, cntCend; // uint32 [N+1] per-row counts / diff arrays
+    DevBuf geom_zero;       // zeroed per pass: per-row counts / diff arrays, top fill, carry counts, sweep flags
     DevBuf vert_off, curve_off;             // uint32 [N+1]
     DevBuf vert, curve, curve_color;
     DevBuf curve_ref;       // uint32 [n_curve] edge id per curve record
     DevBuf curve_row;       // uint32 [n_curve] row per curve record
-    DevBuf top_fill;        // uint32 [N]
-    DevBuf carry_cnt, carry_off, carry;     // sweep carry-in lists
+    DevBuf carry_off, carry;                // sweep carry-in lists
     DevBuf scan_tmp;        // scan workspace
     DevBuf scal;            // uint64 [16] device scalars (totals)
     DevBuf rowflags;        // uint8 [N] bit0 zero-height strip, bit1 child strip empty, bit2 parent strip empty
-    DevBuf carry_fill;      // uint32 [nch]
-    DevBuf sweep_err;       // uint32 [16]: [0] LDS sweep overflow, [1] chunks listed for the LDS sweep
     DevBuf sweep_big;       // uint32 [nch] chunks too wide for the register sweep
     uint32_t sweep_reg_cap = 512;   // edges per chunk the register sweep holds (WG_OPT_SWEEP_REG)
     const float *edge_y = nullptr;   // per edge {child_y, parent_y} override (row-sharded geometry), or null
@@ -186,6 +183,8 @@ struct wg_ctx {
     DevBuf vtx_off;         // uint64 [rows+1]
     DevBuf vtx;             // wg_vertex [n_vtx]
     DevBuf palette;         // float [32]
+    float   palette_host[WG_PALETTE_SIZE * 4];   // last uploaded palette
+    bool    palette_valid = false;
     DevBuf chk;             // uint64 [1]
     DevBuf tile_first;      // uint4 [tiles+1] per-tile record (first row, first vertical, first curve, straddles)
     // ---- host-side tables --------------------------------------------------------

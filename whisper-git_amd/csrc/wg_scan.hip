@@ -76,6 +76,33 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_down(const TI *in, TO *ou
     if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
 }
 
+// down-sweep whose block offset is the sum of the preceding tile sums,
+// reduced by the block itself (tile count <= SCAN_TILE): no separate scan of
+// the tile sums
+template <class TI, class TO>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_down2(const TI *in, TO *out, const TO *__restrict__ bsum, uint64_t n) {
+    TO pre = 0;
+    for (uint64_t b = threadIdx.x; b < blockIdx.x; b += SCAN_THREADS) pre += bsum[b];
+    TO ptot;
+    (void)block_excl_scan<TO>(pre, ptot);
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    TO v[SCAN_ITEMS];
+    TO s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        v[k] = (base + k < n) ? (TO)in[base + k] : (TO)0;
+        s += v[k];
+    }
+    TO tot;
+    TO run = block_excl_scan<TO>(s, tot) + ptot;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
+    }
+    if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
+}
+
 uint64_t nblocks(uint64_t n) { return n == 0 ? 1 : (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 template <class TO>
@@ -95,6 +122,10 @@ hipError_t scan_rec(const TI *in, TO *out, uint64_t n, char *tmp, hipStream_t s)
     TO *bsum = reinterpret_cast<TO *>(tmp);
     char *next = tmp + (((nb + 1) * sizeof(TO) + 255) & ~size_t(255));
     hipLaunchKernelGGL((k_scan_reduce<TI, TO>), dim3(nb), dim3(SCAN_THREADS), 0, s, in, bsum, n);
+    if (nb <= SCAN_TILE) {   // two launches: tile sums, then tiles with self-reduced offsets
+        hipLaunchKernelGGL((k_scan_down2<TI, TO>), dim3(nb), dim3(SCAN_THREADS), 0, s, in, out, (const TO *)bsum, n);
+        return hipGetLastError();
+    }
     hipError_t e = scan_rec<TO, TO>(bsum, bsum, nb, next, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_scan_down<TI, TO>), dim3(nb), dim3(SCAN_THREADS), 0, s, in, out, (const TO *)bsum, n);
