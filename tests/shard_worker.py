@@ -78,6 +78,15 @@ def run_case(eng, comm, torch, kind, n, seed, world, rank, errors):
     got = eng.geometry()
     for k, v in geometry_slice(og, s, e).items():
         same("band_" + k, got[k], v)
+    if n <= 100_000:   # fractional bands: the rounding regime of row_top inside every shard
+        fb = np.random.default_rng(seed).uniform(0, 40, d.n).astype(np.float32)
+        eng.shard_geometry(comm, band=fb)
+        ogf = o.row_geometry(fb)
+        got = eng.geometry()
+        for k, v in geometry_slice(ogf, s, e).items():
+            same("fband_" + k, got[k], v)
+        eng.shard_geometry(comm, band=d.band)
+        og = o.row_geometry(d.band)
     sel = (s + e) // 2 if e > s else -1
     eng.emit_vertices(s, e, selected=sel)
     ov, ooff = o.emit_vertices(s, e, selected=sel)

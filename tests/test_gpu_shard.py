@@ -51,5 +51,11 @@ def test_three_shards(tmp_path):
     run_world(3, "random13:20000:11,wide16:1000:12,linux:25000:13", tmp_path)
 
 
+def test_two_shards_row_top_beyond_2_25(tmp_path):
+    """1.4M linux-shaped rows: rank 1's row_top prefix crosses 2^24 and 2^25
+    (transducer walk over super-chunks) and its shard sums past 2^25."""
+    run_world(2, "linux:1400000:31", tmp_path)
+
+
 def test_four_shards_small(tmp_path):
     run_world(4, "wide16:4000:21,random13:64:22", tmp_path)
