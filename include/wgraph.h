@@ -263,9 +263,15 @@ int wg_shard_build_begin(wg_ctx *ctx, const wg_commits *commits, int world, int 
 int wg_shard_geometry_begin(wg_ctx *ctx, const float *band, int32_t band_residency, wg_shard_msg *out);
 /* Copy this rank's current message (device or host destination). */
 int wg_shard_copy_msg(wg_ctx *ctx, void *dst);
-/* Deliver the all-gathered messages; runs to the next exchange or the end. */
+/* Deliver the all-gathered messages; runs to the next exchange or the end.
+ * Every message starts with a 16-byte header; `heads` (may be NULL) is a host
+ * copy of them (rank r's at heads[4r..4r+3]) that saves the engine a device
+ * read when the transport already brought them to the host.  Reads of
+ * `gathered` may still be queued on the engine's stream when the call
+ * returns: keep the buffer until the next wg_shard_copy_msg returns (or
+ * wg_synchronize). */
 int wg_shard_exchange(wg_ctx *ctx, const void *gathered, uint64_t stride, const uint64_t *sizes,
-                      wg_shard_msg *out);
+                      const uint32_t *heads, wg_shard_msg *out);
 
 /* ---- SDF font atlas (legacy TextRenderer atlas, docs/render_engine.md:105-112;
  * frozen spec WG-SDF-1) -------------------------------------

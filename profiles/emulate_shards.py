@@ -1,0 +1,222 @@
+"""Emulate the N-GPU row-sharded bench step on ONE GPU, rank by rank.
+
+The driver runs the real multi-GPU bench (`torch.distributed.run ... bench.py
+--gpus N`); this script answers "what does each rank's step cost" before an
+8-GPU node is available.  N engines (one per emulated rank, each on its own
+stream and thread) run the same wg_shard_* protocol as bench.py's sharded
+step, but a lock lets only one rank use the GPU at a time: every segment of
+a rank's step (from one exchange to the next, ending in a stream sync) is
+timed alone.  The all-gathers are emulated by device copies outside the
+timed segments; their cost on xGMI is NOT measured here, only counted
+(exchanges per step, bytes per exchange).
+
+  rank time  = sum of its segments (build + geometry + emission)
+  step bound = max over ranks + exchanges x (RCCL all-gather latency)
+
+usage: python3 profiles/emulate_shards.py [--world 8] [--rows-per-rank 1000000]
+           [--kind wide16] [--steps 3] [--out profiles/r01_shard_emulation.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "whisper-git_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--rows-per-rank", type=int, default=1_000_000)
+    ap.add_argument("--kind", default="wide16")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import torch
+    import wgraph
+    from wgraph import abi, synth
+    from wgraph.shard import ShardComm
+
+    W, R = args.world, args.rows_per_rank
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    t0 = time.perf_counter()
+    dag = synth.generate(args.kind, W * R)
+    print(f"generated {args.kind} {dag.n} rows in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    keep = [torch.from_numpy(a).to(dev) for a in (dag.oid.reshape(-1), dag.time, dag.parent_off.view(np.int32),
+                                                   dag.parent_oid.reshape(-1), dag.flags, dag.band)]
+    commits = abi.Commits()
+    commits.n_commits, commits.n_parents = dag.n, dag.e
+    commits.oid, commits.time, commits.parent_off, commits.parent_oid, commits.flags = (t.data_ptr() for t in keep[:5])
+    commits.residency = abi.WG_DEVICE
+    band_ptr = keep[5].data_ptr()
+    pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
+
+    gpu = threading.Lock()
+    bar = threading.Barrier(W)
+    slots: list = [None] * W
+    seg = [[] for _ in range(W)]          # per rank: (label, seconds)
+    xlog = []                             # per exchange: (step, bytes per rank)
+
+    class EmuComm:
+        """Lock-step stand-in for ShardComm.allgather between W threads."""
+
+        def __init__(self, rank, eng, stream):
+            self.rank, self.eng, self.stream = rank, eng, stream
+            self.t = None
+            self.label = ""
+
+        def start(self, label):
+            gpu.acquire()
+            self.label = label
+            self.t = time.perf_counter()
+
+        def stop(self, final=False):
+            # between exchanges only the engine's main stream is drained (as
+            # wg_shard_copy_msg does); side-stream work may run on
+            if final:
+                self.eng.synchronize()
+            else:
+                self.stream.synchronize()
+            seg[self.rank].append((self.label, time.perf_counter() - self.t))
+            gpu.release()
+
+        def allgather(self, nbytes, fill, step=0):
+            cap = ShardComm.round_cap(nbytes)
+            with torch.cuda.stream(self.stream):
+                send = torch.zeros(cap, dtype=torch.uint8, device=dev)
+            if nbytes:
+                fill(send.data_ptr())
+            self.stop()
+            slots[self.rank] = (send, nbytes)
+            bar.wait()
+            stride = ShardComm.round_cap(max(s[1] for s in slots)) + ShardComm.HDR
+            if self.rank == 0:
+                xlog.append((step, [s[1] for s in slots]))
+            with gpu:
+                with torch.cuda.stream(self.stream):
+                    out = torch.zeros(W * stride, dtype=torch.uint8, device=dev)
+                    for r, (b, n) in enumerate(slots):
+                        if n:
+                            out[r * stride + ShardComm.HDR: r * stride + ShardComm.HDR + n].copy_(b[:n])
+                    # ShardComm brings every message's 16-byte header to the host with the sizes
+                    self.heads = np.ascontiguousarray(out.view(W, stride)[:, 16:32].cpu().numpy()).view(np.uint32)
+                self.stream.synchronize()
+            sizes = [s[1] for s in slots]
+            bar.wait()
+            self.start(self.label)
+            return out, ShardComm.HDR, stride, sizes
+
+    engines, streams = [], []
+    for r in range(W):
+        e = wgraph.Engine(0)
+        s = torch.cuda.Stream(dev)
+        e.set_stream(s.cuda_stream)
+        engines.append(e)
+        streams.append(s)
+
+    stage_ms = [dict() for _ in range(W)]
+    errors = []
+
+    def rank_main(r):
+        try:
+            eng = engines[r]
+            comm = EmuComm(r, eng, streams[r])
+            s0, s1 = r * R, min(dag.n, (r + 1) * R)
+            for it in range(args.steps + 1):
+                if it == 1:
+                    eng.enable_timing(True, reserve=64 * (args.steps + 1))
+                comm.start("build")
+                eng.shard_build(commits, W, r, s0, s1, comm)
+                comm.stop()
+                comm.start("geometry")
+                eng.shard_geometry(comm, device_ptr=band_ptr)
+                comm.stop()
+                comm.start("emit")
+                eng.emit_vertices(s0, s1, selected=s0 + 7, palette=pal)
+                comm.stop(final=True)
+                if it == 0:
+                    seg[r].clear()
+                    if r == 0:
+                        xlog.clear()
+                bar.wait()
+            for name, ms in eng.timings():
+                stage_ms[r][name] = stage_ms[r].get(name, 0.0) + ms / args.steps
+            eng.enable_timing(False)
+        except Exception as ex:   # surface worker failures in the main thread
+            errors.append((r, repr(ex)))
+            bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errors:
+        raise SystemExit(f"emulated rank failed: {errors}")
+
+    counters = [int(e.debug_counters()[5]) for e in engines]
+
+    # the single-GPU step on an R-row list of the same kind, for comparison
+    single = wgraph.Engine(0)
+    dag1 = synth.generate(args.kind, R)
+    k1 = [torch.from_numpy(a).to(dev) for a in (dag1.oid.reshape(-1), dag1.time, dag1.parent_off.view(np.int32),
+                                                 dag1.parent_oid.reshape(-1), dag1.flags, dag1.band)]
+    c1 = abi.Commits()
+    c1.n_commits, c1.n_parents = dag1.n, dag1.e
+    c1.oid, c1.time, c1.parent_off, c1.parent_oid, c1.flags = (t.data_ptr() for t in k1[:5])
+    c1.residency = abi.WG_DEVICE
+
+    def one():
+        single.build(commits=c1)
+        single.row_geometry(device_ptr=k1[5].data_ptr())
+        single.emit_vertices(0, R, selected=7, palette=pal)
+        single.synchronize()
+    one()
+    times = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        one()
+        times.append(time.perf_counter() - t0)
+    single_ms = 1e3 * float(np.median(times))
+
+    per_rank = []
+    for r in range(W):
+        tot = {}
+        nseg = len(seg[r]) // args.steps
+        for k in range(nseg):   # per segment: median over the steps
+            lab = seg[r][k][0]
+            tot[lab] = tot.get(lab, 0.0) + 1e3 * float(np.median([seg[r][k + j * nseg][1] for j in range(args.steps)]))
+        per_rank.append({"rank": r, "ms": round(sum(tot.values()), 4),
+                         **{k: round(v, 4) for k, v in tot.items()},
+                         "segments_per_step": len(seg[r]) // args.steps,
+                         "segment_ms": [round(1e3 * float(np.median([seg[r][k + j * (len(seg[r]) // args.steps)][1]
+                                                                   for j in range(args.steps)])), 4)
+                                        for k in range(len(seg[r]) // args.steps)],
+                         "mode": counters[r],
+                         "stages_ms": {k: round(v, 4) for k, v in sorted(stage_ms[r].items())}})
+    n_x = len(xlog) // args.steps
+    xbytes = {}
+    for step, sizes in xlog[:n_x]:
+        xbytes[f"X{step}" if step not in xbytes else f"X{step}b"] = sizes
+    worst = max(p["ms"] for p in per_rank)
+    res = {"world": W, "rows_per_rank": R, "kind": args.kind, "steps": args.steps,
+           "single_gpu_step_ms": round(single_ms, 4), "max_rank_ms_without_collectives": round(worst, 4),
+           "exchanges_per_step": n_x, "exchange_bytes_per_rank": xbytes,
+           "efficiency_without_collectives": round(single_ms / worst, 4), "ranks": per_rank}
+    print(json.dumps(res, indent=1))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

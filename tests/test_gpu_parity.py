@@ -206,6 +206,35 @@ def test_bands_with_fractional_and_negative_values(engine):
             assert_bits(k, got[k], og[k])
 
 
+def test_banded_passes_reuse_the_swept_lists(engine):
+    """Geometry passes on the same layout reuse the swept lists: the curve
+    superset is re-filtered only when a row's strip flags change (bands that
+    zero a row's height or put its node at the row's bottom).  Every pass must
+    equal the oracle's."""
+    from oracle import oracle_c
+    d = synth.generate("wide16", 30000, seed=9)
+    o = oracle_c.OracleLayout(d)
+    engine.build(d)
+    h = engine.row_heights()
+    rng = np.random.default_rng(3)
+    plain = rng.uniform(0, 20, d.n).astype(np.float32)
+    odd = plain.copy()
+    pick = rng.random(d.n) < 0.02
+    odd[pick] = -h[pick]                                  # zero-height rows
+    lift = (rng.random(d.n) < 0.02) & ~pick
+    odd[lift] = (6.0 - h[lift]).astype(np.float32)        # node below the row's bottom
+    engine.enable_timing(True, reserve=256)
+    for band in (plain, plain, odd, odd, plain, None):
+        engine.row_geometry(band)
+        og = o.row_geometry(band)
+        got = engine.geometry()
+        for k in ("row_top", "height", "node_y", "vert_off", "vert", "curve_off", "curve", "curve_color"):
+            assert_bits(k, got[k], og[k])
+    names = [n for n, _ in engine.timings()]
+    engine.enable_timing(False)
+    assert names.count("geom_reuse") == 6 and names.count("geom_lists") == 0
+
+
 def test_empty_and_single(engine):
     d = synth.generate("linear", 1)
     engine.build(d)

@@ -31,7 +31,7 @@ def _worker(rank, world, port, q):
             out, off, stride, sizes = comm.allgather(length, lambda ptr: ctypes.memmove(ptr, payload, length),
                                                      step=min(step, 3))
             got.append((stride, sizes, [bytes(out[off + r * stride:off + r * stride + sizes[r]].numpy())
-                                        for r in range(world)]))
+                                        for r in range(world)], comm.heads.tobytes()))
         q.put((rank, got, (comm.exchanges, comm.collectives)))
     finally:
         dist.destroy_process_group()
@@ -52,8 +52,10 @@ def test_allgather_world2_gloo():
                lambda r: 3000]
     for step, length_of in enumerate(lengths):
         for rank in range(world):
-            stride, sizes, msgs = res[rank][0][step]
+            stride, sizes, msgs, heads = res[rank][0][step]
             assert sizes == [length_of(r) for r in range(world)]
+            # host copy of each message's first 16 bytes (zero padded), handed to wg_shard_exchange
+            assert heads == b"".join((msgs[r][:16] + bytes(16))[:16] for r in range(world))
             assert stride % 16 == 0 and stride >= max(max(sizes), 16)
             for r in range(world):
                 assert msgs[r] == bytes((r * 31 + step + i) & 0xFF for i in range(length_of(r)))

@@ -48,6 +48,45 @@ __global__ void k_fetch(FetchArgs a, unsigned long long *out) {
 }
 }  // namespace
 
+int wg_side_fork(wg_ctx *c) {
+    if (!c->side) {
+        WG_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
+    if (const int rc = wg_side_join(c)) return rc;
+    WG_HIP(c, hipEventRecord(c->ev_fork, c->stream));
+    WG_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    c->side_main = c->stream;
+    c->stream = c->side;
+    return WG_OK;
+}
+
+void wg_side_done(wg_ctx *c) {
+    if (c->stream != c->side || !c->side_main) return;
+    const hipError_t e = hipEventRecord(c->ev_join, c->side);
+    c->stream = c->side_main;
+    c->side_main = nullptr;
+    if (e == hipSuccess) c->side_pending = true;
+    else (void)hipStreamSynchronize(c->side);   // no event: order by waiting
+}
+
+int wg_side_join(wg_ctx *c) {
+    if (!c->side_pending) return WG_OK;
+    c->side_pending = false;
+    WG_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    return WG_OK;
+}
+
+int wg_side_zero_rowtop(wg_ctx *c, uint64_t m, float *h, float *rt, uint64_t row_lo) {
+    int rc = wg_side_fork(c);
+    if (rc != WG_OK) return rc;
+    rc = wg_heights_run(c, m, c->n_list, h);
+    if (rc == WG_OK) rc = wg_rowtop_run(c, m, h, nullptr, rt, row_lo);
+    wg_side_done(c);
+    return rc;
+}
+
 int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out) {
     return wg_fetch_n(c, (int)items.size(), items.begin(), out);
 }
@@ -97,14 +136,17 @@ wg_ctx *wg_create(int device_ordinal) {
 void wg_destroy(wg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->side_main) c->stream = c->side_main;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     DevBuf *bufs[] = {&c->in_oid, &c->in_time, &c->in_poff, &c->in_poid, &c->in_flags, &c->hash, &c->canon,
                       &c->prow, &c->lane_asg, &c->lane_out, &c->color_out, &c->lane_scalars, &c->edge_cnt,
                       &c->edges, &c->heights, &c->band, &c->g_height, &c->g_node_y, &c->g_row_top,
                       &c->rt_chunk, &c->rt_tables, &c->rt_sup, &c->rt_flags, &c->geom_zero,
                       &c->vert_off, &c->curve_off, &c->vert, &c->curve, &c->curve_color,
                       &c->curve_ref, &c->curve_row, &c->carry_off, &c->carry,
-                      &c->scan_tmp, &c->scal, &c->rowflags, &c->sweep_big, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
+                      &c->scan_tmp, &c->scal, &c->rowflags, &c->rowflags_lists, &c->geom_diff, &c->scurve_off,
+                      &c->scurve_ref, &c->scurve_row, &c->sweep_big, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
     for (DevBuf *b : bufs) b->release();
     for (DevBuf &b : c->lf) b.release();
     ShardState &S = c->sh;
@@ -125,6 +167,9 @@ void wg_destroy(wg_ctx *c) {
     }
     if (c->h_fetch) (void)hipHostFree(c->h_fetch);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -163,6 +208,7 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
 
 int wg_synchronize(wg_ctx *c) {
     if (!c) return WG_E_INVALID;
+    if (wg_side_join(c) != WG_OK) return WG_E_HIP;
     WG_HIP(c, hipStreamSynchronize(c->stream));
     return WG_OK;
 }
@@ -174,6 +220,7 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     if (!c || !in) return WG_E_INVALID;
     (void)hipSetDevice(c->device);
     c->have_layout = c->have_geom = c->have_vtx = c->have_text = false;
+    c->lists_gen = ~0ull;
     c->sh.on = false;
     c->sh.step = 0;
     c->edge_y = nullptr;
@@ -230,13 +277,19 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
         return wg_fail(c, WG_E_INVALID, "bad residency %d", in->residency);
     }
     int rc;
+    // heights and the zero-band row_top depend on the commit times only: they
+    // run on the side stream while the hash join and the lanes run here
+    c->n_list = n;
+    WG_ALLOC(c, c->heights, n * 4 + 4);
+    WG_ALLOC(c, c->g_row_top, (n + 1) * 4);
+    if ((rc = wg_side_zero_rowtop(c, n, c->heights.as<float>(), c->g_row_top.as<float>(), 0)) != WG_OK) return rc;
     if ((rc = wg_stage_hash_join(c)) != WG_OK) return rc;
     if ((rc = wg_stage_lanes(c)) != WG_OK) return rc;
     if ((rc = wg_stage_edges(c)) != WG_OK) return rc;
-    if ((rc = wg_stage_heights(c)) != WG_OK) return rc;
     c->have_layout = true;
+    c->layout_gen++;
     // self.row_geometry with the default node_y / zero bands (:322-346)
-    if ((rc = wg_stage_rowtop(c, nullptr)) != WG_OK) return rc;
+    if ((rc = wg_side_join(c)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
     c->have_geom = true;
     return WG_OK;

@@ -419,12 +419,12 @@ __device__ __forceinline__ Cubic subcurve(const Cubic &c, float a, float b) {   
     return left;
 }
 
-__global__ void k_curves(uint64_t nc, const uint32_t *__restrict__ curve_ref, const uint32_t *__restrict__ curve_row,
-                         const wg_edge *__restrict__ edges, const float *__restrict__ row_top,
-                         const float *__restrict__ node_y, const float2 *__restrict__ edge_y,
-                         wg_curve *__restrict__ out, uint8_t *__restrict__ out_color) {
+__global__ void k_curves(const uint32_t *__restrict__ nc, const uint32_t *__restrict__ curve_ref,
+                         const uint32_t *__restrict__ curve_row, const wg_edge *__restrict__ edges,
+                         const float *__restrict__ row_top, const float *__restrict__ node_y,
+                         const float2 *__restrict__ edge_y, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nc) return;
+    if (k >= *nc) return;   // grid sized by an upper bound; the count lives on the device
     const uint32_t ref = curve_ref[k];
     const wg_edge e = edges[ref];
     const uint32_t row = curve_row[k];
@@ -457,9 +457,79 @@ __global__ void k_curves(uint64_t nc, const uint32_t *__restrict__ curve_ref, co
 
 inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
 
+// Curve lists are swept once per layout as a superset (every cross-lane
+// segment c <= r <= p, strip flags ignored) and filtered per geometry pass by
+// the row's own flags (:577): r == c needs a child strip, r == p a parent
+// strip, c < r < p a non-zero-height row.
+__device__ __forceinline__ bool curve_kept(uint32_t r, const wg_edge &e, uint32_t f) {
+    const uint32_t skip = (r == e.child_row) ? (f & RF_CHILD) : (r == e.parent_row) ? (f & RF_PARENT) : (f & RF_ZERO);
+    return skip == 0;
+}
+
+__global__ void k_curve_keep(uint64_t n, const uint32_t *__restrict__ soff, const uint32_t *__restrict__ sref,
+                             const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
+                             uint32_t *__restrict__ cnt) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t a = soff[r], b = soff[r + 1], f = rowflags[r];
+    uint32_t k = b - a;
+    if (f) {
+        k = 0;
+        for (uint32_t j = a; j < b; j++) k += curve_kept((uint32_t)r, edges[sref[j]], f) ? 1u : 0u;
+    }
+    cnt[r] = k;
+}
+
+__global__ void k_curve_compact(uint64_t n, const uint32_t *__restrict__ soff, const uint32_t *__restrict__ sref,
+                                const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
+                                const uint32_t *__restrict__ coff, uint32_t *__restrict__ ref, uint32_t *__restrict__ row) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t a = soff[r], b = soff[r + 1], f = rowflags[r];
+    uint32_t o = coff[r];
+    for (uint32_t j = a; j < b; j++) {
+        const uint32_t k = sref[j];
+        if (f && !curve_kept((uint32_t)r, edges[k], f)) continue;
+        ref[o] = k;
+        row[o] = (uint32_t)r;
+        o++;
+    }
+}
+
+__global__ void k_flags_diff(uint64_t n, const uint8_t *__restrict__ a, const uint8_t *__restrict__ b, uint32_t *diff) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool d = r < n && a[r] != b[r];
+    if (__any(d) && (threadIdx.x & 63) == 0) atomicOr(diff, 1u);
+}
+
 }  // namespace
 
+// filter the curve superset by this pass's row flags -> curve_off / curve_ref / curve_row
+static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s) {
+    uint32_t *coff = c->curve_off.as<uint32_t>();
+    hipLaunchKernelGGL(k_curve_keep, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
+                       c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
+                       coff);
+    WG_HIP(c, wg_exclusive_scan_u32(coff, coff, n, c->scan_tmp.p, s));
+    hipLaunchKernelGGL(k_curve_compact, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
+                       c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
+                       (const uint32_t *)coff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>());
+    WG_ALLOC(c, c->rowflags_lists, n + 4);
+    WG_HIP(c, hipMemcpyAsync(c->rowflags_lists.p, c->rowflags.p, n, hipMemcpyDeviceToDevice, s));
+    WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+static void launch_curves(wg_ctx *c, uint64_t n, uint64_t n_upper, hipStream_t s) {
+    if (!n_upper) return;
+    hipLaunchKernelGGL(k_curves, dim3(blocks(n_upper)), dim3(T), 0, s, c->curve_off.as<const uint32_t>() + n,
+                       c->curve_ref.as<const uint32_t>(), c->curve_row.as<const uint32_t>(), c->edges.as<const wg_edge>(),
+                       c->g_row_top.as<const float>(), c->g_node_y.as<const float>(),
+                       reinterpret_cast<const float2 *>(c->edge_y), c->curve.as<wg_curve>(), c->curve_color.as<uint8_t>());
+}
+
 int wg_stage_geometry(wg_ctx *c, const float *d_band) {
+    if (const int rc = wg_side_join(c)) return rc;
     const uint64_t n = c->n, ne = c->n_edges;
     hipStream_t s = c->stream;
     WG_ALLOC(c, c->g_height, n * 4 + 4);
@@ -467,39 +537,70 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     WG_ALLOC(c, c->rowflags, n + 4);
     WG_ALLOC(c, c->vert_off, (n + 2) * 4);
     WG_ALLOC(c, c->curve_off, (n + 2) * 4);
+    WG_ALLOC(c, c->scurve_off, (n + 2) * 4);
     { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
+    const float *h = c->heights.as<const float>();
+    const float *rt = c->g_row_top.as<const float>();
+    if (n && c->lists_gen == c->layout_gen && c->lists_n == n && c->lists_ne == ne) {
+        // same layout: the lists stand; only the curve filter can change with the flags
+        WG_ALLOC(c, c->geom_diff, 64);
+        wg_stage_begin(c, "geom_reuse");
+        WG_HIP(c, hipMemsetAsync(c->geom_diff.p, 0, 4, s));
+        hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
+                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>());
+        hipLaunchKernelGGL(k_flags_diff, dim3(blocks(n)), dim3(T), 0, s, n, c->rowflags.as<const uint8_t>(),
+                           c->rowflags_lists.as<const uint8_t>(), c->geom_diff.as<uint32_t>());
+        uint64_t chk[3] = {1, 0, 0};
+        int rc = wg_fetch(c, {{c->geom_diff.p, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false}}, chk);
+        if (rc != WG_OK) return rc;
+        if (chk[0]) {
+            if ((rc = filter_curves(c, n, s)) != WG_OK) return rc;
+            uint64_t nc = 0;
+            if ((rc = wg_fetch(c, {{c->curve_off.as<uint32_t>() + n, false}}, &nc)) != WG_OK) return rc;
+            c->n_curve = nc;
+        }
+        wg_stage_end(c);
+        wg_stage_begin(c, "geom_curves");
+        launch_curves(c, n, c->n_curve, s);
+        WG_HIP(c, hipGetLastError());
+        wg_stage_end(c);
+        const uint32_t tbits = (uint32_t)chk[1];
+        std::memcpy(&c->total_height, &tbits, 4);
+        c->scan_path = chk[2] ? 1u : 0u;
+        return WG_OK;
+    }
+    c->lists_gen = ~0ull;
     c->n_vert = c->n_curve = 0;
     if (n == 0) {
         WG_HIP(c, hipMemsetAsync(c->vert_off.p, 0, 4, s));
         WG_HIP(c, hipMemsetAsync(c->curve_off.p, 0, 4, s));
         return WG_OK;
     }
-    const float *h = c->heights.as<const float>();
-    const float *rt = c->g_row_top.as<const float>();
     const wg_edge *E = c->edges.as<const wg_edge>();
     const uint32_t *edge_off = c->edge_cnt.as<const uint32_t>();
-    // every counter array that starts at zero lives in one workspace: one memset
+    // every array that starts at zero lives in one workspace: one memset.  The
+    // last region is an all-zero flag row: the lists are swept as a superset.
     const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
     const uint64_t rowa = (n + 2 + 63) & ~63ull, cha = (nch + 2 + 63) & ~63ull;
-    WG_ALLOC(c, c->geom_zero, (6 * rowa + 2 * cha + 64) * 4);
+    const uint64_t zwords = 6 * rowa + 2 * cha + 64 + rowa / 4;
+    WG_ALLOC(c, c->geom_zero, zwords * 4);
     uint32_t *cntF = c->geom_zero.as<uint32_t>(), *cntT = cntF + rowa, *cntB = cntT + rowa;
     uint32_t *cntC = cntB + rowa, *cntCend = cntC + rowa, *top_fill = cntCend + rowa;
     uint32_t *carry_cnt = top_fill + rowa, *carry_fill = carry_cnt + cha, *sweep_err = carry_fill + cha;
-    uint32_t *voff = c->vert_off.as<uint32_t>(), *coff = c->curve_off.as<uint32_t>();
+    const uint8_t *zflags = reinterpret_cast<const uint8_t *>(sweep_err + 64);
+    uint32_t *voff = c->vert_off.as<uint32_t>(), *soff = c->scurve_off.as<uint32_t>();
 
     wg_stage_begin(c, "geom_counts");
-    WG_HIP(c, hipMemsetAsync(c->geom_zero.p, 0, (6 * rowa + 2 * cha + 64) * 4, s));
+    WG_HIP(c, hipMemsetAsync(c->geom_zero.p, 0, zwords * 4, s));
     hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
                        c->g_node_y.as<float>(), c->rowflags.as<uint8_t>());
     if (ne)
-        hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, c->rowflags.as<const uint8_t>(), cntB,
-                           cntT, cntF, cntC, cntCend);
+        hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntB, cntT, cntF, cntC, cntCend);
     WG_HIP(c, wg_exclusive_scan_u32(cntF, cntF, n + 1, c->scan_tmp.p, s));
     WG_HIP(c, wg_exclusive_scan_u32(cntC, cntC, n + 1, c->scan_tmp.p, s));
-    hipLaunchKernelGGL(k_row_counts, dim3(blocks(n)), dim3(T), 0, s, n, cntF, cntC, cntT, cntB, cntCend,
-                       c->rowflags.as<const uint8_t>(), voff, coff);
+    hipLaunchKernelGGL(k_row_counts, dim3(blocks(n)), dim3(T), 0, s, n, cntF, cntC, cntT, cntB, cntCend, zflags, voff, soff);
     WG_HIP(c, wg_exclusive_scan_u32(voff, voff, n, c->scan_tmp.p, s));
-    WG_HIP(c, wg_exclusive_scan_u32(coff, coff, n, c->scan_tmp.p, s));
+    WG_HIP(c, wg_exclusive_scan_u32(soff, soff, n, c->scan_tmp.p, s));
     // carry-in registration
     WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
     if (ne) hipLaunchKernelGGL(k_carry_diff, dim3(blocks(ne)), dim3(T), 0, s, ne, E, carry_cnt);
@@ -509,18 +610,20 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     WG_HIP(c, wg_exclusive_scan_u32(c->carry_off.as<uint32_t>(), c->carry_off.as<uint32_t>(), nch, c->scan_tmp.p, s));
     uint64_t tot[3] = {0, 0, 0};
     {
-        const int rc = wg_fetch(c, {{voff + n, false}, {coff + n, false}, {c->carry_off.as<uint32_t>() + nch, false}}, tot);
+        const int rc = wg_fetch(c, {{voff + n, false}, {soff + n, false}, {c->carry_off.as<uint32_t>() + nch, false}}, tot);
         if (rc != WG_OK) return rc;
     }
     wg_stage_end(c);
     c->n_vert = tot[0];
-    c->n_curve = tot[1];
+    const uint64_t n_super = tot[1];
     const uint64_t ncarry = tot[2];
     WG_ALLOC(c, c->vert, c->n_vert * 4 + 16);
-    WG_ALLOC(c, c->curve, c->n_curve * sizeof(wg_curve) + 64);
-    WG_ALLOC(c, c->curve_color, c->n_curve + 16);
-    WG_ALLOC(c, c->curve_ref, c->n_curve * 4 + 16);
-    WG_ALLOC(c, c->curve_row, c->n_curve * 4 + 16);
+    WG_ALLOC(c, c->scurve_ref, n_super * 4 + 16);
+    WG_ALLOC(c, c->scurve_row, n_super * 4 + 16);
+    WG_ALLOC(c, c->curve, n_super * sizeof(wg_curve) + 64);
+    WG_ALLOC(c, c->curve_color, n_super + 16);
+    WG_ALLOC(c, c->curve_ref, n_super * 4 + 16);
+    WG_ALLOC(c, c->curve_row, n_super * 4 + 16);
     WG_ALLOC(c, c->carry, ncarry * 8 + 16);
 
     wg_stage_begin(c, "geom_lists");
@@ -539,29 +642,34 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     uint32_t *big_n = sweep_err + 1;
     WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
     hipLaunchKernelGGL(k_sweep, dim3((nch + SW_WAVES - 1) / SW_WAVES), dim3(64 * SW_WAVES), 0, s, n, nch, E, edge_off,
-                       c->carry_off.as<const uint32_t>(), (const uint32_t *)carry_sorted, c->rowflags.as<const uint8_t>(),
-                       voff, coff, vert, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(),
+                       c->carry_off.as<const uint32_t>(), (const uint32_t *)carry_sorted, zflags,
+                       voff, (const uint32_t *)soff, vert, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
                        c->sweep_big.as<uint32_t>(), big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS);
     hipLaunchKernelGGL(k_sweep_lds, dim3(64), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)c->sweep_big.as<uint32_t>(),
                        (const uint32_t *)big_n, E, edge_off, c->carry_off.as<const uint32_t>(),
-                       (const uint32_t *)carry_sorted, c->rowflags.as<const uint8_t>(), voff, coff, vert,
-                       c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), sweep_err);
+                       (const uint32_t *)carry_sorted, zflags, voff, (const uint32_t *)soff, vert,
+                       c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(), sweep_err);
     WG_HIP(c, hipGetLastError());
+    {
+        const int rc = filter_curves(c, n, s);
+        if (rc != WG_OK) return rc;
+    }
     wg_stage_end(c);
     wg_stage_begin(c, "geom_curves");
-    if (c->n_curve)
-        hipLaunchKernelGGL(k_curves, dim3(blocks(c->n_curve)), dim3(T), 0, s, c->n_curve, c->curve_ref.as<const uint32_t>(),
-                           c->curve_row.as<const uint32_t>(), E, rt, c->g_node_y.as<const float>(),
-                           reinterpret_cast<const float2 *>(c->edge_y), c->curve.as<wg_curve>(),
-                           c->curve_color.as<uint8_t>());
+    launch_curves(c, n, n_super, s);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
-    uint64_t fin[3] = {0, 0, 0};
+    uint64_t fin[4] = {0, 0, 0, 0};
     {
-        const int rc = wg_fetch(c, {{sweep_err, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false}}, fin);
+        const int rc = wg_fetch(c, {{sweep_err, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false},
+                                    {c->curve_off.as<uint32_t>() + n, false}}, fin);
         if (rc != WG_OK) return rc;
     }
     if (fin[0]) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP);
+    c->n_curve = fin[3];
+    c->lists_gen = c->layout_gen;
+    c->lists_n = n;
+    c->lists_ne = ne;
     const uint32_t tbits = (uint32_t)fin[1];
     std::memcpy(&c->total_height, &tbits, 4);
     c->scan_path = fin[2] ? 1u : 0u;

@@ -83,6 +83,7 @@ struct ShardState {
     uint64_t E0 = 0, E1 = 0;  // own parent references [parent_off[s], parent_off[e])
     uint64_t row_base = 0;    // index of row s in the context's row arrays
     DevBuf msg;               // this rank's outgoing message
+    const uint32_t *heads = nullptr;   // host copy of the gathered 16-byte headers (one exchange call)
     uint64_t msg_bytes = 0;
     DevBuf ptable;            // id partition table (global duplicate check)
     DevBuf prow;              // int32 [E1-E0] parent rows of own references
@@ -95,7 +96,8 @@ struct ShardState {
     uint64_t nev_own = 0, naux_own = 0;
     DevBuf xtok, xt;          // chain token per crossing entry: shard-local / global
     DevBuf dev_small;
-    DevBuf h_g, rt_g;         // heights / row_top of rows [0, e)
+    DevBuf h_g, rt_g;         // heights of rows [0, e) / row_top of rows [s, e] (below s: unspecified)
+    bool rt_zero = false;     // rt_g holds the zero-band row_top (computed at build begin, side stream)
     DevBuf band_host;         // device copy of a host band array [N]
     const float *band_g = nullptr;
     DevBuf xchild, xpar;      // per crossing entry: child lane/colour, parent lane/y
@@ -117,10 +119,16 @@ struct wg_ctx {
     int         device = 0;
     hipStream_t stream = nullptr;
     bool        own_stream = false;
+    // side stream: the build's zero-band row_top (a function of the commit
+    // times only) runs there, overlapping the latency-bound lane phases
+    hipStream_t side = nullptr, side_main = nullptr;
+    hipEvent_t  ev_fork = nullptr, ev_join = nullptr;
+    bool        side_pending = false;
     std::string err;
 
     // ---- last layout build -------------------------------------------------
     uint64_t n = 0, e_refs = 0, n_edges = 0;
+    uint64_t n_list = 0;      // rows of the whole list (n differs for a row shard)
     bool     have_layout = false;
     uint32_t max_lane = 0, n_slots = 0, lane_path = 1;
     float    graph_width = 24.0f;
@@ -173,6 +181,16 @@ struct wg_ctx {
     DevBuf scan_tmp;        // scan workspace
     DevBuf scal;            // uint64 [16] device scalars (totals)
     DevBuf rowflags;        // uint8 [N] bit0 zero-height strip, bit1 child strip empty, bit2 parent strip empty
+    // The ordered lists (vert, curve_ref/curve_row, offsets) depend on the
+    // layout and the row flags only, not on row_top: a geometry pass on the
+    // same layout whose flags equal those the lists were built with reuses
+    // them and recomputes heights, row_top, node_y and the curves.
+    uint64_t layout_gen = 0;            // bumped by every layout build
+    uint64_t lists_gen = ~0ull;         // layout_gen the lists were built for (~0: none)
+    uint64_t lists_n = 0, lists_ne = 0;
+    DevBuf rowflags_lists;              // the flags the curve lists were filtered with
+    DevBuf scurve_off, scurve_ref, scurve_row;   // curve superset (flags ignored), swept once per layout
+    DevBuf geom_diff;                   // uint32: flags differ
     DevBuf sweep_big;       // uint32 [nch] chunks too wide for the register sweep
     uint32_t sweep_reg_cap = 512;   // edges per chunk the register sweep holds (WG_OPT_SWEEP_REG)
     const float *edge_y = nullptr;   // per edge {child_y, parent_y} override (row-sharded geometry), or null
@@ -261,7 +279,16 @@ int wg_lf_replay(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, 
 int wg_lf_lanes(wg_ctx *c, const LfRange &R, const uint8_t *slots, uint32_t *lane);
 int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
 int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out);             // rows [0,m) of an n-row list
-int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top);
+// side stream (wg_api.hip): wg_side_fork makes the context's launches go to
+// the side stream (ordered after the work queued so far) until wg_side_done;
+// wg_side_join orders the main stream after that work (no host wait).
+int wg_side_fork(wg_ctx *c);
+void wg_side_done(wg_ctx *c);
+int wg_side_join(wg_ctx *c);
+// heights of rows [0, m) of the list + zero-band row_top into (h, rt), on the side stream
+int wg_side_zero_rowtop(wg_ctx *c, uint64_t m, float *h, float *rt, uint64_t row_lo);
+int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top,
+                  uint64_t row_lo);   // rows below row_lo: walked, not written
 int wg_stage_rowtop(wg_ctx *c, const float *d_band);   // wg_rowtop.hip
 int wg_stage_geometry(wg_ctx *c, const float *d_band); // wg_geom.hip
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel);  // wg_vertex.hip

@@ -23,8 +23,8 @@
 //   rt_walk    one wave, from the first non-exact chunk: composes 64 chunk
 //              transducers per step (ordered shuffle scan) from the exact
 //              running f32 value; a chunk in which acc crosses a binade is
-//              replayed by the wave 64 rows at a time with one transducer
-//              scan per crossing
+//              replayed by the wave, 16 rows per lane, one transducer scan
+//              per crossing (replay_chunk)
 //   rt_rows    per chunk: exact prefix, or block scan of row transducers from
 //              the chunk's exact start
 // Negative or non-finite steps make the walk replay every row one by one
@@ -84,20 +84,21 @@ __device__ __forceinline__ Td td_shfl(const Td &v, int lane) {
 // The step at binade k: acc = 2^k + p*u represents every acc of parity p.
 __device__ __forceinline__ Td row_td(float s, int k) {
     if (k < -100 || k > 126) return td_invalid();
-    const float base = ldexpf(1.0f, k), u = ldexpf(1.0f, k - 23), top = ldexpf(1.0f, k + 1);
+    // x / u == x * 2^(23-k) exactly: every quotient below is an integer < 2^24
+    const float base = ldexpf(1.0f, k), u = ldexpf(1.0f, k - 23), iu = ldexpf(1.0f, 23 - k), top = ldexpf(1.0f, k + 1);
     Td t;
     t.f = 4u;
     {
         const float a = base, r = a + s;
         if (!(r < top)) return td_invalid();
-        t.d0 = (uint32_t)((r - a) / u);
-        t.f |= ((uint32_t)((r - base) / u)) & 1u;
+        t.d0 = (uint32_t)((r - a) * iu);
+        t.f |= ((uint32_t)((r - base) * iu)) & 1u;
     }
     {
         const float a = base + u, r = a + s;
         if (!(r < top)) return td_invalid();
-        t.d1 = (uint32_t)((r - a) / u);
-        t.f |= (((uint32_t)((r - base) / u)) & 1u) << 1;
+        t.d1 = (uint32_t)((r - a) * iu);
+        t.f |= (((uint32_t)((r - base) * iu)) & 1u) << 1;
     }
     return t;
 }
@@ -107,6 +108,8 @@ __device__ __forceinline__ float step_of(const float *__restrict__ h, const floa
 }
 
 __device__ __forceinline__ int binade_of(float a) { return ilogbf(a); }
+// parity of a / 2^(k-23) for a in binade k (the quotient is an integer < 2^24)
+__device__ __forceinline__ uint32_t parity_at(float a, int k) { return ((uint32_t)(a * ldexpf(1.0f, 23 - k))) & 1u; }
 
 // ---------------------------------------------------------------------------
 // heights
@@ -287,7 +290,7 @@ __global__ void __launch_bounds__(64) k_rt_fill(uint64_t nch, const SupState *__
     const int lid = threadIdx.x & 63;
     const uint64_t cc = S * RT_SUP + lid;
     const float u = ldexpf(1.0f, st.k - 23);
-    const uint32_t p0 = ((uint32_t)(st.start / u)) & 1u;
+    const uint32_t p0 = parity_at(st.start, st.k);
     const int b = st.k - ch[cc].kguess + 1;
     const uint4 q = tables[cc * WG_RT_NBIN + b];   // valid: the super table was composed from these
     Td t = Td{q.x, q.y, q.z};
@@ -344,7 +347,7 @@ __device__ float replay_rows(uint64_t r0, uint64_t r1, float acc, const float *_
             const int k = binade_of(acc);
             const float u = ldexpf(1.0f, k - 23);
             const double top = ldexp(1.0, k + 1);
-            const uint32_t p = ((uint32_t)(acc / u)) & 1u;
+            const uint32_t p = parity_at(acc, k);
             Td t = (lid >= j && lid < cnt) ? row_td(sv, k) : td_identity();
             for (int d = 1; d < 64; d <<= 1) {
                 const Td o = td_shfl_up(t, d);
@@ -367,6 +370,91 @@ __device__ float replay_rows(uint64_t r0, uint64_t r1, float acc, const float *_
         }
         if (lid < cnt) row_top[i] = mine;
     }
+    return acc;
+}
+
+// Replay one chunk's rows [r0, r1) (at most 64 * 16) from acc > 0: lane L
+// holds rows 16L..16L+15.  Per pass, the lanes' 16-row transducers at the
+// binade of acc are scanned; every lane before the first one whose rows reach
+// the next binade is placed in parallel, that lane's 16 rows are added one
+// by one (plain f32 adds, the reference's own operation), and the next pass
+// starts after it.  A chunk with b binade crossings takes b + 1 passes.
+constexpr int RP_Q = 16;
+static_assert(WG_RT_CHUNK <= 64 * RP_Q, "a chunk is replayed by one wave");
+__device__ float replay_chunk(uint64_t r0, uint64_t r1, float acc, const float *__restrict__ h,
+                              const float *__restrict__ band, float *__restrict__ row_top) {
+    const uint32_t lid = threadIdx.x & 63;
+    const uint32_t cnt = (uint32_t)(r1 - r0);
+    float sv[RP_Q], mine[RP_Q];
+#pragma unroll
+    for (int q = 0; q < RP_Q; q++) {
+        const uint32_t j = lid * RP_Q + q;
+        sv[q] = j < cnt ? step_of(h, band, r0 + j) : 0.0f;
+        mine[q] = 0.0f;
+    }
+    uint32_t j0 = 0;   // first row not yet placed (uniform, a multiple of RP_Q)
+    while (j0 < cnt) {
+        if (!(acc >= 1.0e-30f)) {   // zero / tiny: the row-by-row replay takes over
+#pragma unroll
+            for (int q = 0; q < RP_Q; q++)
+                if (lid * RP_Q + q < j0) row_top[r0 + lid * RP_Q + q] = mine[q];
+            return replay_rows(r0 + j0, r1, acc, h, band, row_top);
+        }
+        const int k = binade_of(acc);
+        const float u = ldexpf(1.0f, k - 23);
+        const double top = ldexp(1.0, k + 1);
+        const uint32_t p = parity_at(acc, k);
+        Td t = td_identity();
+#pragma unroll
+        for (int q = 0; q < RP_Q; q++) {
+            const uint32_t j = lid * RP_Q + q;
+            if (j >= j0 && j < cnt) t = td_compose(t, row_td(sv[q], k));
+        }
+        Td inc = t;
+        for (int d = 1; d < 64; d <<= 1) {
+            const Td o = td_shfl_up(inc, d);
+            if (lid >= (uint32_t)d) inc = td_compose(o, inc);
+        }
+        Td ex = td_shfl_up(inc, 1);
+        if (lid == 0) ex = td_identity();
+        const uint32_t Dinc = p ? inc.d1 : inc.d0;
+        const bool ok = (inc.f & 4u) && (double)acc + (double)Dinc * (double)u < top;
+        const uint64_t okm = __ballot(ok);
+        const uint32_t f = okm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);
+        if (lid < f) {
+            uint32_t D = p ? ex.d1 : ex.d0;
+            uint32_t par = p ? ((ex.f >> 1) & 1u) : (ex.f & 1u);
+#pragma unroll
+            for (int q = 0; q < RP_Q; q++) {
+                const uint32_t j = lid * RP_Q + q;
+                if (j >= j0 && j < cnt) {
+                    mine[q] = acc + (float)D * u;
+                    const Td r = row_td(sv[q], k);
+                    D += par ? r.d1 : r.d0;
+                    par = (r.f >> par) & 1u;
+                }
+            }
+        }
+        if (f == 64u) {
+            acc = acc + (float)(uint32_t)__shfl((int)Dinc, 63, 64) * u;
+            break;
+        }
+        float a = acc + (float)(f == 0u ? 0u : (uint32_t)__shfl((int)Dinc, (int)f - 1, 64)) * u;
+#pragma unroll
+        for (int q = 0; q < RP_Q; q++) {
+            const uint32_t j = f * RP_Q + q;
+            if (j >= j0 && j < cnt) {
+                const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sv[q]), (int)f));
+                if (lid == f) mine[q] = a;
+                a = a + sj;
+            }
+        }
+        acc = a;
+        j0 = (f + 1u) * RP_Q;
+    }
+#pragma unroll
+    for (int q = 0; q < RP_Q; q++)
+        if (lid * RP_Q + q < cnt) row_top[r0 + lid * RP_Q + q] = mine[q];
     return acc;
 }
 
@@ -398,7 +486,7 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
             const int k = binade_of(A);
             const float u = ldexpf(1.0f, k - 23);
             const double top = ldexp(1.0, k + 1);
-            const uint32_t p = ((uint32_t)(A / u)) & 1u;
+            const uint32_t p = parity_at(A, k);
             const uint64_t ss = c / RT_SUP + lid;
             Td t = td_invalid();
             if (ss < nsup) {
@@ -425,7 +513,7 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
             const int k = binade_of(A);
             const float u = ldexpf(1.0f, k - 23);
             const double top = ldexp(1.0, k + 1);
-            const uint32_t p = ((uint32_t)(A / u)) & 1u;
+            const uint32_t p = parity_at(A, k);
             const uint64_t cc = c + lid;
             Td t = td_invalid();
             if (cc < nch) {
@@ -462,7 +550,8 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
         }
         if (do_replay && c < nch) {
             const uint64_t r0 = c * WG_RT_CHUNK, r1 = (r0 + WG_RT_CHUNK < n) ? r0 + WG_RT_CHUNK : n;
-            A = all_serial ? serial_rows(r0, r1, A, h, band, row_top) : replay_rows(r0, r1, A, h, band, row_top);
+            A = all_serial ? serial_rows(r0, r1, A, h, band, row_top)
+                           : (A >= 1.0e-30f ? replay_chunk(r0, r1, A, h, band, row_top) : replay_rows(r0, r1, A, h, band, row_top));
             if (lid == 0) ch[c].mode = MODE_REPLAYED;
             c++;
             replayed++;
@@ -475,9 +564,10 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
     }
 }
 
-__global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
-                                                  const RtChunk *__restrict__ ch, float *__restrict__ row_top) {
-    const uint64_t c = blockIdx.x;
+__global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, uint64_t c_lo, const float *__restrict__ h,
+                                                  const float *__restrict__ band, const RtChunk *__restrict__ ch,
+                                                  float *__restrict__ row_top) {
+    const uint64_t c = c_lo + blockIdx.x;
     const uint32_t mode = ch[c].mode;
     if (mode == MODE_REPLAYED) return;
     const int lid = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -508,7 +598,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, const float *__res
     }
     const int k = ch[c].kstart;
     const float u = ldexpf(1.0f, k - 23);
-    const uint32_t p0 = ((uint32_t)(A / u)) & 1u;
+    const uint32_t p0 = parity_at(A, k);
     Td tr[RT_Q];
     Td t = td_identity();
 #pragma unroll
@@ -582,12 +672,16 @@ int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out) {
 }
 
 int wg_stage_heights(wg_ctx *c) {
+    if (const int rc = wg_side_join(c)) return rc;
+    c->n_list = c->n;
     WG_ALLOC(c, c->heights, c->n * 4 + 4);
     return wg_heights_run(c, c->n, c->n, c->heights.as<float>());
 }
 
-// row_top[0..n] of n rows with heights h (+ band, may be null)
-int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top) {
+// row_top[0..n] of n rows with heights h (+ band, may be null).  Rows below
+// row_lo are only walked through (a row shard needs row_top of its own rows;
+// entries below row_lo are left unspecified).
+int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top, uint64_t row_lo) {
     const uint64_t nch = (n + WG_RT_CHUNK - 1) / WG_RT_CHUNK;
     WG_ALLOC(c, c->rt_chunk, (nch + 1) * sizeof(RtChunk));
     WG_ALLOC(c, c->rt_tables, (nch + 1) * WG_RT_NBIN * sizeof(uint4));
@@ -620,13 +714,17 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
     if (nsup)
         hipLaunchKernelGGL(k_rt_fill, dim3(nsup), dim3(64), 0, c->stream, nch, (const SupState *)sup, ch,
                            c->rt_tables.as<const uint4>());
-    hipLaunchKernelGGL(k_rt_rows, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch, row_top);
+    const uint64_t c_lo = (row_lo < n ? row_lo : n) / WG_RT_CHUNK;
+    if (c_lo < nch)
+        hipLaunchKernelGGL(k_rt_rows, dim3(nch - c_lo), dim3(RT_T), 0, c->stream, n, c_lo, h, d_band, (const RtChunk *)ch,
+                           row_top);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;
 }
 
 int wg_stage_rowtop(wg_ctx *c, const float *d_band) {
+    if (const int rc = wg_side_join(c)) return rc;   // the side stream's row_top shares the scan buffers
     WG_ALLOC(c, c->g_row_top, (c->n + 1) * 4);
-    return wg_rowtop_run(c, c->n, c->heights.as<const float>(), d_band, c->g_row_top.as<float>());
+    return wg_rowtop_run(c, c->n, c->heights.as<const float>(), d_band, c->g_row_top.as<float>(), 0);
 }

@@ -228,18 +228,21 @@ __global__ void k_sh_pack_ends(uint64_t s, uint64_t e, const WgXEnt *__restrict_
                                const uint8_t *__restrict__ color_l, const float *__restrict__ rt_g,
                                const float *__restrict__ band, uint4 *__restrict__ out) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // child record {entry, lane, colour, y}; parent record {entry, lane, y, 0};
+    // entry ~0 = no record (row_top below the shard is not known here)
     if (q < nown) {
         const uint64_t x = xown_begin + q;
         const uint64_t c = xall[x].c;
-        out[q] = make_uint4((uint32_t)x, lane_l[c - s + 1], color_l[c - s + 1], 1u);
+        const float y = rt_g[c] + node_y_of(band, c);
+        out[q] = make_uint4((uint32_t)x, lane_l[c - s + 1], color_l[c - s + 1], __float_as_uint(y));
     } else if (q < nown + xin_end) {
         const uint64_t x = q - nown;
         const uint64_t p = xall[x].p;
         if (p >= s && p < e) {
             const float y = rt_g[p] + node_y_of(band, p);
-            out[q] = make_uint4((uint32_t)x, lane_l[p - s + 1], __float_as_uint(y), 1u);
+            out[q] = make_uint4((uint32_t)x, lane_l[p - s + 1], __float_as_uint(y), 0u);
         } else {
-            out[q] = make_uint4((uint32_t)x, 0u, 0u, 0u);
+            out[q] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
         }
     }
 }
@@ -252,7 +255,7 @@ __global__ void k_sh_unpack_ends(Sections S, const uint64_t *__restrict__ nown, 
     const uint32_t r = section_of(S, g);
     const uint64_t q = g - S.off[r];
     const uint4 v = reinterpret_cast<const uint4 *>(S.base + r * S.stride + 16)[q];
-    if (!v.w) return;
+    if (v.x == 0xFFFFFFFFu) return;
     if (q < nown[r]) xchild[v.x] = v;
     else xpar[v.x] = v;
 }
@@ -338,7 +341,7 @@ __global__ void k_sh_edges_in(LocalEdgeArgs A) {
     ed.parent_lane = plane;
     ed.color = A.xchild[x].z;
     A.edges[o] = ed;
-    A.edge_y[o] = make_float2(A.rt_g[en.c] + node_y_of(A.band, en.c), py);
+    A.edge_y[o] = make_float2(__uint_as_float(A.xchild[x].w), py);   // the child's shard sent its y
 }
 
 __global__ void k_sh_edges_own(LocalEdgeArgs A) {
@@ -369,6 +372,9 @@ __global__ void k_sh_edges_own(LocalEdgeArgs A) {
         o++;
     }
 }
+
+// a message's 16-byte header (kernel arguments: no host buffer outlives the call)
+__global__ void k_sh_put_head(uint4 *__restrict__ dst, uint4 v) { *dst = v; }
 
 __global__ void k_sh_lane_out(uint64_t s, uint64_t nl, const uint32_t *__restrict__ lane_asg, const uint8_t *__restrict__ flags,
                               uint32_t *__restrict__ lane_l, uint8_t *__restrict__ color_l) {
@@ -416,10 +422,15 @@ static Sections make_sections(const void *gathered, uint64_t stride, int world, 
     return S;
 }
 
-// per-rank 16-byte headers of a gathered buffer
+// per-rank 16-byte headers of a gathered buffer (from the caller's host copy when given)
 static int read_headers(wg_ctx *c, const void *gathered, uint64_t stride, std::vector<uint32_t> &hdr) {
     const int W = c->sh.world;
     hdr.assign((size_t)W * 4, 0);
+    if (c->sh.heads) {
+        for (int r = 0; r < W; r++)
+            for (int k = 0; k < 3; k++) hdr[4 * r + k] = c->sh.heads[4 * r + k];
+        return WG_OK;
+    }
     WgFetch it[64];
     for (int r = 0; r < W; r++)
         for (int k = 0; k < 3; k++) it[3 * r + k] = WgFetch{(const uint8_t *)gathered + r * stride + 4 * k, false};
@@ -462,6 +473,7 @@ static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
     if ((rc = wg_stage_edges(c)) != WG_OK) return rc;
     if ((rc = wg_stage_heights(c)) != WG_OK) return rc;
     c->have_layout = true;
+    c->layout_gen++;
     if ((rc = wg_stage_rowtop(c, nullptr)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
     c->have_geom = true;
@@ -470,27 +482,30 @@ static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
     return WG_OK;
 }
 
-// geometry pass, part 1: row_top for rows [0, e), endpoint records (X6)
+// geometry pass, part 1: row_top of rows [s, e] (walked from row 0), endpoint records (X6)
 static int sh_geometry_begin(wg_ctx *c, const float *band_g, wg_shard_msg *out) {
     ShardState &S = c->sh;
     const uint64_t e = S.e;
-    WG_ALLOC(c, S.rt_g, (e + 1) * 4);
-    int rc = wg_rowtop_run(c, e, S.h_g.as<const float>(), band_g, S.rt_g.as<float>());
+    int rc = wg_side_join(c);
     if (rc != WG_OK) return rc;
+    if (band_g || !S.rt_zero) {   // the zero-band row_top may be left from the build's side stream
+        WG_ALLOC(c, S.rt_g, (e + 1) * 4);
+        if ((rc = wg_rowtop_run(c, e, S.h_g.as<const float>(), band_g, S.rt_g.as<float>(), S.s)) != WG_OK) return rc;
+        S.rt_zero = band_g == nullptr;
+    }
     S.band_g = band_g;
     const uint64_t nown = S.xoff[S.rank + 1] - S.xoff[S.rank], xin = S.xoff[S.rank];
     S.step = SH_X6;
     if ((rc = sh_send(c, 16 + (nown + xin) * 16, out)) != WG_OK) return rc;
     uint32_t hdr[4] = {(uint32_t)nown, (uint32_t)xin, 0, 0};
-    WG_HIP(c, hipMemcpyAsync(S.msg.p, hdr, 16, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, c->stream, S.msg.as<uint4>(), make_uint4(hdr[0], hdr[1], hdr[2], hdr[3]));
     if (nown + xin)
         hipLaunchKernelGGL(k_sh_pack_ends, dim3(blocks(nown + xin)), dim3(T), 0, c->stream, S.s, S.e,
                            S.xall.as<const WgXEnt>(), S.xoff[S.rank], nown, xin, c->lane_out.as<const uint32_t>(),
                            c->color_out.as<const uint8_t>(), S.rt_g.as<const float>(), band_g,
                            reinterpret_cast<uint4 *>(S.msg.as<uint8_t>() + 16));
     WG_HIP(c, hipGetLastError());
-    WG_HIP(c, hipStreamSynchronize(c->stream));   // the caller copies the message on another stream
-    return WG_OK;
+    return WG_OK;   // wg_shard_copy_msg orders the copy after these kernels
 }
 
 // geometry pass, part 2: the local problem and the unchanged geometry stages
@@ -592,6 +607,7 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     S.Etot = in->n_parents;
     S.row_base = 1;
     c->have_layout = c->have_geom = c->have_vtx = c->have_text = false;
+    c->lists_gen = ~0ull;
     c->edge_y = nullptr;
     c->d_oid = in->oid;
     c->d_time = in->time;
@@ -614,8 +630,17 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     S.E0 = eo[0];
     S.E1 = eo[1];
     c->e_refs_own = S.E1 - S.E0;
+    S.rt_zero = false;
     if (world == 1) return sh_fallback(c, out);
     const uint64_t nl = row_end - row_begin, El = S.E1 - S.E0;
+    // heights of rows [0, e) (the last row of the LIST is ROW_HEIGHT) and the
+    // zero-band row_top of the own rows: side stream, overlapping the exchanges
+    c->n_list = N;
+    WG_ALLOC(c, S.h_g, row_end * 4 + 4);
+    WG_ALLOC(c, S.rt_g, (row_end + 1) * 4);
+    int rc = wg_side_zero_rowtop(c, row_end, S.h_g.as<float>(), S.rt_g.as<float>(), row_begin);
+    if (rc != WG_OK) return rc;
+    S.rt_zero = true;
     // ---- local table, probes, global duplicate scan -------------------------------------
     uint64_t cap = 1024;
     while (cap < 2 * nl) cap <<= 1;
@@ -649,15 +674,14 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     S.n_unres = h[2];
     S.step = SH_X1;
     // X1: {violation | duplicate, n} + one 32-byte record per unresolved reference, row order
-    int rc = sh_send(c, 16 + (uint64_t)h[2] * 32, out);
+    rc = sh_send(c, 16 + (uint64_t)h[2] * 32, out);
     if (rc != WG_OK) return rc;
     uint32_t hdr[4] = {(uint32_t)(h[0] | h[1]), (uint32_t)h[2], 0, 0};
-    WG_HIP(c, hipMemcpyAsync(S.msg.p, hdr, 16, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), make_uint4(hdr[0], hdr[1], hdr[2], hdr[3]));
     if (nl) hipLaunchKernelGGL(k_sh_pack_unres, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid, S.E0,
                                S.prow.as<const int32_t>(), S.xcnt.as<const uint32_t>(),
                                reinterpret_cast<uint32_t *>(S.msg.as<uint8_t>() + 16));
     WG_HIP(c, hipGetLastError());
-    WG_HIP(c, hipStreamSynchronize(st));
     wg_stage_end(c);
     return WG_OK;
 }
@@ -669,9 +693,12 @@ int wg_shard_copy_msg(wg_ctx *c, void *dst) {
     return WG_OK;
 }
 
-int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const uint64_t *sizes, wg_shard_msg *out) {
+int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const uint64_t *sizes, const uint32_t *heads,
+                      wg_shard_msg *out) {
     if (!c || !out || !sizes) return WG_E_INVALID;
     ShardState &S = c->sh;
+    S.heads = heads;   // valid for this call only
+    struct ClearHeads { ShardState &S; ~ClearHeads() { S.heads = nullptr; } } clear_heads{S};
     const int W = S.world;
     if (!S.on || S.step == SH_IDLE) return wg_fail(c, WG_E_STATE, "no sharded call in progress");
     for (int r = 0; r < W; r++)
@@ -703,7 +730,6 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         if (L) hipLaunchKernelGGL(k_sh_probe_gathered, dim3(blocks(L)), dim3(T), 0, st, L, S.unres.as<const uint32_t>(),
                                   c->d_oid, c->hash.as<const unsigned long long>(), c->hcap - 1, S.msg.as<int32_t>());
         WG_HIP(c, hipGetLastError());
-        WG_HIP(c, hipStreamSynchronize(st));
         return WG_OK;
     }
     case SH_X2: {   // rows of every unresolved reference -> crossing table; lanes up to the chain tokens
@@ -751,9 +777,8 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         S.step = SH_X3;
         if ((rc = sh_send(c, 16 + nown * 4, out)) != WG_OK) return rc;
         uint32_t h4[4] = {(uint32_t)nev, (uint32_t)naux, viol, 0};
-        WG_HIP(c, hipMemcpyAsync(S.msg.p, h4, 16, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), make_uint4(h4[0], h4[1], h4[2], h4[3]));
         if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(S.msg.as<uint8_t>() + 16))) != WG_OK) return rc;
-        WG_HIP(c, hipStreamSynchronize(st));
         return WG_OK;
     }
     case SH_X3: {   // global event ids; this shard's event records
@@ -785,13 +810,12 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         const uint64_t nev = S.nev_own, naux = S.naux_own;
         if ((rc = sh_send(c, 16 + nev * 16 + naux * 4, out)) != WG_OK) return rc;
         uint32_t h5[4] = {(uint32_t)nev, (uint32_t)naux, 0, 0};
-        WG_HIP(c, hipMemcpyAsync(S.msg.p, h5, 16, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), make_uint4(h5[0], h5[1], h5[2], h5[3]));
         LfRange R = sh_range(c);
         uint8_t *m = S.msg.as<uint8_t>();
         if ((rc = wg_lf_events(c, R, (uint32_t)S.evoff[S.rank], S.xt.as<const uint32_t>(), reinterpret_cast<uint4 *>(m + 16),
                                reinterpret_cast<uint32_t *>(m + 16 + nev * 16), (uint32_t)S.auxoff[S.rank])) != WG_OK)
             return rc;
-        WG_HIP(c, hipStreamSynchronize(st));
         return WG_OK;
     }
     case SH_X4: {   // replay the global event stream; lanes of own rows; default geometry
@@ -830,10 +854,8 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_ALLOC(c, c->color_out, nloc + 4);
         hipLaunchKernelGGL(k_sh_lane_out, dim3(blocks(nloc)), dim3(T), 0, st, s, nl, c->lane_asg.as<const uint32_t>(),
                            c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>());
-        // heights of rows [0, e) (the last row of the LIST is ROW_HEIGHT)
-        WG_ALLOC(c, S.h_g, e * 4 + 4);
-        if ((rc = wg_heights_run(c, e, S.N, S.h_g.as<float>())) != WG_OK) return rc;
         c->have_layout = true;
+        c->layout_gen++;
         return sh_geometry_begin(c, nullptr, out);
     }
     case SH_X6:

@@ -76,7 +76,7 @@ def lib():
                                       ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_geometry_begin": ([vp, vp, i32, ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_copy_msg": ([vp, vp], ctypes.c_int),
-            "wg_shard_exchange": ([vp, vp, u64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(abi.ShardMsg)],
+            "wg_shard_exchange": ([vp, vp, u64, ctypes.POINTER(ctypes.c_uint64), vp, ctypes.POINTER(abi.ShardMsg)],
                                   ctypes.c_int),
         }
         for name, (args, res) in sig.items():
@@ -169,11 +169,17 @@ class Engine:
         self._shard_loop(msg, comm)
 
     def _shard_loop(self, msg, comm):
+        # wg_shard_exchange may leave reads of the gathered buffer queued on the
+        # engine's stream: each buffer is kept until the next wg_shard_copy_msg
+        # (which synchronises that stream) has returned
         while not msg.done:
             gathered, off, stride, sizes = comm.allgather(
                 int(msg.bytes), lambda dst: self._check(lib().wg_shard_copy_msg(self._ctx, dst)), step=int(msg.step))
+            self._gathered = gathered
             sz = (ctypes.c_uint64 * len(sizes))(*sizes)
-            self._check(lib().wg_shard_exchange(self._ctx, gathered.data_ptr() + off, stride, sz, ctypes.byref(msg)))
+            heads = getattr(comm, "heads", None)   # host copy of each message's 16-byte header, if the comm has it
+            hp = heads.ctypes.data if heads is not None else None
+            self._check(lib().wg_shard_exchange(self._ctx, gathered.data_ptr() + off, stride, sz, hp, ctypes.byref(msg)))
             del gathered
 
     def layout_summary(self) -> abi.LayoutSummary:

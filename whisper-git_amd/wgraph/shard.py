@@ -7,6 +7,7 @@ device buffer: rank r's message at r * stride.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -46,6 +47,7 @@ class ShardComm:
         self.exchanges = 0
         self.collectives = 0
         self.bytes_sent = 0
+        self.heads = None   # host copy of every message's first 16 bytes (uint32 [world, 4]), last exchange
 
     @staticmethod
     def round_cap(n: int) -> int:
@@ -71,15 +73,18 @@ class ShardComm:
             else:
                 dist.all_gather(list(out.view(self.world, stride).unbind(0)), send, group=self.group)
             self.collectives += 1
-            sizes = [int(x) for x in out.view(self.world, stride)[:, :8].contiguous().view(torch.int64).view(-1).cpu()]
+            # one device->host read: every slot's length and its message's 16-byte header
+            head = out.view(self.world, stride)[:, :32].cpu().numpy()
+            sizes = [int(x) for x in head[:, :8].copy().view(np.int64).reshape(-1)]
+            self.heads = np.ascontiguousarray(head[:, 16:32]).view(np.uint32).reshape(self.world, 4)
             if max(sizes) <= cap:
                 break
             cap = self.round_cap(max(sizes))
         self.caps[step] = cap
         if not self.on_device and self.device.type != "cpu":
             out = out.to(self.device)
-        if self.device.type != "cpu":
-            torch.cuda.current_stream(self.device).synchronize()
+        if self.device.type != "cpu" and not self.on_device:
+            torch.cuda.current_stream(self.device).synchronize()   # the H2D copy above
         self.exchanges += 1
         self.bytes_sent += nbytes
         return out, self.HDR, stride, sizes
