@@ -98,6 +98,8 @@ struct ShardState {
     DevBuf dev_small;
     DevBuf h_g, rt_g;         // heights of rows [0, e) / row_top of rows [s, e] (below s: unspecified)
     bool rt_zero = false;     // rt_g holds the zero-band row_top (computed at build begin, side stream)
+    uint64_t local_gen = ~0ull;           // layout_gen of the local edges (c->edges / edge_cnt / in_scan)
+    uint64_t local_ne = 0, local_nin = 0; // local edges, of which incoming
     DevBuf band_host;         // device copy of a host band array [N]
     const float *band_g = nullptr;
     DevBuf xchild, xpar;      // per crossing entry: child lane/colour, parent lane/y

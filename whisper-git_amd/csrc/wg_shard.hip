@@ -248,15 +248,16 @@ __global__ void k_sh_pack_ends(uint64_t s, uint64_t e, const WgXEnt *__restrict_
 }
 
 // scatter every rank's endpoint records into per-entry tables
-__global__ void k_sh_unpack_ends(Sections S, const uint64_t *__restrict__ nown, uint4 *__restrict__ xchild,
-                                 uint4 *__restrict__ xpar) {
+struct RankCounts { uint64_t v[16]; };   // by value: no host buffer outlives the launch
+
+__global__ void k_sh_unpack_ends(Sections S, RankCounts nown, uint4 *__restrict__ xchild, uint4 *__restrict__ xpar) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= S.off[S.world]) return;
     const uint32_t r = section_of(S, g);
     const uint64_t q = g - S.off[r];
     const uint4 v = reinterpret_cast<const uint4 *>(S.base + r * S.stride + 16)[q];
     if (v.x == 0xFFFFFFFFu) return;
-    if (q < nown[r]) xchild[v.x] = v;
+    if (q < nown.v[r]) xchild[v.x] = v;
     else xpar[v.x] = v;
 }
 
@@ -310,6 +311,7 @@ struct LocalEdgeArgs {
     wg_edge *edges;             // local
     float2 *edge_y;
     wg_edge *own_g;             // own edges, global numbering
+    uint32_t y_only;            // same layout as the last pass: the edges stand, only edge_y changes
 };
 
 __device__ __forceinline__ void far_parent(const LocalEdgeArgs &A, uint64_t p, uint64_t x, uint32_t *pl, uint32_t *plane,
@@ -334,6 +336,8 @@ __global__ void k_sh_edges_in(LocalEdgeArgs A) {
     uint32_t pl, plane;
     float py;
     far_parent(A, en.p, x, &pl, &plane, &py);
+    A.edge_y[o] = make_float2(__uint_as_float(A.xchild[x].w), py);   // the child's shard sent its y
+    if (A.y_only) return;
     wg_edge ed;
     ed.child_row = 0;
     ed.child_lane = A.xchild[x].y;
@@ -341,7 +345,6 @@ __global__ void k_sh_edges_in(LocalEdgeArgs A) {
     ed.parent_lane = plane;
     ed.color = A.xchild[x].z;
     A.edges[o] = ed;
-    A.edge_y[o] = make_float2(__uint_as_float(A.xchild[x].w), py);   // the child's shard sent its y
 }
 
 __global__ void k_sh_edges_own(LocalEdgeArgs A) {
@@ -358,6 +361,8 @@ __global__ void k_sh_edges_own(LocalEdgeArgs A) {
         uint32_t pl, plane;
         float py;
         far_parent(A, (uint64_t)p, (uint64_t)p >= A.e ? A.xown_begin + A.refx[k] : 0, &pl, &plane, &py);
+        A.edge_y[o] = make_float2(cy, py);
+        if (A.y_only) { o++; continue; }
         wg_edge ed;
         ed.child_row = (uint32_t)(i + 1);
         ed.child_lane = cl;
@@ -365,7 +370,6 @@ __global__ void k_sh_edges_own(LocalEdgeArgs A) {
         ed.parent_lane = plane;
         ed.color = col;
         A.edges[o] = ed;
-        A.edge_y[o] = make_float2(cy, py);
         ed.child_row = (uint32_t)gi;
         ed.parent_row = (uint32_t)p;
         A.own_g[o - n_in] = ed;
@@ -517,16 +521,15 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     std::vector<uint32_t> hdr;
     int rc = read_headers(c, gathered, stride, hdr);
     if (rc != WG_OK) return rc;
-    std::vector<uint64_t> cnt(W), nown(W);
-    for (int r = 0; r < W; r++) { nown[r] = hdr[4 * r]; cnt[r] = hdr[4 * r] + hdr[4 * r + 1]; }
+    std::vector<uint64_t> cnt(W);
+    RankCounts nown{};
+    for (int r = 0; r < W; r++) { nown.v[r] = hdr[4 * r]; cnt[r] = hdr[4 * r] + hdr[4 * r + 1]; }
     WG_ALLOC(c, S.xchild, nx * 16 + 16);
     WG_ALLOC(c, S.xpar, nx * 16 + 16);
-    WG_ALLOC(c, S.dev_small, 64 * 8);
-    WG_HIP(c, hipMemcpyAsync(S.dev_small.p, nown.data(), W * 8, hipMemcpyHostToDevice, st));
     Sections SX = make_sections(gathered, stride, W, cnt);
     if (SX.off[W])
-        hipLaunchKernelGGL(k_sh_unpack_ends, dim3(blocks(SX.off[W])), dim3(T), 0, st, SX, S.dev_small.as<const uint64_t>(),
-                           S.xchild.as<uint4>(), S.xpar.as<uint4>());
+        hipLaunchKernelGGL(k_sh_unpack_ends, dim3(blocks(SX.off[W])), dim3(T), 0, st, SX, nown, S.xchild.as<uint4>(),
+                           S.xpar.as<uint4>());
     // local rows
     const float *band_g = S.band_g;
     WG_ALLOC(c, c->heights, nloc * 4 + 4);
@@ -535,26 +538,33 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     hipLaunchKernelGGL(k_sh_local_rows, dim3(blocks(nloc + 1)), dim3(T), 0, st, s, nl, S.h_g.as<const float>(), band_g,
                        S.rt_g.as<const float>(), c->heights.as<float>(), band_g ? c->band.as<float>() : nullptr,
                        c->g_row_top.as<float>());
-    // local edges: incoming (earlier shards, edge order) then own
+    // local edges: incoming (earlier shards, edge order) then own.  A later pass
+    // on the same layout keeps them and rewrites only their endpoint y.
     const uint64_t xin = S.xoff[S.rank];
-    WG_ALLOC(c, S.in_scan, (xin + 2) * 4);
-    WG_ALLOC(c, c->edge_cnt, (nloc + 2) * 4);
-    { const int _sr = wg_scan_reserve(c, nloc + xin + 2); if (_sr != WG_OK) return _sr; }
-    WG_HIP(c, hipMemsetAsync(S.in_scan.p, 0, 8, st));
-    if (xin) hipLaunchKernelGGL(k_sh_in_flags, dim3(blocks(xin)), dim3(T), 0, st, s, S.xall.as<const WgXEnt>(), xin,
-                                S.in_scan.as<uint32_t>());
-    WG_HIP(c, wg_exclusive_scan_u32(S.in_scan.as<uint32_t>(), S.in_scan.as<uint32_t>(), xin, c->scan_tmp.p, st));
     const int32_t *prow = S.prow.as<const int32_t>() - S.E0;
-    hipLaunchKernelGGL(k_sh_own_counts, dim3(blocks(nloc)), dim3(T), 0, st, s, nl, c->d_poff, prow,
-                       S.in_scan.as<const uint32_t>(), xin, c->edge_cnt.as<uint32_t>());
-    WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), nloc, c->scan_tmp.p, st));
-    uint64_t tot[2] = {0, 0};
-    if ((rc = wg_fetch(c, {{c->edge_cnt.as<uint32_t>() + nloc, false}, {c->edge_cnt.as<uint32_t>() + 1, false}}, tot)) != WG_OK)
-        return rc;
-    const uint64_t ne = tot[0], n_in = tot[1];
-    WG_ALLOC(c, c->edges, ne * sizeof(wg_edge) + 16);
-    WG_ALLOC(c, S.edge_y, ne * 8 + 16);
-    WG_ALLOC(c, S.own_edges, (ne - n_in) * sizeof(wg_edge) + 16);
+    const bool same_layout = S.local_gen == c->layout_gen;
+    if (!same_layout) {
+        WG_ALLOC(c, S.in_scan, (xin + 2) * 4);
+        WG_ALLOC(c, c->edge_cnt, (nloc + 2) * 4);
+        { const int _sr = wg_scan_reserve(c, nloc + xin + 2); if (_sr != WG_OK) return _sr; }
+        WG_HIP(c, hipMemsetAsync(S.in_scan.p, 0, 8, st));
+        if (xin) hipLaunchKernelGGL(k_sh_in_flags, dim3(blocks(xin)), dim3(T), 0, st, s, S.xall.as<const WgXEnt>(), xin,
+                                    S.in_scan.as<uint32_t>());
+        WG_HIP(c, wg_exclusive_scan_u32(S.in_scan.as<uint32_t>(), S.in_scan.as<uint32_t>(), xin, c->scan_tmp.p, st));
+        hipLaunchKernelGGL(k_sh_own_counts, dim3(blocks(nloc)), dim3(T), 0, st, s, nl, c->d_poff, prow,
+                           S.in_scan.as<const uint32_t>(), xin, c->edge_cnt.as<uint32_t>());
+        WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), nloc, c->scan_tmp.p, st));
+        uint64_t tot[2] = {0, 0};
+        if ((rc = wg_fetch(c, {{c->edge_cnt.as<uint32_t>() + nloc, false}, {c->edge_cnt.as<uint32_t>() + 1, false}}, tot)) !=
+            WG_OK)
+            return rc;
+        S.local_ne = tot[0];
+        S.local_nin = tot[1];
+        WG_ALLOC(c, c->edges, S.local_ne * sizeof(wg_edge) + 16);
+        WG_ALLOC(c, S.edge_y, S.local_ne * 8 + 16);
+        WG_ALLOC(c, S.own_edges, (S.local_ne - S.local_nin) * sizeof(wg_edge) + 16);
+    }
+    const uint64_t ne = S.local_ne, n_in = S.local_nin;
     LocalEdgeArgs A;
     A.s = s; A.nl = nl; A.e = e; A.xin_end = xin; A.xown_begin = S.xoff[S.rank];
     A.xall = S.xall.as<const WgXEnt>();
@@ -572,6 +582,7 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     A.edges = c->edges.as<wg_edge>();
     A.edge_y = S.edge_y.as<float2>();
     A.own_g = S.own_edges.as<wg_edge>();
+    A.y_only = same_layout ? 1u : 0u;
     if (xin) hipLaunchKernelGGL(k_sh_edges_in, dim3(blocks(xin)), dim3(T), 0, st, A);
     if (nl) hipLaunchKernelGGL(k_sh_edges_own, dim3(blocks(nl)), dim3(T), 0, st, A);
     WG_HIP(c, hipGetLastError());
@@ -579,6 +590,7 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     c->n_edges = ne;
     c->edge_y = S.edge_y.as<const float>();
     S.n_own_edges = ne - n_in;
+    S.local_gen = c->layout_gen;
     rc = wg_stage_geometry(c, band_g ? c->band.as<const float>() : nullptr);
     if (rc != WG_OK) return rc;
     c->have_geom = true;
