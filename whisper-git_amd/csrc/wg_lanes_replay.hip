@@ -33,6 +33,10 @@
 namespace {
 
 enum : uint32_t { F_A = 1u, F_O = 2u, F_C = 4u, F_M = 8u, F_IN0 = 1u << 14, F_IN1 = 1u << 22 };
+#ifndef WG_JMAX
+#define WG_JMAX 6
+#endif
+constexpr int JMAX = WG_JMAX;   // speculative passes per batch before the scalar replay takes over
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
@@ -68,13 +72,17 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
     if (e0 >= A.nev) return;
     const uint64_t e1 = (e0 + A.chunk < A.nev) ? e0 + A.chunk : A.nev;
     uint64_t occ = c == 0 ? 0ull : A.occ_prev[c - 1];
-    uint32_t max_lane = 0, max_s = 0;
+    uint64_t occ_or = 0, alloc_or = 0;   // OR of the occupancy after each occupying allocation / of allocated slots
     bool diff = false;
     uint32_t prev_v = 0;
     const uint4 *ev = A.ev;
     uint4 rec = ev[e0 + lid];
     uint4 rec1 = ev[e0 + 64 + lid];
     uint32_t q0_v = 0, q1_v = 0;
+    // the previous iteration's slot of every event: the guess of the batch's
+    // speculative replay and the reference of the change check
+    uint32_t gp_v = (e0 + lid < e1) ? A.slot_prev[e0 + lid] : 0u;
+    uint64_t occ_or_v = 0, alloc_or_v = 0;   // per-lane parts of max_lane / max_s
     // old tokens of the first batch: all born before e0 -> iteration i-1
     if ((rec.x & F_C) && (uint64_t)rec.y < e0) q0_v = A.slot_prev[rec.y];
     if ((rec.x & F_C) && (uint64_t)rec.z < e0) q1_v = A.slot_prev[rec.z];
@@ -82,6 +90,7 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         const uint32_t f_v = (base + lid < e1) ? rec.x : 0u;   // lanes past the chunk: no-op
         const uint32_t t0_v = rec.y, t1_v = rec.z, row_v = rec.w;
         const uint4 rec2 = ev[base + 128 + lid];
+        const uint32_t gp_next = (base + 64 + lid < e1) ? A.slot_prev[base + 64 + lid] : 0u;
         // old tokens of the next batch (born before `base`): earlier chunks from
         // iteration i-1, this chunk's earlier batches from this iteration
         uint32_t n0_v = 0, n1_v = 0;
@@ -111,9 +120,73 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
             const uint32_t so = (uint32_t)__shfl_up((int)st, d, 64);
             if (lid >= (uint32_t)d && !st) { q &= qo; st |= so; }
         }
-        // ---- sequential part: special events only ----------------------------------
         const uint64_t sm = __ballot(special);
         uint64_t smask = sm;
+        // ---- speculative replay of the whole batch --------------------------------------
+        // Every event is a map occ -> (occ & Am) | Om of the occupancy; given a
+        // guess of every special event's slot, one ordered scan of the maps gives
+        // the occupancy before each event and from it each event's slot
+        // (allocation: lowest free slot; merge: the minimum waiter).  Iterating
+        // guess <- result is exact at a fixed point (lane 0 is exact from the
+        // entry occupancy, lane i once lanes < i are), and lanes before the first
+        // mismatch are exact at any time, so the scalar replay below only takes
+        // over from there.  The guess is the previous iteration's slot, which is
+        // already right for every chunk whose entry did not change.
+        if (sm && !__any((f_v & F_M) != 0)) {
+            const bool isA = (f_v & F_A) != 0, occupy = (f_v & F_O) != 0;
+            const bool clrS = isC && special && !isA;
+            const uint32_t src0 = (f_v >> 8) & 63u, src1 = (f_v >> 16) & 63u;
+            uint32_t g = special ? gp_v : cur_v;
+            uint64_t ob = occ, oa = occ, mism = ~0ull;
+            for (int it = 0; it < JMAX && mism; it++) {
+                const uint32_t ga = (uint32_t)__shfl((int)g, (int)src0, 64);
+                const uint32_t gb = (uint32_t)__shfl((int)g, (int)src1, 64);
+                const uint32_t a = (f_v & F_IN0) ? ga : s0, b = (f_v & F_IN1) ? gb : s1;
+                const uint32_t m = a < b ? a : b;
+                uint64_t Am = amask, Om = 0;
+                if (isA) { Am = ~0ull; Om = occupy ? 1ull << (g & 63u) : 0ull; }
+                else if (clrS) { Am = ~((1ull << (a & 63u)) | (1ull << (b & 63u))); Om = occupy ? 1ull << (m & 63u) : 0ull; }
+                for (int d = 1; d < 64; d <<= 1) {   // inclusive scan of the maps, in event order
+                    const uint64_t Ap = shfl_up64(Am, d), Op = shfl_up64(Om, d);
+                    if (lid >= (uint32_t)d) { Om = (Op & Am) | Om; Am = Ap & Am; }
+                }
+                oa = (occ & Am) | Om;
+                ob = shfl_up64(oa, 1);
+                if (lid == 0) ob = occ;
+                const uint32_t ng = isA ? (uint32_t)__builtin_ctzll(~ob | (1ull << 63)) : (clrS ? m : cur_v);
+                mism = __ballot(ng != g);   // lanes before the first mismatch kept their (exact) slot and oa
+                g = ng;
+            }
+            // lanes [0, lim) are exact (and lane lim's slot, from an exact occupancy)
+            const uint32_t lim = mism ? (uint32_t)__builtin_ctzll(mism) : 64u;
+            if (lid < lim) {
+                if (isA && occupy) occ_or_v |= oa;
+                if (isA) alloc_or_v |= 1ull << (g & 63u);
+            }
+            if (!mism) {
+                cur_v = g;
+                occ = rl64(oa, 63);
+                smask = 0;                                   // the scan already covered every event
+            } else {
+                cur_v = (lid <= lim) ? g : cur_v;
+                occ = rl64(ob, lim);                          // exact occupancy before event lim
+                smask = sm & (~0ull << lim);
+                const uint64_t bit = 1ull << (rl(g, lim) & 63u);
+                const uint32_t fl = rl(f_v, lim);
+                if (fl & F_A) {                              // event lim itself is exact: apply it
+                    alloc_or |= bit;
+                    if (fl & F_O) { occ |= bit; occ_or |= occ; }
+                } else {
+                    const uint32_t pk = rl(s0, lim), pk1 = rl(s1, lim);
+                    const uint32_t a = (fl & F_IN0) ? rl(cur_v, (fl >> 8) & 63u) : pk;
+                    const uint32_t b = (fl & F_IN1) ? rl(cur_v, (fl >> 16) & 63u) : pk1;
+                    occ &= ~((1ull << (a & 63u)) | (1ull << (b & 63u)));
+                    if (fl & F_O) occ |= bit;
+                }
+                smask &= smask - 1;                          // continue after event lim
+            }
+        }
+        // ---- sequential part: special events (from the first unresolved one) --------
         while (smask) {
             const uint32_t k = (uint32_t)__builtin_ctzll(smask);
             smask &= smask - 1;
@@ -122,12 +195,11 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
             uint32_t s;
             if (f & F_A) {
                 s = (uint32_t)__builtin_ctzll(~occ | (1ull << 63));
+                alloc_or |= 1ull << s;
                 if (f & F_O) {
                     occ |= 1ull << s;
-                    const uint32_t hb = 63u - (uint32_t)__builtin_clzll(occ);
-                    max_lane = hb > max_lane ? hb : max_lane;
+                    occ_or |= occ;
                 }
-                max_s = s > max_s ? s : max_s;
             } else {
                 // tokens born in this batch, or more than two waiters
                 uint32_t a = rl(s0, k), b = rl(s1, k);
@@ -158,9 +230,10 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         occ &= (sm >> 63) ? ~0ull : rl64(q, 63);
         if (base + lid < e1) {
             const uint8_t nv = (uint8_t)cur_v;
-            diff |= A.slot_prev[base + lid] != nv;
+            diff |= gp_v != nv;
             A.slot_next[base + lid] = nv;
         }
+        gp_v = gp_next;
         // same-wave vector memory ops to one address complete in order; only keep
         // the compiler from moving the next batch's token loads above the store
         asm volatile("" ::: "memory");
@@ -170,10 +243,18 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         q0_v = n0_v;
         q1_v = n1_v;
     }
+    for (int d = 32; d >= 1; d >>= 1) {
+        occ_or_v |= ((uint64_t)(uint32_t)__shfl_xor((int)(occ_or_v >> 32), d, 64) << 32) |
+                    (uint32_t)__shfl_xor((int)(uint32_t)occ_or_v, d, 64);
+        alloc_or_v |= ((uint64_t)(uint32_t)__shfl_xor((int)(alloc_or_v >> 32), d, 64) << 32) |
+                      (uint32_t)__shfl_xor((int)(uint32_t)alloc_or_v, d, 64);
+    }
+    occ_or |= occ_or_v;
+    alloc_or |= alloc_or_v;
     if (lid == 0) {
         A.occ_next[c] = occ;
-        A.chunk_stats[2 * c] = max_lane;
-        A.chunk_stats[2 * c + 1] = max_s;
+        A.chunk_stats[2 * c] = occ_or ? 63u - (uint32_t)__builtin_clzll(occ_or) : 0u;         // max_lane
+        A.chunk_stats[2 * c + 1] = alloc_or ? 63u - (uint32_t)__builtin_clzll(alloc_or) : 0u; // max slot
     }
     if (__any(diff) || (lid == 0 && occ != A.occ_prev[c])) A.changed[A.iter] = 1u;
 }
