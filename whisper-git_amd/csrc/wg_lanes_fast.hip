@@ -207,11 +207,46 @@ __global__ void k_lf_sp_init(uint64_t nl, const uint32_t *__restrict__ winfo, co
     else sp[j] = ch[ch_off[j]];                                 // waiter = the only first-parent child
 }
 
-__global__ void k_lf_jump(uint64_t nl, const uint32_t *__restrict__ in, uint32_t *__restrict__ out) {
+// Chain sources: sp[j] is a token (tagged) or the row whose token row j
+// inherits, always an earlier row.  Resolution in two phases:
+//   k_lf_jump_tile  pointer jumping inside tiles of JT_ROWS rows in LDS:
+//                   afterwards every pointer leaves its tile (or is a token);
+//   k_lf_jump4      each pass follows up to 4 links, so P becomes P^4: every
+//                   link crosses a tile, and ceil(log4(tiles)) passes finish.
+constexpr int JT_THREADS = 1024, JT_ROWS = 4096;
+
+__global__ void __launch_bounds__(JT_THREADS) k_lf_jump_tile(uint64_t nl, uint32_t *__restrict__ sp) {
+    __shared__ uint32_t L[JT_ROWS];
+    const uint64_t t0 = (uint64_t)blockIdx.x * JT_ROWS;
+    const uint32_t nt = (uint32_t)((nl - t0) < (uint64_t)JT_ROWS ? (nl - t0) : (uint64_t)JT_ROWS);
+    for (uint32_t i = threadIdx.x; i < nt; i += JT_THREADS) L[i] = sp[t0 + i];
+    __syncthreads();
+    // in place: a stored value is always a later link of the same chain, so a
+    // racing read only skips further; stop once no pointer stays in the tile
+    for (;;) {
+        int moved = 0;
+        for (uint32_t i = threadIdx.x; i < nt; i += JT_THREADS) {
+            const uint32_t v = L[i];
+            if (!(v & TAGS) && (uint64_t)v >= t0) {   // pointer inside the tile (always to an earlier row)
+                L[i] = L[v - t0];
+                moved = 1;
+            }
+        }
+        if (!__syncthreads_or(moved)) break;
+    }
+    for (uint32_t i = threadIdx.x; i < nt; i += JT_THREADS) sp[t0 + i] = L[i];
+}
+
+__global__ void k_lf_jump4(uint64_t nl, const uint32_t *__restrict__ in, uint32_t *__restrict__ out) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nl) return;
-    const uint32_t v = in[j];
-    out[j] = (v & TAGS) ? v : in[v];
+    uint32_t v = in[j];
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        if (v & TAGS) break;
+        v = in[v];
+    }
+    out[j] = v;
 }
 
 // token of every own crossing entry: the chain of its child row (first
@@ -378,12 +413,14 @@ int wg_lf_chain(wg_ctx *c, const LfRange &R) {
     if (n) hipLaunchKernelGGL(k_lf_sp_init, dim3(blocks(n)), dim3(T), 0, s, n, winfo.as<const uint32_t>(),
                               ev_off.as<const uint32_t>(), ch_off.as<const uint32_t>(), ch.as<const uint32_t>(),
                               secev.as<const uint32_t>(), spA.as<uint32_t>());
-    // pointer jumping: after r rounds every pointer skips 2^r chain links
+    // chain resolution: tiles in LDS, then passes of 4 links over the tile crossings
+    const uint64_t ntiles = (n + JT_ROWS - 1) / JT_ROWS;
+    if (n) hipLaunchKernelGGL(k_lf_jump_tile, dim3(ntiles), dim3(JT_THREADS), 0, s, n, spA.as<uint32_t>());
     int rounds = 0;
-    while ((1ull << rounds) < n + 1) rounds++;
+    for (uint64_t reach = 1; reach < ntiles; reach *= 4) rounds++;
     DevBuf *in = &spA, *out = &spB;
     for (int r = 0; r < rounds; r++) {
-        hipLaunchKernelGGL(k_lf_jump, dim3(blocks(n)), dim3(T), 0, s, n, in->as<const uint32_t>(), out->as<uint32_t>());
+        hipLaunchKernelGGL(k_lf_jump4, dim3(blocks(n)), dim3(T), 0, s, n, in->as<const uint32_t>(), out->as<uint32_t>());
         DevBuf *t = in; in = out; out = t;
     }
     c->lf_sp_b = (in == &spB);
