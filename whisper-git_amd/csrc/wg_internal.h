@@ -154,6 +154,7 @@ struct wg_ctx {
     DevBuf lf[24];          // event-compressed lane path workspaces (wg_lanes_fast.hip)
     uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
     uint32_t replay_iters = 0;     // iterations the last replay needed
+    uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
     uint64_t n_events = 0;  // events of the last fast-path lane build
     uint64_t e_refs_own = 0;   // parent references of the rows this context owns
     bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])
@@ -266,10 +267,18 @@ hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, 
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
 int wg_stage_lanes(wg_ctx *c);                // wg_lanes.hip
 int wg_lanes_fast(wg_ctx *c, bool *used);     // wg_lanes_fast.hip
-hipError_t wg_lane_replay(wg_ctx *c, hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *aux,
-                          uint8_t *slots_a, uint8_t *slots_b, unsigned long long *occ_a, unsigned long long *occ_b,
-                          uint32_t *stats, uint32_t *flags, uint32_t max_iters, uint32_t *scal, uint8_t **slot_out,
-                          uint32_t *iters);  // wg_lanes_replay.hip
+// event replay to a fixed point (wg_lanes_replay.hip)
+struct ReplayRun {
+    uint64_t nev = 0, nch = 0;
+    uint32_t chunk = 512, it = 0, max_iters = 0;
+    const uint4 *ev = nullptr;
+    const uint32_t *aux = nullptr;
+    uint8_t *slots_a = nullptr, *slots_b = nullptr, *sp_prev = nullptr, *sp_next = nullptr;   // sp_prev: last written
+    unsigned long long *occ_a = nullptr, *occ_b = nullptr, *op = nullptr, *on = nullptr;
+    uint32_t *stats = nullptr, *flags = nullptr, *scal = nullptr;
+};
+hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blind);
+hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged);
 int wg_stage_edges(wg_ctx *c);                // wg_lanes.hip
 // event-compressed lane phases over a row range (wg_lanes_fast.hip)
 int wg_lf_refs(wg_ctx *c, const LfRange &R, uint32_t *viol, uint64_t *nev, uint64_t *naux);
@@ -277,8 +286,10 @@ int wg_lf_chain(wg_ctx *c, const LfRange &R);
 int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok);
 int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint4 *ev_out, uint32_t *aux_out,
                  uint32_t aux_base);
-int wg_lf_replay(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, const uint8_t **slots, bool *converged);
-int wg_lf_lanes(wg_ctx *c, const LfRange &R, const uint8_t *slots, uint32_t *lane);
+// replay + lanes of the range + their scalars; *ok = false: no fixed point or
+// more than 63 slots (the caller takes its fallback)
+int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                       bool *ok);
 int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
 int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out);             // rows [0,m) of an n-row list
 // side stream (wg_api.hip): wg_side_fork makes the context's launches go to

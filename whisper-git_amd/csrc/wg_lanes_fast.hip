@@ -456,36 +456,67 @@ int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *
     return WG_OK;
 }
 
-// Replays nev global events (records padded with 256 zero records) and
-// leaves the slot of every event in *slots; scalars in c->lane_scalars.
-int wg_lf_replay(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, const uint8_t **slots, bool *converged) {
+// Replays nev global events (records padded with 256 zero records) to the
+// fixed point and assigns the lanes of the range; c->max_lane / n_slots.
+// The replay's convergence check rides on the lane-scalar read: steady-state
+// builds launch exactly the iterations they need with one host sync.
+int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                       bool *ok) {
     hipStream_t s = c->stream;
+    *ok = false;
     wg_stage_begin(c, "lf_loop");
-    const uint32_t chunk = c->replay_chunk;
-    const uint64_t nch = (nev + chunk - 1) / chunk + 1;
-    const uint32_t max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
+    ReplayRun run;
+    run.nev = nev;
+    run.chunk = c->replay_chunk;
+    const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
+    run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
     DevBuf &rflags = c->lf[LF_RFLAGS];
     WG_ALLOC(c, slot_a, nev + 64);
     WG_ALLOC(c, slot_b, nev + 64);
     WG_ALLOC(c, occ, nch * 16 + 16);
     WG_ALLOC(c, stats, nch * 8 + 8);
-    WG_ALLOC(c, rflags, (max_iters + 2) * 4);
-    uint8_t *out = nullptr;
-    uint32_t iters = 0;
-    WG_HIP(c, wg_lane_replay(c, s, nev, chunk, ev, aux, slot_a.as<uint8_t>(), slot_b.as<uint8_t>(),
-                             occ.as<unsigned long long>(), occ.as<unsigned long long>() + nch, stats.as<uint32_t>(),
-                             rflags.as<uint32_t>(), max_iters, c->lane_scalars.as<uint32_t>(), &out, &iters));
-    c->replay_iters = iters;
+    WG_ALLOC(c, rflags, (run.max_iters + 2) * 4);
+    run.ev = ev;
+    run.aux = aux;
+    run.slots_a = slot_a.as<uint8_t>();
+    run.slots_b = slot_b.as<uint8_t>();
+    run.occ_a = occ.as<unsigned long long>();
+    run.occ_b = occ.as<unsigned long long>() + nch;
+    run.stats = stats.as<uint32_t>();
+    run.flags = rflags.as<uint32_t>();
+    run.scal = c->lane_scalars.as<uint32_t>();
+    WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind));
+    const uint32_t blind = run.it;
+    const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
+    uint64_t sc[5] = {0, 0, 0, 1, 1};
+    bool conv = nev == 0;
+    for (int pass = 0; pass < 2; pass++) {
+        if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
+        WG_HIP(c, hipGetLastError());
+        if (nev && !conv) {
+            int rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}, {run.flags + run.it - 1, false},
+                                  {run.flags + run.it, false}}, sc);
+            if (rc != WG_OK) return rc;
+            conv = sc[3] == 0 || sc[4] == 0;
+        } else {
+            int rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc);
+            if (rc != WG_OK) return rc;
+        }
+        if (conv) break;
+        WG_HIP(c, wg_replay_resume(c, s, run, &conv));   // not there yet: iterate with polls
+        if (!conv) break;
+    }
     wg_stage_end(c);
-    *slots = out;
-    *converged = iters <= max_iters;
-    return WG_OK;
-}
-
-int wg_lf_lanes(wg_ctx *c, const LfRange &R, const uint8_t *slots, uint32_t *lane) {
-    if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, c->stream, R.nl, lf_sp(c), slots, lane);
-    WG_HIP(c, hipGetLastError());
+    c->replay_iters = run.it;
+    // next build: as many blind iterations as this one needed (one fewer if the
+    // fixed point came a launch early)
+    if (run.it > blind) c->replay_blind = run.it;
+    else if (sc[3] == 0 && c->replay_blind > 2) c->replay_blind--;
+    if (!conv || sc[2]) return WG_OK;               // no fixed point / more than 63 slots
+    c->max_lane = (uint32_t)sc[0];
+    c->n_slots = (uint32_t)sc[1];
+    *ok = true;
     return WG_OK;
 }
 
@@ -512,17 +543,10 @@ int wg_lanes_fast(wg_ctx *c, bool *used) {
     WG_ALLOC(c, aux, naux * 4 + 4);
     WG_HIP(c, hipMemsetAsync(evrec.as<uint4>() + nev, 0, 256 * 16, c->stream));   // no-op padding for the replay prefetch
     if ((rc = wg_lf_events(c, R, 0, nullptr, evrec.as<uint4>(), aux.as<uint32_t>(), 0)) != WG_OK) return rc;
-    const uint8_t *slots = nullptr;
-    bool conv = false;
-    if ((rc = wg_lf_replay(c, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(), &slots, &conv)) != WG_OK) return rc;
-    if (!conv) return WG_OK;                         // no fixed point within budget: general walk
-    if ((rc = wg_lf_lanes(c, R, slots, c->lane_asg.as<uint32_t>())) != WG_OK) return rc;
-    const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
-    uint64_t sc[3];
-    if ((rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc)) != WG_OK) return rc;
-    if (sc[2]) return WG_OK;                        // more than 63 slots: general walk
-    c->max_lane = (uint32_t)sc[0];
-    c->n_slots = (uint32_t)sc[1];
+    bool ok = false;
+    rc = wg_lf_replay_lanes(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(), c->lane_asg.as<uint32_t>(), &ok);
+    if (rc != WG_OK) return rc;
+    if (!ok) return WG_OK;                           // no fixed point / more than 63 slots: general walk
     c->lane_path = 0;
     *used = true;
     return WG_OK;

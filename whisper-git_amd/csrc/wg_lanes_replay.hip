@@ -28,6 +28,8 @@
 // ctz(~occ), :414-423), tokens born in the same batch and merges with more
 // than two waiters are replayed in order by the scalar unit.  max_lane is
 // the highest occupied slot after each occupying allocation (:462-471).
+#include <utility>
+
 #include "wg_internal.h"
 
 namespace {
@@ -286,49 +288,60 @@ __global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict_
 
 }  // namespace
 
-// Replays nev events into slot_out (one byte per event).  ws_* are caller
-// workspaces: slots (2 x (nev + 64) bytes), occ (2 x nchunks x 8 bytes),
-// stats (2 x nchunks x 4 bytes), flags (max_iters + 1 words).
-// Returns the number of iterations used (0 on a HIP error) in *iters.
-hipError_t wg_lane_replay(wg_ctx *c, hipStream_t s, uint64_t nev, uint32_t chunk, const uint4 *ev, const uint32_t *aux,
-                          uint8_t *slots_a, uint8_t *slots_b, unsigned long long *occ_a, unsigned long long *occ_b,
-                          uint32_t *stats, uint32_t *flags, uint32_t max_iters, uint32_t *scal, uint8_t **slot_out,
-                          uint32_t *iters) {
-    const uint64_t nch = (nev + chunk - 1) / chunk;
-    *iters = 0;
-    if (nev == 0) {
-        hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, (uint64_t)0, stats, scal);
-        *slot_out = slots_a;
+// Replay driver.  wg_replay_start initialises and launches `blind` iterations
+// without looking at the device (a fixed point found early makes the rest
+// exit at once); the caller reads flags[it - 1] / flags[it] together with
+// its own scalars and calls wg_replay_resume only when neither iteration was
+// a fixed point.  Chunk c is exact after c + 1 iterations, so nch + 1
+// iterations always reach the fixed point.
+hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blind) {
+    R.nch = (R.nev + R.chunk - 1) / R.chunk;
+    R.it = 0;
+    R.sp_prev = R.slots_a;
+    R.sp_next = R.slots_b;
+    R.op = R.occ_a;
+    R.on = R.occ_b;
+    if (R.max_iters > R.nch + 1) R.max_iters = (uint32_t)(R.nch + 1);
+    if (R.nev == 0) {
+        hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, (uint64_t)0, R.stats, R.scal);
         return hipGetLastError();
     }
-    const uint64_t ninit = nch > max_iters + 1 ? nch : max_iters + 1;
-    hipLaunchKernelGGL(k_lf_replay_init, dim3((ninit + 255) / 256), dim3(256), 0, s, nch, occ_a, flags, max_iters + 1);
-    hipError_t e = hipMemsetAsync(slots_a, 0, nev, s);
+    const uint64_t ninit = R.nch > R.max_iters + 1 ? R.nch : R.max_iters + 1;
+    hipLaunchKernelGGL(k_lf_replay_init, dim3((ninit + 255) / 256), dim3(256), 0, s, R.nch, R.occ_a, R.flags, R.max_iters + 1);
+    hipError_t e = hipMemsetAsync(R.slots_a, 0, R.nev, s);
     if (e != hipSuccess) return e;
-    uint8_t *sp_prev = slots_a, *sp_next = slots_b;
-    unsigned long long *op = occ_a, *on = occ_b;
-    uint32_t done_check = 0, next_poll = 3;
-    // chunk c is exact after c + 1 iterations, so nch + 1 iterations always converge
-    if (max_iters > nch + 1) max_iters = (uint32_t)(nch + 1);
-    for (uint32_t it = 1; it <= max_iters; it++) {
-        ReplayArgs a{nev, chunk, it, ev, aux, sp_prev, sp_next, op, on, stats, flags};
-        hipLaunchKernelGGL(k_lf_replay, dim3(nch), dim3(64), 0, s, a);
+    if (blind > R.max_iters) blind = R.max_iters;
+    for (uint32_t k = 0; k < blind; k++) {
+        R.it++;
+        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags};
+        hipLaunchKernelGGL(k_lf_replay, dim3(R.nch), dim3(64), 0, s, a);
         // after a fixed point later iterations do nothing; the converged slots are
         // in both buffers, so either pointer is final
-        uint8_t *t = sp_prev; sp_prev = sp_next; sp_next = t;
-        unsigned long long *o = op; op = on; on = o;
-        // poll at iterations 3, 6, 12, 24, ... (launches after a fixed point exit at once)
-        if (it == next_poll || it == max_iters) {
-            next_poll *= 2;
+        std::swap(R.sp_prev, R.sp_next);
+        std::swap(R.op, R.on);
+    }
+    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal);
+    return hipGetLastError();
+}
+
+// Continue with polls (every 3rd iteration, then doubling) until a fixed
+// point or max_iters; *converged tells which.
+hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged) {
+    *converged = R.nev == 0;
+    uint32_t next_poll = R.it + 3;
+    while (!*converged && R.it < R.max_iters) {
+        R.it++;
+        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags};
+        hipLaunchKernelGGL(k_lf_replay, dim3(R.nch), dim3(64), 0, s, a);
+        std::swap(R.sp_prev, R.sp_next);
+        std::swap(R.op, R.on);
+        if (R.it == next_poll || R.it == R.max_iters) {
+            next_poll = R.it + (next_poll - R.it + 3) * 2;
             uint64_t fl[2] = {1, 1};
-            if (wg_fetch(c, {{flags + it - 1, false}, {flags + it, false}}, fl) != WG_OK) return hipErrorUnknown;
-            done_check = it;
-            if (fl[0] == 0 || fl[1] == 0) { *iters = it; break; }
+            if (wg_fetch(c, {{R.flags + R.it - 1, false}, {R.flags + R.it, false}}, fl) != WG_OK) return hipErrorUnknown;
+            *converged = fl[0] == 0 || fl[1] == 0;
         }
     }
-    (void)done_check;
-    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, nch, stats, scal);
-    *slot_out = sp_prev;   // the buffer written last (== the other one at convergence)
-    if (*iters == 0) *iters = max_iters + 1;   // did not converge within max_iters
+    if (R.nev) hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal);
     return hipGetLastError();
 }

@@ -844,19 +844,13 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
                                                hipMemcpyDeviceToDevice, st));
         }
         c->n_events = nev;
-        const uint8_t *slots = nullptr;
-        bool conv = false;
-        if ((rc = wg_lf_replay(c, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(), &slots, &conv)) != WG_OK) return rc;
-        if (!conv) return sh_fallback(c, out);
         WG_ALLOC(c, c->lane_asg, nl * 4 + 4);
         LfRange R = sh_range(c);
-        if ((rc = wg_lf_lanes(c, R, slots, c->lane_asg.as<uint32_t>())) != WG_OK) return rc;
-        const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
-        uint64_t sc[3];
-        if ((rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc)) != WG_OK) return rc;
-        if (sc[2]) return sh_fallback(c, out);      // more than 63 slots: same decision on every rank
-        c->max_lane = (uint32_t)sc[0];
-        c->n_slots = (uint32_t)sc[1];
+        bool ok = false;
+        if ((rc = wg_lf_replay_lanes(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
+                                     c->lane_asg.as<uint32_t>(), &ok)) != WG_OK)
+            return rc;
+        if (!ok) return sh_fallback(c, out);        // no fixed point / > 63 slots: same decision on every rank
         c->lane_path = 0;
         const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
         const float gw = (float)vis * WG_LANE_W;
