@@ -91,10 +91,11 @@ int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out) {
     return wg_fetch_n(c, (int)items.size(), items.begin(), out);
 }
 
-int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out) {
+// mapped pinned words: [0, FETCH_MAX) for wg_fetch, [FETCH_MAX, 2 FETCH_MAX) for wg_fetch_begin
+static int fetch_launch(wg_ctx *c, int n, const WgFetch *items, uint64_t slot0) {
     if (n < 0 || n > FETCH_MAX) return wg_fail(c, WG_E_INVALID, "wg_fetch: too many items");
     if (!c->h_fetch) {
-        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, FETCH_MAX * sizeof(uint64_t), hipHostMallocMapped));
+        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, 2 * FETCH_MAX * sizeof(uint64_t), hipHostMallocMapped));
         WG_HIP(c, hipHostGetDevicePointer((void **)&c->d_fetch, c->h_fetch, 0));
     }
     FetchArgs a{};
@@ -104,10 +105,33 @@ int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out) {
         if (items[i].wide) a.wide |= 1ull << a.n;
         a.n++;
     }
-    hipLaunchKernelGGL(k_fetch, dim3(1), dim3(64), 0, c->stream, a, (unsigned long long *)c->d_fetch);
+    hipLaunchKernelGGL(k_fetch, dim3(1), dim3(64), 0, c->stream, a, (unsigned long long *)c->d_fetch + slot0);
     WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out) {
+    if (const int rc = fetch_launch(c, n, items, 0)) return rc;
     WG_HIP(c, hipStreamSynchronize(c->stream));
-    for (uint32_t i = 0; i < a.n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[i];
+    for (int i = 0; i < n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[i];
+    return WG_OK;
+}
+
+int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items) {
+    if (c->fetch_pending) return wg_fail(c, WG_E_STATE, "wg_fetch_begin: a fetch is pending");
+    if (const int rc = fetch_launch(c, (int)items.size(), items.begin(), FETCH_MAX)) return rc;
+    if (!c->ev_fetch) WG_HIP(c, hipEventCreateWithFlags(&c->ev_fetch, hipEventDisableTiming));
+    WG_HIP(c, hipEventRecord(c->ev_fetch, c->stream));
+    c->fetch_pending = (int)items.size();
+    return WG_OK;
+}
+
+int wg_fetch_end(wg_ctx *c, uint64_t *out) {
+    if (!c->fetch_pending) return wg_fail(c, WG_E_STATE, "wg_fetch_end: nothing pending");
+    const int n = c->fetch_pending;
+    c->fetch_pending = 0;
+    WG_HIP(c, hipEventSynchronize(c->ev_fetch));
+    for (int i = 0; i < n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[FETCH_MAX + i];
     return WG_OK;
 }
 
@@ -170,6 +194,7 @@ void wg_destroy(wg_ctx *c) {
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_fetch) (void)hipEventDestroy(c->ev_fetch);
     delete c;
 }
 

@@ -223,7 +223,9 @@ struct wg_ctx {
     int        stage_stack[8] = {0};
     int        stage_depth = 0;
     uint64_t   scratch_host[16];
-    uint64_t  *h_fetch = nullptr;   // mapped pinned host memory for wg_fetch
+    uint64_t  *h_fetch = nullptr;   // mapped pinned host memory for wg_fetch / wg_fetch_begin
+    hipEvent_t ev_fetch = nullptr;  // completion of the pending wg_fetch_begin
+    int        fetch_pending = 0;   // words of the pending wg_fetch_begin
     uint64_t  *d_fetch = nullptr;
 };
 
@@ -233,6 +235,10 @@ struct wg_ctx {
 struct WgFetch { const void *p; bool wide; };   // wide: 8-byte value, else 4-byte
 int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out);
 int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out);   // n <= 64
+// the same read without waiting: queue it, queue more work, then wg_fetch_end
+// (one pending at a time)
+int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items);
+int wg_fetch_end(wg_ctx *c, uint64_t *out);
 
 // error helpers -------------------------------------------------------------
 int wg_fail(wg_ctx *c, int code, const char *fmt, ...);

@@ -65,11 +65,15 @@ __global__ void k_vtx_counts(uint64_t rb, uint64_t re, int64_t sel, const uint32
 // A tile's verticals are vert[A(t) .. A(t+1) + sV(t+1)) and its curves
 // curve[K0(t) .. K0(t+1) + sC(t+1)), because every row's entries are
 // contiguous and rows are consecutive; a sentinel record closes the range.
+// tcap: tile records the buffer holds (the launch may precede the host's
+// knowledge of the total; a list that does not fit writes nothing)
 __global__ void k_tile_info(uint64_t rb, uint64_t rows, const uint64_t *__restrict__ vtx_off,
                             const uint32_t *__restrict__ voff, const uint32_t *__restrict__ coff,
-                            uint64_t ntiles, uint4 *__restrict__ info) {
+                            uint64_t tcap, uint4 *__restrict__ info) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= rows) return;
+    const uint64_t ntiles = (vtx_off[rows] + TILE - 1) / TILE;
+    if (ntiles + 1 > tcap) return;
     const uint64_t r = rb + j;
     const uint64_t s = vtx_off[j], e = vtx_off[j + 1];
     const uint32_t vo = voff[r], nv = voff[r + 1] - vo, co = coff[r], nc = coff[r + 1] - co;
@@ -114,7 +118,7 @@ __device__ __forceinline__ float clamp_rs(float x, float lo, float hi) {
     return x;
 }
 
-__global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint64_t total, uint32_t vis,
+__global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint64_t vcap, uint32_t vis,
         const uint64_t *__restrict__ vtx_off, const uint32_t *__restrict__ voff, const uint32_t *__restrict__ vert,
         const uint32_t *__restrict__ coff, const wg_curve *__restrict__ curve, const uint8_t *__restrict__ curve_color,
         const float *__restrict__ height, const float *__restrict__ node_y, const uint32_t *__restrict__ lane_out,
@@ -131,6 +135,10 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     __shared__ float2 circ[3][WG_TESS_NODE_SEGMENTS + 2];   // r*(cos, sin) for node, ring inner, ring outer radius
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t v0 = (uint64_t)blockIdx.x * TILE;
+    // the grid may be sized by the buffer's capacity: tiles past the total
+    // exit, and a total beyond the capacity writes nothing (the host relaunches)
+    const uint64_t total = vtx_off[re - rb];
+    if (v0 >= total || total > vcap) return;
     if (tid < 3 * (WG_TESS_NODE_SEGMENTS + 1)) {
         const uint32_t w = tid / (WG_TESS_NODE_SEGMENTS + 1), q = tid % (WG_TESS_NODE_SEGMENTS + 1);
         const float r = w == 0 ? WG_NODE_RADIUS
@@ -325,30 +333,42 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     hipLaunchKernelGGL(k_vtx_counts, dim3((rows + 255) / 256), dim3(256), 0, s, rb, re, sel,
                        c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off);
     WG_HIP(c, wg_exclusive_scan_u64(off, off, rows, c->scan_tmp.p, s));
-    uint64_t total = 0;
-    {
-        const int rc = wg_fetch(c, {{off + rows, true}}, &total);
-        if (rc != WG_OK) return rc;
-    }
-    c->n_vtx = total;
-    WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
     float q = roundf(c->graph_width / WG_LANE_W);
     uint32_t vis = q <= 0.0f ? 0u : (uint32_t)q;
     if (vis < 1) vis = 1;
+    // The total is read back without stalling the stream: the tiles are
+    // launched right away into the buffers as they are (steady-state frames
+    // fit the last frame's capacity; the kernels exit past the total and
+    // write nothing when it does not fit), and relaunched only if needed.
+    if (const int rc = wg_fetch_begin(c, {{off + rows, true}})) return rc;
+    auto launch = [&](uint64_t vcap, uint64_t tcap, uint64_t grid) {
+        hipLaunchKernelGGL(k_tile_info, dim3((rows + 255) / 256), dim3(256), 0, s, rb, rows, (const uint64_t *)off,
+                           c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), tcap,
+                           c->tile_first.as<uint4>());
+        wg_stage_end(c);
+        wg_stage_begin(c, "vtx_emit");
+        hipLaunchKernelGGL(k_vtx_tile, dim3(grid), dim3(VT), 0, s, rb, re, vcap, vis, (const uint64_t *)off,
+                           c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
+                           c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
+                           c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
+                           c->palette.as<const float4>(), c->tile_first.as<const uint4>(), c->vtx.as<float4>());
+        wg_stage_end(c);
+    };
+    const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;
+    const uint64_t tcap = c->tile_first.cap / sizeof(uint4);
+    const bool early = vcap > 0 && tcap > 1;
+    if (early) launch(vcap, tcap, std::min((vcap + TILE - 1) / TILE, tcap - 1));
+    uint64_t total = 0;
+    if (const int rc = wg_fetch_end(c, &total)) return rc;
+    c->n_vtx = total;
     const uint64_t ntiles = (total + TILE - 1) / TILE;
-    WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
-    hipLaunchKernelGGL(k_tile_info, dim3((rows + 255) / 256), dim3(256), 0, s, rb, rows, (const uint64_t *)off,
-                       c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), ntiles,
-                       c->tile_first.as<uint4>());
-    wg_stage_end(c);
-    wg_stage_begin(c, "vtx_emit");
-    hipLaunchKernelGGL(k_vtx_tile, dim3(ntiles), dim3(VT), 0, s, rb, re, total, vis, (const uint64_t *)off,
-                       c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
-                       c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
-                       c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
-                       c->palette.as<const float4>(), c->tile_first.as<const uint4>(), c->vtx.as<float4>());
+    if (!early || total > vcap || ntiles + 1 > tcap) {   // did not fit: size the buffers and launch again
+        if (early) wg_stage_begin(c, "vtx_counts");
+        WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
+        WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
+        launch(total, ntiles + 1, ntiles);
+    }
     WG_HIP(c, hipGetLastError());
-    wg_stage_end(c);
     return WG_OK;
 }
 
