@@ -118,7 +118,10 @@ int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out) {
 }
 
 int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items) {
-    if (c->fetch_pending) return wg_fail(c, WG_E_STATE, "wg_fetch_begin: a fetch is pending");
+    if (c->fetch_pending) {   // left behind by a failed call: drop it
+        (void)hipEventSynchronize(c->ev_fetch);
+        c->fetch_pending = 0;
+    }
     if (const int rc = fetch_launch(c, (int)items.size(), items.begin(), FETCH_MAX)) return rc;
     if (!c->ev_fetch) WG_HIP(c, hipEventCreateWithFlags(&c->ev_fetch, hipEventDisableTiming));
     WG_HIP(c, hipEventRecord(c->ev_fetch, c->stream));

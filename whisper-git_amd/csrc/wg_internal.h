@@ -287,7 +287,8 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
 hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged);
 int wg_stage_edges(wg_ctx *c);                // wg_lanes.hip
 // event-compressed lane phases over a row range (wg_lanes_fast.hip)
-int wg_lf_refs(wg_ctx *c, const LfRange &R, uint32_t *viol, uint64_t *nev, uint64_t *naux);
+int wg_lf_refs(wg_ctx *c, const LfRange &R);   // + wg_lf_refs_end after queueing wg_lf_chain
+int wg_lf_refs_end(wg_ctx *c, uint32_t *viol, uint64_t *nev, uint64_t *naux);
 int wg_lf_chain(wg_ctx *c, const LfRange &R);
 int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok);
 int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint4 *ev_out, uint32_t *aux_out,

@@ -222,12 +222,14 @@ __global__ void __launch_bounds__(JT_THREADS) k_lf_jump_tile(uint64_t nl, uint32
     for (uint32_t i = threadIdx.x; i < nt; i += JT_THREADS) L[i] = sp[t0 + i];
     __syncthreads();
     // in place: a stored value is always a later link of the same chain, so a
-    // racing read only skips further; stop once no pointer stays in the tile
-    for (;;) {
+    // racing read only skips further; stop once no pointer stays in the tile.
+    // Pointers lead to earlier rows on the inputs this path accepts, so 13
+    // rounds always suffice; the bound keeps any other input finite.
+    for (int round = 0; round < 32; round++) {
         int moved = 0;
         for (uint32_t i = threadIdx.x; i < nt; i += JT_THREADS) {
             const uint32_t v = L[i];
-            if (!(v & TAGS) && (uint64_t)v >= t0) {   // pointer inside the tile (always to an earlier row)
+            if (!(v & TAGS) && (uint64_t)v >= t0 && (uint64_t)v < t0 + nt && v - t0 != i) {   // inside the tile
                 L[i] = L[v - t0];
                 moved = 1;
             }
@@ -343,7 +345,7 @@ enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_C
 
 static const uint32_t *lf_sp(wg_ctx *c) { return c->lf_sp_b ? c->lf[LF_SPB].as<const uint32_t>() : c->lf[LF_SPA].as<const uint32_t>(); }
 
-int wg_lf_refs(wg_ctx *c, const LfRange &R, uint32_t *viol, uint64_t *nev, uint64_t *naux) {
+int wg_lf_refs(wg_ctx *c, const LfRange &R) {
     const uint64_t n = R.nl;
     hipStream_t s = c->stream;
     DevBuf &first_ref = c->lf[LF_FIRST], &fpc = c->lf[LF_FPC], &winfo = c->lf[LF_WINFO], &ev_off = c->lf[LF_EVOFF];
@@ -370,13 +372,15 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, uint32_t *viol, uint64_t *nev, uint6
                               fpc.as<const uint32_t>(), winfo.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(ev_off.as<uint32_t>(), ev_off.as<uint32_t>(), n, c->scan_tmp.p, s));
     WG_HIP(c, wg_exclusive_scan_u32(aux_off.as<uint32_t>(), aux_off.as<uint32_t>(), n, c->scan_tmp.p, s));
-    uint64_t hdr[3] = {0, 0, 0};
-    {
-        const int rc = wg_fetch(c, {{flags.p, false}, {ev_off.as<uint32_t>() + n, false}, {aux_off.as<uint32_t>() + n, false}},
-                                hdr);
-        if (rc != WG_OK) return rc;
-    }
+    // read back while the chain phase runs (wg_lf_refs_end)
+    const int rc = wg_fetch_begin(c, {{flags.p, false}, {ev_off.as<uint32_t>() + n, false}, {aux_off.as<uint32_t>() + n, false}});
     wg_stage_end(c);
+    return rc;
+}
+
+int wg_lf_refs_end(wg_ctx *c, uint32_t *viol, uint64_t *nev, uint64_t *naux) {
+    uint64_t hdr[3] = {0, 0, 0};
+    if (const int rc = wg_fetch_end(c, hdr)) return rc;
     *viol = (uint32_t)hdr[0];
     *nev = hdr[1];
     *naux = hdr[2];
@@ -533,11 +537,14 @@ int wg_lanes_fast(wg_ctx *c, bool *used) {
     c->e_refs_own = c->e_refs;
     uint32_t viol = 0;
     uint64_t nev = 0, naux = 0;
-    int rc = wg_lf_refs(c, R, &viol, &nev, &naux);
+    int rc = wg_lf_refs(c, R);
     if (rc != WG_OK) return rc;
+    rc = wg_lf_chain(c, R);                          // queued before the flags are back (bounded on any input)
+    const int rc2 = wg_lf_refs_end(c, &viol, &nev, &naux);
+    if (rc != WG_OK) return rc;
+    if (rc2 != WG_OK) return rc2;
     if (viol) return WG_OK;                          // not well formed: general walk
     c->n_events = nev;
-    if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
     DevBuf &evrec = c->lf[LF_EVREC], &aux = c->lf[LF_AUX];
     WG_ALLOC(c, evrec, (nev + 256) * 16);
     WG_ALLOC(c, aux, naux * 4 + 4);

@@ -780,8 +780,11 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         wg_stage_begin(c, "lanes");
         uint32_t viol = 0;
         uint64_t nev = 0, naux = 0;
-        if ((rc = wg_lf_refs(c, R, &viol, &nev, &naux)) != WG_OK) return rc;
-        if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
+        if ((rc = wg_lf_refs(c, R)) != WG_OK) return rc;
+        rc = wg_lf_chain(c, R);                   // queued before the flags are back
+        const int rc2 = wg_lf_refs_end(c, &viol, &nev, &naux);
+        if (rc != WG_OK) return rc;
+        if (rc2 != WG_OK) return rc2;
         wg_stage_end(c);
         S.nev_own = nev;
         S.naux_own = naux;
