@@ -341,6 +341,40 @@ int wg_copy_glyph_vertices(wg_ctx *ctx, uint64_t first, uint64_t count, wg_text_
 /* per-row first quad (row_end-row_begin+1 entries) */
 int wg_copy_glyph_offsets(wg_ctx *ctx, uint64_t *dst);
 
+/* ---- search-match flags (history_view, commit_graph.rs:1320-1332;
+ * commit_matches_query, :1509-1523) ------------------------
+ * query = the raw search text (UTF-8); the engine lowers it with Rust's
+ * str::to_lowercase semantics (:1326; Unicode tables of wgraph's
+ * WG_UNICODE_VERSION) and flags every row r of [row_begin, row_end) of the
+ * last build's commit list whose lowered summary or author contains it, whose
+ * short id (first 7 hex digits, none for synthetic rows, git/mod.rs:300, 360)
+ * contains it, or whose 40-digit hex id starts with it.  An empty query
+ * matches every row and turns dimming off.  After a non-empty query,
+ * wg_emit_vertices and wg_emit_glyphs draw rows flagged 0 at opacity
+ * WG_DIM_ALPHA (:1467, 1482: row_el.opacity(0.3)): every vertex's alpha is
+ * multiplied by it (rows outside [row_begin, row_end) are not dimmed; the
+ * next layout build clears the flags).
+ * Text fields: CSR bytes + [N+1] u64 offsets of the WHOLE list (host or
+ * device, per residency); a NULL offset array = that field empty on every
+ * row.  match_count (may be NULL) receives the number of flagged rows.     */
+#define WG_DIM_ALPHA 0.3f
+typedef struct wg_row_text {
+    const uint8_t  *summary;      /* CommitInfo::summary bytes, concatenated   */
+    const uint64_t *summary_off;  /* [N+1]                                      */
+    const uint8_t  *author;       /* CommitInfo::author bytes                   */
+    const uint64_t *author_off;   /* [N+1]                                      */
+    int32_t         residency;    /* WG_HOST or WG_DEVICE                       */
+    int32_t         reserved;
+} wg_row_text;
+int wg_match_rows(wg_ctx *ctx, const uint8_t *query, uint64_t query_len, uint64_t row_begin, uint64_t row_end,
+                  const wg_row_text *text, uint64_t *match_count);
+/* flags of the last wg_match_rows: row_end-row_begin bytes (1 = match) */
+int wg_copy_match_flags(wg_ctx *ctx, uint8_t *dst);
+/* str::to_lowercase of a UTF-8 byte string with the engine's tables (host):
+ * writes min(len, cap) bytes to dst (may be NULL) and the full length to
+ * *out_len. */
+int wg_lower_utf8(const uint8_t *src, uint64_t len, uint8_t *dst, uint64_t cap, uint64_t *out_len);
+
 /* ---- timing (HIP events on the context's stream) ------------------------ */
 #define WG_STAGE_MAX 1024
 /* on = 0 disables; on > 0 enables and restarts the stage log (on > 1 also

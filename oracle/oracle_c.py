@@ -110,8 +110,12 @@ class OracleLayout:
             raise MemoryError("wgo_row_geometry failed")
         return _geom_to_dict(self._g)
 
-    def emit_vertices(self, row_begin, row_end, selected=-1, palette=None, use_build_geometry=False):
-        """Vertices of rows [row_begin,row_end) from the last row_geometry()."""
+    def emit_vertices(self, row_begin, row_end, selected=-1, palette=None, use_build_geometry=False,
+                      match=None, match_rb=0):
+        """Vertices of rows [row_begin,row_end) from the last row_geometry().
+        match: search-match flags of rows [match_rb, match_rb + len(match)):
+        rows flagged 0 are drawn at opacity 0.3 (history_view,
+        commit_graph.rs:1467, 1482: every vertex alpha * 0.3f)."""
         pal = np.ascontiguousarray(abi.DEFAULT_PALETTE if palette is None else palette, np.float32)
         g = self._L.geom if (use_build_geometry or self._g is None) else self._g
         pv, po, pn = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
@@ -124,6 +128,8 @@ class OracleLayout:
         off = _arr(po.value, np.uint64, row_end - row_begin + 1)
         lib().wgo_free(pv.value)
         lib().wgo_free(po.value)
+        if match is not None:
+            dim_rows(v, off, row_begin, match, match_rb, "a")
         return v, off
 
     def close(self):
@@ -139,6 +145,20 @@ class OracleLayout:
             self.close()
         except Exception:
             pass
+
+
+def dim_rows(v, off, row_begin, match, match_rb, alpha_field):
+    """Search dimming: alpha *= 0.3f (f32) on the vertices of rows whose flag is 0."""
+    rows = len(off) - 1
+    for j in range(rows):
+        r = row_begin + j
+        k = r - match_rb
+        if 0 <= k < len(match) and not match[k]:
+            seg = v[int(off[j]):int(off[j + 1])]
+            if alpha_field is None:        # plain f32 [n, 8] TextVertex arrays: alpha = column 7
+                seg[:, 7] = seg[:, 7] * np.float32(0.3)
+            else:
+                seg[alpha_field] = seg[alpha_field] * np.float32(0.3)
 
 
 def vertex_checksum(v: np.ndarray) -> int:

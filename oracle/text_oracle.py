@@ -39,8 +39,11 @@ def short_id(oid_row: np.ndarray) -> bytes:
     return bytes(oid_row[:4]).hex()[:7].encode()
 
 
-def emit_glyphs(dag, node_y, glyphs, atlas_w, atlas_h, spread, em_px, rb, re, summaries=None, **params):
-    """-> (TextVertex f32 array (6 per quad, 8 floats each), per-row quad offsets)."""
+def emit_glyphs(dag, node_y, glyphs, atlas_w, atlas_h, spread, em_px, rb, re, summaries=None, match=None, match_rb=0,
+                **params):
+    """-> (TextVertex f32 array (6 per quad, 8 floats each), per-row quad offsets).
+    match: search-match flags of rows [match_rb, ...): rows flagged 0 at
+    opacity 0.3 (commit_graph.rs:1467, 1482; alpha * 0.3f)."""
     from wgraph import abi
     p = dict(abi.TEXT_DEFAULTS, **params)
     first = int(glyphs[0]["codepoint"])
@@ -93,4 +96,8 @@ def emit_glyphs(dag, node_y, glyphs, atlas_w, atlas_h, spread, em_px, rb, re, su
                                           (x1, y0, u1, v0), (x1, y1, u1, v1), (x0, y1, u0, v1))):
             out[i * 6 + k, :4] = (x, y, u, v)
             out[i * 6 + k, 4:] = col[rid]
-    return out, np.array(offs, np.uint64)
+    offs = np.array(offs, np.uint64)
+    if match is not None:
+        from oracle.oracle_c import dim_rows
+        dim_rows(out, offs * 6, rb, match, match_rb, None)
+    return out, offs

@@ -1,0 +1,121 @@
+"""GPU search-match flags (commit_matches_query, commit_graph.rs:1509-1523;
+history_view :1320-1332) against the oracle, bit for bit, through the C ABI:
+ASCII and Unicode queries (final sigma, dotted I, Kelvin sign, titlecase
+digraphs), short-id / id-prefix queries, synthetic rows, queries longer than
+the LDS copy, rows too wide to stage, host and device text, row ranges —
+and the search dimming of vertex and glyph emission (:1467, 1482)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_DIR
+from oracle import search_oracle as so
+from wgraph import abi, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def data():
+    d = synth.generate("anomaly", 6000, seed=5)        # synthetic and orphan rows, duplicate ids
+    summ, auth = synth.text_fields(d.n, seed=2)
+    return d, summ, auth
+
+
+def _queries(d):
+    hexid = d.oid[123].tobytes().hex()
+    return ["fix", "FIX", "Graph L", "ΣΟΦΙΑ", "σοφια", "όδος", "ας.", "ς", "σ", "İstanbul", "i̇", "STRASSE", "straße",
+            "ǆ", "ǅemal", "K", "k", "ångström", "日本", "🚀", "dmitry", "дмитрий", " ", "a", "aab", "e e",
+            hexid[:4], hexid[:7], hexid[2:6], hexid[:12], hexid, hexid + "0", "ʼn", "\xc3".encode("latin-1"),
+            "x" * 3000, "remove " * 400]
+
+
+@pytest.mark.parametrize("residency", ["host", "device"])
+def test_match_flags_equal_oracle(engine, data, residency):
+    import torch
+    d, summ, auth = data
+    engine.build(d)
+    dev = None
+    if residency == "device":
+        t = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (summ[0], summ[1].view(np.int64),
+                                                                          auth[0], auth[1].view(np.int64))]
+        dev = ((t[0].data_ptr(), t[1].data_ptr()), (t[2].data_ptr(), t[3].data_ptr()))
+    try:
+        for q in _queries(d):
+            qb = q if isinstance(q, bytes) else q.encode()
+            for rb, re_ in ((0, d.n), (777, 4321)):
+                if dev is not None:
+                    n = engine.match_rows(qb, rb, re_, device=dev)
+                else:
+                    n = engine.match_rows(qb, rb, re_, summaries=summ, authors=auth)
+                want, wn = so.match_rows(d, qb, summ, auth, rb, re_)
+                got = engine.match_flags()
+                assert n == wn, (q, rb)
+                assert (got == want).all(), (q, rb, np.flatnonzero(got != want)[:5])
+    finally:
+        engine.match_rows("")
+
+
+def test_match_without_text_fields_and_wide_rows(engine):
+    d = synth.generate("random13", 3000, seed=9)
+    engine.build(d)
+    # rows whose summaries are far too long for the 24 KiB LDS stage (read from HBM instead)
+    rng = np.random.default_rng(1)
+    lens = rng.integers(0, 400, d.n)
+    lens[100:400] = 5000
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    words = np.frombuffer(b"abc Abd aBe ABF \xce\xa3\xce\x91\xce\xa3 ", np.uint8)
+    body = np.resize(words, int(off[-1]))
+    try:
+        for q in ("abf", "σας", "σασ", "ab", d.oid[5].tobytes().hex()[:9]):
+            n = engine.match_rows(q, summaries=(body, off))
+            want, wn = so.match_rows(d, q.encode(), (body, off), None)
+            assert n == wn and (engine.match_flags() == want).all(), q
+        n = engine.match_rows(d.oid[7].tobytes().hex()[:5])          # id fields only
+        want, wn = so.match_rows(d, d.oid[7].tobytes().hex()[:5].encode())
+        assert n == wn and (engine.match_flags() == want).all()
+    finally:
+        engine.match_rows("")
+
+
+def test_empty_query_matches_all_and_build_clears(engine, data):
+    d, summ, auth = data
+    engine.build(d)
+    assert engine.match_rows("", summaries=summ, authors=auth) == d.n
+    assert engine.match_flags().all()
+
+
+def test_search_dimming_of_vertices_and_glyphs(engine, data):
+    from oracle import oracle_c, text_oracle
+    d, summ, auth = data
+    engine.build(d)
+    engine.row_geometry(d.band)
+    o = oracle_c.OracleLayout(d)
+    og = o.row_geometry(d.band)
+    try:
+        engine.match_rows("fix", 1000, 5000, summaries=summ, authors=auth)
+        flags = engine.match_flags()
+        assert 0 < flags.sum() < len(flags)
+        engine.emit_vertices(500, 5500, selected=1003)
+        want, _ = o.emit_vertices(500, 5500, selected=1003, match=flags, match_rb=1000)
+        assert engine.vertex_summary().checksum == oracle_c.vertex_checksum(want)
+        got = engine.vertices()
+        assert got.tobytes() == want.tobytes()
+        # glyph quads of the same rows
+        z = np.load(os.path.join(GOLDEN_DIR, "font_regular.npz"), allow_pickle=False)
+        p = abi.ATLAS_DEFAULTS
+        engine.build_font_atlas(0)
+        kw = dict(now=int(d.time.max()) + 86400)
+        engine.emit_glyphs(900, 1200, summaries=summ, **kw)
+        tv, _ = text_oracle.emit_glyphs(d, og["node_y"], z["glyphs"], p["width"], p["height"], p["spread"], p["em_px"],
+                                        900, 1200, summaries=summ, match=flags, match_rb=1000, **kw)
+        assert engine.glyph_vertices().view(np.float32).reshape(-1, 8).tobytes() == tv.tobytes()
+        # empty query: no dimming
+        engine.match_rows("")
+        engine.emit_vertices(500, 5500, selected=1003)
+        plain, _ = o.emit_vertices(500, 5500, selected=1003)
+        assert engine.vertex_summary().checksum == oracle_c.vertex_checksum(plain)
+    finally:
+        engine.match_rows("")
+        o.close()

@@ -250,6 +250,7 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     c->have_layout = c->have_geom = c->have_vtx = c->have_text = false;
     c->lists_gen = ~0ull;
     c->sh.on = false;
+    c->match_on = false;   // match flags belong to the previous commit list
     c->sh.step = 0;
     c->edge_y = nullptr;
     const uint64_t n = in->n_commits;
@@ -494,9 +495,12 @@ int wg_emit_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel, const flo
                        (unsigned long long)re, (unsigned long long)S.s, (unsigned long long)S.e);
     (void)hipSetDevice(c->device);
     c->have_vtx = false;
-    WG_ALLOC(c, c->palette, WG_PALETTE_SIZE * 4 * sizeof(float));
-    if (!c->palette_valid || std::memcmp(c->palette_host, palette, sizeof(c->palette_host)) != 0) {   // upload on change only
-        std::memcpy(c->palette_host, palette, sizeof(c->palette_host));
+    WG_ALLOC(c, c->palette, 2 * WG_PALETTE_SIZE * 4 * sizeof(float));
+    if (!c->palette_valid || std::memcmp(c->palette_host, palette, WG_PALETTE_SIZE * 4 * sizeof(float)) != 0) {   // upload on change only
+        // entries 8..15: the same colours at opacity WG_DIM_ALPHA (search dimming)
+        std::memcpy(c->palette_host, palette, WG_PALETTE_SIZE * 4 * sizeof(float));
+        for (int i = 0; i < 4 * WG_PALETTE_SIZE; i++)
+            c->palette_host[4 * WG_PALETTE_SIZE + i] = (i & 3) == 3 ? palette[i] * WG_DIM_ALPHA : palette[i];
         WG_HIP(c, hipMemcpyAsync(c->palette.p, c->palette_host, sizeof(c->palette_host), hipMemcpyHostToDevice, c->stream));
         WG_HIP(c, hipStreamSynchronize(c->stream));   // palette_host may change before the copy ran
         c->palette_valid = true;

@@ -203,8 +203,8 @@ struct wg_ctx {
     int64_t  selected = -1;
     DevBuf vtx_off;         // uint64 [rows+1]
     DevBuf vtx;             // wg_vertex [n_vtx]
-    DevBuf palette;         // float [32]
-    float   palette_host[WG_PALETTE_SIZE * 4];   // last uploaded palette
+    DevBuf palette;         // float [64]: palette, then the same at WG_DIM_ALPHA
+    float   palette_host[2 * WG_PALETTE_SIZE * 4];   // last uploaded palette (+ dimmed)
     bool    palette_valid = false;
     DevBuf chk;             // uint64 [1]
     DevBuf tile_first;      // uint4 [tiles+1] per-tile record (first row, first vertical, first curve, straddles)
@@ -216,6 +216,14 @@ struct wg_ctx {
     bool     have_text = false;
     uint64_t text_rb = 0, text_re = 0, n_quads = 0;
     DevBuf text_sum, text_sum_off, text_off, text_rec, text_vtx;
+    // ---- search-match flags (wg_search.hip) -------------------------------------------
+    bool     match_on = false;      // a non-empty query is active: emission dims non-matching rows
+    uint64_t match_rb = 0, match_re = 0, match_count = 0;
+    DevBuf   match_flags;           // uint8 [match_re - match_rb]
+    DevBuf   match_q;               // {count u64, pad} + fail u16[m] + q u8[m]
+    DevBuf   match_txt[2], match_off[2];   // device copies of host summary / author text
+    std::vector<uint64_t> match_rel[2];
+    std::vector<uint8_t>  match_qhost;
     // ---- timing ----------------------------------------------------------------------
     bool       timing = false;
     StageTimer stages[WG_STAGE_MAX];

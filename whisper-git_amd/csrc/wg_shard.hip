@@ -622,6 +622,7 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     c->lists_gen = ~0ull;
     c->edge_y = nullptr;
     c->d_oid = in->oid;
+    c->match_on = false;   // match flags belong to the previous commit list
     c->d_time = in->time;
     c->d_poff = in->parent_off;
     c->d_poid = in->parent_oid;

@@ -41,6 +41,8 @@ struct TextArgs {
     float scale;                     // text_px / em_px
     float sha_x, summary_x, summary_max_x, time_right_x, baseline_dy;
     int64_t now;
+    const uint8_t *match;            // search-match flags of global rows [mrb, mre), or null (no dimming)
+    uint64_t mrb, mre;
 };
 
 // format_relative_time (git/mod.rs:34-49) into buf, returns the length
@@ -126,9 +128,11 @@ __global__ void k_text_rows(TextArgs A, uint64_t *__restrict__ cnt, const uint64
     const float tx = A.time_right_x - run_width(A, reinterpret_cast<const uint8_t *>(tb), nt);
     uint4 *out = WRITE ? rec : nullptr;
     uint32_t o = WRITE ? (uint32_t)(off[j]) : 0u;
-    uint32_t n = run(A, sha, nsha, A.sha_x, 3.0e38f, base, 0, out, o);
-    n += run(A, sum, nsum, A.summary_x, A.summary_max_x, base, 1, out, o + n);
-    n += run(A, reinterpret_cast<const uint8_t *>(tb), nt, tx, 3.0e38f, base, 2, out, o + n);
+    // search dimming (commit_graph.rs:1467, 1482): colours 3..5 = the run colours at WG_DIM_ALPHA
+    const uint32_t d = (A.match && r >= A.mrb && r < A.mre && !A.match[r - A.mrb]) ? 3u : 0u;
+    uint32_t n = run(A, sha, nsha, A.sha_x, 3.0e38f, base, 0 + d, out, o);
+    n += run(A, sum, nsum, A.summary_x, A.summary_max_x, base, 1 + d, out, o + n);
+    n += run(A, reinterpret_cast<const uint8_t *>(tb), nt, tx, 3.0e38f, base, 2 + d, out, o + n);
     if (!WRITE) cnt[j] = n;
 }
 
@@ -137,7 +141,7 @@ struct QuadArgs {
     const uint4 *rec;
     const wg_glyph *glyphs;
     float scale, spread, inv_w, inv_h;
-    float4 color[3];
+    float4 color[6];                 // run colours, then the same at WG_DIM_ALPHA
 };
 
 constexpr int QT = 256;
@@ -242,6 +246,9 @@ int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, 
     A.time_right_x = p->time_right_x;
     A.baseline_dy = p->baseline_dy;
     A.now = p->now;
+    A.match = c->match_on ? c->match_flags.as<const uint8_t>() : nullptr;
+    A.mrb = c->match_rb;
+    A.mre = c->match_re;
     if ('?' < F.first_char || '?' - F.first_char >= F.glyphs.size())
         return wg_fail(c, WG_E_UNSUPPORTED, "atlas lacks '?' (the substitute glyph)");
     WG_ALLOC(c, c->text_off, (rows + 2) * 8);
@@ -280,6 +287,7 @@ int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, 
         for (int k = 0; k < 3; k++) {
             const float *col = k == 0 ? p->color_sha : (k == 1 ? p->color_summary : p->color_time);
             Q.color[k] = make_float4(col[0], col[1], col[2], col[3]);
+            Q.color[k + 3] = make_float4(col[0], col[1], col[2], col[3] * WG_DIM_ALPHA);
         }
         hipLaunchKernelGGL(k_text_quads, dim3((uint32_t)((nq + QT - 1) / QT)), dim3(QT), 0, s, Q, c->text_vtx.as<float4>());
         WG_HIP(c, hipGetLastError());

@@ -106,6 +106,7 @@ struct RowInfo {
     uint32_t voff, nv, coff, nc;
     float    h, ny, cx;
     uint32_t ncol;
+    uint32_t dim;   // 0, or 8 for a row dimmed by the search (palette entries 8..15)
 };
 
 __device__ __forceinline__ float lane_x(uint32_t lane, uint32_t vis) {   // lane_center_x (:786-790)
@@ -123,7 +124,8 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         const uint32_t *__restrict__ coff, const wg_curve *__restrict__ curve, const uint8_t *__restrict__ curve_color,
         const float *__restrict__ height, const float *__restrict__ node_y, const uint32_t *__restrict__ lane_out,
         const uint8_t *__restrict__ color_out, const float4 *__restrict__ palette,
-        const uint4 *__restrict__ tinfo, float4 *__restrict__ out) {
+        const uint4 *__restrict__ tinfo, const uint8_t *__restrict__ match, int64_t mlo, int64_t mhi,
+        float4 *__restrict__ out) {
     __shared__ RowInfo rows[MAXR];
     __shared__ uint8_t pair_row[PAIRS];            // row (within the tile) of every vertex pair
     __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
@@ -131,7 +133,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     __shared__ uint32_t vents[MAXV];               // the tile's vertical entries
     __shared__ __attribute__((aligned(16))) float4 stage[VT / 64][64 * 3];
     __shared__ uint32_t wmax[VT / 64];
-    __shared__ float4 pal[WG_PALETTE_SIZE];
+    __shared__ float4 pal[2 * WG_PALETTE_SIZE];    // palette, then the same at WG_DIM_ALPHA
     __shared__ float2 circ[3][WG_TESS_NODE_SEGMENTS + 2];   // r*(cos, sin) for node, ring inner, ring outer radius
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t v0 = (uint64_t)blockIdx.x * TILE;
@@ -149,7 +151,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     const uint64_t v1 = (v0 + TILE < total) ? v0 + TILE : total;
     const uint64_t nrows = re - rb;
     const float visf = (float)(vis - 1);
-    if (tid < WG_PALETTE_SIZE) pal[tid] = palette[tid];
+    if (tid < 2 * WG_PALETTE_SIZE) pal[tid] = palette[tid];
     for (uint32_t p = tid; p < PAIRS; p += VT) pair_row[p] = 0;
     const uint4 ti = tinfo[blockIdx.x], tn = tinfo[blockIdx.x + 1];
     const uint64_t first = ti.x;
@@ -172,6 +174,9 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         ri.ny = node_y[r];
         ri.cx = lane_x(lane_out[r], vis);
         ri.ncol = color_out[r];
+        // search dimming (history_view, commit_graph.rs:1467, 1482): rows of the
+        // match range whose flag is 0 take the dimmed palette
+        ri.dim = (match && (int64_t)r >= mlo && (int64_t)r < mhi && !match[(int64_t)r - mlo]) ? 8u : 0u;
         if (lane < (uint32_t)MAXR && j0 < nrows && ri.vstart < v1) {
             rows[lane] = ri;
             const uint32_t sp = ri.vstart > v0 ? (uint32_t)((ri.vstart - v0) >> 1) : 0u;
@@ -279,7 +284,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
                 xb = ri.cx + ob.x; yb = ri.ny + ob.y;
                 col = WG_COLOR_FOREGROUND;
             }
-            const float4 c4 = pal[col & 7u];
+            const float4 c4 = pal[(col & 7u) | ri.dim];
             st[lane * 3 + 0] = make_float4(xa, ya, c4.x, c4.y);
             st[lane * 3 + 1] = make_float4(c4.z, c4.w, xb, yb);
             st[lane * 3 + 2] = c4;
@@ -341,6 +346,10 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     // fit the last frame's capacity; the kernels exit past the total and
     // write nothing when it does not fit), and relaunched only if needed.
     if (const int rc = wg_fetch_begin(c, {{off + rows, true}})) return rc;
+    // search-match flags of global rows [match_rb, match_re) -> context rows [mlo, mhi)
+    const uint8_t *match = c->match_on ? c->match_flags.as<const uint8_t>() : nullptr;
+    const int64_t mlo = (int64_t)c->match_rb - (int64_t)c->sh.s + (int64_t)c->sh.row_base;
+    const int64_t mhi = mlo + (int64_t)(c->match_re - c->match_rb);
     auto launch = [&](uint64_t vcap, uint64_t tcap, uint64_t grid) {
         hipLaunchKernelGGL(k_tile_info, dim3((rows + 255) / 256), dim3(256), 0, s, rb, rows, (const uint64_t *)off,
                            c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), tcap,
@@ -351,7 +360,8 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
                            c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
                            c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
                            c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
-                           c->palette.as<const float4>(), c->tile_first.as<const uint4>(), c->vtx.as<float4>());
+                           c->palette.as<const float4>(), c->tile_first.as<const uint4>(), match, mlo, mhi,
+                           c->vtx.as<float4>());
         wg_stage_end(c);
     };
     const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;

@@ -76,6 +76,10 @@ def lib():
                                       ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_geometry_begin": ([vp, vp, i32, ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_copy_msg": ([vp, vp], ctypes.c_int),
+            "wg_match_rows": ([vp, vp, u64, u64, u64, ctypes.POINTER(abi.RowText), ctypes.POINTER(ctypes.c_uint64)],
+                              ctypes.c_int),
+            "wg_copy_match_flags": ([vp, vp], ctypes.c_int),
+            "wg_lower_utf8": ([vp, u64, vp, u64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "wg_shard_exchange": ([vp, vp, u64, ctypes.POINTER(ctypes.c_uint64), vp, ctypes.POINTER(abi.ShardMsg)],
                                   ctypes.c_int),
         }
@@ -94,7 +98,22 @@ EXPORTED_SYMBOLS = (
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
     "wg_shard_copy_msg", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
-    "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets")
+    "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets",
+    "wg_match_rows", "wg_copy_match_flags", "wg_lower_utf8")
+
+
+def to_lowercase(b: bytes) -> bytes:
+    """Rust str::to_lowercase of UTF-8 bytes with the engine's own tables (host)."""
+    b = bytes(b)
+    src = np.frombuffer(b, np.uint8) if b else np.zeros(1, np.uint8)
+    n = ctypes.c_uint64()
+    rc = lib().wg_lower_utf8(src.ctypes.data, len(b), None, 0, ctypes.byref(n))
+    if rc != abi.WG_OK:
+        raise WgError(rc, "wg_lower_utf8")
+    out = np.empty(max(1, n.value), np.uint8)
+    lib().wg_lower_utf8(src.ctypes.data, len(b), out.ctypes.data, n.value, ctypes.byref(n))
+    return out[:n.value].tobytes()
+
 
 FONT_DIR = os.path.join(os.path.dirname(_HERE), "fonts")
 FONTS = {0: os.path.join(FONT_DIR, "Roboto-Regular.ttf"), 1: os.path.join(FONT_DIR, "Roboto-Bold.ttf")}
@@ -313,6 +332,48 @@ class Engine:
             self._text_keep = (b, o)
             self._check(lib().wg_emit_glyphs(self._ctx, row_begin, row_end, b.ctypes.data if b.size else o.ctypes.data,
                                              o.ctypes.data, abi.WG_HOST, ctypes.byref(p)))
+
+    # -- search-match flags (commit_matches_query, commit_graph.rs:1509-1523) -------------
+    def match_rows(self, query, row_begin=0, row_end=None, summaries=None, authors=None, device=None) -> int:
+        """history_view's match flags (:1320-1332) for rows [row_begin, row_end)
+        of the built list; returns the match count.  summaries / authors:
+        (bytes uint8, offsets uint64 [N+1]) host arrays, or device=((sum_ptr,
+        sum_off_ptr), (auth_ptr, auth_off_ptr)) device pointers (None: empty).
+        Later emissions dim the rows that do not match (empty query: none)."""
+        if row_end is None:
+            row_end = self._n_list()
+        q = query.encode() if isinstance(query, str) else bytes(query)
+        t = abi.RowText()
+        keep = []
+        if device is not None:
+            t.residency = abi.WG_DEVICE
+            (t.summary, t.summary_off), (t.author, t.author_off) = [(None, None) if f is None else f for f in device]
+        else:
+            t.residency = abi.WG_HOST
+            for f, (bn, on) in ((summaries, ("summary", "summary_off")), (authors, ("author", "author_off"))):
+                if f is None:
+                    continue
+                b = np.ascontiguousarray(f[0], np.uint8)
+                o = np.ascontiguousarray(f[1], np.uint64)
+                keep += [b, o]
+                setattr(t, bn, b.ctypes.data if b.size else o.ctypes.data)
+                setattr(t, on, o.ctypes.data)
+        self._match_keep = keep
+        qa = np.frombuffer(q, np.uint8) if q else np.zeros(1, np.uint8)
+        cnt = ctypes.c_uint64()
+        self._check(lib().wg_match_rows(self._ctx, qa.ctypes.data, len(q), row_begin, row_end, ctypes.byref(t),
+                                        ctypes.byref(cnt)))
+        self._match_rows = row_end - row_begin
+        return int(cnt.value)
+
+    def match_flags(self) -> np.ndarray:
+        out = np.empty(getattr(self, "_match_rows", 0), np.uint8)
+        self._check(lib().wg_copy_match_flags(self._ctx, out.ctypes.data if out.size else None))
+        return out
+
+    def _n_list(self) -> int:
+        c = getattr(self, "_commits", None)
+        return int(c.n_commits) if c is not None else self.layout_summary().n_rows
 
     def glyph_summary(self) -> abi.GlyphSummary:
         s = abi.GlyphSummary()

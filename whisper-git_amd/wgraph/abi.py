@@ -86,6 +86,14 @@ def text_params(**kw) -> TextParams:
     return p
 
 
+class RowText(ctypes.Structure):
+    _fields_ = [("summary", ctypes.c_void_p), ("summary_off", ctypes.c_void_p), ("author", ctypes.c_void_p),
+                ("author_off", ctypes.c_void_p), ("residency", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+WG_DIM_ALPHA = 0.3
+
+
 class ShardMsg(ctypes.Structure):
     _fields_ = [("send", ctypes.c_void_p), ("bytes", ctypes.c_uint64), ("done", ctypes.c_int32),
                 ("step", ctypes.c_int32)]

@@ -156,3 +156,58 @@ def summaries(n: int, seed: int = 0, mean_words: float = 6.0, p_empty: float = 0
     odd = rng.random(out.size) < 0.01
     out[odd & (out != ord(" "))] = 0xC3
     return out, off
+
+
+# Non-ASCII words for the search fields: Latin-1 / Extended-A letters, Greek
+# with final-sigma contexts, Turkish dotted I, Kelvin / capital sharp s,
+# titlecase digraphs, Cyrillic, CJK, an emoji, combining marks.
+_UNI_WORDS = [w.encode() for w in (
+    "Naïve", "FAÇADE", "Ørjan", "Ødegård", "ŁUKASZ", "Żółć", "Grüße", "STRAẞE", "İstanbul", "İİ", "ΣΟΦΙΑ", "ΌΔΟΣ",
+    "Σ", "ΑΣ.", "ΑΣ'Σ", "ΣΑΣ:ΣΑ", "Οδυσσεύς", "ΦΩΣ", "ǅemal", "ǈubljana", "ᾼ", "Kelvin", "Ångström", "ДМИТРИЙ",
+    "Москва", "日本語", "🚀", "éclair", "ΆͅΣ", "ΣΣ", "ⅫΣ")]
+_NAMES = [w.encode() for w in (
+    "Linus Torvalds", "Greg Kroah-Hartman", "José García", "Łukasz Nowak", "Ørjan Ødegård", "Σωκράτης ΠΑΠΑΔΟΠΟΥΛΟΣ",
+    "İlker Yılmaz", "Дмитрий Иванов", "山田 太郎", "Zoë Ångström", "ǅemal Ǉubić", "dependabot[bot]", "Unknown",
+    "ANNA-LENA MÜLLER", "Chloé Dubois", "Anders Ösäter")]
+
+
+def _join_words(rng, n, vocab, counts, sep=b" "):
+    """Rows of `counts[i]` words drawn from vocab joined by sep: (bytes, offsets)."""
+    vb = np.frombuffer(b"".join(vocab), np.uint8)
+    vlen = np.array([len(w) for w in vocab], np.int64)
+    vstart = np.concatenate([[0], np.cumsum(vlen)[:-1]])
+    ids = rng.integers(0, len(vocab), int(counts.sum()))
+    wl = vlen[ids]
+    row_of = np.repeat(np.arange(n), counts)
+    row_bytes = np.zeros(n, np.int64)
+    np.add.at(row_bytes, row_of, wl + len(sep))
+    row_bytes = np.maximum(row_bytes - len(sep) * (counts > 0), 0)
+    off = np.concatenate([[0], np.cumsum(row_bytes)]).astype(np.uint64)
+    out = np.empty(int(off[-1]), np.uint8)
+    if out.size:
+        # word k of row i starts at off[i] + (sum of the earlier words of row i + separators)
+        first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        cum = np.cumsum(wl + len(sep)) - (wl + len(sep))
+        start = off[row_of].astype(np.int64) + cum - np.repeat(cum[first[counts > 0]], counts[counts > 0])
+        seps = start[np.concatenate([np.diff(row_of) == 0, [False]])] + wl[np.concatenate([np.diff(row_of) == 0, [False]])]
+        for k, b in enumerate(sep):
+            out[seps + k] = b
+        tot = int(wl.sum())
+        inner = np.arange(tot) - np.repeat(np.cumsum(wl) - wl, wl)
+        out[np.repeat(start, wl) + inner] = vb[np.repeat(vstart[ids], wl) + inner]
+    return out, off
+
+
+def text_fields(n: int, seed: int = 0, p_unicode: float = 0.15):
+    """Search fields for n rows (commit_matches_query, commit_graph.rs:1509-1523):
+    summaries (ASCII words with ~p_unicode non-ASCII words, ~2% empty) and
+    authors (a name pool with non-ASCII names), each as (bytes, offsets[n+1])."""
+    rng = np.random.default_rng(0x5EA4C + seed)
+    counts = rng.poisson(6.0, n).clip(1, 14)
+    counts[rng.random(n) < 0.02] = 0
+    ascii_words = [w.capitalize() if i % 7 == 0 else w for i, w in enumerate(_WORDS)]
+    n_uni = max(1, int(round(len(ascii_words) * p_unicode / (1 - p_unicode))))
+    vocab = ascii_words + [_UNI_WORDS[i % len(_UNI_WORDS)] for i in range(n_uni)]
+    summ = _join_words(rng, n, vocab, counts)
+    auth = _join_words(rng, n, _NAMES, np.ones(n, np.int64))
+    return summ, auth
