@@ -138,6 +138,61 @@ def extra_measurements(eng, dag, dev, torch, r0, r1, args, log):
                           "text_quads_ms": round(quad_ms, 4),
                           "text_quads_GBps": round(gs.n_quads * (192 + 16) / (quad_ms * 1e-3) / 1e9, 1),
                           "data": "synthetic summaries (wgraph.synth.summaries), relative times vs max(time)+1d"}
+    # search-match flags (commit_matches_query, commit_graph.rs:1509-1523) over the same rows
+    (sb, so_), (ab, ao) = synth.text_fields(dag.n)
+    dt_ = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (sb, so_.view(np.int64), ab, ao.view(np.int64))]
+    devp = ((dt_[0].data_ptr(), dt_[1].data_ptr()), (dt_[2].data_ptr(), dt_[3].data_ptr()))
+    query = "Fix"
+    eng.match_rows(query, r0, r1, device=devp)
+    torch.cuda.synchronize()
+    eng.enable_timing(True, reserve=64 * 2)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        nm = eng.match_rows(query, r0, r1, device=devp)
+    dt = (time.perf_counter() - t0) / args.steps
+    ev = [ms for name, ms in eng.timings() if name == "match"]
+    eng.enable_timing(False)
+    eng.match_rows("")
+    kms = float(np.mean(ev)) if ev else float("nan")
+    text_bytes = int(so_[r1] - so_[r0]) + int(ao[r1] - ao[r0])
+    alg = text_bytes + 16 * (r1 - r0) + (r1 - r0) * (20 + 1 + 1)   # text + offsets + id + flags + flag out
+    srch = {"rows": int(r1 - r0), "query": query, "matches": int(nm), "ms_per_call": round(dt * 1e3, 4),
+            "kernel_ms": round(kms, 4), "kernel_GBps": round(alg / (kms * 1e-3) / 1e9, 1),
+            "algorithmic_bytes": alg, "data": "synthetic summaries + authors (wgraph.synth.text_fields), ~15% non-ASCII words"}
+    if not args.no_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import search_oracle   # baseline only
+        m = min(100_000, r1 - r0)
+        t0 = time.perf_counter()
+        search_oracle.match_rows(dag, query.encode(), (sb, so_), (ab, ao), r0, r0 + m)
+        srch["cpu_rows_per_s"] = round(m / (time.perf_counter() - t0), 1)
+        srch["cpu_kind"] = f"port (Python str.lower restatement, 1 thread, first {m} rows)"
+    out["search"] = srch
+    # row order (commit_graph_with_orphans + insert_synthetics_sorted) of the same list
+    rng = np.random.default_rng(11)
+    orph = np.sort(rng.choice(dag.time, 100))[::-1].copy()
+    syn = rng.choice(dag.time, 4)
+    t_w, t_o, t_s = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (dag.time, orph, syn))
+    perm_d = torch.empty(dag.n + 104, dtype=torch.int32, device=dev)
+    devo = ((t_w.data_ptr(), dag.n), (t_o.data_ptr(), 100), (t_s.data_ptr(), 4))
+    eng.order_rows(None, device=devo, out_device_ptr=perm_d.data_ptr())
+    eng.enable_timing(True, reserve=64 * 2)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.order_rows(None, device=devo, out_device_ptr=perm_d.data_ptr())
+    dt = (time.perf_counter() - t0) / args.steps
+    ev = [ms for name, ms in eng.timings() if name == "order"]
+    eng.enable_timing(False)
+    order = {"rows": int(dag.n + 104), "orphans": 100, "synthetics": 4, "ms_per_call": round(dt * 1e3, 4),
+             "gpu_ms": round(float(np.mean(ev)), 4) if ev else None}
+    if not args.no_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import order_oracle   # baseline only
+        t0 = time.perf_counter()
+        order_oracle.order_rows(dag.time, orph, syn)
+        order["cpu_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        order["cpu_kind"] = "port (Python stable sort + list inserts, 1 thread)"
+    out["order"] = order
     log("extras:", json.dumps(out))
     return out
 

@@ -341,6 +341,21 @@ int wg_copy_glyph_vertices(wg_ctx *ctx, uint64_t first, uint64_t count, wg_text_
 /* per-row first quad (row_end-row_begin+1 entries) */
 int wg_copy_glyph_offsets(wg_ctx *ctx, uint64_t *dst);
 
+/* ---- row order of the commit list -------------------
+ * The order GraphLayout::build receives (repo_tab.rs:607-611, 975-980):
+ * commit_graph_with_orphans (git/mod.rs:761-775) appends the reflog orphans
+ * to the revwalk list and, when there are any, re-sorts everything by time,
+ * newest first, with a stable sort; insert_synthetics_sorted (git/mod.rs:
+ * 234-242) then inserts each synthetic row, in order, before the first row
+ * whose time <= its time (or at the end).  perm[final row] = source row,
+ * sources numbered walk rows [0, n_walk), orphans [n_walk, n_walk +
+ * n_orphans), synthetics after them.  Times in host or device memory
+ * (residency); perm (n_walk + n_orphans + n_syn entries) written to host or
+ * device memory (out_residency).  n_syn <= 4096.                          */
+int wg_order_rows(wg_ctx *ctx, const int64_t *walk_time, uint64_t n_walk, const int64_t *orphan_time,
+                  uint64_t n_orphans, const int64_t *syn_time, uint64_t n_syn, int32_t residency,
+                  uint32_t *perm, int32_t out_residency);
+
 /* ---- search-match flags (history_view, commit_graph.rs:1320-1332;
  * commit_matches_query, :1509-1523) ------------------------
  * query = the raw search text (UTF-8); the engine lowers it with Rust's

@@ -224,6 +224,10 @@ struct wg_ctx {
     DevBuf   match_txt[2], match_off[2];   // device copies of host summary / author text
     std::vector<uint64_t> match_rel[2];
     std::vector<uint8_t>  match_qhost;
+    // ---- row order (wg_order.hip) ------------------------------------------------------
+    DevBuf   ord[8];
+    std::vector<uint32_t> ord_host;
+    uint64_t ord_n = 0;
     // ---- timing ----------------------------------------------------------------------
     bool       timing = false;
     StageTimer stages[WG_STAGE_MAX];

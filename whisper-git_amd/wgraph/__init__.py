@@ -79,6 +79,7 @@ def lib():
             "wg_match_rows": ([vp, vp, u64, u64, u64, ctypes.POINTER(abi.RowText), ctypes.POINTER(ctypes.c_uint64)],
                               ctypes.c_int),
             "wg_copy_match_flags": ([vp, vp], ctypes.c_int),
+            "wg_order_rows": ([vp, vp, u64, vp, u64, vp, u64, i32, vp, i32], ctypes.c_int),
             "wg_lower_utf8": ([vp, u64, vp, u64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "wg_shard_exchange": ([vp, vp, u64, ctypes.POINTER(ctypes.c_uint64), vp, ctypes.POINTER(abi.ShardMsg)],
                                   ctypes.c_int),
@@ -99,7 +100,7 @@ EXPORTED_SYMBOLS = (
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
     "wg_shard_copy_msg", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
     "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets",
-    "wg_match_rows", "wg_copy_match_flags", "wg_lower_utf8")
+    "wg_match_rows", "wg_copy_match_flags", "wg_lower_utf8", "wg_order_rows")
 
 
 def to_lowercase(b: bytes) -> bytes:
@@ -332,6 +333,27 @@ class Engine:
             self._text_keep = (b, o)
             self._check(lib().wg_emit_glyphs(self._ctx, row_begin, row_end, b.ctypes.data if b.size else o.ctypes.data,
                                              o.ctypes.data, abi.WG_HOST, ctypes.byref(p)))
+
+    # -- row order (commit_graph_with_orphans git/mod.rs:761-775, insert_synthetics_sorted :234-242) ----
+    def order_rows(self, walk_time, orphan_time=None, syn_time=None, device=None, out_device_ptr=None):
+        """perm[final row] = source row (walk, then orphans, then synthetics).
+        Host int64 arrays, or device=((walk_ptr, n), (orphan_ptr, n), (syn_ptr, n));
+        out_device_ptr: write the permutation to device memory instead (returns None)."""
+        if device is not None:
+            (pw, nw), (po, no), (ps, ns) = device
+            res = abi.WG_DEVICE
+        else:
+            arrs = [np.ascontiguousarray(np.zeros(0) if a is None else a, np.int64)
+                    for a in (walk_time, orphan_time, syn_time)]
+            self._order_keep = arrs
+            (pw, po, ps), (nw, no, ns) = [a.ctypes.data if a.size else None for a in arrs], [a.size for a in arrs]
+            res = abi.WG_HOST
+        if out_device_ptr is not None:
+            self._check(lib().wg_order_rows(self._ctx, pw, nw, po, no, ps, ns, res, out_device_ptr, abi.WG_DEVICE))
+            return None
+        perm = np.empty(max(1, nw + no + ns), np.uint32)
+        self._check(lib().wg_order_rows(self._ctx, pw, nw, po, no, ps, ns, res, perm.ctypes.data, abi.WG_HOST))
+        return perm[:nw + no + ns]
 
     # -- search-match flags (commit_matches_query, commit_graph.rs:1509-1523) -------------
     def match_rows(self, query, row_begin=0, row_end=None, summaries=None, authors=None, device=None) -> int:
