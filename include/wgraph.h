@@ -390,6 +390,34 @@ int wg_copy_match_flags(wg_ctx *ctx, uint8_t *dst);
  * *out_len. */
 int wg_lower_utf8(const uint8_t *src, uint64_t len, uint8_t *dst, uint64_t cap, uint64_t *out_len);
 
+/* ---- consumer adapter: rasterise the emitted buffers
+ * The headless screenshot path (screenshot_mode.rs:101-141) renders the UI
+ * into an offscreen image cleared to the theme colour and saves a PNG; the
+ * reference's rasteriser (aetna-vulkano) is absent, so the engine freezes
+ * WG-RAST-1 (wg_render.hip): rows in order, per row its
+ * graph triangles then its glyph quads, one sample per pixel centre,
+ * owner-edge rule, flat graph colours, bilinear SDF text coverage, "over"
+ * blending in f32 onto the clear colour, RGBA8 output (alpha 255).
+ * Row r of the last emissions lands at image y = ((row_top[r] -
+ * row_top[top_row]) + origin_y) * scale; graph vertices are shifted by
+ * graph_x, glyph vertices keep their x.                                   */
+#define WG_RENDER_GRAPH 1
+#define WG_RENDER_TEXT  2
+typedef struct wg_render_params {
+    uint32_t width, height;   /* image size in pixels (<= 16384)            */
+    float    scale;           /* pixels per logical px (scale factor)       */
+    float    graph_x;         /* x of the graph column (logical px)         */
+    float    origin_y;        /* image y of top_row's top (logical px)      */
+    uint64_t top_row;         /* global row at origin_y                     */
+    float    clear[4];        /* background RGBA (alpha ignored: opaque)     */
+    uint32_t layers;          /* WG_RENDER_GRAPH | WG_RENDER_TEXT            */
+    uint32_t reserved;
+} wg_render_params;
+/* RGBA8 image (width * height * 4 bytes) into host or device memory. */
+int wg_render(wg_ctx *ctx, const wg_render_params *params, uint8_t *rgba, int32_t out_residency);
+/* Write an RGBA8 image as a PNG file (host; stored deflate, no compression). */
+int wg_write_png(const char *path, const uint8_t *rgba, uint32_t width, uint32_t height);
+
 /* ---- timing (HIP events on the context's stream) ------------------------ */
 #define WG_STAGE_MAX 1024
 /* on = 0 disables; on > 0 enables and restarts the stage log (on > 1 also

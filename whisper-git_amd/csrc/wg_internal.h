@@ -216,6 +216,10 @@ struct wg_ctx {
     bool     have_text = false;
     uint64_t text_rb = 0, text_re = 0, n_quads = 0;
     DevBuf text_sum, text_sum_off, text_off, text_rec, text_vtx;
+    int32_t text_slot = 0;          // atlas slot of the last glyph emission
+    float    text_scale = 1.0f;     // its text_px / em_px
+    // ---- rasteriser (wg_render.hip) -------------------------------------------------
+    DevBuf render_small, render_img;
     // ---- search-match flags (wg_search.hip) -------------------------------------------
     bool     match_on = false;      // a non-empty query is active: emission dims non-matching rows
     uint64_t match_rb = 0, match_re = 0, match_count = 0;

@@ -255,6 +255,8 @@ int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, 
     { const int _sr = wg_scan_reserve(c, rows + 2); if (_sr != WG_OK) return _sr; }
     c->text_rb = rb;
     c->text_re = re;
+    c->text_slot = p->slot;
+    c->text_scale = A.scale;
     c->n_quads = 0;
     wg_stage_begin(c, "text_rows");
     uint64_t nq = 0;

@@ -80,6 +80,8 @@ def lib():
                               ctypes.c_int),
             "wg_copy_match_flags": ([vp, vp], ctypes.c_int),
             "wg_order_rows": ([vp, vp, u64, vp, u64, vp, u64, i32, vp, i32], ctypes.c_int),
+            "wg_render": ([vp, ctypes.POINTER(abi.RenderParams), vp, i32], ctypes.c_int),
+            "wg_write_png": ([ctypes.c_char_p, vp, ctypes.c_uint32, ctypes.c_uint32], ctypes.c_int),
             "wg_lower_utf8": ([vp, u64, vp, u64, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "wg_shard_exchange": ([vp, vp, u64, ctypes.POINTER(ctypes.c_uint64), vp, ctypes.POINTER(abi.ShardMsg)],
                                   ctypes.c_int),
@@ -100,7 +102,7 @@ EXPORTED_SYMBOLS = (
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
     "wg_shard_copy_msg", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
     "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets",
-    "wg_match_rows", "wg_copy_match_flags", "wg_lower_utf8", "wg_order_rows")
+    "wg_match_rows", "wg_copy_match_flags", "wg_lower_utf8", "wg_order_rows", "wg_render", "wg_write_png")
 
 
 def to_lowercase(b: bytes) -> bytes:
@@ -114,6 +116,15 @@ def to_lowercase(b: bytes) -> bytes:
     out = np.empty(max(1, n.value), np.uint8)
     lib().wg_lower_utf8(src.ctypes.data, len(b), out.ctypes.data, n.value, ctypes.byref(n))
     return out[:n.value].tobytes()
+
+
+def write_png(path: str, rgba: np.ndarray) -> None:
+    """RGBA8 [H, W, 4] -> PNG file (the engine's writer, host code)."""
+    a = np.ascontiguousarray(rgba, np.uint8)
+    h, w = a.shape[:2]
+    rc = lib().wg_write_png(os.fsencode(path), a.ctypes.data, w, h)
+    if rc != abi.WG_OK:
+        raise WgError(rc, f"wg_write_png({path})")
 
 
 FONT_DIR = os.path.join(os.path.dirname(_HERE), "fonts")
@@ -333,6 +344,23 @@ class Engine:
             self._text_keep = (b, o)
             self._check(lib().wg_emit_glyphs(self._ctx, row_begin, row_end, b.ctypes.data if b.size else o.ctypes.data,
                                              o.ctypes.data, abi.WG_HOST, ctypes.byref(p)))
+
+    # -- consumer adapter (screenshot_mode.rs:101-141; WG-RAST-1) ---------------------------
+    def render(self, width, height, top_row=None, scale=1.0, graph_x=0.0, origin_y=0.0, clear=(0.09, 0.1, 0.12, 1.0),
+               graph=True, text=True, device_ptr: int | None = None):
+        """Rasterise the last emissions into RGBA8 [height, width, 4] (host),
+        or into device memory at device_ptr (returns None)."""
+        p = abi.RenderParams()
+        p.width, p.height, p.scale, p.graph_x, p.origin_y = width, height, scale, graph_x, origin_y
+        p.top_row = self.layout_summary().row_begin if top_row is None else top_row
+        p.clear[:] = [float(x) for x in (list(clear) + [1.0])[:4]]
+        p.layers = (abi.WG_RENDER_GRAPH if graph else 0) | (abi.WG_RENDER_TEXT if text else 0)
+        if device_ptr is not None:
+            self._check(lib().wg_render(self._ctx, ctypes.byref(p), device_ptr, abi.WG_DEVICE))
+            return None
+        img = np.empty((height, width, 4), np.uint8)
+        self._check(lib().wg_render(self._ctx, ctypes.byref(p), img.ctypes.data, abi.WG_HOST))
+        return img
 
     # -- row order (commit_graph_with_orphans git/mod.rs:761-775, insert_synthetics_sorted :234-242) ----
     def order_rows(self, walk_time, orphan_time=None, syn_time=None, device=None, out_device_ptr=None):

@@ -92,6 +92,13 @@ class RowText(ctypes.Structure):
 
 
 WG_DIM_ALPHA = 0.3
+WG_RENDER_GRAPH, WG_RENDER_TEXT = 1, 2
+
+
+class RenderParams(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_uint32), ("height", ctypes.c_uint32), ("scale", ctypes.c_float),
+                ("graph_x", ctypes.c_float), ("origin_y", ctypes.c_float), ("top_row", ctypes.c_uint64),
+                ("clear", ctypes.c_float * 4), ("layers", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class ShardMsg(ctypes.Structure):
