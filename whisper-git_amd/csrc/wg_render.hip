@@ -68,31 +68,31 @@ __device__ __forceinline__ bool owns(float ax, float ay, float bx, float by) {
     return by < ay || (by == ay && bx > ax);
 }
 
-// largest extent of any row's vertices outside [0, height] (row-local), both layers
-__global__ void k_row_overshoot(RenderArgs A, const float *__restrict__ height, float *__restrict__ margin) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// rows [lo, hi) (context) of the active layers: the largest extent of any
+// row's vertices outside [0, height] (row-local), and whether row_top fails to
+// be non-decreasing over them (then tiles walk every row)
+__global__ void k_row_overshoot(RenderArgs A, uint64_t lo, uint64_t hi, const float *__restrict__ height,
+                                float *__restrict__ margin) {
+    const uint64_t r = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= hi) return;
     float m = 0.0f;
-    if (A.g_vtx && j < A.g_re - A.g_rb) {
-        const float h = height[A.g_rb + j];
+    const float h = height[r];
+    if (A.g_vtx && r >= A.g_rb && r < A.g_re) {
         const float *v = reinterpret_cast<const float *>(A.g_vtx);
-        for (uint64_t i = A.g_off[j]; i < A.g_off[j + 1]; i++) {
+        for (uint64_t i = A.g_off[r - A.g_rb]; i < A.g_off[r - A.g_rb + 1]; i++) {
             const float y = v[i * 6 + 1];
             m = fmaxf(m, fmaxf(-y, y - h));
         }
     }
-    if (A.t_vtx && j < A.t_re - A.t_rb) {
-        const float h = height[A.t_rb + j];
+    if (A.t_vtx && r >= A.t_rb && r < A.t_re) {
         const float *v = reinterpret_cast<const float *>(A.t_vtx);
-        for (uint64_t i = A.t_off[j] * 6; i < A.t_off[j + 1] * 6; i++) {
+        for (uint64_t i = A.t_off[r - A.t_rb] * 6; i < A.t_off[r - A.t_rb + 1] * 6; i++) {
             const float y = v[i * 8 + 1];
             m = fmaxf(m, fmaxf(-y, y - h));
         }
     }
     if (m > 0.0f) atomicMax(reinterpret_cast<unsigned int *>(margin), __float_as_uint(m));   // non-negative floats order as ints
-    // a negative (or NaN) strip height makes row_top non-monotonic: tiles then walk every row
-    const uint64_t jj = A.g_vtx ? j : ~0ull;
-    if (jj < A.g_re - A.g_rb && !(height[A.g_rb + jj] >= 0.0f)) reinterpret_cast<unsigned int *>(margin)[1] = 1u;
-    if (A.t_vtx && j < A.t_re - A.t_rb && !(height[A.t_rb + j] >= 0.0f)) reinterpret_cast<unsigned int *>(margin)[1] = 1u;
+    if (!(A.row_top[r + 1] >= A.row_top[r])) reinterpret_cast<unsigned int *>(margin)[1] = 1u;
 }
 
 struct Tri {
@@ -119,7 +119,10 @@ __global__ __launch_bounds__(RT) void k_raster(RenderArgs A, uint8_t *__restrict
     if (threadIdx.x == 0) {
         // the same f32 expression as the triangles' row offset Yr
         auto yl = [&](uint64_t r) { return (A.row_top[r] - A.row_top[A.top_ctx]) + A.origin_y; };
-        const float m = A.margin[0] + 1.0f;
+        // slack: 1 px plus a few f32 ulps of the row_top magnitudes involved
+        const float mag = fmaxf(fmaxf(fabsf(A.row_top[lo2]), fabsf(A.row_top[hi])), fabsf(A.row_top[A.top_ctx])) +
+                          fabsf(A.origin_y);
+        const float m = A.margin[0] + 1.0f + mag * 1.0e-6f;
         const float ya = (float)ty0 / A.scale - m, yb = (float)(ty0 + TS) / A.scale + m;
         uint64_t a = lo2, c = hi;
         if (!__float_as_uint(A.margin[1])) {   // row_top is non-decreasing: binary searches
@@ -315,11 +318,13 @@ int wg_render(wg_ctx *c, const wg_render_params *p, uint8_t *rgba, int32_t out_r
         dst = c->render_img.as<uint8_t>();
     }
     wg_stage_begin(c, "render");
-    const uint64_t rows = std::max(g ? A.g_re - A.g_rb : 0, t ? A.t_re - A.t_rb : 0);
-    if (rows) {
+    uint64_t lo = ~0ull, hi = 0;   // rows of the active layers (context)
+    if (g) { lo = A.g_rb; hi = A.g_re; }
+    if (t) { lo = std::min(lo, A.t_rb); hi = std::max(hi, A.t_re); }
+    if (hi > lo) {
         RenderArgs B = A;
         if (!g) B.g_vtx = nullptr;
-        hipLaunchKernelGGL(k_row_overshoot, dim3((uint32_t)((rows + 255) / 256)), dim3(256), 0, s, B,
+        hipLaunchKernelGGL(k_row_overshoot, dim3((uint32_t)((hi - lo + 255) / 256)), dim3(256), 0, s, B, lo, hi,
                            c->g_height.as<const float>(), c->render_small.as<float>());
     }
     if (!g) A.g_vtx = nullptr;
