@@ -1,0 +1,53 @@
+"""GPU per-frame geometry (history_view recomputes row_geometry_with_bands every
+frame, commit_graph.rs:1419-1421): a frame with the same layout and bitwise the
+same bands reuses the geometry in place; any changed band (host or device, in
+place or not) recomputes it — always equal to the oracle."""
+import numpy as np
+import pytest
+
+from oracle import oracle_c
+from wgraph import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(engine, o, band):
+    og = o.row_geometry(band)
+    g = engine.geometry()
+    for k in ("row_top", "height", "node_y", "vert_off", "vert", "curve_off", "curve"):
+        assert g[k].tobytes() == og[k].tobytes(), k
+
+
+def test_frames_reuse_and_recompute(engine):
+    import torch
+    d = synth.generate("random13", 30000, seed=21)
+    engine.build(d)
+    o = oracle_c.OracleLayout(d)
+    band = d.band.copy()
+    engine.row_geometry(band)
+    _check(engine, o, band)
+    engine.row_geometry(band)                 # same bands: reused
+    _check(engine, o, band)
+    band[20000] = 30.0                        # a new pills band late in the list
+    engine.row_geometry(band)
+    _check(engine, o, band)
+    band[5] = 0.0 if band[5] else 30.0        # and one early
+    engine.row_geometry(band)
+    _check(engine, o, band)
+    tb = torch.from_numpy(band).cuda()        # device bands, changed in place between frames
+    torch.cuda.synchronize()
+    engine.row_geometry(device_ptr=tb.data_ptr())
+    _check(engine, o, band)
+    tb[12345] = 7.5
+    band[12345] = 7.5
+    torch.cuda.synchronize()
+    engine.row_geometry(device_ptr=tb.data_ptr())
+    _check(engine, o, band)
+    engine.row_geometry(device_ptr=tb.data_ptr())
+    _check(engine, o, band)
+    engine.row_geometry()                     # back to build()'s zero-band geometry
+    _check(engine, o, None)
+    engine.emit_vertices(0, 500, selected=3)
+    v, _ = o.emit_vertices(0, 500, selected=3, use_build_geometry=True)
+    assert engine.vertex_summary().checksum == oracle_c.vertex_checksum(v)
+    o.close()

@@ -321,6 +321,8 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     if ((rc = wg_side_join(c)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
     c->have_geom = true;
+    c->geom_key_gen = c->layout_gen;   // the geometry of (this layout, no bands)
+    c->geom_key_band = false;
     return WG_OK;
 }
 
@@ -392,11 +394,19 @@ int wg_copy_row_heights(wg_ctx *c, float *h) {
 // ---------------------------------------------------------------------------
 // row_geometry_with_bands (:367-399)
 // ---------------------------------------------------------------------------
+// first row whose band differs bitwise from the previous frame's (atomicMin)
+__global__ void k_band_diff(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b, uint64_t n,
+                            unsigned long long *first) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (a[i] != b[i]) { atomicMin(first, (unsigned long long)i); return; }
+}
+
 int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
     if (!c) return WG_E_INVALID;
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
     if (c->sh.on && !c->sh.replicated) return wg_fail(c, WG_E_STATE, "sharded layout: use wg_shard_geometry_begin");
     (void)hipSetDevice(c->device);
+    const bool had_geom = c->have_geom;
     c->have_geom = c->have_vtx = c->have_text = false;
     const float *d_band = nullptr;
     if (band) {
@@ -410,10 +420,31 @@ int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
             return wg_fail(c, WG_E_INVALID, "bad residency %d", residency);
         }
     }
+    // Per-frame reuse (history_view recomputes
+    // row_geometry_with_bands every frame, commit_graph.rs:1419-1421): the same
+    // layout with bitwise the same bands as the geometry in place -> nothing to do.
+    const bool same_layout = had_geom && c->geom_key_gen == c->layout_gen;
+    if (same_layout && !band && !c->geom_key_band) { c->have_geom = true; return WG_OK; }
+    if (same_layout && band && c->geom_key_band && c->n) {
+        WG_ALLOC(c, c->geom_diff_first, 16);
+        WG_HIP(c, hipMemsetAsync(c->geom_diff_first.p, 0xFF, 8, c->stream));
+        const uint64_t g = std::min<uint64_t>((c->n + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_band_diff, dim3((uint32_t)g), dim3(256), 0, c->stream, reinterpret_cast<const uint32_t *>(d_band),
+                           c->band_prev.as<const uint32_t>(), c->n, c->geom_diff_first.as<unsigned long long>());
+        uint64_t first = 0;
+        if (const int frc = wg_fetch(c, {{c->geom_diff_first.p, true}}, &first)) return frc;
+        if (first == ~0ull) { c->have_geom = true; return WG_OK; }
+    }
     int rc;
     if ((rc = wg_stage_rowtop(c, d_band)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, d_band)) != WG_OK) return rc;
     c->have_geom = true;
+    c->geom_key_gen = c->layout_gen;
+    c->geom_key_band = band != nullptr;
+    if (band && c->n) {   // the bands this geometry was made with (compared by the next frame)
+        WG_ALLOC(c, c->band_prev, c->n * 4 + 4);
+        WG_HIP(c, hipMemcpyAsync(c->band_prev.p, d_band, c->n * 4, hipMemcpyDeviceToDevice, c->stream));
+    }
     return WG_OK;
 }
 

@@ -194,6 +194,11 @@ struct wg_ctx {
     DevBuf rowflags_lists;              // the flags the curve lists were filtered with
     DevBuf scurve_off, scurve_ref, scurve_row;   // curve superset (flags ignored), swept once per layout
     DevBuf geom_diff;                   // uint32: flags differ
+    // per-frame reuse: the geometry in place was made for (layout geom_key_gen, bands or none)
+    uint64_t geom_key_gen = ~0ull;
+    bool     geom_key_band = false;
+    DevBuf   band_prev;                 // float [N] the bands of that geometry
+    DevBuf   geom_diff_first;           // u64: first row whose band differs
     DevBuf sweep_big;       // uint32 [nch] chunks too wide for the register sweep
     uint32_t sweep_reg_cap = 512;   // edges per chunk the register sweep holds (WG_OPT_SWEEP_REG)
     const float *edge_y = nullptr;   // per edge {child_y, parent_y} override (row-sharded geometry), or null
