@@ -76,6 +76,35 @@ def cpu_baseline(dag, rows, log, min_seconds=10.0, max_reps=4):
                       f"row_geometry_with_bands + vertex emission, 1 thread, {total:.1f}s total"}
 
 
+def cpu_baseline_threads(dag, rows, log, threads=None, min_seconds=5.0, max_reps=4):
+    """The same CPU oracle with the per-row stage spread over host threads:
+    build and row_geometry_with_bands stay sequential (the greedy lane walk and
+    the f32 row_top prefix are sequential in the reference), graph_cell
+    emission runs on `threads` threads over 50k-row chunks (ctypes releases the
+    GIL inside the C oracle)."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, ROOT)
+    from oracle import oracle_c   # baseline only
+    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    d = dag.slice_rows(min(rows, dag.n))
+    total, reps = 0.0, 0
+    with ThreadPoolExecutor(threads) as ex:
+        while reps < max_reps and (reps == 0 or total < min_seconds):
+            t0 = time.perf_counter()
+            o = oracle_c.OracleLayout(d)
+            o.row_geometry(d.band)
+            step = 50_000
+            list(ex.map(lambda r0: len(o.emit_vertices(r0, min(d.n, r0 + step), selected=7 if r0 == 0 else -1)[0]),
+                        range(0, d.n, step)))
+            total += time.perf_counter() - t0
+            reps += 1
+            o.close()
+    log(f"cpu baseline ({threads} threads for emission): {d.n} rows x {reps} in {total:.2f}s")
+    return {"value": d.n * reps / total, "unit": "commit-rows/s", "cores": threads, "kind": "port",
+            "sample": f"first {d.n} rows of the same workload, {reps} passes: oracle build + row_geometry_with_bands "
+                      f"(sequential) + vertex emission on {threads} threads"}
+
+
 def extra_measurements(eng, dag, dev, torch, r0, r1, args, log):
     """Side measurements beside the headline metric (never `value`):
     glyph quads (A13) for the same rows with synthetic summaries, and the
@@ -362,9 +391,10 @@ def main():
         f"build mode {int(eng.debug_counters()[5])}" + (f", exchanges/step {comm.exchanges / (args.steps + args.warmup):.1f}"
                                                          if comm else ""))
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(dag, args.cpu_rows, log)
+        cpu_mt = cpu_baseline_threads(dag, args.cpu_rows, log)
 
     if rank == 0:
         out = {"metric": "commit-rows/sec to vertex buffers, 1M-commit synthetic DAG per GPU",
@@ -375,7 +405,7 @@ def main():
                           "rows_total": rows_total, "rows_per_gpu": args.rows_per_gpu,
                           "vertices_per_gpu": int(vs.n_vertices), "parallelism": f"row-shard x{world}"},
                "stages_ms": stages, "host_input_rows_per_s": None if host_rate is None else round(host_rate, 1),
-               "roofline": roofline, "cpu_baseline": cpu, **extras}
+               "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_threads": cpu_mt, **extras}
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:
