@@ -37,3 +37,16 @@ def engine():
     e = Engine(0)
     yield e
     e.close()
+
+
+# GPU tests run the §8(a)-(e) hot path first (layout/geometry/vertex parity,
+# shards, atlas, glyph quads), then the §8(f) rows (order, search, frames,
+# render), so a failure in a widening row never hides hot-path results.
+_FIRST = ("test_gpu_parity", "test_gpu_shard", "test_gpu_font", "test_gpu_text")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        mod = item.module.__name__.rsplit(".", 1)[-1] if item.module else ""
+        return (0, _FIRST.index(mod)) if mod in _FIRST else (1, 0)
+    items.sort(key=rank)   # stable: file order is kept within each group
