@@ -92,7 +92,15 @@ def run_case(eng, comm, torch, kind, n, seed, world, rank, errors):
     ov, ooff = o.emit_vertices(s, e, selected=sel)
     same("vtx_off", eng.vertex_offsets(), ooff)
     if eng.vertex_summary().checksum != oracle_c.vertex_checksum(ov):
-        errors.append(f"{kind}/{n}/w{world} rank {rank}: vertex checksum")
+        gv = eng.vertices()
+        gw = np.ascontiguousarray(gv).view(np.uint32).reshape(len(gv), -1)
+        ow = np.ascontiguousarray(ov).view(np.uint32).reshape(len(ov), -1)
+        bad = np.nonzero((gw != ow).any(axis=1))[0] if gw.shape == ow.shape else np.array([0])
+        i = int(bad[0]) if len(bad) else -1
+        row = s + int(np.searchsorted(ooff.astype(np.int64), i, side="right")) - 1 if i >= 0 else -1
+        errors.append(f"{kind}/{n}/w{world} rank {rank}: vertex checksum; {len(bad)} vertices differ, first {i} "
+                      f"(row {row}, sel {sel}): got {gw[i].view(np.float32) if i >= 0 else None} "
+                      f"want {ow[i].view(np.float32) if i >= 0 else None}")
     o.close()
     del keep
 

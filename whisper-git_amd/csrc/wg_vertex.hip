@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         const uint4 *__restrict__ tinfo, const uint8_t *__restrict__ match, int64_t mlo, int64_t mhi,
         float4 *__restrict__ out) {
     __shared__ RowInfo rows[MAXR];
-    __shared__ uint8_t pair_row[PAIRS];            // row (within the tile) of every vertex pair
+    __shared__ __attribute__((aligned(4))) uint8_t pair_row[PAIRS];   // row (within the tile) of every vertex pair
     __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
     __shared__ uint32_t curve_col[MAXC];
     __shared__ uint32_t vents[MAXV];               // the tile's vertical entries
@@ -152,7 +152,6 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     const uint64_t nrows = re - rb;
     const float visf = (float)(vis - 1);
     if (tid < 2 * WG_PALETTE_SIZE) pal[tid] = palette[tid];
-    for (uint32_t p = tid; p < PAIRS; p += VT) pair_row[p] = 0;
     const uint4 ti = tinfo[blockIdx.x], tn = tinfo[blockIdx.x + 1];
     const uint64_t first = ti.x;
     const uint32_t A = ti.y, K0 = ti.z;
@@ -161,6 +160,13 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     nC = nC < (uint32_t)MAXC ? nC : (uint32_t)MAXC;
     // ---- 1. one round of independent global loads: rows, verticals, curves ---------
     if (wid == 0) {
+        // wave 0 alone clears pair_row and then marks the row starts: LDS ops of
+        // one wave complete in order, so no other wave can clear a mark after it
+        // was written (the clear used to be spread over all waves, unordered
+        // against wave 0's marks before the barrier)
+        for (uint32_t i = lane; i < PAIRS / 4; i += 64) reinterpret_cast<uint32_t *>(pair_row)[i] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
         const uint64_t j0 = first + lane;
         const uint64_t j = j0 < nrows ? j0 : nrows - 1;
         const uint64_t r = rb + j;
