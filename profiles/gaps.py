@@ -1,0 +1,37 @@
+"""Per-step kernel timeline from a rocprofv3 --kernel-trace CSV: kernels of
+the last step (k_vtx_tile end to k_vtx_tile end), their durations and the
+idle gap before each one (host synchronisations show up as gaps).
+
+usage: python3 profiles/gaps.py <run_kernel_trace.csv> [min_gap_us]
+"""
+import csv
+import re
+import sys
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1], newline="")))
+    min_gap = float(sys.argv[2]) if len(sys.argv) > 2 else 3.0
+    ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                  re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))) for r in rows))
+    ends = [i for i, k in enumerate(ks) if k[2] == "k_vtx_tile"]
+    a, b = ends[-2], ends[-1]
+    step = ks[a + 1:b + 1]
+    t0 = ks[a][1]
+    busy = sum(e - s for s, e, _ in step)
+    span = step[-1][1] - t0
+    print(f"step span {span / 1e3:.1f} us, busy {busy / 1e3:.1f} us, {len(step)} kernels")
+    prev = t0
+    idle_total = 0
+    for s, e, n in step:
+        gap = (s - prev) / 1e3
+        if gap > 0:
+            idle_total += gap
+        mark = "  <-- gap" if gap >= min_gap else ""
+        print(f"{(s - t0) / 1e3:9.1f} {gap:7.1f} {(e - s) / 1e3:8.1f}  {n}{mark}")
+        prev = max(prev, e)
+    print(f"idle {idle_total:.1f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -11,11 +11,14 @@
 // the snapshot.  WG-TEXT-1 freezes that layout on top of the WG-SDF-1 atlas.
 //
 // Two kernels:
-//   k_text_rows    one thread per row: builds the three runs (hex digits,
+//   k_text_rows    one lane per row: builds the three runs (hex digits,
 //                  summary bytes, relative-time text), advances the pen
 //                  sequentially in f32 (the order a CPU layout loop uses),
 //                  clips the summary at summary_max_x and writes one 16-byte
-//                  record per visible glyph {pen x, baseline, glyph, run}
+//                  record per visible glyph {pen x, baseline, glyph, run},
+//                  staged per wave and flushed as per-row runs.  VALU-issue
+//                  bound (one character per lane per iteration, lanes idle
+//                  past their row's end), not memory bound.
 //   k_text_quads   one thread per glyph record: 6 TextVertex (192 B) staged
 //                  per wave in LDS and written as contiguous 1 KiB stores
 // Rows are counted first (same walk, counts only) so every record has a
@@ -57,7 +60,15 @@ __device__ __forceinline__ uint32_t relative_time(int64_t now, int64_t t, char *
     int64_t v;
     const char *unit;
     uint32_t ul;
-    if (d < 3600) { v = d / 60; unit = "m"; ul = 1; }
+    if (d < 4294967296ll) {   // same quotients in 32-bit arithmetic
+        const uint32_t d32 = (uint32_t)d;
+        if (d32 < 3600u) { v = d32 / 60u; unit = "m"; ul = 1; }
+        else if (d32 < 86400u) { v = d32 / 3600u; unit = "h"; ul = 1; }
+        else if (d32 < 604800u) { v = d32 / 86400u; unit = "d"; ul = 1; }
+        else if (d32 < 2592000u) { v = d32 / 604800u; unit = "w"; ul = 1; }
+        else if (d32 < 31536000u) { v = d32 / 2592000u; unit = "mo"; ul = 2; }
+        else { v = d32 / 31536000u; unit = "y"; ul = 1; }
+    } else if (d < 3600) { v = d / 60; unit = "m"; ul = 1; }
     else if (d < 86400) { v = d / 3600; unit = "h"; ul = 1; }
     else if (d < 604800) { v = d / 86400; unit = "d"; ul = 1; }
     else if (d < 2592000) { v = d / 604800; unit = "w"; ul = 1; }
@@ -65,7 +76,12 @@ __device__ __forceinline__ uint32_t relative_time(int64_t now, int64_t t, char *
     else { v = d / 31536000; unit = "y"; ul = 1; }
     char tmp[20];
     uint32_t n = 0;
-    do { tmp[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    if (v < 4294967296ll) {   // 32-bit digits (the common case)
+        uint32_t v32 = (uint32_t)v;
+        do { tmp[n++] = (char)('0' + v32 % 10u); v32 /= 10u; } while (v32);
+    } else {
+        do { tmp[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    }
     uint32_t len = 0;
     while (n) buf[len++] = tmp[--n];
     for (uint32_t i = 0; i < ul; i++) buf[len++] = unit[i];
@@ -78,62 +94,126 @@ __device__ __forceinline__ uint32_t glyph_of(const TextArgs &A, uint32_t ch) {
     return g;
 }
 
-// one run: returns the number of visible glyphs; writes records when out != null
-__device__ __forceinline__ uint32_t run(const TextArgs &A, const uint8_t *s, uint32_t len, float x, float max_x,
-                                        float base, uint32_t run_id, uint4 *out, uint32_t o) {
-    uint32_t n = 0;
-    float pen = x;
-    for (uint32_t i = 0; i < len; i++) {
-        const uint32_t g = glyph_of(A, s[i]);
-        const wg_glyph gl = A.glyphs[g];
-        const float next = pen + gl.advance * A.scale;
-        if (next > max_x) break;                       // clipped (summary column)
-        if (gl.w) {
-            if (out) out[o + n] = make_uint4(__float_as_uint(pen), __float_as_uint(base), g, run_id);
-            n++;
-        }
-        pen = next;
-    }
-    return n;
-}
-
-__device__ __forceinline__ float run_width(const TextArgs &A, const uint8_t *s, uint32_t len) {
-    float w = 0.0f;
-    for (uint32_t i = 0; i < len; i++) w = w + A.glyphs[glyph_of(A, s[i])].advance * A.scale;
-    return w;
-}
+// The pen walk is sequential in f32 per row, so a lane owns a row; the 64
+// rows of a wave advance in lock step, one character per iteration (a run
+// switch takes one iteration), which keeps the loop wave-uniform:
+//   * byte -> {glyph, visible, advance * scale} from a 256-entry LDS table
+//     (every byte maps through glyph_of; the product is the same f32 value the
+//     per-glyph multiply gives);
+//   * the short SHA and the relative-time text sit in LDS per lane;
+//   * records go to a per-wave LDS stage (pen + glyph/run, 8 B; the baseline is
+//     per row), one slot per lane per iteration, and every RT_R iterations the
+//     wave flushes them: a lane's pending records are contiguous in the
+//     output, so RT_R lanes write one row's (<= RT_R * 16 B) run per store instruction
+//     instead of 64 scattered 16-B stores.
+constexpr int RT_R = 8;                    // iterations between flushes (record slots per lane)
+constexpr int RT_STR = 24;                 // per lane: SHA at [0, 7), time text at [8, 8 + 14]
 
 template <bool WRITE>
-__global__ void k_text_rows(TextArgs A, uint64_t *__restrict__ cnt, const uint64_t *__restrict__ off, uint4 *__restrict__ rec) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t r = A.rb + j;
-    if (r >= A.re) return;
-    const float base = A.node_y[A.row_base + r] + A.baseline_dy;
-    uint8_t sha[7];
-    uint32_t nsha = 0;
-    if (!(A.flags[r] & WG_FLAG_SYNTHETIC)) {
-        const char *hex = "0123456789abcdef";
-        for (int i = 0; i < 7; i++) {
-            const uint8_t b = A.oid[r * 20 + i / 2];
-            sha[i] = (uint8_t)hex[(i & 1) ? (b & 15) : (b >> 4)];
-        }
-        nsha = 7;
+__global__ void __launch_bounds__(T) k_text_rows(TextArgs A, uint64_t *__restrict__ cnt, const uint64_t *__restrict__ off,
+                                                 uint4 *__restrict__ rec) {
+    __shared__ float s_adv[256];
+    __shared__ uint32_t s_gl[256];                          // glyph | visible << 31
+    __shared__ uint8_t s_str[T / 64][RT_STR][64];           // [wave][char][lane]
+    __shared__ uint2 s_rec[WRITE ? T / 64 : 1][WRITE ? RT_R : 1][64];   // {pen, glyph | run << 24}
+    __shared__ uint64_t s_base[WRITE ? T / 64 : 1][64];
+    __shared__ uint32_t s_pend[WRITE ? T / 64 : 1][64];
+    __shared__ float s_y[WRITE ? T / 64 : 1][64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    {
+        const uint32_t g = glyph_of(A, tid);
+        const wg_glyph gl = A.glyphs[g];
+        s_adv[tid] = gl.advance * A.scale;
+        s_gl[tid] = g | (gl.w ? 0x80000000u : 0u);
     }
-    const uint8_t *sum = A.sum ? A.sum + A.sum_off[r] : nullptr;
-    uint32_t nsum = A.sum ? (uint32_t)(A.sum_off[r + 1] - A.sum_off[r]) : 0;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + tid;
+    const uint64_t r = A.rb + j;
+    const bool live = r < A.re;
+    float base = 0.0f, tx = 0.0f;
+    uint32_t nsha = 0, nt = 0, nsum = 0, d = 0;
+    const uint8_t *sum = nullptr;
+    bool nosum = false;
+    uint8_t(*str)[64] = s_str[w];
+    if (live) {
+        base = A.node_y[A.row_base + r] + A.baseline_dy;
+        if (!(A.flags[r] & WG_FLAG_SYNTHETIC)) {
+            const char *hex = "0123456789abcdef";
+            for (int i = 0; i < 7; i++) {
+                const uint8_t b = A.oid[r * 20 + i / 2];
+                str[i][lane] = (uint8_t)hex[(i & 1) ? (b & 15) : (b >> 4)];
+            }
+            nsha = 7;
+        }
+        if (A.sum) {
+            const uint64_t so = A.sum_off[r];
+            nsum = (uint32_t)(A.sum_off[r + 1] - so);
+            sum = A.sum + so;
+        }
+        if (nsum == 0) { nosum = true; nsum = 12; }
+        char tb[16];
+        nt = relative_time(A.now, A.time[r], tb);
+        for (uint32_t i = 0; i < nt; i++) str[8 + i][lane] = (uint8_t)tb[i];
+        // search dimming (commit_graph.rs:1467, 1482): colours 3..5 = the run colours at WG_DIM_ALPHA
+        d = (A.match && r >= A.mrb && r < A.mre && !A.match[r - A.mrb]) ? 3u : 0u;
+    }
+    if (WRITE) s_y[w][lane] = base;
+    __syncthreads();   // glyph table, strings
+    if (live) {
+        float wdt = 0.0f;   // run_width: f32 sum of advances in order
+        for (uint32_t i = 0; i < nt; i++) wdt = wdt + s_adv[str[8 + i][lane]];
+        tx = A.time_right_x - wdt;
+    }
     const uint8_t *none = reinterpret_cast<const uint8_t *>("(no summary)");
-    if (nsum == 0) { sum = none; nsum = 12; }
-    char tb[24];
-    const uint32_t nt = relative_time(A.now, A.time[r], tb);
-    const float tx = A.time_right_x - run_width(A, reinterpret_cast<const uint8_t *>(tb), nt);
-    uint4 *out = WRITE ? rec : nullptr;
-    uint32_t o = WRITE ? (uint32_t)(off[j]) : 0u;
-    // search dimming (commit_graph.rs:1467, 1482): colours 3..5 = the run colours at WG_DIM_ALPHA
-    const uint32_t d = (A.match && r >= A.mrb && r < A.mre && !A.match[r - A.mrb]) ? 3u : 0u;
-    uint32_t n = run(A, sha, nsha, A.sha_x, 3.0e38f, base, 0 + d, out, o);
-    n += run(A, sum, nsum, A.summary_x, A.summary_max_x, base, 1 + d, out, o + n);
-    n += run(A, reinterpret_cast<const uint8_t *>(tb), nt, tx, 3.0e38f, base, 2 + d, out, o + n);
-    if (!WRITE) cnt[j] = n;
+    // per-lane walk state: run 0 sha, 1 summary, 2 time, 3 done
+    uint32_t run = 0, i = 0, len = nsha, n = 0, flushed = 0;
+    float pen = A.sha_x, max_x = 3.0e38f;
+    bool active = live;
+    const uint64_t obase = WRITE && live ? off[j] : 0ull;
+    while (__any(active)) {
+#pragma unroll 1
+        for (int it = 0; it < RT_R; it++) {
+            if (!active) continue;
+            if (i >= len) {   // next run
+                run++;
+                i = 0;
+                if (run == 1) { len = nsum; pen = A.summary_x; max_x = A.summary_max_x; }
+                else if (run == 2) { len = nt; pen = tx; max_x = 3.0e38f; }
+                else { active = false; }
+                continue;
+            }
+            const uint32_t ch = run == 1 ? (nosum ? none[i] : sum[i]) : str[run == 0 ? i : 8 + i][lane];
+            const float next = pen + s_adv[ch];
+            if (next > max_x) { i = len; continue; }   // clipped (summary column)
+            const uint32_t gv = s_gl[ch];
+            if (gv >> 31) {
+                if (WRITE) s_rec[w][n - flushed][lane] = make_uint2(__float_as_uint(pen), (gv & 0xFFFFFFu) | ((run + d) << 24));
+                n++;
+            }
+            pen = next;
+            i++;
+        }
+        if (WRITE) {
+            s_base[w][lane] = obase + flushed;
+            s_pend[w][lane] = n - flushed;
+            flushed = n;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t q = lane % RT_R;
+#pragma unroll
+            for (int t = 0; t < RT_R; t++) {
+                const uint32_t row = t * (64 / RT_R) + lane / RT_R;
+                if (q < s_pend[w][row]) {
+                    const uint2 v = s_rec[w][q][row];
+                    rec[s_base[w][row] + q] = make_uint4(v.x, __float_as_uint(s_y[w][row]), v.y & 0xFFFFFFu, v.y >> 24);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    if (!WRITE && live) cnt[j] = n;
 }
 
 struct QuadArgs {

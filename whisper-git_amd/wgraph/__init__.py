@@ -41,6 +41,16 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: build it with `make engine` or __graft_entry__.build()")
+        # One HIP runtime per process.  torch ships its own libamdhip64
+        # (SONAME libamdhip64.so.7) and loads it by the name libamdhip64.so,
+        # which does not match an /opt/rocm copy loaded earlier: loading the
+        # engine first leaves two runtimes in a process that later uses
+        # torch.cuda ("No HIP GPUs are available").  With torch imported first
+        # the engine binds to torch's runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         vp, u64, i64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int32
         sig = {
