@@ -263,6 +263,13 @@ int wg_shard_build_begin(wg_ctx *ctx, const wg_commits *commits, int world, int 
 int wg_shard_geometry_begin(wg_ctx *ctx, const float *band, int32_t band_residency, wg_shard_msg *out);
 /* Copy this rank's current message (device or host destination). */
 int wg_shard_copy_msg(wg_ctx *ctx, void *dst);
+/* Write this rank's transport slot into device memory, queued on the
+ * engine's stream without a host synchronisation: a 16-byte header (message
+ * length as u64, then zeros), then the message when it fits in `cap` bytes
+ * (the payload's first 16 bytes are zero for shorter messages).  `slot` is
+ * 16-byte aligned and holds 16 + max(cap, 16) bytes.  The caller orders its
+ * all-gather after the engine's stream (e.g. RCCL on that same stream). */
+int wg_shard_pack_slot(wg_ctx *ctx, void *slot, uint64_t cap);
 /* Deliver the all-gathered messages; runs to the next exchange or the end.
  * Every message starts with a 16-byte header; `heads` (may be NULL) is a host
  * copy of them (rank r's at heads[4r..4r+3]) that saves the engine a device

@@ -73,6 +73,7 @@ def main():
             self.rank, self.eng, self.stream = rank, eng, stream
             self.t = None
             self.label = ""
+            self.on_device, self.device = True, dev   # slots packed in stream order, as over RCCL
 
         def start(self, label):
             gpu.acquire()
@@ -89,12 +90,17 @@ def main():
             seg[self.rank].append((self.label, time.perf_counter() - self.t))
             gpu.release()
 
-        def allgather(self, nbytes, fill, step=0):
+        def allgather(self, nbytes, fill, step=0, pack=None):
             cap = ShardComm.round_cap(nbytes)
             with torch.cuda.stream(self.stream):
-                send = torch.zeros(cap, dtype=torch.uint8, device=dev)
-            if nbytes:
-                fill(send.data_ptr())
+                if pack is not None:
+                    slot = torch.empty(cap + ShardComm.HDR, dtype=torch.uint8, device=dev)
+                    pack(slot.data_ptr(), cap)
+                    send = slot[ShardComm.HDR:]
+                else:
+                    send = torch.zeros(cap, dtype=torch.uint8, device=dev)
+                    if nbytes:
+                        fill(send.data_ptr())
             self.stop()
             slots[self.rank] = (send, nbytes)
             bar.wait()
@@ -127,6 +133,10 @@ def main():
     errors = []
 
     def rank_main(r):
+        with torch.cuda.stream(streams[r]):   # the engine's stream is the transport's stream
+            rank_body(r)
+
+    def rank_body(r):
         try:
             eng = engines[r]
             comm = EmuComm(r, eng, streams[r])

@@ -59,3 +59,95 @@ def test_two_shards_row_top_beyond_2_25(tmp_path):
 
 def test_four_shards_small(tmp_path):
     run_world(4, "wide16:4000:21,random13:64:22", tmp_path)
+
+
+def _lockstep(engines, begin):
+    """Drive every rank's exchange protocol in one thread: slots written by
+    wg_shard_pack_slot in stream order (the device-transport path ShardComm
+    takes over RCCL), gathered by placing the slots side by side."""
+    import ctypes
+
+    import numpy as np
+    import torch
+    from wgraph import abi, lib
+    from wgraph.shard import ShardComm
+
+    W = len(engines)
+    msgs = [abi.ShardMsg() for _ in range(W)]
+    for r, e in enumerate(engines):
+        e._check(begin(e, r, ctypes.byref(msgs[r])))
+    rounds = 0
+    while not msgs[0].done:
+        assert all(not m.done for m in msgs) and len({int(m.step) for m in msgs}) == 1
+        cap = ShardComm.round_cap(max(int(m.bytes) for m in msgs))
+        stride = cap + ShardComm.HDR
+        slots = torch.empty(W * stride, dtype=torch.uint8, device="cuda")
+        for r, e in enumerate(engines):
+            e._check(lib().wg_shard_pack_slot(e._ctx, slots.data_ptr() + r * stride, cap))
+        head = slots.view(W, stride)[:, :32].cpu().numpy()
+        sizes = [int(m.bytes) for m in msgs]
+        assert [int(x) for x in head[:, :8].copy().view(np.int64).reshape(-1)] == sizes
+        assert not head[:, 8:16].any()
+        heads = np.ascontiguousarray(head[:, 16:32]).view(np.uint32).reshape(W, 4)
+        sz = (ctypes.c_uint64 * W)(*sizes)
+        for r, e in enumerate(engines):
+            e._check(lib().wg_shard_exchange(e._ctx, slots.data_ptr() + ShardComm.HDR, stride, sz,
+                                              heads.ctypes.data, ctypes.byref(msgs[r])))
+        torch.cuda.current_stream().synchronize()
+        rounds += 1
+    assert all(m.done for m in msgs)
+    return rounds
+
+
+@pytest.mark.parametrize("world,kind,n", [(2, "wide16", 40000), (3, "random13", 20000), (4, "linux", 30000)])
+def test_packed_slots_in_one_process(world, kind, n):
+    """wg_shard_pack_slot: every rank's slot packed on the shared stream, no
+    host synchronisation before the gather; shards equal the oracle."""
+    import ctypes
+    import sys as _sys
+
+    import numpy as np
+    import torch
+    _sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+    _sys.path.insert(0, ROOT)
+    import wgraph
+    from oracle import oracle_c
+    from wgraph import abi, lib, synth
+    from wgraph.shard import shard_rows
+
+    d = synth.generate(kind, n, seed=21)
+    dev = torch.device("cuda", 0)
+    keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                   d.parent_oid.reshape(-1), d.flags, d.band)]
+    c = abi.Commits()
+    c.n_commits, c.n_parents = d.n, d.e
+    c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
+    c.residency = abi.WG_DEVICE
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    engines = [wgraph.Engine(0) for _ in range(world)]
+    o = oracle_c.OracleLayout(d)
+    try:
+        for e in engines:
+            e.set_stream(stream)
+        rng = [shard_rows(d.n, world, r) for r in range(world)]
+        _lockstep(engines, lambda e, r, m: lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), world, r,
+                                                                       rng[r][0], rng[r][1], m))
+        _lockstep(engines, lambda e, r, m: lib().wg_shard_geometry_begin(e._ctx, keep[5].data_ptr(), abi.WG_DEVICE, m))
+        og = o.row_geometry(d.band)
+        for r, e in enumerate(engines):
+            s, t = rng[r]
+            assert int(e.debug_counters()[5]) == 1, "sharded path expected"
+            lane, color = e.lanes()
+            assert lane.tobytes() == o.lane[s:t].tobytes() and color.tobytes() == o.color[s:t].tobytes()
+            g = e.geometry()
+            vo = og["vert_off"].astype(np.int64)
+            assert g["row_top"].tobytes() == og["row_top"][s:t + 1].tobytes()
+            assert g["vert"].tobytes() == og["vert"][vo[s]:vo[t]].tobytes()
+            e.emit_vertices(s, t, selected=s + 3)
+            ov, _ = o.emit_vertices(s, t, selected=s + 3)
+            assert e.vertex_summary().checksum == oracle_c.vertex_checksum(ov), f"rank {r} vertices"
+    finally:
+        o.close()
+        for e in engines:
+            e.close()
+        del keep

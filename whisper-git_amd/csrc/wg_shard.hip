@@ -379,6 +379,11 @@ __global__ void k_sh_edges_own(LocalEdgeArgs A) {
 
 // a message's 16-byte header (kernel arguments: no host buffer outlives the call)
 __global__ void k_sh_put_head(uint4 *__restrict__ dst, uint4 v) { *dst = v; }
+// transport slot: 16-byte length header, then the payload's first 16 bytes zeroed (overwritten by the payload copy)
+__global__ void k_sh_slot_head(uint4 *__restrict__ dst, uint4 v) {
+    dst[0] = v;
+    dst[1] = make_uint4(0u, 0u, 0u, 0u);
+}
 
 __global__ void k_sh_lane_out(uint64_t s, uint64_t nl, const uint32_t *__restrict__ lane_asg, const uint8_t *__restrict__ flags,
                               uint32_t *__restrict__ lane_l, uint8_t *__restrict__ color_l) {
@@ -703,6 +708,19 @@ int wg_shard_copy_msg(wg_ctx *c, void *dst) {
     if (!c || (!dst && c->sh.msg_bytes)) return WG_E_INVALID;
     if (c->sh.msg_bytes) WG_HIP(c, hipMemcpyAsync(dst, c->sh.msg.p, c->sh.msg_bytes, hipMemcpyDefault, c->stream));
     WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
+int wg_shard_pack_slot(wg_ctx *c, void *slot, uint64_t cap) {
+    if (!c || !slot || (reinterpret_cast<uintptr_t>(slot) & 15u)) return WG_E_INVALID;
+    if (!c->sh.on || c->sh.step == SH_IDLE) return wg_fail(c, WG_E_STATE, "no sharded call in progress");
+    (void)hipSetDevice(c->device);
+    const uint64_t b = c->sh.msg_bytes;
+    hipLaunchKernelGGL(k_sh_slot_head, dim3(1), dim3(1), 0, c->stream, static_cast<uint4 *>(slot),
+                       make_uint4((uint32_t)b, (uint32_t)(b >> 32), 0u, 0u));
+    if (b && b <= cap)
+        WG_HIP(c, hipMemcpyAsync(static_cast<uint8_t *>(slot) + 16, c->sh.msg.p, b, hipMemcpyDeviceToDevice, c->stream));
+    WG_HIP(c, hipGetLastError());
     return WG_OK;
 }
 

@@ -55,18 +55,24 @@ class ShardComm:
         m = max(n, 16)
         return (m + 15) // 16 * 16
 
-    def allgather(self, nbytes: int, fill, step: int = 0):
+    def allgather(self, nbytes: int, fill, step: int = 0, pack=None):
         """fill(ptr) writes this rank's nbytes-long message to ptr (device or
-        host memory).  Returns (gathered device tensor, payload offset, stride,
-        sizes): rank r's message starts at offset + r * stride."""
+        host memory); or, on a device transport, pack(slot_ptr, cap) writes the
+        whole slot (header + message) in stream order on the current stream.
+        Returns (gathered device tensor, payload offset, stride, sizes): rank
+        r's message starts at offset + r * stride."""
         dev = self.device if self.on_device else torch.device("cpu")
         cap = self.caps.get(step, self.initial_cap)
         while True:
             stride = cap + self.HDR
-            send = torch.zeros(stride, dtype=torch.uint8, device=dev)
-            send[:8].view(torch.int64)[0] = nbytes
-            if nbytes and nbytes <= cap:
-                fill(send.data_ptr() + self.HDR)
+            if self.on_device and pack is not None:
+                send = torch.empty(stride, dtype=torch.uint8, device=dev)
+                pack(send.data_ptr(), cap)
+            else:
+                send = torch.zeros(stride, dtype=torch.uint8, device=dev)
+                send[:8].view(torch.int64)[0] = nbytes
+                if nbytes and nbytes <= cap:
+                    fill(send.data_ptr() + self.HDR)
             out = torch.empty(self.world * stride, dtype=torch.uint8, device=dev)
             if self.on_device:
                 dist.all_gather_into_tensor(out, send, group=self.group)
