@@ -42,7 +42,19 @@ __global__ void k_time_range(const int64_t *__restrict__ t, uint64_t n, unsigned
         lo = a < lo ? a : lo;
         hi = b > hi ? b : hi;
     }
-    if ((threadIdx.x & 63) == 0) { atomicMin(scal, lo); atomicMax(scal + 1, hi); }
+    // one atomic pair per workgroup: every wave's atomics on the same two
+    // words serialise at the memory side
+    __shared__ unsigned long long s_lo[OT / 64], s_hi[OT / 64];
+    if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < OT / 64; w++) {
+            lo = s_lo[w] < lo ? s_lo[w] : lo;
+            hi = s_hi[w] > hi ? s_hi[w] : hi;
+        }
+        atomicMin(scal, lo);
+        atomicMax(scal + 1, hi);
+    }
 }
 
 // key = tmax - time (ascending key = descending time), payload = source row
@@ -62,11 +74,27 @@ __global__ void k_syn_first(const uint32_t *__restrict__ perm, uint64_t nb, cons
                             const int64_t *__restrict__ to, const int64_t *__restrict__ ts, uint32_t ns,
                             unsigned int *__restrict__ first) {
     const uint64_t i = (uint64_t)blockIdx.x * OT + threadIdx.x;
-    if (i >= nb) return;
-    const uint32_t src = perm ? perm[i] : (uint32_t)i;
-    const int64_t t = src < nw ? tw[src] : to[src - nw];
-    for (uint32_t j = 0; j < ns; j++)
-        if (t <= ts[j]) atomicMin(first + j, (unsigned int)i);
+    const bool live = i < nb;
+    int64_t t = 0;
+    if (live) {
+        const uint32_t src = perm ? perm[i] : (uint32_t)i;
+        t = src < nw ? tw[src] : to[src - nw];
+    }
+    // wave minimum first: one atomic per wave and synthetic (the per-row
+    // atomics on ns words serialised at the memory side)
+    for (uint32_t j = 0; j < ns; j++) {
+        const bool q = live && t <= ts[j];
+        if (!__any(q)) continue;
+        uint32_t m = q ? (uint32_t)i : 0xFFFFFFFFu;
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint32_t o = (uint32_t)__shfl_down((int)m, d, 64);
+            m = o < m ? o : m;
+        }
+        // early rows usually qualify: skip the atomic once a smaller row is in
+        if ((threadIdx.x & 63) == 0 && m != 0xFFFFFFFFu &&
+            m < __hip_atomic_load(first + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMin(first + j, m);
+    }
 }
 
 // final position of base row i: i + (synthetics anchored at base rows <= i)
@@ -129,7 +157,7 @@ int wg_order_rows(wg_ctx *c, const int64_t *walk_time, uint64_t n_walk, const in
         unsigned long long *scal = B[6].as<unsigned long long>();
         WG_HIP(c, hipMemsetAsync(scal, 0xFF, 8, s));   // min <- ~0
         WG_HIP(c, hipMemsetAsync(scal + 1, 0, 8, s));  // max <- 0
-        const uint32_t g = std::min<uint32_t>(oblocks(nb), 1024);
+        const uint32_t g = std::min<uint32_t>(oblocks(nb), 512);
         hipLaunchKernelGGL(k_time_range, dim3(g), dim3(OT), 0, s, tw, n_walk, scal);
         if (n_orphans) hipLaunchKernelGGL(k_time_range, dim3(1), dim3(OT), 0, s, to, n_orphans, scal);
         hipLaunchKernelGGL(k_sort_keys, dim3(oblocks(nb)), dim3(OT), 0, s, tw, n_walk, to, nb, (const unsigned long long *)scal,

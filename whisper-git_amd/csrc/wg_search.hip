@@ -64,7 +64,16 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     __shared__ uint32_t s_txt[STAGE_WORDS];
     __shared__ uint8_t s_q[QLDS];
     __shared__ uint16_t s_fail[QLDS];
-    const WgCaseTables T{c_lower, c_cased, c_ign};
+    // the case tables (6.5 KiB) in LDS: the binary searches of non-ASCII code
+    // points are chains of dependent loads, ~5x shorter from LDS than through
+    // the constant/L2 path
+    __shared__ uint32_t s_lower[WG_LOWER_N][3];
+    __shared__ uint32_t s_cased[WG_CASED_N][2];
+    __shared__ uint32_t s_ign[WG_IGNORABLE_N][2];
+    for (uint32_t i = threadIdx.x; i < WG_LOWER_N * 3; i += MT) (&s_lower[0][0])[i] = (&c_lower[0][0])[i];
+    for (uint32_t i = threadIdx.x; i < WG_CASED_N * 2; i += MT) (&s_cased[0][0])[i] = (&c_cased[0][0])[i];
+    for (uint32_t i = threadIdx.x; i < WG_IGNORABLE_N * 2; i += MT) (&s_ign[0][0])[i] = (&c_ign[0][0])[i];
+    const WgCaseTables T{s_lower, s_cased, s_ign};
     const uint64_t r0 = A.rb + (uint64_t)blockIdx.x * MT;
     const uint64_t r1 = r0 + MT < A.re ? r0 + MT : A.re;
     const uint64_t r = r0 + threadIdx.x;
@@ -72,6 +81,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     const bool qlds = A.m <= (uint32_t)QLDS;
     if (qlds)
         for (uint32_t i = threadIdx.x; i < A.m; i += MT) { s_q[i] = A.q[i]; s_fail[i] = A.fail[i]; }
+    __syncthreads();   // tables and query
     WgKmp km{qlds ? s_q : A.q, qlds ? s_fail : A.fail, A.m, 0};
     bool hit = false;
     // summary, then author: stage the workgroup's byte range, match from LDS

@@ -262,7 +262,13 @@ __global__ void __launch_bounds__(QT) k_text_quads(QuadArgs A, float4 *__restric
     for (int k = 0; k < 12; k++) {
         const uint32_t i = k * 64 + lane;
         typedef float v4f __attribute__((ext_vector_type(4)));
-        if (i < cnt * 12) __builtin_nontemporal_store(reinterpret_cast<const v4f *>(st)[i], reinterpret_cast<v4f *>(dst) + i);
+        if (i < cnt * 12) {
+#ifdef WG_PLAIN_STORES
+            reinterpret_cast<v4f *>(dst)[i] = reinterpret_cast<const v4f *>(st)[i];
+#else
+            __builtin_nontemporal_store(reinterpret_cast<const v4f *>(st)[i], reinterpret_cast<v4f *>(dst) + i);
+#endif
+        }
     }
 }
 

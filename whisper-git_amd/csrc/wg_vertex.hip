@@ -305,7 +305,13 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         for (int k = 0; k < 3; k++) {
             const uint32_t i = k * 64 + lane;
             // streaming (non-temporal) stores: the buffer is not re-read by this pass
-            if (i < cnt * 3) __builtin_nontemporal_store(reinterpret_cast<const v4f *>(st)[i], reinterpret_cast<v4f *>(dst) + i);
+            if (i < cnt * 3) {
+#ifdef WG_PLAIN_STORES
+                reinterpret_cast<v4f *>(dst)[i] = reinterpret_cast<const v4f *>(st)[i];
+#else
+                __builtin_nontemporal_store(reinterpret_cast<const v4f *>(st)[i], reinterpret_cast<v4f *>(dst) + i);
+#endif
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
