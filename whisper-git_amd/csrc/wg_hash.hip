@@ -13,7 +13,8 @@
 
 namespace {
 
-__global__ void k_hash_insert(const uint8_t *__restrict__ oid, uint64_t n, unsigned long long *table, uint64_t mask) {
+__global__ void k_hash_insert(const uint8_t *__restrict__ oid, uint64_t n, unsigned long long *table, uint64_t mask,
+                              uint32_t *dup) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Key k = load_key(oid + i * 20);
@@ -29,16 +30,20 @@ __global__ void k_hash_insert(const uint8_t *__restrict__ oid, uint64_t n, unsig
         }
         if ((uint32_t)(cur >> 32) == fp && key_eq(k, oid + (uint64_t)(uint32_t)cur * 20)) {
             atomicMax(&table[h], mine);    // same key: the last row wins (:273-274)
+            atomicAnd(dup, 0u);            // the word after the table starts all ones
             return;
         }
         h = (h + 1) & mask;
     }
 }
 
+// ids all distinct (no insert met its own key): every row is canonical and
+// the second probe pass is skipped
 __global__ void k_canon(const uint8_t *__restrict__ oid, uint64_t n, const unsigned long long *__restrict__ table,
-                        uint64_t mask, uint32_t *__restrict__ canon) {
+                        uint64_t mask, const uint32_t *__restrict__ dup, uint32_t *__restrict__ canon) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (*dup == 0xFFFFFFFFu) { canon[i] = (uint32_t)i; return; }
     int64_t r = hash_find(load_key(oid + i * 20), oid, table, mask);
     canon[i] = r < 0 ? (uint32_t)i : (uint32_t)r;
 }
@@ -57,17 +62,20 @@ int wg_stage_hash_join(wg_ctx *c) {
     uint64_t cap = 1024;
     while (cap < 2 * n) cap <<= 1;
     c->hcap = cap;
-    WG_ALLOC(c, c->hash, cap * 8);
+    WG_ALLOC(c, c->hash, cap * 8 + 64);
     WG_ALLOC(c, c->canon, n * 4 + 4);
     WG_ALLOC(c, c->prow, e * 4 + 4);
     wg_stage_begin(c, "hash_join");
-    WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8, c->stream));
+    // one fill: the table (empty = all ones) and, after it, the duplicate flag (all ones = none)
+    WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8 + 4, c->stream));
+    uint32_t *dup = reinterpret_cast<uint32_t *>(c->hash.as<unsigned long long>() + cap);
     const int T = 256;
     if (n) {
         hipLaunchKernelGGL(k_hash_insert, dim3((n + T - 1) / T), dim3(T), 0, c->stream, c->d_oid, n,
-                           c->hash.as<unsigned long long>(), cap - 1);
+                           c->hash.as<unsigned long long>(), cap - 1, dup);
         hipLaunchKernelGGL(k_canon, dim3((n + T - 1) / T), dim3(T), 0, c->stream, c->d_oid, n,
-                           c->hash.as<const unsigned long long>(), cap - 1, c->canon.as<uint32_t>());
+                           c->hash.as<const unsigned long long>(), cap - 1, dup,
+                           c->canon.as<uint32_t>());
     }
     if (e)
         hipLaunchKernelGGL(k_probe_parents, dim3((e + T - 1) / T), dim3(T), 0, c->stream, c->d_poid, e, c->d_oid,

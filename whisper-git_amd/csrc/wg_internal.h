@@ -142,7 +142,7 @@ struct wg_ctx {
     const uint8_t  *d_poid = nullptr;
     const uint8_t  *d_flags = nullptr;
     // hash join
-    DevBuf hash;            // uint64 [hcap]  (fingerprint<<32 | row)
+    DevBuf hash;            // uint64 [hcap]  (fingerprint<<32 | row), then the duplicate flag word
     uint64_t hcap = 0;
     DevBuf canon;           // uint32 [N]  last row holding the same id
     DevBuf prow;            // int32  [E]  canonical parent row or -1
