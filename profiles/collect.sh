@@ -5,7 +5,10 @@
 # 2. PMC passes for the dominant kernel (k_vtx_tile), one counter group per
 #    run and kernel trace only (MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 #    WRITE_SIZE cannot share a pass; never combined with sys/runtime traces);
-# 3. profiles/summarize.py turns them into <tag>_kernels.md / <tag>_pmc.json.
+# 3. kernel statistics of the full bench (side measurements: glyph quads,
+#    atlas, search, order) and the store-bandwidth ceiling microbenchmark;
+# 4. profiles/summarize.py turns them into <tag>_kernels.md / <tag>_pmc.json /
+#    <tag>_side_kernels.md / <tag>_store_ceiling.jsonl.
 # Everything lands in gpurun_out/prof_<tag>/; the summaries are then copied
 # into profiles/ by hand and committed.
 set -e -o pipefail
@@ -18,4 +21,8 @@ BENCH="$ROOT/bench.py --steps 5 --warmup 2 --no-cpu --no-extras"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH > "$OUT/trace.json" 2> "$OUT/trace.err"
 timeout -k 10 300 rocprofv3 --kernel-include-regex k_vtx_tile --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH > "$OUT/fetch.json" 2> "$OUT/fetch.err"
 timeout -k 10 300 rocprofv3 --kernel-include-regex k_vtx_tile --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $BENCH > "$OUT/write.json" 2> "$OUT/write.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/side" -o run -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu > "$OUT/side.json" 2> "$OUT/side.err"
+if [ -x "$ROOT/profiles/microbench/store_ceiling" ]; then
+    timeout -k 10 120 "$ROOT/profiles/microbench/store_ceiling" > "$OUT/store_ceiling.jsonl" 2> "$OUT/store_ceiling.err"
+fi
 python3 "$ROOT/profiles/summarize.py" "$OUT" "$TAG"

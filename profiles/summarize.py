@@ -123,6 +123,24 @@ def main():
                       f"(x2 gfx950 correction -> {rd / 1e9:.3f} GB read), WRITE_SIZE "
                       f"{pmc['write_size_kib_per_launch']:.0f} KiB ({wr / 1e9:.3f} GB written)"
                       + (f"; algorithmic {pmc['algorithmic_bytes_per_launch'] / 1e9:.3f} GB" if bench else "")]
+    side = os.path.join(src, "side", "run_kernel_stats.csv")
+    if os.path.exists(side):
+        sb = bench_line(os.path.join(src, "side.json"))
+        sl = [f"# {tag}: kernel statistics of the full bench (`bench.py --steps 2 --warmup 1 --no-cpu`, "
+              "side measurements included: glyph quads, font atlas, search, order)", "",
+              "| kernel | calls | avg us |", "|---|---:|---:|"]
+        for r in read_csv(side):
+            sl.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} |")
+        if sb:
+            for k in ("glyph_quads", "font_atlas", "search", "order"):
+                if k in sb:
+                    sl += ["", f"{k}: `{json.dumps(sb[k])}`"]
+        with open(os.path.join(dest, f"{tag}_side_kernels.md"), "w") as f:
+            f.write("\n".join(sl) + "\n")
+    sc = os.path.join(src, "store_ceiling.jsonl")
+    if os.path.exists(sc):
+        with open(sc) as f_in, open(os.path.join(dest, f"{tag}_store_ceiling.jsonl"), "w") as f_out:
+            f_out.write(f_in.read())
     with open(os.path.join(dest, f"{tag}_pmc.json"), "w") as f:
         json.dump(pmc, f, indent=1)
     with open(os.path.join(dest, f"{tag}_kernels.md"), "w") as f:
