@@ -188,6 +188,11 @@ void wg_destroy(wg_ctx *c) {
         for (DevBuf *b : fb) b->release();
     }
     c->tile_first.release();
+    DevBuf *xb[] = {&c->band_prev, &c->geom_diff_first, &c->render_small, &c->render_img, &c->match_flags,
+                    &c->match_q, &c->match_lut2};
+    for (DevBuf *b : xb) b->release();
+    for (int f = 0; f < 2; f++) { c->match_txt[f].release(); c->match_off[f].release(); }
+    for (DevBuf &b : c->ord) b.release();
     for (int i = 0; i < WG_STAGE_MAX; i++) {
         if (c->stages[i].a) (void)hipEventDestroy(c->stages[i].a);
         if (c->stages[i].b) (void)hipEventDestroy(c->stages[i].b);

@@ -10,13 +10,21 @@
 // (:1323-1324).  Non-matching rows are drawn at opacity 0.3 (:1467, 1482):
 // wg_emit_vertices / wg_emit_glyphs scale their alpha by WG_DIM_ALPHA.
 //
-// HBM-bound byte work (≈ the text bytes + 20 B of id per row).  A workgroup
-// owns 256 consecutive rows; their summary bytes (one contiguous range of
-// the CSR) and then their author bytes are staged in LDS with coalesced
-// 4-byte loads, and each thread lowers its row's fields as a byte stream
-// (ASCII inline, other code points through the Unicode tables, Final_Sigma
-// by a scan of the neighbouring code points) into a Knuth-Morris-Pratt matcher of the lowered
-// query (query and failure table in LDS).
+// Per-row byte work (~the text bytes + 20 B of id per row).  A lane owns a
+// row: its summary and then its author bytes are copied into the lane's
+// column of a lane-major LDS block (batched aligned loads; the wave then reads
+// consecutive words at every step), and the lane lowers them as a byte
+// stream (ASCII inline; other code points through the Unicode tables in LDS,
+// the two-byte range by a direct delta table, Final_Sigma by a scan of the
+// neighbouring code points in the column) into the matcher: a 64-bit shift
+// register for queries of <= 8 lowered bytes, else Knuth-Morris-Pratt with
+// the query and failure table in LDS.  VALU-bound: a wave runs its longest
+// row, and a lane at a non-ASCII code point holds the others for the whole
+// decode / lower / encode path (measured: ~0.37 ms per 1M rows with ASCII
+// summaries and the name pool's non-ASCII authors, ~0.6 ms with 15%
+// non-ASCII summary words, whatever the byte path: flat or LDS reads, KMP or
+// shift register).  Rows longer than 128 bytes, or queries longer than the
+// LDS copy, take the generic stream from HBM.
 #include "wg_internal.h"
 #include "wg_unicase.h"
 
@@ -25,7 +33,6 @@
 namespace {
 
 constexpr int MT = 256;                 // rows per workgroup
-constexpr int STAGE_WORDS = 6144;       // 24 KiB of staged text per field
 constexpr int QLDS = 2048;              // query bytes held in LDS
 
 __constant__ uint32_t c_lower[WG_LOWER_N][3] = WG_LOWER_TABLE_INIT;
@@ -41,67 +48,144 @@ struct MatchArgs {
     const uint64_t *sum_off, *auth_off;    // [N+1] global (or rebased host copies)
     const uint8_t *oid, *flags;
     const uint8_t *q;                      // lowered query [m]
+    const int16_t *lut2;                   // [WG_LUT2_N] simple lowercase deltas of U+0080..U+07FF
     const uint16_t *fail;                  // KMP failure table [m]
     uint32_t m;
     uint8_t *out;                          // [re - rb]
     unsigned long long *count;
 };
 
-// stage bytes [b0, b1) of text into LDS words; false if they do not fit
-__device__ bool stage_field(const uint8_t *text, uint64_t b0, uint64_t b1, uint32_t *s_words, uint32_t &shift) {
-    const uint64_t a0 = b0 & ~3ull;
-    const uint64_t nw = (b1 - a0 + 3) >> 2;
-    shift = (uint32_t)(b0 - a0);
-    if (nw > (uint64_t)STAGE_WORDS) return false;
-    // aligned 4-byte loads: every word holds at least one byte of [b0, b1), so
-    // no load leaves the page of a byte the caller owns
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(text + a0);
-    for (uint64_t i = threadIdx.x; i < nw; i += MT) s_words[i] = w[i];
-    return true;
+// Rows of a wave are transposed into LDS lane-major: word j of lane k's row
+// at col[j * 64 + k].  A per-lane walk over its own row then reads
+// consecutive words across the wave at every step — the byte-offset layout
+// put the 64 lanes' reads at effectively random banks (about 5-way
+// conflicts on every read).  Rows longer than TT_W words go through the
+// stream from HBM.
+constexpr uint32_t TT_W = 32;             // words (128 bytes) of a row held in LDS
+
+// a row's bytes in its lane-major LDS column
+struct LdsCol {
+    const uint32_t *col;
+    __device__ uint8_t operator[](uint32_t i) const { return (uint8_t)(col[(i >> 2) * 64] >> (8u * (i & 3u))); }
+};
+
+// the lowered bytes of the non-ASCII unit at g[i] (row g[0, n) in the column), as wg_lower_stream
+__device__ __forceinline__ uint32_t lower_unit(const WgCaseTables &T, const LdsCol &g, uint32_t i, uint32_t n,
+                                               uint32_t *len, uint8_t *buf) {
+    const uint32_t cp = wg_utf8_decode(g, i, n, len);
+    if (cp & 0x80000000u) { buf[0] = (uint8_t)cp; return 1; }
+    if (cp == 0x130) { buf[0] = 'i'; buf[1] = 0xCC; buf[2] = 0x87; return 3; }   // SpecialCasing
+    if (cp == 0x3A3) return wg_utf8_encode(wg_final_sigma(T, g, i, n) ? 0x3C2u : 0x3C3u, buf);
+    return wg_utf8_encode(wg_lower_simple(T, cp), buf);
+}
+
+// row's lowered stream against the query: the last <= 8 bytes in a 64-bit
+// shift register (m <= 8), or KMP with q / fail in LDS
+template <bool SHORT>
+__device__ __forceinline__ bool match_row(const WgCaseTables &T, const uint32_t *col, uint32_t n,
+                                          uint64_t qv, uint64_t qmask, const uint8_t *q, const uint16_t *fail, uint32_t m) {
+    uint64_t win = 0;
+    uint32_t fed = 0, k = 0, widx = 0xFFFFFFFFu, w = 0;
+    auto feed = [&](uint32_t c) -> bool {
+        if (SHORT) {
+            win = (win << 8) | c;
+            fed++;
+            return fed >= m && (win & qmask) == qv;
+        }
+        while (k && q[k] != c) k = fail[k];
+        if (q[k] == c) k++;
+        return k == m;
+    };
+    for (uint32_t i = 0; i < n;) {
+        if ((i >> 2) != widx) { widx = i >> 2; w = col[widx * 64]; }
+        const uint32_t b0 = (w >> (8u * (i & 3u))) & 0xFFu;
+        if (b0 < 0x80u) {
+            if (feed((b0 - 'A' < 26u) ? b0 + 32 : b0)) return true;
+            i++;
+            continue;
+        }
+        uint32_t len;
+        uint8_t buf[4];
+        const uint32_t nb = lower_unit(T, LdsCol{col}, i, n, &len, buf);
+        for (uint32_t j = 0; j < nb; j++)
+            if (feed(buf[j])) return true;
+        i += len;
+    }
+    return false;
 }
 
 __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
-    __shared__ uint32_t s_txt[STAGE_WORDS];
+    __shared__ uint32_t s_tt[MT / 64][TT_W * 64];
     __shared__ uint8_t s_q[QLDS];
     __shared__ uint16_t s_fail[QLDS];
-    // the case tables (6.5 KiB) in LDS: the binary searches of non-ASCII code
-    // points are chains of dependent loads, ~5x shorter from LDS than through
-    // the constant/L2 path
+    // the case tables (6.5 KiB) and the two-byte range's deltas in LDS
     __shared__ uint32_t s_lower[WG_LOWER_N][3];
     __shared__ uint32_t s_cased[WG_CASED_N][2];
     __shared__ uint32_t s_ign[WG_IGNORABLE_N][2];
+    __shared__ int16_t s_lut2[WG_LUT2_N];
     for (uint32_t i = threadIdx.x; i < WG_LOWER_N * 3; i += MT) (&s_lower[0][0])[i] = (&c_lower[0][0])[i];
     for (uint32_t i = threadIdx.x; i < WG_CASED_N * 2; i += MT) (&s_cased[0][0])[i] = (&c_cased[0][0])[i];
     for (uint32_t i = threadIdx.x; i < WG_IGNORABLE_N * 2; i += MT) (&s_ign[0][0])[i] = (&c_ign[0][0])[i];
-    const WgCaseTables T{s_lower, s_cased, s_ign};
-    const uint64_t r0 = A.rb + (uint64_t)blockIdx.x * MT;
-    const uint64_t r1 = r0 + MT < A.re ? r0 + MT : A.re;
-    const uint64_t r = r0 + threadIdx.x;
-    const bool live = r < r1;
-    const bool qlds = A.m <= (uint32_t)QLDS;
+    for (uint32_t i = threadIdx.x; i < WG_LUT2_N / 2; i += MT)
+        reinterpret_cast<uint32_t *>(s_lut2)[i] = reinterpret_cast<const uint32_t *>(A.lut2)[i];
+    const WgCaseTables T{s_lower, s_cased, s_ign, s_lut2};
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t r = A.rb + (uint64_t)blockIdx.x * MT + threadIdx.x;
+    const bool live = r < A.re;
+    const uint32_t m = A.m;
+    const bool qlds = m <= (uint32_t)QLDS;
     if (qlds)
-        for (uint32_t i = threadIdx.x; i < A.m; i += MT) { s_q[i] = A.q[i]; s_fail[i] = A.fail[i]; }
+        for (uint32_t i = threadIdx.x; i < m; i += MT) { s_q[i] = A.q[i]; s_fail[i] = A.fail[i]; }
+    uint64_t qv = 0, qmask = 0;   // short queries: the query's bytes as the shift register holds them
+    if (m <= 8)
+        for (uint32_t i = 0; i < m; i++) { qv = (qv << 8) | A.q[i]; qmask = (qmask << 8) | 0xFFu; }
     __syncthreads();   // tables and query
-    WgKmp km{qlds ? s_q : A.q, qlds ? s_fail : A.fail, A.m, 0};
+    WgKmp km{qlds ? s_q : A.q, qlds ? s_fail : A.fail, m, 0};
     bool hit = false;
-    // summary, then author: stage the workgroup's byte range, match from LDS
+    uint32_t *col = &s_tt[wv][lane];
+    // summary, then author
     for (int f = 0; f < 2; f++) {
         const uint8_t *text = f ? A.auth : A.sum;
         const uint64_t *off = f ? A.auth_off : A.sum_off;
         if (!off) continue;
-        const uint64_t b0 = off[r0], b1 = off[r1];
-        __syncthreads();   // the previous field's readers are done with s_txt
-        uint32_t shift = 0;
-        const bool staged = b1 > b0 && stage_field(text, b0, b1, s_txt, shift);
-        __syncthreads();
-        if (live && !hit) {
-            const uint64_t s = off[r], n = off[r + 1] - s;
-            const uint8_t *p = staged ? reinterpret_cast<const uint8_t *>(s_txt) + shift + (s - b0) : text + s;
-            km.k = 0;
-            if (n) hit = wg_lower_stream(T, p, (uint32_t)n, km);
+        const uint64_t s = live ? off[r] : 0, n = live ? off[r + 1] - s : 0;
+        const uint8_t *g = text + s;
+        const bool lds = n <= TT_W * 4 && qlds;
+        if (lds && !hit) {
+            // this lane's row into its LDS column: 4-byte windows from aligned words
+            // (a second word only when the window reaches into it: no read past the row)
+            // (only aligned words holding a byte of the row are read; the loads of
+            // a batch are all issued before the first is waited for)
+            const uintptr_t base = reinterpret_cast<uintptr_t>(g);
+            const uint32_t sh = (uint32_t)(base & 3u);
+            const uint32_t *aw = reinterpret_cast<const uint32_t *>(base - sh);
+            const uint32_t nw = (uint32_t)((n + 3) >> 2), naw = (uint32_t)((n + sh + 3) >> 2);
+            for (uint32_t j0 = 0; j0 < nw; j0 += 8) {
+                uint32_t x[9];
+#pragma unroll
+                for (int u = 0; u < 9; u++) x[u] = (j0 + u < naw) ? aw[j0 + u] : 0u;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (j0 + u < nw) col[(j0 + u) * 64] = __builtin_amdgcn_alignbyte(x[u + 1], x[u], sh);
+            }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (live && !hit && n) {
+            if (lds) {
+                hit = m <= 8 ? match_row<true>(T, col, (uint32_t)n, qv, qmask, s_q, s_fail, m)
+                             : match_row<false>(T, col, (uint32_t)n, qv, qmask, s_q, s_fail, m);
+            } else {
+                km.k = 0;
+                hit = wg_lower_stream(T, g, (uint32_t)n, km);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the column is rewritten by the next field
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (live && !hit && A.m <= 40) {
+    if (live && !hit && m <= 40) {
         // id hex (lowercase already): short_id contains q (non-synthetic rows), id starts with q
         uint8_t hex[40];
         const uint8_t *id = A.oid + r * 20;
@@ -112,9 +196,9 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         }
         const uint8_t *q = km.q;
         bool pre = true;
-        for (uint32_t i = 0; i < A.m; i++) pre &= hex[i] == q[i];
+        for (uint32_t i = 0; i < m; i++) pre &= hex[i] == q[i];
         hit = pre;
-        if (!hit && A.m <= 7 && !(A.flags[r] & WG_FLAG_SYNTHETIC)) {
+        if (!hit && m <= 7 && !(A.flags[r] & WG_FLAG_SYNTHETIC)) {
             km.k = 0;
             for (int i = 0; i < 7 && !hit; i++) hit = km(hex[i]);
         }
@@ -200,6 +284,14 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
             }
         }
     }
+    if (!c->match_lut2.p) {   // once per context: the two-byte range's deltas, from the host tables
+        const WgCaseTables HT{h_lower, h_cased, h_ign};
+        std::vector<int16_t> lut(WG_LUT2_N);
+        for (uint32_t cp = 0x80; cp < 0x800; cp++) lut[cp - 0x80] = (int16_t)((int32_t)wg_lower_simple(HT, cp) - (int32_t)cp);
+        WG_ALLOC(c, c->match_lut2, WG_LUT2_N * 2 + 16);
+        WG_HIP(c, hipMemcpyAsync(c->match_lut2.p, lut.data(), WG_LUT2_N * 2, hipMemcpyHostToDevice, s));
+        WG_HIP(c, hipStreamSynchronize(s));
+    }
     WG_ALLOC(c, c->match_q, 16 + m * 3 + 16);
     std::vector<uint8_t> &qh = c->match_qhost;
     qh.assign(16 + (size_t)m * 3, 0);
@@ -219,6 +311,7 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     A.fail = reinterpret_cast<const uint16_t *>(c->match_q.as<uint8_t>() + 16);
     A.q = c->match_q.as<uint8_t>() + 16 + (size_t)m * 2;
     A.m = m;
+    A.lut2 = c->match_lut2.as<const int16_t>();
     A.out = c->match_flags.as<uint8_t>();
     A.count = c->match_q.as<unsigned long long>();
     wg_stage_begin(c, "match");

@@ -30,12 +30,16 @@ struct WgCaseTables {
     const uint32_t (*lower)[3];   // WG_LOWER_N    {lo, hi, delta<<2 | step}
     const uint32_t (*cased)[2];   // WG_CASED_N    {lo, hi}
     const uint32_t (*ign)[2];     // WG_IGNORABLE_N
+    const int16_t *lut2 = nullptr;   // optional: simple lowercase delta of U+0080..U+07FF (the two-byte range)
 };
+#define WG_LUT2_N (0x800 - 0x80)
 
 // UTF-8 decode at p[i] (i < n).  Returns the code point and its length, or
 // 0x80000000 | byte with length 1 for a byte that starts no well-formed sequence.
-WG_HD inline uint32_t wg_utf8_decode(const uint8_t *p, uint32_t i, uint32_t n, uint32_t *len) {
-    const uint32_t b0 = p[i];
+// P: any byte source with p[i] (a pointer, or a strided LDS column)
+template <class P>
+WG_HD inline uint32_t wg_utf8_decode(const P &p, uint32_t i, uint32_t n, uint32_t *len) {
+    const uint32_t b0 = (uint8_t)p[i];
     *len = 1;
     if (b0 < 0x80) return b0;
     uint32_t need, cp, lo = 0x80, hi = 0xBF;
@@ -53,7 +57,7 @@ WG_HD inline uint32_t wg_utf8_decode(const uint8_t *p, uint32_t i, uint32_t n, u
     }
     if (i + need >= n) return 0x80000000u | b0;   // truncated
     for (uint32_t k = 1; k <= need; k++) {
-        const uint32_t b = p[i + k];
+        const uint32_t b = (uint8_t)p[i + k];
         if (b < (k == 1 ? lo : 0x80u) || b > (k == 1 ? hi : 0xBFu)) return 0x80000000u | b0;
         cp = (cp << 6) | (b & 0x3F);
     }
@@ -88,6 +92,7 @@ WG_HD inline int wg_range_find(const uint32_t (*tab)[W], int n, uint32_t cp) {
 
 WG_HD inline uint32_t wg_lower_simple(const WgCaseTables &T, uint32_t cp) {
     if (cp < 0x80) return (cp - 'A' < 26u) ? cp + 32 : cp;
+    if (T.lut2 && cp < 0x800) return (uint32_t)((int32_t)cp + T.lut2[cp - 0x80]);
     const int r = wg_range_find<3>(T.lower, WG_LOWER_N, cp);
     if (r < 0 || cp > T.lower[r][1]) return cp;
     const uint32_t step = T.lower[r][2] & 3u;
@@ -111,18 +116,20 @@ WG_HD inline bool wg_is_ignorable(const WgCaseTables &T, uint32_t cp) {
 }
 
 // the code point that ends at byte i > 0 (a code point boundary) and its start
-WG_HD inline uint32_t wg_utf8_prev(const uint8_t *p, uint32_t i, uint32_t n, uint32_t *start) {
+template <class P>
+WG_HD inline uint32_t wg_utf8_prev(const P &p, uint32_t i, uint32_t n, uint32_t *start) {
     uint32_t j = i - 1;
-    while (j > 0 && i - j < 4 && (p[j] & 0xC0) == 0x80) j--;
+    while (j > 0 && i - j < 4 && ((uint8_t)p[j] & 0xC0) == 0x80) j--;
     uint32_t len;
     const uint32_t cp = wg_utf8_decode(p, j, n, &len);
     if (!(cp & 0x80000000u) && j + len == i) { *start = j; return cp; }
     *start = i - 1;   // byte i-1 is not the end of a well-formed sequence: it stands alone
-    return 0x80000000u | p[i - 1];
+    return 0x80000000u | (uint8_t)p[i - 1];
 }
 
 // Final_Sigma for the U+03A3 at byte i (length 2) of p[0, n)
-WG_HD inline bool wg_final_sigma(const WgCaseTables &T, const uint8_t *p, uint32_t i, uint32_t n) {
+template <class P>
+WG_HD inline bool wg_final_sigma(const WgCaseTables &T, const P &p, uint32_t i, uint32_t n) {
     // before: the last non-ignorable code point in [0, i) is cased
     bool before = false;
     for (uint32_t j = i; j > 0;) {
