@@ -222,8 +222,44 @@ def extra_measurements(eng, dag, dev, torch, r0, r1, args, log):
         order["cpu_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
         order["cpu_kind"] = "port (Python stable sort + list inserts, 1 thread)"
     out["order"] = order
+    out["baseline_configs"] = config_rates(eng, dev, torch, args)
     log("extras:", json.dumps(out))
     return out
+
+
+def config_rates(eng, dev, torch, args):
+    """The same step (build + banded geometry + emission, inputs in HBM) on
+    BASELINE.json's other single-GPU DAG configs: C3 (100k commits, 1.3
+    parents on average) and C4 (Linux-kernel-shaped 1.3M commits; its vertex
+    buffer checksum equals the CPU oracle's in tests/test_gpu_parity.py)."""
+    from wgraph import abi, synth
+    res = {}
+    for cid, kind, n in (("C3", "random13", 100_000), ("C4", "linux", 1_300_000)):
+        d = synth.generate(kind, n)
+        keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                       d.parent_oid.reshape(-1), d.flags, d.band)]
+        c = abi.Commits()
+        c.n_commits, c.n_parents = d.n, d.e
+        c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
+        c.residency = abi.WG_DEVICE
+
+        def step():
+            eng.build(commits=c)
+            eng.row_geometry(device_ptr=keep[5].data_ptr())
+            eng.emit_vertices(0, d.n, selected=7)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3 / args.steps
+        res[cid] = {"workload": f"{kind} synthetic DAG, {n} commits", "ms_per_step": round(ms, 4),
+                    "rows_per_s": round(n / ms * 1e3, 1), "vertices": int(eng.vertex_summary().n_vertices),
+                    "max_lane": int(eng.layout_summary().max_lane)}
+        del keep
+    return res
 
 
 def pmc_traffic(args, workload):

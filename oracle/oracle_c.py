@@ -52,6 +52,8 @@ def lib():
         L.wgo_free.argtypes = [ctypes.c_void_p]
         L.wgo_vertex_checksum.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.wgo_vertex_checksum.restype = ctypes.c_uint64
+        L.wgo_vertex_checksum_at.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
+        L.wgo_vertex_checksum_at.restype = ctypes.c_uint64
         for f in ("wgo_cubic_y_at", "wgo_cubic_t_at_y"):
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_float]
             getattr(L, f).restype = ctypes.c_float
@@ -161,9 +163,11 @@ def dim_rows(v, off, row_begin, match, match_rb, alpha_field):
                 seg[alpha_field] = seg[alpha_field] * np.float32(0.3)
 
 
-def vertex_checksum(v: np.ndarray) -> int:
+def vertex_checksum(v: np.ndarray, first_vertex: int = 0) -> int:
+    """Checksum of v as the piece of a buffer starting at vertex first_vertex
+    (pieces of one buffer add up, mod 2^64, to the whole buffer's checksum)."""
     v = np.ascontiguousarray(v)
-    return int(lib().wgo_vertex_checksum(v.ctypes.data, v.shape[0]))
+    return int(lib().wgo_vertex_checksum_at(v.ctypes.data, v.shape[0], first_vertex))
 
 
 def cubic_y_at(p8, t):

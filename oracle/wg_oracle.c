@@ -571,13 +571,18 @@ void wgo_free(void *p) { free(p); }
 
 /* Order-sensitive 64-bit checksum of a vertex buffer (shared definition
  * with the engine's on-device checksum).                   */
-uint64_t wgo_vertex_checksum(const wg_vertex *v, uint64_t n) {
+uint64_t wgo_vertex_checksum_at(const wg_vertex *v, uint64_t n, uint64_t first_vertex) {
+    /* the sum over words is additive: a buffer checksummed in pieces, each
+     * piece at its position (first_vertex) in the whole buffer            */
     const uint32_t *w = (const uint32_t *)v;
     uint64_t acc = 0;
-    for (uint64_t i = 0; i < n * 6; i++) {
-        uint64_t x = ((uint64_t)w[i] << 32) ^ (i * 0x9E3779B97F4A7C15ull);
+    for (uint64_t j = 0; j < n * 6; j++) {
+        const uint64_t i = first_vertex * 6 + j;
+        uint64_t x = ((uint64_t)w[j] << 32) ^ (i * 0x9E3779B97F4A7C15ull);
         x ^= x >> 33; x *= 0xFF51AFD7ED558CCDull; x ^= x >> 33; x *= 0xC4CEB9FE1A85EC53ull; x ^= x >> 33;
         acc += x;
     }
     return acc;
 }
+
+uint64_t wgo_vertex_checksum(const wg_vertex *v, uint64_t n) { return wgo_vertex_checksum_at(v, n, 0); }

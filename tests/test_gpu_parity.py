@@ -189,6 +189,36 @@ def test_row_top_exact_beyond_2_24(engine):
     assert engine.geometry_summary().scan_path == 0
 
 
+@pytest.mark.parametrize("kind,n", [("random13", 100_000), ("linux", 1_300_000)], ids=["C3", "C4"])
+def test_baseline_configs_vertex_checksum(engine, kind, n):
+    """BASELINE configs C3 (100k DAG, 1.3 parents per commit) and C4 (the
+    Linux-kernel-shaped 1.3M-commit DAG) on one GPU, full path (build + banded
+    geometry + emission): the whole vertex buffer checksummed against the CPU
+    oracle's (emitted and checksummed in pieces of 100k rows, each at its
+    offset)."""
+    from oracle import oracle_c
+    d = synth.generate(kind, n)
+    o = oracle_c.OracleLayout(d)
+    try:
+        engine.build(d)
+        engine.row_geometry(d.band)
+        sel = n // 2 + 1
+        engine.emit_vertices(0, d.n, selected=sel)
+        vs = engine.vertex_summary()
+        o.row_geometry(d.band)
+        total, first = 0, 0
+        for a in range(0, d.n, 100_000):
+            b = min(d.n, a + 100_000)
+            ov, _ = o.emit_vertices(a, b, selected=sel)
+            total = (total + oracle_c.vertex_checksum(ov, first)) & 0xFFFFFFFFFFFFFFFF
+            first += len(ov)
+            del ov
+        assert vs.n_vertices == first
+        assert vs.checksum == total
+    finally:
+        o.close()
+
+
 def test_bands_with_fractional_and_negative_values(engine):
     """Non-integer bands keep the transducer path exact; a negative band forces
     the serial path, which must also be exact."""
