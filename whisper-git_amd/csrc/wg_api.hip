@@ -91,11 +91,12 @@ int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out) {
     return wg_fetch_n(c, (int)items.size(), items.begin(), out);
 }
 
-// mapped pinned words: [0, FETCH_MAX) for wg_fetch, [FETCH_MAX, 2 FETCH_MAX) for wg_fetch_begin
+// mapped pinned words: [0, FETCH_MAX) for wg_fetch, [FETCH_MAX, 2 FETCH_MAX) for wg_fetch_begin,
+// [2 FETCH_MAX, 3 FETCH_MAX) for wg_fetch_defer
 static int fetch_launch(wg_ctx *c, int n, const WgFetch *items, uint64_t slot0) {
     if (n < 0 || n > FETCH_MAX) return wg_fail(c, WG_E_INVALID, "wg_fetch: too many items");
     if (!c->h_fetch) {
-        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, 2 * FETCH_MAX * sizeof(uint64_t), hipHostMallocMapped));
+        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, 3 * FETCH_MAX * sizeof(uint64_t), hipHostMallocMapped));
         WG_HIP(c, hipHostGetDevicePointer((void **)&c->d_fetch, c->h_fetch, 0));
     }
     FetchArgs a{};
@@ -126,6 +127,26 @@ int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items) {
     if (!c->ev_fetch) WG_HIP(c, hipEventCreateWithFlags(&c->ev_fetch, hipEventDisableTiming));
     WG_HIP(c, hipEventRecord(c->ev_fetch, c->stream));
     c->fetch_pending = (int)items.size();
+    return WG_OK;
+}
+
+// Deferred read: the words are copied in stream order now and read by the
+// host later (wg_fetch_deferred), typically after a synchronisation the
+// stage needed anyway — a value the host needs only later costs no stall.
+int wg_fetch_defer(wg_ctx *c, std::initializer_list<WgFetch> items) {
+    if (const int rc = fetch_launch(c, (int)items.size(), items.begin(), 2 * FETCH_MAX)) return rc;
+    if (!c->ev_defer) WG_HIP(c, hipEventCreateWithFlags(&c->ev_defer, hipEventDisableTiming));
+    WG_HIP(c, hipEventRecord(c->ev_defer, c->stream));
+    c->defer_pending = (int)items.size();
+    return WG_OK;
+}
+
+int wg_fetch_deferred(wg_ctx *c, uint64_t *out) {
+    if (!c->defer_pending) return wg_fail(c, WG_E_STATE, "wg_fetch_deferred: nothing deferred");
+    const int n = c->defer_pending;
+    c->defer_pending = 0;
+    WG_HIP(c, hipEventSynchronize(c->ev_defer));
+    for (int i = 0; i < n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[2 * FETCH_MAX + i];
     return WG_OK;
 }
 
@@ -203,6 +224,7 @@ void wg_destroy(wg_ctx *c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->ev_fetch) (void)hipEventDestroy(c->ev_fetch);
+    if (c->ev_defer) (void)hipEventDestroy(c->ev_defer);
     delete c;
 }
 

@@ -55,6 +55,17 @@ __global__ void k_probe_parents(const uint8_t *__restrict__ poid, uint64_t e, co
     prow[k] = (int32_t)hash_find(load_key(poid + k * 20), oid, table, mask);
 }
 
+// edges per row = parents found in the list (:306-311); lane-independent, so
+// the edge offsets and the total are ready before the lanes are
+__global__ void k_edge_cnt(uint64_t n, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow,
+                           uint32_t *__restrict__ edge_cnt) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t cnt = 0;
+    for (uint32_t k = poff[i]; k < poff[i + 1]; k++) cnt += prow[k] >= 0;
+    edge_cnt[i] = cnt;
+}
+
 }  // namespace
 
 int wg_stage_hash_join(wg_ctx *c) {
@@ -80,6 +91,15 @@ int wg_stage_hash_join(wg_ctx *c) {
     if (e)
         hipLaunchKernelGGL(k_probe_parents, dim3((e + T - 1) / T), dim3(T), 0, c->stream, c->d_poid, e, c->d_oid,
                            c->hash.as<const unsigned long long>(), cap - 1, c->prow.as<int32_t>());
+    WG_ALLOC(c, c->edge_cnt, (n + 1) * 4);
+    { const int _sr = wg_scan_reserve(c, n + 1); if (_sr != WG_OK) return _sr; }
+    if (n) {
+        hipLaunchKernelGGL(k_edge_cnt, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->d_poff,
+                           c->prow.as<const int32_t>(), c->edge_cnt.as<uint32_t>());
+        WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), n, c->scan_tmp.p, c->stream));
+        // read by wg_stage_edges after the lane stage's own synchronisation
+        if (const int rc = wg_fetch_defer(c, {{c->edge_cnt.as<uint32_t>() + n, false}})) return rc;
+    }
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;

@@ -248,6 +248,8 @@ struct wg_ctx {
     uint64_t  *h_fetch = nullptr;   // mapped pinned host memory for wg_fetch / wg_fetch_begin
     hipEvent_t ev_fetch = nullptr;  // completion of the pending wg_fetch_begin
     int        fetch_pending = 0;   // words of the pending wg_fetch_begin
+    hipEvent_t ev_defer = nullptr;  // completion of the last wg_fetch_defer
+    int        defer_pending = 0;   // words of the last wg_fetch_defer
     uint64_t  *d_fetch = nullptr;
 };
 
@@ -261,6 +263,8 @@ int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out);   // n <=
 // (one pending at a time)
 int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items);
 int wg_fetch_end(wg_ctx *c, uint64_t *out);
+int wg_fetch_defer(wg_ctx *c, std::initializer_list<WgFetch> items);
+int wg_fetch_deferred(wg_ctx *c, uint64_t *out);
 
 // error helpers -------------------------------------------------------------
 int wg_fail(wg_ctx *c, int code, const char *fmt, ...);

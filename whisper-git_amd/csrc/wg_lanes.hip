@@ -149,17 +149,13 @@ __global__ void __launch_bounds__(64) k_lanes_general(uint64_t n, const uint32_t
 // layouts.get(id) per row + colour rule (:278-283, history_view :1363-1367)
 __global__ void k_lane_out(uint64_t n, const uint32_t *__restrict__ canon, const uint32_t *__restrict__ lane_asg,
                            const uint8_t *__restrict__ flags, uint32_t *__restrict__ lane_out,
-                           uint8_t *__restrict__ color_out, uint32_t *__restrict__ edge_cnt,
-                           const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow) {
+                           uint8_t *__restrict__ color_out) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t ci = canon[i];
     const uint32_t l = lane_asg[ci];
     lane_out[i] = l;
     color_out[i] = (flags[ci] & WG_FLAG_ORPHAN) ? (uint8_t)WG_COLOR_ORPHAN : (uint8_t)(l % 6u);
-    uint32_t cnt = 0;
-    for (uint32_t k = poff[i]; k < poff[i + 1]; k++) cnt += prow[k] >= 0;
-    edge_cnt[i] = cnt;
 }
 
 // edge list (:301-320): child_row asc, then parent order
@@ -240,25 +236,21 @@ int wg_stage_edges(wg_ctx *c) {
     const uint64_t n = c->n;
     WG_ALLOC(c, c->lane_out, n * 4 + 4);
     WG_ALLOC(c, c->color_out, n + 4);
-    WG_ALLOC(c, c->edge_cnt, (n + 1) * 4);
-    { const int _sr = wg_scan_reserve(c, n + 1); if (_sr != WG_OK) return _sr; }
     c->n_edges = 0;
     if (n == 0) {
+        WG_ALLOC(c, c->edge_cnt, 16);
         WG_HIP(c, hipMemsetAsync(c->edge_cnt.p, 0, 4, c->stream));
         return WG_OK;
     }
     wg_stage_begin(c, "edges");
     const int T = 256;
     hipLaunchKernelGGL(k_lane_out, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->canon.as<const uint32_t>(),
-                       c->lane_asg.as<const uint32_t>(), c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>(),
-                       c->edge_cnt.as<uint32_t>(), c->d_poff, c->prow.as<const int32_t>());
+                       c->lane_asg.as<const uint32_t>(), c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>());
     WG_HIP(c, hipGetLastError());
-    WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), n, c->scan_tmp.p, c->stream));
+    // edge offsets: scanned after the hash join (wg_stage_hash_join); the
+    // total was copied out then and the lane stage has synchronised since
     uint64_t ne = 0;
-    {
-        const int rc = wg_fetch(c, {{c->edge_cnt.as<uint32_t>() + n, false}}, &ne);
-        if (rc != WG_OK) return rc;
-    }
+    if (const int rc = wg_fetch_deferred(c, &ne)) return rc;
     c->n_edges = ne;
     WG_ALLOC(c, c->edges, (uint64_t)ne * sizeof(wg_edge) + 16);
     hipLaunchKernelGGL(k_edges, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->edge_cnt.as<const uint32_t>(),
