@@ -601,11 +601,9 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
                        c->g_node_y.as<float>(), c->rowflags.as<uint8_t>());
     if (ne)
         hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntB, cntT, cntF, cntC, cntCend);
-    WG_HIP(c, wg_exclusive_scan_u32(cntF, cntF, n + 1, c->scan_tmp.p, s));
-    WG_HIP(c, wg_exclusive_scan_u32(cntC, cntC, n + 1, c->scan_tmp.p, s));
+    WG_HIP(c, wg_exclusive_scan2_u32(cntF, cntF, cntC, cntC, n + 1, c->scan_tmp.p, s));
     hipLaunchKernelGGL(k_row_counts, dim3(blocks(n)), dim3(T), 0, s, n, cntF, cntC, cntT, cntB, cntCend, zflags, voff, soff);
-    WG_HIP(c, wg_exclusive_scan_u32(voff, voff, n, c->scan_tmp.p, s));
-    WG_HIP(c, wg_exclusive_scan_u32(soff, soff, n, c->scan_tmp.p, s));
+    WG_HIP(c, wg_exclusive_scan2_u32(voff, voff, soff, soff, n, c->scan_tmp.p, s));
     // carry-in registration
     WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
     if (ne) hipLaunchKernelGGL(k_carry_diff, dim3(blocks(ne)), dim3(T), 0, s, ne, E, carry_cnt);

@@ -293,6 +293,9 @@ void wg_stage_end(wg_ctx *c);
 size_t wg_scan_tmp_bytes(uint64_t n);
 int wg_scan_reserve(wg_ctx *c, uint64_t n);   // grow c->scan_tmp for scans of up to n elements
 hipError_t wg_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, void *tmp, hipStream_t s);
+// two independent arrays of the same length scanned in the same launches
+hipError_t wg_exclusive_scan2_u32(const uint32_t *in0, uint32_t *out0, const uint32_t *in1, uint32_t *out1, uint64_t n,
+                                  void *tmp, hipStream_t s);
 hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, hipStream_t s);
 
 // stages -------------------------------------------------------------------------

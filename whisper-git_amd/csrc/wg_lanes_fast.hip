@@ -370,8 +370,8 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R) {
         hipLaunchKernelGGL(k_lf_xfirst, dim3(blocks(R.xown_end - R.xown_begin)), dim3(T), 0, s, R);
     if (n) hipLaunchKernelGGL(k_lf_rows, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<const unsigned long long>(),
                               fpc.as<const uint32_t>(), winfo.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>());
-    WG_HIP(c, wg_exclusive_scan_u32(ev_off.as<uint32_t>(), ev_off.as<uint32_t>(), n, c->scan_tmp.p, s));
-    WG_HIP(c, wg_exclusive_scan_u32(aux_off.as<uint32_t>(), aux_off.as<uint32_t>(), n, c->scan_tmp.p, s));
+    WG_HIP(c, wg_exclusive_scan2_u32(ev_off.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>(),
+                                     aux_off.as<uint32_t>(), n, c->scan_tmp.p, s));
     // read back while the chain phase runs (wg_lf_refs_end)
     const int rc = wg_fetch_begin(c, {{flags.p, false}, {ev_off.as<uint32_t>() + n, false}, {aux_off.as<uint32_t>() + n, false}});
     wg_stage_end(c);

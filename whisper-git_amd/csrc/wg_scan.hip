@@ -103,6 +103,47 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_down2(const TI *in, TO *o
     if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
 }
 
+// two arrays of the same length in the same two launches (blockIdx.y picks the array)
+struct Pair32 { const uint32_t *in[2]; uint32_t *out[2]; uint32_t *bsum[2]; };
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan2_reduce(Pair32 P, uint64_t n) {
+    const uint32_t *in = P.in[blockIdx.y];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++)
+        if (base + k < n) s += in[base + k];
+    uint32_t tot;
+    (void)block_excl_scan<uint32_t>(s, tot);
+    if (threadIdx.x == 0) P.bsum[blockIdx.y][blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan2_down(Pair32 P, uint64_t n) {
+    const uint32_t *in = P.in[blockIdx.y];
+    uint32_t *out = P.out[blockIdx.y];
+    const uint32_t *bsum = P.bsum[blockIdx.y];
+    uint32_t pre = 0;
+    for (uint64_t b = threadIdx.x; b < blockIdx.x; b += SCAN_THREADS) pre += bsum[b];
+    uint32_t ptot;
+    (void)block_excl_scan<uint32_t>(pre, ptot);
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        v[k] = (base + k < n) ? in[base + k] : 0u;
+        s += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan<uint32_t>(s, tot) + ptot;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
+    }
+    if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
+}
+
 uint64_t nblocks(uint64_t n) { return n == 0 ? 1 : (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 template <class TO>
@@ -141,6 +182,22 @@ hipError_t wg_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, 
 }
 hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, hipStream_t s) {
     return scan_rec<uint64_t, uint64_t>(in, out, n, (char *)tmp, s);
+}
+
+hipError_t wg_exclusive_scan2_u32(const uint32_t *in0, uint32_t *out0, const uint32_t *in1, uint32_t *out1, uint64_t n,
+                                  void *tmp, hipStream_t s) {
+    const uint64_t nb = nblocks(n);
+    if (nb <= 1 || nb > SCAN_TILE) {   // one tile, or more tiles than one block reduces: one scan at a time
+        hipError_t e = scan_rec<uint32_t, uint32_t>(in0, out0, n, (char *)tmp, s);
+        return e != hipSuccess ? e : scan_rec<uint32_t, uint32_t>(in1, out1, n, (char *)tmp, s);
+    }
+    Pair32 P;
+    P.in[0] = in0; P.in[1] = in1; P.out[0] = out0; P.out[1] = out1;
+    P.bsum[0] = reinterpret_cast<uint32_t *>(tmp);
+    P.bsum[1] = P.bsum[0] + ((nb + 63) & ~63ull);   // wg_scan_tmp_bytes holds (nb + 1) u64 >= 2 * (nb + 64) u32
+    hipLaunchKernelGGL(k_scan2_reduce, dim3((uint32_t)nb, 2), dim3(SCAN_THREADS), 0, s, P, n);
+    hipLaunchKernelGGL(k_scan2_down, dim3((uint32_t)nb, 2), dim3(SCAN_THREADS), 0, s, P, n);
+    return hipGetLastError();
 }
 
 int wg_scan_reserve(wg_ctx *c, uint64_t n) {
