@@ -337,6 +337,17 @@ __global__ void k_lf_lanes(uint64_t nl, const uint32_t *__restrict__ sp, const u
     lane[j] = slot_of[sp[j] & ~WG_TOK_EV];
 }
 
+// the lane stage's initial state in one launch (instead of four fills):
+// first references "none", per-row counters and the chain fill counters 0,
+// the flag words 0
+__global__ void k_lf_clear(uint64_t n, unsigned long long *__restrict__ first_ref, uint32_t *__restrict__ fpc,
+                           uint32_t *__restrict__ ch_fill, uint32_t *__restrict__ flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) first_ref[i] = REF_NONE;
+    if (i < n + 2) { fpc[i] = 0u; ch_fill[i] = 0u; }
+    if (i < 16) flags[i] = 0u;
+}
+
 }  // namespace
 
 // workspace slots in c->lf
@@ -356,11 +367,12 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R) {
     WG_ALLOC(c, ev_off, (n + 2) * 4);
     WG_ALLOC(c, aux_off, (n + 2) * 4);
     WG_ALLOC(c, flags, 64);
+    DevBuf &ch_fill = c->lf[LF_CHFILL];
+    WG_ALLOC(c, ch_fill, (n + 2) * 4);
     { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "lf_refs");
-    WG_HIP(c, hipMemsetAsync(first_ref.p, 0xFF, n * 8, s));
-    WG_HIP(c, hipMemsetAsync(fpc.p, 0, (n + 2) * 4, s));
-    WG_HIP(c, hipMemsetAsync(flags.p, 0, 64, s));
+    hipLaunchKernelGGL(k_lf_clear, dim3(blocks(n + 16)), dim3(T), 0, s, n, first_ref.as<unsigned long long>(),
+                       fpc.as<uint32_t>(), ch_fill.as<uint32_t>(), flags.as<uint32_t>());
     if (n) hipLaunchKernelGGL(k_lf_refs, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<unsigned long long>(),
                               fpc.as<uint32_t>(), flags.as<uint32_t>());
     if (R.xin_end)
@@ -402,7 +414,7 @@ int wg_lf_chain(wg_ctx *c, const LfRange &R) {
     WG_ALLOC(c, spA, n * 4 + 4);
     WG_ALLOC(c, spB, n * 4 + 4);
     wg_stage_begin(c, "lf_chain");
-    WG_HIP(c, hipMemsetAsync(ch_fill.p, 0, (n + 2) * 4, s));
+    // ch_fill was cleared with the stage's other state (k_lf_clear)
     if (n) hipLaunchKernelGGL(k_lf_secev, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<const unsigned long long>(),
                               winfo.as<const uint32_t>(), ev_off.as<const uint32_t>(), secev.as<uint32_t>());
     if (R.xin_end)
