@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (host-input rate, glyph quads, font atlas)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (host rehearsal)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--all-stage-events", action="store_true",
+                    help="record every stage's HIP events inside the timed region (default: only the emission "
+                         "kernel's, for the roofline; the stage breakdown comes from a separate pass)")
     return ap.parse_args()
 
 
@@ -342,8 +345,12 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # per-stage HIP events on the engine's stream, logged across the whole timed
-    # region and read back only after it (no per-step readback)
+    # HIP events on the engine's stream, logged across the whole timed region
+    # and read back only after it (no per-step readback): the emission kernel's
+    # (the roofline's launch duration) and, with --all-stage-events, every
+    # stage's; the stage breakdown is otherwise a separate pass below
+    lib_opt = wgraph.lib().wg_set_option
+    eng._check(lib_opt(eng._ctx, 4, 0 if args.all_stage_events else 1))   # WG_OPT_TIMING_EMIT_ONLY
     eng.enable_timing(True, reserve=64 * (args.steps + 1))
 
     # timed region: barrier + sync on both sides, exactly K steps
@@ -366,6 +373,17 @@ def main():
         stage_ms[name] = stage_ms.get(name, 0.0) + ms / args.steps
         launches.setdefault(name, []).append(ms)
     eng.enable_timing(False)
+    if not args.all_stage_events:   # stage breakdown: a few more steps with every stage's events
+        eng._check(lib_opt(eng._ctx, 4, 0))
+        nb = min(args.steps, 5)
+        eng.enable_timing(True, reserve=64 * (nb + 1))
+        for _ in range(nb):
+            step()
+        torch.cuda.synchronize()
+        stage_ms = {}
+        for name, ms in eng.timings():
+            stage_ms[name] = stage_ms.get(name, 0.0) + ms / nb
+        eng.enable_timing(False)
 
     ms_per_step = elapsed * 1e3 / args.steps
     rows_done = rows_total  # all ranks together emit every row once per step

@@ -196,6 +196,10 @@ int         wg_synchronize(wg_ctx *ctx);
  * registers (0..512, default 512); wider chunks use the LDS sweep.  Affects
  * speed only, never results. */
 #define WG_OPT_SWEEP_REG 3
+/* WG_OPT_TIMING_EMIT_ONLY: 1 = the stage-timing log (wg_enable_timing) keeps
+ * only the vertex-emission stage ("vtx_emit"), so a timed loop carries two
+ * events per step instead of two per stage; 0 = every stage (default). */
+#define WG_OPT_TIMING_EMIT_ONLY 4
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------

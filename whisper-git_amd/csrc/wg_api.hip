@@ -24,7 +24,11 @@ int wg_fail(wg_ctx *c, int code, const char *fmt, ...) {
 // Stages nest: begin takes the next slot and pushes it, end closes the top.
 void wg_stage_begin(wg_ctx *c, const char *name) {
     if (!c->timing) return;
-    if (c->n_stages >= WG_STAGE_MAX || c->stage_depth >= 8) { c->stage_stack[c->stage_depth++ & 7] = -1; return; }
+    if (c->n_stages >= WG_STAGE_MAX || c->stage_depth >= 8 ||
+        (c->timing_emit_only && std::strcmp(name, "vtx_emit") != 0)) {
+        c->stage_stack[c->stage_depth++ & 7] = -1;
+        return;
+    }
     StageTimer &t = c->stages[c->n_stages];
     if (!t.a) { (void)hipEventCreate(&t.a); (void)hipEventCreate(&t.b); }
     t.name = name;
@@ -253,6 +257,7 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         if (value < 64 || value > (1 << 20) || (value & 63)) return wg_fail(c, WG_E_INVALID, "replay chunk must be a multiple of 64");
         c->replay_chunk = (uint32_t)value;
         return WG_OK;
+    case WG_OPT_TIMING_EMIT_ONLY: c->timing_emit_only = value != 0; return WG_OK;
     case WG_OPT_SWEEP_REG:
         if (value < 0 || value > 512) return wg_fail(c, WG_E_INVALID, "sweep register capacity must be 0..512");
         c->sweep_reg_cap = (uint32_t)value;

@@ -240,6 +240,7 @@ struct wg_ctx {
     uint64_t ord_n = 0;
     // ---- timing ----------------------------------------------------------------------
     bool       timing = false;
+    bool       timing_emit_only = false;   // WG_OPT_TIMING_EMIT_ONLY
     StageTimer stages[WG_STAGE_MAX];
     int        n_stages = 0;
     int        stage_stack[8] = {0};
