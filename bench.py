@@ -225,9 +225,43 @@ def extra_measurements(eng, dag, dev, torch, r0, r1, args, log):
         order["cpu_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
         order["cpu_kind"] = "port (Python stable sort + list inserts, 1 thread)"
     out["order"] = order
+    out["frames"] = frame_rates(eng, dag, dev, torch, args)
     out["baseline_configs"] = config_rates(eng, dev, torch, args)
     log("extras:", json.dumps(out))
     return out
+
+
+def frame_rates(eng, dag, dev, torch, args):
+    """Per-frame geometry (history_view recomputes
+    row_geometry_with_bands every frame, commit_graph.rs:1419-1421) on the
+    bench list: bands unchanged (one compare pass), one band changed at 90%
+    of the list (rows and curves from there on), one band changed at row 0
+    (the whole pass); device-resident bands, ms per frame."""
+    from wgraph import abi
+    keep = [torch.from_numpy(a).to(dev) for a in (dag.oid.reshape(-1), dag.time, dag.parent_off.view(np.int32),
+                                                   dag.parent_oid.reshape(-1), dag.flags)]
+    c = abi.Commits()
+    c.n_commits, c.n_parents = dag.n, dag.e
+    c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep)
+    c.residency = abi.WG_DEVICE
+    eng.build(commits=c)
+    band = torch.from_numpy(dag.band.copy()).to(dev)
+    eng.row_geometry(device_ptr=band.data_ptr())
+    res = {}
+    for name, row in (("unchanged", None), ("changed_at_90pct", int(dag.n * 0.9)), ("changed_at_row0", 0)):
+        times = []
+        for k in range(args.steps):
+            if row is not None:
+                band[row] = float(30.0 if k % 2 == 0 else 0.0)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.row_geometry(device_ptr=band.data_ptr())
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        res[name + "_ms"] = round(1e3 * float(np.median(times)), 4)
+    res["rows"] = int(dag.n)
+    del keep
+    return res
 
 
 def config_rates(eng, dev, torch, args):

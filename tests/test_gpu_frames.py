@@ -51,3 +51,31 @@ def test_frames_reuse_and_recompute(engine):
     v, _ = o.emit_vertices(0, 500, selected=3, use_build_geometry=True)
     assert engine.vertex_summary().checksum == oracle_c.vertex_checksum(v)
     o.close()
+
+
+def test_frames_recompute_from_first_changed_row(engine):
+    """A frame whose bands differ from the last frame's only from row r0 on
+    recomputes heights / flags of rows >= r0 and the curves of edges ending at
+    or after r0 (the others keep theirs); every frame equals the oracle's whole
+    pass, including frames whose change re-filters the curve lists (a band
+    that zeroes a row's height) and the vertices emitted from them."""
+    d = synth.generate("wide16", 40000, seed=8)
+    engine.build(d)
+    o = oracle_c.OracleLayout(d)
+    h = engine.row_heights()
+    band = d.band.copy()
+    engine.enable_timing(True, reserve=256)
+    engine.row_geometry(band)
+    _check(engine, o, band)
+    for r0, val in ((39990, 30.0), (30000, 12.5), (20001, 0.0), (35000, None), (39999, 3.0), (100, 30.0)):
+        band[r0] = np.float32(-h[r0]) if val is None else np.float32(val)   # None: a zero-height row
+        band[r0 + 1:r0 + 40] = np.float32(1.0)
+        engine.row_geometry(band)
+        _check(engine, o, band)
+        engine.emit_vertices(r0 - 5 if r0 >= 5 else 0, min(d.n, r0 + 60), selected=r0)
+        v, _ = o.emit_vertices(r0 - 5 if r0 >= 5 else 0, min(d.n, r0 + 60), selected=r0)
+        assert engine.vertex_summary().checksum == oracle_c.vertex_checksum(v), r0
+    names = [n for n, _ in engine.timings()]
+    engine.enable_timing(False)
+    assert names.count("geom_reuse") == 7
+    o.close()

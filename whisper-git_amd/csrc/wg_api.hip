@@ -466,6 +466,7 @@ int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
         uint64_t first = 0;
         if (const int frc = wg_fetch(c, {{c->geom_diff_first.p, true}}, &first)) return frc;
         if (first == ~0ull) { c->have_geom = true; return WG_OK; }
+        c->geom_r0 = first;   // rows below `first` keep their geometry
     }
     int rc;
     if ((rc = wg_stage_rowtop(c, d_band)) != WG_OK) return rc;
@@ -473,6 +474,7 @@ int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
     c->have_geom = true;
     c->geom_key_gen = c->layout_gen;
     c->geom_key_band = band != nullptr;
+    c->geom_r0 = 0;
     if (band && c->n) {   // the bands this geometry was made with (compared by the next frame)
         WG_ALLOC(c, c->band_prev, c->n * 4 + 4);
         WG_HIP(c, hipMemcpyAsync(c->band_prev.p, d_band, c->n * 4, hipMemcpyDeviceToDevice, c->stream));

@@ -33,10 +33,11 @@ __device__ __forceinline__ uint32_t pack_vert(uint32_t lane, uint32_t kind, uint
 }
 
 // RowGeometry {height, node_y} + per-row strip flags
+// rows [lo, n) (lo > 0: a frame whose bands equal the last frame's below lo)
 __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
                             const float *__restrict__ row_top, float *__restrict__ height, float *__restrict__ node_y,
-                            uint8_t *__restrict__ rowflags) {
-    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                            uint8_t *__restrict__ rowflags, uint64_t lo = 0) {
+    uint64_t r = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     float ht, ny;
     if (band) {
@@ -424,14 +425,18 @@ __device__ __forceinline__ Cubic subcurve(const Cubic &c, float a, float b) {   
     return left;
 }
 
+// pmin > 0: records of edges whose parent row is below pmin are left as they
+// are (a frame whose bands and row_top are unchanged above row pmin)
 __global__ void k_curves(const uint32_t *__restrict__ nc, const uint32_t *__restrict__ curve_ref,
                          const uint32_t *__restrict__ curve_row, const wg_edge *__restrict__ edges,
                          const float *__restrict__ row_top, const float *__restrict__ node_y,
-                         const float2 *__restrict__ edge_y, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color) {
+                         const float2 *__restrict__ edge_y, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color,
+                         uint32_t pmin) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= *nc) return;   // grid sized by an upper bound; the count lives on the device
     const uint32_t ref = curve_ref[k];
     const wg_edge e = edges[ref];
+    if (e.parent_row < pmin) return;
     const uint32_t row = curve_row[k];
     float child_y, parent_y;
     if (edge_y) {   // row-sharded geometry: endpoints may lie in other shards
@@ -501,8 +506,9 @@ __global__ void k_curve_compact(uint64_t n, const uint32_t *__restrict__ soff, c
     }
 }
 
-__global__ void k_flags_diff(uint64_t n, const uint8_t *__restrict__ a, const uint8_t *__restrict__ b, uint32_t *diff) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_flags_diff(uint64_t n, const uint8_t *__restrict__ a, const uint8_t *__restrict__ b, uint32_t *diff,
+                             uint64_t lo = 0) {
+    const uint64_t r = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool d = r < n && a[r] != b[r];
     if (__any(d) && (threadIdx.x & 63) == 0) atomicOr(diff, 1u);
 }
@@ -525,12 +531,13 @@ static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s) {
     return WG_OK;
 }
 
-static void launch_curves(wg_ctx *c, uint64_t n, uint64_t n_upper, hipStream_t s) {
+static void launch_curves(wg_ctx *c, uint64_t n, uint64_t n_upper, hipStream_t s, uint32_t pmin = 0) {
     if (!n_upper) return;
     hipLaunchKernelGGL(k_curves, dim3(blocks(n_upper)), dim3(T), 0, s, c->curve_off.as<const uint32_t>() + n,
                        c->curve_ref.as<const uint32_t>(), c->curve_row.as<const uint32_t>(), c->edges.as<const wg_edge>(),
                        c->g_row_top.as<const float>(), c->g_node_y.as<const float>(),
-                       reinterpret_cast<const float2 *>(c->edge_y), c->curve.as<wg_curve>(), c->curve_color.as<uint8_t>());
+                       reinterpret_cast<const float2 *>(c->edge_y), c->curve.as<wg_curve>(), c->curve_color.as<uint8_t>(),
+                       pmin);
 }
 
 int wg_stage_geometry(wg_ctx *c, const float *d_band) {
@@ -548,13 +555,18 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     const float *rt = c->g_row_top.as<const float>();
     if (n && c->lists_gen == c->layout_gen && c->lists_n == n && c->lists_ne == ne) {
         // same layout: the lists stand; only the curve filter can change with the flags
+        // a frame whose bands equal the last frame's below row r0 (wg_row_geometry):
+        // rows below r0 keep height / node_y / flags, and curve records of edges
+        // that end above r0 keep their geometry (row_top up to r0 is unchanged)
+        const uint64_t r0 = c->geom_r0 < n ? c->geom_r0 : 0;
+        c->geom_r0 = 0;
         WG_ALLOC(c, c->geom_diff, 64);
         wg_stage_begin(c, "geom_reuse");
         WG_HIP(c, hipMemsetAsync(c->geom_diff.p, 0, 4, s));
-        hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
-                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>());
-        hipLaunchKernelGGL(k_flags_diff, dim3(blocks(n)), dim3(T), 0, s, n, c->rowflags.as<const uint8_t>(),
-                           c->rowflags_lists.as<const uint8_t>(), c->geom_diff.as<uint32_t>());
+        hipLaunchKernelGGL(k_row_basic, dim3(blocks(n - r0)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
+                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), r0);
+        hipLaunchKernelGGL(k_flags_diff, dim3(blocks(n - r0)), dim3(T), 0, s, n, c->rowflags.as<const uint8_t>(),
+                           c->rowflags_lists.as<const uint8_t>(), c->geom_diff.as<uint32_t>(), r0);
         uint64_t chk[3] = {1, 0, 0};
         int rc = wg_fetch(c, {{c->geom_diff.p, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false}}, chk);
         if (rc != WG_OK) return rc;
@@ -566,7 +578,8 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         }
         wg_stage_end(c);
         wg_stage_begin(c, "geom_curves");
-        launch_curves(c, n, c->n_curve, s);
+        // re-filtered lists move every record: all of them are recomputed then
+        launch_curves(c, n, c->n_curve, s, chk[0] ? 0u : (uint32_t)r0);
         WG_HIP(c, hipGetLastError());
         wg_stage_end(c);
         const uint32_t tbits = (uint32_t)chk[1];

@@ -199,6 +199,7 @@ struct wg_ctx {
     bool     geom_key_band = false;
     DevBuf   band_prev;                 // float [N] the bands of that geometry
     DevBuf   geom_diff_first;           // u64: first row whose band differs
+    uint64_t geom_r0 = 0;               // that row, for the next geometry pass (0: whole pass)
     DevBuf sweep_big;       // uint32 [nch] chunks too wide for the register sweep
     uint32_t sweep_reg_cap = 512;   // edges per chunk the register sweep holds (WG_OPT_SWEEP_REG)
     const float *edge_y = nullptr;   // per edge {child_y, parent_y} override (row-sharded geometry), or null
