@@ -22,13 +22,14 @@ __global__ void __launch_bounds__(256) k_stride(v4f *out, size_t n) {
     }
 }
 
-// one 48 KiB block per workgroup (3072 float4), written as 12 rounds of 256 lanes
-template <bool NT>
+// one contiguous block per workgroup (R rounds of 256 lanes x 16 B: R = 12 is
+// 48 KiB, R = 6 is 24 KiB — k_vtx_tile's tile shapes)
+template <bool NT, int R>
 __global__ void __launch_bounds__(256) k_block(v4f *out, size_t n) {
     const v4f v = {1.0f, 2.0f, 3.0f, 4.0f};
-    const size_t b = (size_t)blockIdx.x * 3072;
+    const size_t b = (size_t)blockIdx.x * (256 * R);
 #pragma unroll
-    for (int k = 0; k < 12; k++) {
+    for (int k = 0; k < R; k++) {
         const size_t i = b + k * 256 + threadIdx.x;
         if (i < n) {
             if (NT) __builtin_nontemporal_store(v, out + i);
@@ -65,11 +66,15 @@ int main() {
                name, bytes, best, sum / reps, bytes / (best * 1e-3) / 1e12, bytes / (sum / reps * 1e-3) / 1e12);
     };
     const unsigned grid_stride = 256 * 32;
-    const unsigned grid_block = (unsigned)((n + 3071) / 3072);
+    const unsigned g48 = (unsigned)((n + 3071) / 3072), g24 = (unsigned)((n + 1535) / 1536), g12 = (unsigned)((n + 767) / 768);
     run("grid-stride plain", [&] { hipLaunchKernelGGL(k_stride<false>, dim3(grid_stride), dim3(256), 0, 0, out, n); });
     run("grid-stride nontemporal", [&] { hipLaunchKernelGGL(k_stride<true>, dim3(grid_stride), dim3(256), 0, 0, out, n); });
-    run("48KiB-block plain", [&] { hipLaunchKernelGGL(k_block<false>, dim3(grid_block), dim3(256), 0, 0, out, n); });
-    run("48KiB-block nontemporal", [&] { hipLaunchKernelGGL(k_block<true>, dim3(grid_block), dim3(256), 0, 0, out, n); });
+    run("48KiB-block plain", [&] { hipLaunchKernelGGL((k_block<false, 12>), dim3(g48), dim3(256), 0, 0, out, n); });
+    run("48KiB-block nontemporal", [&] { hipLaunchKernelGGL((k_block<true, 12>), dim3(g48), dim3(256), 0, 0, out, n); });
+    run("24KiB-block plain", [&] { hipLaunchKernelGGL((k_block<false, 6>), dim3(g24), dim3(256), 0, 0, out, n); });
+    run("24KiB-block nontemporal", [&] { hipLaunchKernelGGL((k_block<true, 6>), dim3(g24), dim3(256), 0, 0, out, n); });
+    run("12KiB-block plain", [&] { hipLaunchKernelGGL((k_block<false, 3>), dim3(g12), dim3(256), 0, 0, out, n); });
+    run("12KiB-block nontemporal", [&] { hipLaunchKernelGGL((k_block<true, 3>), dim3(g12), dim3(256), 0, 0, out, n); });
     CHECK(hipFree(out));
     return 0;
 }

@@ -11,7 +11,7 @@
 // vertices, ring -> 24 quads = 144 vertices.
 //
 // HBM-write-bound: 24 B per vertex out, a few bytes of geometry in.  A
-// workgroup owns a fixed tile of 2048 vertices (48 KiB out):
+// workgroup owns a fixed tile of 1024 vertices (24 KiB out):
 //   1. one round of independent global loads, all addressed from a per-tile
 //      record (k_tile_info): the rows overlapping the tile, its vertical
 //      entries (one contiguous range of vert[]) and its curve segments (one
@@ -34,12 +34,13 @@ namespace {
 #define WG_VTX_THREADS 256
 #endif
 #ifndef WG_VTX_TILE_VERTS
-#define WG_VTX_TILE_VERTS 2048
+#define WG_VTX_TILE_VERTS 1024   // 24 KiB out per workgroup (tile sweep: 1024 0.98 ms, 1536 1.01, 2048 1.05, 512 1.07)
 #endif
 constexpr int VT = WG_VTX_THREADS;
 constexpr int TILE = WG_VTX_TILE_VERTS;     // vertices per workgroup
-constexpr int PAIRS = TILE / 2;             // 1024
-constexpr int ROUNDS = PAIRS / VT;          // 4
+constexpr int PAIRS = TILE / 2;             // 512
+constexpr int ROUNDS = PAIRS / VT;          // 2
+static_assert(PAIRS % VT == 0, "a tile is a whole number of rounds of one pair per thread");
 typedef float v4f __attribute__((ext_vector_type(4)));
 static_assert(TILE / WG_VTX_PER_NODE + 3 <= 64, "rows of a tile are loaded by one wave");
 constexpr int MAXR = TILE / WG_VTX_PER_NODE + 3;          // rows overlapping a tile
