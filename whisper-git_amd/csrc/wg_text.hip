@@ -224,7 +224,10 @@ struct QuadArgs {
     float4 color[6];                 // run colours, then the same at WG_DIM_ALPHA
 };
 
-constexpr int QT = 256;
+#ifndef WG_QUAD_THREADS
+#define WG_QUAD_THREADS 256
+#endif
+constexpr int QT = WG_QUAD_THREADS;
 
 __global__ void __launch_bounds__(QT) k_text_quads(QuadArgs A, float4 *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) float4 stage[QT / 64][64 * 12];
