@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--kind", default="wide16")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--stage-events", action="store_true", help="record every stage's HIP events (stages_ms)")
     args = ap.parse_args()
 
     import torch
@@ -143,6 +144,10 @@ def main():
             s0, s1 = r * R, min(dag.n, (r + 1) * R)
             for it in range(args.steps + 1):
                 if it == 1:
+                    # per-stage events only with --stage-events: each costs a few us of
+                    # GPU time, which would inflate the segments against the
+                    # uninstrumented single-GPU step
+                    wgraph.lib().wg_set_option(eng._ctx, 4, 0 if args.stage_events else 1)
                     eng.enable_timing(True, reserve=64 * (args.steps + 1))
                 comm.start("build")
                 eng.shard_build(commits, W, r, s0, s1, comm)
