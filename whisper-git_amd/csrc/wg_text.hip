@@ -164,55 +164,72 @@ __global__ void __launch_bounds__(T) k_text_rows(TextArgs A, uint64_t *__restric
         tx = A.time_right_x - wdt;
     }
     const uint8_t *none = reinterpret_cast<const uint8_t *>("(no summary)");
-    // per-lane walk state: run 0 sha, 1 summary, 2 time, 3 done
-    uint32_t run = 0, i = 0, len = nsha, n = 0, flushed = 0;
-    float pen = A.sha_x, max_x = 3.0e38f;
-    bool active = live;
+    uint32_t n = 0, flushed = 0, it = 0;
     const uint64_t obase = WRITE && live ? off[j] : 0ull;
-    while (__any(active)) {
-#pragma unroll 1
-        for (int it = 0; it < RT_R; it++) {
-            if (!active) continue;
-            if (i >= len) {   // next run
-                run++;
-                i = 0;
-                if (run == 1) { len = nsum; pen = A.summary_x; max_x = A.summary_max_x; }
-                else if (run == 2) { len = nt; pen = tx; max_x = 3.0e38f; }
-                else { active = false; }
-                continue;
-            }
-            const uint32_t ch = run == 1 ? (nosum ? none[i] : sum[i]) : str[run == 0 ? i : 8 + i][lane];
-            const float next = pen + s_adv[ch];
-            if (next > max_x) { i = len; continue; }   // clipped (summary column)
-            const uint32_t gv = s_gl[ch];
-            if (gv >> 31) {
-                if (WRITE) s_rec[w][n - flushed][lane] = make_uint2(__float_as_uint(pen), (gv & 0xFFFFFFu) | ((run + d) << 24));
-                n++;
-            }
-            pen = next;
-            i++;
-        }
-        if (WRITE) {
-            s_base[w][lane] = obase + flushed;
-            s_pend[w][lane] = n - flushed;
-            flushed = n;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint32_t q = lane % RT_R;
+    // the wave writes the records staged so far: a lane's pending records are
+    // contiguous in the output (8 lanes per row and store instruction)
+    auto flush = [&]() {
+        s_base[w][lane] = obase + flushed;
+        s_pend[w][lane] = n - flushed;
+        flushed = n;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t q = lane % RT_R;
 #pragma unroll
-            for (int t = 0; t < RT_R; t++) {
-                const uint32_t row = t * (64 / RT_R) + lane / RT_R;
-                if (q < s_pend[w][row]) {
-                    const uint2 v = s_rec[w][q][row];
-                    rec[s_base[w][row] + q] = make_uint4(v.x, __float_as_uint(s_y[w][row]), v.y & 0xFFFFFFu, v.y >> 24);
-                }
+        for (int t = 0; t < RT_R; t++) {
+            const uint32_t row = t * (64 / RT_R) + lane / RT_R;
+            if (q < s_pend[w][row]) {
+                const uint2 v = s_rec[w][q][row];
+                rec[s_base[w][row] + q] = make_uint4(v.x, __float_as_uint(s_y[w][row]), v.y & 0xFFFFFFu, v.y >> 24);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // one glyph of run `run` at pen: returns false when the run is clipped
+    auto glyph = [&](uint32_t ch, float &pen, float max_x, uint32_t run) -> bool {
+        const float next = pen + s_adv[ch];
+        if (next > max_x) return false;   // clipped (summary column)
+        const uint32_t gv = s_gl[ch];
+        if (gv >> 31) {
+            if (WRITE) s_rec[w][n - flushed][lane] = make_uint2(__float_as_uint(pen), (gv & 0xFFFFFFu) | ((run + d) << 24));
+            n++;
+        }
+        pen = next;
+        return true;
+    };
+    // the three runs one after the other, each a wave-uniform loop (one
+    // character per lane per iteration; every RT_R iterations a flush)
+    {   // short SHA: 7 characters (none on synthetic rows)
+        float pen = A.sha_x;
+        bool on = true;   // (a run also stops where the pen passes 3e38, as in the reference walk)
+#pragma unroll 1
+        for (uint32_t i = 0; i < 7; i++) {
+            if (on && i < nsha) on = glyph(str[i][lane], pen, 3.0e38f, 0u);
+            if (WRITE && ++it % RT_R == 0) flush();
         }
     }
+    {   // summary, clipped at summary_max_x
+        float pen = A.summary_x;
+        bool on = live;
+#pragma unroll 1
+        for (uint32_t i = 0; __any(on && i < nsum); i++) {
+            if (on && i < nsum) on = glyph(nosum ? none[i] : sum[i], pen, A.summary_max_x, 1u);
+            if (WRITE && ++it % RT_R == 0) flush();
+        }
+    }
+    {   // relative time, right-aligned at time_right_x
+        float pen = tx;
+        bool on = true;
+#pragma unroll 1
+        for (uint32_t i = 0; __any(on && i < nt); i++) {
+            if (on && i < nt) on = glyph(str[8 + i][lane], pen, 3.0e38f, 2u);
+            if (WRITE && ++it % RT_R == 0) flush();
+        }
+    }
+    if (WRITE) flush();
     if (!WRITE && live) cnt[j] = n;
 }
 
