@@ -324,6 +324,12 @@ int wg_lf_chain(wg_ctx *c, const LfRange &R);
 int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok);
 int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint4 *ev_out, uint32_t *aux_out,
                  uint32_t aux_base);
+// sharded form: records with shard-local tokens / aux offsets (before the
+// crossing tokens are resolved), then, on the gathered records of every rank,
+// the global form (plus the own rows' chain tokens, for the lanes)
+int wg_lf_events_local(wg_ctx *c, const LfRange &R, uint4 *ev_out, uint32_t *aux_out);
+int wg_lf_events_finish(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint64_t nx, uint64_t nev,
+                        uint32_t world, const uint64_t *d_evoff, const uint64_t *d_auxoff, uint4 *ev, uint32_t *aux);
 // replay + lanes of the range + their scalars; *ok = false: no fixed point or
 // more than 63 slots (the caller takes its fallback)
 int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,

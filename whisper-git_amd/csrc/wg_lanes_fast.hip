@@ -278,6 +278,11 @@ __global__ void k_lf_globalize(uint64_t nl, uint32_t ev_base, const uint32_t *__
     if (winfo[j] & 0x80000000u) secev[j] = globalize(secev[j], ev_base, xt);
 }
 
+// LOCAL (sharded build, before the crossing tokens are known): tokens stay
+// tagged (EV = shard-local event, X = crossing-table entry), the flags carry
+// no token bits and aux offsets are shard-local; k_lf_events_finish turns the
+// gathered records into exactly what the global form would have written.
+template <bool LOCAL>
 __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, const uint32_t *__restrict__ xt,
                             const unsigned long long *__restrict__ first_ref, const uint32_t *__restrict__ winfo,
                             const uint32_t *__restrict__ ev_off, const uint32_t *__restrict__ aux_off,
@@ -301,23 +306,25 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
         if (list) list[0] = w;
         for (uint32_t k = ch_off[j]; k < ch_off[j + 1]; k++) {
             const uint32_t v = ch[k];
-            const uint32_t tk = ((v & WG_TOK_X) ? xt[v & ~WG_TOK_X] : sp[v]) & ~WG_TOK_EV;
+            const uint32_t tk = LOCAL ? ((v & WG_TOK_X) ? v : sp[v])
+                                      : ((v & WG_TOK_X) ? xt[v & ~WG_TOK_X] : sp[v]) & ~WG_TOK_EV;
             if (nt < 2) t[nt] = tk;
             if (list) list[1 + nt] = tk;
             nt++;
         }
         if (sec_first) {
-            const uint32_t tk = secev[j] & ~WG_TOK_EV;
+            const uint32_t tk = LOCAL ? secev[j] : secev[j] & ~WG_TOK_EV;
             if (nt < 2) t[nt] = tk;
             if (list) list[1 + nt] = tk;
             nt++;
         }
         const uint32_t f = F_C | (fp_in ? F_O : 0u) | ((w > 2) ? F_M : 0u);
-        ev[e] = make_uint4(f | token_bits(ev_base + e, t[0], t[1]), t[0], t[1], (w > 2) ? aux_base + aux_off[j] : (uint32_t)gj);
+        ev[e] = make_uint4(f | (LOCAL ? 0u : token_bits(ev_base + e, t[0], t[1])), t[0], t[1],
+                           (w > 2) ? aux_base + aux_off[j] : (uint32_t)gj);
         e++;
     } else if (!fp_in) {
-        const uint32_t t0 = sp[j] & ~WG_TOK_EV;
-        ev[e] = make_uint4(F_C | token_bits(ev_base + e, t0, t0), t0, t0, (uint32_t)gj);
+        const uint32_t t0 = LOCAL ? sp[j] : sp[j] & ~WG_TOK_EV;
+        ev[e] = make_uint4(F_C | (LOCAL ? 0u : token_bits(ev_base + e, t0, t0)), t0, t0, (uint32_t)gj);
         e++;
     }
     const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
@@ -346,6 +353,36 @@ __global__ void k_lf_clear(uint64_t n, unsigned long long *__restrict__ first_re
     if (i < n) first_ref[i] = REF_NONE;
     if (i < n + 2) { fpc[i] = 0u; ch_fill[i] = 0u; }
     if (i < 16) flags[i] = 0u;
+}
+
+// gathered shard-local records (k_lf_events<true> of every rank, rank r's at
+// evoff[r] / auxoff[r]) -> global form: tokens through globalize with the
+// owning rank's base, token bits at the global index, aux offsets rebased.
+// Allocation records carry no tokens and are already final.
+__global__ void k_lf_events_finish(uint64_t nev, uint32_t world, const uint64_t *__restrict__ evoff,
+                                   const uint64_t *__restrict__ auxoff, const uint32_t *__restrict__ xt, uint64_t nx,
+                                   uint4 *__restrict__ ev, uint32_t *__restrict__ aux) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nev) return;
+    uint4 r = ev[g];
+    if (!(r.x & F_C)) return;
+    uint32_t k = 0;
+    while (k + 1 < world && evoff[k + 1] <= g) k++;
+    const uint32_t base = (uint32_t)evoff[k];
+    auto glob = [&](uint32_t v) -> uint32_t {
+        if (!(v & WG_TOK_EV) && (v & WG_TOK_X) && (v & ~WG_TOK_X) >= nx) return v;   // not a crossing entry
+        return globalize(v, base, xt) & ~WG_TOK_EV;
+    };
+    r.y = glob(r.y);
+    r.z = glob(r.z);
+    r.x |= token_bits(g, r.y, r.z);
+    if (r.x & F_M) {
+        r.w += (uint32_t)auxoff[k];
+        uint32_t *list = aux + r.w;
+        const uint32_t n = list[0];
+        for (uint32_t q = 1; q <= n; q++) list[q] = glob(list[q]);
+    }
+    ev[g] = r;
 }
 
 }  // namespace
@@ -462,11 +499,41 @@ int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *
     if (ev_base || xt)
         hipLaunchKernelGGL(k_lf_globalize, dim3(blocks(n)), dim3(T), 0, s, n, ev_base, xt, sp, c->lf[LF_SECEV].as<uint32_t>(),
                            c->lf[LF_WINFO].as<const uint32_t>());
-    hipLaunchKernelGGL(k_lf_events, dim3(blocks(n)), dim3(T), 0, s, R, ev_base, aux_base, xt,
+    hipLaunchKernelGGL(k_lf_events<false>, dim3(blocks(n)), dim3(T), 0, s, R, ev_base, aux_base, xt,
                        c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
                        c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
                        c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
                        c->lf[LF_SECEV].as<const uint32_t>(), (const uint32_t *)sp, ev_out, aux_out);
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    return WG_OK;
+}
+
+int wg_lf_events_local(wg_ctx *c, const LfRange &R, uint4 *ev_out, uint32_t *aux_out) {
+    const uint64_t n = R.nl;
+    if (!n) return WG_OK;
+    wg_stage_begin(c, "lf_events");
+    hipLaunchKernelGGL(k_lf_events<true>, dim3(blocks(n)), dim3(T), 0, c->stream, R, 0u, 0u, (const uint32_t *)nullptr,
+                       c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
+                       c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
+                       c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
+                       c->lf[LF_SECEV].as<const uint32_t>(), lf_sp(c), ev_out, aux_out);
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    return WG_OK;
+}
+
+int wg_lf_events_finish(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint64_t nx, uint64_t nev,
+                        uint32_t world, const uint64_t *d_evoff, const uint64_t *d_auxoff, uint4 *ev, uint32_t *aux) {
+    hipStream_t s = c->stream;
+    wg_stage_begin(c, "lf_events");
+    if (R.nl)
+        hipLaunchKernelGGL(k_lf_globalize, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, ev_base, xt,
+                           const_cast<uint32_t *>(lf_sp(c)), c->lf[LF_SECEV].as<uint32_t>(),
+                           c->lf[LF_WINFO].as<const uint32_t>());
+    if (nev)
+        hipLaunchKernelGGL(k_lf_events_finish, dim3(blocks(nev)), dim3(T), 0, s, nev, world, d_evoff, d_auxoff, xt, nx,
+                           ev, aux);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;

@@ -13,9 +13,10 @@
 //   X2  the rows the owning shards found for them: every rank derives the
 //       same table of crossing entries (references to rows beyond the
 //       child's shard), so every shard knows every waiter created before it
-//   X3  event counts and, per crossing entry, the token of its chain
-//       (shard-local event or an earlier crossing entry) -> global event ids
-//   X4  the event records of every shard; each rank replays the global event
+//   X3  event counts, per crossing entry the token of its chain (shard-local
+//       event or an earlier crossing entry), and the shard's event records
+//       with shard-local tokens: every rank resolves the tokens to global
+//       event ids, rewrites the records in place, replays the global event
 //       stream (latency-bound, ~the same cost at 8M rows as at 1M) and reads
 //       its own rows' lanes from it
 //   X6  per geometry pass: lanes, colours and endpoint y of crossing edges
@@ -192,7 +193,7 @@ __global__ void k_sh_xbuild(uint64_t L, const uint32_t *__restrict__ rec, const 
     }
 }
 
-// ---- X4: chain tokens of crossing entries -> global event ids ---------------------------
+// ---- X3: chain tokens of crossing entries -> global event ids ---------------------------
 // entries of rank r are [xoff[r], xoff[r+1]); a token names either an event of
 // the entry's own rank or an entry of an earlier rank (depth < world)
 __global__ void k_sh_resolve(uint64_t nx, uint32_t world, const uint64_t *__restrict__ xoff,
@@ -400,9 +401,9 @@ __global__ void k_sh_lane_out(uint64_t s, uint64_t nl, const uint32_t *__restric
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// exchange points: X1 unresolved references, X2 their rows, X3 chain tokens,
-// X4 event records, X6 crossing-edge endpoints (per geometry pass)
-enum { SH_IDLE = 0, SH_X1, SH_X2, SH_X3, SH_X4, SH_X6 = 6 };
+// exchange points: X1 unresolved references, X2 their rows, X3 chain tokens
+// and event records, X6 crossing-edge endpoints (per geometry pass)
+enum { SH_IDLE = 0, SH_X1, SH_X2, SH_X3, SH_X6 = 6 };
 
 static int sh_send(wg_ctx *c, uint64_t bytes, wg_shard_msg *out) {
     WG_ALLOC(c, c->sh.msg, bytes + 64);
@@ -808,14 +809,21 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         S.nev_own = nev;
         S.naux_own = naux;
         const uint64_t nown = R.xown_end - R.xown_begin;
+        const uint64_t tok_b = (nown * 4 + 15) & ~15ull;          // records start 16-byte aligned
+        const uint64_t rec_b = viol ? 0 : nev * 16 + naux * 4;    // not well formed: every rank falls back at X3
         S.step = SH_X3;
-        if ((rc = sh_send(c, 16 + nown * 4, out)) != WG_OK) return rc;
+        if ((rc = sh_send(c, 16 + tok_b + rec_b, out)) != WG_OK) return rc;
         uint32_t h4[4] = {(uint32_t)nev, (uint32_t)naux, viol, 0};
         hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), make_uint4(h4[0], h4[1], h4[2], h4[3]));
-        if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(S.msg.as<uint8_t>() + 16))) != WG_OK) return rc;
+        uint8_t *m = S.msg.as<uint8_t>() + 16;
+        if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(m))) != WG_OK) return rc;
+        // the event records travel in the same message, with shard-local tokens
+        if (!viol && (rc = wg_lf_events_local(c, R, reinterpret_cast<uint4 *>(m + tok_b),
+                                              reinterpret_cast<uint32_t *>(m + tok_b + nev * 16))) != WG_OK)
+            return rc;
         return WG_OK;
     }
-    case SH_X3: {   // global event ids; this shard's event records
+    case SH_X3: {   // global event ids; replay the global event stream; lanes of own rows; default geometry
         std::vector<uint32_t> hdr;
         if ((rc = read_headers(c, gathered, stride, hdr)) != WG_OK) return rc;
         S.evoff.assign(W + 1, 0);
@@ -835,24 +843,13 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
             if (n) WG_HIP(c, hipMemcpyAsync(S.xtok.as<uint32_t>() + S.xoff[r], (const uint8_t *)gathered + r * stride + 16,
                                             n * 4, hipMemcpyDeviceToDevice, st));
         }
-        WG_ALLOC(c, S.dev_small, 64 * 8);
+        WG_ALLOC(c, S.dev_small, 96 * 8);
         WG_HIP(c, hipMemcpyAsync(S.dev_small.p, S.xoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
         WG_HIP(c, hipMemcpyAsync(S.dev_small.as<uint64_t>() + 32, S.evoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
+        WG_HIP(c, hipMemcpyAsync(S.dev_small.as<uint64_t>() + 64, S.auxoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
         if (nx) hipLaunchKernelGGL(k_sh_resolve, dim3(1), dim3(1024), 0, st, nx, (uint32_t)W, S.dev_small.as<const uint64_t>(),
                                    S.dev_small.as<const uint64_t>() + 32, S.xtok.as<const uint32_t>(), S.xt.as<uint32_t>());
-        S.step = SH_X4;
-        const uint64_t nev = S.nev_own, naux = S.naux_own;
-        if ((rc = sh_send(c, 16 + nev * 16 + naux * 4, out)) != WG_OK) return rc;
-        uint32_t h5[4] = {(uint32_t)nev, (uint32_t)naux, 0, 0};
-        hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), make_uint4(h5[0], h5[1], h5[2], h5[3]));
-        LfRange R = sh_range(c);
-        uint8_t *m = S.msg.as<uint8_t>();
-        if ((rc = wg_lf_events(c, R, (uint32_t)S.evoff[S.rank], S.xt.as<const uint32_t>(), reinterpret_cast<uint4 *>(m + 16),
-                               reinterpret_cast<uint32_t *>(m + 16 + nev * 16), (uint32_t)S.auxoff[S.rank])) != WG_OK)
-            return rc;
-        return WG_OK;
-    }
-    case SH_X4: {   // replay the global event stream; lanes of own rows; default geometry
+        // every rank's records (after its tokens, 16-byte aligned): rank r's events at evoff[r], aux words at auxoff[r]
         const uint64_t nev = S.evoff[W], naux = S.auxoff[W];
         DevBuf &evrec = c->lf[10], &aux = c->lf[18];
         WG_ALLOC(c, evrec, (nev + 256) * 16);
@@ -860,14 +857,19 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_HIP(c, hipMemsetAsync(evrec.as<uint4>() + nev, 0, 256 * 16, st));
         for (int r = 0; r < W; r++) {
             const uint64_t ne_r = S.evoff[r + 1] - S.evoff[r], na_r = S.auxoff[r + 1] - S.auxoff[r];
-            const uint8_t *src = (const uint8_t *)gathered + r * stride + 16;
+            const uint64_t tok_b = ((S.xoff[r + 1] - S.xoff[r]) * 4 + 15) & ~15ull;
+            const uint8_t *src = (const uint8_t *)gathered + r * stride + 16 + tok_b;
             if (ne_r) WG_HIP(c, hipMemcpyAsync(evrec.as<uint4>() + S.evoff[r], src, ne_r * 16, hipMemcpyDeviceToDevice, st));
             if (na_r) WG_HIP(c, hipMemcpyAsync(aux.as<uint32_t>() + S.auxoff[r], src + ne_r * 16, na_r * 4,
                                                hipMemcpyDeviceToDevice, st));
         }
+        LfRange R = sh_range(c);
+        if ((rc = wg_lf_events_finish(c, R, (uint32_t)S.evoff[S.rank], S.xt.as<const uint32_t>(), nx, nev, (uint32_t)W,
+                                      S.dev_small.as<const uint64_t>() + 32, S.dev_small.as<const uint64_t>() + 64,
+                                      evrec.as<uint4>(), aux.as<uint32_t>())) != WG_OK)
+            return rc;
         c->n_events = nev;
         WG_ALLOC(c, c->lane_asg, nl * 4 + 4);
-        LfRange R = sh_range(c);
         bool ok = false;
         if ((rc = wg_lf_replay_lanes(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
                                      c->lane_asg.as<uint32_t>(), &ok)) != WG_OK)
