@@ -3,6 +3,8 @@
 // Each exported function names the GraphLayout item it replaces
 // (/root/reference/src/commit_graph.rs).  No C++ exception crosses the ABI;
 // every failure returns a negative status with a message in wg_last_error().
+#include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstring>
 #include <new>
@@ -44,11 +46,15 @@ void wg_stage_end(wg_ctx *c) {
 namespace {
 constexpr int FETCH_MAX = 64;
 struct FetchArgs { const void *p[FETCH_MAX]; unsigned long long wide; uint32_t n; };
-__global__ void k_fetch(FetchArgs a, unsigned long long *out) {
+// the words, then (system-scope release) the launch's sequence number: the
+// host sees the words once it sees the number, without a runtime wait
+__global__ void k_fetch(FetchArgs a, unsigned long long *out, unsigned long long *seq_word, unsigned long long seq) {
     const uint32_t i = threadIdx.x;
     if (i < a.n) out[i] = ((a.wide >> i) & 1ull) ? *reinterpret_cast<const unsigned long long *>(a.p[i])
                                                  : (unsigned long long)*reinterpret_cast<const uint32_t *>(a.p[i]);
     __threadfence_system();
+    __syncthreads();
+    if (i == 0) __hip_atomic_store(seq_word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 }  // namespace
 
@@ -100,8 +106,10 @@ int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out) {
 static int fetch_launch(wg_ctx *c, int n, const WgFetch *items, uint64_t slot0) {
     if (n < 0 || n > FETCH_MAX) return wg_fail(c, WG_E_INVALID, "wg_fetch: too many items");
     if (!c->h_fetch) {
-        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, 3 * FETCH_MAX * sizeof(uint64_t), hipHostMallocMapped));
+        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, (3 * FETCH_MAX + 8) * sizeof(uint64_t),
+                                hipHostMallocMapped | hipHostMallocCoherent));
         WG_HIP(c, hipHostGetDevicePointer((void **)&c->d_fetch, c->h_fetch, 0));
+        memset(c->h_fetch, 0, (3 * FETCH_MAX + 8) * sizeof(uint64_t));
     }
     FetchArgs a{};
     a.n = 0;
@@ -110,14 +118,34 @@ static int fetch_launch(wg_ctx *c, int n, const WgFetch *items, uint64_t slot0) 
         if (items[i].wide) a.wide |= 1ull << a.n;
         a.n++;
     }
-    hipLaunchKernelGGL(k_fetch, dim3(1), dim3(64), 0, c->stream, a, (unsigned long long *)c->d_fetch + slot0);
+    const int region = (int)(slot0 / FETCH_MAX);
+    c->fetch_want[region] = ++c->fetch_seq;
+    hipLaunchKernelGGL(k_fetch, dim3(1), dim3(64), 0, c->stream, a, (unsigned long long *)c->d_fetch + slot0,
+                       (unsigned long long *)c->d_fetch + 3 * FETCH_MAX + region, (unsigned long long)c->fetch_seq);
     WG_HIP(c, hipGetLastError());
     return WG_OK;
 }
 
+// Spin on the region's sequence word (a few us after k_fetch ends, where a
+// runtime wait costs tens of us of wake-up and bookkeeping); false after 5 ms:
+// the caller takes the runtime wait, which also reports a failed launch.
+static bool fetch_spin(wg_ctx *c, int region) {
+    volatile uint64_t *w = (volatile uint64_t *)c->h_fetch + 3 * FETCH_MAX + region;
+    const uint64_t want = c->fetch_want[region];
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; i++) {
+        if (*w == want) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return true;
+        }
+        __builtin_ia32_pause();
+        if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) return false;
+    }
+}
+
 int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out) {
     if (const int rc = fetch_launch(c, n, items, 0)) return rc;
-    WG_HIP(c, hipStreamSynchronize(c->stream));
+    if (!fetch_spin(c, 0)) WG_HIP(c, hipStreamSynchronize(c->stream));
     for (int i = 0; i < n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[i];
     return WG_OK;
 }
@@ -149,7 +177,7 @@ int wg_fetch_deferred(wg_ctx *c, uint64_t *out) {
     if (!c->defer_pending) return wg_fail(c, WG_E_STATE, "wg_fetch_deferred: nothing deferred");
     const int n = c->defer_pending;
     c->defer_pending = 0;
-    WG_HIP(c, hipEventSynchronize(c->ev_defer));
+    if (!fetch_spin(c, 2)) WG_HIP(c, hipEventSynchronize(c->ev_defer));
     for (int i = 0; i < n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[2 * FETCH_MAX + i];
     return WG_OK;
 }
@@ -158,7 +186,7 @@ int wg_fetch_end(wg_ctx *c, uint64_t *out) {
     if (!c->fetch_pending) return wg_fail(c, WG_E_STATE, "wg_fetch_end: nothing pending");
     const int n = c->fetch_pending;
     c->fetch_pending = 0;
-    WG_HIP(c, hipEventSynchronize(c->ev_fetch));
+    if (!fetch_spin(c, 1)) WG_HIP(c, hipEventSynchronize(c->ev_fetch));
     for (int i = 0; i < n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[FETCH_MAX + i];
     return WG_OK;
 }

@@ -253,6 +253,8 @@ struct wg_ctx {
     hipEvent_t ev_defer = nullptr;  // completion of the last wg_fetch_defer
     int        defer_pending = 0;   // words of the last wg_fetch_defer
     uint64_t  *d_fetch = nullptr;
+    uint64_t   fetch_seq = 0;       // sequence number of the last k_fetch launch
+    uint64_t   fetch_want[3] = {0, 0, 0};   // per fetch region: the launch whose words it holds
 };
 
 // small device -> host reads (wg_api.hip): one tiny kernel writes the values
