@@ -35,6 +35,25 @@ def main():
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / n * 1e6
     print(f"ShardComm.allgather world=1 nccl: {us:.1f} us per exchange (pack path, header read to host)", flush=True)
+    import numpy as np
+    import wgraph
+    eng = wgraph.Engine(0)
+    eng.set_stream(stream)
+
+    def read_heads(ptr, stride):   # the engine's polled read (what Engine._shard_loop passes)
+        h = np.empty(3 * comm.world, np.uint64)
+        wgraph.lib().wg_shard_slot_heads(eng._ctx, ptr, stride, comm.world, h.ctypes.data)
+        return h.reshape(comm.world, 3)
+
+    for _ in range(20):
+        comm.allgather(0, None, step=1, pack=pack, read_heads=read_heads)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        comm.allgather(0, None, step=1, pack=pack, read_heads=read_heads)
+    torch.cuda.synchronize()
+    print(f"ShardComm.allgather world=1 nccl, heads by wg_shard_slot_heads: "
+          f"{(time.perf_counter() - t0) / n * 1e6:.1f} us per exchange", flush=True)
     x = torch.zeros(4096, dtype=torch.uint8, device=dev)
     out = torch.empty(4096, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()

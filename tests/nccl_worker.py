@@ -1,7 +1,8 @@
 """One rank of a world-1 RCCL job (tests/test_gpu_nccl.py): ShardComm over
 the "nccl" backend — the transport bench.py uses for N > 1 — through both the
-stream-ordered slot path (pack) and the copy-out path (fill), with messages
-that overflow the slot (the retry grows it), checked byte for byte."""
+stream-ordered slot path (pack, heads read by the engine's polled
+wg_shard_slot_heads) and the copy-out path (fill), with messages that
+overflow the slot (the retry grows it), checked byte for byte."""
 import ctypes
 import json
 import os
@@ -15,6 +16,7 @@ def main():
     import numpy as np
     import torch
     import torch.distributed as dist
+    import wgraph
     from wgraph.shard import ShardComm
 
     out = sys.argv[1]
@@ -33,6 +35,15 @@ def main():
     errors = []
     try:
         comm = ShardComm(dev, initial_cap=64)
+        eng = wgraph.Engine(0)
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+        def read_heads(ptr, stride):
+            h = np.empty(3 * comm.world, np.uint64)
+            rc = wgraph.lib().wg_shard_slot_heads(eng._ctx, ptr, stride, comm.world, h.ctypes.data)
+            if rc != 0:
+                raise RuntimeError(f"wg_shard_slot_heads: {rc}")
+            return h.reshape(comm.world, 3)
         if not comm.on_device:
             errors.append("nccl group not on device")
         rng = np.random.default_rng(1)
@@ -52,7 +63,8 @@ def main():
                         d2d(slot + 16, msg.data_ptr(), n)
 
                 g, off, stride, sizes = comm.allgather(n, fill, step=step + (100 if use_pack else 0),
-                                                       pack=pack if use_pack else None)
+                                                       pack=pack if use_pack else None,
+                                                       read_heads=read_heads if use_pack else None)
                 tag = f"{'pack' if use_pack else 'fill'} step {step} n {n}"
                 if sizes != [n]:
                     errors.append(f"{tag}: sizes {sizes}")

@@ -725,6 +725,20 @@ int wg_shard_pack_slot(wg_ctx *c, void *slot, uint64_t cap) {
     return WG_OK;
 }
 
+int wg_shard_slot_heads(wg_ctx *c, const void *gathered, uint64_t stride, int world, uint64_t *out) {
+    if (!c || !gathered || !out || world < 1 || 3 * world > 64 || ((reinterpret_cast<uintptr_t>(gathered) | stride) & 7u))
+        return WG_E_INVALID;
+    (void)hipSetDevice(c->device);
+    WgFetch it[64];
+    const uint8_t *g = static_cast<const uint8_t *>(gathered);
+    for (int r = 0; r < world; r++) {
+        it[3 * r] = WgFetch{g + r * stride, true};            // slot length
+        it[3 * r + 1] = WgFetch{g + r * stride + 16, true};   // the message's 16-byte header
+        it[3 * r + 2] = WgFetch{g + r * stride + 24, true};
+    }
+    return wg_fetch_n(c, 3 * world, it, out);
+}
+
 int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const uint64_t *sizes, const uint32_t *heads,
                       wg_shard_msg *out) {
     if (!c || !out || !sizes) return WG_E_INVALID;

@@ -87,6 +87,7 @@ def lib():
             "wg_shard_geometry_begin": ([vp, vp, i32, ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_copy_msg": ([vp, vp], ctypes.c_int),
             "wg_shard_pack_slot": ([vp, vp, u64], ctypes.c_int),
+            "wg_shard_slot_heads": ([vp, vp, u64, ctypes.c_int, vp], ctypes.c_int),
             "wg_match_rows": ([vp, vp, u64, u64, u64, ctypes.POINTER(abi.RowText), ctypes.POINTER(ctypes.c_uint64)],
                               ctypes.c_int),
             "wg_copy_match_flags": ([vp, vp], ctypes.c_int),
@@ -111,7 +112,7 @@ EXPORTED_SYMBOLS = (
     "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
-    "wg_shard_copy_msg", "wg_shard_pack_slot", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
+    "wg_shard_copy_msg", "wg_shard_pack_slot", "wg_shard_slot_heads", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
     "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets",
     "wg_match_rows", "wg_copy_match_flags", "wg_lower_utf8", "wg_order_rows", "wg_render", "wg_write_png")
 
@@ -217,16 +218,22 @@ class Engine:
         # (which synchronises that stream) has returned.  When the engine runs
         # on the transport's stream, slots are packed in stream order instead
         # (wg_shard_pack_slot, no host synchronisation before the collective).
-        pack = None
+        pack = read_heads = None
         if getattr(comm, "on_device", False) and getattr(self, "_stream_ptr", None):
             import torch
             if torch.cuda.current_stream(comm.device).cuda_stream == self._stream_ptr:
                 def pack(slot, cap):
                     self._check(lib().wg_shard_pack_slot(self._ctx, slot, cap))
+
+                if 3 * comm.world <= 64:
+                    def read_heads(ptr, stride):   # polled device read in stream order (no stream sync)
+                        h = np.empty(3 * comm.world, np.uint64)
+                        self._check(lib().wg_shard_slot_heads(self._ctx, ptr, stride, comm.world, h.ctypes.data))
+                        return h.reshape(comm.world, 3)
         while not msg.done:
             gathered, off, stride, sizes = comm.allgather(
                 int(msg.bytes), lambda dst: self._check(lib().wg_shard_copy_msg(self._ctx, dst)), step=int(msg.step),
-                pack=pack)
+                pack=pack, read_heads=read_heads)
             self._gathered = gathered
             sz = (ctypes.c_uint64 * len(sizes))(*sizes)
             heads = getattr(comm, "heads", None)   # host copy of each message's 16-byte header, if the comm has it

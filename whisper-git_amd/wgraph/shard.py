@@ -55,10 +55,12 @@ class ShardComm:
         m = max(n, 16)
         return (m + 15) // 16 * 16
 
-    def allgather(self, nbytes: int, fill, step: int = 0, pack=None):
+    def allgather(self, nbytes: int, fill, step: int = 0, pack=None, read_heads=None):
         """fill(ptr) writes this rank's nbytes-long message to ptr (device or
         host memory); or, on a device transport, pack(slot_ptr, cap) writes the
-        whole slot (header + message) in stream order on the current stream.
+        whole slot (header + message) in stream order on the current stream,
+        and read_heads(ptr, stride) (optional) returns every slot's length and
+        message header as a (world, 3) uint64 array, read in stream order.
         Returns (gathered device tensor, payload offset, stride, sizes): rank
         r's message starts at offset + r * stride."""
         dev = self.device if self.on_device else torch.device("cpu")
@@ -80,9 +82,14 @@ class ShardComm:
                 dist.all_gather(list(out.view(self.world, stride).unbind(0)), send, group=self.group)
             self.collectives += 1
             # one device->host read: every slot's length and its message's 16-byte header
-            head = out.view(self.world, stride)[:, :32].cpu().numpy()
-            sizes = [int(x) for x in head[:, :8].copy().view(np.int64).reshape(-1)]
-            self.heads = np.ascontiguousarray(head[:, 16:32]).view(np.uint32).reshape(self.world, 4)
+            if self.on_device and read_heads is not None:
+                h = read_heads(out.data_ptr(), stride)
+                sizes = [int(x) for x in h[:, 0]]
+                self.heads = np.ascontiguousarray(h[:, 1:3]).view(np.uint32).reshape(self.world, 4)
+            else:
+                head = out.view(self.world, stride)[:, :32].cpu().numpy()
+                sizes = [int(x) for x in head[:, :8].copy().view(np.int64).reshape(-1)]
+                self.heads = np.ascontiguousarray(head[:, 16:32]).view(np.uint32).reshape(self.world, 4)
             if max(sizes) <= cap:
                 break
             cap = self.round_cap(max(sizes))
