@@ -89,6 +89,12 @@ def _lockstep(engines, begin):
         assert [int(x) for x in head[:, :8].copy().view(np.int64).reshape(-1)] == sizes
         assert not head[:, 8:16].any()
         heads = np.ascontiguousarray(head[:, 16:32]).view(np.uint32).reshape(W, 4)
+        # the engine's polled read of the same slot heads (what Engine._shard_loop uses over RCCL)
+        polled = np.empty(3 * W, np.uint64)
+        engines[0]._check(lib().wg_shard_slot_heads(engines[0]._ctx, slots.data_ptr(), stride, W, polled.ctypes.data))
+        polled = polled.reshape(W, 3)
+        assert [int(x) for x in polled[:, 0]] == sizes
+        assert np.array_equal(np.ascontiguousarray(polled[:, 1:3]).view(np.uint32).reshape(W, 4), heads)
         sz = (ctypes.c_uint64 * W)(*sizes)
         for r, e in enumerate(engines):
             e._check(lib().wg_shard_exchange(e._ctx, slots.data_ptr() + ShardComm.HDR, stride, sz,
