@@ -271,14 +271,18 @@ int wg_shard_copy_msg(wg_ctx *ctx, void *dst);
  * engine's stream without a host synchronisation: a 16-byte header (message
  * length as u64, then zeros), then the message when it fits in `cap` bytes
  * (the payload's first 16 bytes are zero for shorter messages).  `slot` is
- * 16-byte aligned and holds 16 + max(cap, 16) bytes.  The caller orders its
+ * 16-byte aligned and holds 16 + cap bytes; `cap` is a multiple of 16, >= 16
+ * (WG_E_INVALID otherwise).  The caller orders its
  * all-gather after the engine's stream (e.g. RCCL on that same stream). */
 int wg_shard_pack_slot(wg_ctx *ctx, void *slot, uint64_t cap);
 /* Read the heads of all-gathered slots in the engine's stream order: per rank
  * r, out[3r] = the slot's u64 length and out[3r+1..3r+2] = its message's
  * 16-byte header (the `heads` wg_shard_exchange takes).  One small device
  * read the host polls for, instead of a copy + stream synchronisation by the
- * transport.  world <= 21; `gathered` and `stride` 8-byte aligned. */
+ * transport.  world <= 21; `gathered` 16-byte aligned; `stride` (= 16 + the
+ * slots' cap) a multiple of 16, >= 32 (WG_E_INVALID otherwise).
+ * wg_shard_exchange checks every length a message header announces against
+ * that rank's entry of `sizes` and fails with WG_E_INVALID on a mismatch. */
 int wg_shard_slot_heads(wg_ctx *ctx, const void *gathered, uint64_t stride, int world, uint64_t *out);
 /* Deliver the all-gathered messages; runs to the next exchange or the end.
  * Every message starts with a 16-byte header; `heads` (may be NULL) is a host

@@ -42,7 +42,9 @@ def main():
 
     def read_heads(ptr, stride):   # the engine's polled read (what Engine._shard_loop passes)
         h = np.empty(3 * comm.world, np.uint64)
-        wgraph.lib().wg_shard_slot_heads(eng._ctx, ptr, stride, comm.world, h.ctypes.data)
+        rc = wgraph.lib().wg_shard_slot_heads(eng._ctx, ptr, stride, comm.world, h.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"wg_shard_slot_heads: {rc}")
         return h.reshape(comm.world, 3)
 
     for _ in range(20):

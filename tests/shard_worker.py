@@ -109,6 +109,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", required=True, help="kind:n:seed,...")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--transport", choices=("host", "device"), default="host",
+                    help="device: HIP tensors through gloo, slots packed in stream order and their heads read by "
+                         "the engine's polled wg_shard_slot_heads (the path bench.py takes over RCCL)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -122,11 +125,12 @@ def main():
         torch.cuda.set_device(dev)
         eng = wgraph.Engine(0)
         eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-        comm = ShardComm(dev)
+        comm = ShardComm(dev, initial_cap=16, device_transport=args.transport == "device")
         for case in args.cases.split(","):
             kind, n, seed = case.split(":")
             run_case(eng, comm, torch, kind, int(n), int(seed), world, rank, errors)
-        result = {"ok": not errors, "errors": errors[:20], "exchanges": comm.exchanges}
+        result = {"ok": not errors, "errors": errors[:20], "exchanges": comm.exchanges,
+                  "collectives": comm.collectives, "on_device": comm.on_device}
         eng.close()
     except Exception:
         result = {"ok": False, "errors": errors[:20] + [traceback.format_exc()]}

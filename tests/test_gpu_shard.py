@@ -25,12 +25,13 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_world(world, cases, tmp_path):
-    out = tmp_path / f"w{world}"
+def run_world(world, cases, tmp_path, transport="host"):
+    out = tmp_path / f"w{world}{transport}"
     out.mkdir()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
-           os.path.join(ROOT, "tests", "shard_worker.py"), "--cases", cases, "--out", str(out)]
+           os.path.join(ROOT, "tests", "shard_worker.py"), "--cases", cases, "--out", str(out),
+           "--transport", transport]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     p = subprocess.run(cmd, cwd=ROOT, env=env, timeout=600, capture_output=True, text=True)
     results = []
@@ -45,6 +46,17 @@ def run_world(world, cases, tmp_path):
 
 def test_two_shards(tmp_path):
     run_world(2, "wide16:60000:3,random13:30000:4,linux:40000:5,linear:5000:6,anomaly:3000:7,wide16:3:8", tmp_path)
+
+
+def test_two_shards_device_transport(tmp_path):
+    """Engine.shard_build / shard_geometry through ShardComm's device path
+    (what bench.py runs over RCCL): slots packed by wg_shard_pack_slot on
+    torch's stream, gathered as HIP tensors (gloo: RCCL refuses two ranks on
+    one GPU), heads read by wg_shard_slot_heads; the slots start at 16 bytes,
+    so every exchange point also takes the overflow-and-resend path once."""
+    res = run_world(2, "wide16:60000:3,linux:40000:5,random13:30000:4,anomaly:3000:7", tmp_path, "device")
+    assert all(r["on_device"] for r in res)
+    assert all(r["collectives"] > r["exchanges"] for r in res)
 
 
 def test_three_shards(tmp_path):
@@ -82,6 +94,13 @@ def _lockstep(engines, begin):
         cap = ShardComm.round_cap(max(int(m.bytes) for m in msgs))
         stride = cap + ShardComm.HDR
         slots = torch.empty(W * stride, dtype=torch.uint8, device="cuda")
+        if rounds == 0:   # size contract: caps / strides that are not 16k bytes (k >= 1) are refused
+            e0 = engines[0]
+            for bad in (0, 8, 24):
+                assert lib().wg_shard_pack_slot(e0._ctx, slots.data_ptr(), bad) == abi.WG_E_INVALID
+            junk = np.empty(3 * W, np.uint64)
+            for bad in (16, 24, 40):
+                assert lib().wg_shard_slot_heads(e0._ctx, slots.data_ptr(), bad, W, junk.ctypes.data) == abi.WG_E_INVALID
         for r, e in enumerate(engines):
             e._check(lib().wg_shard_pack_slot(e._ctx, slots.data_ptr() + r * stride, cap))
         head = slots.view(W, stride)[:, :32].cpu().numpy()

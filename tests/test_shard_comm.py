@@ -70,3 +70,18 @@ def test_shard_rows_partition(n, world):
     for (a, b), (c, d) in zip(bounds, bounds[1:]):
         assert b == c and a <= b
     assert max(b - a for a, b in bounds) - min(b - a for a, b in bounds) <= 1
+
+
+@pytest.mark.parametrize("initial,want", [(0, 16), (1, 16), (15, 16), (16, 16), (17, 32), (4096, 4096), (4100, 4112)])
+def test_initial_slot_is_a_valid_pack_capacity(initial, want):
+    """wg_shard_pack_slot takes capacities that are multiples of 16, >= 16 (its
+    header kernel writes 32 bytes): the first exchange uses the rounded cap."""
+    port = _free_port()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        assert ShardComm(torch.device("cpu"), initial_cap=initial).initial_cap == want
+        with pytest.raises(ValueError):
+            ShardComm(torch.device("cpu"), device_transport=True)
+    finally:
+        dist.destroy_process_group()

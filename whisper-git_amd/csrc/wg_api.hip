@@ -5,6 +5,7 @@
 // every failure returns a negative status with a message in wg_last_error().
 #include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdarg>
 #include <cstring>
 #include <new>
@@ -126,20 +127,37 @@ static int fetch_launch(wg_ctx *c, int n, const WgFetch *items, uint64_t slot0) 
     return WG_OK;
 }
 
-// Spin on the region's sequence word (a few us after k_fetch ends, where a
-// runtime wait costs tens of us of wake-up and bookkeeping); false after 5 ms:
-// the caller takes the runtime wait, which also reports a failed launch.
+static inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#elif defined(__aarch64__)
+    asm volatile("yield");
+#endif
+}
+
+// Wait for the region's sequence word (k_fetch stores it last, system-scope
+// release): a few us after k_fetch ends, where a runtime wait costs tens of
+// us of wake-up and bookkeeping.  Busy for the first 50 us only (a read
+// queued behind a slow collective would otherwise hold a core), then
+// polling with a yield between reads; false after 5 ms: the caller takes
+// the runtime wait, which also reports a failed launch.
 static bool fetch_spin(wg_ctx *c, int region) {
     volatile uint64_t *w = (volatile uint64_t *)c->h_fetch + 3 * FETCH_MAX + region;
     const uint64_t want = c->fetch_want[region];
     const auto t0 = std::chrono::steady_clock::now();
+    bool busy = true;
     for (uint32_t i = 1;; i++) {
         if (*w == want) {
             std::atomic_thread_fence(std::memory_order_acquire);
             return true;
         }
-        __builtin_ia32_pause();
-        if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) return false;
+        if (busy) {
+            cpu_relax();
+            if ((i & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(50)) busy = false;
+        } else {
+            std::this_thread::yield();
+            if ((i & 15u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) return false;
+        }
     }
 }
 

@@ -84,6 +84,7 @@ struct ShardState {
     uint64_t row_base = 0;    // index of row s in the context's row arrays
     DevBuf msg;               // this rank's outgoing message
     const uint32_t *heads = nullptr;   // host copy of the gathered 16-byte headers (one exchange call)
+    const uint64_t *sizes = nullptr;   // every rank's message length (one exchange call)
     uint64_t msg_bytes = 0;
     DevBuf ptable;            // id partition table (global duplicate check)
     DevBuf prow;              // int32 [E1-E0] parent rows of own references
@@ -116,6 +117,11 @@ struct FontSlot {
     std::vector<wg_glyph> glyphs;
     DevBuf edges, gdesc, cov, sdf, gin, gout, d2in, d2out, gtab;
 };
+
+// workspace slots in wg_ctx::lf (wg_lanes_fast.hip; the sharded build reuses LF_EVREC / LF_AUX for the
+// gathered event records)
+enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_CH, LF_SPA, LF_SPB, LF_EVREC,
+       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_COUNT };
 
 struct wg_ctx {
     int         device = 0;
@@ -151,7 +157,7 @@ struct wg_ctx {
     DevBuf lane_out;        // uint32 [N]  layouts.get(id).lane per row
     DevBuf color_out;       // uint8  [N]
     DevBuf lane_scalars;    // uint32 [8]  max_lane, n_slots, overflow, ...
-    DevBuf lf[24];          // event-compressed lane path workspaces (wg_lanes_fast.hip)
+    DevBuf lf[LF_COUNT];    // event-compressed lane path workspaces (wg_lanes_fast.hip), indexed by LF_*
     uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)

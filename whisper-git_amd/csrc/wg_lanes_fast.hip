@@ -387,9 +387,6 @@ __global__ void k_lf_events_finish(uint64_t nev, uint32_t world, const uint64_t 
 
 }  // namespace
 
-// workspace slots in c->lf
-enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_CH, LF_SPA, LF_SPB, LF_EVREC,
-       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX };
 
 static const uint32_t *lf_sp(wg_ctx *c) { return c->lf_sp_b ? c->lf[LF_SPB].as<const uint32_t>() : c->lf[LF_SPA].as<const uint32_t>(); }
 

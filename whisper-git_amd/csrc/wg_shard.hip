@@ -452,6 +452,14 @@ static int read_headers(wg_ctx *c, const void *gathered, uint64_t stride, std::v
     return WG_OK;
 }
 
+// a rank's message must hold what its header announces (a mismatch would turn into reads past its slot)
+static int check_len(wg_ctx *c, int r, uint64_t need, const char *what) {
+    if (need > c->sh.sizes[r])
+        return wg_fail(c, WG_E_INVALID, "%s: rank %d announces %llu bytes, sent %llu", what, r, (unsigned long long)need,
+                       (unsigned long long)c->sh.sizes[r]);
+    return WG_OK;
+}
+
 static LfRange sh_range(wg_ctx *c) {
     ShardState &S = c->sh;
     LfRange R;
@@ -529,7 +537,11 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     if (rc != WG_OK) return rc;
     std::vector<uint64_t> cnt(W);
     RankCounts nown{};
-    for (int r = 0; r < W; r++) { nown.v[r] = hdr[4 * r]; cnt[r] = hdr[4 * r] + hdr[4 * r + 1]; }
+    for (int r = 0; r < W; r++) {
+        nown.v[r] = hdr[4 * r];
+        cnt[r] = (uint64_t)hdr[4 * r] + hdr[4 * r + 1];
+        if ((rc = check_len(c, r, 16 + cnt[r] * 16, "X6 endpoint records")) != WG_OK) return rc;
+    }
     WG_ALLOC(c, S.xchild, nx * 16 + 16);
     WG_ALLOC(c, S.xpar, nx * 16 + 16);
     Sections SX = make_sections(gathered, stride, W, cnt);
@@ -713,7 +725,9 @@ int wg_shard_copy_msg(wg_ctx *c, void *dst) {
 }
 
 int wg_shard_pack_slot(wg_ctx *c, void *slot, uint64_t cap) {
-    if (!c || !slot || (reinterpret_cast<uintptr_t>(slot) & 15u)) return WG_E_INVALID;
+    // k_sh_slot_head writes 32 bytes (slot header + the first 16 message bytes, zero when the message is
+    // longer than the slot) and the receivers read 16-byte vectors: cap is a multiple of 16, >= 16
+    if (!c || !slot || (reinterpret_cast<uintptr_t>(slot) & 15u) || cap < 16 || (cap & 15u)) return WG_E_INVALID;
     if (!c->sh.on || c->sh.step == SH_IDLE) return wg_fail(c, WG_E_STATE, "no sharded call in progress");
     (void)hipSetDevice(c->device);
     const uint64_t b = c->sh.msg_bytes;
@@ -726,7 +740,10 @@ int wg_shard_pack_slot(wg_ctx *c, void *slot, uint64_t cap) {
 }
 
 int wg_shard_slot_heads(wg_ctx *c, const void *gathered, uint64_t stride, int world, uint64_t *out) {
-    if (!c || !gathered || !out || world < 1 || 3 * world > 64 || ((reinterpret_cast<uintptr_t>(gathered) | stride) & 7u))
+    // every slot is read up to byte 32 (length header + the message's 16-byte header): slots of
+    // wg_shard_pack_slot, stride = cap + 16 with cap a multiple of 16, >= 16
+    if (!c || !gathered || !out || world < 1 || 3 * world > 64 || (reinterpret_cast<uintptr_t>(gathered) & 15u) ||
+        stride < 32 || (stride & 15u))
         return WG_E_INVALID;
     (void)hipSetDevice(c->device);
     WgFetch it[64];
@@ -744,7 +761,8 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
     if (!c || !out || !sizes) return WG_E_INVALID;
     ShardState &S = c->sh;
     S.heads = heads;   // valid for this call only
-    struct ClearHeads { ShardState &S; ~ClearHeads() { S.heads = nullptr; } } clear_heads{S};
+    S.sizes = sizes;
+    struct ClearHeads { ShardState &S; ~ClearHeads() { S.heads = nullptr; S.sizes = nullptr; } } clear_heads{S};
     const int W = S.world;
     if (!S.on || S.step == SH_IDLE) return wg_fail(c, WG_E_STATE, "no sharded call in progress");
     for (int r = 0; r < W; r++)
@@ -763,6 +781,8 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         for (int r = 0; r < W; r++) {
             bad |= hdr[4 * r] != 0;
             S.uoffs[r + 1] = S.uoffs[r] + hdr[4 * r + 1];
+            if (!bad && (rc = check_len(c, r, 16 + (uint64_t)hdr[4 * r + 1] * 32, "X1 unresolved references")) != WG_OK)
+                return rc;
         }
         if (bad) return sh_fallback(c, out);
         const uint64_t L = S.uoffs[W];
@@ -780,6 +800,8 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
     }
     case SH_X2: {   // rows of every unresolved reference -> crossing table; lanes up to the chain tokens
         const uint64_t L = S.uoffs[W];
+        for (int r = 0; r < W; r++)
+            if ((rc = check_len(c, r, L * 4, "X2 rows")) != WG_OK) return rc;
         std::vector<uint64_t> dummy(W, 0);
         Sections SF = make_sections(gathered, stride, W, dummy);
         WG_ALLOC(c, S.xt, L * 4 + 16);         // row per record
@@ -850,6 +872,12 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         }
         if (bad || S.evoff[W] >= (1ull << 30)) return sh_fallback(c, out);
         const uint64_t nx = S.xoff[W];
+        for (int r = 0; r < W; r++) {
+            const uint64_t tok_b = ((S.xoff[r + 1] - S.xoff[r]) * 4 + 15) & ~15ull;
+            if ((rc = check_len(c, r, 16 + tok_b + (uint64_t)hdr[4 * r] * 16 + (uint64_t)hdr[4 * r + 1] * 4,
+                                "X3 tokens and event records")) != WG_OK)
+                return rc;
+        }
         WG_ALLOC(c, S.xtok, nx * 4 + 16);
         WG_ALLOC(c, S.xt, nx * 4 + 16);
         for (int r = 0; r < W; r++) {
@@ -865,7 +893,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
                                    S.dev_small.as<const uint64_t>() + 32, S.xtok.as<const uint32_t>(), S.xt.as<uint32_t>());
         // every rank's records (after its tokens, 16-byte aligned): rank r's events at evoff[r], aux words at auxoff[r]
         const uint64_t nev = S.evoff[W], naux = S.auxoff[W];
-        DevBuf &evrec = c->lf[10], &aux = c->lf[18];
+        DevBuf &evrec = c->lf[LF_EVREC], &aux = c->lf[LF_AUX];
         WG_ALLOC(c, evrec, (nev + 256) * 16);
         WG_ALLOC(c, aux, naux * 4 + 4);
         WG_HIP(c, hipMemsetAsync(evrec.as<uint4>() + nev, 0, 256 * 16, st));

@@ -36,13 +36,20 @@ class ShardComm:
 
     HDR = 16
 
-    def __init__(self, device: torch.device, group=None, initial_cap: int = 4096):
+    def __init__(self, device: torch.device, group=None, initial_cap: int = 4096, device_transport: bool | None = None):
+        """device_transport: gather device-resident slots (default: only on an
+        "nccl" group).  True on a gloo group moves HIP tensors through gloo,
+        which lets several ranks on ONE GPU (RCCL refuses a duplicate GPU)
+        exercise the stream-ordered slot path bench.py takes over RCCL."""
         self.device = device
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.on_device = dist.get_backend(group) == "nccl"
-        self.initial_cap = initial_cap
+        self.backend = dist.get_backend(group)
+        self.on_device = self.backend == "nccl" if device_transport is None else bool(device_transport)
+        if self.on_device and device.type == "cpu":
+            raise ValueError("a device transport needs a HIP device")
+        self.initial_cap = self.round_cap(initial_cap)   # wg_shard_pack_slot takes caps of 16k bytes, k >= 1
         self.caps: dict[int, int] = {}
         self.exchanges = 0
         self.collectives = 0
@@ -76,7 +83,7 @@ class ShardComm:
                 if nbytes and nbytes <= cap:
                     fill(send.data_ptr() + self.HDR)
             out = torch.empty(self.world * stride, dtype=torch.uint8, device=dev)
-            if self.on_device:
+            if self.on_device and self.backend == "nccl":
                 dist.all_gather_into_tensor(out, send, group=self.group)
             else:
                 dist.all_gather(list(out.view(self.world, stride).unbind(0)), send, group=self.group)
