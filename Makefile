@@ -1,7 +1,9 @@
 # Build recipes.  `make` builds everything that ships to the GPU box:
 #   whisper-git_amd/wgraph/libwgraph.so   the HIP engine (gfx950) + C ABI
 #   whisper-git_amd/wgraph/libwgsynth.so  synthetic DAG generator (workload)
+#   whisper-git_amd/wgraph/libwgraph_host.so  C++ GraphLayout mirror over the C ABI
 #   oracle/liboracle.so                   CPU oracle (test infrastructure)
+#   tests/cpp/test_graph_layout           C++ tests of the mirror (engine vs oracle)
 #   profiles/microbench/store_ceiling     16-B store bandwidth ceiling (roofline context)
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
@@ -13,17 +15,28 @@ HIPHDR  := $(wildcard $(CSRC)/*.h) include/wgraph.h include/wgraph_tess.h
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt \
             -Wall -Wno-unused-function -Iinclude -I$(CSRC)
+CXXFLAGS_HOST := -O2 -std=c++17 -fPIC -Wall -Wextra -Iinclude
 CFLAGS_ORACLE := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 
-all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so profiles/microbench/store_ceiling
+all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgraph_host.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so \
+     tests/cpp/test_graph_layout profiles/microbench/store_ceiling
 
 $(PKG)/wgraph/libwgraph.so: $(HIPSRC) $(HIPHDR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIPSRC)
 
-$(PKG)/wgraph/libwgsynth.so: $(PKG)/synth/wg_synth.c
+$(PKG)/wgraph/libwgraph_host.so: $(PKG)/host/graph_layout.cpp $(PKG)/host/graph_layout.hpp include/wgraph.h $(PKG)/wgraph/libwgraph.so
+	g++ $(CXXFLAGS_HOST) -shared -o $@ $(PKG)/host/graph_layout.cpp -L$(PKG)/wgraph -lwgraph -Wl,-rpath,'$$ORIGIN'
+
+tests/cpp/test_graph_layout: tests/cpp/test_graph_layout.cpp $(PKG)/host/graph_layout.hpp oracle/wg_oracle.h \
+                             $(PKG)/synth/wg_synth.h $(PKG)/wgraph/libwgraph_host.so oracle/liboracle.so $(PKG)/wgraph/libwgsynth.so
+	g++ $(CXXFLAGS_HOST) -I$(PKG)/host -Ioracle -I$(PKG)/synth -o $@ tests/cpp/test_graph_layout.cpp \
+	    -L$(PKG)/wgraph -lwgraph_host -lwgraph -lwgsynth -Loracle -loracle \
+	    -Wl,-rpath,'$$ORIGIN/../../$(PKG)/wgraph' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+$(PKG)/wgraph/libwgsynth.so: $(PKG)/synth/wg_synth.c $(PKG)/synth/wg_synth.h
 	gcc -O2 -std=c11 -fPIC -shared -Wall -o $@ $< -lm
 
-oracle/liboracle.so: oracle/wg_oracle.c include/wgraph.h include/wgraph_tess.h
+oracle/liboracle.so: oracle/wg_oracle.c oracle/wg_oracle.h include/wgraph.h include/wgraph_tess.h
 	gcc $(CFLAGS_ORACLE) -shared -o $@ oracle/wg_oracle.c -lm
 
 profiles/microbench/store_ceiling: profiles/microbench/store_ceiling.hip
@@ -32,8 +45,9 @@ profiles/microbench/store_ceiling: profiles/microbench/store_ceiling.hip
 oracle: oracle/liboracle.so
 synth: $(PKG)/wgraph/libwgsynth.so
 engine: $(PKG)/wgraph/libwgraph.so
+host: $(PKG)/wgraph/libwgraph_host.so tests/cpp/test_graph_layout
 
 clean:
-	rm -f $(PKG)/wgraph/*.so oracle/*.so profiles/microbench/store_ceiling
+	rm -f $(PKG)/wgraph/*.so oracle/*.so profiles/microbench/store_ceiling tests/cpp/test_graph_layout
 
-.PHONY: all clean oracle synth engine
+.PHONY: all clean oracle synth engine host

@@ -213,6 +213,10 @@ int wg_copy_edges(wg_ctx *ctx, wg_edge *edges);
 
 /* compute_row_heights (:486-507) on the commits of the last build. */
 int wg_copy_row_heights(wg_ctx *ctx, float *heights);
+/* compute_row_heights(&[CommitInfo]) (:486-507), the free function: heights
+ * of any n-row time list (`time`, `heights` both in `residency` memory),
+ * independent of the context's layout.  Bit-exact (threshold table). */
+int wg_compute_row_heights(wg_ctx *ctx, const int64_t *time, uint64_t n, int32_t residency, float *heights);
 
 /* ---- per-frame geometry (row_geometry_with_bands, :367-399) --------------
  * band == NULL reproduces GraphLayout::row_geometry from build (:322-346);

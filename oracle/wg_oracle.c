@@ -31,6 +31,7 @@
 
 #include "../include/wgraph.h"
 #include "../include/wgraph_tess.h"
+#include "wg_oracle.h"
 
 /* ------------------------------------------------------------------------ */
 /* HashMap<Oid, V> with 20-byte keys (std HashMap stand-in, :242, :272-274)  */
@@ -259,24 +260,7 @@ void wgo_compute_row_heights(uint64_t n, const int64_t *time, float *heights) {
 /* ------------------------------------------------------------------------ */
 /* Outputs                                                                    */
 /* ------------------------------------------------------------------------ */
-typedef struct wgo_geometry {
-    uint64_t  n, n_vert, n_curve;
-    float    *height, *node_y, *row_top;
-    uint32_t *vert_off, *vert, *curve_off;
-    wg_curve *curve;
-    uint8_t  *curve_color;
-} wgo_geometry;
-
-typedef struct wgo_layout {
-    uint64_t  n, n_edges;
-    uint32_t  max_lane, n_slots;
-    float     graph_width;
-    uint32_t *lane;       /* per row: layouts.get(&commits[row].id).lane  */
-    uint8_t  *color;
-    wg_edge  *edges;
-    float    *heights;
-    wgo_geometry geom;    /* self.row_geometry from build()               */
-} wgo_layout;
+/* wgo_geometry / wgo_layout: oracle/wg_oracle.h */
 
 static int flatten(rowgeom *rows, uint64_t n, const float *row_top_y, wgo_geometry *g) {
     memset(g, 0, sizeof(*g));

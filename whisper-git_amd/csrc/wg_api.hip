@@ -469,6 +469,29 @@ int wg_copy_row_heights(wg_ctx *c, float *h) {
     return WG_OK;
 }
 
+// compute_row_heights (:486-507) as the free function it is in the reference:
+// heights of any time list, independent of the context's layout
+int wg_compute_row_heights(wg_ctx *c, const int64_t *time, uint64_t n, int32_t residency, float *heights) {
+    if (!c || (n && (!time || !heights))) return WG_E_INVALID;
+    if (residency != WG_HOST && residency != WG_DEVICE) return wg_fail(c, WG_E_INVALID, "bad residency %d", residency);
+    if (n == 0) return WG_OK;
+    (void)hipSetDevice(c->device);
+    const int64_t *d_time = time;
+    float *d_out = heights;
+    if (residency == WG_HOST) {
+        WG_ALLOC(c, c->hs_time, n * 8);
+        WG_ALLOC(c, c->hs_out, n * 4);
+        WG_HIP(c, hipMemcpyAsync(c->hs_time.p, time, n * 8, hipMemcpyHostToDevice, c->stream));
+        d_time = c->hs_time.as<const int64_t>();
+        d_out = c->hs_out.as<float>();
+    }
+    int rc = wg_heights_run(c, n, n, d_out, d_time);
+    if (rc != WG_OK) return rc;
+    if (residency == WG_HOST) WG_HIP(c, hipMemcpyAsync(heights, d_out, n * 4, hipMemcpyDeviceToHost, c->stream));
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    return WG_OK;
+}
+
 // ---------------------------------------------------------------------------
 // row_geometry_with_bands (:367-399)
 // ---------------------------------------------------------------------------

@@ -142,6 +142,7 @@ struct wg_ctx {
     float    graph_width = 24.0f;
     // inputs (device copies when the caller passed host memory)
     DevBuf in_oid, in_time, in_poff, in_poid, in_flags;
+    DevBuf hs_time, hs_out;   // wg_compute_row_heights scratch (independent of the layout)
     const uint8_t  *d_oid = nullptr;
     const int64_t  *d_time = nullptr;
     const uint32_t *d_poff = nullptr;
@@ -343,7 +344,8 @@ int wg_lf_events_finish(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uin
 int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
                        bool *ok);
 int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
-int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out);             // rows [0,m) of an n-row list
+int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out,
+                   const int64_t *time = nullptr);   // rows [0,m) of an n-row list (time: the layout's)
 // side stream (wg_api.hip): wg_side_fork makes the context's launches go to
 // the side stream (ordered after the work queued so far) until wg_side_done;
 // wg_side_join orders the main stream after that work (no host wait).

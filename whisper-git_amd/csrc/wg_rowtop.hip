@@ -660,12 +660,13 @@ void wg_init_height_thresholds(uint32_t *th) {
 
 extern "C" void wg_debug_height_thresholds(uint32_t *out28) { wg_init_height_thresholds(out28); }
 
-int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out) {
+int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out, const int64_t *time) {
     if (m == 0) return WG_OK;
+    if (!time) time = c->d_time;
     Thresh th;
     for (int k = 0; k < 28; k++) th.t[k] = c->h_thresh[k];
     wg_stage_begin(c, "heights");
-    hipLaunchKernelGGL(k_heights, dim3((m + 255) / 256), dim3(256), 0, c->stream, m, n, c->d_time, th, out);
+    hipLaunchKernelGGL(k_heights, dim3((m + 255) / 256), dim3(256), 0, c->stream, m, n, time, th, out);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;

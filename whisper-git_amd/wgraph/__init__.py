@@ -63,6 +63,7 @@ def lib():
             "wg_copy_lanes": ([vp, vp, vp], ctypes.c_int),
             "wg_copy_edges": ([vp, vp], ctypes.c_int),
             "wg_copy_row_heights": ([vp, vp], ctypes.c_int),
+            "wg_compute_row_heights": ([vp, vp, u64, i32, vp], ctypes.c_int),
             "wg_row_geometry": ([vp, vp, i32], ctypes.c_int),
             "wg_geometry_summary_get": ([vp, ctypes.POINTER(abi.GeometrySummary)], ctypes.c_int),
             "wg_copy_geometry": ([vp, ctypes.POINTER(abi.GeometryHost)], ctypes.c_int),
@@ -109,7 +110,7 @@ def lib():
 EXPORTED_SYMBOLS = (
     "wg_abi_version", "wg_create", "wg_destroy", "wg_last_error", "wg_set_stream", "wg_synchronize", "wg_set_option",
     "wg_layout_build", "wg_layout_summary_get", "wg_copy_lanes", "wg_copy_edges", "wg_copy_row_heights",
-    "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
+    "wg_compute_row_heights",    "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
     "wg_shard_copy_msg", "wg_shard_pack_slot", "wg_shard_slot_heads", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
@@ -606,9 +607,11 @@ class GraphLayout:
 def compute_row_heights(commits) -> np.ndarray:
     """compute_row_heights (:486-507) on the engine."""
     dag = commits if hasattr(commits, "parent_off") else commits_to_soa(commits)
+    t = np.ascontiguousarray(dag.time, np.int64)
+    h = np.empty(len(t), np.float32)
     e = Engine()
     try:
-        e.build(dag)
-        return e.row_heights()
+        e._check(lib().wg_compute_row_heights(e._ctx, t.ctypes.data, len(t), abi.WG_HOST, h.ctypes.data))
+        return h
     finally:
         e.close()
