@@ -34,10 +34,16 @@ __device__ __forceinline__ uint32_t pack_vert(uint32_t lane, uint32_t kind, uint
 
 // RowGeometry {height, node_y} + per-row strip flags
 // rows [lo, n) (lo > 0: a frame whose bands equal the last frame's below lo)
+// zws / nz4 (full geometry pass): the stage's zero-initialised workspace,
+// cleared here (grid-stride, 16-byte stores) instead of by a separate fill —
+// the counting kernels that accumulate into it run after this one
 __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
                             const float *__restrict__ row_top, float *__restrict__ height, float *__restrict__ node_y,
-                            uint8_t *__restrict__ rowflags, uint64_t lo = 0) {
-    uint64_t r = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                            uint8_t *__restrict__ rowflags, uint64_t lo = 0, uint4 *__restrict__ zws = nullptr,
+                            uint64_t nz4 = 0) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t i = tid; i < nz4; i += (uint64_t)gridDim.x * blockDim.x) zws[i] = make_uint4(0u, 0u, 0u, 0u);
+    uint64_t r = lo + tid;
     if (r >= n) return;
     float ht, ny;
     if (band) {
@@ -59,13 +65,18 @@ __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float
     rowflags[r] = f;
 }
 
+// per-row list counts (difference arrays for the spans) and, in the same pass
+// over the edges, the sweep's carry-in counts per 64-row chunk (carry_diff)
 __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
-                              uint32_t *cntB, uint32_t *cntT, uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend) {
+                              uint32_t *cntB, uint32_t *cntT, uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend,
+                              uint32_t *carry_diff) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ne) return;
     const wg_edge e = edges[k];
     const uint32_t c = e.child_row, p = e.parent_row;
     if (c >= p) return;                                   // (:526-528)
+    const uint32_t k0 = c / WG_SWEEP_CH + 1, k1 = p / WG_SWEEP_CH;
+    if (k0 <= k1) { atomicAdd(&carry_diff[k0], 1u); atomicAdd(&carry_diff[k1 + 1], 0xFFFFFFFFu); }
     if (e.child_lane == e.parent_lane) {
         atomicAdd(&cntB[c], 1u);
         atomicAdd(&cntT[p], 1u);
@@ -103,12 +114,23 @@ __global__ void k_bottom(uint64_t n, const uint32_t *__restrict__ edge_off, cons
     }
 }
 
-__global__ void k_top_collect(uint64_t ne, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
-                              const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert) {
+// one pass over the edges: same-lane edges' ids into their parent row's
+// top-half slots (sorted and packed by k_top_finish), and every edge into
+// the carry-in list of each 64-row chunk it is alive across (sorted by
+// k_carry_sort)
+__global__ void k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
+                            const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert,
+                            const uint32_t *__restrict__ carry_off, uint32_t *carry_fill, uint32_t *carry) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ne) return;
     const wg_edge e = edges[k];
-    if (!(e.child_row < e.parent_row && e.child_lane == e.parent_lane)) return;
+    if (e.child_row >= e.parent_row) return;
+    const uint32_t k0 = e.child_row / WG_SWEEP_CH + 1, k1 = e.parent_row / WG_SWEEP_CH;
+    for (uint32_t q = k0; q <= k1; q++) {
+        const uint32_t pos = atomicAdd(&carry_fill[q], 1u);
+        carry[carry_off[q] + pos] = (uint32_t)k;
+    }
+    if (e.child_lane != e.parent_lane) return;
     const uint32_t p = e.parent_row;
     const uint32_t pos = atomicAdd(&top_fill[p], 1u);
     vert[vert_off[p] + scanF[p + 1] + pos] = (uint32_t)k;   // edge id, packed below
@@ -134,30 +156,10 @@ __global__ void k_top_finish(uint64_t n, const wg_edge *__restrict__ edges, cons
 }
 
 // ---- carry-in registration for the sweep -------------------------------------
-__global__ void k_carry_diff(uint64_t ne, const wg_edge *__restrict__ edges, uint32_t *diff) {
-    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ne) return;
-    const wg_edge e = edges[k];
-    if (e.child_row >= e.parent_row) return;
-    const uint32_t k0 = e.child_row / WG_SWEEP_CH + 1, k1 = e.parent_row / WG_SWEEP_CH;
-    if (k0 <= k1) { atomicAdd(&diff[k0], 1u); atomicAdd(&diff[k1 + 1], 0xFFFFFFFFu); }
-}
 __global__ void k_carry_counts(uint64_t nch, const uint32_t *__restrict__ scan, uint32_t *__restrict__ cnt) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nch) return;
     cnt[k] = scan[k + 1];
-}
-__global__ void k_carry_fill(uint64_t ne, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ carry_off,
-                             uint32_t *fill, uint32_t *carry) {
-    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ne) return;
-    const wg_edge e = edges[k];
-    if (e.child_row >= e.parent_row) return;
-    const uint32_t k0 = e.child_row / WG_SWEEP_CH + 1, k1 = e.parent_row / WG_SWEEP_CH;
-    for (uint32_t q = k0; q <= k1; q++) {
-        const uint32_t pos = atomicAdd(&fill[q], 1u);
-        carry[carry_off[q] + pos] = (uint32_t)k;
-    }
 }
 // rank sort of each chunk's carry list (one wave per chunk; lists are short)
 __global__ void __launch_bounds__(64) k_carry_sort(uint64_t nch, const uint32_t *__restrict__ carry_off,
@@ -600,7 +602,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     // last region is an all-zero flag row: the lists are swept as a superset.
     const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
     const uint64_t rowa = (n + 2 + 63) & ~63ull, cha = (nch + 2 + 63) & ~63ull;
-    const uint64_t zwords = 6 * rowa + 2 * cha + 64 + rowa / 4;
+    const uint64_t zwords = (6 * rowa + 2 * cha + 64 + rowa / 4 + 3) & ~3ull;   // cleared in 16-byte units
     WG_ALLOC(c, c->geom_zero, zwords * 4);
     uint32_t *cntF = c->geom_zero.as<uint32_t>(), *cntT = cntF + rowa, *cntB = cntT + rowa;
     uint32_t *cntC = cntB + rowa, *cntCend = cntC + rowa, *top_fill = cntCend + rowa;
@@ -609,17 +611,17 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     uint32_t *voff = c->vert_off.as<uint32_t>(), *soff = c->scurve_off.as<uint32_t>();
 
     wg_stage_begin(c, "geom_counts");
-    WG_HIP(c, hipMemsetAsync(c->geom_zero.p, 0, zwords * 4, s));
     hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
-                       c->g_node_y.as<float>(), c->rowflags.as<uint8_t>());
+                       c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), (uint64_t)0, c->geom_zero.as<uint4>(),
+                       (uint64_t)(zwords / 4));
     if (ne)
-        hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntB, cntT, cntF, cntC, cntCend);
+        hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntB, cntT, cntF, cntC, cntCend,
+                           carry_cnt);
     WG_HIP(c, wg_exclusive_scan2_u32(cntF, cntF, cntC, cntC, n + 1, c->scan_tmp.p, s));
     hipLaunchKernelGGL(k_row_counts, dim3(blocks(n)), dim3(T), 0, s, n, cntF, cntC, cntT, cntB, cntCend, zflags, voff, soff);
     WG_HIP(c, wg_exclusive_scan2_u32(voff, voff, soff, soff, n, c->scan_tmp.p, s));
     // carry-in registration
     WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
-    if (ne) hipLaunchKernelGGL(k_carry_diff, dim3(blocks(ne)), dim3(T), 0, s, ne, E, carry_cnt);
     WG_HIP(c, wg_exclusive_scan_u32(carry_cnt, carry_cnt, nch + 1, c->scan_tmp.p, s));
     hipLaunchKernelGGL(k_carry_counts, dim3(blocks(nch)), dim3(T), 0, s, nch, (const uint32_t *)carry_cnt,
                        c->carry_off.as<uint32_t>());
@@ -645,11 +647,9 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     wg_stage_begin(c, "geom_lists");
     uint32_t *vert = c->vert.as<uint32_t>();
     hipLaunchKernelGGL(k_bottom, dim3(blocks(n)), dim3(T), 0, s, n, edge_off, E, voff, cntF, cntT, vert);
-    if (ne) {
-        hipLaunchKernelGGL(k_top_collect, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, vert);
-        hipLaunchKernelGGL(k_carry_fill, dim3(blocks(ne)), dim3(T), 0, s, ne, E, c->carry_off.as<const uint32_t>(),
-                           carry_fill, c->carry.as<uint32_t>());
-    }
+    if (ne)
+        hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, vert,
+                           c->carry_off.as<const uint32_t>(), carry_fill, c->carry.as<uint32_t>());
     hipLaunchKernelGGL(k_top_finish, dim3(blocks(n)), dim3(T), 0, s, n, E, voff, cntF, cntT, vert);
     uint32_t *carry_sorted = c->carry.as<uint32_t>() + ncarry + 2;
     hipLaunchKernelGGL(k_carry_sort, dim3(nch), dim3(64), 0, s, nch, c->carry_off.as<const uint32_t>(),
