@@ -457,7 +457,9 @@ int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
  * Copies up to n (<= 16) 32-bit engine counters of the last layout build:
  * [0] max_lane, [1] slots, [2] lane-table overflow, [3] fixed-point
  * iterations of the lane-event replay, [4] lane events, [5] build mode
- * (0 single, 1 row-sharded, 2 row-sharded request built whole).           */
+ * (0 single, 1 row-sharded, 2 row-sharded request built whole), [6]
+ * speculative builds (one host read per build) on this context, [7] of
+ * which the lanes and [8] the geometry were redone by the exact stages.  */
 int wg_debug_counters(wg_ctx *ctx, uint32_t *out, int n);
 
 #ifdef __cplusplus

@@ -1,0 +1,70 @@
+"""Speculative builds (wg_layout_build with one host read):
+once an exact build has sized a context's buffers, later builds launch
+everything on upper bounds and capacities and validate once at the end;
+what did not hold is redone by the exact stages.  One fresh engine walks a
+sequence of lists through every branch — same list again (no redo), larger
+lists (geometry past its capacity), a list that is not well formed (lanes
+redone by the exact walk), a list whose replay needs more iterations than the
+blind count — and every build is bit-exact against the oracle."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_bits
+from wgraph import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def full_check(eng, d, o, tag):
+    s = eng.layout_summary()
+    assert s.max_lane == o.max_lane, tag
+    assert np.float32(s.graph_width) == np.float32(o.graph_width), tag
+    lane, color = eng.lanes()
+    assert_bits(tag + " lane", lane, o.lane)
+    assert_bits(tag + " color", color, o.color)
+    assert_bits(tag + " edges", eng.edges(), o.edges)
+    got = eng.geometry()
+    for k, v in o.geometry.items():
+        assert_bits(f"{tag} build_{k}", got[k], v)
+    gs = eng.geometry_summary()
+    assert gs.n_vert == len(o.geometry["vert"]) and gs.n_curve == len(o.geometry["curve"]), tag
+    eng.row_geometry(d.band)
+    og = o.row_geometry(d.band)
+    got = eng.geometry()
+    for k, v in og.items():
+        assert_bits(f"{tag} band_{k}", got[k], v)
+    gs = eng.geometry_summary()   # the frame pass's summary is read lazily
+    assert np.float32(gs.total_height) == og["row_top"][-1] and gs.n_curve == len(og["curve"]), tag
+    sel = d.n // 2
+    eng.emit_vertices(0, d.n, selected=sel)
+    ov, _ = o.emit_vertices(0, d.n, selected=sel)
+    from oracle import oracle_c
+    assert eng.vertex_summary().checksum == oracle_c.vertex_checksum(ov), tag
+
+
+def test_speculative_build_sequence():
+    import wgraph
+    from oracle import oracle_c
+    eng = wgraph.Engine(0)
+    try:
+        seq = [("wide16", 3000, 1), ("wide16", 3000, 1), ("wide16", 3000, 2), ("wide16", 40000, 3),
+               ("anomaly", 2000, 4), ("random13", 20000, 5), ("linux", 60000, 6), ("linux", 60000, 6),
+               ("linear", 500, 7), ("wide16", 40000, 3)]
+        redo = []
+        for i, (kind, n, seed) in enumerate(seq):
+            d = synth.generate(kind, n, seed=seed)
+            o = oracle_c.OracleLayout(d)
+            eng.build(d)
+            c = eng.debug_counters()
+            redo.append((int(c[6]), int(c[7]), int(c[8])))
+            full_check(eng, d, o, f"#{i} {kind}/{n}")
+            o.close()
+        builds, redo_lanes, redo_geom = redo[-1]
+        assert builds == len(seq) - 1                 # every build after the first speculated
+        assert redo[1] == (1, 0, 0)                   # the same list again: nothing redone
+        assert redo[3][2] > redo[2][2]                # 40k rows after 3k: lists past their capacity
+        assert redo[4][1] > redo[3][1]                # duplicate ids / skewed parents: the exact walk
+        assert redo[9][2] == redo[8][2]               # 40k rows again: the buffers fit, the geometry stands
+        assert redo[7][1:] == redo[6][1:]             # the Linux-shaped list again: blind count adapted, no redo
+    finally:
+        eng.close()

@@ -390,14 +390,53 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     WG_ALLOC(c, c->heights, n * 4 + 4);
     WG_ALLOC(c, c->g_row_top, (n + 1) * 4);
     if ((rc = wg_side_zero_rowtop(c, n, c->heights.as<float>(), c->g_row_top.as<float>(), 0)) != WG_OK) return rc;
+    // Speculative build (once an exact build has sized this context's
+    // buffers): no host read until the end — event records and edges sized by
+    // upper bounds, the replay run for the last build's iteration count, the
+    // geometry lists sized by the buffers in place, every count read by the
+    // kernels from the device — then one read validating all of it.  What did
+    // not hold (a list that is not well formed, a replay short of its fixed
+    // point, a list past its capacity) is redone by the exact stages.
+    struct SpecOff { wg_ctx *c; ~SpecOff() { c->spec = false; } } spec_off{c};
+    c->spec = c->spec_ready && !c->force_general_lanes && n > 0;
+    const bool spec = c->spec;
     if ((rc = wg_stage_hash_join(c)) != WG_OK) return rc;
-    if ((rc = wg_stage_lanes(c)) != WG_OK) return rc;
-    if ((rc = wg_stage_edges(c)) != WG_OK) return rc;
+    if ((rc = wg_stage_lanes(c, spec)) != WG_OK) return rc;
+    if ((rc = wg_stage_edges(c, spec)) != WG_OK) return rc;
     c->have_layout = true;
     c->layout_gen++;
     // self.row_geometry with the default node_y / zero bands (:322-346)
     if ((rc = wg_side_join(c)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
+    if (spec) {
+        WgFetch it[20];
+        int k = wg_lanes_spec_items(c, it);
+        k += wg_geom_spec_items(c, it + k);
+        it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + n, false};
+        uint64_t v[20] = {0};
+        if ((rc = wg_fetch_n(c, k, it, v)) != WG_OK) return rc;
+        c->spec = false;
+        const uint64_t ne = v[16];
+        const bool lanes_ok = wg_lanes_spec_check(c, v);
+        if (!lanes_ok) {   // the exact lane stage (fast path with its reads, or the general walk)
+            if ((rc = wg_stage_lanes(c, false)) != WG_OK) return rc;
+            if ((rc = wg_stage_edges(c, false, (int64_t)ne)) != WG_OK) return rc;
+            c->layout_gen++;
+        } else {
+            c->n_edges = ne;
+            const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
+            const float gw = (float)vis * WG_LANE_W;   // graph_width (:353-354)
+            c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
+        }
+        c->spec_builds++;
+        c->spec_redo_lanes += !lanes_ok;
+        if (!lanes_ok || !wg_geom_spec_check(c, v + 8)) {
+            c->spec_redo_geom++;
+            c->lists_gen = ~0ull;
+            if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
+        }
+    }
+    c->spec_ready = c->lists_gen == c->layout_gen;   // an exact or validated build: the buffers are sized
     c->have_geom = true;
     c->geom_key_gen = c->layout_gen;   // the geometry of (this layout, no bands)
     c->geom_key_band = false;
@@ -567,6 +606,7 @@ static int own_geometry_range(wg_ctx *c, uint64_t *v0, uint64_t *v1, uint64_t *c
 int wg_geometry_summary_get(wg_ctx *c, wg_geometry_summary *out) {
     if (!c || !out) return WG_E_INVALID;
     if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
+    if (const int rc = wg_geom_summary_sync(c)) return rc;
     out->n_rows = c->sh.e - c->sh.s;
     out->n_vert = c->n_vert;
     out->n_curve = c->n_curve;
@@ -590,6 +630,7 @@ int wg_geometry_summary_get(wg_ctx *c, wg_geometry_summary *out) {
 int wg_copy_geometry(wg_ctx *c, const wg_geometry_host *d) {
     if (!c || !d) return WG_E_INVALID;
     if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
+    if (const int rc = wg_geom_summary_sync(c)) return rc;
     const uint64_t n = c->sh.e - c->sh.s, b = c->sh.row_base;
     uint64_t v0 = 0, v1 = c->n_vert, c0 = 0, c1 = c->n_curve;
     if (c->sh.on) {
@@ -717,6 +758,9 @@ int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
     if (n > 3) out[3] = c->replay_iters;
     if (n > 4) out[4] = (uint32_t)c->n_events;
     if (n > 5) out[5] = c->sh.on ? (c->sh.replicated ? 2u : 1u) : 0u;
+    if (n > 6) out[6] = c->spec_builds;
+    if (n > 7) out[7] = c->spec_redo_lanes;
+    if (n > 8) out[8] = c->spec_redo_geom;
     return WG_OK;
 }
 

@@ -19,6 +19,7 @@
 //
 // Bit-exact f32: built with -ffp-contract=off and the exact operation order
 // of Cubic::y_at (:623-629), split's lerp (:657) and `dy * 0.4` (:557-562).
+#include <algorithm>
 #include <cstring>
 
 #include "wg_internal.h"
@@ -27,6 +28,21 @@ namespace {
 
 constexpr int T = 256;
 constexpr uint32_t RF_ZERO = 1u, RF_CHILD = 2u, RF_PARENT = 4u;
+
+// Capacity guard of a speculative geometry pass (the lists sized by the last
+// pass's capacities, the totals only known on the device): a kernel that
+// writes a list whose scanned total exceeds its capacity writes nothing and
+// raises the overflow word; the end-of-build validation redoes the pass.
+// Exact passes pass cap = ~0u.
+struct Cap {
+    const uint32_t *total;   // the list's scanned total (device)
+    uint32_t cap;
+};
+__device__ __forceinline__ bool over(Cap a, uint32_t *ovf) {
+    if (a.cap == ~0u || *a.total <= a.cap) return false;
+    if (threadIdx.x == 0) atomicOr(ovf, 1u);
+    return true;
+}
 
 __device__ __forceinline__ uint32_t pack_vert(uint32_t lane, uint32_t kind, uint32_t color) {
     return (lane & 0xFFFFFFu) | (kind << 24) | (color << 28);
@@ -69,9 +85,9 @@ __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float
 // over the edges, the sweep's carry-in counts per 64-row chunk (carry_diff)
 __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
                               uint32_t *cntB, uint32_t *cntT, uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend,
-                              uint32_t *carry_diff) {
+                              uint32_t *carry_diff, const uint32_t *__restrict__ ne_dev) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ne) return;
+    if (k >= ne || (ne_dev && k >= *ne_dev)) return;
     const wg_edge e = edges[k];
     const uint32_t c = e.child_row, p = e.parent_row;
     if (c >= p) return;                                   // (:526-528)
@@ -103,9 +119,9 @@ __global__ void k_row_counts(uint64_t n, const uint32_t *__restrict__ scanF, con
 
 __global__ void k_bottom(uint64_t n, const uint32_t *__restrict__ edge_off, const wg_edge *__restrict__ edges,
                          const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ scanF,
-                         const uint32_t *__restrict__ cntT, uint32_t *__restrict__ vert) {
+                         const uint32_t *__restrict__ cntT, uint32_t *__restrict__ vert, Cap vc, uint32_t *ovf) {
     uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
+    if (over(vc, ovf) || r >= n) return;
     uint32_t o = vert_off[r] + scanF[r + 1] + cntT[r];
     for (uint32_t k = edge_off[r]; k < edge_off[r + 1]; k++) {
         const wg_edge e = edges[k];
@@ -120,9 +136,11 @@ __global__ void k_bottom(uint64_t n, const uint32_t *__restrict__ edge_off, cons
 // k_carry_sort)
 __global__ void k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
                             const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert,
-                            const uint32_t *__restrict__ carry_off, uint32_t *carry_fill, uint32_t *carry) {
+                            const uint32_t *__restrict__ carry_off, uint32_t *carry_fill, uint32_t *carry,
+                            const uint32_t *__restrict__ ne_dev, Cap vc, Cap cc, uint32_t *ovf) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ne) return;
+    if (over(vc, ovf) || over(cc, ovf)) return;
+    if (k >= ne || (ne_dev && k >= *ne_dev)) return;
     const wg_edge e = edges[k];
     if (e.child_row >= e.parent_row) return;
     const uint32_t k0 = e.child_row / WG_SWEEP_CH + 1, k1 = e.parent_row / WG_SWEEP_CH;
@@ -137,9 +155,10 @@ __global__ void k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges, cons
 }
 
 __global__ void k_top_finish(uint64_t n, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
-                             const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT, uint32_t *vert) {
+                             const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT, uint32_t *vert, Cap vc,
+                             uint32_t *ovf) {
     uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
+    if (over(vc, ovf) || r >= n) return;
     const uint32_t nt = cntT[r];
     if (nt == 0) return;
     uint32_t *v = vert + vert_off[r] + scanF[r + 1];
@@ -163,9 +182,10 @@ __global__ void k_carry_counts(uint64_t nch, const uint32_t *__restrict__ scan, 
 }
 // rank sort of each chunk's carry list (one wave per chunk; lists are short)
 __global__ void __launch_bounds__(64) k_carry_sort(uint64_t nch, const uint32_t *__restrict__ carry_off,
-                                                    const uint32_t *__restrict__ carry, uint32_t *__restrict__ sorted) {
+                                                    const uint32_t *__restrict__ carry, uint32_t *__restrict__ sorted,
+                                                    Cap cc, uint32_t *ovf) {
     const uint64_t q = blockIdx.x;
-    if (q >= nch) return;
+    if (over(cc, ovf) || q >= nch) return;
     const uint32_t a = carry_off[q], b = carry_off[q + 1], len = b - a;
     for (uint32_t i = threadIdx.x; i < len; i += 64) {
         const uint32_t x = carry[a + i];
@@ -295,7 +315,8 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
-        uint32_t *__restrict__ err) {
+        uint32_t *__restrict__ err, Cap vc, Cap sc, uint32_t *ovf) {
+    if (over(vc, ovf) || over(sc, ovf)) return;
     __shared__ uint32_t s_eid[SW_WAVES][SW_CAP];
     __shared__ uint32_t s_c[SW_WAVES][SW_CAP];
     __shared__ uint32_t s_p[SW_WAVES][SW_CAP];
@@ -324,10 +345,10 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
         const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
-        uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap) {
+        uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, uint32_t *ovf) {
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t q = (uint64_t)blockIdx.x * SW_WAVES + (threadIdx.x >> 6);
-    if (q >= nch) return;
+    if (over(vc, ovf) || over(sc, ovf) || q >= nch) return;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
     const uint32_t a = carry_off[q], ncar = carry_off[q + 1] - a;
@@ -429,13 +450,16 @@ __device__ __forceinline__ Cubic subcurve(const Cubic &c, float a, float b) {   
 
 // pmin > 0: records of edges whose parent row is below pmin are left as they
 // are (a frame whose bands and row_top are unchanged above row pmin)
+// refilt (the frame pass): nonzero = the curve lists were refiltered by this
+// pass, so every record moved and pmin does not apply
 __global__ void k_curves(const uint32_t *__restrict__ nc, const uint32_t *__restrict__ curve_ref,
                          const uint32_t *__restrict__ curve_row, const wg_edge *__restrict__ edges,
                          const float *__restrict__ row_top, const float *__restrict__ node_y,
                          const float2 *__restrict__ edge_y, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color,
-                         uint32_t pmin) {
+                         uint32_t pmin, Cap sc, uint32_t *ovf, const uint32_t *__restrict__ refilt) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= *nc) return;   // grid sized by an upper bound; the count lives on the device
+    if (over(sc, ovf) || k >= *nc) return;   // grid sized by an upper bound; the count lives on the device
+    if (refilt && *refilt) pmin = 0;
     const uint32_t ref = curve_ref[k];
     const wg_edge e = edges[ref];
     if (e.parent_row < pmin) return;
@@ -478,11 +502,15 @@ __device__ __forceinline__ bool curve_kept(uint32_t r, const wg_edge &e, uint32_
     return skip == 0;
 }
 
+// cond (the frame pass): only when *cond (the row flags changed); otherwise
+// the current offsets' per-row counts, so the scan that follows reproduces them
 __global__ void k_curve_keep(uint64_t n, const uint32_t *__restrict__ soff, const uint32_t *__restrict__ sref,
                              const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
-                             uint32_t *__restrict__ cnt) {
+                             uint32_t *__restrict__ cnt, const uint32_t *__restrict__ cond,
+                             const uint32_t *__restrict__ cur_off, Cap sc, uint32_t *ovf) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
+    if (over(sc, ovf) || r >= n) return;
+    if (cond && !*cond) { cnt[r] = cur_off[r + 1] - cur_off[r]; return; }
     const uint32_t a = soff[r], b = soff[r + 1], f = rowflags[r];
     uint32_t k = b - a;
     if (f) {
@@ -494,9 +522,11 @@ __global__ void k_curve_keep(uint64_t n, const uint32_t *__restrict__ soff, cons
 
 __global__ void k_curve_compact(uint64_t n, const uint32_t *__restrict__ soff, const uint32_t *__restrict__ sref,
                                 const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
-                                const uint32_t *__restrict__ coff, uint32_t *__restrict__ ref, uint32_t *__restrict__ row) {
+                                const uint32_t *__restrict__ coff, uint32_t *__restrict__ ref, uint32_t *__restrict__ row,
+                                const uint32_t *__restrict__ cond, Cap sc, uint32_t *ovf) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
+    if (over(sc, ovf) || r >= n) return;
+    if (cond && !*cond) return;   // the lists stand
     const uint32_t a = soff[r], b = soff[r + 1], f = rowflags[r];
     uint32_t o = coff[r];
     for (uint32_t j = a; j < b; j++) {
@@ -517,29 +547,80 @@ __global__ void k_flags_diff(uint64_t n, const uint8_t *__restrict__ a, const ui
 
 }  // namespace
 
-// filter the curve superset by this pass's row flags -> curve_off / curve_ref / curve_row
-static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s) {
+// filter the curve superset by this pass's row flags -> curve_off / curve_ref / curve_row.
+// cond (the frame pass, on the device): refilter only if the flags changed —
+// otherwise the same offsets are rescanned and the lists stand, no host read.
+static Cap no_cap() { return Cap{nullptr, ~0u}; }
+static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *cond, Cap sc, uint32_t *ovf) {
     uint32_t *coff = c->curve_off.as<uint32_t>();
+    WG_ALLOC(c, c->curve_cnt, (n + 2) * 4);
+    uint32_t *cnt = c->curve_cnt.as<uint32_t>();
     hipLaunchKernelGGL(k_curve_keep, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
                        c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
-                       coff);
-    WG_HIP(c, wg_exclusive_scan_u32(coff, coff, n, c->scan_tmp.p, s));
+                       cnt, cond, (const uint32_t *)coff, sc, ovf);
+    WG_HIP(c, wg_exclusive_scan_u32(cnt, coff, n, c->scan_tmp.p, s));
     hipLaunchKernelGGL(k_curve_compact, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
                        c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
-                       (const uint32_t *)coff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>());
+                       (const uint32_t *)coff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), cond, sc, ovf);
     WG_ALLOC(c, c->rowflags_lists, n + 4);
     WG_HIP(c, hipMemcpyAsync(c->rowflags_lists.p, c->rowflags.p, n, hipMemcpyDeviceToDevice, s));
     WG_HIP(c, hipGetLastError());
     return WG_OK;
 }
 
-static void launch_curves(wg_ctx *c, uint64_t n, uint64_t n_upper, hipStream_t s, uint32_t pmin = 0) {
+static void launch_curves(wg_ctx *c, uint64_t n, uint64_t n_upper, hipStream_t s, uint32_t pmin, Cap sc, uint32_t *ovf,
+                          const uint32_t *refilt) {
     if (!n_upper) return;
     hipLaunchKernelGGL(k_curves, dim3(blocks(n_upper)), dim3(T), 0, s, c->curve_off.as<const uint32_t>() + n,
                        c->curve_ref.as<const uint32_t>(), c->curve_row.as<const uint32_t>(), c->edges.as<const wg_edge>(),
                        c->g_row_top.as<const float>(), c->g_node_y.as<const float>(),
                        reinterpret_cast<const float2 *>(c->edge_y), c->curve.as<wg_curve>(), c->curve_color.as<uint8_t>(),
-                       pmin);
+                       pmin, sc, ovf, refilt);
+}
+
+// the lazily read summary of the last pass (total height, scan path, curve count)
+int wg_geom_summary_sync(wg_ctx *c) {
+    if (!c->geom_sum_stale) return WG_OK;
+    uint64_t v[3] = {0, 0, 0};
+    const int rc = wg_fetch(c, {{c->geom_sum_at[0], false}, {c->geom_sum_at[1], false}, {c->geom_sum_at[2], false}}, v);
+    if (rc != WG_OK) return rc;
+    const uint32_t tbits = (uint32_t)v[0];
+    std::memcpy(&c->total_height, &tbits, 4);
+    c->scan_path = v[1] ? 1u : 0u;
+    c->n_curve = v[2];
+    c->geom_sum_stale = false;
+    return WG_OK;
+}
+
+// speculative full pass: its validation words (fills 8 items) and their check
+int wg_geom_spec_items(wg_ctx *c, WgFetch *it) {
+    const uint64_t n = c->n;
+    const uint32_t *err = c->geom_err;
+    it[0] = WgFetch{err + 8, false};                                   // capacity overflow
+    it[1] = WgFetch{err, false};                                       // > SW_CAP edges alive across a row
+    it[2] = WgFetch{c->vert_off.as<uint32_t>() + n, false};
+    it[3] = WgFetch{c->scurve_off.as<uint32_t>() + n, false};
+    it[4] = WgFetch{c->carry_off.as<uint32_t>() + (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH, false};
+    it[5] = WgFetch{c->g_row_top.as<uint32_t>() + n, false};
+    it[6] = WgFetch{c->rt_flags.as<uint32_t>() + 2, false};
+    it[7] = WgFetch{c->curve_off.as<uint32_t>() + n, false};
+    return 8;
+}
+
+// true = the speculative pass fit its capacities (the lists are exact)
+bool wg_geom_spec_check(wg_ctx *c, const uint64_t *v) {
+    if (v[0] || v[1]) return false;   // overflow: the exact pass sizes and redoes; too many edges: it fails
+    c->n_vert = v[2];
+    c->lists_nsuper = v[3];
+    const uint32_t tbits = (uint32_t)v[5];
+    std::memcpy(&c->total_height, &tbits, 4);
+    c->scan_path = v[6] ? 1u : 0u;
+    c->n_curve = v[7];
+    c->geom_sum_stale = false;
+    c->lists_gen = c->layout_gen;
+    c->lists_n = c->n;
+    c->lists_ne = c->n_edges;
+    return true;
 }
 
 int wg_stage_geometry(wg_ctx *c, const float *d_band) {
@@ -559,47 +640,49 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         // same layout: the lists stand; only the curve filter can change with the flags
         // a frame whose bands equal the last frame's below row r0 (wg_row_geometry):
         // rows below r0 keep height / node_y / flags, and curve records of edges
-        // that end above r0 keep their geometry (row_top up to r0 is unchanged)
+        // that end above r0 keep their geometry (row_top up to r0 is unchanged).
+        // No host read: whether the flags changed decides on the device (the
+        // refilter and the curve range); the summary is read when asked for.
         const uint64_t r0 = c->geom_r0 < n ? c->geom_r0 : 0;
         c->geom_r0 = 0;
         WG_ALLOC(c, c->geom_diff, 64);
         wg_stage_begin(c, "geom_reuse");
-        WG_HIP(c, hipMemsetAsync(c->geom_diff.p, 0, 4, s));
+        uint32_t *diff = c->geom_diff.as<uint32_t>();
         hipLaunchKernelGGL(k_row_basic, dim3(blocks(n - r0)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
-                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), r0);
+                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), r0, c->geom_diff.as<uint4>(), (uint64_t)1);
         hipLaunchKernelGGL(k_flags_diff, dim3(blocks(n - r0)), dim3(T), 0, s, n, c->rowflags.as<const uint8_t>(),
-                           c->rowflags_lists.as<const uint8_t>(), c->geom_diff.as<uint32_t>(), r0);
-        uint64_t chk[3] = {1, 0, 0};
-        int rc = wg_fetch(c, {{c->geom_diff.p, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false}}, chk);
+                           c->rowflags_lists.as<const uint8_t>(), diff, r0);
+        int rc = filter_curves(c, n, s, diff, no_cap(), diff + 8);
         if (rc != WG_OK) return rc;
-        if (chk[0]) {
-            if ((rc = filter_curves(c, n, s)) != WG_OK) return rc;
-            uint64_t nc = 0;
-            if ((rc = wg_fetch(c, {{c->curve_off.as<uint32_t>() + n, false}}, &nc)) != WG_OK) return rc;
-            c->n_curve = nc;
-        }
         wg_stage_end(c);
         wg_stage_begin(c, "geom_curves");
         // re-filtered lists move every record: all of them are recomputed then
-        launch_curves(c, n, c->n_curve, s, chk[0] ? 0u : (uint32_t)r0);
+        launch_curves(c, n, c->lists_nsuper, s, (uint32_t)r0, no_cap(), diff + 8, diff);
         WG_HIP(c, hipGetLastError());
         wg_stage_end(c);
-        const uint32_t tbits = (uint32_t)chk[1];
-        std::memcpy(&c->total_height, &tbits, 4);
-        c->scan_path = chk[2] ? 1u : 0u;
+        c->geom_sum_at[0] = rt + n;
+        c->geom_sum_at[1] = c->rt_flags.as<uint32_t>() + 2;
+        c->geom_sum_at[2] = c->curve_off.as<uint32_t>() + n;
+        c->geom_sum_stale = true;
         return WG_OK;
     }
+    const bool spec = c->spec;
     c->lists_gen = ~0ull;
     c->n_vert = c->n_curve = 0;
+    c->geom_sum_stale = false;
     if (n == 0) {
         WG_HIP(c, hipMemsetAsync(c->vert_off.p, 0, 4, s));
         WG_HIP(c, hipMemsetAsync(c->curve_off.p, 0, 4, s));
+        c->lists_nsuper = 0;
         return WG_OK;
     }
     const wg_edge *E = c->edges.as<const wg_edge>();
     const uint32_t *edge_off = c->edge_cnt.as<const uint32_t>();
-    // every array that starts at zero lives in one workspace: one memset.  The
-    // last region is an all-zero flag row: the lists are swept as a superset.
+    // speculative build: the edge count is on the device (ne is its upper bound)
+    const uint32_t *ne_dev = spec ? edge_off + n : nullptr;
+    // every array that starts at zero lives in one workspace, cleared by the
+    // pass's first kernel.  The last region is an all-zero flag row: the lists
+    // are swept as a superset.
     const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
     const uint64_t rowa = (n + 2 + 63) & ~63ull, cha = (nch + 2 + 63) & ~63ull;
     const uint64_t zwords = (6 * rowa + 2 * cha + 64 + rowa / 4 + 3) & ~3ull;   // cleared in 16-byte units
@@ -607,6 +690,8 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     uint32_t *cntF = c->geom_zero.as<uint32_t>(), *cntT = cntF + rowa, *cntB = cntT + rowa;
     uint32_t *cntC = cntB + rowa, *cntCend = cntC + rowa, *top_fill = cntCend + rowa;
     uint32_t *carry_cnt = top_fill + rowa, *carry_fill = carry_cnt + cha, *sweep_err = carry_fill + cha;
+    uint32_t *ovf = sweep_err + 8;   // capacity overflow of a speculative pass
+    c->geom_err = sweep_err;
     const uint8_t *zflags = reinterpret_cast<const uint8_t *>(sweep_err + 64);
     uint32_t *voff = c->vert_off.as<uint32_t>(), *soff = c->scurve_off.as<uint32_t>();
 
@@ -616,65 +701,88 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
                        (uint64_t)(zwords / 4));
     if (ne)
         hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntB, cntT, cntF, cntC, cntCend,
-                           carry_cnt);
+                           carry_cnt, ne_dev);
     WG_HIP(c, wg_exclusive_scan2_u32(cntF, cntF, cntC, cntC, n + 1, c->scan_tmp.p, s));
     hipLaunchKernelGGL(k_row_counts, dim3(blocks(n)), dim3(T), 0, s, n, cntF, cntC, cntT, cntB, cntCend, zflags, voff, soff);
     WG_HIP(c, wg_exclusive_scan2_u32(voff, voff, soff, soff, n, c->scan_tmp.p, s));
     // carry-in registration
     WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
+    uint32_t *carry_off = c->carry_off.as<uint32_t>();
     WG_HIP(c, wg_exclusive_scan_u32(carry_cnt, carry_cnt, nch + 1, c->scan_tmp.p, s));
-    hipLaunchKernelGGL(k_carry_counts, dim3(blocks(nch)), dim3(T), 0, s, nch, (const uint32_t *)carry_cnt,
-                       c->carry_off.as<uint32_t>());
-    WG_HIP(c, wg_exclusive_scan_u32(c->carry_off.as<uint32_t>(), c->carry_off.as<uint32_t>(), nch, c->scan_tmp.p, s));
-    uint64_t tot[3] = {0, 0, 0};
-    {
-        const int rc = wg_fetch(c, {{voff + n, false}, {soff + n, false}, {c->carry_off.as<uint32_t>() + nch, false}}, tot);
+    hipLaunchKernelGGL(k_carry_counts, dim3(blocks(nch)), dim3(T), 0, s, nch, (const uint32_t *)carry_cnt, carry_off);
+    WG_HIP(c, wg_exclusive_scan_u32(carry_off, carry_off, nch, c->scan_tmp.p, s));
+    // list capacities: exact from the totals, or (speculative build) the
+    // buffers as the last pass left them, checked on the device
+    Cap vc = no_cap(), sc = no_cap(), cc = no_cap();
+    uint64_t n_super_grid = 0;
+    if (!spec) {
+        uint64_t tot[3] = {0, 0, 0};
+        const int rc = wg_fetch(c, {{voff + n, false}, {soff + n, false}, {carry_off + nch, false}}, tot);
         if (rc != WG_OK) return rc;
+        c->n_vert = tot[0];
+        const uint64_t n_super = tot[1];
+        const uint64_t ncarry = tot[2];
+        WG_ALLOC(c, c->vert, c->n_vert * 4 + 16);
+        WG_ALLOC(c, c->scurve_ref, n_super * 4 + 16);
+        WG_ALLOC(c, c->scurve_row, n_super * 4 + 16);
+        WG_ALLOC(c, c->curve, n_super * sizeof(wg_curve) + 64);
+        WG_ALLOC(c, c->curve_color, n_super + 16);
+        WG_ALLOC(c, c->curve_ref, n_super * 4 + 16);
+        WG_ALLOC(c, c->curve_row, n_super * 4 + 16);
+        WG_ALLOC(c, c->carry, ncarry * 4 + 16);
+        WG_ALLOC(c, c->carry_sorted, ncarry * 4 + 16);
+        n_super_grid = n_super;
+    } else {
+        auto cap_of = [](const DevBuf &b, size_t elem) -> uint64_t { return b.cap / elem; };
+        const uint64_t vcap = cap_of(c->vert, 4);
+        uint64_t scap = cap_of(c->scurve_ref, 4);
+        scap = std::min(scap, cap_of(c->scurve_row, 4));
+        scap = std::min(scap, cap_of(c->curve, sizeof(wg_curve)));
+        scap = std::min(scap, cap_of(c->curve_color, 1));
+        scap = std::min(scap, cap_of(c->curve_ref, 4));
+        scap = std::min(scap, cap_of(c->curve_row, 4));
+        const uint64_t ccap = std::min(cap_of(c->carry, 4), cap_of(c->carry_sorted, 4));
+        auto u32 = [](uint64_t v) { return (uint32_t)std::min<uint64_t>(v, 0xFFFFFFFEull); };
+        vc = Cap{voff + n, u32(vcap)};
+        sc = Cap{soff + n, u32(scap)};
+        cc = Cap{carry_off + nch, u32(ccap)};
+        n_super_grid = scap;
     }
     wg_stage_end(c);
-    c->n_vert = tot[0];
-    const uint64_t n_super = tot[1];
-    const uint64_t ncarry = tot[2];
-    WG_ALLOC(c, c->vert, c->n_vert * 4 + 16);
-    WG_ALLOC(c, c->scurve_ref, n_super * 4 + 16);
-    WG_ALLOC(c, c->scurve_row, n_super * 4 + 16);
-    WG_ALLOC(c, c->curve, n_super * sizeof(wg_curve) + 64);
-    WG_ALLOC(c, c->curve_color, n_super + 16);
-    WG_ALLOC(c, c->curve_ref, n_super * 4 + 16);
-    WG_ALLOC(c, c->curve_row, n_super * 4 + 16);
-    WG_ALLOC(c, c->carry, ncarry * 8 + 16);
 
     wg_stage_begin(c, "geom_lists");
     uint32_t *vert = c->vert.as<uint32_t>();
-    hipLaunchKernelGGL(k_bottom, dim3(blocks(n)), dim3(T), 0, s, n, edge_off, E, voff, cntF, cntT, vert);
+    hipLaunchKernelGGL(k_bottom, dim3(blocks(n)), dim3(T), 0, s, n, edge_off, E, voff, cntF, cntT, vert, vc, ovf);
     if (ne)
         hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, vert,
-                           c->carry_off.as<const uint32_t>(), carry_fill, c->carry.as<uint32_t>());
-    hipLaunchKernelGGL(k_top_finish, dim3(blocks(n)), dim3(T), 0, s, n, E, voff, cntF, cntT, vert);
-    uint32_t *carry_sorted = c->carry.as<uint32_t>() + ncarry + 2;
-    hipLaunchKernelGGL(k_carry_sort, dim3(nch), dim3(64), 0, s, nch, c->carry_off.as<const uint32_t>(),
-                       c->carry.as<const uint32_t>(), carry_sorted);
+                           (const uint32_t *)carry_off, carry_fill, c->carry.as<uint32_t>(), ne_dev, vc, cc, ovf);
+    hipLaunchKernelGGL(k_top_finish, dim3(blocks(n)), dim3(T), 0, s, n, E, voff, cntF, cntT, vert, vc, ovf);
+    uint32_t *carry_sorted = c->carry_sorted.as<uint32_t>();
+    hipLaunchKernelGGL(k_carry_sort, dim3(nch), dim3(64), 0, s, nch, (const uint32_t *)carry_off,
+                       c->carry.as<const uint32_t>(), carry_sorted, cc, ovf);
     // chunks too wide for the register sweep are listed in sweep_err[2..] and swept through LDS
     uint32_t *big_n = sweep_err + 1;
     WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
     hipLaunchKernelGGL(k_sweep, dim3((nch + SW_WAVES - 1) / SW_WAVES), dim3(64 * SW_WAVES), 0, s, n, nch, E, edge_off,
-                       c->carry_off.as<const uint32_t>(), (const uint32_t *)carry_sorted, zflags,
+                       (const uint32_t *)carry_off, (const uint32_t *)carry_sorted, zflags,
                        voff, (const uint32_t *)soff, vert, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
-                       c->sweep_big.as<uint32_t>(), big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS);
+                       c->sweep_big.as<uint32_t>(), big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS,
+                       vc, sc, ovf);
     hipLaunchKernelGGL(k_sweep_lds, dim3(64), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)c->sweep_big.as<uint32_t>(),
-                       (const uint32_t *)big_n, E, edge_off, c->carry_off.as<const uint32_t>(),
+                       (const uint32_t *)big_n, E, edge_off, (const uint32_t *)carry_off,
                        (const uint32_t *)carry_sorted, zflags, voff, (const uint32_t *)soff, vert,
-                       c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(), sweep_err);
+                       c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(), sweep_err, vc, sc, ovf);
     WG_HIP(c, hipGetLastError());
     {
-        const int rc = filter_curves(c, n, s);
+        const int rc = filter_curves(c, n, s, nullptr, sc, ovf);
         if (rc != WG_OK) return rc;
     }
     wg_stage_end(c);
     wg_stage_begin(c, "geom_curves");
-    launch_curves(c, n, n_super, s);
+    launch_curves(c, n, n_super_grid, s, 0u, sc, ovf, nullptr);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
+    if (spec) return WG_OK;   // validated at the end of the build (wg_geom_spec_items / wg_geom_spec_check)
     uint64_t fin[4] = {0, 0, 0, 0};
     {
         const int rc = wg_fetch(c, {{sweep_err, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false},
@@ -683,6 +791,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     }
     if (fin[0]) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP);
     c->n_curve = fin[3];
+    c->lists_nsuper = n_super_grid;
     c->lists_gen = c->layout_gen;
     c->lists_n = n;
     c->lists_ne = ne;

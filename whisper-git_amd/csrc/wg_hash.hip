@@ -97,8 +97,10 @@ int wg_stage_hash_join(wg_ctx *c) {
         hipLaunchKernelGGL(k_edge_cnt, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->d_poff,
                            c->prow.as<const int32_t>(), c->edge_cnt.as<uint32_t>());
         WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), n, c->scan_tmp.p, c->stream));
-        // read by wg_stage_edges after the lane stage's own synchronisation
-        if (const int rc = wg_fetch_defer(c, {{c->edge_cnt.as<uint32_t>() + n, false}})) return rc;
+        // read by wg_stage_edges after the lane stage's own synchronisation (a
+        // speculative build reads it with its end-of-build validation)
+        if (!c->spec)
+            if (const int rc = wg_fetch_defer(c, {{c->edge_cnt.as<uint32_t>() + n, false}})) return rc;
     }
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);

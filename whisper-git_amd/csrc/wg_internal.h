@@ -123,6 +123,19 @@ struct FontSlot {
 enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_CH, LF_SPA, LF_SPB, LF_EVREC,
        LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_COUNT };
 
+// event replay to a fixed point (wg_lanes_replay.hip)
+struct ReplayRun {
+    uint64_t nev = 0, nch = 0;
+    uint32_t chunk = 512, it = 0, max_iters = 0;
+    const uint4 *ev = nullptr;
+    const uint32_t *aux = nullptr;
+    uint8_t *slots_a = nullptr, *slots_b = nullptr, *sp_prev = nullptr, *sp_next = nullptr;   // sp_prev: last written
+    unsigned long long *occ_a = nullptr, *occ_b = nullptr, *op = nullptr, *on = nullptr;
+    uint32_t *stats = nullptr, *flags = nullptr, *scal = nullptr;
+    const uint32_t *nev_dev = nullptr;   // speculative build: event count on the device (nev = upper bound)
+    const uint32_t *gate = nullptr;      // speculative build: nonzero = not well formed, replay nothing
+};
+
 struct wg_ctx {
     int         device = 0;
     hipStream_t stream = nullptr;
@@ -166,6 +179,13 @@ struct wg_ctx {
     uint64_t e_refs_own = 0;   // parent references of the rows this context owns
     bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])
     bool force_general_lanes = false;   // WG_LANES=general (testing the general walk)
+    ReplayRun spec_run;     // the speculative build's replay (its iteration count and flag words)
+    // speculative build (wg_layout_build): launches sized by upper bounds and
+    // capacities, counts read by the kernels from the device, one host read at
+    // the end validating them (the exact form redoes anything that failed)
+    bool spec = false;          // the build in progress is speculative
+    bool spec_ready = false;    // an exact build sized this context's buffers (speculation may start)
+    uint32_t spec_builds = 0, spec_redo_lanes = 0, spec_redo_geom = 0;   // speculative builds, of which lanes / geometry redone
     // edges
     DevBuf edge_cnt;        // uint32 [N+1] -> edge_off after scan
     DevBuf edges;           // wg_edge [n_edges]
@@ -187,7 +207,12 @@ struct wg_ctx {
     DevBuf vert, curve, curve_color;
     DevBuf curve_ref;       // uint32 [n_curve] edge id per curve record
     DevBuf curve_row;       // uint32 [n_curve] row per curve record
-    DevBuf carry_off, carry;                // sweep carry-in lists
+    DevBuf carry_off, carry, carry_sorted;  // sweep carry-in lists (registration order / edge order)
+    DevBuf curve_cnt;                       // uint32 [N+1] per-row curve counts (filter)
+    uint64_t lists_nsuper = 0;              // curve superset records of the lists in place
+    uint32_t *geom_err = nullptr;           // the last full pass's flag words (sweep error, overflow at +8)
+    bool geom_sum_stale = false;            // total_height / scan_path / n_curve not read back yet
+    const void *geom_sum_at[3] = {nullptr, nullptr, nullptr};   // where they are (row_top[n], scan flag, curve_off[n])
     DevBuf scan_tmp;        // scan workspace
     DevBuf scal;            // uint64 [16] device scalars (totals)
     DevBuf rowflags;        // uint8 [N] bit0 zero-height strip, bit1 child strip empty, bit2 parent strip empty
@@ -311,23 +336,19 @@ hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, 
 
 // stages -------------------------------------------------------------------------
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
-int wg_stage_lanes(wg_ctx *c);                // wg_lanes.hip
-int wg_lanes_fast(wg_ctx *c, bool *used);     // wg_lanes_fast.hip
-// event replay to a fixed point (wg_lanes_replay.hip)
-struct ReplayRun {
-    uint64_t nev = 0, nch = 0;
-    uint32_t chunk = 512, it = 0, max_iters = 0;
-    const uint4 *ev = nullptr;
-    const uint32_t *aux = nullptr;
-    uint8_t *slots_a = nullptr, *slots_b = nullptr, *sp_prev = nullptr, *sp_next = nullptr;   // sp_prev: last written
-    unsigned long long *occ_a = nullptr, *occ_b = nullptr, *op = nullptr, *on = nullptr;
-    uint32_t *stats = nullptr, *flags = nullptr, *scal = nullptr;
-};
+int wg_stage_lanes(wg_ctx *c, bool spec);     // wg_lanes.hip
+int wg_lanes_fast(wg_ctx *c, bool *used, bool spec);   // wg_lanes_fast.hip
+
 hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blind);
+hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blind, uint4 *ev_pad);
 hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged);
-int wg_stage_edges(wg_ctx *c);                // wg_lanes.hip
+int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known = -1);   // wg_lanes.hip
+// speculative build (wg_layout_build): validation words of the lane build
+// (fills 8 items) and their check (wg_lanes_fast.hip)
+int wg_lanes_spec_items(wg_ctx *c, WgFetch *it);
+bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v);
 // event-compressed lane phases over a row range (wg_lanes_fast.hip)
-int wg_lf_refs(wg_ctx *c, const LfRange &R);   // + wg_lf_refs_end after queueing wg_lf_chain
+int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back);   // + wg_lf_refs_end after queueing wg_lf_chain
 int wg_lf_refs_end(wg_ctx *c, uint32_t *viol, uint64_t *nev, uint64_t *naux);
 int wg_lf_chain(wg_ctx *c, const LfRange &R);
 int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok);
@@ -358,6 +379,9 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
                   uint64_t row_lo);   // rows below row_lo: walked, not written
 int wg_stage_rowtop(wg_ctx *c, const float *d_band);   // wg_rowtop.hip
 int wg_stage_geometry(wg_ctx *c, const float *d_band); // wg_geom.hip
+int wg_geom_summary_sync(wg_ctx *c);                   // read a frame pass's summary when asked for
+int wg_geom_spec_items(wg_ctx *c, WgFetch *it);        // speculative full pass: 8 validation words
+bool wg_geom_spec_check(wg_ctx *c, const uint64_t *v);
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel);  // wg_vertex.hip
 int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out);  // wg_vertex.hip
 int wg_words_checksum(wg_ctx *c, const uint32_t *w, uint64_t nwords, uint64_t *out);  // wg_vertex.hip

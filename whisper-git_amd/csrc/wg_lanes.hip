@@ -188,7 +188,9 @@ hipError_t launch_general(wg_ctx *c) {
 
 }  // namespace
 
-int wg_stage_lanes(wg_ctx *c) {
+// spec: the speculative build (wg_layout_build validates afterwards; the
+// general walk is only taken from the exact form)
+int wg_stage_lanes(wg_ctx *c, bool spec) {
     const uint64_t n = c->n;
     WG_ALLOC(c, c->lane_asg, n * 4 + 4);
     WG_ALLOC(c, c->lane_scalars, 64);
@@ -201,8 +203,12 @@ int wg_stage_lanes(wg_ctx *c) {
     WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, c->stream));
     if (!c->force_general_lanes) {
         bool used = false;
-        int rc = wg_lanes_fast(c, &used);
+        int rc = wg_lanes_fast(c, &used, spec);
         if (rc != WG_OK) return rc;
+        if (spec) {   // max_lane / graph_width are set by the validation
+            wg_stage_end(c);
+            return WG_OK;
+        }
         if (used) {
             wg_stage_end(c);
             uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
@@ -232,7 +238,12 @@ int wg_stage_lanes(wg_ctx *c) {
     return WG_OK;
 }
 
-int wg_stage_edges(wg_ctx *c) {
+// ne_known >= 0: the edge count, already read.  spec: the edge count is not
+// read back here; the buffer is sized by its upper
+// bound (the parent references), c->n_edges holds that bound until the
+// end-of-build validation and the geometry kernels read the count from
+// edge_cnt[n] on the device
+int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known) {
     const uint64_t n = c->n;
     WG_ALLOC(c, c->lane_out, n * 4 + 4);
     WG_ALLOC(c, c->color_out, n + 4);
@@ -249,8 +260,10 @@ int wg_stage_edges(wg_ctx *c) {
     WG_HIP(c, hipGetLastError());
     // edge offsets: scanned after the hash join (wg_stage_hash_join); the
     // total was copied out then and the lane stage has synchronised since
-    uint64_t ne = 0;
-    if (const int rc = wg_fetch_deferred(c, &ne)) return rc;
+    uint64_t ne = c->e_refs;
+    if (ne_known >= 0) ne = (uint64_t)ne_known;   // read by the caller (a speculative build's validation)
+    else if (!spec)
+        if (const int rc = wg_fetch_deferred(c, &ne)) return rc;
     c->n_edges = ne;
     WG_ALLOC(c, c->edges, (uint64_t)ne * sizeof(wg_edge) + 16);
     hipLaunchKernelGGL(k_edges, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->edge_cnt.as<const uint32_t>(),

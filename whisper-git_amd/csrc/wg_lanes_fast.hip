@@ -288,9 +288,10 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
                             const uint32_t *__restrict__ ev_off, const uint32_t *__restrict__ aux_off,
                             const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
                             const uint32_t *__restrict__ secev, const uint32_t *__restrict__ sp,
-                            uint4 *__restrict__ ev, uint32_t *__restrict__ aux) {
+                            uint4 *__restrict__ ev, uint32_t *__restrict__ aux, const uint32_t *__restrict__ gate = nullptr) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= R.nl) return;
+    if (gate && *gate) return;   // speculative build: not well formed (the general walk takes over)
     const uint64_t gj = R.s + j;
     const uint32_t wi = winfo[j], w = wi & 0x3FFFFFFFu;
     const bool fp_in = wi & 0x40000000u, sec_first = wi & 0x80000000u;
@@ -338,9 +339,10 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
 }
 
 __global__ void k_lf_lanes(uint64_t nl, const uint32_t *__restrict__ sp, const uint8_t *__restrict__ slot_of,
-                           uint32_t *__restrict__ lane) {
+                           uint32_t *__restrict__ lane, const uint32_t *__restrict__ gate = nullptr) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nl) return;
+    if (gate && *gate) return;
     lane[j] = slot_of[sp[j] & ~WG_TOK_EV];
 }
 
@@ -390,7 +392,7 @@ __global__ void k_lf_events_finish(uint64_t nev, uint32_t world, const uint64_t 
 
 static const uint32_t *lf_sp(wg_ctx *c) { return c->lf_sp_b ? c->lf[LF_SPB].as<const uint32_t>() : c->lf[LF_SPA].as<const uint32_t>(); }
 
-int wg_lf_refs(wg_ctx *c, const LfRange &R) {
+int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back) {
     const uint64_t n = R.nl;
     hipStream_t s = c->stream;
     DevBuf &first_ref = c->lf[LF_FIRST], &fpc = c->lf[LF_FPC], &winfo = c->lf[LF_WINFO], &ev_off = c->lf[LF_EVOFF];
@@ -418,8 +420,11 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R) {
                               fpc.as<const uint32_t>(), winfo.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan2_u32(ev_off.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>(),
                                      aux_off.as<uint32_t>(), n, c->scan_tmp.p, s));
-    // read back while the chain phase runs (wg_lf_refs_end)
-    const int rc = wg_fetch_begin(c, {{flags.p, false}, {ev_off.as<uint32_t>() + n, false}, {aux_off.as<uint32_t>() + n, false}});
+    // read back while the chain phase runs (wg_lf_refs_end); a speculative
+    // build reads the same words with its end-of-build validation instead
+    const int rc = read_back ? wg_fetch_begin(c, {{flags.p, false}, {ev_off.as<uint32_t>() + n, false},
+                                                  {aux_off.as<uint32_t>() + n, false}})
+                             : WG_OK;
     wg_stage_end(c);
     return rc;
 }
@@ -600,8 +605,102 @@ int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *e
     return WG_OK;
 }
 
-// Single-GPU build.  Returns WG_OK with *used = false when the input needs the general walk.
-int wg_lanes_fast(wg_ctx *c, bool *used) {
+// Speculative single-GPU lane build (no host read-back): event records sized
+// by their upper bound n + E (each row makes at most max(1, parents)
+// events; merge token lists hold at most 4/3 (n + E) words), the event count
+// read by the kernels from the device, the replay run for the blind
+// iteration count of the last build, and every kernel after the
+// well-formedness check gated on its flag.  The validation words
+// (wg_lanes_spec_check) are read with the end-of-build validation.
+static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
+    const uint64_t n = R.nl;
+    int rc = wg_lf_refs(c, R, false);
+    if (rc != WG_OK) return rc;
+    if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
+    const uint64_t nev_cap = n + c->e_refs, naux_cap = 2 * (n + c->e_refs) + 16;
+    const uint32_t *gate = c->lf[LF_FLAGS].as<const uint32_t>();
+    const uint32_t *nev_dev = c->lf[LF_EVOFF].as<const uint32_t>() + n;
+    DevBuf &evrec = c->lf[LF_EVREC], &aux = c->lf[LF_AUX];
+    WG_ALLOC(c, evrec, (nev_cap + 256) * 16);
+    WG_ALLOC(c, aux, naux_cap * 4);
+    hipStream_t s = c->stream;
+    wg_stage_begin(c, "lf_events");
+    hipLaunchKernelGGL(k_lf_events<false>, dim3(blocks(n)), dim3(T), 0, s, R, 0u, 0u, (const uint32_t *)nullptr,
+                       c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
+                       c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
+                       c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
+                       c->lf[LF_SECEV].as<const uint32_t>(), lf_sp(c), evrec.as<uint4>(), aux.as<uint32_t>(), gate);
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    wg_stage_begin(c, "lf_loop");
+    ReplayRun &run = c->spec_run;
+    run = ReplayRun{};
+    run.nev = nev_cap;
+    run.chunk = c->replay_chunk;
+    const uint64_t nch = (nev_cap + run.chunk - 1) / run.chunk + 1;
+    run.max_iters = (uint32_t)nch + 1;
+    DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
+    DevBuf &rflags = c->lf[LF_RFLAGS];
+    WG_ALLOC(c, slot_a, nev_cap + 64);
+    WG_ALLOC(c, slot_b, nev_cap + 64);
+    WG_ALLOC(c, occ, nch * 16 + 16);
+    WG_ALLOC(c, stats, nch * 8 + 8);
+    WG_ALLOC(c, rflags, (run.max_iters + 2) * 4);
+    run.ev = evrec.as<const uint4>();
+    run.aux = aux.as<const uint32_t>();
+    run.slots_a = slot_a.as<uint8_t>();
+    run.slots_b = slot_b.as<uint8_t>();
+    run.occ_a = occ.as<unsigned long long>();
+    run.occ_b = occ.as<unsigned long long>() + nch;
+    run.stats = stats.as<uint32_t>();
+    run.flags = rflags.as<uint32_t>();
+    run.scal = c->lane_scalars.as<uint32_t>();
+    run.nev_dev = nev_dev;
+    run.gate = gate;
+    WG_HIP(c, wg_replay_start_spec(c, s, run, c->replay_blind < 2 ? 2u : c->replay_blind, evrec.as<uint4>()));
+    if (n) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(n)), dim3(T), 0, s, n, lf_sp(c), run.sp_prev,
+                              c->lane_asg.as<uint32_t>(), gate);
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    return WG_OK;
+}
+
+// The speculative lane build's validation words: {not well formed, events,
+// aux words, max_lane, slots, > 63 slots, changed at it - 1, changed at it}.
+int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
+    const uint64_t n = c->n;
+    const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
+    const ReplayRun &run = c->spec_run;
+    it[0] = WgFetch{c->lf[LF_FLAGS].p, false};
+    it[1] = WgFetch{c->lf[LF_EVOFF].as<uint32_t>() + n, false};
+    it[2] = WgFetch{c->lf[LF_AUXOFF].as<uint32_t>() + n, false};
+    it[3] = WgFetch{ls, false};
+    it[4] = WgFetch{ls + 1, false};
+    it[5] = WgFetch{ls + 2, false};
+    it[6] = WgFetch{run.flags + run.it - 1, false};
+    it[7] = WgFetch{run.flags + run.it, false};
+    return 8;
+}
+
+// Validation of a speculative lane build from those words: true = the lanes
+// are the greedy's (well formed, a fixed point, <= 63 slots); c->max_lane,
+// n_slots, n_events, the replay's blind count are updated.
+bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v) {
+    const bool conv = v[6] == 0 || v[7] == 0;
+    if (v[0] || v[5] || !conv) return false;
+    c->n_events = v[1];
+    c->max_lane = (uint32_t)v[3];
+    c->n_slots = (uint32_t)v[4];
+    c->replay_iters = c->spec_run.it;
+    if (v[6] == 0 && c->replay_blind > 2) c->replay_blind--;   // the fixed point came a launch early
+    c->lane_path = 0;
+    return true;
+}
+
+// Single-GPU build.  Returns WG_OK with *used = false when the input needs
+// the general walk.  spec: the speculative form (lanes_fast_spec), *used = true
+// and the caller validates.
+int wg_lanes_fast(wg_ctx *c, bool *used, bool spec) {
     *used = false;
     LfRange R;
     R.s = 0;
@@ -611,9 +710,14 @@ int wg_lanes_fast(wg_ctx *c, bool *used) {
     R.prow = c->prow.as<const int32_t>();
     R.canon = c->canon.as<const uint32_t>();
     c->e_refs_own = c->e_refs;
+    if (spec) {
+        const int rc = lanes_fast_spec(c, R);
+        *used = rc == WG_OK;
+        return rc;
+    }
     uint32_t viol = 0;
     uint64_t nev = 0, naux = 0;
-    int rc = wg_lf_refs(c, R);
+    int rc = wg_lf_refs(c, R, true);
     if (rc != WG_OK) return rc;
     rc = wg_lf_chain(c, R);                          // queued before the flags are back (bounded on any input)
     const int rc2 = wg_lf_refs_end(c, &viol, &nev, &naux);

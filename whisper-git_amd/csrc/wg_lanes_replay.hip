@@ -64,15 +64,19 @@ struct ReplayArgs {
     unsigned long long *occ_next;
     uint32_t *chunk_stats;      // per chunk: max_lane, max_slot
     uint32_t *changed;          // [iter] = 1 if iteration iter changed anything
+    const uint32_t *nev_dev;    // speculative build: the event count in device memory (nev = its upper bound)
+    const uint32_t *gate;       // speculative build: nonzero = the list is not well formed, replay nothing
 };
 
 __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
     const uint32_t lid = threadIdx.x & 63;
     if (A.changed[A.iter - 1] == 0) return;          // previous iteration was a fixed point
+    if (A.gate && *A.gate) return;
+    const uint64_t nev = A.nev_dev ? (uint64_t)*A.nev_dev : A.nev;
     const uint64_t c = blockIdx.x;
     const uint64_t e0 = c * A.chunk;
-    if (e0 >= A.nev) return;
-    const uint64_t e1 = (e0 + A.chunk < A.nev) ? e0 + A.chunk : A.nev;
+    if (e0 >= nev) return;
+    const uint64_t e1 = (e0 + A.chunk < nev) ? e0 + A.chunk : nev;
     uint64_t occ = c == 0 ? 0ull : A.occ_prev[c - 1];
     uint64_t occ_or = 0, alloc_or = 0;   // OR of the occupancy after each occupying allocation / of allocated slots
     bool diff = false;
@@ -267,8 +271,27 @@ __global__ void k_lf_replay_init(uint64_t nchunks, unsigned long long *occ_prev,
     if (i < nflags) changed[i] = (i == 0) ? 1u : 0u;
 }
 
-// final: max_lane / slots / overflow over all chunks
-__global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats, uint32_t *__restrict__ scal) {
+// speculative build: the initial state, the slots' initial guess (zero) and
+// the 256 no-op records after the events (the replay prefetches past a
+// chunk's end) in one launch, with the event count read on the device
+__global__ void k_lf_replay_init_spec(uint64_t nchunks, unsigned long long *occ_prev, uint32_t *changed, uint32_t nflags,
+                                      uint4 *__restrict__ slots16, uint64_t nslots16, uint4 *__restrict__ ev,
+                                      const uint32_t *__restrict__ nev_dev) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nchunks) occ_prev[i] = 0ull;
+    if (i < nflags) changed[i] = (i == 0) ? 1u : 0u;
+    if (i < nslots16) slots16[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (i < 256) ev[*nev_dev + i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// final: max_lane / slots / overflow over all chunks (nev_dev: chunks past the
+// device event count hold nothing)
+__global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats, uint32_t *__restrict__ scal,
+                                   const uint32_t *__restrict__ nev_dev = nullptr, uint32_t chunk = 1) {
+    if (nev_dev) {
+        const uint64_t nd = ((uint64_t)*nev_dev + chunk - 1) / chunk;
+        nchunks = nd < nchunks ? nd : nchunks;
+    }
     uint32_t ml = 0, ms = 0;
     for (uint64_t c = threadIdx.x; c < nchunks; c += blockDim.x) {
         ml = stats[2 * c] > ml ? stats[2 * c] : ml;
@@ -313,7 +336,7 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
     if (blind > R.max_iters) blind = R.max_iters;
     for (uint32_t k = 0; k < blind; k++) {
         R.it++;
-        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags};
+        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr};
         hipLaunchKernelGGL(k_lf_replay, dim3(R.nch), dim3(64), 0, s, a);
         // after a fixed point later iterations do nothing; the converged slots are
         // in both buffers, so either pointer is final
@@ -324,6 +347,37 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
     return hipGetLastError();
 }
 
+// Speculative build (no host read of the event count): R.nev is an upper
+// bound (the grid), R.nev_dev the count; `blind` iterations, then the
+// scalars.  The caller checks convergence (flags[it - 1], flags[it]) with
+// its end-of-build validation.
+hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blind, uint4 *ev_pad) {
+    R.nch = (R.nev + R.chunk - 1) / R.chunk;
+    R.it = 0;
+    R.sp_prev = R.slots_a;
+    R.sp_next = R.slots_b;
+    R.op = R.occ_a;
+    R.on = R.occ_b;
+    if (R.max_iters > R.nch + 1) R.max_iters = (uint32_t)(R.nch + 1);
+    if (blind > R.max_iters) blind = R.max_iters;
+    const uint64_t nslots16 = (R.nev + 15) / 16;
+    uint64_t ninit = R.nch > R.max_iters + 1 ? R.nch : R.max_iters + 1;
+    if (ninit < nslots16) ninit = nslots16;
+    if (ninit < 256) ninit = 256;
+    hipLaunchKernelGGL(k_lf_replay_init_spec, dim3((ninit + 255) / 256), dim3(256), 0, s, R.nch, R.occ_a, R.flags,
+                       R.max_iters + 1, reinterpret_cast<uint4 *>(R.slots_a), nslots16, ev_pad, R.nev_dev);
+    for (uint32_t k = 0; k < blind; k++) {
+        R.it++;
+        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, R.nev_dev,
+                     R.gate};
+        hipLaunchKernelGGL(k_lf_replay, dim3(R.nch), dim3(64), 0, s, a);
+        std::swap(R.sp_prev, R.sp_next);
+        std::swap(R.op, R.on);
+    }
+    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, R.nev_dev, R.chunk);
+    return hipGetLastError();
+}
+
 // Continue with polls (every 3rd iteration, then doubling) until a fixed
 // point or max_iters; *converged tells which.
 hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged) {
@@ -331,7 +385,7 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
     uint32_t next_poll = R.it + 3;
     while (!*converged && R.it < R.max_iters) {
         R.it++;
-        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags};
+        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr};
         hipLaunchKernelGGL(k_lf_replay, dim3(R.nch), dim3(64), 0, s, a);
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);

@@ -487,8 +487,8 @@ static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
     c->edge_y = nullptr;
     int rc;
     if ((rc = wg_stage_hash_join(c)) != WG_OK) return rc;
-    if ((rc = wg_stage_lanes(c)) != WG_OK) return rc;
-    if ((rc = wg_stage_edges(c)) != WG_OK) return rc;
+    if ((rc = wg_stage_lanes(c, false)) != WG_OK) return rc;
+    if ((rc = wg_stage_edges(c, false)) != WG_OK) return rc;
     if ((rc = wg_stage_heights(c)) != WG_OK) return rc;
     c->have_layout = true;
     c->layout_gen++;
@@ -836,7 +836,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         wg_stage_begin(c, "lanes");
         uint32_t viol = 0;
         uint64_t nev = 0, naux = 0;
-        if ((rc = wg_lf_refs(c, R)) != WG_OK) return rc;
+        if ((rc = wg_lf_refs(c, R, true)) != WG_OK) return rc;
         rc = wg_lf_chain(c, R);                   // queued before the flags are back
         const int rc2 = wg_lf_refs_end(c, &viol, &nev, &naux);
         if (rc != WG_OK) return rc;
