@@ -68,7 +68,13 @@ struct ReplayArgs {
     const uint32_t *gate;       // speculative build: nonzero = the list is not well formed, replay nothing
 };
 
+// The chunk's own slots of this iteration, mirrored in LDS: a batch reads the
+// slots of tokens born in the chunk's earlier batches right after the wave
+// stored them, which through global memory costs a full round trip per batch.
+constexpr uint32_t LSLOT_MAX = 4096;   // chunks up to this many events (WG_OPT_REPLAY_CHUNK)
+
 __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
+    __shared__ uint8_t lslot[LSLOT_MAX];
     const uint32_t lid = threadIdx.x & 63;
     if (A.changed[A.iter - 1] == 0) return;          // previous iteration was a fixed point
     if (A.gate && *A.gate) return;
@@ -77,6 +83,9 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
     const uint64_t e0 = c * A.chunk;
     if (e0 >= nev) return;
     const uint64_t e1 = (e0 + A.chunk < nev) ? e0 + A.chunk : nev;
+    const bool lds = A.chunk <= LSLOT_MAX;
+    // slot of a token born in this chunk before the current batch (this iteration)
+    auto own = [&](uint64_t t) -> uint32_t { return lds ? (uint32_t)lslot[t - e0] : (uint32_t)A.slot_next[t]; };
     uint64_t occ = c == 0 ? 0ull : A.occ_prev[c - 1];
     uint64_t occ_or = 0, alloc_or = 0;   // OR of the occupancy after each occupying allocation / of allocated slots
     bool diff = false;
@@ -101,9 +110,9 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         // iteration i-1, this chunk's earlier batches from this iteration
         uint32_t n0_v = 0, n1_v = 0;
         if ((rec1.x & F_C) && (uint64_t)rec1.y < base)
-            n0_v = (uint64_t)rec1.y < e0 ? A.slot_prev[rec1.y] : A.slot_next[rec1.y];
+            n0_v = (uint64_t)rec1.y < e0 ? A.slot_prev[rec1.y] : own(rec1.y);
         if ((rec1.x & F_C) && (uint64_t)rec1.z < base)
-            n1_v = (uint64_t)rec1.z < e0 ? A.slot_prev[rec1.z] : A.slot_next[rec1.z];
+            n1_v = (uint64_t)rec1.z < e0 ? A.slot_prev[rec1.z] : own(rec1.z);
         // ---- parallel part: this lane's event ----------------------------------------
         const bool have_prev = base > e0;    // previous batch of this chunk is in prev_v
         const uint64_t pbase = base - 64;
@@ -221,7 +230,7 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
                         uint32_t ts;
                         if (t >= base) ts = rl(cur_v, (uint32_t)(t - base));
                         else if (have_prev && t >= pbase) ts = rl(prev_v, (uint32_t)(t - pbase));
-                        else ts = t < e0 ? A.slot_prev[t] : A.slot_next[t];
+                        else ts = t < e0 ? A.slot_prev[t] : own(t);
                         clr |= 1ull << (ts & 63u);
                         m = ts < m ? ts : m;
                     }
@@ -238,6 +247,7 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
             const uint8_t nv = (uint8_t)cur_v;
             diff |= gp_v != nv;
             A.slot_next[base + lid] = nv;
+            if (lds) lslot[base - e0 + lid] = nv;
         }
         gp_v = gp_next;
         // same-wave vector memory ops to one address complete in order; only keep
