@@ -387,6 +387,8 @@ def main():
     eng._check(lib_opt(eng._ctx, 4, 0 if args.all_stage_events else 1))   # WG_OPT_TIMING_EMIT_ONLY
     eng.enable_timing(True, reserve=64 * (args.steps + 1))
 
+    if comm is not None:
+        comm.set_timing(True)
     # timed region: barrier + sync on both sides, exactly K steps
     if world > 1:
         dist.barrier()
@@ -398,6 +400,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    exchange = None
+    if comm is not None:   # seam exchanges: max over ranks, per step
+        rep = comm.timing_report()
+        comm.set_timing(False)
+        vals = torch.tensor([rep["host_ms"], rep["collective_ms"] or 0.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        exchange = {"exchanges_per_step": rep["exchanges"] / args.steps,
+                    "collective_ms_per_step": round(float(vals[1]) / args.steps, 4) if rep["collective_ms"] is not None else None,
+                    "host_wait_ms_per_step": round(float(vals[0]) / args.steps, 4),
+                    "note": "collective_ms: the all-gathers' own GPU time (HIP events on the stream); host_wait_ms: "
+                            "host time inside ShardComm.allgather, i.e. waiting for the producing kernels, the "
+                            "collective and the slot heads (max over ranks)"}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -494,6 +508,8 @@ def main():
                           "vertices_per_gpu": int(vs.n_vertices), "parallelism": f"row-shard x{world}"},
                "stages_ms": stages, "host_input_rows_per_s": None if host_rate is None else round(host_rate, 1),
                "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_threads": cpu_mt, **extras}
+        if exchange is not None:
+            out["seam_exchange"] = exchange
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

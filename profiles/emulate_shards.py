@@ -75,9 +75,13 @@ def main():
             self.t = None
             self.label = ""
             self.on_device, self.device = True, dev   # slots packed in stream order, as over RCCL
+            self.world = W
+
+        held = False
 
         def start(self, label):
             gpu.acquire()
+            self.held = True
             self.label = label
             self.t = time.perf_counter()
 
@@ -89,9 +93,11 @@ def main():
             else:
                 self.stream.synchronize()
             seg[self.rank].append((self.label, time.perf_counter() - self.t))
+            self.held = False
             gpu.release()
 
-        def allgather(self, nbytes, fill, step=0, pack=None):
+        def allgather(self, nbytes, fill, step=0, pack=None, read_heads=None):
+            # (read_heads: the heads come from the host copy below, as with a gloo transport)
             cap = ShardComm.round_cap(nbytes)
             with torch.cuda.stream(self.stream):
                 if pack is not None:
@@ -138,6 +144,7 @@ def main():
             rank_body(r)
 
     def rank_body(r):
+        comm = None
         try:
             eng = engines[r]
             comm = EmuComm(r, eng, streams[r])
@@ -162,12 +169,17 @@ def main():
                     seg[r].clear()
                     if r == 0:
                         xlog.clear()
+                if r == 0:
+                    print(f"step {it} done", file=sys.stderr, flush=True)
                 bar.wait()
             for name, ms in eng.timings():
                 stage_ms[r][name] = stage_ms[r].get(name, 0.0) + ms / args.steps
             eng.enable_timing(False)
         except Exception as ex:   # surface worker failures in the main thread
             errors.append((r, repr(ex)))
+            if comm is not None and comm.held:   # let the other ranks run into the aborted barrier
+                comm.held = False
+                gpu.release()
             bar.abort()
 
     th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]

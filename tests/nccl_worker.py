@@ -47,6 +47,7 @@ def main():
         if not comm.on_device:
             errors.append("nccl group not on device")
         rng = np.random.default_rng(1)
+        comm.set_timing(True)   # bench.py's seam-exchange breakdown over RCCL
         for use_pack in (True, False):
             for step, n in enumerate([0, 5, 64, 200, 4096, 100]):   # 200 / 4096 overflow the slot
                 msg = torch.from_numpy(rng.integers(0, 256, max(n, 1), dtype=np.uint8)).to(dev)
@@ -74,6 +75,9 @@ def main():
                     errors.append(f"{tag}: payload differs")
                 if comm.heads.tobytes() != (want + bytes(16))[:16]:
                     errors.append(f"{tag}: heads differ")
+        rep = comm.timing_report()
+        if rep["exchanges"] != 12 or not (rep["collective_ms"] or 0) > 0 or not rep["host_ms"] > 0:
+            errors.append(f"timing report {rep}")
         res = {"ok": not errors, "errors": errors, "collectives": comm.collectives, "exchanges": comm.exchanges}
     except Exception:   # report, do not hang the launcher
         import traceback

@@ -54,7 +54,30 @@ class ShardComm:
         self.exchanges = 0
         self.collectives = 0
         self.bytes_sent = 0
+        # seam-exchange timing (set_timing): host seconds inside allgather (the
+        # wait for the producing kernels, the collective and the heads) and,
+        # on a device transport, HIP events around every collective on the stream
+        self.timing = False
+        self.host_s = 0.0
+        self._events = []
         self.heads = None   # host copy of every message's first 16 bytes (uint32 [world, 4]), last exchange
+
+    def set_timing(self, on: bool):
+        """Start (True: counters reset) or stop recording the exchange times."""
+        self.timing = on
+        if on:
+            self.host_s = 0.0
+            self._events = []
+            self._x0 = self.exchanges
+
+    def timing_report(self) -> dict:
+        """{'exchanges', 'host_ms', 'collective_ms'} since set_timing(True);
+        collective_ms (device transport) sums the collectives' own GPU time."""
+        coll = None
+        if self._events:
+            torch.cuda.synchronize(self.device)
+            coll = sum(a.elapsed_time(b) for a, b in self._events)
+        return {"exchanges": self.exchanges - self._x0, "host_ms": self.host_s * 1e3, "collective_ms": coll}
 
     @staticmethod
     def round_cap(n: int) -> int:
@@ -70,6 +93,8 @@ class ShardComm:
         message header as a (world, 3) uint64 array, read in stream order.
         Returns (gathered device tensor, payload offset, stride, sizes): rank
         r's message starts at offset + r * stride."""
+        import time
+        t_host = time.perf_counter() if self.timing else 0.0
         dev = self.device if self.on_device else torch.device("cpu")
         cap = self.caps.get(step, self.initial_cap)
         while True:
@@ -84,7 +109,13 @@ class ShardComm:
                     fill(send.data_ptr() + self.HDR)
             out = torch.empty(self.world * stride, dtype=torch.uint8, device=dev)
             if self.on_device and self.backend == "nccl":
+                if self.timing:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record()
                 dist.all_gather_into_tensor(out, send, group=self.group)
+                if self.timing:
+                    ev[1].record()
+                    self._events.append(ev)
             else:
                 dist.all_gather(list(out.view(self.world, stride).unbind(0)), send, group=self.group)
             self.collectives += 1
@@ -107,4 +138,6 @@ class ShardComm:
             torch.cuda.current_stream(self.device).synchronize()   # the H2D copy above
         self.exchanges += 1
         self.bytes_sent += nbytes
+        if self.timing:
+            self.host_s += time.perf_counter() - t_host
         return out, self.HDR, stride, sizes
