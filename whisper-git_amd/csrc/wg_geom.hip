@@ -360,43 +360,55 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
     }
     // per-row scalars of the chunk, one row per lane
     const uint64_t rr = R0 + lid;
-    const uint32_t rf_v = lid < nr ? rowflags[rr] : 0u;
     const uint32_t voff_v = lid < nr ? vert_off[rr] : 0u;
     const uint32_t coff_v = lid < nr ? curve_off[rr] : 0u;
-    uint32_t ek[SW_SLOTS], ec[SW_SLOTS], ep[SW_SLOTS], ei[SW_SLOTS];
+    // per slot: the edge id, the packed full-vertical entry and two row windows
+    // as (first row, length - 1) for an unsigned compare: full verticals on
+    // rows c < r < p of same-lane edges, curve segments on rows c <= r <= p of
+    // cross-lane edges; an empty window has first row ~0.  The sweep always runs
+    // on the all-zero flag row (the curve lists are a superset, filtered per
+    // pass), so no strip flag enters the row loop.
+    uint32_t ek[SW_SLOTS], fb[SW_SLOTS], fl[SW_SLOTS], cb[SW_SLOTS], cl[SW_SLOTS], pv[SW_SLOTS];
     const uint32_t nslots = (total + 63) / 64;
 #pragma unroll
     for (int sl = 0; sl < SW_SLOTS; sl++) {
         const uint32_t idx = 64u * sl + lid;
-        ek[sl] = 0; ec[sl] = 1; ep[sl] = 0; ei[sl] = 0;   // dead: c >= p
+        ek[sl] = 0; fb[sl] = ~0u; fl[sl] = 0; cb[sl] = ~0u; cl[sl] = 0; pv[sl] = 0;
         if ((uint32_t)sl < nslots && idx < total) {
             const uint32_t k = idx < ncar ? carry_sorted[a + idx] : E0 + (idx - ncar);
             const wg_edge e = edges[k];
             ek[sl] = k;
-            ec[sl] = e.child_row;
-            ep[sl] = e.parent_row;
-            ei[sl] = (e.child_lane & 0xFFFFFFu) | (e.color << 24) | ((e.child_lane == e.parent_lane) ? 0x10000000u : 0u);
+            const uint32_t c = e.child_row, p = e.parent_row;
+            if (c < p) {
+                if (e.child_lane == e.parent_lane) {
+                    if (c + 1 < p) { fb[sl] = c + 1; fl[sl] = p - c - 2; }
+                    pv[sl] = pack_vert(e.child_lane & 0xFFFFFFu, WG_VERT_FULL, e.color & 0xFu);
+                } else {
+                    cb[sl] = c;
+                    cl[sl] = p - c;
+                }
+            }
         }
     }
+    (void)rowflags;
     for (uint32_t j = 0; j < nr; j++) {
         const uint32_t r = (uint32_t)(R0 + j);
-        const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)rf_v, (int)j);
         uint32_t fbase = (uint32_t)__builtin_amdgcn_readlane((int)voff_v, (int)j);
         uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
 #pragma unroll
         for (int sl = 0; sl < SW_SLOTS; sl++) {
             if ((uint32_t)sl >= nslots) break;
-            const uint32_t c = ec[sl], p = ep[sl], info = ei[sl];
-            const bool live = c < p;
-            const bool same = (info & 0x10000000u) != 0;
-            const bool full = live && same && c < r && r < p;
-            const bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
-            const bool curv = live && !same && c <= r && r <= p && !skip;
+            const bool full = r - fb[sl] <= fl[sl];
+            const bool curv = r - cb[sl] <= cl[sl];
             const uint64_t mf = __ballot(full), mc = __ballot(curv);
-            if (full) vert[fbase + mbcnt(mf)] = pack_vert(info & 0xFFFFFFu, WG_VERT_FULL, (info >> 24) & 0xFu);
-            if (curv) { const uint32_t o = cbase + mbcnt(mc); curve_ref[o] = ek[sl]; curve_row[o] = r; }
-            fbase += __builtin_popcountll(mf);
-            cbase += __builtin_popcountll(mc);
+            if (mf) {
+                if (full) vert[fbase + mbcnt(mf)] = pv[sl];
+                fbase += __builtin_popcountll(mf);
+            }
+            if (mc) {
+                if (curv) { const uint32_t o = cbase + mbcnt(mc); curve_ref[o] = ek[sl]; curve_row[o] = r; }
+                cbase += __builtin_popcountll(mc);
+            }
         }
     }
 }
