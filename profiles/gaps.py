@@ -2,7 +2,11 @@
 the last step (k_vtx_tile end to k_vtx_tile end), their durations and the
 idle gap before each one (host synchronisations show up as gaps).
 
-usage: python3 profiles/gaps.py <run_kernel_trace.csv> [min_gap_us]
+usage: python3 profiles/gaps.py <run_kernel_trace.csv> [min_gap_us] [step]
+  step: which step (between the step-th and step+1-th k_vtx_tile, from 0);
+        default the last one.  bench.py's last steps are its stage-breakdown
+        pass, whose per-stage HIP events show up as ~10 us gaps: pick a step
+        of the timed region (after the warmup) to see the timed step.
 """
 import csv
 import re
@@ -15,7 +19,11 @@ def main():
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                   re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))) for r in rows))
     ends = [i for i, k in enumerate(ks) if k[2] == "k_vtx_tile"]
-    a, b = ends[-2], ends[-1]
+    if len(sys.argv) > 3:
+        st = int(sys.argv[3])
+        a, b = ends[st], ends[st + 1]
+    else:
+        a, b = ends[-2], ends[-1]
     step = ks[a + 1:b + 1]
     t0 = ks[a][1]
     busy = sum(e - s for s, e, _ in step)
