@@ -106,6 +106,7 @@ struct ShardState {
     DevBuf xchild, xpar;      // per crossing entry: child lane/colour, parent lane/y
     DevBuf in_scan, edge_y, own_edges;
     uint64_t n_own_edges = 0;
+    bool geom_spec_ready = false;   // an earlier sharded geometry pass sized the lists (speculation may start)
 };
 
 // SDF font atlas slot (wg_font.hip)

@@ -561,6 +561,12 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     const uint64_t xin = S.xoff[S.rank];
     const int32_t *prow = S.prow.as<const int32_t>() - S.E0;
     const bool same_layout = S.local_gen == c->layout_gen;
+    // The first pass on a layout (the build's default geometry) runs
+    // speculatively once an earlier pass sized the buffers: local edges sized
+    // by their bounds (incoming <= the earlier shards' crossing entries, own <=
+    // the shard's references), the geometry lists by capacity, one read at
+    // the end (wg_layout_build's scheme).
+    const bool spec = !same_layout && S.geom_spec_ready;
     if (!same_layout) {
         WG_ALLOC(c, S.in_scan, (xin + 2) * 4);
         WG_ALLOC(c, c->edge_cnt, (nloc + 2) * 4);
@@ -572,15 +578,23 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
         hipLaunchKernelGGL(k_sh_own_counts, dim3(blocks(nloc)), dim3(T), 0, st, s, nl, c->d_poff, prow,
                            S.in_scan.as<const uint32_t>(), xin, c->edge_cnt.as<uint32_t>());
         WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), nloc, c->scan_tmp.p, st));
-        uint64_t tot[2] = {0, 0};
-        if ((rc = wg_fetch(c, {{c->edge_cnt.as<uint32_t>() + nloc, false}, {c->edge_cnt.as<uint32_t>() + 1, false}}, tot)) !=
-            WG_OK)
-            return rc;
-        S.local_ne = tot[0];
-        S.local_nin = tot[1];
-        WG_ALLOC(c, c->edges, S.local_ne * sizeof(wg_edge) + 16);
-        WG_ALLOC(c, S.edge_y, S.local_ne * 8 + 16);
-        WG_ALLOC(c, S.own_edges, (S.local_ne - S.local_nin) * sizeof(wg_edge) + 16);
+        if (spec) {
+            S.local_ne = xin + (S.E1 - S.E0);   // upper bounds until the validation read
+            S.local_nin = xin;
+            WG_ALLOC(c, c->edges, S.local_ne * sizeof(wg_edge) + 16);
+            WG_ALLOC(c, S.edge_y, S.local_ne * 8 + 16);
+            WG_ALLOC(c, S.own_edges, (S.E1 - S.E0) * sizeof(wg_edge) + 16);
+        } else {
+            uint64_t tot[2] = {0, 0};
+            if ((rc = wg_fetch(c, {{c->edge_cnt.as<uint32_t>() + nloc, false}, {c->edge_cnt.as<uint32_t>() + 1, false}},
+                               tot)) != WG_OK)
+                return rc;
+            S.local_ne = tot[0];
+            S.local_nin = tot[1];
+            WG_ALLOC(c, c->edges, S.local_ne * sizeof(wg_edge) + 16);
+            WG_ALLOC(c, S.edge_y, S.local_ne * 8 + 16);
+            WG_ALLOC(c, S.own_edges, (S.local_ne - S.local_nin) * sizeof(wg_edge) + 16);
+        }
     }
     const uint64_t ne = S.local_ne, n_in = S.local_nin;
     LocalEdgeArgs A;
@@ -609,8 +623,29 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     c->edge_y = S.edge_y.as<const float>();
     S.n_own_edges = ne - n_in;
     S.local_gen = c->layout_gen;
-    rc = wg_stage_geometry(c, band_g ? c->band.as<const float>() : nullptr);
+    const float *band_l = band_g ? c->band.as<const float>() : nullptr;
+    c->spec = spec;
+    rc = wg_stage_geometry(c, band_l);
+    c->spec = false;
     if (rc != WG_OK) return rc;
+    if (spec) {
+        WgFetch it[12];
+        int k = wg_geom_spec_items(c, it);
+        it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + nloc, false};
+        it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + 1, false};
+        uint64_t v[12] = {0};
+        if ((rc = wg_fetch_n(c, k, it, v)) != WG_OK) return rc;
+        S.local_ne = v[8];
+        S.local_nin = v[9];
+        c->n_edges = S.local_ne;
+        S.n_own_edges = S.local_ne - S.local_nin;
+        if (!wg_geom_spec_check(c, v)) {   // past a capacity: the exact pass (the local edges are in place)
+            c->spec_redo_geom++;
+            c->lists_gen = ~0ull;
+            if ((rc = wg_stage_geometry(c, band_l)) != WG_OK) return rc;
+        }
+    }
+    S.geom_spec_ready = c->lists_gen == c->layout_gen;
     c->have_geom = true;
     sh_done(c, out);
     return WG_OK;
