@@ -91,11 +91,13 @@ __global__ void k_sh_dupscan(const uint8_t *__restrict__ oid, uint64_t n, uint32
 }
 
 // own rows' references against the local table; per-row count of the unresolved
+// (E0 = parent_off[s]: the shard's first reference, read here rather than by the host)
 __global__ void k_sh_probe(uint64_t s, uint64_t nl, const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
-                           uint64_t E0, const uint8_t *__restrict__ oid, const unsigned long long *__restrict__ table,
+                           const uint8_t *__restrict__ oid, const unsigned long long *__restrict__ table,
                            uint64_t mask, int32_t *__restrict__ prow_l, uint32_t *__restrict__ ucnt, uint32_t *flags) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nl) return;
+    const uint64_t E0 = poff[s];
     const uint64_t gi = s + i;
     const uint32_t pa = poff[gi], pb = poff[gi + 1];
     uint32_t nu = 0;
@@ -113,10 +115,11 @@ __global__ void k_sh_probe(uint64_t s, uint64_t nl, const uint32_t *__restrict__
 
 // unresolved reference record: {child row, parent index, id[5], 0} (32 bytes), row order
 __global__ void k_sh_pack_unres(uint64_t s, uint64_t nl, const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
-                                uint64_t E0, const int32_t *__restrict__ prow_l, const uint32_t *__restrict__ uoff,
+                                const int32_t *__restrict__ prow_l, const uint32_t *__restrict__ uoff,
                                 uint32_t *__restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nl) return;
+    const uint64_t E0 = poff[s];
     const uint64_t gi = s + i;
     const uint32_t pa = poff[gi], pb = poff[gi + 1];
     uint32_t o = uoff[i];
@@ -688,17 +691,25 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     c->n = N;
     c->e_refs = S.Etot;
     hipStream_t st = c->stream;
-    uint64_t eo[2] = {0, 0};
-    if (N) {
-        const int frc = wg_fetch(c, {{c->d_poff + row_begin, false}, {c->d_poff + row_end, false}}, eo);
-        if (frc != WG_OK) return frc;
-    }
-    S.E0 = eo[0];
-    S.E1 = eo[1];
-    c->e_refs_own = S.E1 - S.E0;
     S.rt_zero = false;
-    if (world == 1) return sh_fallback(c, out);
-    const uint64_t nl = row_end - row_begin, El = S.E1 - S.E0;
+    if (world == 1) {
+        uint64_t eo[2] = {0, 0};
+        if (N) {
+            const int frc = wg_fetch(c, {{c->d_poff + row_begin, false}, {c->d_poff + row_end, false}}, eo);
+            if (frc != WG_OK) return frc;
+        }
+        S.E0 = eo[0];
+        S.E1 = eo[1];
+        c->e_refs_own = S.E1 - S.E0;
+        return sh_fallback(c, out);
+    }
+    // The shard's reference range [E0, E1) = parent_off[s], parent_off[e] is
+    // read with this segment's closing read: reading it first would wait for
+    // the previous step's emission and leave the GPU idle while this
+    // segment's kernels are queued.  Until then the own references' rows are
+    // sized by the list's reference count and indexed from parent_off[s] on
+    // the device.
+    const uint64_t nl = row_end - row_begin, El = S.Etot;
     // heights of rows [0, e) (the last row of the LIST is ROW_HEIGHT) and the
     // zero-band row_top of the own rows: side stream, overlapping the exchanges
     c->n_list = N;
@@ -726,16 +737,20 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
                                c->hash.as<unsigned long long>(), cap - 1);
     if (N) hipLaunchKernelGGL(k_sh_dupscan, dim3(blocks(N)), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
                               S.ptable.as<unsigned long long>(), pcap - 1, S.flags.as<uint32_t>());
-    if (nl) hipLaunchKernelGGL(k_sh_probe, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid, S.E0,
+    if (nl) hipLaunchKernelGGL(k_sh_probe, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid,
                                c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>(),
                                S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(S.xcnt.as<uint32_t>(), S.xcnt.as<uint32_t>(), nl, c->scan_tmp.p, st));
-    uint64_t h[3] = {0, 0, 0};
+    uint64_t h[5] = {0, 0, 0, 0, 0};
     {
         const int frc = wg_fetch(c, {{S.flags.as<uint32_t>(), false}, {S.flags.as<uint32_t>() + 1, false},
-                                     {S.xcnt.as<uint32_t>() + nl, false}}, h);
+                                     {S.xcnt.as<uint32_t>() + nl, false}, {c->d_poff + row_begin, false},
+                                     {c->d_poff + row_end, false}}, h);
         if (frc != WG_OK) return frc;
     }
+    S.E0 = h[3];
+    S.E1 = h[4];
+    c->e_refs_own = S.E1 - S.E0;
     c->hcap = cap;
     S.n_unres = h[2];
     S.step = SH_X1;
@@ -744,7 +759,7 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     if (rc != WG_OK) return rc;
     uint32_t hdr[4] = {(uint32_t)(h[0] | h[1]), (uint32_t)h[2], 0, 0};
     hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), make_uint4(hdr[0], hdr[1], hdr[2], hdr[3]));
-    if (nl) hipLaunchKernelGGL(k_sh_pack_unres, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid, S.E0,
+    if (nl) hipLaunchKernelGGL(k_sh_pack_unres, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid,
                                S.prow.as<const int32_t>(), S.xcnt.as<const uint32_t>(),
                                reinterpret_cast<uint32_t *>(S.msg.as<uint8_t>() + 16));
     WG_HIP(c, hipGetLastError());
