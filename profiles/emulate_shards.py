@@ -192,6 +192,21 @@ def main():
 
     counters = [int(e.debug_counters()[5]) for e in engines]
 
+    # rank 0's emission again on its sharded geometry, alone on the GPU (no other
+    # rank's segments interleaved): separates the shard data from the emulation
+    reemit_ms = None
+    if args.stage_events:
+        e0 = engines[0]
+        with torch.cuda.stream(streams[0]):
+            e0.synchronize()
+            wgraph.lib().wg_set_option(e0._ctx, 4, 0)
+            e0.enable_timing(True, reserve=64 * args.steps)
+            for _ in range(args.steps):
+                e0.emit_vertices(0, R, selected=7, palette=pal)
+            e0.synchronize()
+            reemit_ms = round(sum(ms for n, ms in e0.timings() if n == "vtx_emit") / args.steps, 4)
+            e0.enable_timing(False)
+
     # the single-GPU step on an R-row list of the same kind, for comparison
     single = wgraph.Engine(0)
     dag1 = synth.generate(args.kind, R)
@@ -202,11 +217,12 @@ def main():
     c1.oid, c1.time, c1.parent_off, c1.parent_oid, c1.flags = (t.data_ptr() for t in k1[:5])
     c1.residency = abi.WG_DEVICE
 
-    def one():
-        single.build(commits=c1)
-        single.row_geometry(device_ptr=k1[5].data_ptr())
-        single.emit_vertices(0, R, selected=7, palette=pal)
-        single.synchronize()
+    def one(eng=None):
+        eng = eng or single
+        eng.build(commits=c1)
+        eng.row_geometry(device_ptr=k1[5].data_ptr())
+        eng.emit_vertices(0, R, selected=7, palette=pal)
+        eng.synchronize()
     one()
     times = []
     for _ in range(args.steps):
@@ -214,6 +230,24 @@ def main():
         one()
         times.append(time.perf_counter() - t0)
     single_ms = 1e3 * float(np.median(times))
+    single_stages = {}
+    if args.stage_events:   # the same stage events on the single-GPU step, for a side-by-side table
+        wgraph.lib().wg_set_option(single._ctx, 4, 0)
+        single.enable_timing(True, reserve=64 * args.steps)
+        for _ in range(args.steps):
+            one()
+        for name, ms in single.timings():
+            single_stages[name] = round(single_stages.get(name, 0.0) + ms / args.steps, 4)
+        single.enable_timing(False)
+        # the same single-GPU step on rank 0's engine (its buffers were sized by the sharded steps)
+        e0 = engines[0]
+        one(e0)
+        wgraph.lib().wg_set_option(e0._ctx, 4, 0)
+        e0.enable_timing(True, reserve=64 * args.steps)
+        for _ in range(args.steps):
+            one(e0)
+        single_stages["rank0_engine_vtx_emit"] = round(sum(ms for n, ms in e0.timings() if n == "vtx_emit") / args.steps, 4)
+        e0.enable_timing(False)
 
     per_rank = []
     for r in range(W):
@@ -236,7 +270,9 @@ def main():
         xbytes[f"X{step}" if step not in xbytes else f"X{step}b"] = sizes
     worst = max(p["ms"] for p in per_rank)
     res = {"world": W, "rows_per_rank": R, "kind": args.kind, "steps": args.steps,
-           "single_gpu_step_ms": round(single_ms, 4), "max_rank_ms_without_collectives": round(worst, 4),
+           "single_gpu_step_ms": round(single_ms, 4), "single_gpu_stages_ms": single_stages,
+           "rank0_reemit_vtx_emit_ms": reemit_ms,
+           "max_rank_ms_without_collectives": round(worst, 4),
            "exchanges_per_step": n_x, "exchange_bytes_per_rank": xbytes,
            "efficiency_without_collectives": round(single_ms / worst, 4), "ranks": per_rank}
     print(json.dumps(res, indent=1))
