@@ -57,7 +57,43 @@ __global__ void k_fetch(FetchArgs a, unsigned long long *out, unsigned long long
     __syncthreads();
     if (i == 0) __hip_atomic_store(seq_word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// one piece per blockIdx.y; 16-byte moves when the piece allows them
+__global__ void __launch_bounds__(256) k_copy_batch(WgCopyBatch B) {
+    const uint32_t k = blockIdx.y;
+    if (k == 0 && blockIdx.x == 0 && threadIdx.x < B.nwords) B.wdst[threadIdx.x] = B.words[threadIdx.x];
+    if (k >= B.n) return;
+    const uint8_t *src = static_cast<const uint8_t *>(B.src[k]);
+    uint8_t *dst = static_cast<uint8_t *>(B.dst[k]);
+    const uint64_t nb = B.bytes[k];
+    const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, ts = (uint64_t)gridDim.x * blockDim.x;
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | nb) & 15u) == 0) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        for (uint64_t i = t0; i < nb / 16; i += ts) d4[i] = s4[i];
+    } else {
+        const uint32_t *s1 = reinterpret_cast<const uint32_t *>(src);
+        uint32_t *d1 = reinterpret_cast<uint32_t *>(dst);
+        for (uint64_t i = t0; i < nb / 4; i += ts) d1[i] = s1[i];
+    }
+}
 }  // namespace
+
+int wg_copy_batch(wg_ctx *c, const WgCopies &cp, hipStream_t s) {
+    if (cp.overflow) return wg_fail(c, WG_E_UNSUPPORTED, "copy batch overflow (more than %d pieces)", WG_BCOPY_MAX);
+    const WgCopyBatch &B = cp.b;
+    if (B.n == 0 && B.nwords == 0) return WG_OK;
+    uint64_t mx = 0;
+    for (uint32_t k = 0; k < B.n; k++) {
+        if (((reinterpret_cast<uintptr_t>(B.src[k]) | reinterpret_cast<uintptr_t>(B.dst[k]) | B.bytes[k]) & 3u) != 0)
+            return wg_fail(c, WG_E_INVALID, "copy batch piece %u not 4-byte aligned", k);
+        mx = B.bytes[k] > mx ? B.bytes[k] : mx;
+    }
+    uint64_t gx = (mx + 4095) / 4096;
+    gx = gx < 1 ? 1 : (gx > 512 ? 512 : gx);
+    hipLaunchKernelGGL(k_copy_batch, dim3((uint32_t)gx, B.n ? B.n : 1u), dim3(256), 0, s, B);
+    WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
 
 int wg_side_fork(wg_ctx *c) {
     if (!c->side) {
@@ -577,16 +613,19 @@ int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
         c->geom_r0 = first;   // rows below `first` keep their geometry
     }
     int rc;
+    // the bands this geometry is made with, kept for the next frame's compare:
+    // written by k_row_basic as it reads them (rows below r0 are equal already)
+    if (band && c->n) {
+        WG_ALLOC(c, c->band_prev, c->n * 4 + 4);
+        c->band_keep = c->band_prev.as<float>();
+    }
+    struct KeepOff { wg_ctx *c; ~KeepOff() { c->band_keep = nullptr; } } keep_off{c};
     if ((rc = wg_stage_rowtop(c, d_band)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, d_band)) != WG_OK) return rc;
     c->have_geom = true;
     c->geom_key_gen = c->layout_gen;
     c->geom_key_band = band != nullptr;
     c->geom_r0 = 0;
-    if (band && c->n) {   // the bands this geometry was made with (compared by the next frame)
-        WG_ALLOC(c, c->band_prev, c->n * 4 + 4);
-        WG_HIP(c, hipMemcpyAsync(c->band_prev.p, d_band, c->n * 4, hipMemcpyDeviceToDevice, c->stream));
-    }
     return WG_OK;
 }
 

@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t pack_vert(uint32_t lane, uint32_t kind, uint
 __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
                             const float *__restrict__ row_top, float *__restrict__ height, float *__restrict__ node_y,
                             uint8_t *__restrict__ rowflags, uint64_t lo = 0, uint4 *__restrict__ zws = nullptr,
-                            uint64_t nz4 = 0) {
+                            uint64_t nz4 = 0, float *__restrict__ band_keep = nullptr) {
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t i = tid; i < nz4; i += (uint64_t)gridDim.x * blockDim.x) zws[i] = make_uint4(0u, 0u, 0u, 0u);
     uint64_t r = lo + tid;
@@ -64,6 +64,7 @@ __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float
     float ht, ny;
     if (band) {
         const float b = band[r];
+        if (band_keep) band_keep[r] = b;   // the bands of this geometry (compared by the next frame)
         ht = roundf(h[r] + b);        // (h + band).round()  (:389)
         ny = roundf(b + WG_NODE_Y);   // (band + NODE_Y).round() (:390)
     } else {
@@ -519,11 +520,14 @@ __device__ __forceinline__ bool curve_kept(uint32_t r, const wg_edge &e, uint32_
 __global__ void k_curve_keep(uint64_t n, const uint32_t *__restrict__ soff, const uint32_t *__restrict__ sref,
                              const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
                              uint32_t *__restrict__ cnt, const uint32_t *__restrict__ cond,
-                             const uint32_t *__restrict__ cur_off, Cap sc, uint32_t *ovf) {
+                             const uint32_t *__restrict__ cur_off, Cap sc, uint32_t *ovf,
+                             uint8_t *__restrict__ flags_kept) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (over(sc, ovf) || r >= n) return;
+    const uint32_t f = rowflags[r];
+    flags_kept[r] = (uint8_t)f;   // the flags the curve lists are filtered with (equal when cond is 0)
     if (cond && !*cond) { cnt[r] = cur_off[r + 1] - cur_off[r]; return; }
-    const uint32_t a = soff[r], b = soff[r + 1], f = rowflags[r];
+    const uint32_t a = soff[r], b = soff[r + 1];
     uint32_t k = b - a;
     if (f) {
         k = 0;
@@ -566,16 +570,15 @@ static Cap no_cap() { return Cap{nullptr, ~0u}; }
 static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *cond, Cap sc, uint32_t *ovf) {
     uint32_t *coff = c->curve_off.as<uint32_t>();
     WG_ALLOC(c, c->curve_cnt, (n + 2) * 4);
+    WG_ALLOC(c, c->rowflags_lists, n + 4);
     uint32_t *cnt = c->curve_cnt.as<uint32_t>();
     hipLaunchKernelGGL(k_curve_keep, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
                        c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
-                       cnt, cond, (const uint32_t *)coff, sc, ovf);
+                       cnt, cond, (const uint32_t *)coff, sc, ovf, c->rowflags_lists.as<uint8_t>());
     WG_HIP(c, wg_exclusive_scan_u32(cnt, coff, n, c->scan_tmp.p, s));
     hipLaunchKernelGGL(k_curve_compact, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
                        c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
                        (const uint32_t *)coff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), cond, sc, ovf);
-    WG_ALLOC(c, c->rowflags_lists, n + 4);
-    WG_HIP(c, hipMemcpyAsync(c->rowflags_lists.p, c->rowflags.p, n, hipMemcpyDeviceToDevice, s));
     WG_HIP(c, hipGetLastError());
     return WG_OK;
 }
@@ -661,7 +664,8 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         wg_stage_begin(c, "geom_reuse");
         uint32_t *diff = c->geom_diff.as<uint32_t>();
         hipLaunchKernelGGL(k_row_basic, dim3(blocks(n - r0)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
-                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), r0, c->geom_diff.as<uint4>(), (uint64_t)1);
+                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), r0, c->geom_diff.as<uint4>(), (uint64_t)1,
+                           c->band_keep);
         hipLaunchKernelGGL(k_flags_diff, dim3(blocks(n - r0)), dim3(T), 0, s, n, c->rowflags.as<const uint8_t>(),
                            c->rowflags_lists.as<const uint8_t>(), diff, r0);
         int rc = filter_curves(c, n, s, diff, no_cap(), diff + 8);
@@ -710,7 +714,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     wg_stage_begin(c, "geom_counts");
     hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
                        c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), (uint64_t)0, c->geom_zero.as<uint4>(),
-                       (uint64_t)(zwords / 4));
+                       (uint64_t)(zwords / 4), c->band_keep);
     if (ne)
         hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntB, cntT, cntF, cntC, cntCend,
                            carry_cnt, ne_dev);

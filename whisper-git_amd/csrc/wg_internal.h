@@ -231,6 +231,7 @@ struct wg_ctx {
     uint64_t geom_key_gen = ~0ull;
     bool     geom_key_band = false;
     DevBuf   band_prev;                 // float [N] the bands of that geometry
+    float   *band_keep = nullptr;       // wg_row_geometry: k_row_basic writes the bands it reads here (band_prev)
     DevBuf   geom_diff_first;           // u64: first row whose band differs
     uint64_t geom_r0 = 0;               // that row, for the next geometry pass (0: whole pass)
     DevBuf sweep_big;       // uint32 [nch] chunks too wide for the register sweep
@@ -302,6 +303,39 @@ int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items);
 int wg_fetch_end(wg_ctx *c, uint64_t *out);
 int wg_fetch_defer(wg_ctx *c, std::initializer_list<WgFetch> items);
 int wg_fetch_deferred(wg_ctx *c, uint64_t *out);
+
+// Batched device copies (+ a few host words) in ONE launch: the sharded
+// exchanges move every rank's piece of a gathered buffer into place, which as
+// one hipMemcpyAsync per piece was one blit launch each (~3 W launches per
+// exchange); host words travel in the kernel arguments instead of a copy from
+// pageable memory.  Byte counts and addresses are multiples of 4.
+constexpr int WG_BCOPY_MAX = 48, WG_BCOPY_WORDS = 64;
+struct WgCopyBatch {
+    const void *src[WG_BCOPY_MAX];
+    void       *dst[WG_BCOPY_MAX];
+    uint64_t    bytes[WG_BCOPY_MAX];
+    uint64_t   *wdst;                   // inline words -> wdst[0 .. nwords)
+    uint64_t    words[WG_BCOPY_WORDS];
+    uint32_t    n, nwords;
+};
+struct WgCopies {
+    WgCopyBatch b{};
+    bool overflow = false;
+    void add(void *dst, const void *src, uint64_t bytes) {
+        if (!bytes) return;
+        if (b.n >= (uint32_t)WG_BCOPY_MAX) { overflow = true; return; }
+        b.src[b.n] = src; b.dst[b.n] = dst; b.bytes[b.n] = bytes; b.n++;
+    }
+    // words [0, n) -> dst[at .. at + n) (one destination buffer per batch)
+    void words(uint64_t *dst, uint32_t at, const uint64_t *w, uint32_t n) {
+        if (b.wdst && b.wdst != dst) { overflow = true; return; }
+        if (at + n > (uint32_t)WG_BCOPY_WORDS) { overflow = true; return; }
+        b.wdst = dst;
+        for (uint32_t i = 0; i < n; i++) b.words[at + i] = w[i];
+        b.nwords = at + n > b.nwords ? at + n : b.nwords;
+    }
+};
+int wg_copy_batch(wg_ctx *c, const WgCopies &cp, hipStream_t s);   // wg_api.hip
 
 // error helpers -------------------------------------------------------------
 int wg_fail(wg_ctx *c, int code, const char *fmt, ...);

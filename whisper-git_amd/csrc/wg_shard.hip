@@ -836,11 +836,14 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         }
         if (bad) return sh_fallback(c, out);
         const uint64_t L = S.uoffs[W];
-        WG_ALLOC(c, S.unres, L * 32 + 32);      // every rank's records, compacted
-        for (int r = 0; r < W; r++)
-            if (hdr[4 * r + 1])
-                WG_HIP(c, hipMemcpyAsync(S.unres.as<uint8_t>() + S.uoffs[r] * 32, (const uint8_t *)gathered + r * stride + 16,
-                                         (uint64_t)hdr[4 * r + 1] * 32, hipMemcpyDeviceToDevice, st));
+        WG_ALLOC(c, S.unres, L * 32 + 32);      // every rank's records, compacted (one launch)
+        {
+            WgCopies cp;
+            for (int r = 0; r < W; r++)
+                cp.add(S.unres.as<uint8_t>() + S.uoffs[r] * 32, (const uint8_t *)gathered + r * stride + 16,
+                       (uint64_t)hdr[4 * r + 1] * 32);
+            if ((rc = wg_copy_batch(c, cp, st)) != WG_OK) return rc;
+        }
         S.step = SH_X2;
         if ((rc = sh_send(c, L * 4, out)) != WG_OK) return rc;
         if (L) hipLaunchKernelGGL(k_sh_probe_gathered, dim3(blocks(L)), dim3(T), 0, st, L, S.unres.as<const uint32_t>(),
@@ -930,34 +933,36 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         }
         WG_ALLOC(c, S.xtok, nx * 4 + 16);
         WG_ALLOC(c, S.xt, nx * 4 + 16);
-        for (int r = 0; r < W; r++) {
-            const uint64_t n = S.xoff[r + 1] - S.xoff[r];
-            if (n) WG_HIP(c, hipMemcpyAsync(S.xtok.as<uint32_t>() + S.xoff[r], (const uint8_t *)gathered + r * stride + 16,
-                                            n * 4, hipMemcpyDeviceToDevice, st));
-        }
-        WG_ALLOC(c, S.dev_small, 96 * 8);
-        WG_HIP(c, hipMemcpyAsync(S.dev_small.p, S.xoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
-        WG_HIP(c, hipMemcpyAsync(S.dev_small.as<uint64_t>() + 32, S.evoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
-        WG_HIP(c, hipMemcpyAsync(S.dev_small.as<uint64_t>() + 64, S.auxoff.data(), (W + 1) * 8, hipMemcpyHostToDevice, st));
-        if (nx) hipLaunchKernelGGL(k_sh_resolve, dim3(1), dim3(1024), 0, st, nx, (uint32_t)W, S.dev_small.as<const uint64_t>(),
-                                   S.dev_small.as<const uint64_t>() + 32, S.xtok.as<const uint32_t>(), S.xt.as<uint32_t>());
-        // every rank's records (after its tokens, 16-byte aligned): rank r's events at evoff[r], aux words at auxoff[r]
+        // every rank's crossing tokens, event records and aux words (after its
+        // tokens, 16-byte aligned: rank r's events at evoff[r], aux words at
+        // auxoff[r]) and the three offset tables: one launch
         const uint64_t nev = S.evoff[W], naux = S.auxoff[W];
         DevBuf &evrec = c->lf[LF_EVREC], &aux = c->lf[LF_AUX];
         WG_ALLOC(c, evrec, (nev + 256) * 16);
         WG_ALLOC(c, aux, naux * 4 + 4);
+        WG_ALLOC(c, S.dev_small, 96 * 8);
         WG_HIP(c, hipMemsetAsync(evrec.as<uint4>() + nev, 0, 256 * 16, st));
-        for (int r = 0; r < W; r++) {
-            const uint64_t ne_r = S.evoff[r + 1] - S.evoff[r], na_r = S.auxoff[r + 1] - S.auxoff[r];
-            const uint64_t tok_b = ((S.xoff[r + 1] - S.xoff[r]) * 4 + 15) & ~15ull;
-            const uint8_t *src = (const uint8_t *)gathered + r * stride + 16 + tok_b;
-            if (ne_r) WG_HIP(c, hipMemcpyAsync(evrec.as<uint4>() + S.evoff[r], src, ne_r * 16, hipMemcpyDeviceToDevice, st));
-            if (na_r) WG_HIP(c, hipMemcpyAsync(aux.as<uint32_t>() + S.auxoff[r], src + ne_r * 16, na_r * 4,
-                                               hipMemcpyDeviceToDevice, st));
+        {
+            WgCopies cp;
+            for (int r = 0; r < W; r++) {
+                const uint64_t n = S.xoff[r + 1] - S.xoff[r];
+                const uint64_t ne_r = S.evoff[r + 1] - S.evoff[r], na_r = S.auxoff[r + 1] - S.auxoff[r];
+                const uint64_t tok_b = (n * 4 + 15) & ~15ull;
+                const uint8_t *src = (const uint8_t *)gathered + r * stride + 16;
+                cp.add(S.xtok.as<uint32_t>() + S.xoff[r], src, n * 4);
+                cp.add(evrec.as<uint4>() + S.evoff[r], src + tok_b, ne_r * 16);
+                cp.add(aux.as<uint32_t>() + S.auxoff[r], src + tok_b + ne_r * 16, na_r * 4);
+            }
+            cp.words(S.dev_small.as<uint64_t>(), 0, S.xoff.data(), (uint32_t)W + 1);
+            cp.words(S.dev_small.as<uint64_t>(), 20, S.evoff.data(), (uint32_t)W + 1);
+            cp.words(S.dev_small.as<uint64_t>(), 40, S.auxoff.data(), (uint32_t)W + 1);
+            if ((rc = wg_copy_batch(c, cp, st)) != WG_OK) return rc;
         }
+        if (nx) hipLaunchKernelGGL(k_sh_resolve, dim3(1), dim3(1024), 0, st, nx, (uint32_t)W, S.dev_small.as<const uint64_t>(),
+                                   S.dev_small.as<const uint64_t>() + 20, S.xtok.as<const uint32_t>(), S.xt.as<uint32_t>());
         LfRange R = sh_range(c);
         if ((rc = wg_lf_events_finish(c, R, (uint32_t)S.evoff[S.rank], S.xt.as<const uint32_t>(), nx, nev, (uint32_t)W,
-                                      S.dev_small.as<const uint64_t>() + 32, S.dev_small.as<const uint64_t>() + 64,
+                                      S.dev_small.as<const uint64_t>() + 20, S.dev_small.as<const uint64_t>() + 40,
                                       evrec.as<uint4>(), aux.as<uint32_t>())) != WG_OK)
             return rc;
         c->n_events = nev;
