@@ -19,7 +19,7 @@ CXXFLAGS_HOST := -O2 -std=c++17 -fPIC -Wall -Wextra -Iinclude
 CFLAGS_ORACLE := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 
 all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgraph_host.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so \
-     tests/cpp/test_graph_layout profiles/microbench/store_ceiling profiles/microbench/launch_cost
+     tests/cpp/test_graph_layout profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost
 
 $(PKG)/wgraph/libwgraph.so: $(HIPSRC) $(HIPHDR)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIPSRC)
@@ -42,6 +42,9 @@ oracle/liboracle.so: oracle/wg_oracle.c oracle/wg_oracle.h include/wgraph.h incl
 profiles/microbench/store_ceiling: profiles/microbench/store_ceiling.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
+profiles/microbench/store_sweep: profiles/microbench/store_sweep.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
 profiles/microbench/launch_cost: profiles/microbench/launch_cost.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Wno-unused-value -Wno-unused-result -o $@ $<
 
@@ -51,6 +54,6 @@ engine: $(PKG)/wgraph/libwgraph.so
 host: $(PKG)/wgraph/libwgraph_host.so tests/cpp/test_graph_layout
 
 clean:
-	rm -f $(PKG)/wgraph/*.so oracle/*.so profiles/microbench/store_ceiling profiles/microbench/launch_cost tests/cpp/test_graph_layout
+	rm -f $(PKG)/wgraph/*.so oracle/*.so profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost tests/cpp/test_graph_layout
 
 .PHONY: all clean oracle synth engine host

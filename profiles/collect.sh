@@ -25,4 +25,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 if [ -x "$ROOT/profiles/microbench/store_ceiling" ]; then
     timeout -k 10 120 "$ROOT/profiles/microbench/store_ceiling" > "$OUT/store_ceiling.jsonl" 2> "$OUT/store_ceiling.err"
 fi
+if [ -x "$ROOT/profiles/microbench/store_sweep" ]; then
+    timeout -k 10 200 "$ROOT/profiles/microbench/store_sweep" > "$OUT/store_sweep.jsonl" 2> "$OUT/store_sweep.err"
+fi
 python3 "$ROOT/profiles/summarize.py" "$OUT" "$TAG"

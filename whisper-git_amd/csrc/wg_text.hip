@@ -239,6 +239,7 @@ struct QuadArgs {
     const wg_glyph *glyphs;
     float scale, spread, inv_w, inv_h;
     float4 color[6];                 // run colours, then the same at WG_DIM_ALPHA
+    uint64_t nblk, per_xcd;          // blocks of QT quads; blocks per XCD (XCD-aware order)
 };
 
 #ifndef WG_QUAD_THREADS
@@ -249,7 +250,11 @@ constexpr int QT = WG_QUAD_THREADS;
 __global__ void __launch_bounds__(QT) k_text_quads(QuadArgs A, float4 *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) float4 stage[QT / 64][64 * 12];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t q0 = (uint64_t)blockIdx.x * QT + w * 64;   // this wave's first quad
+    // XCD-aware order (as k_vtx_tile): workgroup b runs on XCD b % 8, which
+    // writes one contiguous eighth of the buffer
+    const uint64_t blk = (uint64_t)(blockIdx.x % 8u) * A.per_xcd + blockIdx.x / 8u;
+    if (blk >= A.nblk) return;
+    const uint64_t q0 = blk * QT + w * 64;   // this wave's first quad
     if (q0 >= A.nq) return;
     const uint64_t q = q0 + lane;
     float4 *st = stage[w];
@@ -397,7 +402,9 @@ int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, 
             Q.color[k] = make_float4(col[0], col[1], col[2], col[3]);
             Q.color[k + 3] = make_float4(col[0], col[1], col[2], col[3] * WG_DIM_ALPHA);
         }
-        hipLaunchKernelGGL(k_text_quads, dim3((uint32_t)((nq + QT - 1) / QT)), dim3(QT), 0, s, Q, c->text_vtx.as<float4>());
+        Q.nblk = (nq + QT - 1) / QT;
+        Q.per_xcd = (Q.nblk + 7) / 8;
+        hipLaunchKernelGGL(k_text_quads, dim3((uint32_t)(Q.per_xcd * 8)), dim3(QT), 0, s, Q, c->text_vtx.as<float4>());
         WG_HIP(c, hipGetLastError());
     }
     wg_stage_end(c);

@@ -126,7 +126,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         const float *__restrict__ height, const float *__restrict__ node_y, const uint32_t *__restrict__ lane_out,
         const uint8_t *__restrict__ color_out, const float4 *__restrict__ palette,
         const uint4 *__restrict__ tinfo, const uint8_t *__restrict__ match, int64_t mlo, int64_t mhi,
-        float4 *__restrict__ out) {
+        float4 *__restrict__ out, uint64_t ntl) {
     __shared__ RowInfo rows[MAXR];
     __shared__ __attribute__((aligned(4))) uint8_t pair_row[PAIRS];   // row (within the tile) of every vertex pair
     __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
@@ -137,11 +137,22 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     __shared__ float4 pal[2 * WG_PALETTE_SIZE];    // palette, then the same at WG_DIM_ALPHA
     __shared__ float2 circ[3][WG_TESS_NODE_SEGMENTS + 2];   // r*(cos, sin) for node, ring inner, ring outer radius
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint64_t v0 = (uint64_t)blockIdx.x * TILE;
-    // the grid may be sized by the buffer's capacity: tiles past the total
-    // exit, and a total beyond the capacity writes nothing (the host relaunches)
+    // the grid may be sized by the buffer's capacity (ntl tiles): workgroups
+    // past the total's tiles exit, and a total beyond the capacity writes
+    // nothing (the host relaunches)
     const uint64_t total = vtx_off[re - rb];
-    if (v0 >= total || total > vcap) return;
+    const uint64_t nt = (total + TILE - 1) / TILE;
+    if (total > vcap || nt > ntl) return;   // the tile records would not fit either
+    // XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin, so
+    // workgroup b runs on XCD b % 8; that XCD writes one contiguous eighth of the
+    // buffer (per tiles) instead of every 8th tile.  Store-only kernels of this
+    // shape: 5.6 -> 6.1-6.3 TB/s (profiles/microbench/store_sweep.hip).  The
+    // split follows the device's total, so the working workgroups are the
+    // first 8 * per of the grid, on all eight XCDs, whatever the capacity.
+    const uint64_t per = (nt + 7) / 8;
+    const uint64_t tile = (uint64_t)(blockIdx.x % 8u) * per + blockIdx.x / 8u;
+    if (blockIdx.x / 8u >= per || tile >= nt) return;
+    const uint64_t v0 = tile * TILE;
     if (tid < 3 * (WG_TESS_NODE_SEGMENTS + 1)) {
         const uint32_t w = tid / (WG_TESS_NODE_SEGMENTS + 1), q = tid % (WG_TESS_NODE_SEGMENTS + 1);
         const float r = w == 0 ? WG_NODE_RADIUS
@@ -153,7 +164,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     const uint64_t nrows = re - rb;
     const float visf = (float)(vis - 1);
     if (tid < 2 * WG_PALETTE_SIZE) pal[tid] = palette[tid];
-    const uint4 ti = tinfo[blockIdx.x], tn = tinfo[blockIdx.x + 1];
+    const uint4 ti = tinfo[tile], tn = tinfo[tile + 1];
     const uint64_t first = ti.x;
     const uint32_t A = ti.y, K0 = ti.z;
     uint32_t nV = tn.y + (tn.w & 1u) - A, nC = tn.z + ((tn.w >> 1) & 1u) - K0;
@@ -376,12 +387,13 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
                            c->tile_first.as<uint4>());
         wg_stage_end(c);
         wg_stage_begin(c, "vtx_emit");
-        hipLaunchKernelGGL(k_vtx_tile, dim3(grid), dim3(VT), 0, s, rb, re, vcap, vis, (const uint64_t *)off,
+        // (grid rounded up to whole XCD rounds: k_vtx_tile's tile order)
+        hipLaunchKernelGGL(k_vtx_tile, dim3((uint32_t)((grid + 7) / 8 * 8)), dim3(VT), 0, s, rb, re, vcap, vis, (const uint64_t *)off,
                            c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
                            c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
                            c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
                            c->palette.as<const float4>(), c->tile_first.as<const uint4>(), match, mlo, mhi,
-                           c->vtx.as<float4>());
+                           c->vtx.as<float4>(), grid);
         wg_stage_end(c);
     };
     const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;
