@@ -137,10 +137,11 @@ def main():
                     sl += ["", f"{k}: `{json.dumps(sb[k])}`"]
         with open(os.path.join(dest, f"{tag}_side_kernels.md"), "w") as f:
             f.write("\n".join(sl) + "\n")
-    sc = os.path.join(src, "store_ceiling.jsonl")
-    if os.path.exists(sc):
-        with open(sc) as f_in, open(os.path.join(dest, f"{tag}_store_ceiling.jsonl"), "w") as f_out:
-            f_out.write(f_in.read())
+    for name in ("store_ceiling", "store_sweep"):
+        sc = os.path.join(src, f"{name}.jsonl")
+        if os.path.exists(sc):
+            with open(sc) as f_in, open(os.path.join(dest, f"{tag}_{name}.jsonl"), "w") as f_out:
+                f_out.write(f_in.read())
     with open(os.path.join(dest, f"{tag}_pmc.json"), "w") as f:
         json.dump(pmc, f, indent=1)
     with open(os.path.join(dest, f"{tag}_kernels.md"), "w") as f:
