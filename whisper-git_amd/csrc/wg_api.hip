@@ -280,7 +280,8 @@ void wg_destroy(wg_ctx *c) {
                       &c->vert_off, &c->curve_off, &c->vert, &c->curve, &c->curve_color,
                       &c->curve_ref, &c->curve_row, &c->carry_off, &c->carry,
                       &c->scan_tmp, &c->scal, &c->rowflags, &c->rowflags_lists, &c->geom_diff, &c->scurve_off,
-                      &c->scurve_ref, &c->scurve_row, &c->sweep_big, &c->vtx_off, &c->vtx, &c->palette, &c->chk};
+                      &c->scurve_ref, &c->scurve_row, &c->sweep_big, &c->vtx_off, &c->vtx, &c->palette, &c->chk,
+                      &c->carry_sorted, &c->curve_cnt, &c->tile_first, &c->hs_time, &c->hs_out};
     for (DevBuf *b : bufs) b->release();
     for (DevBuf &b : c->lf) b.release();
     ShardState &S = c->sh;
@@ -300,6 +301,10 @@ void wg_destroy(wg_ctx *c) {
     for (DevBuf *b : xb) b->release();
     for (int f = 0; f < 2; f++) { c->match_txt[f].release(); c->match_off[f].release(); }
     for (DevBuf &b : c->ord) b.release();
+    for (FontSlot &f : c->fonts) {
+        DevBuf *fb[] = {&f.edges, &f.gdesc, &f.cov, &f.sdf, &f.gin, &f.gout, &f.d2in, &f.d2out, &f.gtab};
+        for (DevBuf *b : fb) b->release();
+    }
     for (int i = 0; i < WG_STAGE_MAX; i++) {
         if (c->stages[i].a) (void)hipEventDestroy(c->stages[i].a);
         if (c->stages[i].b) (void)hipEventDestroy(c->stages[i].b);
