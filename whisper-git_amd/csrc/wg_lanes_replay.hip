@@ -32,6 +32,14 @@
 
 #include "wg_internal.h"
 
+#ifdef WG_REPLAY_PROFILE
+// per iteration: [0] chunks run, [1] batches, [2] batches without scalar events,
+// [3] scalar special events, [4] of which merges with > 2 waiters, [5] cycles
+// per chunk (summed), [6] cycles in the scalar loop, [7] cycles in merges > 2
+__device__ unsigned long long g_rp[64][8];
+#define RP_ADD(i, v) atomicAdd(&g_rp[A.iter & 63][i], (unsigned long long)(v))
+#endif
+
 namespace {
 
 enum : uint32_t { F_A = 1u, F_O = 2u, F_C = 4u, F_M = 8u, F_IN0 = 1u << 14, F_IN1 = 1u << 22 };
@@ -39,12 +47,23 @@ enum : uint32_t { F_A = 1u, F_O = 2u, F_C = 4u, F_M = 8u, F_IN0 = 1u << 14, F_IN
 #define WG_JMAX 6
 #endif
 constexpr int JMAX = WG_JMAX;   // speculative passes per batch before the scalar replay takes over
+#ifndef WG_JMIN_ADV
+#define WG_JMIN_ADV 4
+#endif
+constexpr int JMIN_ADV = WG_JMIN_ADV;   // lanes a pass must resolve beyond the previous one to go on
 
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t lane) {
     return ((uint64_t)rl((uint32_t)(v >> 32), lane) << 32) | rl((uint32_t)v, lane);
+}
+// wave-uniform values loaded by every lane (global / LDS loads return VGPRs):
+// moved to SGPRs so the scalar replay's occupancy stays in SGPRs (SALU chains
+// instead of VALU + readlane hazards)
+__device__ __forceinline__ uint32_t ufl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t ufl64(uint64_t v) {
+    return ((uint64_t)ufl((uint32_t)(v >> 32)) << 32) | ufl((uint32_t)v);
 }
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
     const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64);
@@ -84,9 +103,13 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
     if (e0 >= nev) return;
     const uint64_t e1 = (e0 + A.chunk < nev) ? e0 + A.chunk : nev;
     const bool lds = A.chunk <= LSLOT_MAX;
+#ifdef WG_REPLAY_PROFILE
+    const unsigned long long rp_t0 = clock64();
+    unsigned long long rp_batches = 0, rp_fast = 0, rp_sev = 0, rp_fm = 0, rp_cs = 0, rp_cfm = 0;
+#endif
     // slot of a token born in this chunk before the current batch (this iteration)
     auto own = [&](uint64_t t) -> uint32_t { return lds ? (uint32_t)lslot[t - e0] : (uint32_t)A.slot_next[t]; };
-    uint64_t occ = c == 0 ? 0ull : A.occ_prev[c - 1];
+    uint64_t occ = c == 0 ? 0ull : ufl64(A.occ_prev[c - 1]);
     uint64_t occ_or = 0, alloc_or = 0;   // OR of the occupancy after each occupying allocation / of allocated slots
     bool diff = false;
     uint32_t prev_v = 0;
@@ -147,13 +170,25 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         // mismatch are exact at any time, so the scalar replay below only takes
         // over from there.  The guess is the previous iteration's slot, which is
         // already right for every chunk whose entry did not change.
-        if (sm && !__any((f_v & F_M) != 0)) {
+        // Iteration 1 has no previous slots (the guesses are the zero fill):
+        // its batches go to the scalar replay directly.  Passes that stop
+        // resolving lanes (fewer than JMIN_ADV more exact lanes than the
+        // previous pass: the guesses are wrong throughout, as in the first
+        // iterations after a chunk's entry changed) hand over to the scalar
+        // replay early instead of spending all JMAX passes.
+        if (sm && A.iter > 1 && !__any((f_v & F_M) != 0)) {
             const bool isA = (f_v & F_A) != 0, occupy = (f_v & F_O) != 0;
             const bool clrS = isC && special && !isA;
             const uint32_t src0 = (f_v >> 8) & 63u, src1 = (f_v >> 16) & 63u;
             uint32_t g = special ? gp_v : cur_v;
             uint64_t ob = occ, oa = occ, mism = ~0ull;
+            uint32_t lim_prev = 0;
             for (int it = 0; it < JMAX && mism; it++) {
+                if (it > 0) {   // progress of the last pass: lanes [0, lim) are exact
+                    const uint32_t lim_now = (uint32_t)__builtin_ctzll(mism);
+                    if (lim_now < lim_prev + (uint32_t)JMIN_ADV) break;
+                    lim_prev = lim_now;
+                }
                 const uint32_t ga = (uint32_t)__shfl((int)g, (int)src0, 64);
                 const uint32_t gb = (uint32_t)__shfl((int)g, (int)src1, 64);
                 const uint32_t a = (f_v & F_IN0) ? ga : s0, b = (f_v & F_IN1) ? gb : s1;
@@ -202,7 +237,15 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
             }
         }
         // ---- sequential part: special events (from the first unresolved one) --------
+#ifdef WG_REPLAY_PROFILE
+        rp_batches++;
+        if (!smask) rp_fast++;
+        const unsigned long long rp_s0 = clock64();
+#endif
         while (smask) {
+#ifdef WG_REPLAY_PROFILE
+            rp_sev++;
+#endif
             const uint32_t k = (uint32_t)__builtin_ctzll(smask);
             smask &= smask - 1;
             occ &= rl64(q, k);                                  // the folded run before event k
@@ -223,17 +266,24 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
                 uint64_t clr = (1ull << (a & 63u)) | (1ull << (b & 63u));
                 uint32_t m = a < b ? a : b;
                 if (f & F_M) {
+#ifdef WG_REPLAY_PROFILE
+                    rp_fm++;
+                    const unsigned long long rp_m0 = clock64();
+#endif
                     const uint32_t off = rl(row_v, k);      // record.w = aux offset: {count, tokens...}
-                    const uint32_t cnt = A.aux[off];
+                    const uint32_t cnt = ufl(A.aux[off]);
                     for (uint32_t x = 0; x < cnt; x++) {
-                        const uint32_t t = A.aux[off + 1 + x];
+                        const uint32_t t = ufl(A.aux[off + 1 + x]);
                         uint32_t ts;
                         if (t >= base) ts = rl(cur_v, (uint32_t)(t - base));
                         else if (have_prev && t >= pbase) ts = rl(prev_v, (uint32_t)(t - pbase));
-                        else ts = t < e0 ? A.slot_prev[t] : own(t);
+                        else ts = ufl(t < e0 ? A.slot_prev[t] : own(t));
                         clr |= 1ull << (ts & 63u);
                         m = ts < m ? ts : m;
                     }
+#ifdef WG_REPLAY_PROFILE
+                    rp_cfm += clock64() - rp_m0;
+#endif
                 }
                 occ &= ~clr;
                 if (f & F_O) occ |= 1ull << (m & 63u);
@@ -241,6 +291,9 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
             }
             cur_v = (lid == k) ? s : cur_v;
         }
+#ifdef WG_REPLAY_PROFILE
+        rp_cs += clock64() - rp_s0;
+#endif
         // the run after the last special event
         occ &= (sm >> 63) ? ~0ull : rl64(q, 63);
         if (base + lid < e1) {
@@ -273,6 +326,12 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         A.chunk_stats[2 * c + 1] = alloc_or ? 63u - (uint32_t)__builtin_clzll(alloc_or) : 0u; // max slot
     }
     if (__any(diff) || (lid == 0 && occ != A.occ_prev[c])) A.changed[A.iter] = 1u;
+#ifdef WG_REPLAY_PROFILE
+    if (lid == 0) {
+        RP_ADD(0, 1); RP_ADD(1, rp_batches); RP_ADD(2, rp_fast); RP_ADD(3, rp_sev); RP_ADD(4, rp_fm);
+        RP_ADD(5, clock64() - rp_t0); RP_ADD(6, rp_cs); RP_ADD(7, rp_cfm);
+    }
+#endif
 }
 
 __global__ void k_lf_replay_init(uint64_t nchunks, unsigned long long *occ_prev, uint32_t *changed, uint32_t nflags) {
@@ -409,3 +468,15 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
     if (R.nev) hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal);
     return hipGetLastError();
 }
+
+#ifdef WG_REPLAY_PROFILE
+// profiling builds only (-DWG_REPLAY_PROFILE): copy (and with reset, clear) the per-iteration counters
+extern "C" int wg_debug_replay_profile(unsigned long long *out, int reset) {
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rp), sizeof(g_rp)) != hipSuccess) return WG_E_HIP;
+    if (reset) {
+        static unsigned long long zero[64][8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_rp), zero, sizeof(zero)) != hipSuccess) return WG_E_HIP;
+    }
+    return WG_OK;
+}
+#endif
