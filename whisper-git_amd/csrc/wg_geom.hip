@@ -465,11 +465,44 @@ __device__ __forceinline__ Cubic subcurve(const Cubic &c, float a, float b) {   
 // are (a frame whose bands and row_top are unchanged above row pmin)
 // refilt (the frame pass): nonzero = the curve lists were refiltered by this
 // pass, so every record moved and pmin does not apply
-__global__ void k_curves(const uint32_t *__restrict__ nc, const uint32_t *__restrict__ curve_ref,
-                         const uint32_t *__restrict__ curve_row, const wg_edge *__restrict__ edges,
-                         const float *__restrict__ row_top, const float *__restrict__ node_y,
-                         const float2 *__restrict__ edge_y, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color,
-                         uint32_t pmin, Cap sc, uint32_t *ovf, const uint32_t *__restrict__ refilt) {
+// A segment's cubic (:552-562): child_y / parent_y from row_top + node_y, or
+// per edge (edge_y: row-sharded geometry, endpoints may lie in other shards)
+__device__ __forceinline__ Cubic edge_cubic(const wg_edge &e, uint32_t ref, const float *__restrict__ row_top,
+                                            const float *__restrict__ node_y, const float2 *__restrict__ edge_y,
+                                            float *child_y, float *parent_y) {
+    if (edge_y) {
+        const float2 ey = edge_y[ref];
+        *child_y = ey.x;
+        *parent_y = ey.y;
+    } else {
+        *child_y = row_top[e.child_row] + node_y[e.child_row];     // :554
+        *parent_y = row_top[e.parent_row] + node_y[e.parent_row];  // :555
+    }
+    const float dy = *parent_y - *child_y;
+    Cubic cv;
+    cv.p0 = Pt{(float)e.child_lane, *child_y};
+    cv.p1 = Pt{(float)e.child_lane, *child_y + dy * 0.4f};
+    cv.p2 = Pt{(float)e.parent_lane, *parent_y - dy * 0.4f};
+    cv.p3 = Pt{(float)e.parent_lane, *parent_y};
+    return cv;
+}
+
+// Curve clipping in two launches.  The strip bottom of an edge's segment in
+// row r (row_top[r + 1], r below the parent row) is the strip top of the same
+// edge's segment in row r + 1, so its t_at_y is the same value: k_curves_tb
+// bisects every segment's bottom once (t_b), k_curves takes each segment's
+// top from the same edge's record in the row above (a short search of that
+// row's edge-ordered list; a record filtered out there — an empty strip — is
+// bisected here instead): one bisection per segment instead of two.
+// pmin > 0: records of edges whose parent row is below pmin are left as they
+// are (a frame whose bands and row_top are unchanged above row pmin)
+// refilt (the frame pass): nonzero = the curve lists were refiltered by this
+// pass (every record moved: all are recomputed)
+__global__ void k_curves_tb(const uint32_t *__restrict__ nc, const uint32_t *__restrict__ curve_ref,
+                            const uint32_t *__restrict__ curve_row, const wg_edge *__restrict__ edges,
+                            const float *__restrict__ row_top, const float *__restrict__ node_y,
+                            const float2 *__restrict__ edge_y, float *__restrict__ tb, uint32_t pmin, Cap sc,
+                            uint32_t *ovf, const uint32_t *__restrict__ refilt) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (over(sc, ovf) || k >= *nc) return;   // grid sized by an upper bound; the count lives on the device
     if (refilt && *refilt) pmin = 0;
@@ -477,26 +510,38 @@ __global__ void k_curves(const uint32_t *__restrict__ nc, const uint32_t *__rest
     const wg_edge e = edges[ref];
     if (e.parent_row < pmin) return;
     const uint32_t row = curve_row[k];
+    if (row == e.parent_row) return;         // t_b = 1 (:589-593)
     float child_y, parent_y;
-    if (edge_y) {   // row-sharded geometry: endpoints may lie in other shards
-        const float2 ey = edge_y[ref];
-        child_y = ey.x;
-        parent_y = ey.y;
-    } else {
-        child_y = row_top[e.child_row] + node_y[e.child_row];     // :554
-        parent_y = row_top[e.parent_row] + node_y[e.parent_row];  // :555
-    }
-    const float dy = parent_y - child_y;
-    Cubic cv;
-    cv.p0 = Pt{(float)e.child_lane, child_y};
-    cv.p1 = Pt{(float)e.child_lane, child_y + dy * 0.4f};
-    cv.p2 = Pt{(float)e.parent_lane, parent_y - dy * 0.4f};
-    cv.p3 = Pt{(float)e.parent_lane, parent_y};
-    const float rtop = row_top[row], rbot = row_top[row + 1];
+    const Cubic cv = edge_cubic(e, ref, row_top, node_y, edge_y, &child_y, &parent_y);
+    tb[k] = t_at_y(cv, row_top[row + 1]);    // strip_bot = row bottom (:574-578)
+}
+
+__global__ void k_curves(const uint32_t *__restrict__ nc, const uint32_t *__restrict__ curve_ref,
+                         const uint32_t *__restrict__ curve_row, const uint32_t *__restrict__ curve_off,
+                         const wg_edge *__restrict__ edges, const float *__restrict__ row_top,
+                         const float *__restrict__ node_y, const float2 *__restrict__ edge_y,
+                         const float *__restrict__ tb, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color,
+                         uint32_t pmin, Cap sc, uint32_t *ovf, const uint32_t *__restrict__ refilt) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (over(sc, ovf) || k >= *nc) return;
+    if (refilt && *refilt) pmin = 0;
+    const uint32_t ref = curve_ref[k];
+    const wg_edge e = edges[ref];
+    if (e.parent_row < pmin) return;
+    const uint32_t row = curve_row[k];
+    float child_y, parent_y;
+    const Cubic cv = edge_cubic(e, ref, row_top, node_y, edge_y, &child_y, &parent_y);
+    const float rtop = row_top[row];
     const float strip_top = (row == e.child_row) ? child_y : rtop;
-    const float strip_bot = (row == e.parent_row) ? parent_y : rbot;
-    const float t_a = (row == e.child_row) ? 0.0f : t_at_y(cv, strip_top);
-    const float t_b = (row == e.parent_row) ? 1.0f : t_at_y(cv, strip_bot);
+    float t_a = 0.0f;
+    if (row != e.child_row) {
+        // the same edge's record in row - 1 holds t_at_y(row_top[row]) as its t_b
+        const uint32_t a0 = curve_off[row - 1], a1 = curve_off[row];
+        uint32_t j = a0;
+        while (j < a1 && curve_ref[j] < ref) j++;   // edge order
+        t_a = (j < a1 && curve_ref[j] == ref) ? tb[j] : t_at_y(cv, strip_top);
+    }
+    const float t_b = (row == e.parent_row) ? 1.0f : tb[k];
     const Cubic s = subcurve(cv, t_a, t_b);
     float4 *o = reinterpret_cast<float4 *>(out + k);
     o[0] = make_float4(s.p0.x, s.p0.y - rtop, s.p1.x, s.p1.y - rtop);
@@ -586,11 +631,15 @@ static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *c
 static void launch_curves(wg_ctx *c, uint64_t n, uint64_t n_upper, hipStream_t s, uint32_t pmin, Cap sc, uint32_t *ovf,
                           const uint32_t *refilt) {
     if (!n_upper) return;
-    hipLaunchKernelGGL(k_curves, dim3(blocks(n_upper)), dim3(T), 0, s, c->curve_off.as<const uint32_t>() + n,
+    hipLaunchKernelGGL(k_curves_tb, dim3(blocks(n_upper)), dim3(T), 0, s, c->curve_off.as<const uint32_t>() + n,
                        c->curve_ref.as<const uint32_t>(), c->curve_row.as<const uint32_t>(), c->edges.as<const wg_edge>(),
                        c->g_row_top.as<const float>(), c->g_node_y.as<const float>(),
-                       reinterpret_cast<const float2 *>(c->edge_y), c->curve.as<wg_curve>(), c->curve_color.as<uint8_t>(),
-                       pmin, sc, ovf, refilt);
+                       reinterpret_cast<const float2 *>(c->edge_y), c->curve_tb.as<float>(), pmin, sc, ovf, refilt);
+    hipLaunchKernelGGL(k_curves, dim3(blocks(n_upper)), dim3(T), 0, s, c->curve_off.as<const uint32_t>() + n,
+                       c->curve_ref.as<const uint32_t>(), c->curve_row.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
+                       c->edges.as<const wg_edge>(), c->g_row_top.as<const float>(), c->g_node_y.as<const float>(),
+                       reinterpret_cast<const float2 *>(c->edge_y), c->curve_tb.as<const float>(), c->curve.as<wg_curve>(),
+                       c->curve_color.as<uint8_t>(), pmin, sc, ovf, refilt);
 }
 
 // the lazily read summary of the last pass (total height, scan path, curve count)
@@ -745,6 +794,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         WG_ALLOC(c, c->curve_color, n_super + 16);
         WG_ALLOC(c, c->curve_ref, n_super * 4 + 16);
         WG_ALLOC(c, c->curve_row, n_super * 4 + 16);
+        WG_ALLOC(c, c->curve_tb, n_super * 4 + 16);
         WG_ALLOC(c, c->carry, ncarry * 4 + 16);
         WG_ALLOC(c, c->carry_sorted, ncarry * 4 + 16);
         n_super_grid = n_super;
@@ -757,6 +807,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         scap = std::min(scap, cap_of(c->curve_color, 1));
         scap = std::min(scap, cap_of(c->curve_ref, 4));
         scap = std::min(scap, cap_of(c->curve_row, 4));
+        scap = std::min(scap, cap_of(c->curve_tb, 4));
         const uint64_t ccap = std::min(cap_of(c->carry, 4), cap_of(c->carry_sorted, 4));
         auto u32 = [](uint64_t v) { return (uint32_t)std::min<uint64_t>(v, 0xFFFFFFFEull); };
         vc = Cap{voff + n, u32(vcap)};

@@ -208,6 +208,7 @@ struct wg_ctx {
     DevBuf vert, curve, curve_color;
     DevBuf curve_ref;       // uint32 [n_curve] edge id per curve record
     DevBuf curve_row;       // uint32 [n_curve] row per curve record
+    DevBuf curve_tb;        // float [n_curve] each record's t at its strip bottom (k_curves_tb)
     DevBuf carry_off, carry, carry_sorted;  // sweep carry-in lists (registration order / edge order)
     DevBuf curve_cnt;                       // uint32 [N+1] per-row curve counts (filter)
     uint64_t lists_nsuper = 0;              // curve superset records of the lists in place
