@@ -51,8 +51,9 @@ __global__ void __launch_bounds__(TH) k_tiles(v4f *out, size_t n, size_t ntiles)
     }
 }
 
-int main() {
-    const size_t bytes = 5856279118ull & ~(size_t)15;
+int main(int argc, char **argv) {
+    // optional argv[1]: bytes written per launch (default: the 1M-row wide16 vertex buffer)
+    const size_t bytes = (argc > 1 ? strtoull(argv[1], nullptr, 10) : 5856279118ull) & ~(size_t)15;
     const size_t n = bytes / 16;
     v4f *out;
     CHECK(hipMalloc(&out, bytes));
@@ -74,8 +75,8 @@ int main() {
             best = ms < best ? ms : best;
             sum += ms;
         }
-        printf("{\"variant\": \"%s\", \"best_ms\": %.4f, \"avg_ms\": %.4f, \"best_TBps\": %.3f, \"avg_TBps\": %.3f}\n", name,
-               best, sum / reps, bytes / (best * 1e-3) / 1e12, bytes / (sum / reps * 1e-3) / 1e12);
+        printf("{\"variant\": \"%s\", \"bytes\": %zu, \"best_ms\": %.4f, \"avg_ms\": %.4f, \"best_TBps\": %.3f, \"avg_TBps\": %.3f}\n",
+               name, bytes, best, sum / reps, bytes / (best * 1e-3) / 1e12, bytes / (sum / reps * 1e-3) / 1e12);
         fflush(stdout);
     };
 #define V(NT, R, TH, MAP, GRID, NAME)                                                                          \
@@ -99,6 +100,7 @@ int main() {
     V(true, 3, 512, MAP_XCD, 0, "24KiB/512 nt xcd-split");
     V(true, 12, 256, MAP_XCD, 0, "48KiB/256 nt xcd-split");
     V(false, 12, 256, MAP_XCD, 0, "48KiB/256 plain xcd-split");
+    V(true, 18, 256, MAP_XCD, 0, "72KiB/256 nt xcd-split");
     CHECK(hipFree(out));
     return 0;
 }

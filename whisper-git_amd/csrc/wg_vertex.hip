@@ -153,24 +153,92 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     const uint64_t tile = (uint64_t)(blockIdx.x % 8u) * per + blockIdx.x / 8u;
     if (blockIdx.x / 8u >= per || tile >= nt) return;
     const uint64_t v0 = tile * TILE;
-    if (tid < 3 * (WG_TESS_NODE_SEGMENTS + 1)) {
-        const uint32_t w = tid / (WG_TESS_NODE_SEGMENTS + 1), q = tid % (WG_TESS_NODE_SEGMENTS + 1);
-        const float r = w == 0 ? WG_NODE_RADIUS
-                      : w == 1 ? WG_NODE_RADIUS - WG_SELECTED_RING_WIDTH * 0.5f
-                               : WG_NODE_RADIUS + WG_SELECTED_RING_WIDTH * 0.5f;
-        circ[w][q] = make_float2(r * c_cos[q], r * c_sin[q]);
-    }
+    const uint4 ti = tinfo[tile], tn = tinfo[tile + 1];   // everything below hangs on these
     const uint64_t v1 = (v0 + TILE < total) ? v0 + TILE : total;
     const uint64_t nrows = re - rb;
     const float visf = (float)(vis - 1);
-    if (tid < 2 * WG_PALETTE_SIZE) pal[tid] = palette[tid];
-    const uint4 ti = tinfo[tile], tn = tinfo[tile + 1];
     const uint64_t first = ti.x;
     const uint32_t A = ti.y, K0 = ti.z;
     uint32_t nV = tn.y + (tn.w & 1u) - A, nC = tn.z + ((tn.w >> 1) & 1u) - K0;
     nV = nV < (uint32_t)MAXV ? nV : (uint32_t)MAXV;   // bounds hold by construction; never overrun LDS
     nC = nC < (uint32_t)MAXC ? nC : (uint32_t)MAXC;
     // ---- 1. one round of independent global loads: rows, verticals, curves ---------
+    // Every load of the tile is issued before any is used (wave 0 the rows, the
+    // other waves first the vertical entries, every thread its curve strip
+    // points' records): once the geometry no longer sits in the Infinity Cache
+    // each round trip costs microseconds under the saturated write stream, and
+    // rows -> verticals -> curves one after the other in wave 0 took the
+    // Linux-shaped list's emission from 2.3 to 3.3 ms.
+    // only the rows overlapping the tile, [first, first row of the next tile]:
+    // loading a fixed 64-row window made every XCD's L2 fetch nearly every
+    // row (tiles are dealt round-robin to the 8 XCDs) — 0.3 GB of HBM reads
+    // per 1M-row launch
+    const uint64_t jr = first + lane;
+    const uint32_t span = tn.x >= first ? (uint32_t)(tn.x - first) : 0u;
+    const bool rowok = wid == 0 && jr < nrows && lane <= span && lane < (uint32_t)MAXR;
+    // the row's words as loaded: no arithmetic on them until every load is out
+    uint64_t r_vstart = 0;
+    uint32_t r_v0 = 0, r_v1 = 0, r_c0 = 0, r_c1 = 0, r_lane = 0, r_col = 0, r_m = 1;
+    float r_h = 0.0f, r_ny = 0.0f;
+    if (rowok) {
+        const uint64_t r = rb + jr;
+        r_vstart = vtx_off[jr];
+        r_v0 = voff[r];
+        r_v1 = voff[r + 1];
+        r_c0 = coff[r];
+        r_c1 = coff[r + 1];
+        r_h = height[r];
+        r_ny = node_y[r];
+        r_lane = lane_out[r];
+        r_col = color_out[r];
+        // search dimming (history_view, commit_graph.rs:1467, 1482): rows of the
+        // match range whose flag is 0 take the dimmed palette
+        if (match && (int64_t)r >= mlo && (int64_t)r < mhi) r_m = match[(int64_t)r - mlo];
+    }
+    constexpr int VPT = (MAXV + VT - 1) / VT, CPT = (MAXC * NPTS + VT - 1) / VT;
+    const uint32_t vi0 = (tid + VT - 64) % VT;   // vertical entries: waves 1.. first (wave 0 loads the rows)
+    uint32_t vv[VPT];
+#pragma unroll
+    for (int q = 0; q < VPT; q++) {
+        const uint32_t i = vi0 + q * VT;
+        vv[q] = i < nV ? vert[A + i] : 0u;
+    }
+    float4 ca[CPT], cb[CPT];
+    uint32_t ccol[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; q++) {
+        const uint32_t task = tid + q * VT, k = K0 + task / NPTS;
+        ca[q] = cb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        ccol[q] = 0;
+        if (task < nC * NPTS) {
+            ca[q] = reinterpret_cast<const float4 *>(curve + k)[0];
+            cb[q] = reinterpret_cast<const float4 *>(curve + k)[1];
+            if (task % NPTS == 0) ccol[q] = curve_color[k];
+        }
+    }
+    float4 palv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < 2 * WG_PALETTE_SIZE) palv = palette[tid];
+    const uint32_t cw = tid / (WG_TESS_NODE_SEGMENTS + 1), cq = tid % (WG_TESS_NODE_SEGMENTS + 1);
+    float cc = 0.0f, cs = 0.0f;
+    if (tid < 3 * (WG_TESS_NODE_SEGMENTS + 1)) { cc = c_cos[cq]; cs = c_sin[cq]; }
+    if (tid < 3 * (WG_TESS_NODE_SEGMENTS + 1)) {
+        const float r = cw == 0 ? WG_NODE_RADIUS
+                      : cw == 1 ? WG_NODE_RADIUS - WG_SELECTED_RING_WIDTH * 0.5f
+                                : WG_NODE_RADIUS + WG_SELECTED_RING_WIDTH * 0.5f;
+        circ[cw][cq] = make_float2(r * cc, r * cs);
+    }
+    if (tid < 2 * WG_PALETTE_SIZE) pal[tid] = palv;
+    RowInfo ri;
+    ri.vstart = r_vstart;
+    ri.voff = r_v0;
+    ri.nv = r_v1 - r_v0;
+    ri.coff = r_c0;
+    ri.nc = r_c1 - r_c0;
+    ri.h = r_h;
+    ri.ny = r_ny;
+    ri.cx = lane_x(r_lane, vis);
+    ri.ncol = r_col;
+    ri.dim = r_m ? 0u : 8u;
     if (wid == 0) {
         // wave 0 alone clears pair_row and then marks the row starts: LDS ops of
         // one wave complete in order, so no other wave can clear a mark after it
@@ -179,44 +247,26 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         for (uint32_t i = lane; i < PAIRS / 4; i += 64) reinterpret_cast<uint32_t *>(pair_row)[i] = 0u;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        // only the rows overlapping the tile, [first, first row of the next tile]:
-        // loading a fixed 64-row window made every XCD's L2 fetch nearly every
-        // row (tiles are dealt round-robin to the 8 XCDs) — 0.3 GB of HBM reads
-        // per 1M-row launch
-        const uint64_t j0 = first + lane;
-        const uint32_t span = tn.x >= first ? (uint32_t)(tn.x - first) : 0u;
-        if (j0 < nrows && lane <= span && lane < (uint32_t)MAXR) {
-        const uint64_t j = j0;
-        const uint64_t r = rb + j;
-        RowInfo ri;
-        ri.vstart = vtx_off[j];
-        ri.voff = voff[r];
-        ri.nv = voff[r + 1] - ri.voff;
-        ri.coff = coff[r];
-        ri.nc = coff[r + 1] - ri.coff;
-        ri.h = height[r];
-        ri.ny = node_y[r];
-        ri.cx = lane_x(lane_out[r], vis);
-        ri.ncol = color_out[r];
-        // search dimming (history_view, commit_graph.rs:1467, 1482): rows of the
-        // match range whose flag is 0 take the dimmed palette
-        ri.dim = (match && (int64_t)r >= mlo && (int64_t)r < mhi && !match[(int64_t)r - mlo]) ? 8u : 0u;
-        if (ri.vstart < v1) {
+        if (rowok && ri.vstart < v1) {
             rows[lane] = ri;
             const uint32_t sp = ri.vstart > v0 ? (uint32_t)((ri.vstart - v0) >> 1) : 0u;
             pair_row[sp] = lane;   // distinct rows start at distinct pairs (>= 36 pairs per row)
         }
-        }
     }
-    for (uint32_t i = tid; i < nV; i += VT) vents[i] = vert[A + i];
+#pragma unroll
+    for (int q = 0; q < VPT; q++) {
+        const uint32_t i = vi0 + q * VT;
+        if (i < nV) vents[i] = vv[q];
+    }
     {
+        // the <= MAXC curve segments overlapping the tile, tessellated once
         const float hw = WG_LINE_WIDTH * 0.5f;
-        for (uint32_t task = tid; task < nC * NPTS; task += VT) {
+#pragma unroll
+        for (int q = 0; q < CPT; q++) {
+            const uint32_t task = tid + q * VT;
+            if (task >= nC * NPTS) break;
             const uint32_t slot = task / NPTS, jj = task % NPTS;
-            const uint32_t k = K0 + slot;
-            const float4 a = reinterpret_cast<const float4 *>(curve + k)[0];
-            const float4 b = reinterpret_cast<const float4 *>(curve + k)[1];
-            float X[4] = {a.x, a.z, b.x, b.z}, Y[4] = {a.y, a.w, b.y, b.w};
+            float X[4] = {ca[q].x, ca[q].z, cb[q].x, cb[q].z}, Y[4] = {ca[q].y, ca[q].w, cb[q].y, cb[q].w};
 #pragma unroll
             for (int i = 0; i < 4; i++) X[i] = clamp_rs(X[i], 0.0f, visf) * WG_LANE_W + WG_LANE_W * 0.5f;  // to_x (:847-850)
             const float t = (float)jj * WG_TESS_DT;
@@ -229,7 +279,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
             float nx, ny;
             if (len > 0.0f) { nx = -dy / len; ny = dx / len; } else { nx = 1.0f; ny = 0.0f; }
             pts[task] = make_float4(px + hw * nx, py + hw * ny, px - hw * nx, py - hw * ny);
-            if (jj == 0) curve_col[slot] = curve_color[k];
+            if (jj == 0) curve_col[slot] = ccol[q];
         }
     }
     __syncthreads();
