@@ -42,7 +42,19 @@ constexpr uint32_t XT_PENDING = 0xFFFFFFFEu;
 inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
 
 // ---- X1 / X2: parent resolution ------------------------------------------------
-__global__ void k_sh_insert(const uint8_t *__restrict__ oid, uint64_t s, uint64_t nl, unsigned long long *table,
+// Local table of the shard's own rows, in the two passes of wg_hash.hip
+// (place: plain store to the home slot; settle: the rows that lost their home
+// slot probe on with compare-and-swap)
+__global__ void k_sh_place(const uint8_t *__restrict__ oid, uint64_t s, uint64_t nl, unsigned long long *table,
+                           uint64_t mask) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const uint64_t gi = s + i;
+    const Key k = load_key(oid + gi * 20);
+    table[key_hash(k) & mask] = ((unsigned long long)key_fp(k) << 32) | (uint32_t)gi;
+}
+
+__global__ void k_sh_settle(const uint8_t *__restrict__ oid, uint64_t s, uint64_t nl, unsigned long long *table,
                             uint64_t mask) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nl) return;
@@ -50,8 +62,9 @@ __global__ void k_sh_insert(const uint8_t *__restrict__ oid, uint64_t s, uint64_
     const Key k = load_key(oid + gi * 20);
     const unsigned long long mine = ((unsigned long long)key_fp(k) << 32) | (uint32_t)gi;
     uint64_t h = key_hash(k) & mask;
+    unsigned long long cur = table[h];
+    if (cur == mine) return;
     for (uint64_t probes = 0; probes <= mask; probes++) {
-        unsigned long long cur = table[h];
         if (cur == HEMPTY) {
             const unsigned long long prev = atomicCAS(&table[h], HEMPTY, mine);
             if (prev == HEMPTY) return;
@@ -62,12 +75,24 @@ __global__ void k_sh_insert(const uint8_t *__restrict__ oid, uint64_t s, uint64_
             return;
         }
         h = (h + 1) & mask;
+        cur = table[h];
     }
 }
 
-// every id whose partition (hash) is this rank: any id seen twice?
-__global__ void k_sh_dupscan(const uint8_t *__restrict__ oid, uint64_t n, uint32_t world, uint32_t rank,
-                             unsigned long long *table, uint64_t mask, uint32_t *flags) {
+// every id whose partition (hash) is this rank: any id seen twice?  Same two
+// passes over the partition table; a settling row that meets its own key flags it.
+__global__ void k_sh_dup_place(const uint8_t *__restrict__ oid, uint64_t n, uint32_t world, uint32_t rank,
+                               unsigned long long *table, uint64_t mask) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Key k = load_key(oid + i * 20);
+    const uint64_t hk = key_hash(k);
+    if ((uint32_t)((hk >> 40) % world) != rank) return;
+    table[hk & mask] = ((unsigned long long)key_fp(k) << 32) | (uint32_t)i;
+}
+
+__global__ void k_sh_dup_settle(const uint8_t *__restrict__ oid, uint64_t n, uint32_t world, uint32_t rank,
+                                unsigned long long *table, uint64_t mask, uint32_t *flags) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Key k = load_key(oid + i * 20);
@@ -75,8 +100,9 @@ __global__ void k_sh_dupscan(const uint8_t *__restrict__ oid, uint64_t n, uint32
     if ((uint32_t)((hk >> 40) % world) != rank) return;
     const unsigned long long mine = ((unsigned long long)key_fp(k) << 32) | (uint32_t)i;
     uint64_t h = hk & mask;
+    unsigned long long cur = table[h];
+    if (cur == mine) return;
     for (uint64_t probes = 0; probes <= mask; probes++) {
-        unsigned long long cur = table[h];
         if (cur == HEMPTY) {
             const unsigned long long prev = atomicCAS(&table[h], HEMPTY, mine);
             if (prev == HEMPTY) return;
@@ -87,6 +113,7 @@ __global__ void k_sh_dupscan(const uint8_t *__restrict__ oid, uint64_t n, uint32
             return;
         }
         h = (h + 1) & mask;
+        cur = table[h];
     }
 }
 
@@ -733,9 +760,13 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8, st));
     WG_HIP(c, hipMemsetAsync(S.ptable.p, 0xFF, pcap * 8, st));
     WG_HIP(c, hipMemsetAsync(S.flags.p, 0, 64, st));
-    if (nl) hipLaunchKernelGGL(k_sh_insert, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
+    if (nl) hipLaunchKernelGGL(k_sh_place, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
                                c->hash.as<unsigned long long>(), cap - 1);
-    if (N) hipLaunchKernelGGL(k_sh_dupscan, dim3(blocks(N)), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
+    if (N) hipLaunchKernelGGL(k_sh_dup_place, dim3(blocks(N)), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
+                              S.ptable.as<unsigned long long>(), pcap - 1);
+    if (nl) hipLaunchKernelGGL(k_sh_settle, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
+                               c->hash.as<unsigned long long>(), cap - 1);
+    if (N) hipLaunchKernelGGL(k_sh_dup_settle, dim3(blocks(N)), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
                               S.ptable.as<unsigned long long>(), pcap - 1, S.flags.as<uint32_t>());
     if (nl) hipLaunchKernelGGL(k_sh_probe, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid,
                                c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>(),
