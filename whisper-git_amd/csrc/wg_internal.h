@@ -11,6 +11,45 @@
 
 #include "wgraph.h"
 
+// ---- wave-level scans on DPP (no LDS round trip per step) --------------------
+// __shfl_up compiles to ds_bpermute: every step of a shuffle scan is an LDS
+// round trip (~50+ cycles), and the single-wave kernels (row_top walk, lane
+// replay) are chains of such scans.  These use the GFX9 DPP row shifts and
+// row broadcasts instead (the pattern of rocPRIM's warp scan); the combine is
+// applied in order, comb(earlier, later), so it need not commute.
+template <int CTRL, int ROWMASK, class T>
+__device__ __forceinline__ T wg_dpp(const T &old, const T &x) {
+    static_assert(sizeof(T) % 4 == 0, "DPP moves 32-bit words");
+    constexpr int N = sizeof(T) / 4;
+    uint32_t o[N], v[N], r[N];
+    __builtin_memcpy(o, &old, sizeof(T));
+    __builtin_memcpy(v, &x, sizeof(T));
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        r[i] = (uint32_t)__builtin_amdgcn_update_dpp((int)o[i], (int)v[i], CTRL, ROWMASK, 0xF, false);
+    T out;
+    __builtin_memcpy(&out, r, sizeof(T));
+    return out;
+}
+// inclusive scan over the 64 lanes: lane i gets comb(x_0, ..., x_i); id = identity
+template <class T, class C>
+__device__ __forceinline__ T wg_wave_scan(T x, const T &id, C comb) {
+    x = comb(wg_dpp<0x111, 0xF>(id, x), x);   // row_shr:1
+    x = comb(wg_dpp<0x112, 0xF>(id, x), x);   // row_shr:2
+    x = comb(wg_dpp<0x114, 0xF>(id, x), x);   // row_shr:4
+    x = comb(wg_dpp<0x118, 0xF>(id, x), x);   // row_shr:8
+    x = comb(wg_dpp<0x142, 0xA>(id, x), x);   // row_bcast:15 into rows 1, 3
+    x = comb(wg_dpp<0x143, 0xC>(id, x), x);   // row_bcast:31 into rows 2, 3
+    return x;
+}
+// lane i gets lane i - 1's value, lane 0 gets id (exclusive from inclusive)
+template <class T>
+__device__ __forceinline__ T wg_wave_shr1(const T &x, const T &id) { return wg_dpp<0x138, 0xF>(id, x); }
+// lane `lane`'s value in every lane (lane wave-uniform)
+__device__ __forceinline__ uint32_t wg_lane(uint32_t v, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
 #define WG_EMPTY 0xFFFFFFFFu   // "None" slot / empty hash entry / no row
 
 // ---------------------------------------------------------------------------

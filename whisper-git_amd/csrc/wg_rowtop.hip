@@ -68,17 +68,9 @@ __device__ __forceinline__ Td td_compose(const Td &A, const Td &B) {
     r.f = o0 | (o1 << 1) | (A.f & B.f & 4u);
     return r;
 }
-__device__ __forceinline__ Td td_shfl_up(const Td &v, int d) {
-    return Td{(uint32_t)__shfl_up((int)v.d0, d, 64), (uint32_t)__shfl_up((int)v.d1, d, 64),
-              (uint32_t)__shfl_up((int)v.f, d, 64)};
-}
-__device__ __forceinline__ Td td_shfl_down(const Td &v, int d) {
-    return Td{(uint32_t)__shfl_down((int)v.d0, d, 64), (uint32_t)__shfl_down((int)v.d1, d, 64),
-              (uint32_t)__shfl_down((int)v.f, d, 64)};
-}
-__device__ __forceinline__ Td td_shfl(const Td &v, int lane) {
-    return Td{(uint32_t)__shfl((int)v.d0, lane, 64), (uint32_t)__shfl((int)v.d1, lane, 64),
-              (uint32_t)__shfl((int)v.f, lane, 64)};
+// ordered inclusive scan of the lanes' transducers: lane i gets T_0 o ... o T_i
+__device__ __forceinline__ Td td_scan(const Td &t) {
+    return wg_wave_scan(t, td_identity(), [](const Td &a, const Td &b) { return td_compose(a, b); });
 }
 
 // The step at binade k: acc = 2^k + p*u represents every acc of parity p.
@@ -180,14 +172,10 @@ __global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__res
         const uint64_t c = base + threadIdx.x;
         const double v = c < nch ? ch[c].sum : 0.0;
         const uint32_t nonint = (c < nch && !ch[c].integral) ? 1u : 0u;
-        double inc = v;
-        uint32_t ninc = nonint;   // inclusive count of non-integral chunks
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        for (int d = 1; d < 64; d <<= 1) {
-            const double o = __shfl_up(inc, d, 64);
-            const uint32_t on = (uint32_t)__shfl_up((int)ninc, d, 64);
-            if (lane >= d) { inc += o; ninc += on; }
-        }
+        // chunk sums of integral steps are integers: the f64 prefix is exact in any order
+        const double inc = wg_wave_scan(v, 0.0, [](double a, double b) { return a + b; });
+        const uint32_t ninc = wg_wave_scan(nonint, 0u, [](uint32_t a, uint32_t b) { return a + b; });   // inclusive count of non-integral chunks
         if (lane == 63) { ws[w] = inc; wn[w] = ninc; }
         __syncthreads();
         double wb = 0.0, tot = 0.0;
@@ -229,12 +217,8 @@ __global__ void __launch_bounds__(RT_T) k_rt_tables(uint64_t n, const float *__r
 #pragma unroll
         for (int q = 0; q < RT_Q; q++)
             if (r0 + q < n) t = td_compose(t, row_td(s[q], k));
-        // ordered wave reduction: lane i absorbs [i, i+2d)
-        for (int d = 1; d < 64; d <<= 1) {
-            Td o = td_shfl_down(t, d);
-            if (((threadIdx.x & 63) & (2 * d - 1)) == 0 && (threadIdx.x & 63) + d < 64) t = td_compose(t, o);
-        }
-        if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = t;
+        t = td_scan(t);   // lane 63: the wave's rows composed in order
+        if ((threadIdx.x & 63) == 63) wt[threadIdx.x >> 6] = t;
         __syncthreads();
         if (threadIdx.x == 0) {
             Td a = wt[0];
@@ -249,13 +233,8 @@ __global__ void __launch_bounds__(RT_T) k_rt_tables(uint64_t n, const float *__r
 constexpr int RT_SUP = 64;
 struct SupState { float start; int32_t k; uint32_t mode; uint32_t pad; };   // mode 1: walked at super level
 
-__device__ __forceinline__ Td td_reduce64(Td t) {   // ordered: lane 0 gets T_0 o ... o T_63
-    const int lid = threadIdx.x & 63;
-    for (int d = 1; d < 64; d <<= 1) {
-        const Td o = td_shfl_down(t, d);
-        if ((lid & (2 * d - 1)) == 0 && lid + d < 64) t = td_compose(t, o);
-    }
-    return t;
+__device__ __forceinline__ Td td_reduce64(Td t) {   // ordered: lane 63 gets T_0 o ... o T_63
+    return td_scan(t);
 }
 
 __global__ void __launch_bounds__(64) k_rt_super(uint64_t nch, const RtChunk *__restrict__ ch, const uint4 *__restrict__ tables,
@@ -276,7 +255,7 @@ __global__ void __launch_bounds__(64) k_rt_super(uint64_t nch, const RtChunk *__
         t = td_reduce64(t);
         // ulp counts stay far below 2^32 only where the ulp is >= 2 (k >= 24) and the sum is bounded
         const bool fits = full && k >= 24 && k < 120 && sm < ldexp(1.0, k - 23) * 2147483648.0;
-        if ((threadIdx.x & 63) == 0) stab[S * WG_RT_NBIN + j] = fits ? make_uint4(t.d0, t.d1, t.f, 0u) : make_uint4(0u, 0u, 2u, 0u);
+        if ((threadIdx.x & 63) == 63) stab[S * WG_RT_NBIN + j] = fits ? make_uint4(t.d0, t.d1, t.f, 0u) : make_uint4(0u, 0u, 2u, 0u);
     }
     if ((threadIdx.x & 63) == 0) skbase[S] = k0;
 }
@@ -293,13 +272,8 @@ __global__ void __launch_bounds__(64) k_rt_fill(uint64_t nch, const SupState *__
     const uint32_t p0 = parity_at(st.start, st.k);
     const int b = st.k - ch[cc].kguess + 1;
     const uint4 q = tables[cc * WG_RT_NBIN + b];   // valid: the super table was composed from these
-    Td t = Td{q.x, q.y, q.z};
-    for (int d = 1; d < 64; d <<= 1) {
-        const Td o = td_shfl_up(t, d);
-        if (lid >= d) t = td_compose(o, t);
-    }
-    Td ex = td_shfl_up(t, 1);
-    if (lid == 0) ex = td_identity();
+    const Td t = td_scan(Td{q.x, q.y, q.z});
+    const Td ex = wg_wave_shr1(t, td_identity());
     const uint32_t D = p0 ? ex.d1 : ex.d0;
     ch[cc].start = st.start + (float)D * u;
     ch[cc].kstart = st.k;
@@ -348,18 +322,14 @@ __device__ float replay_rows(uint64_t r0, uint64_t r1, float acc, const float *_
             const float u = ldexpf(1.0f, k - 23);
             const double top = ldexp(1.0, k + 1);
             const uint32_t p = parity_at(acc, k);
-            Td t = (lid >= j && lid < cnt) ? row_td(sv, k) : td_identity();
-            for (int d = 1; d < 64; d <<= 1) {
-                const Td o = td_shfl_up(t, d);
-                if (lid >= (uint32_t)d) t = td_compose(o, t);
-            }
+            const Td t = td_scan((lid >= j && lid < cnt) ? row_td(sv, k) : td_identity());
             const uint32_t D = p ? t.d1 : t.d0;   // ulps added through this lane's row
             const bool ok = (t.f & 4u) && (double)acc + (double)D * (double)u < top;
             const uint64_t okm = __ballot(ok || lid < j) | (cnt < 64 ? (~0ull << cnt) : 0ull);
             const uint32_t f = okm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);   // first row crossing the binade
-            const uint32_t Dprev = (uint32_t)__shfl_up((int)D, 1, 64);
+            const uint32_t Dprev = wg_wave_shr1(D, 0u);
             if (lid >= j && lid < f) mine = acc + (float)(lid == j ? 0u : Dprev) * u;
-            if (f > j) acc = acc + (float)(uint32_t)__shfl((int)D, (int)(f - 1), 64) * u;
+            if (f > j) acc = acc + (float)wg_lane(D, f - 1) * u;
             j = f;
             if (j < cnt) {   // the crossing row itself: one ordinary f32 add
                 const float sj = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, sv), (int)j));
@@ -410,13 +380,8 @@ __device__ float replay_chunk(uint64_t r0, uint64_t r1, float acc, const float *
             const uint32_t j = lid * RP_Q + q;
             if (j >= j0 && j < cnt) t = td_compose(t, row_td(sv[q], k));
         }
-        Td inc = t;
-        for (int d = 1; d < 64; d <<= 1) {
-            const Td o = td_shfl_up(inc, d);
-            if (lid >= (uint32_t)d) inc = td_compose(o, inc);
-        }
-        Td ex = td_shfl_up(inc, 1);
-        if (lid == 0) ex = td_identity();
+        const Td inc = td_scan(t);
+        const Td ex = wg_wave_shr1(inc, td_identity());
         const uint32_t Dinc = p ? inc.d1 : inc.d0;
         const bool ok = (inc.f & 4u) && (double)acc + (double)Dinc * (double)u < top;
         const uint64_t okm = __ballot(ok);
@@ -436,10 +401,10 @@ __device__ float replay_chunk(uint64_t r0, uint64_t r1, float acc, const float *
             }
         }
         if (f == 64u) {
-            acc = acc + (float)(uint32_t)__shfl((int)Dinc, 63, 64) * u;
+            acc = acc + (float)wg_lane(Dinc, 63) * u;
             break;
         }
-        float a = acc + (float)(f == 0u ? 0u : (uint32_t)__shfl((int)Dinc, (int)f - 1, 64)) * u;
+        float a = acc + (float)(f == 0u ? 0u : wg_lane(Dinc, f - 1)) * u;
 #pragma unroll
         for (int q = 0; q < RP_Q; q++) {
             const uint32_t j = f * RP_Q + q;
@@ -493,18 +458,15 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
                 const int b = k - skbase[ss];
                 if (b >= 0 && b < WG_RT_NBIN) { const uint4 q = stab[ss * WG_RT_NBIN + b]; t = Td{q.x, q.y, q.z}; }
             }
-            for (int d = 1; d < 64; d <<= 1) {
-                Td o = td_shfl_up(t, d);
-                if (lid >= d) t = td_compose(o, t);
-            }
+            t = td_scan(t);
             const uint32_t D = p ? t.d1 : t.d0;
             const bool ok = (t.f & 4u) && ss < nsup && (double)A + (double)D * (double)u < top;
             const uint64_t okm = __ballot(ok);
             const int f = okm == ~0ull ? 64 : (int)__builtin_ctzll(~okm);
-            const uint32_t Dprev = (uint32_t)__shfl_up((int)D, 1, 64);
+            const uint32_t Dprev = wg_wave_shr1(D, 0u);
             if (lid < f) sup[ss] = SupState{A + (float)(lid == 0 ? 0u : Dprev) * u, k, 1u, 0u};
             if (f > 0) {
-                A = A + (float)(uint32_t)__shfl((int)D, f - 1, 64) * u;
+                A = A + (float)wg_lane(D, (uint32_t)f - 1) * u;
                 c += (uint64_t)f * RT_SUP;
                 continue;
             }
@@ -523,17 +485,13 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
                     t = Td{q.x, q.y, q.z};
                 }
             }
-            // ordered inclusive scan: P_j = T_c o ... o T_{c+j}
-            for (int d = 1; d < 64; d <<= 1) {
-                Td o = td_shfl_up(t, d);
-                if (lid >= d) t = td_compose(o, t);
-            }
+            t = td_scan(t);   // ordered inclusive scan: P_j = T_c o ... o T_{c+j}
             const uint32_t D = p ? t.d1 : t.d0;
             const bool ok = (t.f & 4u) && cc < nch && cc / RT_SUP == c / RT_SUP &&   // stop at the super boundary
                             (double)A + (double)D * (double)u < top;
             const uint64_t okm = __ballot(ok);
             const int f = okm == ~0ull ? 64 : (int)__builtin_ctzll(~okm);   // leading run of valid lanes
-            const uint32_t Dprev = (uint32_t)__shfl_up((int)D, 1, 64);
+            const uint32_t Dprev = wg_wave_shr1(D, 0u);
             if (lid < f) {
                 const uint32_t dp = lid == 0 ? 0u : Dprev;
                 ch[cc].start = A + (float)dp * u;
@@ -541,7 +499,7 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
                 ch[cc].mode = MODE_TABLE;
             }
             if (f > 0) {
-                const uint32_t Dl = (uint32_t)__shfl((int)D, f - 1, 64);
+                const uint32_t Dl = wg_lane(D, (uint32_t)f - 1);
                 A = A + (float)Dl * u;
                 c += f;
             }
@@ -578,11 +536,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, uint64_t c_lo, con
         float s[RT_Q], t = 0.0f;
 #pragma unroll
         for (int q = 0; q < RT_Q; q++) { s[q] = (r0 + q < n) ? step_of(h, band, r0 + q) : 0.0f; t += s[q]; }
-        float inc = t;
-        for (int d = 1; d < 64; d <<= 1) {
-            const float o = __shfl_up(inc, d, 64);
-            if (lid >= d) inc += o;
-        }
+        const float inc = wg_wave_scan(t, 0.0f, [](float a, float b) { return a + b; });   // exact integers
         __shared__ float wsum[RT_T / 64];
         if (lid == 63) wsum[w] = inc;
         __syncthreads();
@@ -607,15 +561,10 @@ __global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, uint64_t c_lo, con
         t = td_compose(t, tr[q]);
     }
     // ordered block exclusive scan
-    Td inc = t;
-    for (int d = 1; d < 64; d <<= 1) {
-        Td o = td_shfl_up(inc, d);
-        if (lid >= d) inc = td_compose(o, inc);
-    }
+    const Td inc = td_scan(t);
     __shared__ Td wt[RT_T / 64];
     if (lid == 63) wt[w] = inc;
-    Td ex = td_shfl_up(inc, 1);
-    if (lid == 0) ex = td_identity();
+    Td ex = wg_wave_shr1(inc, td_identity());
     __syncthreads();
     Td wp = td_identity();
     for (int k2 = 0; k2 < w; k2++) wp = td_compose(wp, wt[k2]);
