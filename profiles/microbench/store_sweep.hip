@@ -18,7 +18,7 @@
 typedef float v4f __attribute__((ext_vector_type(4)));
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
-enum { MAP_DISPATCH = 0, MAP_XCD = 1, MAP_PERSIST_STRIDE = 2, MAP_PERSIST_CONTIG = 3 };
+enum { MAP_DISPATCH = 0, MAP_XCD = 1, MAP_PERSIST_STRIDE = 2, MAP_PERSIST_CONTIG = 3, MAP_XCD_STAGGER = 4 };
 
 template <bool NT, int R, int TH>
 __device__ __forceinline__ void write_tile(v4f *out, size_t n, size_t t) {
@@ -43,6 +43,12 @@ __global__ void __launch_bounds__(TH) k_tiles(v4f *out, size_t n, size_t ntiles)
         const size_t per = (ntiles + 7) / 8;
         const size_t t = (b % 8) * per + b / 8;
         if (t < ntiles) write_tile<NT, R, TH>(out, n, t);
+    } else if (MAP == MAP_XCD_STAGGER) {
+        // as MAP_XCD, but XCD x starts its eighth x/8 of the way in (and wraps):
+        // the eight write streams sit at different phases of their regions
+        const size_t per = (ntiles + 7) / 8, x = b % 8;
+        const size_t t = x * per + (b / 8 + x * per / 8) % per;
+        if (b / 8 < per && t < ntiles) write_tile<NT, R, TH>(out, n, t);
     } else if (MAP == MAP_PERSIST_STRIDE) {
         for (size_t t = b; t < ntiles; t += g) write_tile<NT, R, TH>(out, n, t);
     } else {
@@ -83,12 +89,13 @@ int main(int argc, char **argv) {
     {                                                                                                          \
         const size_t nt_ = (n + (size_t)TH * R - 1) / ((size_t)TH * R);                                        \
         size_t grid_ = (GRID) ? (size_t)(GRID) : nt_;                                                          \
-        if (MAP == MAP_XCD) grid_ = ((nt_ + 7) / 8) * 8;                                                       \
+        if (MAP == MAP_XCD || MAP == MAP_XCD_STAGGER) grid_ = ((nt_ + 7) / 8) * 8;                                                       \
         run(NAME, [&] { hipLaunchKernelGGL((k_tiles<NT, R, TH, MAP>), dim3((unsigned)grid_), dim3(TH), 0, 0, out, n, nt_); }); \
     }
     V(true, 6, 256, MAP_DISPATCH, 0, "24KiB/256 nt dispatch");
     V(false, 6, 256, MAP_DISPATCH, 0, "24KiB/256 plain dispatch");
     V(true, 6, 256, MAP_XCD, 0, "24KiB/256 nt xcd-split");
+    V(true, 6, 256, MAP_XCD_STAGGER, 0, "24KiB/256 nt xcd-stagger");
     V(false, 6, 256, MAP_XCD, 0, "24KiB/256 plain xcd-split");
     V(true, 3, 256, MAP_XCD, 0, "12KiB/256 nt xcd-split");
     V(true, 3, 256, MAP_DISPATCH, 0, "12KiB/256 nt dispatch");
