@@ -13,7 +13,7 @@
 // HBM-write-bound: 24 B per vertex out, a few bytes of geometry in.  A
 // workgroup owns a fixed tile of 1024 vertices (24 KiB out):
 //   1. one round of independent global loads, all addressed from a per-tile
-//      record (k_tile_info): the rows overlapping the tile, its vertical
+//      record (k_vtx_prep): the rows overlapping the tile, its vertical
 //      entries (one contiguous range of vert[]) and its curve segments (one
 //      contiguous range of curve[]); pair -> row by a prefix-max of row starts
 //      (every primitive has an even vertex count, so vertex PAIRS never
@@ -51,45 +51,53 @@ constexpr int MAXV = TILE / WG_VTX_PER_VERTICAL + 2;      // vertical entries ov
 __constant__ float c_cos[25] = WG_UNIT_CIRCLE_COS_INIT;
 __constant__ float c_sin[25] = WG_UNIT_CIRCLE_SIN_INIT;
 
-__global__ void k_vtx_counts(uint64_t rb, uint64_t re, int64_t sel, const uint32_t *__restrict__ voff,
-                             const uint32_t *__restrict__ coff, uint64_t *__restrict__ cnt) {
-    uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= re) return;
-    uint64_t v = (uint64_t)WG_VTX_PER_VERTICAL * (voff[r + 1] - voff[r]) +
-                 (uint64_t)WG_VTX_PER_CURVE * (coff[r + 1] - coff[r]) + WG_VTX_PER_NODE;
-    if (sel >= 0 && (uint64_t)sel == r) v += WG_VTX_PER_RING;
-    cnt[r - rb] = v;
+// Vertex offset of row j of [rb, re) in closed form: a row's vertex count is
+// 6 per vertical entry, 96 per curve segment, 72 for the node and 144 more on
+// the selected row, and vert_off / curve_off are prefix sums already — no
+// count pass and no scan.
+__device__ __forceinline__ uint64_t vtx_at(uint64_t rb, uint64_t j, int64_t sel, const uint32_t *__restrict__ voff,
+                                           const uint32_t *__restrict__ coff, uint32_t v0, uint32_t c0) {
+    const uint64_t r = rb + j;
+    uint64_t v = (uint64_t)WG_VTX_PER_VERTICAL * (voff[r] - v0) + (uint64_t)WG_VTX_PER_CURVE * (coff[r] - c0) +
+                 (uint64_t)WG_VTX_PER_NODE * j;
+    if (sel >= 0 && (uint64_t)sel >= rb && (uint64_t)sel < r) v += WG_VTX_PER_RING;
+    return v;
 }
 
-// Per-tile record, written by the row whose vertex range contains the tile
-// start: {first row, first vertical entry A, first curve K0, straddle bits}.
-// A tile's verticals are vert[A(t) .. A(t+1) + sV(t+1)) and its curves
-// curve[K0(t) .. K0(t+1) + sC(t+1)), because every row's entries are
-// contiguous and rows are consecutive; a sentinel record closes the range.
-// tcap: tile records the buffer holds (the launch may precede the host's
-// knowledge of the total; a list that does not fit writes nothing)
-__global__ void k_tile_info(uint64_t rb, uint64_t rows, const uint64_t *__restrict__ vtx_off,
-                            const uint32_t *__restrict__ voff, const uint32_t *__restrict__ coff,
-                            uint64_t tcap, uint4 *__restrict__ info) {
+// vtx_off[0..rows] and the per-tile records, written by the row whose vertex
+// range contains the tile start: {first row, first vertical entry A, first
+// curve K0, straddle bits}.  A tile's verticals are vert[A(t) .. A(t+1) +
+// sV(t+1)) and its curves curve[K0(t) .. K0(t+1) + sC(t+1)), because every
+// row's entries are contiguous and rows are consecutive; a sentinel record
+// closes the range.  tcap: tile records the buffer holds (the launch may
+// precede the host's knowledge of the total; a list that does not fit writes
+// no records).
+__global__ void k_vtx_prep(uint64_t rb, uint64_t rows, int64_t sel, const uint32_t *__restrict__ voff,
+                           const uint32_t *__restrict__ coff, uint64_t *__restrict__ vtx_off, uint64_t tcap,
+                           uint4 *__restrict__ info) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= rows) return;
-    const uint64_t ntiles = (vtx_off[rows] + TILE - 1) / TILE;
+    if (j > rows) return;
+    const uint32_t v0 = voff[rb], c0 = coff[rb];
+    const uint64_t s = vtx_at(rb, j, sel, voff, coff, v0, c0);
+    vtx_off[j] = s;
+    if (j == rows) return;
+    const uint64_t e = vtx_at(rb, j + 1, sel, voff, coff, v0, c0);
+    const uint64_t ntiles = (vtx_at(rb, rows, sel, voff, coff, v0, c0) + TILE - 1) / TILE;
     if (ntiles + 1 > tcap) return;
     const uint64_t r = rb + j;
-    const uint64_t s = vtx_off[j], e = vtx_off[j + 1];
     const uint32_t vo = voff[r], nv = voff[r + 1] - vo, co = coff[r], nc = coff[r + 1] - co;
     const uint64_t cv = s + (uint64_t)WG_VTX_PER_VERTICAL * nv;
     for (uint64_t t = (s + TILE - 1) / TILE; t * TILE < e; t++) {
-        const uint64_t v0 = t * TILE;
+        const uint64_t vt = t * TILE;
         uint32_t A, K0, fl = 0;
-        if (v0 < cv) {
-            const uint64_t d = v0 - s;
+        if (vt < cv) {
+            const uint64_t d = vt - s;
             A = vo + (uint32_t)(d / WG_VTX_PER_VERTICAL);
             fl |= (d % WG_VTX_PER_VERTICAL) ? 1u : 0u;
             K0 = co;
         } else {
             A = vo + nv;
-            const uint64_t d = v0 - cv;
+            const uint64_t d = vt - cv;
             if (d < (uint64_t)WG_VTX_PER_CURVE * nc) {
                 K0 = co + (uint32_t)(d / WG_VTX_PER_CURVE);
                 fl |= (d % WG_VTX_PER_CURVE) ? 2u : 0u;
@@ -416,9 +424,15 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     }
     wg_stage_begin(c, "vtx_counts");
     uint64_t *off = c->vtx_off.as<uint64_t>();
-    hipLaunchKernelGGL(k_vtx_counts, dim3((rows + 255) / 256), dim3(256), 0, s, rb, re, sel,
-                       c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off);
-    WG_HIP(c, wg_exclusive_scan_u64(off, off, rows, c->scan_tmp.p, s));
+    auto prep = [&](uint64_t tcap) {   // vtx_off + tile records (none when tcap is too small)
+        hipLaunchKernelGGL(k_vtx_prep, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
+                           c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
+                           c->tile_first.as<uint4>());
+    };
+    const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;
+    const uint64_t tcap = c->tile_first.cap / sizeof(uint4);
+    const bool early = vcap > 0 && tcap > 1;
+    prep(early ? tcap : 0);
     float q = roundf(c->graph_width / WG_LANE_W);
     uint32_t vis = q <= 0.0f ? 0u : (uint32_t)q;
     if (vis < 1) vis = 1;
@@ -431,10 +445,7 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const uint8_t *match = c->match_on ? c->match_flags.as<const uint8_t>() : nullptr;
     const int64_t mlo = (int64_t)c->match_rb - (int64_t)c->sh.s + (int64_t)c->sh.row_base;
     const int64_t mhi = mlo + (int64_t)(c->match_re - c->match_rb);
-    auto launch = [&](uint64_t vcap, uint64_t tcap, uint64_t grid) {
-        hipLaunchKernelGGL(k_tile_info, dim3((rows + 255) / 256), dim3(256), 0, s, rb, rows, (const uint64_t *)off,
-                           c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), tcap,
-                           c->tile_first.as<uint4>());
+    auto launch = [&](uint64_t vcap, uint64_t grid) {
         wg_stage_end(c);
         wg_stage_begin(c, "vtx_emit");
         // (grid rounded up to whole XCD rounds: k_vtx_tile's tile order)
@@ -446,10 +457,7 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
                            c->vtx.as<float4>(), grid);
         wg_stage_end(c);
     };
-    const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;
-    const uint64_t tcap = c->tile_first.cap / sizeof(uint4);
-    const bool early = vcap > 0 && tcap > 1;
-    if (early) launch(vcap, tcap, std::min((vcap + TILE - 1) / TILE, tcap - 1));
+    if (early) launch(vcap, std::min((vcap + TILE - 1) / TILE, tcap - 1));
     uint64_t total = 0;
     if (const int rc = wg_fetch_end(c, &total)) return rc;
     c->n_vtx = total;
@@ -458,7 +466,8 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         if (early) wg_stage_begin(c, "vtx_counts");
         WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
         WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
-        launch(total, ntiles + 1, ntiles);
+        prep(ntiles + 1);
+        launch(total, ntiles);
     }
     WG_HIP(c, hipGetLastError());
     return WG_OK;
