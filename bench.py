@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (host-input rate, glyph quads, font atlas)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (host rehearsal)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--device-transport", action="store_true",
+                    help="gloo rehearsal: move HIP-resident slots through gloo (the stream-ordered slot path of RCCL)")
     ap.add_argument("--all-stage-events", action="store_true",
                     help="record every stage's HIP events inside the timed region (default: only the emission "
                          "kernel's, for the roofline; the stage breakdown comes from a separate pass)")
@@ -365,7 +367,7 @@ def main():
     comm = None
     if world > 1:
         from wgraph.shard import ShardComm
-        comm = ShardComm(dev)
+        comm = ShardComm(dev, device_transport=True if args.device_transport else None)
 
     def step():
         if comm is None:
