@@ -260,7 +260,10 @@ int wg_device_views_get(wg_ctx *ctx, wg_device_views *out);
  * whole on every rank instead, with the same results.                     */
 typedef struct wg_shard_msg {
     const void *send;         /* engine-owned device buffer (diagnostic)      */
-    uint64_t    bytes;        /* length of this rank's message                */
+    uint64_t    bytes;        /* length of this rank's message, or
+                                 WG_SHARD_BYTES_ON_DEVICE: written by the
+                                 engine's kernels (wg_shard_msg_bytes reads it;
+                                 wg_shard_pack_slot needs no host copy)        */
     int32_t     done;         /* 1: the call is complete, nothing to exchange */
     int32_t     step;         /* exchange index                               */
 } wg_shard_msg;
@@ -269,8 +272,14 @@ int wg_shard_build_begin(wg_ctx *ctx, const wg_commits *commits, int world, int 
                          uint64_t row_begin, uint64_t row_end, wg_shard_msg *out);
 /* row_geometry_with_bands (:367-399) of the shard; band = the whole [N] array. */
 int wg_shard_geometry_begin(wg_ctx *ctx, const float *band, int32_t band_residency, wg_shard_msg *out);
+#define WG_SHARD_BYTES_ON_DEVICE UINT64_MAX
 /* Copy this rank's current message (device or host destination). */
 int wg_shard_copy_msg(wg_ctx *ctx, void *dst);
+/* Exact length of this rank's current message (synchronises the engine's
+ * stream when the length is still on the device).  Host transports, which
+ * write the slot header themselves, call it when wg_shard_msg.bytes is
+ * WG_SHARD_BYTES_ON_DEVICE. */
+int wg_shard_msg_bytes(wg_ctx *ctx, uint64_t *out);
 /* Write this rank's transport slot into device memory, queued on the
  * engine's stream without a host synchronisation: a 16-byte header (message
  * length as u64, then zeros), then the message when it fits in `cap` bytes

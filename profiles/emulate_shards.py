@@ -96,19 +96,34 @@ def main():
             self.held = False
             gpu.release()
 
+        caps: dict = {}
+
         def allgather(self, nbytes, fill, step=0, pack=None, read_heads=None):
             # (read_heads: the heads come from the host copy below, as with a gloo transport)
-            cap = ShardComm.round_cap(nbytes)
             with torch.cuda.stream(self.stream):
                 if pack is not None:
+                    # the slot header carries the length (set on the device when
+                    # the engine left it there): read after the timed segment,
+                    # repacked with a larger slot if the message did not fit
+                    cap = self.caps.get(step, 4096)
                     slot = torch.empty(cap + ShardComm.HDR, dtype=torch.uint8, device=dev)
                     pack(slot.data_ptr(), cap)
-                    send = slot[ShardComm.HDR:]
                 else:
+                    cap = ShardComm.round_cap(nbytes)
                     send = torch.zeros(cap, dtype=torch.uint8, device=dev)
                     if nbytes:
                         fill(send.data_ptr())
             self.stop()
+            if pack is not None:
+                with torch.cuda.stream(self.stream):
+                    nbytes = int(slot[:8].cpu().view(torch.int64).item())
+                    if nbytes > cap:
+                        cap = ShardComm.round_cap(nbytes)
+                        slot = torch.empty(cap + ShardComm.HDR, dtype=torch.uint8, device=dev)
+                        pack(slot.data_ptr(), cap)
+                    self.stream.synchronize()
+                self.caps[step] = cap
+                send = slot[ShardComm.HDR:]
             slots[self.rank] = (send, nbytes)
             bar.wait()
             stride = ShardComm.round_cap(max(s[1] for s in slots)) + ShardComm.HDR

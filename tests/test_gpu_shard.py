@@ -88,10 +88,18 @@ def _lockstep(engines, begin):
     msgs = [abi.ShardMsg() for _ in range(W)]
     for r, e in enumerate(engines):
         e._check(begin(e, r, ctypes.byref(msgs[r])))
+    def msg_bytes(e, m):   # a length the engine left on the device (WG_SHARD_BYTES_ON_DEVICE) is read back
+        if int(m.bytes) != abi.WG_SHARD_BYTES_ON_DEVICE:
+            return int(m.bytes)
+        n = ctypes.c_uint64(0)
+        e._check(lib().wg_shard_msg_bytes(e._ctx, ctypes.byref(n)))
+        return int(n.value)
+
     rounds = 0
     while not msgs[0].done:
         assert all(not m.done for m in msgs) and len({int(m.step) for m in msgs}) == 1
-        cap = ShardComm.round_cap(max(int(m.bytes) for m in msgs))
+        sizes = [msg_bytes(e, m) for e, m in zip(engines, msgs)]
+        cap = ShardComm.round_cap(max(sizes))
         stride = cap + ShardComm.HDR
         slots = torch.empty(W * stride, dtype=torch.uint8, device="cuda")
         if rounds == 0:   # size contract: caps / strides that are not 16k bytes (k >= 1) are refused
@@ -104,7 +112,6 @@ def _lockstep(engines, begin):
         for r, e in enumerate(engines):
             e._check(lib().wg_shard_pack_slot(e._ctx, slots.data_ptr() + r * stride, cap))
         head = slots.view(W, stride)[:, :32].cpu().numpy()
-        sizes = [int(m.bytes) for m in msgs]
         assert [int(x) for x in head[:, :8].copy().view(np.int64).reshape(-1)] == sizes
         assert not head[:, 8:16].any()
         heads = np.ascontiguousarray(head[:, 16:32]).view(np.uint32).reshape(W, 4)

@@ -124,7 +124,9 @@ struct ShardState {
     DevBuf msg;               // this rank's outgoing message
     const uint32_t *heads = nullptr;   // host copy of the gathered 16-byte headers (one exchange call)
     const uint64_t *sizes = nullptr;   // every rank's message length (one exchange call)
-    uint64_t msg_bytes = 0;
+    uint64_t msg_bytes = 0;   // exact length, or (msg_dev) the buffer's capacity
+    bool msg_dev = false;     // the length is on the device (msg_len), written by the producing kernels
+    DevBuf msg_len;           // u64: device-resident message length
     DevBuf ptable;            // id partition table (global duplicate check)
     DevBuf prow;              // int32 [E1-E0] parent rows of own references
     DevBuf unres;             // unresolved-reference records of every rank (32 B each)

@@ -410,6 +410,29 @@ __global__ void k_sh_edges_own(LocalEdgeArgs A) {
 
 // a message's 16-byte header (kernel arguments: no host buffer outlives the call)
 __global__ void k_sh_put_head(uint4 *__restrict__ dst, uint4 v) { *dst = v; }
+// X1 header from the device: {violation | duplicate, unresolved references,
+// E0 = parent_off[s], E1 = parent_off[e]} and the message length
+__global__ void k_sh_x1_head(uint4 *__restrict__ dst, unsigned long long *__restrict__ len, const uint32_t *__restrict__ flags,
+                             const uint32_t *__restrict__ ucnt_off, uint64_t nl, const uint32_t *__restrict__ poff,
+                             uint64_t s, uint64_t e) {
+    const uint32_t nu = ucnt_off[nl];
+    *dst = make_uint4(flags[0] | flags[1], nu, poff[s], poff[e]);
+    *len = 16ull + (unsigned long long)nu * 32ull;
+}
+// transport slot of a message whose length is on the device: header, then the
+// payload when it fits (its first 16 bytes zero otherwise); 16-byte moves
+__global__ void __launch_bounds__(256) k_sh_pack_dev(uint4 *__restrict__ slot, uint64_t cap, const uint4 *__restrict__ msg,
+                                                     const unsigned long long *__restrict__ len) {
+    const uint64_t b = *len;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, ts = (uint64_t)gridDim.x * blockDim.x;
+    if (t == 0) slot[0] = make_uint4((uint32_t)b, (uint32_t)(b >> 32), 0u, 0u);
+    if (b > cap) {
+        if (t == 0) slot[1] = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
+    for (uint64_t i = t; i < (b + 15) / 16; i += ts) slot[1 + i] = msg[i];
+    if (b == 0 && t == 0) slot[1] = make_uint4(0u, 0u, 0u, 0u);
+}
 // transport slot: 16-byte length header, then the payload's first 16 bytes zeroed (overwritten by the payload copy)
 __global__ void k_sh_slot_head(uint4 *__restrict__ dst, uint4 v) {
     dst[0] = v;
@@ -438,8 +461,22 @@ enum { SH_IDLE = 0, SH_X1, SH_X2, SH_X3, SH_X6 = 6 };
 static int sh_send(wg_ctx *c, uint64_t bytes, wg_shard_msg *out) {
     WG_ALLOC(c, c->sh.msg, bytes + 64);
     c->sh.msg_bytes = bytes;
+    c->sh.msg_dev = false;
     out->send = c->sh.msg.p;
     out->bytes = bytes;
+    out->done = 0;
+    out->step = c->sh.step;
+    return WG_OK;
+}
+// a message whose length the producing kernels write to msg_len: `cap_bytes`
+// bounds it (the buffer's size); the host learns the length from the heads
+static int sh_send_dev(wg_ctx *c, uint64_t cap_bytes, wg_shard_msg *out) {
+    WG_ALLOC(c, c->sh.msg, cap_bytes + 64);
+    WG_ALLOC(c, c->sh.msg_len, 16);
+    c->sh.msg_bytes = cap_bytes;
+    c->sh.msg_dev = true;
+    out->send = c->sh.msg.p;
+    out->bytes = WG_SHARD_BYTES_ON_DEVICE;
     out->done = 0;
     out->step = c->sh.step;
     return WG_OK;
@@ -468,17 +505,17 @@ static int read_headers(wg_ctx *c, const void *gathered, uint64_t stride, std::v
     hdr.assign((size_t)W * 4, 0);
     if (c->sh.heads) {
         for (int r = 0; r < W; r++)
-            for (int k = 0; k < 3; k++) hdr[4 * r + k] = c->sh.heads[4 * r + k];
+            for (int k = 0; k < 4; k++) hdr[4 * r + k] = c->sh.heads[4 * r + k];
         return WG_OK;
     }
     WgFetch it[64];
     for (int r = 0; r < W; r++)
-        for (int k = 0; k < 3; k++) it[3 * r + k] = WgFetch{(const uint8_t *)gathered + r * stride + 4 * k, false};
+        for (int k = 0; k < 4; k++) it[4 * r + k] = WgFetch{(const uint8_t *)gathered + r * stride + 4 * k, false};
     uint64_t v[64];
-    const int rc = wg_fetch_n(c, 3 * W, it, v);
+    const int rc = wg_fetch_n(c, 4 * W, it, v);
     if (rc != WG_OK) return rc;
     for (int r = 0; r < W; r++)
-        for (int k = 0; k < 3; k++) hdr[4 * r + k] = (uint32_t)v[3 * r + k];
+        for (int k = 0; k < 4; k++) hdr[4 * r + k] = (uint32_t)v[4 * r + k];
     return WG_OK;
 }
 
@@ -772,24 +809,17 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
                                c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>(),
                                S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
     WG_HIP(c, wg_exclusive_scan_u32(S.xcnt.as<uint32_t>(), S.xcnt.as<uint32_t>(), nl, c->scan_tmp.p, st));
-    uint64_t h[5] = {0, 0, 0, 0, 0};
-    {
-        const int frc = wg_fetch(c, {{S.flags.as<uint32_t>(), false}, {S.flags.as<uint32_t>() + 1, false},
-                                     {S.xcnt.as<uint32_t>() + nl, false}, {c->d_poff + row_begin, false},
-                                     {c->d_poff + row_end, false}}, h);
-        if (frc != WG_OK) return frc;
-    }
-    S.E0 = h[3];
-    S.E1 = h[4];
-    c->e_refs_own = S.E1 - S.E0;
     c->hcap = cap;
-    S.n_unres = h[2];
     S.step = SH_X1;
-    // X1: {violation | duplicate, n} + one 32-byte record per unresolved reference, row order
-    rc = sh_send(c, 16 + (uint64_t)h[2] * 32, out);
+    // X1: {violation | duplicate, n, E0, E1} + one 32-byte record per unresolved
+    // reference, row order.  Nothing is read back here: the header and the
+    // length are written on the device, bounded by the list's references, and
+    // this rank learns its own counts from the gathered heads (X1 exchange).
+    rc = sh_send_dev(c, 16 + El * 32, out);
     if (rc != WG_OK) return rc;
-    uint32_t hdr[4] = {(uint32_t)(h[0] | h[1]), (uint32_t)h[2], 0, 0};
-    hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), make_uint4(hdr[0], hdr[1], hdr[2], hdr[3]));
+    hipLaunchKernelGGL(k_sh_x1_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), S.msg_len.as<unsigned long long>(),
+                       (const uint32_t *)S.flags.as<uint32_t>(), (const uint32_t *)S.xcnt.as<uint32_t>(), nl, c->d_poff,
+                       row_begin, row_end);
     if (nl) hipLaunchKernelGGL(k_sh_pack_unres, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid,
                                S.prow.as<const int32_t>(), S.xcnt.as<const uint32_t>(),
                                reinterpret_cast<uint32_t *>(S.msg.as<uint8_t>() + 16));
@@ -798,9 +828,23 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     return WG_OK;
 }
 
+int wg_shard_msg_bytes(wg_ctx *c, uint64_t *out) {
+    if (!c || !out) return WG_E_INVALID;
+    if (!c->sh.msg_dev) { *out = c->sh.msg_bytes; return WG_OK; }
+    (void)hipSetDevice(c->device);
+    uint64_t b = 0;
+    if (const int rc = wg_fetch(c, {{c->sh.msg_len.p, true}}, &b)) return rc;
+    if (b > c->sh.msg_bytes) return wg_fail(c, WG_E_INVALID, "message length %llu beyond its buffer", (unsigned long long)b);
+    *out = b;
+    return WG_OK;
+}
+
 int wg_shard_copy_msg(wg_ctx *c, void *dst) {
-    if (!c || (!dst && c->sh.msg_bytes)) return WG_E_INVALID;
-    if (c->sh.msg_bytes) WG_HIP(c, hipMemcpyAsync(dst, c->sh.msg.p, c->sh.msg_bytes, hipMemcpyDefault, c->stream));
+    if (!c) return WG_E_INVALID;
+    uint64_t b = 0;
+    if (const int rc = wg_shard_msg_bytes(c, &b)) return rc;
+    if (!dst && b) return WG_E_INVALID;
+    if (b) WG_HIP(c, hipMemcpyAsync(dst, c->sh.msg.p, b, hipMemcpyDefault, c->stream));
     WG_HIP(c, hipStreamSynchronize(c->stream));
     return WG_OK;
 }
@@ -811,6 +855,14 @@ int wg_shard_pack_slot(wg_ctx *c, void *slot, uint64_t cap) {
     if (!c || !slot || (reinterpret_cast<uintptr_t>(slot) & 15u) || cap < 16 || (cap & 15u)) return WG_E_INVALID;
     if (!c->sh.on || c->sh.step == SH_IDLE) return wg_fail(c, WG_E_STATE, "no sharded call in progress");
     (void)hipSetDevice(c->device);
+    if (c->sh.msg_dev) {   // length on the device: one kernel writes the header and copies what fits
+        const uint64_t nvec = std::min(cap, c->sh.msg_bytes + 15) / 16 + 1;
+        const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((nvec + 255) / 256, 1024));
+        hipLaunchKernelGGL(k_sh_pack_dev, dim3((uint32_t)g), dim3(256), 0, c->stream, static_cast<uint4 *>(slot), cap,
+                           c->sh.msg.as<const uint4>(), c->sh.msg_len.as<const unsigned long long>());
+        WG_HIP(c, hipGetLastError());
+        return WG_OK;
+    }
     const uint64_t b = c->sh.msg_bytes;
     hipLaunchKernelGGL(k_sh_slot_head, dim3(1), dim3(1), 0, c->stream, static_cast<uint4 *>(slot),
                        make_uint4((uint32_t)b, (uint32_t)(b >> 32), 0u, 0u));
@@ -857,6 +909,15 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
     case SH_X1: {   // everyone's unresolved references -> rows this shard owns
         std::vector<uint32_t> hdr;
         if ((rc = read_headers(c, gathered, stride, hdr)) != WG_OK) return rc;
+        // this rank's own reference range and unresolved count came back in its header
+        S.E0 = hdr[4 * S.rank + 2];
+        S.E1 = hdr[4 * S.rank + 3];
+        S.n_unres = hdr[4 * S.rank + 1];
+        if (S.E1 < S.E0 || S.E1 > S.Etot)
+            return wg_fail(c, WG_E_INVALID, "X1 header of rank %d: references [%llu, %llu) of %llu (%u %u %u %u / %u %u %u %u)",
+                           S.rank, (unsigned long long)S.E0, (unsigned long long)S.E1, (unsigned long long)S.Etot,
+                           hdr[0], hdr[1], hdr[2], hdr[3], hdr[4], hdr[5], hdr[6], hdr[7]);
+        c->e_refs_own = S.E1 - S.E0;
         S.uoffs.assign(W + 1, 0);
         bool bad = false;
         for (int r = 0; r < W; r++) {

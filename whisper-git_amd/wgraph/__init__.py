@@ -89,6 +89,7 @@ def lib():
             "wg_shard_copy_msg": ([vp, vp], ctypes.c_int),
             "wg_shard_pack_slot": ([vp, vp, u64], ctypes.c_int),
             "wg_shard_slot_heads": ([vp, vp, u64, ctypes.c_int, vp], ctypes.c_int),
+            "wg_shard_msg_bytes": ([vp, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
             "wg_match_rows": ([vp, vp, u64, u64, u64, ctypes.POINTER(abi.RowText), ctypes.POINTER(ctypes.c_uint64)],
                               ctypes.c_int),
             "wg_copy_match_flags": ([vp, vp], ctypes.c_int),
@@ -113,7 +114,7 @@ EXPORTED_SYMBOLS = (
     "wg_compute_row_heights",    "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
-    "wg_shard_copy_msg", "wg_shard_pack_slot", "wg_shard_slot_heads", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
+    "wg_shard_copy_msg", "wg_shard_msg_bytes", "wg_shard_pack_slot", "wg_shard_slot_heads", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
     "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets",
     "wg_match_rows", "wg_copy_match_flags", "wg_lower_utf8", "wg_order_rows", "wg_render", "wg_write_png")
 
@@ -232,8 +233,16 @@ class Engine:
                         self._check(lib().wg_shard_slot_heads(self._ctx, ptr, stride, comm.world, h.ctypes.data))
                         return h.reshape(comm.world, 3)
         while not msg.done:
+            nbytes = int(msg.bytes)
+            if nbytes == abi.WG_SHARD_BYTES_ON_DEVICE:
+                if pack is not None:
+                    nbytes = 0   # the slot is written on the device, length included
+                else:            # a host transport writes the slot header itself: it needs the length
+                    n = ctypes.c_uint64(0)
+                    self._check(lib().wg_shard_msg_bytes(self._ctx, ctypes.byref(n)))
+                    nbytes = int(n.value)
             gathered, off, stride, sizes = comm.allgather(
-                int(msg.bytes), lambda dst: self._check(lib().wg_shard_copy_msg(self._ctx, dst)), step=int(msg.step),
+                nbytes, lambda dst: self._check(lib().wg_shard_copy_msg(self._ctx, dst)), step=int(msg.step),
                 pack=pack, read_heads=read_heads)
             self._gathered = gathered
             sz = (ctypes.c_uint64 * len(sizes))(*sizes)

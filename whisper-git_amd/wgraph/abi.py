@@ -101,6 +101,9 @@ class RenderParams(ctypes.Structure):
                 ("clear", ctypes.c_float * 4), ("layers", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
+WG_SHARD_BYTES_ON_DEVICE = 2 ** 64 - 1   # wg_shard_msg.bytes: the length is written by the engine's kernels
+
+
 class ShardMsg(ctypes.Structure):
     _fields_ = [("send", ctypes.c_void_p), ("bytes", ctypes.c_uint64), ("done", ctypes.c_int32),
                 ("step", ctypes.c_int32)]
