@@ -33,10 +33,12 @@ def main():
     c.n_commits, c.n_parents = dag.n, dag.e
     c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
     c.residency = abi.WG_DEVICE
-    eng = wgraph.Engine(0)
-    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     ref = None
     for ch in [int(x) for x in args.chunks.split(",")]:
+        # a fresh engine per chunk size: the replay's blind iteration count
+        # adapts per context and must not carry over from another chunk size
+        eng = wgraph.Engine(0)
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         eng._check(lib().wg_set_option(eng._ctx, 2, ch))
 
         def step():
@@ -63,6 +65,7 @@ def main():
         print(json.dumps({"chunk": ch, "step_ms": round(ms, 4), "lf_loop_ms": round(st.get("lf_loop", 0), 4),
                           "lanes_ms": round(st.get("lanes", 0), 4), "same_lanes": same,
                           "debug": [int(x) for x in dbg[:8]]}), flush=True)
+        eng.close()
 
 
 if __name__ == "__main__":

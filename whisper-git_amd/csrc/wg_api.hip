@@ -451,13 +451,13 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
     if (spec) {
         WgFetch it[20];
-        int k = wg_lanes_spec_items(c, it);
-        k += wg_geom_spec_items(c, it + k);
+        const int kl = wg_lanes_spec_items(c, it);
+        int k = kl + wg_geom_spec_items(c, it + kl);
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + n, false};
         uint64_t v[20] = {0};
         if ((rc = wg_fetch_n(c, k, it, v)) != WG_OK) return rc;
         c->spec = false;
-        const uint64_t ne = v[16];
+        const uint64_t ne = v[k - 1];
         const bool lanes_ok = wg_lanes_spec_check(c, v);
         if (!lanes_ok) {   // the exact lane stage (fast path with its reads, or the general walk)
             if ((rc = wg_stage_lanes(c, false)) != WG_OK) return rc;
@@ -471,7 +471,7 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
         }
         c->spec_builds++;
         c->spec_redo_lanes += !lanes_ok;
-        if (!lanes_ok || !wg_geom_spec_check(c, v + 8)) {
+        if (!lanes_ok || !wg_geom_spec_check(c, v + kl)) {
             c->spec_redo_geom++;
             c->lists_gen = ~0ull;
             if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;

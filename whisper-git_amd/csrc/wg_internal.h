@@ -217,6 +217,15 @@ struct wg_ctx {
     uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
+    // After a replay that reached its fixed point at iteration fp (the first that
+    // changed nothing), the next build's blind count: up at once, down by half
+    // the excess per build (it used to fall by one per build: after a list that
+    // needed hundreds of iterations, later builds launched hundreds of empty ones).
+    void replay_adapt(uint32_t fp) {
+        if (fp == 0) return;
+        replay_blind = fp >= replay_blind ? fp : (fp > (replay_blind + fp) / 2 ? fp : (replay_blind + fp) / 2);
+        if (replay_blind < 2) replay_blind = 2;
+    }
     uint64_t n_events = 0;  // events of the last fast-path lane build
     uint64_t e_refs_own = 0;   // parent references of the rows this context owns
     bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])

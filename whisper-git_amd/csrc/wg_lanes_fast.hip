@@ -574,14 +574,14 @@ int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *e
     WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind));
     const uint32_t blind = run.it;
     const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
-    uint64_t sc[5] = {0, 0, 0, 1, 1};
+    uint64_t sc[6] = {0, 0, 0, 1, 1, 0};
     bool conv = nev == 0;
     for (int pass = 0; pass < 2; pass++) {
         if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
         WG_HIP(c, hipGetLastError());
         if (nev && !conv) {
             int rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}, {run.flags + run.it - 1, false},
-                                  {run.flags + run.it, false}}, sc);
+                                  {run.flags + run.it, false}, {ls + 3, false}}, sc);
             if (rc != WG_OK) return rc;
             conv = sc[3] == 0 || sc[4] == 0;
         } else {
@@ -594,10 +594,11 @@ int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *e
     }
     wg_stage_end(c);
     c->replay_iters = run.it;
-    // next build: as many blind iterations as this one needed (one fewer if the
-    // fixed point came a launch early)
-    if (run.it > blind) c->replay_blind = run.it;
-    else if (sc[3] == 0 && c->replay_blind > 2) c->replay_blind--;
+    // next build: the iterations this one needed — up to the first iteration
+    // that changed nothing (k_lf_replay_finish) — at once if more, halving the
+    // excess if fewer (a list that needed many must not hold later ones for long)
+    if (sc[5] >= 1) c->replay_adapt((uint32_t)sc[5]);
+    else if (run.it > blind) c->replay_blind = run.it;
     if (!conv || sc[2]) return WG_OK;               // no fixed point / more than 63 slots
     c->max_lane = (uint32_t)sc[0];
     c->n_slots = (uint32_t)sc[1];
@@ -679,7 +680,8 @@ int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
     it[5] = WgFetch{ls + 2, false};
     it[6] = WgFetch{run.flags + run.it - 1, false};
     it[7] = WgFetch{run.flags + run.it, false};
-    return 8;
+    it[8] = WgFetch{ls + 3, false};   // first iteration that changed nothing
+    return 9;
 }
 
 // Validation of a speculative lane build from those words: true = the lanes
@@ -692,7 +694,7 @@ bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v) {
     c->max_lane = (uint32_t)v[3];
     c->n_slots = (uint32_t)v[4];
     c->replay_iters = c->spec_run.it;
-    if (v[6] == 0 && c->replay_blind > 2) c->replay_blind--;   // the fixed point came a launch early
+    c->replay_adapt((uint32_t)v[8]);   // blind count and chunk size from the iterations it took
     c->lane_path = 0;
     return true;
 }

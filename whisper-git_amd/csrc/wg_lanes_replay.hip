@@ -355,8 +355,19 @@ __global__ void k_lf_replay_init_spec(uint64_t nchunks, unsigned long long *occ_
 
 // final: max_lane / slots / overflow over all chunks (nev_dev: chunks past the
 // device event count hold nothing)
+// scal[3]: the first of iterations 1..iters that changed nothing (0: none) —
+// the iterations the next build launches before its first check
 __global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats, uint32_t *__restrict__ scal,
+                                   const uint32_t *__restrict__ flags, uint32_t iters,
                                    const uint32_t *__restrict__ nev_dev = nullptr, uint32_t chunk = 1) {
+    uint32_t fp = ~0u;
+    for (uint32_t i = 1 + threadIdx.x; i <= iters; i += blockDim.x)
+        if (flags[i] == 0 && i < fp) fp = i;
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t o = (uint32_t)__shfl_down((int)fp, d, 64);
+        fp = o < fp ? o : fp;
+    }
+    if (threadIdx.x == 0) scal[3] = fp == ~0u ? 0u : fp;
     if (nev_dev) {
         const uint64_t nd = ((uint64_t)*nev_dev + chunk - 1) / chunk;
         nchunks = nd < nchunks ? nd : nchunks;
@@ -395,7 +406,7 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
     R.on = R.occ_b;
     if (R.max_iters > R.nch + 1) R.max_iters = (uint32_t)(R.nch + 1);
     if (R.nev == 0) {
-        hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, (uint64_t)0, R.stats, R.scal);
+        hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, (uint64_t)0, R.stats, R.scal, (const uint32_t *)R.flags, 0u);
         return hipGetLastError();
     }
     const uint64_t ninit = R.nch > R.max_iters + 1 ? R.nch : R.max_iters + 1;
@@ -412,7 +423,7 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);
     }
-    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal);
+    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it);
     return hipGetLastError();
 }
 
@@ -443,7 +454,8 @@ hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);
     }
-    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, R.nev_dev, R.chunk);
+    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it,
+                       R.nev_dev, R.chunk);
     return hipGetLastError();
 }
 
@@ -465,7 +477,7 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
             *converged = fl[0] == 0 || fl[1] == 0;
         }
     }
-    if (R.nev) hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal);
+    if (R.nev) hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it);
     return hipGetLastError();
 }
 
