@@ -133,6 +133,7 @@ struct ShardState {
     uint64_t n_unres = 0;
     std::vector<uint64_t> uoffs;   // per-rank prefix of those records
     DevBuf flags, xcnt, refx, isfb, xsec;
+    DevBuf dlist;   // the partition's rows {home slot, fingerprint, row} for the duplicate scan's settle pass
     DevBuf xall;              // WgXEnt [nx]: crossing entries of every rank
     std::vector<uint64_t> xoff, evoff, auxoff;   // per-rank prefixes (world + 1)
     uint64_t nev_own = 0, naux_own = 0;

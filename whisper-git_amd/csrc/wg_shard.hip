@@ -80,61 +80,104 @@ __global__ void k_sh_settle(const uint8_t *__restrict__ oid, uint64_t s, uint64_
 }
 
 // every id whose partition (hash) is this rank: any id seen twice?  Same two
-// passes over the partition table; a settling row that meets its own key flags it.
-__global__ void k_sh_dup_place(const uint8_t *__restrict__ oid, uint64_t n, uint32_t world, uint32_t rank,
-                               unsigned long long *table, uint64_t mask) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const Key k = load_key(oid + i * 20);
-    const uint64_t hk = key_hash(k);
-    if ((uint32_t)((hk >> 40) % world) != rank) return;
-    table[hk & mask] = ((unsigned long long)key_fp(k) << 32) | (uint32_t)i;
+// passes over the partition table; a settling row that meets its own key flags
+// it.  The place pass, which streams all N ids, also lists the partition's
+// rows {home slot, fingerprint, row}, compacted per block into the block's own
+// segment of the list (DUP_R * T entries, count in bcnt[block]: no shared
+// counter), so the settle pass touches those ~N/world entries instead of
+// rereading and rehashing every id.
+constexpr int DUP_R = 8;   // rows per thread of the place pass
+inline uint32_t dup_blocks(uint64_t n) { return (uint32_t)((n + (uint64_t)T * DUP_R - 1) / ((uint64_t)T * DUP_R)); }
+
+__global__ void __launch_bounds__(T) k_sh_dup_place(const uint8_t *__restrict__ oid, uint64_t n, uint32_t world,
+                                                    uint32_t rank, unsigned long long *table, uint64_t mask,
+                                                    uint4 *__restrict__ list, uint32_t *__restrict__ bcnt) {
+    __shared__ uint32_t wcnt[T / 64];
+    const int lid = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint4 *seg = list + (uint64_t)blockIdx.x * (T * DUP_R);
+    uint32_t run = 0;   // entries of the block so far (uniform)
+    for (int r = 0; r < DUP_R; r++) {
+        const uint64_t i = ((uint64_t)blockIdx.x * DUP_R + r) * T + threadIdx.x;
+        bool act = false;
+        uint64_t hk = 0;
+        uint32_t fp = 0;
+        if (i < n) {
+            const Key k = load_key(oid + i * 20);
+            hk = key_hash(k);
+            fp = key_fp(k);
+            act = (uint32_t)((hk >> 40) % world) == rank;
+        }
+        if (act) table[hk & mask] = ((unsigned long long)fp << 32) | (uint32_t)i;
+        const uint64_t m = __ballot(act);
+        if (lid == 0) wcnt[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < T / 64; w++) {
+            const uint32_t cw = wcnt[w];
+            before += w < wv ? cw : 0u;
+            total += cw;
+        }
+        if (act) seg[run + before + __popcll(m & ((1ull << lid) - 1ull))] = make_uint4((uint32_t)(hk & mask), fp, (uint32_t)i, 0u);
+        run += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = run;
 }
 
-__global__ void k_sh_dup_settle(const uint8_t *__restrict__ oid, uint64_t n, uint32_t world, uint32_t rank,
-                                unsigned long long *table, uint64_t mask, uint32_t *flags) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const Key k = load_key(oid + i * 20);
-    const uint64_t hk = key_hash(k);
-    if ((uint32_t)((hk >> 40) % world) != rank) return;
-    const unsigned long long mine = ((unsigned long long)key_fp(k) << 32) | (uint32_t)i;
-    uint64_t h = hk & mask;
-    unsigned long long cur = table[h];
-    if (cur == mine) return;
-    for (uint64_t probes = 0; probes <= mask; probes++) {
-        if (cur == HEMPTY) {
-            const unsigned long long prev = atomicCAS(&table[h], HEMPTY, mine);
-            if (prev == HEMPTY) return;
-            cur = prev;
+__global__ void __launch_bounds__(T) k_sh_dup_settle(const uint8_t *__restrict__ oid, unsigned long long *table,
+                                                     uint64_t mask, const uint4 *__restrict__ list,
+                                                     const uint32_t *__restrict__ bcnt, uint32_t *flags) {
+    const uint4 *seg = list + (uint64_t)blockIdx.x * (T * DUP_R);
+    const uint32_t cnt = bcnt[blockIdx.x];
+    for (uint32_t j = threadIdx.x; j < cnt; j += T) {
+        const uint4 en = seg[j];
+        const unsigned long long mine = ((unsigned long long)en.y << 32) | en.z;
+        uint64_t h = en.x;
+        unsigned long long cur = table[h];
+        if (cur == mine) continue;
+        for (uint64_t probes = 0; probes <= mask; probes++) {
+            if (cur == HEMPTY) {
+                const unsigned long long prev = atomicCAS(&table[h], HEMPTY, mine);
+                if (prev == HEMPTY) break;
+                cur = prev;
+            }
+            if ((uint32_t)(cur >> 32) == en.y &&
+                key_eq(load_key(oid + (uint64_t)en.z * 20), oid + (uint64_t)(uint32_t)cur * 20)) {
+                atomicOr(&flags[1], 1u);
+                break;
+            }
+            h = (h + 1) & mask;
+            cur = table[h];
         }
-        if ((uint32_t)(cur >> 32) == key_fp(k) && key_eq(k, oid + (uint64_t)(uint32_t)cur * 20)) {
-            atomicOr(&flags[1], 1u);
-            return;
-        }
-        h = (h + 1) & mask;
-        cur = table[h];
     }
 }
 
-// own rows' references against the local table; per-row count of the unresolved
-// (E0 = parent_off[s]: the shard's first reference, read here rather than by the host)
-__global__ void k_sh_probe(uint64_t s, uint64_t nl, const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
+// own references against the local table, one thread per reference
+// (E0 = parent_off[s], E1 = parent_off[e]: read here rather than by the host)
+__global__ void k_sh_probe(uint64_t s, uint64_t e, const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
                            const uint8_t *__restrict__ oid, const unsigned long long *__restrict__ table,
-                           uint64_t mask, int32_t *__restrict__ prow_l, uint32_t *__restrict__ ucnt, uint32_t *flags) {
+                           uint64_t mask, int32_t *__restrict__ prow_l) {
+    const uint64_t E0 = poff[s], E1 = poff[e];
+    for (uint64_t k = E0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < E1; k += (uint64_t)gridDim.x * blockDim.x)
+        prow_l[k - E0] = (int32_t)hash_find(load_key(poid + k * 20), oid, table, mask);
+}
+
+// per own row: count of the unresolved references; a parent at an earlier row
+// (or the row itself) or more than 2^16 parents flags a violation
+__global__ void k_sh_ucnt(uint64_t s, uint64_t nl, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow_l,
+                          uint32_t *__restrict__ ucnt, uint32_t *flags) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nl) return;
     const uint64_t E0 = poff[s];
     const uint64_t gi = s + i;
     const uint32_t pa = poff[gi], pb = poff[gi + 1];
     uint32_t nu = 0;
-    bool bad = false;
+    bool bad = pb - pa > 0x10000u;
     for (uint32_t k = pa; k < pb; k++) {
-        const int64_t r = hash_find(load_key(poid + (uint64_t)k * 20), oid, table, mask);
-        prow_l[k - E0] = (int32_t)r;
+        const int32_t r = prow_l[k - E0];
         if (r < 0) nu++;
-        else if ((uint64_t)r <= gi) bad = true;       // parent at an earlier row (or itself)
-        if (k - pa > 0xFFFFu) bad = true;
+        else if ((uint64_t)r <= gi) bad = true;
     }
     ucnt[i] = nu;
     if (bad) atomicOr(&flags[0], 1u);
@@ -789,6 +832,7 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     while (pcap < 2 * (N / world + 1) + 1024) pcap <<= 1;
     WG_ALLOC(c, c->hash, cap * 8);
     WG_ALLOC(c, S.ptable, pcap * 8);
+    WG_ALLOC(c, S.dlist, (uint64_t)dup_blocks(N) * (T * DUP_R * 16 + 4) + 16);
     WG_ALLOC(c, S.prow, El * 4 + 4);
     WG_ALLOC(c, S.xcnt, (nl + 2) * 4);
     WG_ALLOC(c, S.flags, 64);
@@ -799,15 +843,20 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     WG_HIP(c, hipMemsetAsync(S.flags.p, 0, 64, st));
     if (nl) hipLaunchKernelGGL(k_sh_place, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
                                c->hash.as<unsigned long long>(), cap - 1);
-    if (N) hipLaunchKernelGGL(k_sh_dup_place, dim3(blocks(N)), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
-                              S.ptable.as<unsigned long long>(), pcap - 1);
+    const uint32_t nbd = dup_blocks(N);
+    uint32_t *bcnt = reinterpret_cast<uint32_t *>(S.dlist.as<uint4>() + (uint64_t)nbd * T * DUP_R);
+    if (N) hipLaunchKernelGGL(k_sh_dup_place, dim3(nbd), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
+                              S.ptable.as<unsigned long long>(), pcap - 1, S.dlist.as<uint4>(), bcnt);
     if (nl) hipLaunchKernelGGL(k_sh_settle, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
                                c->hash.as<unsigned long long>(), cap - 1);
-    if (N) hipLaunchKernelGGL(k_sh_dup_settle, dim3(blocks(N)), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
-                              S.ptable.as<unsigned long long>(), pcap - 1, S.flags.as<uint32_t>());
-    if (nl) hipLaunchKernelGGL(k_sh_probe, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff, c->d_poid,
-                               c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>(),
-                               S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
+    if (N) hipLaunchKernelGGL(k_sh_dup_settle, dim3(nbd), dim3(T), 0, st, c->d_oid, S.ptable.as<unsigned long long>(),
+                              pcap - 1, S.dlist.as<const uint4>(), (const uint32_t *)bcnt, S.flags.as<uint32_t>());
+    if (nl) {
+        hipLaunchKernelGGL(k_sh_probe, dim3(blocks(nl + nl / 2)), dim3(T), 0, st, row_begin, row_end, c->d_poff, c->d_poid,
+                           c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>());
+        hipLaunchKernelGGL(k_sh_ucnt, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff,
+                           S.prow.as<const int32_t>(), S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
+    }
     WG_HIP(c, wg_exclusive_scan_u32(S.xcnt.as<uint32_t>(), S.xcnt.as<uint32_t>(), nl, c->scan_tmp.p, st));
     c->hcap = cap;
     S.step = SH_X1;
