@@ -166,7 +166,8 @@ __global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__res
     __shared__ uint32_t wn[16];
     __shared__ double carry;
     __shared__ uint32_t carry_int;   // all chunks so far integral
-    if (threadIdx.x == 0) { carry = 0.0; carry_int = 1u; }
+    __shared__ uint32_t n_exact;     // the exact regime is a prefix of the chunks: its length
+    if (threadIdx.x == 0) { carry = 0.0; carry_int = 1u; n_exact = 0u; }
     __syncthreads();
     for (uint64_t base = 0; base < nch; base += 1024) {
         const uint64_t c = base + threadIdx.x;
@@ -187,18 +188,19 @@ __global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__res
         }
         const double pre = carry + wb + inc - v;
         const uint32_t nonint_incl = nb + ninc;   // non-integral chunks in [base, c]
+        // exact regime: every chunk up to c integral and the sum after c <= 2^24
+        const bool exact = c < nch && carry_int && nonint_incl == 0 && pre + v <= TWO24 && !flags[0];
         if (c < nch) {
             ch[c].prefix = pre;
             ch[c].kguess = pre > 0.0 ? ilogb(pre) : -1000;
-            // exact regime: every chunk up to c integral and the sum after c <= 2^24
-            const bool exact = carry_int && nonint_incl == 0 && pre + v <= TWO24 && !flags[0];
             ch[c].mode = exact ? MODE_EXACT : MODE_REPLAYED;
             ch[c].start = (float)pre;
         }
-        __syncthreads();
-        if (threadIdx.x == 0) { carry += tot; if (ntot) carry_int = 0u; }
+        const int nx = __syncthreads_count(exact);
+        if (threadIdx.x == 0) { carry += tot; if (ntot) carry_int = 0u; n_exact += (uint32_t)nx; }
         __syncthreads();
     }
+    if (threadIdx.x == 0) flags[3] = n_exact;   // the walk starts after the exact regime
 }
 
 __global__ void __launch_bounds__(RT_T) k_rt_tables(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
@@ -423,6 +425,19 @@ __device__ float replay_chunk(uint64_t r0, uint64_t r1, float acc, const float *
     return acc;
 }
 
+// table b of a chunk's (or super-chunk's) WG_RT_NBIN binade tables, invalid
+// outside them; all of them are loaded, so the loads do not wait for b
+__device__ __forceinline__ Td pick_table(const uint4 *__restrict__ tab, int b) {
+    uint4 q[WG_RT_NBIN];
+#pragma unroll
+    for (int j = 0; j < WG_RT_NBIN; j++) q[j] = tab[j];
+    uint4 r = make_uint4(0u, 0u, 2u, 0u);   // td_invalid()
+#pragma unroll
+    for (int j = 0; j < WG_RT_NBIN; j++)
+        if (b == j) r = q[j];
+    return Td{r.x, r.y, r.z};
+}
+
 __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const float *__restrict__ h,
                                                 const float *__restrict__ band, RtChunk *__restrict__ ch,
                                                 const uint4 *__restrict__ tables, uint32_t *__restrict__ flags,
@@ -430,16 +445,11 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
                                                 const int32_t *__restrict__ skbase, SupState *__restrict__ sup) {
     const int lid = threadIdx.x & 63;
     const bool all_serial = flags[0] != 0;
-    // skip the exact-regime prefix (its chunks are independent prefix sums)
+    // skip the exact-regime prefix (its chunks are independent prefix sums;
+    // k_rt_prefix counted them)
     uint64_t c = 0;
     if (!all_serial) {
-        for (uint64_t b = 0; b < nch; b += 64) {
-            const uint64_t cc = b + lid;
-            const uint64_t m = __ballot(cc < nch && ch[cc].mode == MODE_EXACT);
-            if (m == ~0ull) { c = b + 64; continue; }
-            c = b + (uint64_t)__builtin_ctzll(~m);
-            break;
-        }
+        c = flags[3];
         if (c > nch) c = nch;
     }
     float A = c == 0 ? 0.0f : (float)(ch[c - 1].prefix + ch[c - 1].sum);   // exact (<= 2^24, integral)
@@ -453,11 +463,9 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
             const double top = ldexp(1.0, k + 1);
             const uint32_t p = parity_at(A, k);
             const uint64_t ss = c / RT_SUP + lid;
+            // the base and all WG_RT_NBIN tables in one load round; the binade picks after
             Td t = td_invalid();
-            if (ss < nsup) {
-                const int b = k - skbase[ss];
-                if (b >= 0 && b < WG_RT_NBIN) { const uint4 q = stab[ss * WG_RT_NBIN + b]; t = Td{q.x, q.y, q.z}; }
-            }
+            if (ss < nsup) t = pick_table(stab + ss * WG_RT_NBIN, k - skbase[ss]);
             t = td_scan(t);
             const uint32_t D = p ? t.d1 : t.d0;
             const bool ok = (t.f & 4u) && ss < nsup && (double)A + (double)D * (double)u < top;
@@ -478,13 +486,7 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
             const uint32_t p = parity_at(A, k);
             const uint64_t cc = c + lid;
             Td t = td_invalid();
-            if (cc < nch) {
-                const int b = k - ch[cc].kguess + 1;
-                if (b >= 0 && b < WG_RT_NBIN) {
-                    const uint4 q = tables[cc * WG_RT_NBIN + b];
-                    t = Td{q.x, q.y, q.z};
-                }
-            }
+            if (cc < nch) t = pick_table(tables + cc * WG_RT_NBIN, k - ch[cc].kguess + 1);
             t = td_scan(t);   // ordered inclusive scan: P_j = T_c o ... o T_{c+j}
             const uint32_t D = p ? t.d1 : t.d0;
             const bool ok = (t.f & 4u) && cc < nch && cc / RT_SUP == c / RT_SUP &&   // stop at the super boundary
