@@ -79,3 +79,24 @@ def test_frames_recompute_from_first_changed_row(engine):
     engine.enable_timing(False)
     assert names.count("geom_reuse") == 7
     o.close()
+
+
+def test_frames_rescan_row_top_beyond_2_24(engine):
+    """row_top of a frame whose bands changed from r0 on is rescanned from the
+    unchanged value at r0's chunk: starts past 2^24 (the transducer walk from
+    a non-zero accumulator, binade crossings after it), in the exact regime,
+    and from a non-integral value — every frame bit-exact against the oracle."""
+    d = synth.generate("wide16", 600000, seed=5)
+    engine.build(d)
+    o = oracle_c.OracleLayout(d)
+    band = d.band.copy()
+    engine.row_geometry(band)
+    assert engine.geometry()["row_top"][-1] > 2 ** 24
+    for r0, val in ((500000, 30.0), (599990, 0.0), (430000, 30.0), (300000, 30.0), (450000, 7.25), (550000, 30.0)):
+        band[r0] = np.float32(val)
+        engine.row_geometry(band)
+        g = engine.geometry()
+        og = o.row_geometry(band)
+        assert g["row_top"].tobytes() == og["row_top"].tobytes(), r0
+        assert g["curve"].tobytes() == og["curve"].tobytes(), r0
+    o.close()

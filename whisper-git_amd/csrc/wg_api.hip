@@ -605,6 +605,7 @@ int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
     // row_geometry_with_bands every frame, commit_graph.rs:1419-1421): the same
     // layout with bitwise the same bands as the geometry in place -> nothing to do.
     const bool same_layout = had_geom && c->geom_key_gen == c->layout_gen;
+    c->geom_r0 = 0;   // whole pass unless the compare below finds equal leading bands
     if (same_layout && !band && !c->geom_key_band) { c->have_geom = true; return WG_OK; }
     if (same_layout && band && c->geom_key_band && c->n) {
         WG_ALLOC(c, c->geom_diff_first, 16);
@@ -625,7 +626,8 @@ int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
         c->band_keep = c->band_prev.as<float>();
     }
     struct KeepOff { wg_ctx *c; ~KeepOff() { c->band_keep = nullptr; } } keep_off{c};
-    if ((rc = wg_stage_rowtop(c, d_band)) != WG_OK) return rc;
+    // bands equal below geom_r0: row_top is rescanned from there
+    if ((rc = wg_stage_rowtop(c, d_band, c->geom_r0)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, d_band)) != WG_OK) return rc;
     c->have_geom = true;
     c->geom_key_gen = c->layout_gen;

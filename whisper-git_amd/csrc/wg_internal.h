@@ -463,8 +463,9 @@ int wg_side_join(wg_ctx *c);
 // heights of rows [0, m) of the list + zero-band row_top into (h, rt), on the side stream
 int wg_side_zero_rowtop(wg_ctx *c, uint64_t m, float *h, float *rt, uint64_t row_lo);
 int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top,
-                  uint64_t row_lo);   // rows below row_lo: walked, not written
-int wg_stage_rowtop(wg_ctx *c, const float *d_band);   // wg_rowtop.hip
+                  uint64_t row_lo,    // rows below row_lo: walked, not written
+                  uint64_t r_from = 0);   // steps below r_from unchanged since row_top was last written: rescan from there
+int wg_stage_rowtop(wg_ctx *c, const float *d_band, uint64_t r_from = 0);   // wg_rowtop.hip
 int wg_stage_geometry(wg_ctx *c, const float *d_band); // wg_geom.hip
 int wg_geom_summary_sync(wg_ctx *c);                   // read a frame pass's summary when asked for
 int wg_geom_spec_items(wg_ctx *c, WgFetch *it);        // speculative full pass: 8 validation words

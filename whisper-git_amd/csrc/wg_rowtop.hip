@@ -161,13 +161,22 @@ __global__ void __launch_bounds__(RT_T) k_rt_sum(uint64_t n, const float *__rest
 }
 
 // exact f64 prefix over chunks; exact-regime marking; binade guesses
-__global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__restrict__ ch, uint32_t *__restrict__ flags) {
+// a0: the accumulator before row 0 (a suffix recomputed from an unchanged
+// row_top value, wg_rowtop_run's r_from), null = 0
+__global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__restrict__ ch, uint32_t *__restrict__ flags,
+                                                    const float *__restrict__ a0) {
     __shared__ double ws[16];
     __shared__ uint32_t wn[16];
     __shared__ double carry;
     __shared__ uint32_t carry_int;   // all chunks so far integral
     __shared__ uint32_t n_exact;     // the exact regime is a prefix of the chunks: its length
-    if (threadIdx.x == 0) { carry = 0.0; carry_int = 1u; n_exact = 0u; }
+    if (threadIdx.x == 0) {
+        // an exact start: a finite integer within 2^24 (row_top there is the exact sum)
+        const float A0 = a0 ? *a0 : 0.0f;
+        carry = (double)A0;
+        carry_int = (A0 >= 0.0f && A0 <= 16777216.0f && A0 == truncf(A0)) ? 1u : 0u;
+        n_exact = 0u;
+    }
     __syncthreads();
     for (uint64_t base = 0; base < nch; base += 1024) {
         const uint64_t c = base + threadIdx.x;
@@ -442,7 +451,8 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
                                                 const float *__restrict__ band, RtChunk *__restrict__ ch,
                                                 const uint4 *__restrict__ tables, uint32_t *__restrict__ flags,
                                                 float *__restrict__ row_top, uint64_t nsup, const uint4 *__restrict__ stab,
-                                                const int32_t *__restrict__ skbase, SupState *__restrict__ sup) {
+                                                const int32_t *__restrict__ skbase, SupState *__restrict__ sup,
+                                                const float *__restrict__ a0) {
     const int lid = threadIdx.x & 63;
     const bool all_serial = flags[0] != 0;
     // skip the exact-regime prefix (its chunks are independent prefix sums;
@@ -452,7 +462,7 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
         c = flags[3];
         if (c > nch) c = nch;
     }
-    float A = c == 0 ? 0.0f : (float)(ch[c - 1].prefix + ch[c - 1].sum);   // exact (<= 2^24, integral)
+    float A = c == 0 ? (a0 ? *a0 : 0.0f) : (float)(ch[c - 1].prefix + ch[c - 1].sum);   // exact (<= 2^24, integral)
     uint64_t replayed = 0;
     while (c < nch) {
         bool do_replay = all_serial || !(A > 0.0f) || !isfinite(A);
@@ -633,7 +643,23 @@ int wg_stage_heights(wg_ctx *c) {
 // row_top[0..n] of n rows with heights h (+ band, may be null).  Rows below
 // row_lo are only walked through (a row shard needs row_top of its own rows;
 // entries below row_lo are left unspecified).
-int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top, uint64_t row_lo) {
+int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top, uint64_t row_lo,
+                  uint64_t r_from) {
+    // Rows below r_from kept their steps: row_top up to r_from is unchanged, so
+    // the scan restarts at the chunk boundary below it from the row_top value
+    // already there (the sequential sum carries nothing else).
+    const float *a0 = nullptr;
+    if (r_from > 0 && r_from <= n) {
+        const uint64_t cs = r_from / WG_RT_CHUNK * WG_RT_CHUNK;
+        if (cs > 0) {
+            h += cs;
+            if (d_band) d_band += cs;
+            row_top += cs;
+            a0 = row_top;
+            n -= cs;
+            row_lo = row_lo > cs ? row_lo - cs : 0;
+        }
+    }
     const uint64_t nch = (n + WG_RT_CHUNK - 1) / WG_RT_CHUNK;
     WG_ALLOC(c, c->rt_chunk, (nch + 1) * sizeof(RtChunk));
     WG_ALLOC(c, c->rt_tables, (nch + 1) * WG_RT_NBIN * sizeof(uint4));
@@ -641,14 +667,14 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
     wg_stage_begin(c, "row_top");
     WG_HIP(c, hipMemsetAsync(c->rt_flags.p, 0, 64, c->stream));
     if (n == 0) {
-        WG_HIP(c, hipMemsetAsync(row_top, 0, 4, c->stream));
+        if (!a0) WG_HIP(c, hipMemsetAsync(row_top, 0, 4, c->stream));
         wg_stage_end(c);
         return WG_OK;
     }
     RtChunk *ch = c->rt_chunk.as<RtChunk>();
     uint32_t *fl = c->rt_flags.as<uint32_t>();
     hipLaunchKernelGGL(k_rt_sum, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, ch, fl);
-    hipLaunchKernelGGL(k_rt_prefix, dim3(1), dim3(1024), 0, c->stream, nch, ch, fl);
+    hipLaunchKernelGGL(k_rt_prefix, dim3(1), dim3(1024), 0, c->stream, nch, ch, fl, a0);
     hipLaunchKernelGGL(k_rt_tables, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch,
                        c->rt_tables.as<uint4>());
     const uint64_t nsup = nch / RT_SUP;   // full super-chunks only
@@ -662,7 +688,7 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
                            c->rt_tables.as<const uint4>(), stab, skb);
     }
     hipLaunchKernelGGL(k_rt_walk, dim3(1), dim3(64), 0, c->stream, n, nch, h, d_band, ch,
-                       c->rt_tables.as<const uint4>(), fl, row_top, nsup, (const uint4 *)stab, (const int32_t *)skb, sup);
+                       c->rt_tables.as<const uint4>(), fl, row_top, nsup, (const uint4 *)stab, (const int32_t *)skb, sup, a0);
     if (nsup)
         hipLaunchKernelGGL(k_rt_fill, dim3(nsup), dim3(64), 0, c->stream, nch, (const SupState *)sup, ch,
                            c->rt_tables.as<const uint4>());
@@ -675,8 +701,8 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
     return WG_OK;
 }
 
-int wg_stage_rowtop(wg_ctx *c, const float *d_band) {
+int wg_stage_rowtop(wg_ctx *c, const float *d_band, uint64_t r_from) {
     if (const int rc = wg_side_join(c)) return rc;   // the side stream's row_top shares the scan buffers
     WG_ALLOC(c, c->g_row_top, (c->n + 1) * 4);
-    return wg_rowtop_run(c, c->n, c->heights.as<const float>(), d_band, c->g_row_top.as<float>(), 0);
+    return wg_rowtop_run(c, c->n, c->heights.as<const float>(), d_band, c->g_row_top.as<float>(), 0, r_from);
 }
