@@ -82,10 +82,38 @@ __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float
     rowflags[r] = f;
 }
 
-// per-row list counts (difference arrays for the spans) and, in the same pass
-// over the edges, the sweep's carry-in counts per 64-row chunk (carry_diff)
+// per-row list counts (difference arrays for the spans) and the sweep's
+// carry-in counts per 64-row chunk (carry_diff), in two passes: the child
+// side per row over the row's edges (edges are in child order: plain stores,
+// one carry count per wave, whose 64 rows share a chunk), then the parent
+// side per edge with atomics (:526-528: child_row >= parent_row adds nothing)
+__global__ void __launch_bounds__(256) k_edge_counts_child(uint64_t n, const uint32_t *__restrict__ edge_off,
+                                                           const wg_edge *__restrict__ edges, uint32_t *cntB,
+                                                           uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend,
+                                                           uint32_t *carry_diff) {
+    static_assert(WG_SWEEP_CH == 64, "a wave's rows are one sweep chunk");
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t b = 0, f = 0, cc = 0, ce = 0, cd = 0;
+    if (r < n) {
+        for (uint32_t k = edge_off[r]; k < edge_off[r + 1]; k++) {
+            const wg_edge e = edges[k];
+            const uint32_t c = e.child_row, p = e.parent_row;
+            if (c >= p) continue;
+            cd += c / WG_SWEEP_CH + 1 <= p / WG_SWEEP_CH;
+            if (e.child_lane == e.parent_lane) { b++; f += c + 1 < p; }
+            else { cc += c + 1 < p; ce++; }   // (the swept lists' flag row is all zero: no child-end filter)
+        }
+        cntB[r] = b;
+        diffF[r + 1] = f;
+        diffC[r + 1] = cc;
+        cntCend[r] = ce;
+    }
+    const uint32_t tot = wg_wave_scan(cd, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    if ((threadIdx.x & 63) == 63 && r - 63 < n) carry_diff[r / WG_SWEEP_CH + 1] = tot;
+}
+
 __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
-                              uint32_t *cntB, uint32_t *cntT, uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend,
+                              uint32_t *cntT, uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend,
                               uint32_t *carry_diff, const uint32_t *__restrict__ ne_dev) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ne || (ne_dev && k >= *ne_dev)) return;
@@ -93,14 +121,12 @@ __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, co
     const uint32_t c = e.child_row, p = e.parent_row;
     if (c >= p) return;                                   // (:526-528)
     const uint32_t k0 = c / WG_SWEEP_CH + 1, k1 = p / WG_SWEEP_CH;
-    if (k0 <= k1) { atomicAdd(&carry_diff[k0], 1u); atomicAdd(&carry_diff[k1 + 1], 0xFFFFFFFFu); }
+    if (k0 <= k1) atomicAdd(&carry_diff[k1 + 1], 0xFFFFFFFFu);
     if (e.child_lane == e.parent_lane) {
-        atomicAdd(&cntB[c], 1u);
         atomicAdd(&cntT[p], 1u);
-        if (c + 1 < p) { atomicAdd(&diffF[c + 1], 1u); atomicAdd(&diffF[p], 0xFFFFFFFFu); }
+        if (c + 1 < p) atomicAdd(&diffF[p], 0xFFFFFFFFu);
     } else {
-        if (c + 1 < p) { atomicAdd(&diffC[c + 1], 1u); atomicAdd(&diffC[p], 0xFFFFFFFFu); }
-        if (!(rowflags[c] & RF_CHILD)) atomicAdd(&cntCend[c], 1u);
+        if (c + 1 < p) atomicAdd(&diffC[p], 0xFFFFFFFFu);
         if (!(rowflags[p] & RF_PARENT)) atomicAdd(&cntCend[p], 1u);
     }
 }
@@ -764,8 +790,10 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
                        c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), (uint64_t)0, c->geom_zero.as<uint4>(),
                        (uint64_t)(zwords / 4), c->band_keep);
+    hipLaunchKernelGGL(k_edge_counts_child, dim3(blocks(n)), dim3(256), 0, s, n, edge_off, E, cntB, cntF, cntC, cntCend,
+                       carry_cnt);
     if (ne)
-        hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntB, cntT, cntF, cntC, cntCend,
+        hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntT, cntF, cntC, cntCend,
                            carry_cnt, ne_dev);
     WG_HIP(c, wg_exclusive_scan2_u32(cntF, cntF, cntC, cntC, n + 1, c->scan_tmp.p, s));
     hipLaunchKernelGGL(k_row_counts, dim3(blocks(n)), dim3(T), 0, s, n, cntF, cntC, cntT, cntB, cntCend, zflags, voff, soff);
