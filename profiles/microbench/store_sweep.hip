@@ -18,7 +18,7 @@
 typedef float v4f __attribute__((ext_vector_type(4)));
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
-enum { MAP_DISPATCH = 0, MAP_XCD = 1, MAP_PERSIST_STRIDE = 2, MAP_PERSIST_CONTIG = 3, MAP_XCD_STAGGER = 4 };
+enum { MAP_DISPATCH = 0, MAP_XCD = 1, MAP_PERSIST_STRIDE = 2, MAP_PERSIST_CONTIG = 3, MAP_XCD_STAGGER = 4, MAP_XCD_DYN = 5 };
 
 template <bool NT, int R, int TH>
 __device__ __forceinline__ void write_tile(v4f *out, size_t n, size_t t) {
@@ -35,8 +35,27 @@ __device__ __forceinline__ void write_tile(v4f *out, size_t n, size_t t) {
 }
 
 template <bool NT, int R, int TH, int MAP>
-__global__ void __launch_bounds__(TH) k_tiles(v4f *out, size_t n, size_t ntiles) {
+__global__ void __launch_bounds__(TH) k_tiles(v4f *out, size_t n, size_t ntiles, unsigned *ctr) {
     const size_t g = gridDim.x, b = blockIdx.x;
+    if (MAP == MAP_XCD_DYN) {
+        // XCD x's workgroups claim the tiles of its eighth in order (one counter
+        // per XCD); once that eighth is taken they claim from the others'
+        __shared__ unsigned s_t;
+        const size_t per = (ntiles + 7) / 8;
+        if (threadIdx.x == 0) {
+            const unsigned x = (unsigned)(b % 8);
+            unsigned t = ~0u;
+            for (unsigned k = 0; k < 8 && t == ~0u; k++) {
+                const unsigned xx = (x + k) % 8;
+                const unsigned i = atomicAdd(&ctr[xx * 32], 1u);
+                if (i < per && xx * per + i < ntiles) t = (unsigned)(xx * per + i);
+            }
+            s_t = t;
+        }
+        __syncthreads();
+        if (s_t != ~0u) write_tile<NT, R, TH>(out, n, s_t);
+        return;
+    }
     if (MAP == MAP_DISPATCH) {
         write_tile<NT, R, TH>(out, n, b);
     } else if (MAP == MAP_XCD) {
@@ -63,6 +82,8 @@ int main(int argc, char **argv) {
     const size_t n = bytes / 16;
     v4f *out;
     CHECK(hipMalloc(&out, bytes));
+    unsigned *ctr;
+    CHECK(hipMalloc(&ctr, 8 * 32 * 4));
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
@@ -90,8 +111,16 @@ int main(int argc, char **argv) {
         const size_t nt_ = (n + (size_t)TH * R - 1) / ((size_t)TH * R);                                        \
         size_t grid_ = (GRID) ? (size_t)(GRID) : nt_;                                                          \
         if (MAP == MAP_XCD || MAP == MAP_XCD_STAGGER) grid_ = ((nt_ + 7) / 8) * 8;                                                       \
-        run(NAME, [&] { hipLaunchKernelGGL((k_tiles<NT, R, TH, MAP>), dim3((unsigned)grid_), dim3(TH), 0, 0, out, n, nt_); }); \
+        if (MAP == MAP_XCD_DYN) grid_ = nt_;                                                                   \
+        run(NAME, [&] {                                                                                        \
+            if (MAP == MAP_XCD_DYN) CHECK(hipMemsetAsync(ctr, 0, 8 * 32 * 4, 0));                              \
+            hipLaunchKernelGGL((k_tiles<NT, R, TH, MAP>), dim3((unsigned)grid_), dim3(TH), 0, 0, out, n, nt_, ctr); \
+        });                                                                                                    \
     }
+    V(true, 6, 256, MAP_XCD, 0, "24KiB/256 nt xcd-split");
+    V(true, 6, 256, MAP_XCD_DYN, 0, "24KiB/256 nt xcd-dynamic");
+    V(true, 3, 256, MAP_XCD, 0, "12KiB/256 nt xcd-split");
+    V(true, 3, 256, MAP_XCD_DYN, 0, "12KiB/256 nt xcd-dynamic");
     V(true, 6, 256, MAP_DISPATCH, 0, "24KiB/256 nt dispatch");
     V(false, 6, 256, MAP_DISPATCH, 0, "24KiB/256 plain dispatch");
     V(true, 6, 256, MAP_XCD, 0, "24KiB/256 nt xcd-split");
@@ -109,5 +138,6 @@ int main(int argc, char **argv) {
     V(false, 12, 256, MAP_XCD, 0, "48KiB/256 plain xcd-split");
     V(true, 18, 256, MAP_XCD, 0, "72KiB/256 nt xcd-split");
     CHECK(hipFree(out));
+    CHECK(hipFree(ctr));
     return 0;
 }
