@@ -73,6 +73,13 @@ def test_four_shards_small(tmp_path):
     run_world(4, "wide16:4000:21,random13:64:22", tmp_path)
 
 
+def test_eight_shards_small(tmp_path):
+    """The C5 shape's world size (eight ranks, here all on one GPU over gloo):
+    eight sections in every exchange, eight id partitions in the duplicate
+    scan, a shard of 3 rows and the anomaly preset's fallback."""
+    run_world(8, "wide16:16000:41,random13:24:42,anomaly:2000:43", tmp_path)
+
+
 def _lockstep(engines, begin):
     """Drive every rank's exchange protocol in one thread: slots written by
     wg_shard_pack_slot in stream order (the device-transport path ShardComm
