@@ -80,6 +80,13 @@ def test_eight_shards_small(tmp_path):
     run_world(8, "wide16:16000:41,random13:24:42,anomaly:2000:43", tmp_path)
 
 
+def test_eight_shards_device_transport(tmp_path):
+    """Eight ranks through ShardComm's device path (bench.py's RCCL path, here
+    HIP tensors over gloo): every slot starts at 16 bytes and overflows once."""
+    res = run_world(8, "wide16:16000:44,linux:12000:45", tmp_path, "device")
+    assert all(r["on_device"] for r in res)
+
+
 def _lockstep(engines, begin):
     """Drive every rank's exchange protocol in one thread: slots written by
     wg_shard_pack_slot in stream order (the device-transport path ShardComm
