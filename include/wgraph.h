@@ -26,7 +26,12 @@
 extern "C" {
 #endif
 
-#define WGRAPH_ABI_VERSION 1
+/* ABI 2 (from 1): wg_shard_msg.bytes may be WG_SHARD_BYTES_ON_DEVICE (the
+ * first build exchange of a multi-rank build always is; ask
+ * wg_shard_msg_bytes); wg_shard_pack_slot / wg_shard_slot_heads take caps
+ * and strides that are multiples of 16 only; wg_shard_exchange fails when a
+ * message header announces more than that rank's sizes[] entry. */
+#define WGRAPH_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 #define WG_OK             0

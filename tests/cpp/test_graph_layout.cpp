@@ -276,6 +276,14 @@ TEST(row_geometry_with_short_band_list) {
     CHECK_EQ(g[6].height, ROW_HEIGHT);
     // the build's geometry (zero bands) is not touched by a frame's call
     CHECK_EQ(layout.row_geometry[0].node_y, NODE_Y);
+    // an empty band list: every band is zero, the build's geometry again
+    const auto g0 = layout.row_geometry_with_bands(commits, {});
+    CHECK_EQ(g0.size(), commits.size());
+    for (size_t r = 0; r < g0.size(); r++) {
+        CHECK_EQ(g0[r].height, layout.row_geometry[r].height);
+        CHECK_EQ(g0[r].node_y, NODE_Y);
+        CHECK_EQ(g0[r].curves.size(), layout.row_geometry[r].curves.size());
+    }
     bool threw = false;
     try {
         (void)layout.row_geometry_with_bands(uniform_list(3), {});

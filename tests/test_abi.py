@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
     assert not missing, missing
     assert set(wgraph.EXPORTED_SYMBOLS) <= set(declared_functions())
-    assert lib.wg_abi_version() == 1
+    assert lib.wg_abi_version() == 2
 
 
 def test_engine_refuses_without_gpu_instead_of_falling_back():

@@ -450,11 +450,13 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     if ((rc = wg_side_join(c)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
     if (spec) {
-        WgFetch it[20];
+        constexpr int K = WG_LANES_SPEC_ITEMS + WG_GEOM_SPEC_ITEMS + 1;
+        static_assert(K <= FETCH_MAX, "validation words exceed one fetch");
+        WgFetch it[K];
         const int kl = wg_lanes_spec_items(c, it);
         int k = kl + wg_geom_spec_items(c, it + kl);
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + n, false};
-        uint64_t v[20] = {0};
+        uint64_t v[K] = {0};
         if ((rc = wg_fetch_n(c, k, it, v)) != WG_OK) return rc;
         c->spec = false;
         const uint64_t ne = v[k - 1];

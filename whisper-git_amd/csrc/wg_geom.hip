@@ -682,7 +682,7 @@ int wg_geom_summary_sync(wg_ctx *c) {
     return WG_OK;
 }
 
-// speculative full pass: its validation words (fills 8 items) and their check
+// speculative full pass: its validation words (WG_GEOM_SPEC_ITEMS) and their check
 int wg_geom_spec_items(wg_ctx *c, WgFetch *it) {
     const uint64_t n = c->n;
     const uint32_t *err = c->geom_err;
@@ -694,7 +694,7 @@ int wg_geom_spec_items(wg_ctx *c, WgFetch *it) {
     it[5] = WgFetch{c->g_row_top.as<uint32_t>() + n, false};
     it[6] = WgFetch{c->rt_flags.as<uint32_t>() + 2, false};
     it[7] = WgFetch{c->curve_off.as<uint32_t>() + n, false};
-    return 8;
+    return WG_GEOM_SPEC_ITEMS;
 }
 
 // true = the speculative pass fit its capacities (the lists are exact)

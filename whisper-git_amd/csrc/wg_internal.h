@@ -431,7 +431,9 @@ hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t
 hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged);
 int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known = -1);   // wg_lanes.hip
 // speculative build (wg_layout_build): validation words of the lane build
-// (fills 8 items) and their check (wg_lanes_fast.hip)
+// (fills WG_LANES_SPEC_ITEMS items) and their check (wg_lanes_fast.hip)
+constexpr int WG_LANES_SPEC_ITEMS = 9;
+constexpr int WG_GEOM_SPEC_ITEMS = 8;
 int wg_lanes_spec_items(wg_ctx *c, WgFetch *it);
 bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v);
 // event-compressed lane phases over a row range (wg_lanes_fast.hip)
@@ -468,7 +470,7 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
 int wg_stage_rowtop(wg_ctx *c, const float *d_band, uint64_t r_from = 0);   // wg_rowtop.hip
 int wg_stage_geometry(wg_ctx *c, const float *d_band); // wg_geom.hip
 int wg_geom_summary_sync(wg_ctx *c);                   // read a frame pass's summary when asked for
-int wg_geom_spec_items(wg_ctx *c, WgFetch *it);        // speculative full pass: 8 validation words
+int wg_geom_spec_items(wg_ctx *c, WgFetch *it);        // speculative full pass: WG_GEOM_SPEC_ITEMS validation words
 bool wg_geom_spec_check(wg_ctx *c, const uint64_t *v);
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel);  // wg_vertex.hip
 int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out);  // wg_vertex.hip

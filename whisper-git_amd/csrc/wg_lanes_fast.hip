@@ -666,8 +666,9 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     return WG_OK;
 }
 
-// The speculative lane build's validation words: {not well formed, events,
-// aux words, max_lane, slots, > 63 slots, changed at it - 1, changed at it}.
+// The speculative lane build's validation words (WG_LANES_SPEC_ITEMS): {not
+// well formed, events, aux words, max_lane, slots, > 63 slots, changed at
+// it - 1, changed at it, first iteration that changed nothing}.
 int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
     const uint64_t n = c->n;
     const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
@@ -681,7 +682,7 @@ int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
     it[6] = WgFetch{run.flags + run.it - 1, false};
     it[7] = WgFetch{run.flags + run.it, false};
     it[8] = WgFetch{ls + 3, false};   // first iteration that changed nothing
-    return 9;
+    return WG_LANES_SPEC_ITEMS;
 }
 
 // Validation of a speculative lane build from those words: true = the lanes

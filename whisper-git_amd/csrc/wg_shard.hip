@@ -739,14 +739,14 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     c->spec = false;
     if (rc != WG_OK) return rc;
     if (spec) {
-        WgFetch it[12];
+        WgFetch it[WG_GEOM_SPEC_ITEMS + 4];
         int k = wg_geom_spec_items(c, it);
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + nloc, false};
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + 1, false};
-        uint64_t v[12] = {0};
+        uint64_t v[WG_GEOM_SPEC_ITEMS + 4] = {0};
         if ((rc = wg_fetch_n(c, k, it, v)) != WG_OK) return rc;
-        S.local_ne = v[8];
-        S.local_nin = v[9];
+        S.local_ne = v[WG_GEOM_SPEC_ITEMS];
+        S.local_nin = v[WG_GEOM_SPEC_ITEMS + 1];
         c->n_edges = S.local_ne;
         S.n_own_edges = S.local_ne - S.local_nin;
         if (!wg_geom_spec_check(c, v)) {   // past a capacity: the exact pass (the local edges are in place)

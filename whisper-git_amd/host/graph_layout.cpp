@@ -96,7 +96,7 @@ const CommitLayout *GraphLayout::get(const Oid &id) const {
 }
 
 std::vector<RowGeometry> GraphLayout::row_geometry_with_bands(const std::vector<CommitInfo> &commits,
-                                                              const std::vector<float> &band_heights) const {
+                                                              const std::vector<float> &band_heights) {
     if (commits.size() != time_.size())
         throw std::invalid_argument("row_geometry_with_bands: commits is not the list of the last build");
     for (size_t i = 0; i < commits.size(); i++)

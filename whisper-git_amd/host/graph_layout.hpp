@@ -152,9 +152,12 @@ public:
     void build(const std::vector<CommitInfo> &commits);
     // :357 — the layout of the last row holding `id` (HashMap insert order)
     const CommitLayout *get(const Oid &id) const;
-    // :367-399 — band_heights[i] (missing entries = 0) above row i
+    // :367-399 — band_heights[i] (missing entries = 0) above row i.  Not
+    // const, unlike the reference's `&self`: the engine's current geometry
+    // becomes the banded one, so emit_vertices() draws it afterwards (the
+    // pub field row_geometry keeps the build's copy).
     std::vector<RowGeometry> row_geometry_with_bands(const std::vector<CommitInfo> &commits,
-                                                     const std::vector<float> &band_heights) const;
+                                                     const std::vector<float> &band_heights);
 
     // pub fields (:244-257)
     size_t max_lane = 0;

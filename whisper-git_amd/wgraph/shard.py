@@ -60,6 +60,7 @@ class ShardComm:
         self.timing = False
         self.host_s = 0.0
         self._events = []
+        self._x0 = 0
         self.heads = None   # host copy of every message's first 16 bytes (uint32 [world, 4]), last exchange
 
     def set_timing(self, on: bool):
@@ -137,7 +138,7 @@ class ShardComm:
         if self.device.type != "cpu" and not self.on_device:
             torch.cuda.current_stream(self.device).synchronize()   # the H2D copy above
         self.exchanges += 1
-        self.bytes_sent += nbytes
+        self.bytes_sent += sizes[self.rank]   # nbytes is 0 when the length lives on the device
         if self.timing:
             self.host_s += time.perf_counter() - t_host
         return out, self.HDR, stride, sizes
