@@ -1,0 +1,109 @@
+"""GPU parity of the event-compressed lane path on the lists the reference
+actually builds (VERDICT r02 "what's missing" #1):
+
+* parents at earlier rows — commit_graph_with_orphans re-sorts the whole list
+  by time when reflog orphans exist (git/mod.rs:767-772), so clock skew puts a
+  parent above its child; the reference then leaks the waiting slot
+  (commit_graph.rs:414-423, :441-454).  These are leaky events of the fast
+  path, not a reason to fall back to the single-wave walk;
+* more than 63 concurrent slots — `active_lanes` grows without bound; the
+  replay's occupancy widens from 1 to 4 to 16 words (63 / 255 / 1023 slots).
+
+Every case is bit-exact against the C oracle (oracle/wg_oracle.c) and must
+stay on lane_path 0.
+"""
+import numpy as np
+import pytest
+
+from wgraph import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(d):
+    from oracle import oracle_c
+    return oracle_c.OracleLayout(d)
+
+
+def _check_lanes(engine, d, o):
+    s = engine.layout_summary()
+    assert s.lane_path == 0, "left the parallel lane path"
+    assert (s.max_lane, s.n_slots) == (o.max_lane, o.n_slots)
+    lane, color = engine.lanes()
+    assert lane.tobytes() == o.lane.astype(np.uint32).tobytes(), np.nonzero(lane != o.lane)[0][:5]
+    assert color.tobytes() == o.color.tobytes()
+    assert engine.edges().tobytes() == o.edges.tobytes()
+
+
+@pytest.mark.parametrize("kind,n,over", [
+    ("skew", 1_000_000, {}),                       # clock skew + 100 orphans, time-sorted (leaky refs)
+    ("linuxwide", 1_000_000, {}),                  # > 100 concurrent lanes (4-word occupancy)
+    ("linux", 200_000, {"max_lines": 400}),        # > 255 slots (16-word occupancy)
+    ("skew", 300_000, {"p_clock_skew": 2e-3}),     # ~1000 leaked slots' worth of skew
+], ids=["skew-1M", "linuxwide-1M", "linux400-200k", "skew-heavy-300k"])
+def test_fast_lanes_on_real_shapes(engine, kind, n, over):
+    d = synth.generate(kind, n, **over)
+    o = _oracle(d)
+    try:
+        if o.n_slots >= 1024:
+            pytest.skip(f"{o.n_slots} slots: beyond the engine's 1023-slot occupancy")
+        engine.build(d)
+        _check_lanes(engine, d, o)
+    finally:
+        o.close()
+
+
+@pytest.mark.parametrize("kind,n", [("skew", 60_000), ("linuxwide", 40_000)])
+def test_leaky_and_wide_full_pipeline(engine, kind, n):
+    """Geometry and vertices of the same lists (edges whose parent sits at an
+    earlier row are skipped by decompose_edge_into_rows, :526-528)."""
+    from oracle import oracle_c
+    d = synth.generate(kind, n, seed=4242)
+    o = _oracle(d)
+    try:
+        engine.build(d)
+        _check_lanes(engine, d, o)
+        engine.row_geometry(d.band)
+        og = o.row_geometry(d.band)
+        got = engine.geometry()
+        for k, v in og.items():
+            assert got[k].tobytes() == v.tobytes(), k
+        sel = n // 3
+        engine.emit_vertices(0, n, selected=sel)
+        ov, ooff = o.emit_vertices(0, n, selected=sel)
+        assert engine.vertex_offsets().tobytes() == ooff.tobytes()
+        assert engine.vertex_summary().checksum == oracle_c.vertex_checksum(ov)
+    finally:
+        o.close()
+
+
+def test_anomalies_without_duplicate_ids_stay_parallel(engine):
+    """The anomaly preset (skewed and self parents, parents outside the list,
+    repeated parents, octopus merges) minus duplicate ids: fast path, exact."""
+    d = synth.generate("anomaly", 50_000, seed=31, p_dup_oid=0.0)
+    o = _oracle(d)
+    try:
+        engine.build(d)
+        _check_lanes(engine, d, o)
+    finally:
+        o.close()
+
+
+def test_speculative_builds_across_widths(engine):
+    """One context builds lists of alternating width: the speculative build
+    replays at the last build's occupancy width, and a list that outgrows it is
+    redone wider by the exact stages — every build equals the oracle."""
+    seq = [("wide16", 100_000, {}), ("linuxwide", 100_000, {}), ("linuxwide", 100_000, {}),
+           ("wide16", 100_000, {}), ("linux", 100_000, {"max_lines": 400}), ("skew", 100_000, {}),
+           ("skew", 100_000, {})]
+    c0 = engine.debug_counters()
+    for kind, n, over in seq:
+        d = synth.generate(kind, n, **over)
+        o = _oracle(d)
+        try:
+            engine.build(d)
+            _check_lanes(engine, d, o)
+        finally:
+            o.close()
+    c1 = engine.debug_counters()
+    assert int(c1[6]) > int(c0[6]), "no speculative build in the sequence"

@@ -100,6 +100,11 @@ struct LfRange {
     uint64_t xown_begin = 0, xown_end = 0;   // this shard's own entries
     uint8_t *isfb = nullptr;          // by global ref index: target beyond e and first reference to it
     uint32_t *xsec = nullptr;         // by global ref index: SECALLOC token of such a secondary reference
+    // by target row - s: the first (row, parent index) reference to the target
+    // from the target's own row or a later one (a parent at an earlier row:
+    // clock skew, orphans re-sorted by time, self parents).  Null: such
+    // references make the list "not well formed" (general walk).
+    unsigned long long *lfirst = nullptr;
 };
 
 // Row-top transducer scan geometry (wg_rowtop.hip)
@@ -164,7 +169,7 @@ struct FontSlot {
 // workspace slots in wg_ctx::lf (wg_lanes_fast.hip; the sharded build reuses LF_EVREC / LF_AUX for the
 // gathered event records)
 enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_CH, LF_SPA, LF_SPB, LF_EVREC,
-       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_COUNT };
+       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_LFIRST, LF_COUNT };
 
 // event replay to a fixed point (wg_lanes_replay.hip)
 struct ReplayRun {
@@ -172,7 +177,8 @@ struct ReplayRun {
     uint32_t chunk = 512, it = 0, max_iters = 0;
     const uint4 *ev = nullptr;
     const uint32_t *aux = nullptr;
-    uint8_t *slots_a = nullptr, *slots_b = nullptr, *sp_prev = nullptr, *sp_next = nullptr;   // sp_prev: last written
+    uint16_t *slots_a = nullptr, *slots_b = nullptr, *sp_prev = nullptr, *sp_next = nullptr;   // sp_prev: last written
+    uint32_t nw = 1;                     // occupancy words (1, 4 or 16: up to 63, 255, 1023 slots)
     unsigned long long *occ_a = nullptr, *occ_b = nullptr, *op = nullptr, *on = nullptr;
     uint32_t *stats = nullptr, *flags = nullptr, *scal = nullptr;
     const uint32_t *nev_dev = nullptr;   // speculative build: event count on the device (nev = upper bound)
@@ -218,6 +224,9 @@ struct wg_ctx {
     uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
+    uint32_t replay_nw = 1;        // occupancy words of the next replay (from the last build's slot count)
+    // the narrowest occupancy (1, 4, 16 words) holding n_slots slots below the sentinel
+    static uint32_t nw_for_slots(uint32_t slots) { return slots < 64 ? 1u : (slots < 256 ? 4u : 16u); }
     // After a replay that reached its fixed point at iteration fp (the first that
     // changed nothing), the next build's blind count: up at once, down by half
     // the excess per build (it used to fall by one per build: after a list that

@@ -2,10 +2,9 @@
 // part 1), bit-identical to GraphLayout::build's greedy (commit_graph.rs:
 // 276-295, 401-471) on well-formed commit lists.
 //
-// Well-formed = every id distinct and every in-list parent at a larger row
-// (checked in parallel; anything else — duplicate ids, clock-skewed parents,
-// self parents — takes the general walk in wg_lanes.hip).  Then the
-// sequential state has a static description:
+// Well-formed = every id distinct (checked in parallel; duplicate ids take
+// the general walk in wg_lanes.hip).  Then the sequential state has a static
+// description:
 //   * a slot waiting for commit j is set only by a child of j (rows < j) and
 //     stays until row j, so the waiters of j are: one slot per first-parent
 //     child, plus one slot if the FIRST in-list reference to j (row, parent
@@ -15,6 +14,16 @@
 //     the others freed (MIN, :287-291).  First parent outside the list: the
 //     slot is freed (FREE) or never occupied (probe ALLOC).  First
 //     references through a secondary parent: SECALLOC (:454-458).
+//   * a parent p at an earlier row (or the row itself: clock skew, orphans
+//     re-sorted by time, git/mod.rs:767-772; self parents) is "leaky": its
+//     row is processed, so nothing ever frees a slot set to wait for it
+//     (:287-291 only runs at p's own row).  A leaky first parent keeps the
+//     row's slot occupied for good (the row's chain never ends); a leaky
+//     secondary parent allocates (SECALLOC, never consumed) unless an
+//     earlier leaky reference — from a row in [p, i), or an earlier parent
+//     of the same row — already holds a slot for p (:450-452).  So a leaky
+//     reference is "first" by the minimum (row, parent index) among the
+//     leaky references to p (LfRange::lfirst), apart from p's own waiters.
 // Only those events touch the slot-occupancy state, and they are a few
 // percent of rows.  The pipeline:
 //   refs     first reference + first-parent child count per row (atomics)
@@ -72,6 +81,8 @@ __device__ __forceinline__ bool first_in_row(const int32_t *__restrict__ prow, u
 // is ref k (row gi, index kidx, target p) the first in-list reference to p?
 __device__ __forceinline__ bool is_first_ref(const LfRange &R, const unsigned long long *__restrict__ first_ref,
                                              uint64_t gi, uint32_t k, uint32_t kidx, uint64_t p) {
+    if (p <= gi)   // leaky; without lfirst (or before s) k_lf_refs flagged the list and nothing here is used
+        return R.lfirst && p >= R.s && R.lfirst[p - R.s] == ref_key(gi, kidx);
     if (p >= R.e) return R.isfb[k] != 0;
     return first_ref[p - R.s] == ref_key(gi, kidx);
 }
@@ -85,8 +96,12 @@ __global__ void k_lf_refs(LfRange R, unsigned long long *first_ref, uint32_t *fp
     for (uint32_t k = pa; k < pb; k++) {
         const int32_t p = R.prow[k];
         if (p < 0) continue;
-        if ((uint64_t)p <= gi) { bad = true; continue; }
         if (k - pa > 0xFFFFu) { bad = true; continue; }
+        if ((uint64_t)p <= gi) {                     // leaky: target at this row or earlier
+            if (!R.lfirst || (uint64_t)p < R.s) { bad = true; continue; }
+            if (first_in_row(R.prow, pa, k, p)) atomicMin(&R.lfirst[p - R.s], ref_key(gi, k - pa));
+            continue;
+        }
         if ((uint64_t)p >= R.e) continue;            // beyond the shard: crossing entry
         if (!first_in_row(R.prow, pa, k, p)) continue;
         atomicMin(&first_ref[p - R.s], ref_key(gi, k - pa));
@@ -159,7 +174,8 @@ __global__ void k_lf_secev(LfRange R, const unsigned long long *__restrict__ fir
     for (uint32_t k = pa + 1; k < pb; k++) {
         const int32_t p = R.prow[k];
         if (p < 0 || !is_first_ref(R, first_ref, gj, k, k - pa, (uint64_t)p)) continue;
-        if ((uint64_t)p < R.e) secev[p - R.s] = WG_TOK_EV | e;
+        if ((uint64_t)p <= gj) {}                    // leaky: nothing waits for this slot
+        else if ((uint64_t)p < R.e) secev[p - R.s] = WG_TOK_EV | e;
         else R.xsec[k] = WG_TOK_EV | e;
         e++;
     }
@@ -182,7 +198,7 @@ __global__ void k_lf_children(LfRange R, const uint32_t *__restrict__ ch_off, ui
     const uint32_t pa = R.poff[gi];
     if (pa == R.poff[gi + 1]) return;
     const int32_t p = R.prow[pa];
-    if (p < 0 || (uint64_t)p >= R.e) return;
+    if (p < 0 || (uint64_t)p >= R.e || (uint64_t)p <= gi) return;   // beyond the range / leaky
     const uint64_t pl = (uint64_t)p - R.s;
     ch[ch_off[pl] + atomicAdd(&ch_fill[pl], 1u)] = (uint32_t)i;
 }
@@ -338,7 +354,7 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
     }
 }
 
-__global__ void k_lf_lanes(uint64_t nl, const uint32_t *__restrict__ sp, const uint8_t *__restrict__ slot_of,
+__global__ void k_lf_lanes(uint64_t nl, const uint32_t *__restrict__ sp, const uint16_t *__restrict__ slot_of,
                            uint32_t *__restrict__ lane, const uint32_t *__restrict__ gate = nullptr) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nl) return;
@@ -350,9 +366,11 @@ __global__ void k_lf_lanes(uint64_t nl, const uint32_t *__restrict__ sp, const u
 // first references "none", per-row counters and the chain fill counters 0,
 // the flag words 0
 __global__ void k_lf_clear(uint64_t n, unsigned long long *__restrict__ first_ref, uint32_t *__restrict__ fpc,
-                           uint32_t *__restrict__ ch_fill, uint32_t *__restrict__ flags) {
+                           uint32_t *__restrict__ ch_fill, uint32_t *__restrict__ flags,
+                           unsigned long long *__restrict__ lfirst) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) first_ref[i] = REF_NONE;
+    if (lfirst && i < n) lfirst[i] = REF_NONE;
     if (i < n + 2) { fpc[i] = 0u; ch_fill[i] = 0u; }
     if (i < 16) flags[i] = 0u;
 }
@@ -408,7 +426,7 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back) {
     { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "lf_refs");
     hipLaunchKernelGGL(k_lf_clear, dim3(blocks(n + 16)), dim3(T), 0, s, n, first_ref.as<unsigned long long>(),
-                       fpc.as<uint32_t>(), ch_fill.as<uint32_t>(), flags.as<uint32_t>());
+                       fpc.as<uint32_t>(), ch_fill.as<uint32_t>(), flags.as<uint32_t>(), R.lfirst);
     if (n) hipLaunchKernelGGL(k_lf_refs, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<unsigned long long>(),
                               fpc.as<uint32_t>(), flags.as<uint32_t>());
     if (R.xin_end)
@@ -545,29 +563,46 @@ int wg_lf_events_finish(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uin
 // fixed point and assigns the lanes of the range; c->max_lane / n_slots.
 // The replay's convergence check rides on the lane-scalar read: steady-state
 // builds launch exactly the iterations they need with one host sync.
+static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                           uint32_t nw, bool *ok, bool *overflow);
+
 int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
                        bool *ok) {
+    *ok = false;
+    // the occupancy width of the last build first; a replay that overflowed
+    // it is redone wider (63 -> 255 -> 1023 slots)
+    for (uint32_t nw = c->replay_nw;; nw = nw < 4 ? 4u : 16u) {
+        bool overflow = false;
+        const int rc = replay_lanes_at(c, R, nev, ev, aux, lane, nw, ok, &overflow);
+        if (rc != WG_OK || !overflow || nw >= 16) return rc;
+    }
+}
+
+static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                           uint32_t nw, bool *ok, bool *overflow) {
     hipStream_t s = c->stream;
     *ok = false;
+    *overflow = false;
     wg_stage_begin(c, "lf_loop");
     ReplayRun run;
     run.nev = nev;
+    run.nw = nw;
     run.chunk = c->replay_chunk;
     const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
     DevBuf &rflags = c->lf[LF_RFLAGS];
-    WG_ALLOC(c, slot_a, nev + 64);
-    WG_ALLOC(c, slot_b, nev + 64);
-    WG_ALLOC(c, occ, nch * 16 + 16);
+    WG_ALLOC(c, slot_a, (nev + 64) * sizeof(uint16_t));
+    WG_ALLOC(c, slot_b, (nev + 64) * sizeof(uint16_t));
+    WG_ALLOC(c, occ, (nch * 16 + 16) * nw);
     WG_ALLOC(c, stats, nch * 8 + 8);
     WG_ALLOC(c, rflags, (run.max_iters + 2) * 4);
     run.ev = ev;
     run.aux = aux;
-    run.slots_a = slot_a.as<uint8_t>();
-    run.slots_b = slot_b.as<uint8_t>();
+    run.slots_a = slot_a.as<uint16_t>();
+    run.slots_b = slot_b.as<uint16_t>();
     run.occ_a = occ.as<unsigned long long>();
-    run.occ_b = occ.as<unsigned long long>() + nch;
+    run.occ_b = occ.as<unsigned long long>() + nch * nw;
     run.stats = stats.as<uint32_t>();
     run.flags = rflags.as<uint32_t>();
     run.scal = c->lane_scalars.as<uint32_t>();
@@ -599,9 +634,11 @@ int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *e
     // excess if fewer (a list that needed many must not hold later ones for long)
     if (sc[5] >= 1) c->replay_adapt((uint32_t)sc[5]);
     else if (run.it > blind) c->replay_blind = run.it;
-    if (!conv || sc[2]) return WG_OK;               // no fixed point / more than 63 slots
+    if (conv && sc[2]) *overflow = true;            // more than 64 nw - 1 slots: the caller widens
+    if (!conv || sc[2]) return WG_OK;               // no fixed point / overflow
     c->max_lane = (uint32_t)sc[0];
     c->n_slots = (uint32_t)sc[1];
+    c->replay_nw = wg_ctx::nw_for_slots(c->n_slots);
     *ok = true;
     return WG_OK;
 }
@@ -637,22 +674,23 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     ReplayRun &run = c->spec_run;
     run = ReplayRun{};
     run.nev = nev_cap;
+    run.nw = c->replay_nw;
     run.chunk = c->replay_chunk;
     const uint64_t nch = (nev_cap + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
     DevBuf &rflags = c->lf[LF_RFLAGS];
-    WG_ALLOC(c, slot_a, nev_cap + 64);
-    WG_ALLOC(c, slot_b, nev_cap + 64);
-    WG_ALLOC(c, occ, nch * 16 + 16);
+    WG_ALLOC(c, slot_a, (nev_cap + 64) * sizeof(uint16_t));
+    WG_ALLOC(c, slot_b, (nev_cap + 64) * sizeof(uint16_t));
+    WG_ALLOC(c, occ, (nch * 16 + 16) * run.nw);
     WG_ALLOC(c, stats, nch * 8 + 8);
     WG_ALLOC(c, rflags, (run.max_iters + 2) * 4);
     run.ev = evrec.as<const uint4>();
     run.aux = aux.as<const uint32_t>();
-    run.slots_a = slot_a.as<uint8_t>();
-    run.slots_b = slot_b.as<uint8_t>();
+    run.slots_a = slot_a.as<uint16_t>();
+    run.slots_b = slot_b.as<uint16_t>();
     run.occ_a = occ.as<unsigned long long>();
-    run.occ_b = occ.as<unsigned long long>() + nch;
+    run.occ_b = occ.as<unsigned long long>() + nch * run.nw;
     run.stats = stats.as<uint32_t>();
     run.flags = rflags.as<uint32_t>();
     run.scal = c->lane_scalars.as<uint32_t>();
@@ -667,8 +705,8 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
 }
 
 // The speculative lane build's validation words (WG_LANES_SPEC_ITEMS): {not
-// well formed, events, aux words, max_lane, slots, > 63 slots, changed at
-// it - 1, changed at it, first iteration that changed nothing}.
+// well formed, events, aux words, max_lane, slots, past the occupancy width,
+// changed at it - 1, changed at it, first iteration that changed nothing}.
 int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
     const uint64_t n = c->n;
     const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
@@ -686,7 +724,7 @@ int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
 }
 
 // Validation of a speculative lane build from those words: true = the lanes
-// are the greedy's (well formed, a fixed point, <= 63 slots); c->max_lane,
+// are the greedy's (well formed, a fixed point, within the width); c->max_lane,
 // n_slots, n_events, the replay's blind count are updated.
 bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v) {
     const bool conv = v[6] == 0 || v[7] == 0;
@@ -694,6 +732,7 @@ bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v) {
     c->n_events = v[1];
     c->max_lane = (uint32_t)v[3];
     c->n_slots = (uint32_t)v[4];
+    c->replay_nw = wg_ctx::nw_for_slots(c->n_slots);
     c->replay_iters = c->spec_run.it;
     c->replay_adapt((uint32_t)v[8]);   // blind count and chunk size from the iterations it took
     c->lane_path = 0;
@@ -712,6 +751,8 @@ int wg_lanes_fast(wg_ctx *c, bool *used, bool spec) {
     R.poff = c->d_poff;
     R.prow = c->prow.as<const int32_t>();
     R.canon = c->canon.as<const uint32_t>();
+    WG_ALLOC(c, c->lf[LF_LFIRST], c->n * 8 + 8);
+    R.lfirst = c->lf[LF_LFIRST].as<unsigned long long>();   // parents at earlier rows stay on this path
     c->e_refs_own = c->e_refs;
     if (spec) {
         const int rc = lanes_fast_spec(c, R);

@@ -77,9 +77,9 @@ struct ReplayArgs {
     uint32_t iter;              // iteration index (>= 1)
     const uint4 *ev;            // records, padded with >= 256 zero records
     const uint32_t *aux;        // token lists of merges with more than two waiters
-    const uint8_t *slot_prev;   // iteration i-1
-    uint8_t *slot_next;         // iteration i
-    const unsigned long long *occ_prev;  // exit occupancy per chunk, iteration i-1
+    const uint16_t *slot_prev;  // iteration i-1
+    uint16_t *slot_next;        // iteration i
+    const unsigned long long *occ_prev;  // exit occupancy per chunk (NW words each), iteration i-1
     unsigned long long *occ_next;
     uint32_t *chunk_stats;      // per chunk: max_lane, max_slot
     uint32_t *changed;          // [iter] = 1 if iteration iter changed anything
@@ -87,13 +87,114 @@ struct ReplayArgs {
     const uint32_t *gate;       // speculative build: nonzero = the list is not well formed, replay nothing
 };
 
+// The occupancy of up to 64*NW - 1 slots (active_lanes, commit_graph.rs:414-423
+// grows without bound; the last bit is the overflow sentinel) as NW 64-bit
+// words.  Words are only ever indexed by compile-time constants (unrolled
+// loops with a compare), so the mask stays in registers.  NW = 1 is the
+// common case and compiles to the single-word code.
+template <int NW>
+struct Occ {
+    uint64_t w[NW];
+    __device__ __forceinline__ static Occ fill(uint64_t v) {
+        Occ m;
+#pragma unroll
+        for (int k = 0; k < NW; k++) m.w[k] = v;
+        return m;
+    }
+    __device__ __forceinline__ static Occ bit(uint32_t s) {
+        s &= 64u * NW - 1u;
+        Occ m;
+#pragma unroll
+        for (int k = 0; k < NW; k++) m.w[k] = ((s >> 6) == (uint32_t)k) ? 1ull << (s & 63u) : 0ull;
+        return m;
+    }
+    __device__ __forceinline__ Occ operator&(const Occ &o) const {
+        Occ m;
+#pragma unroll
+        for (int k = 0; k < NW; k++) m.w[k] = w[k] & o.w[k];
+        return m;
+    }
+    __device__ __forceinline__ Occ operator|(const Occ &o) const {
+        Occ m;
+#pragma unroll
+        for (int k = 0; k < NW; k++) m.w[k] = w[k] | o.w[k];
+        return m;
+    }
+    __device__ __forceinline__ Occ operator~() const {
+        Occ m;
+#pragma unroll
+        for (int k = 0; k < NW; k++) m.w[k] = ~w[k];
+        return m;
+    }
+    __device__ __forceinline__ bool any() const {
+        uint64_t a = 0;
+#pragma unroll
+        for (int k = 0; k < NW; k++) a |= w[k];
+        return a != 0;
+    }
+    __device__ __forceinline__ bool operator!=(const Occ &o) const {
+        uint64_t a = 0;
+#pragma unroll
+        for (int k = 0; k < NW; k++) a |= w[k] ^ o.w[k];
+        return a != 0;
+    }
+    // lowest_free_lane (:414-423): the lowest clear bit; the sentinel (last
+    // bit) is never reported free, so a full table reports 64*NW - 1
+    __device__ __forceinline__ uint32_t lowest_free() const {
+        uint32_t r = 64u * NW - 1u;
+#pragma unroll
+        for (int k = NW - 1; k >= 0; k--) {
+            const uint64_t f = ~w[k] | (k == NW - 1 ? 1ull << 63 : 0ull);
+            if (f) r = 64u * k + (uint32_t)__builtin_ctzll(f);
+        }
+        return r;
+    }
+    // highest set bit, 0 for an empty mask
+    __device__ __forceinline__ uint32_t highest() const {
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < NW; k++)
+            if (w[k]) r = 64u * k + 63u - (uint32_t)__builtin_clzll(w[k]);
+        return r;
+    }
+    __device__ __forceinline__ Occ shfl_up(int d) const {
+        Occ m;
+#pragma unroll
+        for (int k = 0; k < NW; k++) m.w[k] = shfl_up64(w[k], d);
+        return m;
+    }
+    __device__ __forceinline__ Occ readlane(uint32_t lane) const {
+        Occ m;
+#pragma unroll
+        for (int k = 0; k < NW; k++) m.w[k] = rl64(w[k], lane);
+        return m;
+    }
+    __device__ __forceinline__ Occ xor_or_reduce() const {   // OR over the wave
+        Occ m = *this;
+        for (int d = 32; d >= 1; d >>= 1)
+#pragma unroll
+            for (int k = 0; k < NW; k++)
+                m.w[k] |= ((uint64_t)(uint32_t)__shfl_xor((int)(m.w[k] >> 32), d, 64) << 32) |
+                          (uint32_t)__shfl_xor((int)(uint32_t)m.w[k], d, 64);
+        return m;
+    }
+    __device__ __forceinline__ static Occ load_uniform(const unsigned long long *p) {
+        Occ m;
+#pragma unroll
+        for (int k = 0; k < NW; k++) m.w[k] = ufl64(p[k]);
+        return m;
+    }
+};
+
 // The chunk's own slots of this iteration, mirrored in LDS: a batch reads the
 // slots of tokens born in the chunk's earlier batches right after the wave
 // stored them, which through global memory costs a full round trip per batch.
 constexpr uint32_t LSLOT_MAX = 4096;   // chunks up to this many events (WG_OPT_REPLAY_CHUNK)
 
+template <int NW>
 __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
-    __shared__ uint8_t lslot[LSLOT_MAX];
+    using M = Occ<NW>;
+    __shared__ uint16_t lslot[LSLOT_MAX];
     const uint32_t lid = threadIdx.x & 63;
     if (A.changed[A.iter - 1] == 0) return;          // previous iteration was a fixed point
     if (A.gate && *A.gate) return;
@@ -109,8 +210,8 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
 #endif
     // slot of a token born in this chunk before the current batch (this iteration)
     auto own = [&](uint64_t t) -> uint32_t { return lds ? (uint32_t)lslot[t - e0] : (uint32_t)A.slot_next[t]; };
-    uint64_t occ = c == 0 ? 0ull : ufl64(A.occ_prev[c - 1]);
-    uint64_t occ_or = 0, alloc_or = 0;   // OR of the occupancy after each occupying allocation / of allocated slots
+    M occ = c == 0 ? M::fill(0ull) : M::load_uniform(A.occ_prev + (c - 1) * NW);
+    M occ_or = M::fill(0ull), alloc_or = M::fill(0ull);   // OR of the occupancy after each occupying allocation / of allocated slots
     bool diff = false;
     uint32_t prev_v = 0;
     const uint4 *ev = A.ev;
@@ -120,7 +221,7 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
     // the previous iteration's slot of every event: the guess of the batch's
     // speculative replay and the reference of the change check
     uint32_t gp_v = (e0 + lid < e1) ? A.slot_prev[e0 + lid] : 0u;
-    uint64_t occ_or_v = 0, alloc_or_v = 0;   // per-lane parts of max_lane / max_s
+    M occ_or_v = M::fill(0ull), alloc_or_v = M::fill(0ull);   // per-lane parts of max_lane / max_s
     // old tokens of the first batch: all born before e0 -> iteration i-1
     if ((rec.x & F_C) && (uint64_t)rec.y < e0) q0_v = A.slot_prev[rec.y];
     if ((rec.x & F_C) && (uint64_t)rec.z < e0) q1_v = A.slot_prev[rec.z];
@@ -146,17 +247,17 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         const bool isC = f_v & F_C;
         const bool special = (f_v & F_A) || (f_v & (F_IN0 | F_IN1 | F_M)) != 0;
         const uint32_t smin = s0 < s1 ? s0 : s1;
-        uint64_t tokbits = (1ull << (s0 & 63u)) | (1ull << (s1 & 63u));
-        if (f_v & F_O) tokbits &= ~(1ull << (smin & 63u));   // MIN keep: the minimum stays occupied
-        const uint64_t amask = (isC && !special) ? ~tokbits : ~0ull;
+        M tokbits = M::bit(s0) | M::bit(s1);
+        if (f_v & F_O) tokbits = tokbits & ~M::bit(smin);   // MIN keep: the minimum stays occupied
+        const M amask = (isC && !special) ? ~tokbits : M::fill(~0ull);
         uint32_t cur_v = (isC && !special) ? smin : 0u;
         // segmented inclusive AND-scan: a segment starts right after each special lane
-        uint64_t q = amask;
+        M q = amask;
         uint32_t st = (lid == 0 || __shfl_up((int)special, 1, 64)) ? 1u : 0u;
         for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t qo = shfl_up64(q, d);
+            const M qo = q.shfl_up(d);
             const uint32_t so = (uint32_t)__shfl_up((int)st, d, 64);
-            if (lid >= (uint32_t)d && !st) { q &= qo; st |= so; }
+            if (lid >= (uint32_t)d && !st) { q = q & qo; st |= so; }
         }
         const uint64_t sm = __ballot(special);
         uint64_t smask = sm;
@@ -181,7 +282,8 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
             const bool clrS = isC && special && !isA;
             const uint32_t src0 = (f_v >> 8) & 63u, src1 = (f_v >> 16) & 63u;
             uint32_t g = special ? gp_v : cur_v;
-            uint64_t ob = occ, oa = occ, mism = ~0ull;
+            M ob = occ, oa = occ;
+            uint64_t mism = ~0ull;
             uint32_t lim_prev = 0;
             for (int it = 0; it < JMAX && mism; it++) {
                 if (it > 0) {   // progress of the last pass: lanes [0, lim) are exact
@@ -193,45 +295,45 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
                 const uint32_t gb = (uint32_t)__shfl((int)g, (int)src1, 64);
                 const uint32_t a = (f_v & F_IN0) ? ga : s0, b = (f_v & F_IN1) ? gb : s1;
                 const uint32_t m = a < b ? a : b;
-                uint64_t Am = amask, Om = 0;
-                if (isA) { Am = ~0ull; Om = occupy ? 1ull << (g & 63u) : 0ull; }
-                else if (clrS) { Am = ~((1ull << (a & 63u)) | (1ull << (b & 63u))); Om = occupy ? 1ull << (m & 63u) : 0ull; }
+                M Am = amask, Om = M::fill(0ull);
+                if (isA) { Am = M::fill(~0ull); Om = occupy ? M::bit(g) : M::fill(0ull); }
+                else if (clrS) { Am = ~(M::bit(a) | M::bit(b)); Om = occupy ? M::bit(m) : M::fill(0ull); }
                 for (int d = 1; d < 64; d <<= 1) {   // inclusive scan of the maps, in event order
-                    const uint64_t Ap = shfl_up64(Am, d), Op = shfl_up64(Om, d);
+                    const M Ap = Am.shfl_up(d), Op = Om.shfl_up(d);
                     if (lid >= (uint32_t)d) { Om = (Op & Am) | Om; Am = Ap & Am; }
                 }
                 oa = (occ & Am) | Om;
-                ob = shfl_up64(oa, 1);
+                ob = oa.shfl_up(1);
                 if (lid == 0) ob = occ;
-                const uint32_t ng = isA ? (uint32_t)__builtin_ctzll(~ob | (1ull << 63)) : (clrS ? m : cur_v);
+                const uint32_t ng = isA ? ob.lowest_free() : (clrS ? m : cur_v);
                 mism = __ballot(ng != g);   // lanes before the first mismatch kept their (exact) slot and oa
                 g = ng;
             }
             // lanes [0, lim) are exact (and lane lim's slot, from an exact occupancy)
             const uint32_t lim = mism ? (uint32_t)__builtin_ctzll(mism) : 64u;
             if (lid < lim) {
-                if (isA && occupy) occ_or_v |= oa;
-                if (isA) alloc_or_v |= 1ull << (g & 63u);
+                if (isA && occupy) occ_or_v = occ_or_v | oa;
+                if (isA) alloc_or_v = alloc_or_v | M::bit(g);
             }
             if (!mism) {
                 cur_v = g;
-                occ = rl64(oa, 63);
+                occ = oa.readlane(63);
                 smask = 0;                                   // the scan already covered every event
             } else {
                 cur_v = (lid <= lim) ? g : cur_v;
-                occ = rl64(ob, lim);                          // exact occupancy before event lim
+                occ = ob.readlane(lim);                       // exact occupancy before event lim
                 smask = sm & (~0ull << lim);
-                const uint64_t bit = 1ull << (rl(g, lim) & 63u);
+                const M bit = M::bit(rl(g, lim));
                 const uint32_t fl = rl(f_v, lim);
                 if (fl & F_A) {                              // event lim itself is exact: apply it
-                    alloc_or |= bit;
-                    if (fl & F_O) { occ |= bit; occ_or |= occ; }
+                    alloc_or = alloc_or | bit;
+                    if (fl & F_O) { occ = occ | bit; occ_or = occ_or | occ; }
                 } else {
                     const uint32_t pk = rl(s0, lim), pk1 = rl(s1, lim);
                     const uint32_t a = (fl & F_IN0) ? rl(cur_v, (fl >> 8) & 63u) : pk;
                     const uint32_t b = (fl & F_IN1) ? rl(cur_v, (fl >> 16) & 63u) : pk1;
-                    occ &= ~((1ull << (a & 63u)) | (1ull << (b & 63u)));
-                    if (fl & F_O) occ |= bit;
+                    occ = occ & ~(M::bit(a) | M::bit(b));
+                    if (fl & F_O) occ = occ | bit;
                 }
                 smask &= smask - 1;                          // continue after event lim
             }
@@ -248,22 +350,22 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
 #endif
             const uint32_t k = (uint32_t)__builtin_ctzll(smask);
             smask &= smask - 1;
-            occ &= rl64(q, k);                                  // the folded run before event k
+            occ = occ & q.readlane(k);                          // the folded run before event k
             const uint32_t f = rl(f_v, k);
             uint32_t s;
             if (f & F_A) {
-                s = (uint32_t)__builtin_ctzll(~occ | (1ull << 63));
-                alloc_or |= 1ull << s;
+                s = occ.lowest_free();
+                alloc_or = alloc_or | M::bit(s);
                 if (f & F_O) {
-                    occ |= 1ull << s;
-                    occ_or |= occ;
+                    occ = occ | M::bit(s);
+                    occ_or = occ_or | occ;
                 }
             } else {
                 // tokens born in this batch, or more than two waiters
                 uint32_t a = rl(s0, k), b = rl(s1, k);
                 if (f & F_IN0) a = rl(cur_v, (f >> 8) & 63u);
                 if (f & F_IN1) b = rl(cur_v, (f >> 16) & 63u);
-                uint64_t clr = (1ull << (a & 63u)) | (1ull << (b & 63u));
+                M clr = M::bit(a) | M::bit(b);
                 uint32_t m = a < b ? a : b;
                 if (f & F_M) {
 #ifdef WG_REPLAY_PROFILE
@@ -278,15 +380,15 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
                         if (t >= base) ts = rl(cur_v, (uint32_t)(t - base));
                         else if (have_prev && t >= pbase) ts = rl(prev_v, (uint32_t)(t - pbase));
                         else ts = ufl(t < e0 ? A.slot_prev[t] : own(t));
-                        clr |= 1ull << (ts & 63u);
+                        clr = clr | M::bit(ts);
                         m = ts < m ? ts : m;
                     }
 #ifdef WG_REPLAY_PROFILE
                     rp_cfm += clock64() - rp_m0;
 #endif
                 }
-                occ &= ~clr;
-                if (f & F_O) occ |= 1ull << (m & 63u);
+                occ = occ & ~clr;
+                if (f & F_O) occ = occ | M::bit(m);
                 s = m;
             }
             cur_v = (lid == k) ? s : cur_v;
@@ -295,9 +397,9 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         rp_cs += clock64() - rp_s0;
 #endif
         // the run after the last special event
-        occ &= (sm >> 63) ? ~0ull : rl64(q, 63);
+        if (!(sm >> 63)) occ = occ & q.readlane(63);
         if (base + lid < e1) {
-            const uint8_t nv = (uint8_t)cur_v;
+            const uint16_t nv = (uint16_t)cur_v;
             diff |= gp_v != nv;
             A.slot_next[base + lid] = nv;
             if (lds) lslot[base - e0 + lid] = nv;
@@ -312,20 +414,22 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         q0_v = n0_v;
         q1_v = n1_v;
     }
-    for (int d = 32; d >= 1; d >>= 1) {
-        occ_or_v |= ((uint64_t)(uint32_t)__shfl_xor((int)(occ_or_v >> 32), d, 64) << 32) |
-                    (uint32_t)__shfl_xor((int)(uint32_t)occ_or_v, d, 64);
-        alloc_or_v |= ((uint64_t)(uint32_t)__shfl_xor((int)(alloc_or_v >> 32), d, 64) << 32) |
-                      (uint32_t)__shfl_xor((int)(uint32_t)alloc_or_v, d, 64);
+    occ_or = occ_or | occ_or_v.xor_or_reduce();
+    alloc_or = alloc_or | alloc_or_v.xor_or_reduce();
+    bool occ_changed = false;
+    if (lid < (uint32_t)NW) {
+        uint64_t w = 0;
+#pragma unroll
+        for (int k = 0; k < NW; k++)
+            if ((uint32_t)k == lid) w = occ.w[k];
+        A.occ_next[c * NW + lid] = w;
+        occ_changed = w != A.occ_prev[c * NW + lid];
     }
-    occ_or |= occ_or_v;
-    alloc_or |= alloc_or_v;
     if (lid == 0) {
-        A.occ_next[c] = occ;
-        A.chunk_stats[2 * c] = occ_or ? 63u - (uint32_t)__builtin_clzll(occ_or) : 0u;         // max_lane
-        A.chunk_stats[2 * c + 1] = alloc_or ? 63u - (uint32_t)__builtin_clzll(alloc_or) : 0u; // max slot
+        A.chunk_stats[2 * c] = occ_or.highest();          // max_lane
+        A.chunk_stats[2 * c + 1] = alloc_or.highest();    // max slot
     }
-    if (__any(diff) || (lid == 0 && occ != A.occ_prev[c])) A.changed[A.iter] = 1u;
+    if (__any(diff) || occ_changed) A.changed[A.iter] = 1u;
 #ifdef WG_REPLAY_PROFILE
     if (lid == 0) {
         RP_ADD(0, 1); RP_ADD(1, rp_batches); RP_ADD(2, rp_fast); RP_ADD(3, rp_sev); RP_ADD(4, rp_fm);
@@ -336,7 +440,7 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
 
 __global__ void k_lf_replay_init(uint64_t nchunks, unsigned long long *occ_prev, uint32_t *changed, uint32_t nflags) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nchunks) occ_prev[i] = 0ull;    // initial guess (any guess is sound)
+    if (i < nchunks) occ_prev[i] = 0ull;    // initial guess (any guess is sound); nchunks counts words
     if (i < nflags) changed[i] = (i == 0) ? 1u : 0u;
 }
 
@@ -347,7 +451,7 @@ __global__ void k_lf_replay_init_spec(uint64_t nchunks, unsigned long long *occ_
                                       uint4 *__restrict__ slots16, uint64_t nslots16, uint4 *__restrict__ ev,
                                       const uint32_t *__restrict__ nev_dev) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nchunks) occ_prev[i] = 0ull;
+    if (i < nchunks) occ_prev[i] = 0ull;   // nchunks counts words
     if (i < nflags) changed[i] = (i == 0) ? 1u : 0u;
     if (i < nslots16) slots16[i] = make_uint4(0u, 0u, 0u, 0u);
     if (i < 256) ev[*nev_dev + i] = make_uint4(0u, 0u, 0u, 0u);
@@ -358,7 +462,7 @@ __global__ void k_lf_replay_init_spec(uint64_t nchunks, unsigned long long *occ_
 // scal[3]: the first of iterations 1..iters that changed nothing (0: none) —
 // the iterations the next build launches before its first check
 __global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats, uint32_t *__restrict__ scal,
-                                   const uint32_t *__restrict__ flags, uint32_t iters,
+                                   const uint32_t *__restrict__ flags, uint32_t iters, uint32_t slot_cap,
                                    const uint32_t *__restrict__ nev_dev = nullptr, uint32_t chunk = 1) {
     uint32_t fp = ~0u;
     for (uint32_t i = 1 + threadIdx.x; i <= iters; i += blockDim.x)
@@ -385,11 +489,18 @@ __global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict_
     if (threadIdx.x == 0) {
         scal[0] = ml;
         scal[1] = ms + 1;
-        scal[2] = ms >= 63 ? 1u : 0u;
+        scal[2] = ms >= slot_cap ? 1u : 0u;   // the sentinel slot was handed out: the occupancy overflowed
     }
 }
 
 }  // namespace
+
+// one iteration at the run's occupancy width (R.nw words: up to 64 R.nw - 1 slots)
+static void launch_replay(const ReplayRun &R, const ReplayArgs &a, hipStream_t s) {
+    if (R.nw <= 1) hipLaunchKernelGGL(k_lf_replay<1>, dim3(R.nch), dim3(64), 0, s, a);
+    else if (R.nw <= 4) hipLaunchKernelGGL(k_lf_replay<4>, dim3(R.nch), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_lf_replay<16>, dim3(R.nch), dim3(64), 0, s, a);
+}
 
 // Replay driver.  wg_replay_start initialises and launches `blind` iterations
 // without looking at the device (a fixed point found early makes the rest
@@ -406,24 +517,28 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
     R.on = R.occ_b;
     if (R.max_iters > R.nch + 1) R.max_iters = (uint32_t)(R.nch + 1);
     if (R.nev == 0) {
-        hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, (uint64_t)0, R.stats, R.scal, (const uint32_t *)R.flags, 0u);
+        hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, (uint64_t)0, R.stats, R.scal, (const uint32_t *)R.flags, 0u,
+                           64u * R.nw - 1u);
         return hipGetLastError();
     }
     const uint64_t ninit = R.nch > R.max_iters + 1 ? R.nch : R.max_iters + 1;
-    hipLaunchKernelGGL(k_lf_replay_init, dim3((ninit + 255) / 256), dim3(256), 0, s, R.nch, R.occ_a, R.flags, R.max_iters + 1);
-    hipError_t e = hipMemsetAsync(R.slots_a, 0, R.nev, s);
+    const uint64_t ninit_w = ninit > R.nch * R.nw ? ninit : R.nch * R.nw;
+    hipLaunchKernelGGL(k_lf_replay_init, dim3((ninit_w + 255) / 256), dim3(256), 0, s, R.nch * R.nw, R.occ_a, R.flags,
+                       R.max_iters + 1);
+    hipError_t e = hipMemsetAsync(R.slots_a, 0, R.nev * sizeof(uint16_t), s);
     if (e != hipSuccess) return e;
     if (blind > R.max_iters) blind = R.max_iters;
     for (uint32_t k = 0; k < blind; k++) {
         R.it++;
         ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr};
-        hipLaunchKernelGGL(k_lf_replay, dim3(R.nch), dim3(64), 0, s, a);
+        launch_replay(R, a, s);
         // after a fixed point later iterations do nothing; the converged slots are
         // in both buffers, so either pointer is final
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);
     }
-    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it);
+    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it,
+                       64u * R.nw - 1u);
     return hipGetLastError();
 }
 
@@ -440,22 +555,23 @@ hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t
     R.on = R.occ_b;
     if (R.max_iters > R.nch + 1) R.max_iters = (uint32_t)(R.nch + 1);
     if (blind > R.max_iters) blind = R.max_iters;
-    const uint64_t nslots16 = (R.nev + 15) / 16;
+    const uint64_t nslots16 = (R.nev * sizeof(uint16_t) + 15) / 16;
     uint64_t ninit = R.nch > R.max_iters + 1 ? R.nch : R.max_iters + 1;
     if (ninit < nslots16) ninit = nslots16;
+    if (ninit < R.nch * R.nw) ninit = R.nch * R.nw;
     if (ninit < 256) ninit = 256;
-    hipLaunchKernelGGL(k_lf_replay_init_spec, dim3((ninit + 255) / 256), dim3(256), 0, s, R.nch, R.occ_a, R.flags,
+    hipLaunchKernelGGL(k_lf_replay_init_spec, dim3((ninit + 255) / 256), dim3(256), 0, s, R.nch * R.nw, R.occ_a, R.flags,
                        R.max_iters + 1, reinterpret_cast<uint4 *>(R.slots_a), nslots16, ev_pad, R.nev_dev);
     for (uint32_t k = 0; k < blind; k++) {
         R.it++;
         ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, R.nev_dev,
                      R.gate};
-        hipLaunchKernelGGL(k_lf_replay, dim3(R.nch), dim3(64), 0, s, a);
+        launch_replay(R, a, s);
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);
     }
     hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it,
-                       R.nev_dev, R.chunk);
+                       64u * R.nw - 1u, R.nev_dev, R.chunk);
     return hipGetLastError();
 }
 
@@ -467,7 +583,7 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
     while (!*converged && R.it < R.max_iters) {
         R.it++;
         ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr};
-        hipLaunchKernelGGL(k_lf_replay, dim3(R.nch), dim3(64), 0, s, a);
+        launch_replay(R, a, s);
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);
         if (R.it == next_poll || R.it == R.max_iters) {
@@ -477,7 +593,9 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
             *converged = fl[0] == 0 || fl[1] == 0;
         }
     }
-    if (R.nev) hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it);
+    if (R.nev)
+        hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it,
+                           64u * R.nw - 1u);
     return hipGetLastError();
 }
 

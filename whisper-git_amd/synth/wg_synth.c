@@ -17,6 +17,17 @@
  *                    parents at earlier rows (clock skew / orphans,
  *                    git/mod.rs:767-772), parents outside the list,
  *                    repeated parents, self-parents, octopus merges.
+ *   WGS_SKEW         the LINUX shape as commit_graph_with_orphans delivers
+ *                    it (git/mod.rs:761-775): ~1e-4 of the commits carry a
+ *                    committer time moved forward by 1 h .. 30 days (clock
+ *                    skew), 100 reflog orphans (short chains off random
+ *                    commits, is_orphaned) are appended and the whole list is
+ *                    stable-sorted by time, newest first — so every child
+ *                    older than a skewed parent now sits BELOW it (a parent
+ *                    at an earlier row), and each such reference holds a lane
+ *                    slot for the rest of the list (commit_graph.rs:414-423).
+ *   WGS_LINUXWIDE    the LINUX shape with up to 160 concurrently active lines
+ *                    (more than 100 concurrent lanes).
  */
 #include <math.h>
 #include <stdint.h>
@@ -44,6 +55,9 @@ int wgs_preset(int kind, uint64_t n, uint64_t seed, wgs_params *p) {
     case WGS_RANDOM13: p->max_lines = 8;  p->p_merge = 0.30; p->p_newtip = 0.06; p->p_fork = 0.10; p->main_weight = 2.0; p->p_feature = 0.3; break;
     case WGS_LINUX:    p->max_lines = 28; p->p_merge = 0.07; p->p_newtip = 0.02; p->p_fork = 0.04; p->p_octopus = 0.002; p->main_weight = 3.0; p->p_feature = 0.5; break;
     case WGS_WIDE16:   p->max_lines = 10; p->p_merge = 0.10; p->p_newtip = 0.01; p->p_fork = 0.03; p->main_weight = 2.0; p->p_feature = 0.3; break;
+    case WGS_SKEW:     p->max_lines = 28; p->p_merge = 0.07; p->p_newtip = 0.02; p->p_fork = 0.04; p->p_octopus = 0.002; p->main_weight = 3.0; p->p_feature = 0.5;
+                       p->p_clock_skew = 1e-4; p->n_orphans = n >= 1000 ? 100 : n / 10; break;
+    case WGS_LINUXWIDE: p->max_lines = 160; p->p_merge = 0.07; p->p_newtip = 0.03; p->p_fork = 0.02; p->p_octopus = 0.002; p->main_weight = 3.0; p->p_feature = 0.5; break;
     case WGS_ANOMALY:  p->max_lines = 9;  p->p_merge = 0.25; p->p_newtip = 0.10; p->p_fork = 0.08; p->p_octopus = 0.05;
                        p->p_dup_oid = 0.03; p->p_skew = 0.04; p->p_external = 0.05; p->p_self = 0.01;
                        p->p_dup_parent = 0.03; p->p_orphan_flag = 0.05; p->band_frac = 0.1; p->truncated = 1; p->p_feature = 0.3; break;
@@ -77,7 +91,24 @@ void wgs_free(wgs_dag *d) {
     free(d->flags); free(d->band); free(d);
 }
 
+static int orphans_and_time_sort(wgs_dag *d, const wgs_params *p, uint64_t *rs);
+
 wgs_dag *wgs_generate(const wgs_params *p) {
+    if (p->n_orphans > 0 || p->p_clock_skew > 0) {
+        /* the revwalk list (n - n_orphans rows), then the reflog orphans */
+        wgs_params b = *p;
+        const uint64_t no = p->n_orphans < p->n ? p->n_orphans : p->n;
+        b.n = p->n - no;
+        b.n_orphans = 0;
+        b.p_clock_skew = 0;
+        wgs_dag *d = wgs_generate(&b);
+        if (!d) return NULL;
+        uint64_t rs = p->seed * 0xD1B54A32D192ED03ull + 0x0125ull;
+        b.n_orphans = no;
+        b.p_clock_skew = p->p_clock_skew;
+        if (orphans_and_time_sort(d, &b, &rs)) { wgs_free(d); return NULL; }
+        return d;
+    }
     const uint64_t n = p->n;
     uint64_t rs = p->seed * 0x2545F4914F6CDD1Dull + 0x5EEDull;
     wgs_dag *d = (wgs_dag *)calloc(1, sizeof(wgs_dag));
@@ -261,4 +292,107 @@ void wgs_copy(const wgs_dag *d, uint8_t *oid, int64_t *time, uint32_t *parent_of
     if (parent_oid) memcpy(parent_oid, d->parent_oid, d->e * 20);
     if (flags) memcpy(flags, d->flags, d->n);
     if (band) memcpy(band, d->band, d->n * sizeof(float));
+}
+
+/* WGS_SKEW's second half (git/mod.rs:761-775 on a skewed history):
+ * clock skew on the walk rows, the reflog orphans appended (newest first,
+ * git/mod.rs:748-751), then a stable sort of the whole list by time desc. */
+typedef struct { int64_t t; uint64_t row; } tkey;
+static int tkey_cmp(const void *a, const void *b) {
+    const tkey *x = (const tkey *)a, *y = (const tkey *)b;
+    if (x->t != y->t) return x->t > y->t ? -1 : 1;   /* Reverse(time) */
+    return x->row < y->row ? -1 : (x->row > y->row);   /* stable */
+}
+
+static int orphans_and_time_sort(wgs_dag *d, const wgs_params *p, uint64_t *rs) {
+    const uint64_t nw = d->n, no = p->n_orphans, n = nw + no;
+    /* clock skew: committer time moved forward by 1 h .. 30 days */
+    for (uint64_t i = 0; i < nw; i++)
+        if (urand(rs) < p->p_clock_skew) {
+            double lg = log(3600.0) + urand(rs) * (log(2592000.0) - log(3600.0));
+            d->time[i] += (int64_t)exp(lg);
+        }
+    /* orphans: chains of 1-8 commits, the oldest one's parent a walk row,
+     * each newer than its parent by 1 min .. 2 days */
+    uint8_t *oid = (uint8_t *)malloc(n * 20);
+    int64_t *time = (int64_t *)malloc(n * sizeof(int64_t));
+    uint8_t *flags = (uint8_t *)calloc(n, 1);
+    float *band = (float *)calloc(n, sizeof(float));
+    uint32_t *poff = (uint32_t *)malloc((n + 1) * sizeof(uint32_t));
+    uint8_t *poid = (uint8_t *)malloc((d->e + no + 1) * 20);
+    tkey *key = (tkey *)malloc(n * sizeof(tkey));
+    uint64_t *src = (uint64_t *)malloc(n * sizeof(uint64_t));   /* source row per orphan-extended row */
+    int64_t *opar = (int64_t *)malloc((no + 1) * sizeof(int64_t)); /* orphan parent: walk row or -(1 + orphan) */
+    if (!oid || !time || !flags || !band || !poff || !poid || !key || !src || !opar) goto fail;
+    memcpy(oid, d->oid, nw * 20);
+    memcpy(time, d->time, nw * sizeof(int64_t));
+    memcpy(flags, d->flags, nw);
+    memcpy(band, d->band, nw * sizeof(float));
+    {
+        /* generated oldest first inside a chain, then listed newest first */
+        uint64_t k = 0;
+        while (k < no) {
+            uint64_t len = 1 + urange(rs, 8);
+            if (len > no - k) len = no - k;
+            const uint64_t base = nw ? urange(rs, nw) : 0;
+            int64_t t = nw ? d->time[base] : 1704067200;
+            for (uint64_t j = 0; j < len; j++) {
+                const uint64_t o = nw + k + j;
+                for (int b = 0; b < 20; b += 8) {
+                    uint64_t r = sm64(rs);
+                    memcpy(oid + o * 20 + b, &r, (b + 8 <= 20) ? 8 : 4);
+                }
+                double lg = log(60.0) + urand(rs) * (log(172800.0) - log(60.0));
+                t += (int64_t)exp(lg);
+                time[o] = t;
+                flags[o] = 1;   /* is_orphaned */
+                opar[k + j] = j == 0 ? (nw ? (int64_t)base : INT64_MIN) : -(int64_t)(k + j);   /* previous orphan */
+            }
+            k += len;
+        }
+    }
+    for (uint64_t i = 0; i < n; i++) { key[i].t = time[i]; key[i].row = i; }
+    qsort(key, n, sizeof(tkey), tkey_cmp);
+    {
+        uint64_t e = 0;
+        for (uint64_t r = 0; r < n; r++) {
+            const uint64_t i = key[r].row;
+            src[r] = i;
+            poff[r] = (uint32_t)e;
+            if (i < nw) {
+                const uint64_t pa = d->parent_off[i], pb = d->parent_off[i + 1];
+                memcpy(poid + e * 20, d->parent_oid + pa * 20, (pb - pa) * 20);
+                e += pb - pa;
+            } else {
+                const int64_t q = opar[i - nw];
+                if (q == INT64_MIN) continue;
+                const uint64_t pr = q >= 0 ? (uint64_t)q : nw + (uint64_t)(-q - 1);
+                memcpy(poid + e * 20, oid + pr * 20, 20);
+                e++;
+            }
+        }
+        poff[n] = (uint32_t)e;
+        d->e = e;
+    }
+    {
+        uint8_t *oid2 = (uint8_t *)malloc(n * 20);
+        int64_t *time2 = (int64_t *)malloc(n * sizeof(int64_t));
+        uint8_t *flags2 = (uint8_t *)malloc(n);
+        float *band2 = (float *)malloc(n * sizeof(float));
+        if (!oid2 || !time2 || !flags2 || !band2) { free(oid2); free(time2); free(flags2); free(band2); goto fail; }
+        for (uint64_t r = 0; r < n; r++) {
+            memcpy(oid2 + r * 20, oid + src[r] * 20, 20);
+            time2[r] = time[src[r]];
+            flags2[r] = flags[src[r]];
+            band2[r] = band[src[r]];
+        }
+        free(d->oid); free(d->time); free(d->flags); free(d->band); free(d->parent_off); free(d->parent_oid);
+        d->oid = oid2; d->time = time2; d->flags = flags2; d->band = band2; d->parent_off = poff; d->parent_oid = poid;
+        d->n = n;
+    }
+    free(oid); free(time); free(flags); free(band); free(key); free(src); free(opar);
+    return 0;
+fail:
+    free(oid); free(time); free(flags); free(band); free(poff); free(poid); free(key); free(src); free(opar);
+    return -1;
 }

@@ -11,7 +11,7 @@
 extern "C" {
 #endif
 
-enum { WGS_LINEAR = 0, WGS_RANDOM13 = 1, WGS_LINUX = 2, WGS_WIDE16 = 3, WGS_ANOMALY = 4 };
+enum { WGS_LINEAR = 0, WGS_RANDOM13 = 1, WGS_LINUX = 2, WGS_WIDE16 = 3, WGS_ANOMALY = 4, WGS_SKEW = 5, WGS_LINUXWIDE = 6 };
 
 typedef struct wgs_params {
     int32_t  kind;
@@ -33,6 +33,9 @@ typedef struct wgs_params {
     int32_t  truncated;      /* unresolved first parents point outside    */
     int32_t  reserved;
     double   p_feature;      /* a merge's second parent starts a new line */
+    double   p_clock_skew;   /* a commit's time moved forward (1 h .. 30 d) */
+    uint64_t n_orphans;      /* reflog orphans appended, then the whole list
+                                stable-sorted by time desc (git/mod.rs:761-775) */
 } wgs_params;
 
 typedef struct wgs_dag {

@@ -2,7 +2,9 @@
 
 The generator itself is C (whisper-git_amd/synth/wg_synth.c).  Presets follow
 SURVEY.md §8(d): LINEAR (C1), RANDOM13 (C3), LINUX (C4), WIDE16 (C5) and
-ANOMALY (the edge cases GraphLayout::build tolerates).
+ANOMALY (the edge cases GraphLayout::build tolerates), SKEW (LINUX with clock
+skew and 100 reflog orphans, re-sorted by time as git/mod.rs:761-775 does)
+and LINUXWIDE (LINUX with more than 100 concurrent lanes).
 """
 from __future__ import annotations
 
@@ -12,8 +14,9 @@ from dataclasses import dataclass
 
 import numpy as np
 
-LINEAR, RANDOM13, LINUX, WIDE16, ANOMALY = 0, 1, 2, 3, 4
-PRESETS = {"linear": LINEAR, "random13": RANDOM13, "linux": LINUX, "wide16": WIDE16, "anomaly": ANOMALY}
+LINEAR, RANDOM13, LINUX, WIDE16, ANOMALY, SKEW, LINUXWIDE = 0, 1, 2, 3, 4, 5, 6
+PRESETS = {"linear": LINEAR, "random13": RANDOM13, "linux": LINUX, "wide16": WIDE16, "anomaly": ANOMALY,
+           "skew": SKEW, "linuxwide": LINUXWIDE}
 SEED_BASE = 0x5EED  # seed = 0x5EED + config id
 
 
@@ -27,7 +30,8 @@ class Params(ctypes.Structure):
                 ("p_self", ctypes.c_double), ("p_dup_parent", ctypes.c_double),
                 ("p_orphan_flag", ctypes.c_double), ("band_frac", ctypes.c_double),
                 ("truncated", ctypes.c_int32), ("reserved", ctypes.c_int32),
-                ("p_feature", ctypes.c_double)]
+                ("p_feature", ctypes.c_double), ("p_clock_skew", ctypes.c_double),
+                ("n_orphans", ctypes.c_uint64)]
 
 
 _lib = None
