@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "whisper-git_amd"))
 
 LISTS = [("wide16", 1_000_000, {}), ("linux", 1_300_000, {}), ("skew", 1_000_000, {}),
-         ("linuxwide", 1_000_000, {}), ("random13", 100_000, {}), ("anomaly", 1_000_000, {})]
+         ("linuxwide", 1_000_000, {}), ("random13", 100_000, {}), ("anomaly", 20_000, {"p_dup_oid": 0.0})]
 
 
 def main():
@@ -41,7 +41,9 @@ def main():
             for name, ms in eng.timings():
                 st[name] = st.get(name, 0.0) + ms / steps
             s = eng.layout_summary()
+            dc = eng.debug_counters()
             print(json.dumps({"list": kind, "rows": d.n, "forced_general": general, "lane_path": int(s.lane_path),
+                              "replay_iterations": int(dc[3]), "events": int(dc[4]),
                               "n_slots": int(s.n_slots), "max_lane": int(s.max_lane),
                               "lanes_ms": round(st.get("lanes", 0.0), 4), "build_wall_ms": round(wall, 4),
                               "stages_ms": {k: round(v, 4) for k, v in st.items()}}), flush=True)
