@@ -16,9 +16,12 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt \
             -Wall -Wno-unused-function -Iinclude -I$(CSRC)
 CXXFLAGS_HOST := -O2 -std=c++17 -fPIC -Wall -Wextra -Iinclude
-CFLAGS_ORACLE := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
+# The oracle doubles as bench.py's single-thread CPU baseline: -O3 with the
+# x86-64-v3 ISA (AVX2/BMI2), not -march=native — it is built in this container
+# and runs on the GPU box's host, whose CPU model differs.  No FMA contraction.
+CFLAGS_ORACLE := -O3 -march=x86-64-v3 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 
-all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgraph_host.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so \
+all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgraph_host.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so oracle/libedt_cpu.so \
      tests/cpp/test_graph_layout profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost
 
 $(PKG)/wgraph/libwgraph.so: $(HIPSRC) $(HIPHDR)
@@ -48,7 +51,11 @@ profiles/microbench/store_sweep: profiles/microbench/store_sweep.hip
 profiles/microbench/launch_cost: profiles/microbench/launch_cost.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Wno-unused-value -Wno-unused-result -o $@ $<
 
-oracle: oracle/liboracle.so
+# C2's CPU leg (bench.py): exact Felzenszwalb-Huttenlocher EDT, OpenMP
+oracle/libedt_cpu.so: oracle/edt_cpu.c
+	gcc $(CFLAGS_ORACLE) -fopenmp -shared -o $@ $< -lm
+
+oracle: oracle/liboracle.so oracle/libedt_cpu.so
 synth: $(PKG)/wgraph/libwgsynth.so
 engine: $(PKG)/wgraph/libwgraph.so
 host: $(PKG)/wgraph/libwgraph_host.so tests/cpp/test_graph_layout

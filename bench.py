@@ -11,8 +11,9 @@ DAG, each rank emits its contiguous 1M-row shard).
 Multi-GPU: every rank holds the whole N-million-row DAG in
 HBM and builds only its contiguous 1M-row shard (wg_shard_* C ABI): parent
 ids, crossing references, chain tokens and the lane-event stream are
-all-gathered over RCCL (torch.distributed "nccl" group) at six exchange
-points per step, then each rank emits its own rows' vertex buffers.
+all-gathered over RCCL (torch.distributed "nccl" group) at the exchange
+points of DESIGN.md §6 (five per step), then each rank emits its own rows'
+vertex buffers.
 Launched per the driver contract:
   python bench.py --gpus 1 --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -55,6 +56,29 @@ def parse():
     return ap.parse_args()
 
 
+def host_threads() -> int:
+    """Threads this process may use on the host (the GPU box gives a 16-CPU
+    share while os.cpu_count() reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def host_cpu() -> dict:
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "logical_cpus": os.cpu_count(), "threads_used_mt": host_threads()}
+
+
 def cpu_baseline(dag, rows, log, min_seconds=10.0, max_reps=4):
     """The CPU oracle (faithful single-thread restatement of commit_graph.rs)
     timed on this host over the first `rows` rows of the same workload; the
@@ -90,7 +114,7 @@ def cpu_baseline_threads(dag, rows, log, threads=None, min_seconds=5.0, max_reps
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, ROOT)
     from oracle import oracle_c   # baseline only
-    threads = threads or max(1, min(16, os.cpu_count() or 1))
+    threads = threads or host_threads()
     d = dag.slice_rows(min(rows, dag.n))
     total, reps = 0.0, 0
     with ThreadPoolExecutor(threads) as ex:
@@ -139,15 +163,25 @@ def extra_measurements(eng, dag, dev, torch, r0, r1, args, log):
              "gpu_ms": round(wall, 3), "gpu_kernel_ms": round(ev.get("font_atlas", 0.0), 4),
              "edt_ms": round(ev.get("font_edt", 0.0), 4), "coverage_ms": round(ev.get("font_coverage", 0.0), 4)}
     if not args.no_cpu:
+        # C2's CPU leg: an exact Felzenszwalb-Huttenlocher EDT in
+        # C (oracle/edt_cpu.c, OpenMP) over the same two coverages, 1 thread and
+        # all the threads this box gives us; its SDF bytes must equal the GPU's
         sys.path.insert(0, ROOT)
-        from oracle import font_oracle   # checker / baseline only
-        from wgraph import FONTS
-        t0 = time.perf_counter()
-        for slot in (0, 1):
-            font_oracle.build_atlas(FONTS[slot], **{k: v for k, v in abi.ATLAS_DEFAULTS.items()
-                                                    if k in ("width", "height", "em_px", "spread")})
-        atlas["cpu_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
-        atlas["cpu_kind"] = "port (numpy restatement, 1 thread)"
+        from oracle import edt_cpu   # baseline only
+        covs = [eng.atlas(slot) for slot in (0, 1)]
+        spread = int(abi.ATLAS_DEFAULTS["spread"])
+        mt = host_threads()
+        for label, th in (("cpu_edt_ms_1t", 1), ("cpu_edt_ms_mt", mt)):
+            edt_cpu.edt_sdf(covs[0]["cov"], spread, th)   # warm (pages, OpenMP pool)
+            reps_c = 5
+            t0 = time.perf_counter()
+            for _ in range(reps_c):
+                res = [edt_cpu.edt_sdf(a["cov"], spread, th) for a in covs]
+            atlas[label] = round((time.perf_counter() - t0) * 1e3 / reps_c, 2)
+        atlas["cpu_edt_threads_mt"] = mt
+        atlas["cpu_edt_sdf_equals_gpu"] = bool(all((r[2] == a["sdf"]).all() for r, a in zip(res, covs)))
+        atlas["cpu_kind"] = ("native C exact Felzenszwalb-Huttenlocher EDT + SDF bytes (oracle/edt_cpu.c, -O3), both "
+                             "fonts, from the GPU atlas's coverage; compare with edt_ms (the GPU's two EDT passes)")
     out["font_atlas"] = atlas
     # glyph quads over the rank's rows
     eng.row_geometry(dag.band)
@@ -228,6 +262,7 @@ def extra_measurements(eng, dag, dev, torch, r0, r1, args, log):
         order["cpu_kind"] = "port (Python stable sort + list inserts, 1 thread)"
     out["order"] = order
     out["frames"] = frame_rates(eng, dag, dev, torch, args)
+    out["builds"] = build_lifecycle(dag, dev, torch, args, np.ascontiguousarray(abi.DEFAULT_PALETTE))
     out["baseline_configs"] = config_rates(eng, dev, torch, args)
     log("extras:", json.dumps(out))
     return out
@@ -273,7 +308,27 @@ def config_rates(eng, dev, torch, args):
     buffer checksum equals the CPU oracle's in tests/test_gpu_parity.py)."""
     from wgraph import abi, synth
     res = {}
-    for cid, kind, n in (("C3", "random13", 100_000), ("C4", "linux", 1_300_000)):
+    # C1: the 10k-commit linear repo on the reference's CPU path (the oracle,
+    # 1 thread: build + row_geometry_with_bands + graph_cell emission; the
+    # headless screenshot_mode itself needs Vulkan + Rust), and the same step here
+    d1 = synth.generate("linear", 10_000)
+    c1 = {"workload": "linear synthetic repo, 10000 commits"}
+    if not args.no_cpu:
+        sys.path.insert(0, ROOT)
+        from oracle import oracle_c   # baseline only
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            o = oracle_c.OracleLayout(d1)
+            o.row_geometry(d1.band)
+            o.emit_vertices(0, d1.n, selected=7)
+            o.close()
+        cms = (time.perf_counter() - t0) * 1e3 / reps
+        c1.update({"cpu_ms_per_step": round(cms, 3), "cpu_rows_per_s": round(d1.n / cms * 1e3, 1), "cpu_cores": 1,
+                   "cpu_kind": "port (oracle/wg_oracle.c, 1 thread)"})
+    res["C1"] = c1
+    for cid, kind, n in (("C1", "linear", 10_000), ("C3", "random13", 100_000), ("C4", "linux", 1_300_000),
+                         ("skew", "skew", 1_000_000), ("linuxwide", "linuxwide", 1_000_000)):
         d = synth.generate(kind, n)
         keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
                                                        d.parent_oid.reshape(-1), d.flags, d.band)]
@@ -294,11 +349,72 @@ def config_rates(eng, dev, torch, args):
             step()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / args.steps
-        res[cid] = {"workload": f"{kind} synthetic DAG, {n} commits", "ms_per_step": round(ms, 4),
-                    "rows_per_s": round(n / ms * 1e3, 1), "vertices": int(eng.vertex_summary().n_vertices),
-                    "max_lane": int(eng.layout_summary().max_lane)}
+        ls = eng.layout_summary()
+        r = res.setdefault(cid, {})
+        if cid == "C1":
+            r.update({"gpu_ms_per_step": round(ms, 4), "gpu_rows_per_s": round(n / ms * 1e3, 1)})
+        else:
+            r.update({"workload": f"{kind} synthetic DAG, {n} commits", "ms_per_step": round(ms, 4),
+                      "rows_per_s": round(n / ms * 1e3, 1)})
+        r.update({"vertices": int(eng.vertex_summary().n_vertices), "max_lane": int(ls.max_lane),
+                  "n_slots": int(ls.n_slots), "lane_path": int(ls.lane_path)})
+        if cid == "skew":
+            r["note"] = ("LINUX shape + clock skew + 100 reflog orphans stable-sorted by time (git/mod.rs:761-775): "
+                         "parents at earlier rows, leaked slots")
+        if cid == "linuxwide":
+            r["note"] = "LINUX shape with > 100 concurrent lanes (4-word replay occupancy)"
         del keep
     return res
+
+
+def build_lifecycle(dag, dev, torch, args, pal):
+    """The builds the reference runs besides the warm steady state
+    (GraphLayout::build on every refresh with a changed list, repo_tab.rs:
+    790-861, 973-979): a cold step on a fresh context (first allocation of
+    every buffer), then a refresh step whose list has 50 new commits
+    prepended (new head chain on the old tips: every row shifts by 50), then
+    the same refreshed list again (warm).  ms per step (build + banded
+    geometry + emission) and wg_debug_counters [6..8] (speculative builds,
+    lanes / geometry redone by the exact stages)."""
+    import wgraph
+    from wgraph import abi, synth
+
+    def upload(d):
+        keep = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in
+                (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32), d.parent_oid.reshape(-1), d.flags, d.band)]
+        c = abi.Commits()
+        c.n_commits, c.n_parents = d.n, d.e
+        c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
+        c.residency = abi.WG_DEVICE
+        return keep, c
+
+    fresh = synth.prepend_commits(dag, 50)
+    k0, c0 = upload(dag)
+    k1, c1 = upload(fresh)
+    eng = wgraph.Engine(dev.index)
+    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+    def step(k, c, n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.build(commits=c)
+        eng.row_geometry(device_ptr=k[5].data_ptr())
+        eng.emit_vertices(0, n, selected=7, palette=pal)
+        torch.cuda.synchronize()
+        return round((time.perf_counter() - t0) * 1e3, 4)
+
+    out = {"rows": int(dag.n), "cold_ms": step(k0, c0, dag.n)}
+    warm = [step(k0, c0, dag.n) for _ in range(3)]
+    out["warm_ms"] = float(np.median(warm))
+    out["refresh_ms"] = step(k1, c1, fresh.n)
+    out["refresh_again_ms"] = step(k1, c1, fresh.n)
+    dc = eng.debug_counters()
+    out.update({"spec_builds": int(dc[6]), "spec_lanes_redone": int(dc[7]), "spec_geometry_redone": int(dc[8]),
+                "note": "refresh = 50 commits prepended (new ids, rows shifted by 50); cold = first step of a fresh "
+                        "context, incl. its device allocations"})
+    eng.close()
+    del k0, k1
+    return out
 
 
 def pmc_traffic(args, workload):
@@ -509,7 +625,8 @@ def main():
                           "rows_total": rows_total, "rows_per_gpu": args.rows_per_gpu,
                           "vertices_per_gpu": int(vs.n_vertices), "parallelism": f"row-shard x{world}"},
                "stages_ms": stages, "host_input_rows_per_s": None if host_rate is None else round(host_rate, 1),
-               "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_threads": cpu_mt, **extras}
+               "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_threads": cpu_mt, "host_cpu": host_cpu(),
+               **extras}
         if exchange is not None:
             out["seam_exchange"] = exchange
         print(json.dumps(out), flush=True)

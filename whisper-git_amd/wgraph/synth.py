@@ -111,6 +111,26 @@ def generate(kind: int | str, n: int, seed: int | None = None, **overrides) -> D
         lib.wgs_free(h)
 
 
+def prepend_commits(d: Dag, k: int, seed: int = 7) -> Dag:
+    """The list after k new commits land on the current head (a refresh:
+    apply_state_result -> rebuild_synthetic_entries, repo_tab.rs:790-861,
+    973-979): rows 0..k-1 are a new first-parent chain, newest first, whose
+    last commit's parent is the old row 0; every old row moves down by k."""
+    rng = np.random.default_rng(seed)
+    oid = rng.integers(0, 256, (k, 20), dtype=np.uint8)
+    t0 = int(d.time[0]) if d.n else 1704067200
+    time = (t0 + 60 * np.arange(k, 0, -1)).astype(np.int64)
+    if d.n:
+        new_par = np.concatenate([oid[1:], d.oid[:1]])
+    else:
+        new_par = oid[1:]
+    m = len(new_par)   # k, or k - 1 on an empty base list (the last new commit has no parent)
+    poff = np.concatenate([np.minimum(np.arange(k), m), d.parent_off.astype(np.int64) + m]).astype(np.uint32)
+    return Dag(np.concatenate([oid, d.oid]), np.concatenate([time, d.time]), poff,
+               np.concatenate([new_par, d.parent_oid]), np.concatenate([np.zeros(k, np.uint8), d.flags]),
+               np.concatenate([np.zeros(k, np.float32), d.band]))
+
+
 def save(d: Dag, path: str) -> None:
     np.savez_compressed(path, oid=d.oid, time=d.time, parent_off=d.parent_off,
                         parent_oid=d.parent_oid, flags=d.flags, band=d.band)
