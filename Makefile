@@ -24,8 +24,15 @@ CFLAGS_ORACLE := -O3 -march=x86-64-v3 -std=c11 -fPIC -ffp-contract=off -fno-fast
 all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgraph_host.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so oracle/libedt_cpu.so \
      tests/cpp/test_graph_layout profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost
 
-$(PKG)/wgraph/libwgraph.so: $(HIPSRC) $(HIPHDR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIPSRC)
+# one object per source (parallel, incremental); device code is per translation
+# unit (no relocatable device code), host code links into one library
+HIPOBJ  := $(patsubst $(CSRC)/%.hip,build/obj/%.o,$(HIPSRC))
+build/obj/%.o: $(CSRC)/%.hip $(HIPHDR)
+	@mkdir -p build/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(PKG)/wgraph/libwgraph.so: $(HIPOBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIPOBJ)
 
 $(PKG)/wgraph/libwgraph_host.so: $(PKG)/host/graph_layout.cpp $(PKG)/host/graph_layout.hpp include/wgraph.h $(PKG)/wgraph/libwgraph.so
 	g++ $(CXXFLAGS_HOST) -shared -o $@ $(PKG)/host/graph_layout.cpp -L$(PKG)/wgraph -lwgraph -Wl,-rpath,'$$ORIGIN'
@@ -61,6 +68,6 @@ engine: $(PKG)/wgraph/libwgraph.so
 host: $(PKG)/wgraph/libwgraph_host.so tests/cpp/test_graph_layout
 
 clean:
-	rm -f $(PKG)/wgraph/*.so oracle/*.so profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost tests/cpp/test_graph_layout
+	rm -rf build/obj; rm -f $(PKG)/wgraph/*.so oracle/*.so profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost tests/cpp/test_graph_layout
 
 .PHONY: all clean oracle synth engine host

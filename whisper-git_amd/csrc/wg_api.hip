@@ -281,7 +281,7 @@ void wg_destroy(wg_ctx *c) {
                       &c->curve_ref, &c->curve_row, &c->carry_off, &c->carry,
                       &c->scan_tmp, &c->scal, &c->rowflags, &c->rowflags_lists, &c->geom_diff, &c->scurve_off,
                       &c->scurve_ref, &c->scurve_row, &c->sweep_big, &c->vtx_off, &c->vtx, &c->palette, &c->chk,
-                      &c->carry_sorted, &c->curve_tb, &c->curve_cnt, &c->tile_first, &c->hs_time, &c->hs_out};
+                      &c->carry_sorted, &c->curve_tb, &c->curve_cnt, &c->tile_first, &c->hs_time, &c->hs_out, &c->htab[0], &c->htab[1], &c->bsum};
     for (DevBuf *b : bufs) b->release();
     for (DevBuf &b : c->lf) b.release();
     ShardState &S = c->sh;

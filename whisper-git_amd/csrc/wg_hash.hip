@@ -22,8 +22,14 @@ namespace {
 // only the rest (~20-30%) pay a CAS, and they pay it without a plain read
 // before it.  Linear probing stays valid: every slot between a key's home and
 // its slot is occupied, because the place pass filled the home slots first.
-__global__ void k_hash_place(const uint8_t *__restrict__ oid, uint64_t n, unsigned long long *table, uint64_t mask) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+//
+// Two tables alternate between builds: the place pass also empties the other
+// one (and its duplicate word) for the next build, so no fill launch precedes
+// the join.
+__global__ void k_hash_place(const uint8_t *__restrict__ oid, uint64_t n, unsigned long long *table, uint64_t mask,
+                             unsigned long long *next_table, uint64_t next_words) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t w = i; w < next_words; w += (uint64_t)gridDim.x * blockDim.x) next_table[w] = HEMPTY;
     if (i >= n) return;
     const Key k = load_key(oid + i * 20);
     table[key_hash(k) & mask] = ((unsigned long long)key_fp(k) << 32) | (uint32_t)i;
@@ -55,33 +61,34 @@ __global__ void k_hash_settle(const uint8_t *__restrict__ oid, uint64_t n, unsig
     }
 }
 
-// ids all distinct (no insert met its own key): every row is canonical and
-// the second probe pass is skipped
-__global__ void k_canon(const uint8_t *__restrict__ oid, uint64_t n, const unsigned long long *__restrict__ table,
-                        uint64_t mask, const uint32_t *__restrict__ dup, uint32_t *__restrict__ canon) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (*dup == 0xFFFFFFFFu) { canon[i] = (uint32_t)i; return; }
-    int64_t r = hash_find(load_key(oid + i * 20), oid, table, mask);
-    canon[i] = r < 0 ? (uint32_t)i : (uint32_t)r;
-}
-
-__global__ void k_probe_parents(const uint8_t *__restrict__ poid, uint64_t e, const uint8_t *__restrict__ oid,
-                                const unsigned long long *__restrict__ table, uint64_t mask, int32_t *__restrict__ prow) {
-    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= e) return;
-    prow[k] = (int32_t)hash_find(load_key(poid + k * 20), oid, table, mask);
-}
-
-// edges per row = parents found in the list (:306-311); lane-independent, so
-// the edge offsets and the total are ready before the lanes are
-__global__ void k_edge_cnt(uint64_t n, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow,
-                           uint32_t *__restrict__ edge_cnt) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// One thread per row: canon[i] (the row itself when no insert met its own
+// key: ids all distinct), prow of the row's parent references (-1: not in
+// the list, :306-311) and the row's edge count (parents found, lane-
+// independent, so the edge offsets are ready before the lanes are) with the
+// block's sum of it for the offsets' scan (wg_scan_bs_u32).
+__global__ void __launch_bounds__(WG_BS_THREADS) k_probe_rows(const uint8_t *__restrict__ oid, uint64_t n,
+                                                             const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
+                                                             const unsigned long long *__restrict__ table, uint64_t mask,
+                                                             const uint32_t *__restrict__ dup, uint32_t *__restrict__ canon,
+                                                             int32_t *__restrict__ prow, uint32_t *__restrict__ edge_cnt,
+                                                             uint32_t *__restrict__ bsum) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t cnt = 0;
-    for (uint32_t k = poff[i]; k < poff[i + 1]; k++) cnt += prow[k] >= 0;
-    edge_cnt[i] = cnt;
+    if (i < n) {
+        if (*dup == 0xFFFFFFFFu) canon[i] = (uint32_t)i;
+        else {
+            const int64_t r = hash_find(load_key(oid + i * 20), oid, table, mask);
+            canon[i] = r < 0 ? (uint32_t)i : (uint32_t)r;
+        }
+        const uint32_t pa = poff[i], pb = poff[i + 1];
+        for (uint32_t k = pa; k < pb; k++) {
+            const int32_t p = (int32_t)hash_find(load_key(poid + (uint64_t)k * 20), oid, table, mask);
+            prow[k] = p;
+            cnt += p >= 0;
+        }
+        edge_cnt[i] = cnt;
+    }
+    wg_bsum_store(cnt, bsum);
 }
 
 }  // namespace
@@ -91,37 +98,47 @@ int wg_stage_hash_join(wg_ctx *c) {
     uint64_t cap = 1024;
     while (cap < 2 * n) cap <<= 1;
     c->hcap = cap;
-    WG_ALLOC(c, c->hash, cap * 8 + 64);
+    const uint64_t words = cap + 1;   // the table, then the duplicate flag word (all ones = none)
+    const int t = c->htab_cur, o = t ^ 1;
+    for (int k : {t, o}) {
+        if (c->htab[k].cap < words * 8 + 64) c->htab_clean[k] = 0;   // (re)allocated below: not known empty
+        WG_ALLOC(c, c->htab[k], words * 8 + 64);
+    }
     WG_ALLOC(c, c->canon, n * 4 + 4);
     WG_ALLOC(c, c->prow, e * 4 + 4);
-    wg_stage_begin(c, "hash_join");
-    // one fill: the table (empty = all ones) and, after it, the duplicate flag (all ones = none)
-    WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8 + 4, c->stream));
-    uint32_t *dup = reinterpret_cast<uint32_t *>(c->hash.as<unsigned long long>() + cap);
-    const int T = 256;
-    if (n) {
-        hipLaunchKernelGGL(k_hash_place, dim3((n + T - 1) / T), dim3(T), 0, c->stream, c->d_oid, n,
-                           c->hash.as<unsigned long long>(), cap - 1);
-        hipLaunchKernelGGL(k_hash_settle, dim3((n + T - 1) / T), dim3(T), 0, c->stream, c->d_oid, n,
-                           c->hash.as<unsigned long long>(), cap - 1, dup);
-        hipLaunchKernelGGL(k_canon, dim3((n + T - 1) / T), dim3(T), 0, c->stream, c->d_oid, n,
-                           c->hash.as<const unsigned long long>(), cap - 1, dup,
-                           c->canon.as<uint32_t>());
-    }
-    if (e)
-        hipLaunchKernelGGL(k_probe_parents, dim3((e + T - 1) / T), dim3(T), 0, c->stream, c->d_poid, e, c->d_oid,
-                           c->hash.as<const unsigned long long>(), cap - 1, c->prow.as<int32_t>());
     WG_ALLOC(c, c->edge_cnt, (n + 1) * 4);
+    WG_ALLOC(c, c->bsum, 3 * (wg_bs_blocks(n) + 64) * 4);
     { const int _sr = wg_scan_reserve(c, n + 1); if (_sr != WG_OK) return _sr; }
+    wg_stage_begin(c, "hash_join");
+    unsigned long long *table = c->htab[t].as<unsigned long long>();
+    if (c->htab_clean[t] < words) WG_HIP(c, hipMemsetAsync(table, 0xFF, words * 8, c->stream));
+    uint32_t *dup = reinterpret_cast<uint32_t *>(table + cap);
+    const int T = WG_BS_THREADS;
+    const uint32_t g = (uint32_t)((n + T - 1) / T);
     if (n) {
-        hipLaunchKernelGGL(k_edge_cnt, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->d_poff,
-                           c->prow.as<const int32_t>(), c->edge_cnt.as<uint32_t>());
-        WG_HIP(c, wg_exclusive_scan_u32(c->edge_cnt.as<uint32_t>(), c->edge_cnt.as<uint32_t>(), n, c->scan_tmp.p, c->stream));
+        hipLaunchKernelGGL(k_hash_place, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1,
+                           c->htab[o].as<unsigned long long>(), words);
+        c->htab_clean[o] = words;
+        hipLaunchKernelGGL(k_hash_settle, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1, dup);
+        hipLaunchKernelGGL(k_probe_rows, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
+                           (const unsigned long long *)table, cap - 1, (const uint32_t *)dup, c->canon.as<uint32_t>(),
+                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->bsum.as<uint32_t>());
+        WgScanBs S;
+        S.na = 1;
+        S.in[0] = c->edge_cnt.as<const uint32_t>();
+        S.out[0] = c->edge_cnt.as<uint32_t>();
+        S.bsum[0] = c->bsum.as<const uint32_t>();
+        WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, c->stream));
         // read by wg_stage_edges after the lane stage's own synchronisation (a
         // speculative build reads it with its end-of-build validation)
         if (!c->spec)
             if (const int rc = wg_fetch_defer(c, {{c->edge_cnt.as<uint32_t>() + n, false}})) return rc;
+    } else {
+        WG_HIP(c, hipMemsetAsync(c->edge_cnt.p, 0, 4, c->stream));
     }
+    c->htab_clean[t] = 0;
+    c->htab_cur = o;
+    c->htab_last = table;
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;

@@ -213,6 +213,12 @@ struct wg_ctx {
     // hash join
     DevBuf hash;            // uint64 [hcap]  (fingerprint<<32 | row), then the duplicate flag word
     uint64_t hcap = 0;
+    // single-GPU join (wg_hash.hip): two tables used in turn; the place pass
+    // empties the one the next build uses.  htab_clean[k]: words known empty.
+    DevBuf htab[2];
+    uint64_t htab_clean[2] = {0, 0};
+    int htab_cur = 0;
+    const unsigned long long *htab_last = nullptr;   // the last join's table (hcap slots)
     DevBuf canon;           // uint32 [N]  last row holding the same id
     DevBuf prow;            // int32  [E]  canonical parent row or -1
     // lanes
@@ -239,6 +245,7 @@ struct wg_ctx {
     uint64_t n_events = 0;  // events of the last fast-path lane build
     uint64_t e_refs_own = 0;   // parent references of the rows this context owns
     bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])
+    bool lane_out_fused = false;   // the lane kernel wrote lane_out / color_out (speculative fast path)
     bool force_general_lanes = false;   // WG_LANES=general (testing the general walk)
     ReplayRun spec_run;     // the speculative build's replay (its iteration count and flag words)
     // speculative build (wg_layout_build): launches sized by upper bounds and
@@ -276,6 +283,7 @@ struct wg_ctx {
     bool geom_sum_stale = false;            // total_height / scan_path / n_curve not read back yet
     const void *geom_sum_at[3] = {nullptr, nullptr, nullptr};   // where they are (row_top[n], scan flag, curve_off[n])
     DevBuf scan_tmp;        // scan workspace
+    DevBuf bsum;            // producer tile sums of the wg_scan_bs_u32 scans (3 arrays of wg_bs_blocks(n) + 64)
     DevBuf scal;            // uint64 [16] device scalars (totals)
     DevBuf rowflags;        // uint8 [N] bit0 zero-height strip, bit1 child strip empty, bit2 parent strip empty
     // The ordered lists (vert, curve_ref/curve_row, offsets) depend on the
@@ -430,13 +438,63 @@ hipError_t wg_exclusive_scan2_u32(const uint32_t *in0, uint32_t *out0, const uin
                                   void *tmp, hipStream_t s);
 hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, hipStream_t s);
 
+// Scans whose tile sums come from the producer (no reduce launch): a producer
+// kernel of WG_BS_THREADS-thread blocks, one element per thread, calls
+// wg_bsum_store(v, bsum) with every thread of the block (it synchronises the
+// block) and so leaves bsum[blockIdx.x] = the block's sum.  The down-sweep
+// then needs one launch (up to WG_BS_SELF tile sums; more add a scan of the
+// sums first).  Up to three arrays of the same length share the launches.
+constexpr int WG_BS_THREADS = 256;
+constexpr uint64_t WG_BS_SELF = 8192;
+__device__ __forceinline__ void wg_bsum_store(uint32_t v, uint32_t *__restrict__ bsum) {
+    __shared__ uint32_t wg_bs_w[WG_BS_THREADS / 64];
+    v = wg_wave_scan(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+    if ((threadIdx.x & 63) == 63) wg_bs_w[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < WG_BS_THREADS / 64; w++) t += wg_bs_w[w];
+        bsum[blockIdx.x] = t;
+    }
+    __syncthreads();   // the staging words are reused by a following call
+}
+struct WgScanBs {
+    int na = 0;
+    const uint32_t *in[3] = {nullptr, nullptr, nullptr};
+    uint32_t *out[3] = {nullptr, nullptr, nullptr};
+    const uint32_t *bsum[3] = {nullptr, nullptr, nullptr};   // [ceil(n / WG_BS_THREADS)] each
+};
+// out[a][0..n] = exclusive scan of in[a] (out[a][n] = total); in may alias out.
+// tmp: c->scan_tmp after wg_scan_reserve(c, n).
+hipError_t wg_scan_bs_u32(const WgScanBs &S, uint64_t n, void *tmp, hipStream_t s);
+inline uint64_t wg_bs_blocks(uint64_t n) { return (n + WG_BS_THREADS - 1) / WG_BS_THREADS; }
+
 // stages -------------------------------------------------------------------------
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
 int wg_stage_lanes(wg_ctx *c, bool spec);     // wg_lanes.hip
 int wg_lanes_fast(wg_ctx *c, bool *used, bool spec);   // wg_lanes_fast.hip
 
 hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blind);
-hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blind, uint4 *ev_pad);
+// speculative build: the replay's initial state is written by the event
+// kernel (k_lf_events, WgReplayInit from wg_replay_prepare_spec), the
+// iterations follow, and the scalars are reduced by the lanes kernel
+// (wg_replay_finish_lanes, which also writes lane_out / colour: the fast path
+// only runs on distinct ids, so every row is its own canonical row)
+struct WgReplayInit {
+    unsigned long long *occ = nullptr;
+    uint64_t occ_words = 0;
+    uint32_t *changed = nullptr;
+    uint32_t nflags = 0;
+    uint4 *slots16 = nullptr;
+    uint64_t nslots16 = 0;
+    const uint32_t *nev_dev = nullptr;   // zero records at ev[*nev_dev .. +256) (the replay prefetches past a chunk)
+    uint64_t total = 0;                  // elements of the largest of these (grid-stride bound)
+};
+WgReplayInit wg_replay_prepare_spec(ReplayRun &R, uint32_t &blind);
+hipError_t wg_replay_iterate_spec(hipStream_t s, ReplayRun &R, uint32_t blind);
+hipError_t wg_replay_finish_lanes(hipStream_t s, const ReplayRun &R, uint64_t nl, const uint32_t *sp, uint32_t *lane,
+                                  uint32_t *lane_out, uint8_t *color_out, const uint8_t *flags);
 hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged);
 int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known = -1);   // wg_lanes.hip
 // speculative build (wg_layout_build): validation words of the lane build
@@ -446,7 +504,8 @@ constexpr int WG_GEOM_SPEC_ITEMS = 8;
 int wg_lanes_spec_items(wg_ctx *c, WgFetch *it);
 bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v);
 // event-compressed lane phases over a row range (wg_lanes_fast.hip)
-int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back);   // + wg_lf_refs_end after queueing wg_lf_chain
+// scal: the lane scalars to clear with the stage's state (single-GPU build), or null
+int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back, uint32_t *scal = nullptr);   // + wg_lf_refs_end after queueing wg_lf_chain
 int wg_lf_refs_end(wg_ctx *c, uint32_t *viol, uint64_t *nev, uint64_t *naux);
 int wg_lf_chain(wg_ctx *c, const LfRange &R);
 int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok);

@@ -198,10 +198,10 @@ int wg_stage_lanes(wg_ctx *c, bool spec) {
     c->n_slots = 0;
     c->lane_path = 1;
     c->graph_width = WG_LANE_W;   // max_lane 0 -> one visible lane (:353-354)
+    c->lane_out_fused = false;
     if (n == 0) return WG_OK;
     wg_stage_begin(c, "lanes");
-    WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, c->stream));
-    if (!c->force_general_lanes) {
+    if (!c->force_general_lanes) {   // (the fast path's first kernel clears the lane scalars)
         bool used = false;
         int rc = wg_lanes_fast(c, &used, spec);
         if (rc != WG_OK) return rc;
@@ -216,8 +216,8 @@ int wg_stage_lanes(wg_ctx *c, bool spec) {
             c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
             return WG_OK;
         }
-        WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, c->stream));
     }
+    WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, c->stream));
     WG_HIP(c, launch_general<1>(c));
     const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
     uint64_t sc[3];
@@ -255,8 +255,9 @@ int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known) {
     }
     wg_stage_begin(c, "edges");
     const int T = 256;
-    hipLaunchKernelGGL(k_lane_out, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->canon.as<const uint32_t>(),
-                       c->lane_asg.as<const uint32_t>(), c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>());
+    if (!c->lane_out_fused)   // (the speculative fast path's lane kernel wrote them)
+        hipLaunchKernelGGL(k_lane_out, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->canon.as<const uint32_t>(),
+                           c->lane_asg.as<const uint32_t>(), c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>());
     WG_HIP(c, hipGetLastError());
     // edge offsets: scanned after the hash join (wg_stage_hash_join); the
     // total was copied out then and the lane stage has synchronised since

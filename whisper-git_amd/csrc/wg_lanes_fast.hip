@@ -138,32 +138,47 @@ __global__ void k_lf_xfirst(LfRange R) {
     R.isfb[k] = first ? 1 : 0;
 }
 
-// per row: w, first-parent-in-list, event count, merge-token count
-__global__ void k_lf_rows(LfRange R, const unsigned long long *__restrict__ first_ref, const uint32_t *__restrict__ fpc,
-                          uint32_t *__restrict__ winfo, uint32_t *__restrict__ ev_cnt, uint32_t *__restrict__ aux_cnt) {
+// per row: w, first-parent-in-list, event count, merge-token count; the
+// block sums of the event / merge-token / first-parent-child counts feed one
+// scan launch for ev_off, aux_off and ch_off (wg_scan_bs_u32)
+__global__ void __launch_bounds__(WG_BS_THREADS) k_lf_rows(LfRange R, const unsigned long long *__restrict__ first_ref,
+                                                          const uint32_t *__restrict__ fpc, uint32_t *__restrict__ winfo,
+                                                          uint32_t *__restrict__ ev_cnt, uint32_t *__restrict__ aux_cnt,
+                                                          uint32_t *__restrict__ bsum, uint32_t nbs) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= R.nl) return;
-    const uint64_t gj = R.s + j;
-    const unsigned long long fr = first_ref[j];
-    const uint32_t sec_first = (fr != REF_NONE && (fr & 0xFFFFu) != 0) ? 1u : 0u;
-    const uint32_t w = fpc[j] + sec_first;
-    const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
-    const bool fp_in = pb > pa && R.prow[pa] >= 0;
-    uint32_t nc = 0;
-    for (uint32_t k = pa + 1; k < pb; k++) {
-        const int32_t p = R.prow[k];
-        if (p >= 0 && is_first_ref(R, first_ref, gj, k, k - pa, (uint64_t)p)) nc++;
+    uint32_t ne = 0, na_aux = 0, nfp = 0;
+    if (j < R.nl) {
+        const uint64_t gj = R.s + j;
+        const unsigned long long fr = first_ref[j];
+        const uint32_t sec_first = (fr != REF_NONE && (fr & 0xFFFFu) != 0) ? 1u : 0u;
+        nfp = fpc[j];
+        const uint32_t w = nfp + sec_first;
+        const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
+        const bool fp_in = pb > pa && R.prow[pa] >= 0;
+        uint32_t nc = 0;
+        for (uint32_t k = pa + 1; k < pb; k++) {
+            const int32_t p = R.prow[k];
+            if (p >= 0 && is_first_ref(R, first_ref, gj, k, k - pa, (uint64_t)p)) nc++;
+        }
+        const uint32_t na = (w != 1) ? 1u : 0u;
+        const uint32_t nb = (w == 1 && !fp_in) ? 1u : 0u;
+        winfo[j] = (w < 0x3FFFFFFFu ? w : 0x3FFFFFFFu) | (fp_in ? 0x40000000u : 0u) | (sec_first ? 0x80000000u : 0u);
+        ne = na + nb + nc;
+        na_aux = w > 2 ? w + 1 : 0u;
+        ev_cnt[j] = ne;
+        aux_cnt[j] = na_aux;
     }
-    const uint32_t na = (w != 1) ? 1u : 0u;
-    const uint32_t nb = (w == 1 && !fp_in) ? 1u : 0u;
-    winfo[j] = (w < 0x3FFFFFFFu ? w : 0x3FFFFFFFu) | (fp_in ? 0x40000000u : 0u) | (sec_first ? 0x80000000u : 0u);
-    ev_cnt[j] = na + nb + nc;
-    aux_cnt[j] = w > 2 ? w + 1 : 0u;
+    wg_bsum_store(ne, bsum);
+    wg_bsum_store(na_aux, bsum + nbs);
+    wg_bsum_store(nfp, bsum + 2 * nbs);
 }
 
-// SECALLOC event of every first reference through a secondary parent
-__global__ void k_lf_secev(LfRange R, const unsigned long long *__restrict__ first_ref, const uint32_t *__restrict__ winfo,
-                           const uint32_t *__restrict__ ev_off, uint32_t *__restrict__ secev) {
+// per row: the SECALLOC event of every first reference through a secondary
+// parent, and the row into its first parent's list of first-parent children
+__global__ void k_lf_secev_children(LfRange R, const unsigned long long *__restrict__ first_ref,
+                                    const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
+                                    uint32_t *__restrict__ secev, const uint32_t *__restrict__ ch_off, uint32_t *ch_fill,
+                                    uint32_t *ch) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= R.nl) return;
     const uint64_t gj = R.s + j;
@@ -179,6 +194,11 @@ __global__ void k_lf_secev(LfRange R, const unsigned long long *__restrict__ fir
         else R.xsec[k] = WG_TOK_EV | e;
         e++;
     }
+    if (pa == pb) return;
+    const int32_t p = R.prow[pa];
+    if (p < 0 || (uint64_t)p >= R.e || (uint64_t)p <= gj) return;   // beyond the range / leaky
+    const uint64_t pl = (uint64_t)p - R.s;
+    ch[ch_off[pl] + atomicAdd(&ch_fill[pl], 1u)] = (uint32_t)j;
 }
 
 // first references into this shard through a secondary parent of an earlier shard
@@ -191,18 +211,6 @@ __global__ void k_lf_xin_secev(LfRange R, const unsigned long long *__restrict__
     if (first_ref[en.p - R.s] == ref_key(en.c, kidx)) secev[en.p - R.s] = WG_TOK_X | (uint32_t)x;
 }
 
-__global__ void k_lf_children(LfRange R, const uint32_t *__restrict__ ch_off, uint32_t *ch_fill, uint32_t *ch) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R.nl) return;
-    const uint64_t gi = R.s + i;
-    const uint32_t pa = R.poff[gi];
-    if (pa == R.poff[gi + 1]) return;
-    const int32_t p = R.prow[pa];
-    if (p < 0 || (uint64_t)p >= R.e || (uint64_t)p <= gi) return;   // beyond the range / leaky
-    const uint64_t pl = (uint64_t)p - R.s;
-    ch[ch_off[pl] + atomicAdd(&ch_fill[pl], 1u)] = (uint32_t)i;
-}
-
 __global__ void k_lf_xin_children(LfRange R, const uint32_t *__restrict__ ch_off, uint32_t *ch_fill, uint32_t *ch) {
     const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= R.xin_end) return;
@@ -212,15 +220,14 @@ __global__ void k_lf_xin_children(LfRange R, const uint32_t *__restrict__ ch_off
     ch[ch_off[pl] + atomicAdd(&ch_fill[pl], 1u)] = WG_TOK_X | (uint32_t)x;
 }
 
-__global__ void k_lf_sp_init(uint64_t nl, const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
-                             const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
-                             const uint32_t *__restrict__ secev, uint32_t *__restrict__ sp) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nl) return;
+// the chain source pointer of row j before jumping
+__device__ __forceinline__ uint32_t sp_init(uint64_t j, const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
+                                            const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
+                                            const uint32_t *__restrict__ secev) {
     const uint32_t wi = winfo[j], w = wi & 0x3FFFFFFFu;
-    if (w != 1) sp[j] = WG_TOK_EV | ev_off[j];                  // own ALLOC / MIN event
-    else if (wi & 0x80000000u) sp[j] = secev[j];                // waiter = secondary allocation
-    else sp[j] = ch[ch_off[j]];                                 // waiter = the only first-parent child
+    if (w != 1) return WG_TOK_EV | ev_off[j];              // own ALLOC / MIN event
+    if (wi & 0x80000000u) return secev[j];                 // waiter = secondary allocation
+    return ch[ch_off[j]];                                  // waiter = the only first-parent child
 }
 
 // Chain sources: sp[j] is a token (tagged) or the row whose token row j
@@ -231,11 +238,14 @@ __global__ void k_lf_sp_init(uint64_t nl, const uint32_t *__restrict__ winfo, co
 //                   link crosses a tile, and ceil(log4(tiles)) passes finish.
 constexpr int JT_THREADS = 1024, JT_ROWS = 4096;
 
-__global__ void __launch_bounds__(JT_THREADS) k_lf_jump_tile(uint64_t nl, uint32_t *__restrict__ sp) {
+__global__ void __launch_bounds__(JT_THREADS) k_lf_jump_tile(uint64_t nl, uint32_t *__restrict__ sp,
+                                                              const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
+                                                              const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
+                                                              const uint32_t *__restrict__ secev) {
     __shared__ uint32_t L[JT_ROWS];
     const uint64_t t0 = (uint64_t)blockIdx.x * JT_ROWS;
     const uint32_t nt = (uint32_t)((nl - t0) < (uint64_t)JT_ROWS ? (nl - t0) : (uint64_t)JT_ROWS);
-    for (uint32_t i = threadIdx.x; i < nt; i += JT_THREADS) L[i] = sp[t0 + i];
+    for (uint32_t i = threadIdx.x; i < nt; i += JT_THREADS) L[i] = sp_init(t0 + i, winfo, ev_off, ch_off, ch, secev);
     __syncthreads();
     // in place: a stored value is always a later link of the same chain, so a
     // racing read only skips further; stop once no pointer stays in the tile.
@@ -304,8 +314,16 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
                             const uint32_t *__restrict__ ev_off, const uint32_t *__restrict__ aux_off,
                             const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
                             const uint32_t *__restrict__ secev, const uint32_t *__restrict__ sp,
-                            uint4 *__restrict__ ev, uint32_t *__restrict__ aux, const uint32_t *__restrict__ gate = nullptr) {
+                            uint4 *__restrict__ ev, uint32_t *__restrict__ aux, const uint32_t *__restrict__ gate = nullptr,
+                            WgReplayInit RI = WgReplayInit{}) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // speculative build: the replay's initial state (wg_replay_prepare_spec)
+    for (uint64_t i = j; i < RI.total; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (i < RI.occ_words) RI.occ[i] = 0ull;
+        if (i < RI.nflags) RI.changed[i] = (i == 0) ? 1u : 0u;
+        if (i < RI.nslots16) RI.slots16[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (RI.nev_dev && i < 256) ev[*RI.nev_dev + i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     if (j >= R.nl) return;
     if (gate && *gate) return;   // speculative build: not well formed (the general walk takes over)
     const uint64_t gj = R.s + j;
@@ -367,12 +385,13 @@ __global__ void k_lf_lanes(uint64_t nl, const uint32_t *__restrict__ sp, const u
 // the flag words 0
 __global__ void k_lf_clear(uint64_t n, unsigned long long *__restrict__ first_ref, uint32_t *__restrict__ fpc,
                            uint32_t *__restrict__ ch_fill, uint32_t *__restrict__ flags,
-                           unsigned long long *__restrict__ lfirst) {
+                           unsigned long long *__restrict__ lfirst, uint32_t *__restrict__ scal) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) first_ref[i] = REF_NONE;
     if (lfirst && i < n) lfirst[i] = REF_NONE;
     if (i < n + 2) { fpc[i] = 0u; ch_fill[i] = 0u; }
     if (i < 16) flags[i] = 0u;
+    if (scal && i < 16) scal[i] = 0u;   // the lane scalars (max_lane, slots, overflow, ...)
 }
 
 // gathered shard-local records (k_lf_events<true> of every rank, rank r's at
@@ -410,23 +429,26 @@ __global__ void k_lf_events_finish(uint64_t nev, uint32_t world, const uint64_t 
 
 static const uint32_t *lf_sp(wg_ctx *c) { return c->lf_sp_b ? c->lf[LF_SPB].as<const uint32_t>() : c->lf[LF_SPA].as<const uint32_t>(); }
 
-int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back) {
+int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back, uint32_t *scal) {
     const uint64_t n = R.nl;
     hipStream_t s = c->stream;
     DevBuf &first_ref = c->lf[LF_FIRST], &fpc = c->lf[LF_FPC], &winfo = c->lf[LF_WINFO], &ev_off = c->lf[LF_EVOFF];
-    DevBuf &flags = c->lf[LF_FLAGS], &aux_off = c->lf[LF_AUXOFF];
+    DevBuf &flags = c->lf[LF_FLAGS], &aux_off = c->lf[LF_AUXOFF], &ch_off = c->lf[LF_CHOFF];
     WG_ALLOC(c, first_ref, n * 8 + 8);
     WG_ALLOC(c, fpc, (n + 2) * 4);
     WG_ALLOC(c, winfo, n * 4 + 4);
     WG_ALLOC(c, ev_off, (n + 2) * 4);
     WG_ALLOC(c, aux_off, (n + 2) * 4);
+    WG_ALLOC(c, ch_off, (n + 2) * 4);
     WG_ALLOC(c, flags, 64);
     DevBuf &ch_fill = c->lf[LF_CHFILL];
     WG_ALLOC(c, ch_fill, (n + 2) * 4);
+    const uint64_t nbs = wg_bs_blocks(n);
+    WG_ALLOC(c, c->bsum, 3 * (nbs + 64) * 4);
     { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "lf_refs");
     hipLaunchKernelGGL(k_lf_clear, dim3(blocks(n + 16)), dim3(T), 0, s, n, first_ref.as<unsigned long long>(),
-                       fpc.as<uint32_t>(), ch_fill.as<uint32_t>(), flags.as<uint32_t>(), R.lfirst);
+                       fpc.as<uint32_t>(), ch_fill.as<uint32_t>(), flags.as<uint32_t>(), R.lfirst, scal);
     if (n) hipLaunchKernelGGL(k_lf_refs, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<unsigned long long>(),
                               fpc.as<uint32_t>(), flags.as<uint32_t>());
     if (R.xin_end)
@@ -434,10 +456,19 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back) {
                            fpc.as<uint32_t>());
     if (R.xown_end > R.xown_begin)
         hipLaunchKernelGGL(k_lf_xfirst, dim3(blocks(R.xown_end - R.xown_begin)), dim3(T), 0, s, R);
+    // event / merge-token / child counts and their block sums, then one scan
+    // launch: ev_off, aux_off (in place) and ch_off (the first-parent children
+    // lists, from fpc)
+    uint32_t *bs = c->bsum.as<uint32_t>();
     if (n) hipLaunchKernelGGL(k_lf_rows, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<const unsigned long long>(),
-                              fpc.as<const uint32_t>(), winfo.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>());
-    WG_HIP(c, wg_exclusive_scan2_u32(ev_off.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>(),
-                                     aux_off.as<uint32_t>(), n, c->scan_tmp.p, s));
+                              fpc.as<const uint32_t>(), winfo.as<uint32_t>(), ev_off.as<uint32_t>(), aux_off.as<uint32_t>(),
+                              bs, (uint32_t)nbs);
+    WgScanBs S;
+    S.na = 3;
+    S.in[0] = ev_off.as<const uint32_t>(); S.out[0] = ev_off.as<uint32_t>(); S.bsum[0] = bs;
+    S.in[1] = aux_off.as<const uint32_t>(); S.out[1] = aux_off.as<uint32_t>(); S.bsum[1] = bs + nbs;
+    S.in[2] = fpc.as<const uint32_t>(); S.out[2] = ch_off.as<uint32_t>(); S.bsum[2] = bs + 2 * nbs;
+    WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, s));
     // read back while the chain phase runs (wg_lf_refs_end); a speculative
     // build reads the same words with its end-of-build validation instead
     const int rc = read_back ? wg_fetch_begin(c, {{flags.p, false}, {ev_off.as<uint32_t>() + n, false},
@@ -459,7 +490,7 @@ int wg_lf_refs_end(wg_ctx *c, uint32_t *viol, uint64_t *nev, uint64_t *naux) {
 int wg_lf_chain(wg_ctx *c, const LfRange &R) {
     const uint64_t n = R.nl;
     hipStream_t s = c->stream;
-    DevBuf &first_ref = c->lf[LF_FIRST], &fpc = c->lf[LF_FPC], &winfo = c->lf[LF_WINFO], &ev_off = c->lf[LF_EVOFF];
+    DevBuf &first_ref = c->lf[LF_FIRST], &winfo = c->lf[LF_WINFO], &ev_off = c->lf[LF_EVOFF];
     DevBuf &secev = c->lf[LF_SECEV], &ch_off = c->lf[LF_CHOFF], &ch_fill = c->lf[LF_CHFILL], &ch = c->lf[LF_CH];
     DevBuf &spA = c->lf[LF_SPA], &spB = c->lf[LF_SPB];
     // children: own rows' first parents in range + earlier shards' first parents
@@ -471,24 +502,22 @@ int wg_lf_chain(wg_ctx *c, const LfRange &R) {
     WG_ALLOC(c, spA, n * 4 + 4);
     WG_ALLOC(c, spB, n * 4 + 4);
     wg_stage_begin(c, "lf_chain");
-    // ch_fill was cleared with the stage's other state (k_lf_clear)
-    if (n) hipLaunchKernelGGL(k_lf_secev, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<const unsigned long long>(),
-                              winfo.as<const uint32_t>(), ev_off.as<const uint32_t>(), secev.as<uint32_t>());
+    // ch_fill was cleared with the stage's other state (k_lf_clear), ch_off
+    // scanned with the event offsets (wg_lf_refs)
+    if (n) hipLaunchKernelGGL(k_lf_secev_children, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<const unsigned long long>(),
+                              winfo.as<const uint32_t>(), ev_off.as<const uint32_t>(), secev.as<uint32_t>(),
+                              ch_off.as<const uint32_t>(), ch_fill.as<uint32_t>(), ch.as<uint32_t>());
     if (R.xin_end)
         hipLaunchKernelGGL(k_lf_xin_secev, dim3(blocks(R.xin_end)), dim3(T), 0, s, R,
                            first_ref.as<const unsigned long long>(), secev.as<uint32_t>());
-    WG_HIP(c, wg_exclusive_scan_u32(fpc.as<uint32_t>(), ch_off.as<uint32_t>(), n, c->scan_tmp.p, s));
-    if (n) hipLaunchKernelGGL(k_lf_children, dim3(blocks(n)), dim3(T), 0, s, R, ch_off.as<const uint32_t>(),
-                              ch_fill.as<uint32_t>(), ch.as<uint32_t>());
     if (R.xin_end)
         hipLaunchKernelGGL(k_lf_xin_children, dim3(blocks(R.xin_end)), dim3(T), 0, s, R, ch_off.as<const uint32_t>(),
                            ch_fill.as<uint32_t>(), ch.as<uint32_t>());
-    if (n) hipLaunchKernelGGL(k_lf_sp_init, dim3(blocks(n)), dim3(T), 0, s, n, winfo.as<const uint32_t>(),
-                              ev_off.as<const uint32_t>(), ch_off.as<const uint32_t>(), ch.as<const uint32_t>(),
-                              secev.as<const uint32_t>(), spA.as<uint32_t>());
     // chain resolution: tiles in LDS, then passes of 4 links over the tile crossings
     const uint64_t ntiles = (n + JT_ROWS - 1) / JT_ROWS;
-    if (n) hipLaunchKernelGGL(k_lf_jump_tile, dim3(ntiles), dim3(JT_THREADS), 0, s, n, spA.as<uint32_t>());
+    if (n) hipLaunchKernelGGL(k_lf_jump_tile, dim3(ntiles), dim3(JT_THREADS), 0, s, n, spA.as<uint32_t>(),
+                              winfo.as<const uint32_t>(), ev_off.as<const uint32_t>(), ch_off.as<const uint32_t>(),
+                              ch.as<const uint32_t>(), secev.as<const uint32_t>());
     int rounds = 0;
     for (uint64_t reach = 1; reach < ntiles; reach *= 4) rounds++;
     DevBuf *in = &spA, *out = &spB;
@@ -652,7 +681,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
 // (wg_lanes_spec_check) are read with the end-of-build validation.
 static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     const uint64_t n = R.nl;
-    int rc = wg_lf_refs(c, R, false);
+    int rc = wg_lf_refs(c, R, false, c->lane_scalars.as<uint32_t>());
     if (rc != WG_OK) return rc;
     if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
     const uint64_t nev_cap = n + c->e_refs, naux_cap = 2 * (n + c->e_refs) + 16;
@@ -662,15 +691,6 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     WG_ALLOC(c, evrec, (nev_cap + 256) * 16);
     WG_ALLOC(c, aux, naux_cap * 4);
     hipStream_t s = c->stream;
-    wg_stage_begin(c, "lf_events");
-    hipLaunchKernelGGL(k_lf_events<false>, dim3(blocks(n)), dim3(T), 0, s, R, 0u, 0u, (const uint32_t *)nullptr,
-                       c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
-                       c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
-                       c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
-                       c->lf[LF_SECEV].as<const uint32_t>(), lf_sp(c), evrec.as<uint4>(), aux.as<uint32_t>(), gate);
-    WG_HIP(c, hipGetLastError());
-    wg_stage_end(c);
-    wg_stage_begin(c, "lf_loop");
     ReplayRun &run = c->spec_run;
     run = ReplayRun{};
     run.nev = nev_cap;
@@ -696,10 +716,24 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     run.scal = c->lane_scalars.as<uint32_t>();
     run.nev_dev = nev_dev;
     run.gate = gate;
-    WG_HIP(c, wg_replay_start_spec(c, s, run, c->replay_blind < 2 ? 2u : c->replay_blind, evrec.as<uint4>()));
-    if (n) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(n)), dim3(T), 0, s, n, lf_sp(c), run.sp_prev,
-                              c->lane_asg.as<uint32_t>(), gate);
+    uint32_t blind = c->replay_blind < 2 ? 2u : c->replay_blind;
+    const WgReplayInit RI = wg_replay_prepare_spec(run, blind);
+    wg_stage_begin(c, "lf_events");
+    hipLaunchKernelGGL(k_lf_events<false>, dim3(blocks(n)), dim3(T), 0, s, R, 0u, 0u, (const uint32_t *)nullptr,
+                       c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
+                       c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
+                       c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
+                       c->lf[LF_SECEV].as<const uint32_t>(), lf_sp(c), evrec.as<uint4>(), aux.as<uint32_t>(), gate, RI);
     WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    wg_stage_begin(c, "lf_loop");
+    WG_HIP(c, wg_replay_iterate_spec(s, run, blind));
+    // scalars + lanes + lane_out / colours in one launch (wg_stage_edges skips k_lane_out)
+    WG_ALLOC(c, c->lane_out, n * 4 + 4);
+    WG_ALLOC(c, c->color_out, n + 4);
+    WG_HIP(c, wg_replay_finish_lanes(s, run, n, lf_sp(c), c->lane_asg.as<uint32_t>(), c->lane_out.as<uint32_t>(),
+                                     c->color_out.as<uint8_t>(), c->d_flags));
+    c->lane_out_fused = true;
     wg_stage_end(c);
     return WG_OK;
 }
@@ -761,7 +795,7 @@ int wg_lanes_fast(wg_ctx *c, bool *used, bool spec) {
     }
     uint32_t viol = 0;
     uint64_t nev = 0, naux = 0;
-    int rc = wg_lf_refs(c, R, true);
+    int rc = wg_lf_refs(c, R, true, c->lane_scalars.as<uint32_t>());
     if (rc != WG_OK) return rc;
     rc = wg_lf_chain(c, R);                          // queued before the flags are back (bounded on any input)
     const int rc2 = wg_lf_refs_end(c, &viol, &nev, &naux);

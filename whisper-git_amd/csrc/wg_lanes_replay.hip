@@ -444,40 +444,28 @@ __global__ void k_lf_replay_init(uint64_t nchunks, unsigned long long *occ_prev,
     if (i < nflags) changed[i] = (i == 0) ? 1u : 0u;
 }
 
-// speculative build: the initial state, the slots' initial guess (zero) and
-// the 256 no-op records after the events (the replay prefetches past a
-// chunk's end) in one launch, with the event count read on the device
-__global__ void k_lf_replay_init_spec(uint64_t nchunks, unsigned long long *occ_prev, uint32_t *changed, uint32_t nflags,
-                                      uint4 *__restrict__ slots16, uint64_t nslots16, uint4 *__restrict__ ev,
-                                      const uint32_t *__restrict__ nev_dev) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nchunks) occ_prev[i] = 0ull;   // nchunks counts words
-    if (i < nflags) changed[i] = (i == 0) ? 1u : 0u;
-    if (i < nslots16) slots16[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (i < 256) ev[*nev_dev + i] = make_uint4(0u, 0u, 0u, 0u);
-}
-
 // final: max_lane / slots / overflow over all chunks (nev_dev: chunks past the
-// device event count hold nothing)
+// device event count hold nothing), by the first wave of the block
 // scal[3]: the first of iterations 1..iters that changed nothing (0: none) —
 // the iterations the next build launches before its first check
-__global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats, uint32_t *__restrict__ scal,
-                                   const uint32_t *__restrict__ flags, uint32_t iters, uint32_t slot_cap,
-                                   const uint32_t *__restrict__ nev_dev = nullptr, uint32_t chunk = 1) {
+__device__ void replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats, uint32_t *__restrict__ scal,
+                              const uint32_t *__restrict__ flags, uint32_t iters, uint32_t slot_cap,
+                              const uint32_t *__restrict__ nev_dev, uint32_t chunk) {
+    const uint32_t lid = threadIdx.x;   // < 64
     uint32_t fp = ~0u;
-    for (uint32_t i = 1 + threadIdx.x; i <= iters; i += blockDim.x)
+    for (uint32_t i = 1 + lid; i <= iters; i += 64)
         if (flags[i] == 0 && i < fp) fp = i;
     for (int d = 32; d >= 1; d >>= 1) {
         const uint32_t o = (uint32_t)__shfl_down((int)fp, d, 64);
         fp = o < fp ? o : fp;
     }
-    if (threadIdx.x == 0) scal[3] = fp == ~0u ? 0u : fp;
+    if (lid == 0) scal[3] = fp == ~0u ? 0u : fp;
     if (nev_dev) {
         const uint64_t nd = ((uint64_t)*nev_dev + chunk - 1) / chunk;
         nchunks = nd < nchunks ? nd : nchunks;
     }
     uint32_t ml = 0, ms = 0;
-    for (uint64_t c = threadIdx.x; c < nchunks; c += blockDim.x) {
+    for (uint64_t c = lid; c < nchunks; c += 64) {
         ml = stats[2 * c] > ml ? stats[2 * c] : ml;
         ms = stats[2 * c + 1] > ms ? stats[2 * c + 1] : ms;
     }
@@ -486,11 +474,37 @@ __global__ void k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict_
         ml = a > ml ? a : ml;
         ms = b > ms ? b : ms;
     }
-    if (threadIdx.x == 0) {
+    if (lid == 0) {
         scal[0] = ml;
         scal[1] = ms + 1;
         scal[2] = ms >= slot_cap ? 1u : 0u;   // the sentinel slot was handed out: the occupancy overflowed
     }
+}
+
+__global__ void __launch_bounds__(64) k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats,
+                                                        uint32_t *__restrict__ scal, const uint32_t *__restrict__ flags,
+                                                        uint32_t iters, uint32_t slot_cap) {
+    replay_finish(nchunks, stats, scal, flags, iters, slot_cap, nullptr, 1u);
+}
+
+// speculative fast path: the scalars (first wave of block 0), then per row the
+// slot of its chain's event = its lane (layouts.get(id), :278-283: ids are
+// distinct here, so the row is its own canonical row) and its colour
+__global__ void __launch_bounds__(256) k_lf_finish_lanes(uint64_t nchunks, const uint32_t *__restrict__ stats,
+                                                        uint32_t *__restrict__ scal, const uint32_t *__restrict__ rflags,
+                                                        uint32_t iters, uint32_t slot_cap, const uint32_t *__restrict__ nev_dev,
+                                                        uint32_t chunk, uint64_t nl, const uint32_t *__restrict__ sp,
+                                                        const uint16_t *__restrict__ slot_of, uint32_t *__restrict__ lane,
+                                                        uint32_t *__restrict__ lane_out, uint8_t *__restrict__ color_out,
+                                                        const uint8_t *__restrict__ flags, const uint32_t *__restrict__ gate) {
+    if (*gate) return;   // not well formed: the exact stages redo the lanes
+    if (blockIdx.x == 0 && threadIdx.x < 64) replay_finish(nchunks, stats, scal, rflags, iters, slot_cap, nev_dev, chunk);
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nl) return;
+    const uint32_t l = slot_of[sp[j] & ~WG_TOK_EV];
+    lane[j] = l;
+    lane_out[j] = l;
+    color_out[j] = (flags[j] & WG_FLAG_ORPHAN) ? (uint8_t)WG_COLOR_ORPHAN : (uint8_t)(l % 6u);
 }
 
 }  // namespace
@@ -543,10 +557,12 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
 }
 
 // Speculative build (no host read of the event count): R.nev is an upper
-// bound (the grid), R.nev_dev the count; `blind` iterations, then the
-// scalars.  The caller checks convergence (flags[it - 1], flags[it]) with
-// its end-of-build validation.
-hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blind, uint4 *ev_pad) {
+// bound (the grid), R.nev_dev the count.  The initial state (zero occupancy
+// guesses, the flag words, the slots' zero guess, the padding records) is
+// written by the event kernel; then `blind` iterations; the scalars are
+// reduced by the lanes kernel.  The caller checks convergence (flags[it - 1],
+// flags[it]) with its end-of-build validation.
+WgReplayInit wg_replay_prepare_spec(ReplayRun &R, uint32_t &blind) {
     R.nch = (R.nev + R.chunk - 1) / R.chunk;
     R.it = 0;
     R.sp_prev = R.slots_a;
@@ -555,13 +571,21 @@ hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t
     R.on = R.occ_b;
     if (R.max_iters > R.nch + 1) R.max_iters = (uint32_t)(R.nch + 1);
     if (blind > R.max_iters) blind = R.max_iters;
-    const uint64_t nslots16 = (R.nev * sizeof(uint16_t) + 15) / 16;
-    uint64_t ninit = R.nch > R.max_iters + 1 ? R.nch : R.max_iters + 1;
-    if (ninit < nslots16) ninit = nslots16;
-    if (ninit < R.nch * R.nw) ninit = R.nch * R.nw;
-    if (ninit < 256) ninit = 256;
-    hipLaunchKernelGGL(k_lf_replay_init_spec, dim3((ninit + 255) / 256), dim3(256), 0, s, R.nch * R.nw, R.occ_a, R.flags,
-                       R.max_iters + 1, reinterpret_cast<uint4 *>(R.slots_a), nslots16, ev_pad, R.nev_dev);
+    WgReplayInit I;
+    I.occ = R.occ_a;
+    I.occ_words = R.nch * R.nw;
+    I.changed = R.flags;
+    I.nflags = R.max_iters + 1;
+    I.slots16 = reinterpret_cast<uint4 *>(R.slots_a);
+    I.nslots16 = (R.nev * sizeof(uint16_t) + 15) / 16;
+    I.nev_dev = R.nev_dev;
+    uint64_t t = I.occ_words > I.nflags ? I.occ_words : I.nflags;
+    if (t < I.nslots16) t = I.nslots16;
+    I.total = t < 256 ? 256 : t;
+    return I;
+}
+
+hipError_t wg_replay_iterate_spec(hipStream_t s, ReplayRun &R, uint32_t blind) {
     for (uint32_t k = 0; k < blind; k++) {
         R.it++;
         ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, R.nev_dev,
@@ -570,8 +594,15 @@ hipError_t wg_replay_start_spec(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);
     }
-    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it,
-                       64u * R.nw - 1u, R.nev_dev, R.chunk);
+    return hipGetLastError();
+}
+
+hipError_t wg_replay_finish_lanes(hipStream_t s, const ReplayRun &R, uint64_t nl, const uint32_t *sp, uint32_t *lane,
+                                  uint32_t *lane_out, uint8_t *color_out, const uint8_t *flags) {
+    const uint64_t g = nl ? (nl + 255) / 256 : 1;
+    hipLaunchKernelGGL(k_lf_finish_lanes, dim3((uint32_t)g), dim3(256), 0, s, R.nch, (const uint32_t *)R.stats, R.scal,
+                       (const uint32_t *)R.flags, R.it, 64u * R.nw - 1u, R.nev_dev, R.chunk, nl, sp,
+                       (const uint16_t *)R.sp_prev, lane, lane_out, color_out, flags, R.gate);
     return hipGetLastError();
 }
 

@@ -144,6 +144,50 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan2_down(Pair32 P, uint64_t 
     if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
 }
 
+// down-sweep from producer tile sums (WgScanBs): a tile of SCAN_TILE elements
+// holds BS_PER_TILE producer blocks; its offset is the sum of the producer
+// sums before it — summed by the block itself (bpre null) or read from their
+// scanned form bpre (many tiles)
+constexpr uint64_t BS_PER_TILE = SCAN_TILE / WG_BS_THREADS;
+static_assert(SCAN_TILE % WG_BS_THREADS == 0, "producer blocks tile the scan tiles");
+struct ScanBsArgs {
+    const uint32_t *in[3];
+    uint32_t *out[3];
+    const uint32_t *bsum[3];
+    const uint32_t *bpre[3];   // exclusive scan of bsum, or null
+};
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_bs_down(ScanBsArgs P, uint64_t n) {
+    const int a = blockIdx.y;
+    const uint32_t *in = P.in[a];
+    uint32_t *out = P.out[a];
+    const uint64_t b0 = (uint64_t)blockIdx.x * BS_PER_TILE;
+    uint32_t ptot;
+    if (P.bpre[a]) {
+        ptot = P.bpre[a][b0];
+    } else {
+        uint32_t pre = 0;
+        for (uint64_t b = threadIdx.x; b < b0; b += SCAN_THREADS) pre += P.bsum[a][b];
+        (void)block_excl_scan<uint32_t>(pre, ptot);
+    }
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        v[k] = (base + k < n) ? in[base + k] : 0u;
+        s += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan<uint32_t>(s, tot) + ptot;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
+    }
+    if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
+    if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
+}
+
 uint64_t nblocks(uint64_t n) { return n == 0 ? 1 : (n + SCAN_TILE - 1) / SCAN_TILE; }
 
 template <class TO>
@@ -175,7 +219,11 @@ hipError_t scan_rec(const TI *in, TO *out, uint64_t n, char *tmp, hipStream_t s)
 
 }  // namespace
 
-size_t wg_scan_tmp_bytes(uint64_t n) { return tmp_bytes_rec<uint64_t>(n) + 1024; }
+size_t wg_scan_tmp_bytes(uint64_t n) {
+    // + wg_scan_bs_u32's scanned producer sums (three arrays) and their recursion
+    const uint64_t nbs = wg_bs_blocks(n);
+    return tmp_bytes_rec<uint64_t>(n) + 3 * (((nbs + 1) * 4 + 255) & ~size_t(255)) + tmp_bytes_rec<uint64_t>(nbs) + 1024;
+}
 
 hipError_t wg_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, void *tmp, hipStream_t s) {
     return scan_rec<uint32_t, uint32_t>(in, out, n, (char *)tmp, s);
@@ -197,6 +245,29 @@ hipError_t wg_exclusive_scan2_u32(const uint32_t *in0, uint32_t *out0, const uin
     P.bsum[1] = P.bsum[0] + ((nb + 63) & ~63ull);   // wg_scan_tmp_bytes holds (nb + 1) u64 >= 2 * (nb + 64) u32
     hipLaunchKernelGGL(k_scan2_reduce, dim3((uint32_t)nb, 2), dim3(SCAN_THREADS), 0, s, P, n);
     hipLaunchKernelGGL(k_scan2_down, dim3((uint32_t)nb, 2), dim3(SCAN_THREADS), 0, s, P, n);
+    return hipGetLastError();
+}
+
+hipError_t wg_scan_bs_u32(const WgScanBs &S, uint64_t n, void *tmp, hipStream_t s) {
+    ScanBsArgs P{};
+    const uint64_t nbs = wg_bs_blocks(n);
+    char *t = (char *)tmp;
+    for (int a = 0; a < S.na; a++) {
+        P.in[a] = S.in[a];
+        P.out[a] = S.out[a];
+        P.bsum[a] = S.bsum[a];
+        P.bpre[a] = nullptr;
+        if (nbs > WG_BS_SELF) {   // many tiles: scan the producer sums first (one array of the tmp at a time)
+            uint32_t *pre = reinterpret_cast<uint32_t *>(t);
+            t += ((nbs + 1) * 4 + 255) & ~size_t(255);
+            hipError_t e = scan_rec<uint32_t, uint32_t>(S.bsum[a], pre, nbs, t, s);
+            if (e != hipSuccess) return e;
+            P.bpre[a] = pre;
+        }
+    }
+    if (nbs > WG_BS_SELF && (size_t)(t - (char *)tmp) + tmp_bytes_rec<uint64_t>(nbs) > wg_scan_tmp_bytes(n))
+        return hipErrorInvalidValue;   // (cannot happen: 3 (n/256 + 65) u32 + the recursion fit the reserve)
+    hipLaunchKernelGGL(k_scan_bs_down, dim3((uint32_t)nblocks(n), (uint32_t)S.na), dim3(SCAN_THREADS), 0, s, P, n);
     return hipGetLastError();
 }
 
