@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--device-transport", action="store_true",
                     help="gloo rehearsal: move HIP-resident slots through gloo (the stream-ordered slot path of RCCL)")
+    ap.add_argument("--no-defer", action="store_true",
+                    help="validate every speculative build before build() returns (WG_OPT_DEFER_VALIDATION off)")
     ap.add_argument("--all-stage-events", action="store_true",
                     help="record every stage's HIP events inside the timed region (default: only the emission "
                          "kernel's, for the roofline; the stage breakdown comes from a separate pass)")
@@ -393,6 +395,7 @@ def build_lifecycle(dag, dev, torch, args, pal):
     k1, c1 = upload(fresh)
     eng = wgraph.Engine(dev.index)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    eng.set_defer_validation(not args.no_defer)
 
     def step(k, c, n):
         torch.cuda.synchronize()
@@ -475,9 +478,18 @@ def main():
     commits.parent_off, commits.parent_oid = t_poff.data_ptr(), t_poid.data_ptr()
     commits.flags, commits.residency = t_flags.data_ptr(), abi.WG_DEVICE
 
+    # one non-default stream for the engine, the events and the collectives:
+    # the default stream's handle is 0, which wg_set_stream takes as "a stream
+    # of the engine's own" (then the device-packed exchange slots could not be
+    # ordered with RCCL, and ShardComm falls back to host copies)
+    stream = torch.cuda.Stream(dev)
+    stream.wait_stream(torch.cuda.current_stream(dev))
+    torch.cuda.set_stream(stream)
     eng = wgraph.Engine(dev_idx)
-    stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
+    # a step's build is validated with its emission's vertex-total read (one
+    # host wait per step, while the emission runs) instead of mid-step
+    eng.set_defer_validation(not args.no_defer)
     pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
     selected = shard0 + 7
     comm = None

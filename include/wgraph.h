@@ -205,6 +205,22 @@ int         wg_synchronize(wg_ctx *ctx);
  * only the vertex-emission stage ("vtx_emit"), so a timed loop carries two
  * events per step instead of two per stage; 0 = every stage (default). */
 #define WG_OPT_TIMING_EMIT_ONLY 4
+/* WG_OPT_DEFER_VALIDATION: 1 = a speculative wg_layout_build (every build
+ * after one that sized the context's buffers) returns without its
+ * end-of-build host read: its validation words are read with the vertex total
+ * of the next wg_emit_vertices, or by the next call that needs the layout on
+ * the host (summaries, copies, device views, glyphs, shards, ...).  A build
+ * that did not hold is redone there by the exact stages, followed by the frame
+ * pass (wg_row_geometry) and the emission queued after it: results are always
+ * identical.  Device-resident commit inputs must stay valid until that call
+ * (a redo reads them; device bands are kept by the engine).  Default 0: every
+ * build validates before it returns. */
+#define WG_OPT_DEFER_VALIDATION 5
+/* WG_OPT_REPLAY_WARMUP: the lane-event replay's first iteration starts this
+ * many events (multiple of 64, 0..3584) before each chunk, so chunk entry
+ * states are mostly right before the second iteration.  Speed only, never
+ * results. */
+#define WG_OPT_REPLAY_WARMUP 6
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------

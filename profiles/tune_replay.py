@@ -20,7 +20,8 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--kind", default="wide16")
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--chunks", default="64,128,192,256,384,512,1024")
+    ap.add_argument("--chunks", default="64,128,192,256,384,512,1024",
+                    help="chunk sizes, or chunk:warm pairs (WG_OPT_REPLAY_WARMUP)")
     args = ap.parse_args()
     import torch
     import wgraph
@@ -34,12 +35,15 @@ def main():
     c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
     c.residency = abi.WG_DEVICE
     ref = None
-    for ch in [int(x) for x in args.chunks.split(",")]:
+    for spec in args.chunks.split(","):
+        ch, warm = (int(v) for v in spec.split(":")) if ":" in spec else (int(spec), 0)
         # a fresh engine per chunk size: the replay's blind iteration count
         # adapts per context and must not carry over from another chunk size
         eng = wgraph.Engine(0)
         eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         eng._check(lib().wg_set_option(eng._ctx, 2, ch))
+        eng._check(lib().wg_set_option(eng._ctx, 6, warm))
+        eng.set_defer_validation(True)
 
         def step():
             eng.build(commits=c)
@@ -62,9 +66,9 @@ def main():
         same = True if ref is None else bool((lane == ref).all())
         ref = lane if ref is None else ref
         dbg = eng.debug_counters()
-        print(json.dumps({"chunk": ch, "step_ms": round(ms, 4), "lf_loop_ms": round(st.get("lf_loop", 0), 4),
+        print(json.dumps({"kind": args.kind, "rows": args.rows, "chunk": ch, "warm": warm, "step_ms": round(ms, 4), "lf_loop_ms": round(st.get("lf_loop", 0), 4),
                           "lanes_ms": round(st.get("lanes", 0), 4), "same_lanes": same,
-                          "debug": [int(x) for x in dbg[:8]]}), flush=True)
+                          "debug": [int(x) for x in dbg[:12]]}), flush=True)
         eng.close()
 
 

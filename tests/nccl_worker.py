@@ -35,8 +35,13 @@ def main():
     errors = []
     try:
         comm = ShardComm(dev, initial_cap=64)
+        # a non-default stream shared with torch (its collectives and slot
+        # buffers): handle 0, the default stream, would give the engine one of its own
+        ts = torch.cuda.Stream(dev)
+        ts.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(ts)
         eng = wgraph.Engine(0)
-        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        eng.set_stream(ts.cuda_stream)
 
         def read_heads(ptr, stride):
             h = np.empty(3 * comm.world, np.uint64)

@@ -123,8 +123,13 @@ def main():
         from wgraph.shard import ShardComm
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
+        # a non-default stream shared with torch (its collectives and slot
+        # buffers): handle 0, the default stream, would give the engine one of its own
+        ts = torch.cuda.Stream(dev)
+        ts.wait_stream(torch.cuda.current_stream(dev))
+        torch.cuda.set_stream(ts)
         eng = wgraph.Engine(0)
-        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        eng.set_stream(ts.cuda_stream)
         comm = ShardComm(dev, initial_cap=16, device_transport=args.transport == "device")
         for case in args.cases.split(","):
             kind, n, seed = case.split(":")

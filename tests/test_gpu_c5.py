@@ -38,11 +38,17 @@ def test_c5_eight_shards_full_size():
     c.n_commits, c.n_parents = d.n, d.e
     c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
     c.residency = abi.WG_DEVICE
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # a non-default stream shared by the engines and torch (the default
+    # stream's handle 0 would give each engine a stream of its own, unordered
+    # with torch's reads of the packed slots)
+    ts = torch.cuda.Stream(dev)
+    ts.wait_stream(torch.cuda.current_stream(dev))
+    stream_ctx = torch.cuda.stream(ts)
+    stream_ctx.__enter__()
     engines = [wgraph.Engine(0) for _ in range(world)]
     try:
         for e in engines:
-            e.set_stream(stream)
+            e.set_stream(ts.cuda_stream)
         rng = [(g["row_begin"], g["row_end"]) for g in gold["ranks"]]
         _lockstep(engines, lambda e, r, m: lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), world, r,
                                                                        rng[r][0], rng[r][1], m))
@@ -64,5 +70,6 @@ def test_c5_eight_shards_full_size():
     finally:
         for e in engines:
             e.close()
+        stream_ctx.__exit__(None, None, None)
         del keep
         torch.cuda.empty_cache()

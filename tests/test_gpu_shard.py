@@ -134,7 +134,8 @@ def _lockstep(engines, begin):
         engines[0]._check(lib().wg_shard_slot_heads(engines[0]._ctx, slots.data_ptr(), stride, W, polled.ctypes.data))
         polled = polled.reshape(W, 3)
         assert [int(x) for x in polled[:, 0]] == sizes
-        assert np.array_equal(np.ascontiguousarray(polled[:, 1:3]).view(np.uint32).reshape(W, 4), heads)
+        ph = np.ascontiguousarray(polled[:, 1:3]).view(np.uint32).reshape(W, 4)
+        assert np.array_equal(ph, heads), f"round {rounds} step {int(msgs[0].step)} sizes {sizes}: polled {ph.tolist()} heads {heads.tolist()}"
         sz = (ctypes.c_uint64 * W)(*sizes)
         for r, e in enumerate(engines):
             e._check(lib().wg_shard_exchange(e._ctx, slots.data_ptr() + ShardComm.HDR, stride, sz,
@@ -169,12 +170,18 @@ def test_packed_slots_in_one_process(world, kind, n):
     c.n_commits, c.n_parents = d.n, d.e
     c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
     c.residency = abi.WG_DEVICE
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # one non-default stream for the engines and torch: the default stream's
+    # handle is 0, which wg_set_stream takes as "a stream of the engine's own"
+    # (unordered with torch's reads of the slots)
+    ts = torch.cuda.Stream(dev)
+    ts.wait_stream(torch.cuda.current_stream(dev))
+    stream_ctx = torch.cuda.stream(ts)
+    stream_ctx.__enter__()
     engines = [wgraph.Engine(0) for _ in range(world)]
     o = oracle_c.OracleLayout(d)
     try:
         for e in engines:
-            e.set_stream(stream)
+            e.set_stream(ts.cuda_stream)
         rng = [shard_rows(d.n, world, r) for r in range(world)]
         _lockstep(engines, lambda e, r, m: lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), world, r,
                                                                        rng[r][0], rng[r][1], m))
@@ -196,4 +203,5 @@ def test_packed_slots_in_one_process(world, kind, n):
         o.close()
         for e in engines:
             e.close()
+        stream_ctx.__exit__(None, None, None)
         del keep

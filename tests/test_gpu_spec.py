@@ -68,3 +68,53 @@ def test_speculative_build_sequence():
         assert redo[7][1:] == redo[6][1:]             # the Linux-shaped list again: blind count adapted, no redo
     finally:
         eng.close()
+
+
+def test_deferred_validation_sequence():
+    """WG_OPT_DEFER_VALIDATION: each build is validated by the emission's
+    vertex-total read (build -> banded frame pass -> emission with no host
+    read between them); a build that does not hold is redone there together
+    with the frame pass and the emission.  The same branch-walking sequence,
+    every step bit-exact against the oracle; every other build also goes
+    through the settle path of a host query right after the build."""
+    import wgraph
+    from oracle import oracle_c
+    eng = wgraph.Engine(0)
+    try:
+        eng.set_defer_validation(True)
+        seq = [("wide16", 3000, 1), ("wide16", 3000, 1), ("wide16", 40000, 3), ("anomaly", 2000, 4),
+               ("random13", 20000, 5), ("linux", 60000, 6), ("linux", 60000, 6), ("skew", 30000, 8),
+               ("linear", 500, 7), ("wide16", 40000, 3), ("linuxwide", 20000, 9)]
+        last = None
+        for i, (kind, n, seed) in enumerate(seq):
+            d = synth.generate(kind, n, seed=seed)
+            o = oracle_c.OracleLayout(d)
+            tag = f"#{i} {kind}/{n}"
+            eng.build(d)
+            if i % 2:   # a host query settles the build first
+                s = eng.layout_summary()
+                assert s.max_lane == o.max_lane, tag
+                got = eng.geometry()
+                for k, v in o.geometry.items():
+                    assert_bits(f"{tag} build_{k}", got[k], v)
+            eng.row_geometry(d.band)
+            sel = d.n // 3
+            eng.emit_vertices(0, d.n, selected=sel)   # validates a deferred build
+            og = o.row_geometry(d.band)
+            ov, _ = o.emit_vertices(0, d.n, selected=sel)
+            assert eng.vertex_summary().checksum == oracle_c.vertex_checksum(ov), tag
+            assert eng.vertex_summary().n_vertices == len(ov), tag
+            got = eng.geometry()
+            for k, v in og.items():
+                assert_bits(f"{tag} band_{k}", got[k], v)
+            lane, color = eng.lanes()
+            assert_bits(tag + " lane", lane, o.lane)
+            assert_bits(tag + " color", color, o.color)
+            assert_bits(tag + " edges", eng.edges(), o.edges)
+            assert eng.layout_summary().max_lane == o.max_lane, tag
+            o.close()
+            last = eng.debug_counters()
+        assert int(last[6]) == len(seq) - 1   # every build after the first speculated
+        assert int(last[8]) >= 2              # and some were redone (capacity, well-formedness)
+    finally:
+        eng.close()

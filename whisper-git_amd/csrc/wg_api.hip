@@ -205,14 +205,86 @@ int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out) {
 }
 
 int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items) {
+    return wg_fetch_begin_n(c, (int)items.size(), items.begin());
+}
+
+int wg_fetch_begin_n(wg_ctx *c, int n, const WgFetch *items) {
     if (c->fetch_pending) {   // left behind by a failed call: drop it
         (void)hipEventSynchronize(c->ev_fetch);
         c->fetch_pending = 0;
     }
-    if (const int rc = fetch_launch(c, (int)items.size(), items.begin(), FETCH_MAX)) return rc;
+    if (const int rc = fetch_launch(c, n, items, FETCH_MAX)) return rc;
     if (!c->ev_fetch) WG_HIP(c, hipEventCreateWithFlags(&c->ev_fetch, hipEventDisableTiming));
     WG_HIP(c, hipEventRecord(c->ev_fetch, c->stream));
-    c->fetch_pending = (int)items.size();
+    c->fetch_pending = n;
+    return WG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Deferred validation of a speculative build (WG_OPT_DEFER_VALIDATION)
+// ---------------------------------------------------------------------------
+int wg_settle(wg_ctx *c) {
+    if (!c->pend.build) return WG_OK;
+    uint64_t v[WG_PENDING_ITEMS] = {0};
+    if (const int rc = wg_fetch_n(c, c->pend.k, c->pend.it, v)) return rc;
+    bool redone = false;
+    return wg_validate_pending(c, v, &redone);
+}
+
+// The end-of-build check of wg_layout_build on words v (WG_PENDING_ITEMS);
+// what did not hold is redone by the exact stages.  After a deferred build:
+// the frame pass and the emission queued since are redone as well.
+static int build_check(wg_ctx *c, const uint64_t *v, int kl, int k, bool *redo) {
+    const uint64_t ne = v[k - 1];
+    const bool lanes_ok = wg_lanes_spec_check(c, v);
+    int rc;
+    if (!lanes_ok) {   // the exact lane stage (fast path with its reads, or the general walk)
+        if ((rc = wg_stage_lanes(c, false)) != WG_OK) return rc;
+        if ((rc = wg_stage_edges(c, false, (int64_t)ne)) != WG_OK) return rc;
+        c->layout_gen++;
+    } else {
+        c->n_edges = ne;
+        const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
+        const float gw = (float)vis * WG_LANE_W;   // graph_width (:353-354)
+        c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
+    }
+    c->spec_builds++;
+    c->spec_redo_lanes += !lanes_ok;
+    *redo = !lanes_ok || !wg_geom_spec_check(c, v + kl);
+    if (*redo) {
+        c->spec_redo_geom++;
+        c->lists_gen = ~0ull;
+        c->spec = false;
+        if ((rc = wg_side_join(c)) != WG_OK) return rc;
+        if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
+    }
+    c->spec_ready = c->lists_gen == c->layout_gen;   // an exact or validated build: the buffers are sized
+    c->have_geom = true;
+    c->geom_key_gen = c->layout_gen;   // the geometry of (this layout, no bands)
+    c->geom_key_band = false;
+    return WG_OK;
+}
+
+static int row_geometry_impl(wg_ctx *c, const float *band, int32_t residency);
+
+int wg_validate_pending(wg_ctx *c, const uint64_t *v, bool *redone) {
+    *redone = false;
+    if (!c->pend.build) return WG_OK;
+    const PendingBuild P = c->pend;
+    c->pend = PendingBuild{};
+    bool redo = false;
+    int rc = build_check(c, v, P.kl, P.k, &redo);
+    if (rc != WG_OK || !redo) return rc;
+    *redone = true;
+    if (P.frame && (rc = row_geometry_impl(c, P.frame_band ? c->band_prev.as<const float>() : nullptr, WG_DEVICE)) != WG_OK)
+        return rc;
+    if (P.emit) {
+        const ShardState &S = c->sh;
+        const int64_t sel_l = (P.sel >= 0 && (uint64_t)P.sel >= S.s && (uint64_t)P.sel < S.e)
+                                  ? (int64_t)((uint64_t)P.sel - S.s + S.row_base) : -1;
+        if ((rc = wg_stage_vertices(c, P.rb - S.s + S.row_base, P.re - S.s + S.row_base, sel_l)) != WG_OK) return rc;
+        c->have_vtx = true;
+    }
     return WG_OK;
 }
 
@@ -323,6 +395,7 @@ const char *wg_last_error(const wg_ctx *c) { return c ? c->err.c_str() : "null c
 
 int wg_set_stream(wg_ctx *c, void *s) {
     if (!c) return WG_E_INVALID;
+    WG_SETTLE(c);
     (void)hipSetDevice(c->device);
     if (c->own_stream && c->stream) {
         WG_HIP(c, hipStreamSynchronize(c->stream));
@@ -345,6 +418,14 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         c->replay_chunk = (uint32_t)value;
         return WG_OK;
     case WG_OPT_TIMING_EMIT_ONLY: c->timing_emit_only = value != 0; return WG_OK;
+    case WG_OPT_REPLAY_WARMUP:
+        if (value < 0 || value > 3584 || (value & 63)) return wg_fail(c, WG_E_INVALID, "replay warm-up must be a multiple of 64 in 0..3584");
+        c->replay_warm = (uint32_t)value;
+        return WG_OK;
+    case WG_OPT_DEFER_VALIDATION:
+        WG_SETTLE(c);
+        c->defer_validation = value != 0;
+        return WG_OK;
     case WG_OPT_SWEEP_REG:
         if (value < 0 || value > 512) return wg_fail(c, WG_E_INVALID, "sweep register capacity must be 0..512");
         c->sweep_reg_cap = (uint32_t)value;
@@ -355,6 +436,7 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
 
 int wg_synchronize(wg_ctx *c) {
     if (!c) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (wg_side_join(c) != WG_OK) return WG_E_HIP;
     WG_HIP(c, hipStreamSynchronize(c->stream));
     return WG_OK;
@@ -364,6 +446,7 @@ int wg_synchronize(wg_ctx *c) {
 // GraphLayout::build (:265-355)
 // ---------------------------------------------------------------------------
 int wg_layout_build(wg_ctx *c, const wg_commits *in) {
+    if (c) WG_SETTLE(c);
     if (!c || !in) return WG_E_INVALID;
     (void)hipSetDevice(c->device);
     c->have_layout = c->have_geom = c->have_vtx = c->have_text = false;
@@ -450,34 +533,39 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
     if ((rc = wg_side_join(c)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
     if (spec) {
-        constexpr int K = WG_LANES_SPEC_ITEMS + WG_GEOM_SPEC_ITEMS + 1;
-        static_assert(K <= FETCH_MAX, "validation words exceed one fetch");
+        constexpr int K = WG_PENDING_ITEMS;
+        static_assert(K + 1 <= FETCH_MAX, "validation words exceed one fetch");
         WgFetch it[K];
         const int kl = wg_lanes_spec_items(c, it);
         int k = kl + wg_geom_spec_items(c, it + kl);
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + n, false};
+        c->spec = false;
+        if (c->defer_validation) {
+            // no host read: the words are read with the next emission's vertex
+            // total (or by the next call that needs the layout on the host).
+            // Until then the lists are taken as the build's (a frame pass on
+            // this layout reuses them, grids sized by their capacities) and
+            // the emission takes graph_width from the device.
+            PendingBuild &P = c->pend;
+            P = PendingBuild{};
+            P.build = true;
+            P.k = k;
+            P.kl = kl;
+            for (int i = 0; i < k; i++) P.it[i] = it[i];
+            c->lists_gen = c->layout_gen;
+            c->lists_n = n;
+            c->lists_ne = c->n_edges;
+            c->lists_nsuper = c->spec_nsuper_grid;
+            c->geom_sum_stale = false;
+            c->have_geom = true;
+            c->geom_key_gen = c->layout_gen;
+            c->geom_key_band = false;
+            return WG_OK;
+        }
         uint64_t v[K] = {0};
         if ((rc = wg_fetch_n(c, k, it, v)) != WG_OK) return rc;
-        c->spec = false;
-        const uint64_t ne = v[k - 1];
-        const bool lanes_ok = wg_lanes_spec_check(c, v);
-        if (!lanes_ok) {   // the exact lane stage (fast path with its reads, or the general walk)
-            if ((rc = wg_stage_lanes(c, false)) != WG_OK) return rc;
-            if ((rc = wg_stage_edges(c, false, (int64_t)ne)) != WG_OK) return rc;
-            c->layout_gen++;
-        } else {
-            c->n_edges = ne;
-            const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
-            const float gw = (float)vis * WG_LANE_W;   // graph_width (:353-354)
-            c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
-        }
-        c->spec_builds++;
-        c->spec_redo_lanes += !lanes_ok;
-        if (!lanes_ok || !wg_geom_spec_check(c, v + kl)) {
-            c->spec_redo_geom++;
-            c->lists_gen = ~0ull;
-            if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
-        }
+        bool redo = false;
+        return build_check(c, v, kl, k, &redo);
     }
     c->spec_ready = c->lists_gen == c->layout_gen;   // an exact or validated build: the buffers are sized
     c->have_geom = true;
@@ -488,6 +576,7 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
 
 int wg_layout_summary_get(wg_ctx *c, wg_layout_summary *out) {
     if (!c || !out) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
     const ShardState &S = c->sh;
     out->n_rows = S.e - S.s;
@@ -510,6 +599,7 @@ int wg_layout_summary_get(wg_ctx *c, wg_layout_summary *out) {
 
 int wg_copy_lanes(wg_ctx *c, uint32_t *lane, uint8_t *color) {
     if (!c) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
     const uint64_t rows = c->sh.e - c->sh.s, b = c->sh.row_base;
     if (lane && rows)
@@ -522,6 +612,7 @@ int wg_copy_lanes(wg_ctx *c, uint32_t *lane, uint8_t *color) {
 
 int wg_copy_edges(wg_ctx *c, wg_edge *edges) {
     if (!c || !edges) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
     const ShardState &S = c->sh;
     if (S.on && !S.replicated) {
@@ -544,6 +635,7 @@ int wg_copy_edges(wg_ctx *c, wg_edge *edges) {
 
 int wg_copy_row_heights(wg_ctx *c, float *h) {
     if (!c || !h) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
     const uint64_t rows = c->sh.e - c->sh.s;
     if (rows) WG_HIP(c, hipMemcpyAsync(h, c->heights.as<float>() + c->sh.row_base, rows * 4, hipMemcpyDeviceToHost, c->stream));
@@ -586,6 +678,15 @@ __global__ void k_band_diff(const uint32_t *__restrict__ a, const uint32_t *__re
 
 int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
     if (!c) return WG_E_INVALID;
+    if (c->pend.build) {   // a deferred build: this pass is redone with it if it does not hold
+        c->pend.frame = true;
+        c->pend.frame_band = band != nullptr;
+        c->pend.emit = false;
+    }
+    return row_geometry_impl(c, band, residency);
+}
+
+static int row_geometry_impl(wg_ctx *c, const float *band, int32_t residency) {
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
     if (c->sh.on && !c->sh.replicated) return wg_fail(c, WG_E_STATE, "sharded layout: use wg_shard_geometry_begin");
     (void)hipSetDevice(c->device);
@@ -653,6 +754,7 @@ static int own_geometry_range(wg_ctx *c, uint64_t *v0, uint64_t *v1, uint64_t *c
 
 int wg_geometry_summary_get(wg_ctx *c, wg_geometry_summary *out) {
     if (!c || !out) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
     if (const int rc = wg_geom_summary_sync(c)) return rc;
     out->n_rows = c->sh.e - c->sh.s;
@@ -677,6 +779,7 @@ int wg_geometry_summary_get(wg_ctx *c, wg_geometry_summary *out) {
 
 int wg_copy_geometry(wg_ctx *c, const wg_geometry_host *d) {
     if (!c || !d) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
     if (const int rc = wg_geom_summary_sync(c)) return rc;
     const uint64_t n = c->sh.e - c->sh.s, b = c->sh.row_base;
@@ -718,6 +821,12 @@ int wg_emit_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel, const flo
                        (unsigned long long)re, (unsigned long long)S.s, (unsigned long long)S.e);
     (void)hipSetDevice(c->device);
     c->have_vtx = false;
+    if (c->pend.build) {   // a deferred build: validated by this call's vertex-total read (wg_stage_vertices)
+        c->pend.emit = true;
+        c->pend.rb = rb;
+        c->pend.re = re;
+        c->pend.sel = sel;
+    }
     WG_ALLOC(c, c->palette, 2 * WG_PALETTE_SIZE * 4 * sizeof(float));
     if (!c->palette_valid || std::memcmp(c->palette_host, palette, WG_PALETTE_SIZE * 4 * sizeof(float)) != 0) {   // upload on change only
         // entries 8..15: the same colours at opacity WG_DIM_ALPHA (search dimming)
@@ -742,6 +851,7 @@ int wg_emit_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel, const flo
 
 int wg_vertex_summary_get(wg_ctx *c, wg_vertex_summary *out) {
     if (!c || !out) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_vtx) return wg_fail(c, WG_E_STATE, "no vertices emitted");
     out->row_begin = c->vrow_begin;
     out->row_end = c->vrow_end;
@@ -755,6 +865,7 @@ int wg_vertex_summary_get(wg_ctx *c, wg_vertex_summary *out) {
 
 int wg_copy_vertices(wg_ctx *c, uint64_t first, uint64_t count, wg_vertex *dst) {
     if (!c || (!dst && count)) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_vtx) return wg_fail(c, WG_E_STATE, "no vertices emitted");
     if (first > c->n_vtx || count > c->n_vtx - first) return wg_fail(c, WG_E_INVALID, "vertex range out of bounds");
     if (count)
@@ -765,6 +876,7 @@ int wg_copy_vertices(wg_ctx *c, uint64_t first, uint64_t count, wg_vertex *dst) 
 
 int wg_copy_vertex_offsets(wg_ctx *c, uint64_t *dst) {
     if (!c || !dst) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_vtx) return wg_fail(c, WG_E_STATE, "no vertices emitted");
     WG_HIP(c, hipMemcpyAsync(dst, c->vtx_off.p, (c->vrow_end - c->vrow_begin + 1) * 8, hipMemcpyDeviceToHost, c->stream));
     WG_HIP(c, hipStreamSynchronize(c->stream));
@@ -773,6 +885,7 @@ int wg_copy_vertex_offsets(wg_ctx *c, uint64_t *dst) {
 
 int wg_device_views_get(wg_ctx *c, wg_device_views *o) {
     if (!c || !o) return WG_E_INVALID;
+    WG_SETTLE(c);
     std::memset(o, 0, sizeof(*o));
     const uint64_t b = c->sh.row_base;   // views start at the first own row
     if (c->have_layout) {
@@ -799,6 +912,7 @@ int wg_device_views_get(wg_ctx *c, wg_device_views *o) {
 
 int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
     if (!c || !out || n < 0) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (n > 16) n = 16;
     if (!c->lane_scalars.p) return wg_fail(c, WG_E_STATE, "no layout built");
     WG_HIP(c, hipMemcpyAsync(out, c->lane_scalars.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));

@@ -37,8 +37,13 @@ constexpr uint32_t RF_ZERO = 1u, RF_CHILD = 2u, RF_PARENT = 4u;
 struct Cap {
     const uint32_t *total;   // the list's scanned total (device)
     uint32_t cap;
+    // a frame pass on a build not validated yet (WG_OPT_DEFER_VALIDATION): the
+    // build pass's error words (sweep error [0], capacity overflow [8]); set,
+    // its lists are incomplete and nothing may read them
+    const uint32_t *gate;
 };
 __device__ __forceinline__ bool over(Cap a, uint32_t *ovf) {
+    if (a.gate && (a.gate[0] | a.gate[8])) return true;
     if (a.cap == ~0u || *a.total <= a.cap) return false;
     if (threadIdx.x == 0) atomicOr(ovf, 1u);
     return true;
@@ -56,7 +61,8 @@ __device__ __forceinline__ uint32_t pack_vert(uint32_t lane, uint32_t kind, uint
 __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
                             const float *__restrict__ row_top, float *__restrict__ height, float *__restrict__ node_y,
                             uint8_t *__restrict__ rowflags, uint64_t lo = 0, uint4 *__restrict__ zws = nullptr,
-                            uint64_t nz4 = 0, float *__restrict__ band_keep = nullptr) {
+                            uint64_t nz4 = 0, float *__restrict__ band_keep = nullptr,
+                            const uint8_t *__restrict__ flags_ref = nullptr, uint32_t *__restrict__ diff = nullptr) {
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t i = tid; i < nz4; i += (uint64_t)gridDim.x * blockDim.x) zws[i] = make_uint4(0u, 0u, 0u, 0u);
     uint64_t r = lo + tid;
@@ -80,36 +86,103 @@ __global__ void k_row_basic(uint64_t n, const float *__restrict__ h, const float
     if (bot - node_abs < 1e-4f) f |= RF_CHILD;  // strip [child_y, row_bot]
     if (node_abs - top < 1e-4f) f |= RF_PARENT; // strip [row_top, parent_y]
     rowflags[r] = f;
+    if (diff && flags_ref[r] != f) atomicOr(diff, 1u);   // the flags the curve lists were filtered with differ
 }
 
-// per-row list counts (difference arrays for the spans) and the sweep's
-// carry-in counts per 64-row chunk (carry_diff), in two passes: the child
-// side per row over the row's edges (edges are in child order: plain stores,
-// one carry count per wave, whose 64 rows share a chunk), then the parent
-// side per edge with atomics (:526-528: child_row >= parent_row adds nothing)
-__global__ void __launch_bounds__(256) k_edge_counts_child(uint64_t n, const uint32_t *__restrict__ edge_off,
-                                                           const wg_edge *__restrict__ edges, uint32_t *cntB,
-                                                           uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend,
-                                                           uint32_t *carry_diff) {
+// The full pass's first kernel, one thread per row:
+//   * the row's edges (:301-320; when the layout stage left them to this pass:
+//     prow != null) or their records (edges in place);
+//   * RowGeometry {height, node_y} and the strip flags (k_row_basic);
+//   * the child side of the per-row list counts (difference arrays for the
+//     spans) and the sweep's carry-in counts per 64-row chunk (carry_diff):
+//     edges are in child order, so these are plain stores, one carry count
+//     per wave (its 64 rows share a chunk); the parent side follows per edge
+//     with atomics (k_edge_counts, :526-528: child_row >= parent_row adds
+//     nothing);
+//   * the zeros the later atomics and fills start from (cntT, top_fill,
+//     carry_fill, the flag words, the all-zero flag row) — every other count
+//     array is written here in full.
+struct EdgeRowsArgs {
+    const uint32_t *edge_off;
+    const uint32_t *poff;      // null: edges in place
+    const int32_t *prow;
+    const uint32_t *lane_out;
+    const uint8_t *color_out;
+    wg_edge *edges;
+    const float *h, *band, *row_top;
+    float *height, *node_y, *band_keep;
+    uint8_t *rowflags, *zflags;
+    uint32_t *cntB, *diffF, *diffC, *cntCend, *carry_diff, *cntT, *top_fill, *carry_fill, *misc;
+};
+__global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) {
     static_assert(WG_SWEEP_CH == 64, "a wave's rows are one sweep chunk");
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t b = 0, f = 0, cc = 0, ce = 0, cd = 0;
+    uint32_t cd = 0;
     if (r < n) {
-        for (uint32_t k = edge_off[r]; k < edge_off[r + 1]; k++) {
-            const wg_edge e = edges[k];
-            const uint32_t c = e.child_row, p = e.parent_row;
-            if (c >= p) continue;
+        uint32_t b = 0, f = 0, cc = 0, ce = 0;
+        auto count = [&](uint32_t c, uint32_t p, bool same) {
+            if (c >= p) return;
             cd += c / WG_SWEEP_CH + 1 <= p / WG_SWEEP_CH;
-            if (e.child_lane == e.parent_lane) { b++; f += c + 1 < p; }
+            if (same) { b++; f += c + 1 < p; }
             else { cc += c + 1 < p; ce++; }   // (the swept lists' flag row is all zero: no child-end filter)
+        };
+        if (A.prow) {
+            uint32_t o = A.edge_off[r];
+            const uint32_t cl = A.lane_out[r], col = A.color_out[r];
+            for (uint32_t k = A.poff[r]; k < A.poff[r + 1]; k++) {
+                const int32_t p = A.prow[k];
+                if (p < 0) continue;
+                wg_edge e;
+                e.child_row = (uint32_t)r;
+                e.child_lane = cl;
+                e.parent_row = (uint32_t)p;
+                e.parent_lane = A.lane_out[p];
+                e.color = col;
+                A.edges[o] = e;
+                o++;
+                count(e.child_row, e.parent_row, e.child_lane == e.parent_lane);
+            }
+        } else {
+            for (uint32_t k = A.edge_off[r]; k < A.edge_off[r + 1]; k++) {
+                const wg_edge e = A.edges[k];
+                count(e.child_row, e.parent_row, e.child_lane == e.parent_lane);
+            }
         }
-        cntB[r] = b;
-        diffF[r + 1] = f;
-        diffC[r + 1] = cc;
-        cntCend[r] = ce;
+        A.cntB[r] = b;
+        A.diffF[r + 1] = f;
+        A.diffC[r + 1] = cc;
+        A.cntCend[r] = ce;
+        A.cntT[r] = 0u;
+        A.top_fill[r] = 0u;
+        A.zflags[r] = 0;
+        // RowGeometry (k_row_basic)
+        float ht, ny;
+        if (A.band) {
+            const float bd = A.band[r];
+            if (A.band_keep) A.band_keep[r] = bd;
+            ht = roundf(A.h[r] + bd);        // (h + band).round()  (:389)
+            ny = roundf(bd + WG_NODE_Y);     // (band + NODE_Y).round() (:390)
+        } else {
+            ht = A.h[r];                     // build(): height = h, node_y = NODE_Y (:339-341)
+            ny = WG_NODE_Y;
+        }
+        A.height[r] = ht;
+        A.node_y[r] = ny;
+        const float top = A.row_top[r], bot = A.row_top[r + 1];
+        const float node_abs = top + ny;
+        uint8_t fl = 0;
+        if (bot - top < 1e-4f) fl |= RF_ZERO;
+        if (bot - node_abs < 1e-4f) fl |= RF_CHILD;
+        if (node_abs - top < 1e-4f) fl |= RF_PARENT;
+        A.rowflags[r] = fl;
     }
+    if (r == 0) { A.diffF[0] = 0u; A.diffC[0] = 0u; A.carry_diff[0] = 0u; }
+    if (r < 64) A.misc[r] = 0u;
     const uint32_t tot = wg_wave_scan(cd, 0u, [](uint32_t x, uint32_t y) { return x + y; });
-    if ((threadIdx.x & 63) == 63 && r - 63 < n) carry_diff[r / WG_SWEEP_CH + 1] = tot;
+    if ((threadIdx.x & 63) == 63 && r - 63 < n) {
+        A.carry_diff[r / WG_SWEEP_CH + 1] = tot;
+        A.carry_fill[r / WG_SWEEP_CH] = 0u;
+    }
 }
 
 __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
@@ -131,30 +204,164 @@ __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, co
     }
 }
 
-// per-row totals: nV = nF + nT + nB -> vert_off, nC -> curve_off (scanned after)
-__global__ void k_row_counts(uint64_t n, const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ scanC,
-                             const uint32_t *__restrict__ cntT, const uint32_t *__restrict__ cntB,
-                             const uint32_t *__restrict__ cntCend, const uint8_t *__restrict__ rowflags,
-                             uint32_t *__restrict__ nV, uint32_t *__restrict__ nC) {
-    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n) return;
-    const uint32_t nf = scanF[r + 1];
-    const uint32_t ic = scanC[r + 1];
-    nV[r] = nf + cntT[r] + cntB[r];
-    nC[r] = ((rowflags[r] & RF_ZERO) ? 0u : ic) + cntCend[r];
+// 8 consecutive words at a 32-byte aligned address
+__device__ __forceinline__ void ld8(const uint32_t *p, uint32_t (&v)[8]) {
+    const uint4 a = reinterpret_cast<const uint4 *>(p)[0], b = reinterpret_cast<const uint4 *>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8(uint32_t *p, const uint32_t (&v)[8]) {
+    reinterpret_cast<uint4 *>(p)[0] = make_uint4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<uint4 *>(p)[1] = make_uint4(v[4], v[5], v[6], v[7]);
 }
 
-__global__ void k_bottom(uint64_t n, const uint32_t *__restrict__ edge_off, const wg_edge *__restrict__ edges,
-                         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ scanF,
-                         const uint32_t *__restrict__ cntT, uint32_t *__restrict__ vert, Cap vc, uint32_t *ovf) {
-    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (over(vc, ovf) || r >= n) return;
-    uint32_t o = vert_off[r] + scanF[r + 1] + cntT[r];
-    for (uint32_t k = edge_off[r]; k < edge_off[r + 1]; k++) {
-        const wg_edge e = edges[k];
-        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane)
-            vert[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
+// The sweep's carry-in offsets from the chunk difference counts (nch + 1
+// entries) in one single-block launch: their exclusive scan (the edges alive
+// across each chunk start), then the exclusive scan of those counts
+constexpr int CO_T = 1024;
+constexpr uint64_t CO_MAX = 32 * (uint64_t)CO_T;
+__device__ __forceinline__ uint32_t co_block_excl(uint32_t v, uint32_t *ws) {
+    const uint32_t inc = wg_wave_scan(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) base += ws[w];
+    __syncthreads();
+    return base + inc - v;
+}
+// each thread owns a run of q <= 32 consecutive entries, held in registers:
+// both scans cost one load round and one block scan each
+__global__ void __launch_bounds__(CO_T) k_carry_offsets(uint64_t nch, uint32_t *__restrict__ diff, uint32_t *__restrict__ off) {
+    __shared__ uint32_t ws[CO_T / 64];
+    const uint32_t q = (uint32_t)((nch + 1 + CO_T - 1) / CO_T);
+    const uint64_t a = (uint64_t)threadIdx.x * q;
+    uint32_t v[32];
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 32; j++) {
+        v[j] = (j < q && a + j <= nch) ? diff[a + j] : 0u;
+        s += v[j];
     }
+    // pass 1: exclusive scan of diff[0..nch]; entry k + 1 is the count of chunk k
+    uint32_t run = co_block_excl(s, ws);
+#pragma unroll
+    for (uint32_t j = 0; j < 32; j++) {
+        const uint32_t t = v[j];
+        v[j] = run;
+        run += t;
+    }
+    // run = the exclusive value one past this thread's run (the next thread's
+    // first): pass 2 scans the counts off[k] <- scan(ex[k + 1]), k < nch
+    uint32_t w[32];
+    s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 32; j++) {
+        const uint32_t nxt = (j + 1 < 32 && j + 1 < q) ? v[(j + 1) & 31] : run;   // ex[a + j + 1]
+        w[j] = (j < q && a + j < nch) ? nxt : 0u;
+        s += w[j];
+    }
+    run = co_block_excl(s, ws);
+#pragma unroll
+    for (uint32_t j = 0; j < 32; j++) {
+        if (j < q && a + j < nch) off[a + j] = run;
+        run += w[j];
+    }
+    if (a < nch && a + q >= nch) off[nch] = run;   // the thread owning the last count
+    if (nch == 0 && threadIdx.x == 0) off[0] = 0u;
+}
+
+// ordered exclusive block scan (GO_T threads) of two values at once
+constexpr int GO_T = 256, GO_Q = 8;
+constexpr uint64_t GO_TILE = (uint64_t)GO_T * GO_Q;
+__device__ __forceinline__ uint2 go_block_excl(uint2 v, uint2 &tot) {
+    __shared__ uint2 ws[GO_T / 64];
+    const uint32_t a = wg_wave_scan(v.x, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    const uint32_t b = wg_wave_scan(v.y, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) ws[w] = make_uint2(a, b);
+    __syncthreads();
+    uint2 base = make_uint2(0u, 0u), t = make_uint2(0u, 0u);
+#pragma unroll
+    for (int k = 0; k < GO_T / 64; k++) {
+        const uint2 q = ws[k];
+        if (k < w) { base.x += q.x; base.y += q.y; }
+        t.x += q.x; t.y += q.y;
+    }
+    __syncthreads();
+    tot = t;
+    return make_uint2(base.x + a - v.x, base.y + b - v.y);
+}
+
+// One launch after the tile sums of the two difference arrays (scanned
+// over n + 1 entries, in place): the per-row span counts, the per-row list
+// totals nV = nF + nT + nB (-> vert_off) and nC (-> curve_off, the superset:
+// the flag row is all zero) and their 256-row sums for the offsets' scan
+// (wg_scan_bs_u32).
+__global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, uint32_t *C, const uint32_t *__restrict__ tsF,
+                                                      const uint32_t *__restrict__ tsC, const uint32_t *__restrict__ cntT,
+                                                      const uint32_t *__restrict__ cntB, const uint32_t *__restrict__ cntCend,
+                                                      uint32_t *__restrict__ nV, uint32_t *__restrict__ nC,
+                                                      uint32_t *__restrict__ bsV, uint32_t *__restrict__ bsC, uint64_t nbs) {
+    uint2 pre = make_uint2(0u, 0u), ptot;
+    for (uint64_t b = threadIdx.x; b < blockIdx.x; b += GO_T) { pre.x += tsF[b]; pre.y += tsC[b]; }
+    (void)go_block_excl(pre, ptot);
+    const uint64_t base = (uint64_t)blockIdx.x * GO_TILE + (uint64_t)threadIdx.x * GO_Q;
+    uint32_t vF[GO_Q], vC[GO_Q], vT[GO_Q], vB[GO_Q], vE[GO_Q];
+    const bool full = base + GO_Q <= n;   // every item a row (and within the n + 1 entries): 16-byte accesses
+    if (full) {
+        ld8(F + base, vF); ld8(C + base, vC); ld8(cntT + base, vT); ld8(cntB + base, vB); ld8(cntCend + base, vE);
+    } else {
+#pragma unroll
+        for (int k = 0; k < GO_Q; k++) {
+            const bool in = base + k <= n;   // n + 1 entries
+            vF[k] = in ? F[base + k] : 0u;
+            vC[k] = in ? C[base + k] : 0u;
+            const bool row = base + k < n;
+            vT[k] = row ? cntT[base + k] : 0u;
+            vB[k] = row ? cntB[base + k] : 0u;
+            vE[k] = row ? cntCend[base + k] : 0u;
+        }
+    }
+    uint2 sum = make_uint2(0u, 0u);
+#pragma unroll
+    for (int k = 0; k < GO_Q; k++) {
+        sum.x += vF[k];
+        sum.y += vC[k];
+    }
+    uint2 tot;
+    uint2 run = go_block_excl(sum, tot);
+    run.x += ptot.x;
+    run.y += ptot.y;
+    uint32_t tV = 0, tC = 0;
+    uint32_t oF[GO_Q], oC[GO_Q], oV[GO_Q], oN[GO_Q];
+#pragma unroll
+    for (int k = 0; k < GO_Q; k++) {
+        oF[k] = run.x;
+        oC[k] = run.y;
+        run.x += vF[k];
+        run.y += vC[k];
+        // run = the exclusive value at row + 1: the edges alive across the row
+        oV[k] = run.x + vT[k] + vB[k];
+        oN[k] = run.y + vE[k];
+        if (base + k < n) { tV += oV[k]; tC += oN[k]; }
+    }
+    if (full) {
+        st8(F + base, oF); st8(C + base, oC); st8(nV + base, oV); st8(nC + base, oN);
+    } else {
+#pragma unroll
+        for (int k = 0; k < GO_Q; k++) {
+            const uint64_t i = base + k;
+            if (i <= n) { F[i] = oF[k]; C[i] = oC[k]; }
+            if (i < n) { nV[i] = oV[k]; nC[i] = oN[k]; }
+        }
+    }
+    // 256-row sums: 32 threads x 8 rows
+#pragma unroll
+    for (int d = 16; d >= 1; d >>= 1) {
+        tV += (uint32_t)__shfl_xor((int)tV, d, 64);
+        tC += (uint32_t)__shfl_xor((int)tC, d, 64);
+    }
+    const uint64_t sub = (uint64_t)blockIdx.x * (GO_TILE / WG_BS_THREADS) + threadIdx.x / 32;
+    if ((threadIdx.x & 31) == 0 && sub < nbs) { bsV[sub] = tV; bsC[sub] = tC; }
 }
 
 // one pass over the edges: same-lane edges' ids into their parent row's
@@ -181,13 +388,15 @@ __global__ void k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges, cons
     vert[vert_off[p] + scanF[p + 1] + pos] = (uint32_t)k;   // edge id, packed below
 }
 
-__global__ void k_top_finish(uint64_t n, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
-                             const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT, uint32_t *vert, Cap vc,
-                             uint32_t *ovf) {
+// per row: the top-half entries (edge ids placed by k_top_carry) sorted by
+// edge id and packed, then the bottom halves (same-lane edges of child r, in
+// parent order) after them
+__global__ void k_top_finish(uint64_t n, const uint32_t *__restrict__ edge_off, const wg_edge *__restrict__ edges,
+                             const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ scanF,
+                             const uint32_t *__restrict__ cntT, uint32_t *vert, Cap vc, uint32_t *ovf) {
     uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (over(vc, ovf) || r >= n) return;
     const uint32_t nt = cntT[r];
-    if (nt == 0) return;
     uint32_t *v = vert + vert_off[r] + scanF[r + 1];
     for (uint32_t i = 1; i < nt; i++) {   // insertion sort by edge id (in-degree is small)
         uint32_t x = v[i];
@@ -199,14 +408,15 @@ __global__ void k_top_finish(uint64_t n, const wg_edge *__restrict__ edges, cons
         const wg_edge e = edges[v[i]];
         v[i] = pack_vert(e.child_lane, WG_VERT_TOP, e.color);
     }
+    uint32_t o = nt;
+    for (uint32_t k = edge_off[r]; k < edge_off[r + 1]; k++) {
+        const wg_edge e = edges[k];
+        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane)
+            v[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
+    }
 }
 
 // ---- carry-in registration for the sweep -------------------------------------
-__global__ void k_carry_counts(uint64_t nch, const uint32_t *__restrict__ scan, uint32_t *__restrict__ cnt) {
-    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nch) return;
-    cnt[k] = scan[k + 1];
-}
 // rank sort of each chunk's carry list (one wave per chunk; lists are short)
 __global__ void __launch_bounds__(64) k_carry_sort(uint64_t nch, const uint32_t *__restrict__ carry_off,
                                                     const uint32_t *__restrict__ carry, uint32_t *__restrict__ sorted,
@@ -367,24 +577,42 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
 // LDS sweep above.
 constexpr int SW_SLOTS = 8;
 
+// The chunk's carry-in list (registration order) ranked into edge order:
+// edge ids are distinct, so rank = the number of smaller ids
+__device__ __forceinline__ void carry_rank(const uint32_t *__restrict__ carry, uint32_t len, uint32_t *out) {
+    for (uint32_t i = threadIdx.x & 63; i < len; i += 64) {
+        const uint32_t x = carry[i];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < len; j++) rank += carry[j] < x;
+        out[rank] = x;
+    }
+}
+
 __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nch, const wg_edge *__restrict__ edges,
         const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
-        const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
+        const uint32_t *__restrict__ carry, uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
-        uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, uint32_t *ovf) {
+        uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, Cap cc, uint32_t *ovf) {
+    __shared__ uint32_t s_car[SW_WAVES][64 * SW_SLOTS];
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t q = (uint64_t)blockIdx.x * SW_WAVES + (threadIdx.x >> 6);
-    if (over(vc, ovf) || over(sc, ovf) || q >= nch) return;
+    if (over(vc, ovf) || over(sc, ovf) || over(cc, ovf) || q >= nch) return;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
     const uint32_t a = carry_off[q], ncar = carry_off[q + 1] - a;
     const uint32_t E0 = edge_off[R0], E1 = edge_off[R1];
     const uint32_t total = ncar + (E1 - E0);
-    if (total > reg_cap) {
+    if (total > reg_cap || total > 64u * SW_SLOTS) {   // the LDS sweep (k_sweep_lds) reads the ranked list from HBM
+        carry_rank(carry + a, ncar, carry_sorted + a);
         if (lid == 0) big[atomicAdd(big_n, 1u)] = (uint32_t)q;
         return;
     }
+    uint32_t *sorted = s_car[threadIdx.x >> 6];
+    carry_rank(carry + a, ncar, sorted);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // per-row scalars of the chunk, one row per lane
     const uint64_t rr = R0 + lid;
     const uint32_t voff_v = lid < nr ? vert_off[rr] : 0u;
@@ -402,7 +630,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
         const uint32_t idx = 64u * sl + lid;
         ek[sl] = 0; fb[sl] = ~0u; fl[sl] = 0; cb[sl] = ~0u; cl[sl] = 0; pv[sl] = 0;
         if ((uint32_t)sl < nslots && idx < total) {
-            const uint32_t k = idx < ncar ? carry_sorted[a + idx] : E0 + (idx - ncar);
+            const uint32_t k = idx < ncar ? sorted[idx] : E0 + (idx - ncar);
             const wg_edge e = edges[k];
             ek[sl] = k;
             const uint32_t c = e.child_row, p = e.parent_row;
@@ -625,19 +853,12 @@ __global__ void k_curve_compact(uint64_t n, const uint32_t *__restrict__ soff, c
     }
 }
 
-__global__ void k_flags_diff(uint64_t n, const uint8_t *__restrict__ a, const uint8_t *__restrict__ b, uint32_t *diff,
-                             uint64_t lo = 0) {
-    const uint64_t r = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool d = r < n && a[r] != b[r];
-    if (__any(d) && (threadIdx.x & 63) == 0) atomicOr(diff, 1u);
-}
-
 }  // namespace
 
 // filter the curve superset by this pass's row flags -> curve_off / curve_ref / curve_row.
 // cond (the frame pass, on the device): refilter only if the flags changed —
 // otherwise the same offsets are rescanned and the lists stand, no host read.
-static Cap no_cap() { return Cap{nullptr, ~0u}; }
+static Cap no_cap() { return Cap{nullptr, ~0u, nullptr}; }
 static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *cond, Cap sc, uint32_t *ovf) {
     uint32_t *coff = c->curve_off.as<uint32_t>();
     WG_ALLOC(c, c->curve_cnt, (n + 2) * 4);
@@ -735,20 +956,28 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         // refilter and the curve range); the summary is read when asked for.
         const uint64_t r0 = c->geom_r0 < n ? c->geom_r0 : 0;
         c->geom_r0 = 0;
-        WG_ALLOC(c, c->geom_diff, 64);
+        // two sets of flag words used in turn: this pass's row kernel raises the
+        // change flag in one and clears the other for the next pass
+        if (c->geom_diff.cap < 128) {
+            WG_ALLOC(c, c->geom_diff, 128);
+            WG_HIP(c, hipMemsetAsync(c->geom_diff.p, 0, 128, s));
+        }
+        const int par = c->geom_diff_par;
+        c->geom_diff_par ^= 1;
         wg_stage_begin(c, "geom_reuse");
-        uint32_t *diff = c->geom_diff.as<uint32_t>();
+        uint32_t *diff = c->geom_diff.as<uint32_t>() + 16 * par;
         hipLaunchKernelGGL(k_row_basic, dim3(blocks(n - r0)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
-                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), r0, c->geom_diff.as<uint4>(), (uint64_t)1,
-                           c->band_keep);
-        hipLaunchKernelGGL(k_flags_diff, dim3(blocks(n - r0)), dim3(T), 0, s, n, c->rowflags.as<const uint8_t>(),
-                           c->rowflags_lists.as<const uint8_t>(), diff, r0);
-        int rc = filter_curves(c, n, s, diff, no_cap(), diff + 8);
+                           c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), r0,
+                           reinterpret_cast<uint4 *>(c->geom_diff.as<uint32_t>() + 16 * (par ^ 1)), (uint64_t)4,
+                           c->band_keep, c->rowflags_lists.as<const uint8_t>(), diff);
+        // (a build awaiting its validation whose lists did not fit: no reads of them)
+        const Cap bg = Cap{nullptr, ~0u, c->pend.build ? c->geom_err : nullptr};
+        int rc = filter_curves(c, n, s, diff, bg, diff + 8);
         if (rc != WG_OK) return rc;
         wg_stage_end(c);
         wg_stage_begin(c, "geom_curves");
         // re-filtered lists move every record: all of them are recomputed then
-        launch_curves(c, n, c->lists_nsuper, s, (uint32_t)r0, no_cap(), diff + 8, diff);
+        launch_curves(c, n, c->lists_nsuper, s, (uint32_t)r0, bg, diff + 8, diff);
         WG_HIP(c, hipGetLastError());
         wg_stage_end(c);
         c->geom_sum_at[0] = rt + n;
@@ -787,23 +1016,53 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     uint32_t *voff = c->vert_off.as<uint32_t>(), *soff = c->scurve_off.as<uint32_t>();
 
     wg_stage_begin(c, "geom_counts");
-    hipLaunchKernelGGL(k_row_basic, dim3(blocks(n)), dim3(T), 0, s, n, h, d_band, rt, c->g_height.as<float>(),
-                       c->g_node_y.as<float>(), c->rowflags.as<uint8_t>(), (uint64_t)0, c->geom_zero.as<uint4>(),
-                       (uint64_t)(zwords / 4), c->band_keep);
-    hipLaunchKernelGGL(k_edge_counts_child, dim3(blocks(n)), dim3(256), 0, s, n, edge_off, E, cntB, cntF, cntC, cntCend,
-                       carry_cnt);
+    {
+        EdgeRowsArgs A{};
+        A.edge_off = edge_off;
+        if (c->edges_pending) {   // the layout stage left the edge list to this kernel
+            A.poff = c->d_poff;
+            A.prow = c->prow.as<const int32_t>();
+            A.lane_out = c->lane_out.as<const uint32_t>();
+            A.color_out = c->color_out.as<const uint8_t>();
+        }
+        A.edges = c->edges.as<wg_edge>();
+        A.h = h; A.band = d_band; A.row_top = rt;
+        A.height = c->g_height.as<float>(); A.node_y = c->g_node_y.as<float>(); A.band_keep = c->band_keep;
+        A.rowflags = c->rowflags.as<uint8_t>(); A.zflags = const_cast<uint8_t *>(zflags);
+        A.cntB = cntB; A.diffF = cntF; A.diffC = cntC; A.cntCend = cntCend; A.carry_diff = carry_cnt;
+        A.cntT = cntT; A.top_fill = top_fill; A.carry_fill = carry_fill; A.misc = sweep_err;
+        hipLaunchKernelGGL(k_edges_rows, dim3(blocks(n)), dim3(256), 0, s, n, A);
+        c->edges_pending = false;
+    }
     if (ne)
         hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntT, cntF, cntC, cntCend,
                            carry_cnt, ne_dev);
-    WG_HIP(c, wg_exclusive_scan2_u32(cntF, cntF, cntC, cntC, n + 1, c->scan_tmp.p, s));
-    hipLaunchKernelGGL(k_row_counts, dim3(blocks(n)), dim3(T), 0, s, n, cntF, cntC, cntT, cntB, cntCend, zflags, voff, soff);
-    WG_HIP(c, wg_exclusive_scan2_u32(voff, voff, soff, soff, n, c->scan_tmp.p, s));
-    // carry-in registration
+    // carry-in offsets: the exclusive scan of the chunk difference counts, then
+    // of the per-chunk counts it holds one entry later
     WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
     uint32_t *carry_off = c->carry_off.as<uint32_t>();
-    WG_HIP(c, wg_exclusive_scan_u32(carry_cnt, carry_cnt, nch + 1, c->scan_tmp.p, s));
-    hipLaunchKernelGGL(k_carry_counts, dim3(blocks(nch)), dim3(T), 0, s, nch, (const uint32_t *)carry_cnt, carry_off);
-    WG_HIP(c, wg_exclusive_scan_u32(carry_off, carry_off, nch, c->scan_tmp.p, s));
+    if (nch + 1 <= CO_MAX) {
+        hipLaunchKernelGGL(k_carry_offsets, dim3(1), dim3(CO_T), 0, s, nch, carry_cnt, carry_off);
+    } else {   // (more than 2M rows: two scans)
+        WG_HIP(c, wg_exclusive_scan_u32(carry_cnt, carry_cnt, nch + 1, c->scan_tmp.p, s));
+        WG_HIP(c, wg_exclusive_scan_u32(carry_cnt + 1, carry_off, nch, c->scan_tmp.p, s));
+    }
+    // row offsets: tile sums of the two difference arrays, one kernel for their
+    // scans + the per-row list totals (+ 256-row sums), one for the offsets
+    const uint64_t nbs = wg_bs_blocks(n), nt2 = (n + 1 + 2047) / 2048;
+    WG_ALLOC(c, c->bsum, (2 * nbs + 2 * nt2 + 256) * 4);
+    uint32_t *bsV = c->bsum.as<uint32_t>(), *bsC = bsV + nbs, *tsF = bsC + nbs, *tsC = tsF + nt2 + 64;
+    WG_HIP(c, wg_tile_sums2_u32(cntF, cntC, n + 1, tsF, tsC, s));
+    hipLaunchKernelGGL(k_geom_offsets, dim3((uint32_t)nt2), dim3(GO_T), 0, s, n, cntF, cntC, (const uint32_t *)tsF,
+                       (const uint32_t *)tsC, (const uint32_t *)cntT, (const uint32_t *)cntB, (const uint32_t *)cntCend,
+                       voff, soff, bsV, bsC, nbs);
+    {
+        WgScanBs S;
+        S.na = 2;
+        S.in[0] = voff; S.out[0] = voff; S.bsum[0] = bsV;
+        S.in[1] = soff; S.out[1] = soff; S.bsum[1] = bsC;
+        WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, s));
+    }
     // list capacities: exact from the totals, or (speculative build) the
     // buffers as the last pass left them, checked on the device
     Cap vc = no_cap(), sc = no_cap(), cc = no_cap();
@@ -838,31 +1097,29 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         scap = std::min(scap, cap_of(c->curve_tb, 4));
         const uint64_t ccap = std::min(cap_of(c->carry, 4), cap_of(c->carry_sorted, 4));
         auto u32 = [](uint64_t v) { return (uint32_t)std::min<uint64_t>(v, 0xFFFFFFFEull); };
-        vc = Cap{voff + n, u32(vcap)};
-        sc = Cap{soff + n, u32(scap)};
-        cc = Cap{carry_off + nch, u32(ccap)};
+        vc = Cap{voff + n, u32(vcap), nullptr};
+        sc = Cap{soff + n, u32(scap), nullptr};
+        cc = Cap{carry_off + nch, u32(ccap), nullptr};
         n_super_grid = scap;
+        c->spec_nsuper_grid = scap;
     }
     wg_stage_end(c);
 
     wg_stage_begin(c, "geom_lists");
     uint32_t *vert = c->vert.as<uint32_t>();
-    hipLaunchKernelGGL(k_bottom, dim3(blocks(n)), dim3(T), 0, s, n, edge_off, E, voff, cntF, cntT, vert, vc, ovf);
     if (ne)
         hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, vert,
                            (const uint32_t *)carry_off, carry_fill, c->carry.as<uint32_t>(), ne_dev, vc, cc, ovf);
-    hipLaunchKernelGGL(k_top_finish, dim3(blocks(n)), dim3(T), 0, s, n, E, voff, cntF, cntT, vert, vc, ovf);
+    hipLaunchKernelGGL(k_top_finish, dim3(blocks(n)), dim3(T), 0, s, n, edge_off, E, voff, cntF, cntT, vert, vc, ovf);
     uint32_t *carry_sorted = c->carry_sorted.as<uint32_t>();
-    hipLaunchKernelGGL(k_carry_sort, dim3(nch), dim3(64), 0, s, nch, (const uint32_t *)carry_off,
-                       c->carry.as<const uint32_t>(), carry_sorted, cc, ovf);
     // chunks too wide for the register sweep are listed in sweep_err[2..] and swept through LDS
     uint32_t *big_n = sweep_err + 1;
     WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
     hipLaunchKernelGGL(k_sweep, dim3((nch + SW_WAVES - 1) / SW_WAVES), dim3(64 * SW_WAVES), 0, s, n, nch, E, edge_off,
-                       (const uint32_t *)carry_off, (const uint32_t *)carry_sorted, zflags,
+                       (const uint32_t *)carry_off, (const uint32_t *)c->carry.as<uint32_t>(), carry_sorted, zflags,
                        voff, (const uint32_t *)soff, vert, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
                        c->sweep_big.as<uint32_t>(), big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS,
-                       vc, sc, ovf);
+                       vc, sc, cc, ovf);
     hipLaunchKernelGGL(k_sweep_lds, dim3(64), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)c->sweep_big.as<uint32_t>(),
                        (const uint32_t *)big_n, E, edge_off, (const uint32_t *)carry_off,
                        (const uint32_t *)carry_sorted, zflags, voff, (const uint32_t *)soff, vert,

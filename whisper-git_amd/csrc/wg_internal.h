@@ -61,7 +61,10 @@ struct DevBuf {
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
         if (p) { hipError_t e = hipFree(p); p = nullptr; cap = 0; if (e != hipSuccess) return e; }
-        size_t b = bytes < 256 ? 256 : bytes;
+        // 1/16 headroom: a list that grows a little (a refresh prepending a few
+        // commits) fits the buffers in place — no reallocation, and the
+        // speculative build's capacity checks still pass
+        size_t b = bytes < 256 ? 256 : bytes + bytes / 16;
         hipError_t e = hipMalloc(&p, b);
         if (e == hipSuccess) cap = b;
         return e;
@@ -179,10 +182,34 @@ struct ReplayRun {
     const uint32_t *aux = nullptr;
     uint16_t *slots_a = nullptr, *slots_b = nullptr, *sp_prev = nullptr, *sp_next = nullptr;   // sp_prev: last written
     uint32_t nw = 1;                     // occupancy words (1, 4 or 16: up to 63, 255, 1023 slots)
+    uint32_t warm = 0;                   // iteration 1 starts this many events before each chunk
     unsigned long long *occ_a = nullptr, *occ_b = nullptr, *op = nullptr, *on = nullptr;
     uint32_t *stats = nullptr, *flags = nullptr, *scal = nullptr;
     const uint32_t *nev_dev = nullptr;   // speculative build: event count on the device (nev = upper bound)
     const uint32_t *gate = nullptr;      // speculative build: nonzero = not well formed, replay nothing
+};
+
+// small device -> host reads (wg_api.hip): one tiny kernel writes the values
+// into mapped pinned host memory, then the stream is synchronised — instead of
+// one blit per hipMemcpyAsync into pageable memory
+struct WgFetch { const void *p; bool wide; };   // wide: 8-byte value, else 4-byte
+
+// speculative build validation words: lanes + geometry + the edge count
+constexpr int WG_LANES_SPEC_ITEMS = 9;
+constexpr int WG_GEOM_SPEC_ITEMS = 8;
+constexpr int WG_PENDING_ITEMS = WG_LANES_SPEC_ITEMS + WG_GEOM_SPEC_ITEMS + 1;
+
+// A speculative build whose validation was deferred (WG_OPT_DEFER_VALIDATION)
+// and what was queued after it: it is read with the next emission's vertex
+// total (or by wg_settle), and a build that did not hold is redone then
+struct PendingBuild {
+    bool build = false;
+    int k = 0, kl = 0;              // validation items, of which the lane stage's
+    WgFetch it[WG_PENDING_ITEMS];
+    bool frame = false, frame_band = false;   // a frame geometry pass followed (its bands are in band_prev)
+    bool emit = false;              // ... and an emission of rows [rb, re)
+    uint64_t rb = 0, re = 0;
+    int64_t sel = -1;
 };
 
 struct wg_ctx {
@@ -228,6 +255,7 @@ struct wg_ctx {
     DevBuf lane_scalars;    // uint32 [8]  max_lane, n_slots, overflow, ...
     DevBuf lf[LF_COUNT];    // event-compressed lane path workspaces (wg_lanes_fast.hip), indexed by LF_*
     uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
+    uint32_t replay_warm = 0;      // iteration 1's warm-up events before each chunk (WG_OPT_REPLAY_WARMUP)
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
     uint32_t replay_nw = 1;        // occupancy words of the next replay (from the last build's slot count)
@@ -245,7 +273,8 @@ struct wg_ctx {
     uint64_t n_events = 0;  // events of the last fast-path lane build
     uint64_t e_refs_own = 0;   // parent references of the rows this context owns
     bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])
-    bool lane_out_fused = false;   // the lane kernel wrote lane_out / color_out (speculative fast path)
+    bool lane_out_fused = false;
+    bool edges_pending = false;    // the edge list is written by the next full geometry pass (k_edges_rows)   // the lane kernel wrote lane_out / color_out (speculative fast path)
     bool force_general_lanes = false;   // WG_LANES=general (testing the general walk)
     ReplayRun spec_run;     // the speculative build's replay (its iteration count and flag words)
     // speculative build (wg_layout_build): launches sized by upper bounds and
@@ -253,6 +282,9 @@ struct wg_ctx {
     // the end validating them (the exact form redoes anything that failed)
     bool spec = false;          // the build in progress is speculative
     bool spec_ready = false;    // an exact build sized this context's buffers (speculation may start)
+    bool defer_validation = false;   // WG_OPT_DEFER_VALIDATION
+    PendingBuild pend;
+    uint64_t spec_nsuper_grid = 0;   // the speculative geometry pass's curve-record grid (its capacity)
     uint32_t spec_builds = 0, spec_redo_lanes = 0, spec_redo_geom = 0;   // speculative builds, of which lanes / geometry redone
     // edges
     DevBuf edge_cnt;        // uint32 [N+1] -> edge_off after scan
@@ -283,6 +315,7 @@ struct wg_ctx {
     bool geom_sum_stale = false;            // total_height / scan_path / n_curve not read back yet
     const void *geom_sum_at[3] = {nullptr, nullptr, nullptr};   // where they are (row_top[n], scan flag, curve_off[n])
     DevBuf scan_tmp;        // scan workspace
+    DevBuf scan_tmp_side;   // scan workspace of the side stream (geometry carry offsets)
     DevBuf bsum;            // producer tile sums of the wg_scan_bs_u32 scans (3 arrays of wg_bs_blocks(n) + 64)
     DevBuf scal;            // uint64 [16] device scalars (totals)
     DevBuf rowflags;        // uint8 [N] bit0 zero-height strip, bit1 child strip empty, bit2 parent strip empty
@@ -295,7 +328,8 @@ struct wg_ctx {
     uint64_t lists_n = 0, lists_ne = 0;
     DevBuf rowflags_lists;              // the flags the curve lists were filtered with
     DevBuf scurve_off, scurve_ref, scurve_row;   // curve superset (flags ignored), swept once per layout
-    DevBuf geom_diff;                   // uint32: flags differ
+    DevBuf geom_diff;                   // 2 x 16 uint32: flags differ (+ the pass's overflow word at 8), used in turn
+    int geom_diff_par = 0;
     // per-frame reuse: the geometry in place was made for (layout geom_key_gen, bands or none)
     uint64_t geom_key_gen = ~0ull;
     bool     geom_key_band = false;
@@ -360,15 +394,25 @@ struct wg_ctx {
     uint64_t   fetch_want[3] = {0, 0, 0};   // per fetch region: the launch whose words it holds
 };
 
-// small device -> host reads (wg_api.hip): one tiny kernel writes the values
-// into mapped pinned host memory, then the stream is synchronised — instead of
-// one blit per hipMemcpyAsync into pageable memory
-struct WgFetch { const void *p; bool wide; };   // wide: 8-byte value, else 4-byte
 int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out);
 int wg_fetch_n(wg_ctx *c, int n, const WgFetch *items, uint64_t *out);   // n <= 64
 // the same read without waiting: queue it, queue more work, then wg_fetch_end
 // (one pending at a time)
 int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items);
+int wg_fetch_begin_n(wg_ctx *c, int n, const WgFetch *items);
+// deferred validation (WG_OPT_DEFER_VALIDATION, wg_api.hip): wg_settle reads
+// and checks a pending build's words; wg_validate_pending checks words read
+// by the caller.  A build that did not hold is redone with the exact stages,
+// followed by the frame pass and emission queued after it (*redone = true).
+int wg_settle(wg_ctx *c);
+int wg_validate_pending(wg_ctx *c, const uint64_t *v, bool *redone);
+#define WG_SETTLE(c)                                                               \
+    do {                                                                           \
+        if ((c)->pend.build) {                                                     \
+            const int _sr = wg_settle(c);                                          \
+            if (_sr != WG_OK) return _sr;                                          \
+        }                                                                          \
+    } while (0)
 int wg_fetch_end(wg_ctx *c, uint64_t *out);
 int wg_fetch_defer(wg_ctx *c, std::initializer_list<WgFetch> items);
 int wg_fetch_deferred(wg_ctx *c, uint64_t *out);
@@ -468,6 +512,9 @@ struct WgScanBs {
 // out[a][0..n] = exclusive scan of in[a] (out[a][n] = total); in may alias out.
 // tmp: c->scan_tmp after wg_scan_reserve(c, n).
 hipError_t wg_scan_bs_u32(const WgScanBs &S, uint64_t n, void *tmp, hipStream_t s);
+// tile sums (2048-element tiles) of two arrays, for a caller-fused down-sweep
+hipError_t wg_tile_sums2_u32(const uint32_t *in0, const uint32_t *in1, uint64_t n, uint32_t *ts0, uint32_t *ts1,
+                             hipStream_t s);
 inline uint64_t wg_bs_blocks(uint64_t n) { return (n + WG_BS_THREADS - 1) / WG_BS_THREADS; }
 
 // stages -------------------------------------------------------------------------
@@ -499,8 +546,6 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
 int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known = -1);   // wg_lanes.hip
 // speculative build (wg_layout_build): validation words of the lane build
 // (fills WG_LANES_SPEC_ITEMS items) and their check (wg_lanes_fast.hip)
-constexpr int WG_LANES_SPEC_ITEMS = 9;
-constexpr int WG_GEOM_SPEC_ITEMS = 8;
 int wg_lanes_spec_items(wg_ctx *c, WgFetch *it);
 bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v);
 // event-compressed lane phases over a row range (wg_lanes_fast.hip)

@@ -158,27 +158,6 @@ __global__ void k_lane_out(uint64_t n, const uint32_t *__restrict__ canon, const
     color_out[i] = (flags[ci] & WG_FLAG_ORPHAN) ? (uint8_t)WG_COLOR_ORPHAN : (uint8_t)(l % 6u);
 }
 
-// edge list (:301-320): child_row asc, then parent order
-__global__ void k_edges(uint64_t n, const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ poff,
-                        const int32_t *__restrict__ prow, const uint32_t *__restrict__ lane_out,
-                        const uint8_t *__restrict__ color_out, wg_edge *__restrict__ edges) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t o = edge_off[i];
-    const uint32_t cl = lane_out[i], col = color_out[i];
-    for (uint32_t k = poff[i]; k < poff[i + 1]; k++) {
-        const int32_t p = prow[k];
-        if (p < 0) continue;
-        wg_edge e;
-        e.child_row = (uint32_t)i;
-        e.child_lane = cl;
-        e.parent_row = (uint32_t)p;
-        e.parent_lane = lane_out[p];
-        e.color = col;
-        edges[o++] = e;
-    }
-}
-
 template <int NCH>
 hipError_t launch_general(wg_ctx *c) {
     hipLaunchKernelGGL((k_lanes_general<NCH>), dim3(1), dim3(64), 0, c->stream, c->n, c->canon.as<const uint32_t>(),
@@ -267,9 +246,9 @@ int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known) {
         if (const int rc = wg_fetch_deferred(c, &ne)) return rc;
     c->n_edges = ne;
     WG_ALLOC(c, c->edges, (uint64_t)ne * sizeof(wg_edge) + 16);
-    hipLaunchKernelGGL(k_edges, dim3((n + T - 1) / T), dim3(T), 0, c->stream, n, c->edge_cnt.as<const uint32_t>(),
-                       c->d_poff, c->prow.as<const int32_t>(), c->lane_out.as<const uint32_t>(),
-                       c->color_out.as<const uint8_t>(), c->edges.as<wg_edge>());
+    // the records are written by the full geometry pass that follows every
+    // layout build (wg_geom.hip k_edges_rows, with the pass's first counts)
+    c->edges_pending = true;
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;

@@ -617,6 +617,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
     run.nev = nev;
     run.nw = nw;
     run.chunk = c->replay_chunk;
+    run.warm = c->replay_warm;
     const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
@@ -696,6 +697,7 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     run.nev = nev_cap;
     run.nw = c->replay_nw;
     run.chunk = c->replay_chunk;
+    run.warm = c->replay_warm;
     const uint64_t nch = (nev_cap + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];

@@ -85,6 +85,7 @@ struct ReplayArgs {
     uint32_t *changed;          // [iter] = 1 if iteration iter changed anything
     const uint32_t *nev_dev;    // speculative build: the event count in device memory (nev = its upper bound)
     const uint32_t *gate;       // speculative build: nonzero = the list is not well formed, replay nothing
+    uint32_t warm;              // iteration 1: start this many events before the chunk (multiple of 64)
 };
 
 // The occupancy of up to 64*NW - 1 slots (active_lanes, commit_graph.rs:414-423
@@ -203,42 +204,54 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
     const uint64_t e0 = c * A.chunk;
     if (e0 >= nev) return;
     const uint64_t e1 = (e0 + A.chunk < nev) ? e0 + A.chunk : nev;
-    const bool lds = A.chunk <= LSLOT_MAX;
+    // Iteration 1 (no earlier iteration to take an entry state from) may start
+    // `warm` events before the chunk from an empty table: the replay forgets a
+    // wrong start within a few dozen events, so the chunk's own events — and
+    // the next iteration's guesses — are mostly right already.  Warm-up slots
+    // live in LDS only; nothing before e0 is written or counted.
+    uint64_t ew = e0;
+    if (A.iter == 1 && A.warm && e1 - e0 < LSLOT_MAX) {
+        uint64_t w = A.warm;
+        if (w > LSLOT_MAX - (e1 - e0)) w = (LSLOT_MAX - (e1 - e0)) & ~63ull;
+        ew = e0 > w ? e0 - w : 0;
+    }
+    const bool lds = e1 - ew <= LSLOT_MAX;
 #ifdef WG_REPLAY_PROFILE
     const unsigned long long rp_t0 = clock64();
     unsigned long long rp_batches = 0, rp_fast = 0, rp_sev = 0, rp_fm = 0, rp_cs = 0, rp_cfm = 0;
 #endif
     // slot of a token born in this chunk before the current batch (this iteration)
-    auto own = [&](uint64_t t) -> uint32_t { return lds ? (uint32_t)lslot[t - e0] : (uint32_t)A.slot_next[t]; };
-    M occ = c == 0 ? M::fill(0ull) : M::load_uniform(A.occ_prev + (c - 1) * NW);
+    auto own = [&](uint64_t t) -> uint32_t { return lds ? (uint32_t)lslot[t - ew] : (uint32_t)A.slot_next[t]; };
+    M occ = (c == 0 || ew < e0) ? M::fill(0ull) : M::load_uniform(A.occ_prev + (c - 1) * NW);
     M occ_or = M::fill(0ull), alloc_or = M::fill(0ull);   // OR of the occupancy after each occupying allocation / of allocated slots
     bool diff = false;
     uint32_t prev_v = 0;
     const uint4 *ev = A.ev;
-    uint4 rec = ev[e0 + lid];
-    uint4 rec1 = ev[e0 + 64 + lid];
+    uint4 rec = ev[ew + lid];
+    uint4 rec1 = ev[ew + 64 + lid];
     uint32_t q0_v = 0, q1_v = 0;
     // the previous iteration's slot of every event: the guess of the batch's
     // speculative replay and the reference of the change check
-    uint32_t gp_v = (e0 + lid < e1) ? A.slot_prev[e0 + lid] : 0u;
+    uint32_t gp_v = (ew + lid >= e0 && ew + lid < e1) ? A.slot_prev[ew + lid] : 0u;
     M occ_or_v = M::fill(0ull), alloc_or_v = M::fill(0ull);   // per-lane parts of max_lane / max_s
-    // old tokens of the first batch: all born before e0 -> iteration i-1
-    if ((rec.x & F_C) && (uint64_t)rec.y < e0) q0_v = A.slot_prev[rec.y];
-    if ((rec.x & F_C) && (uint64_t)rec.z < e0) q1_v = A.slot_prev[rec.z];
-    for (uint64_t base = e0; base < e1; base += 64) {
+    // old tokens of the first batch: all born before ew -> iteration i-1
+    if ((rec.x & F_C) && (uint64_t)rec.y < ew) q0_v = A.slot_prev[rec.y];
+    if ((rec.x & F_C) && (uint64_t)rec.z < ew) q1_v = A.slot_prev[rec.z];
+    for (uint64_t base = ew; base < e1; base += 64) {
+        const bool counted = base >= e0;   // (warm-up batches: no slots written, no max_lane)
         const uint32_t f_v = (base + lid < e1) ? rec.x : 0u;   // lanes past the chunk: no-op
         const uint32_t t0_v = rec.y, t1_v = rec.z, row_v = rec.w;
         const uint4 rec2 = ev[base + 128 + lid];
-        const uint32_t gp_next = (base + 64 + lid < e1) ? A.slot_prev[base + 64 + lid] : 0u;
+        const uint32_t gp_next = (base + 64 + lid >= e0 && base + 64 + lid < e1) ? A.slot_prev[base + 64 + lid] : 0u;
         // old tokens of the next batch (born before `base`): earlier chunks from
         // iteration i-1, this chunk's earlier batches from this iteration
         uint32_t n0_v = 0, n1_v = 0;
         if ((rec1.x & F_C) && (uint64_t)rec1.y < base)
-            n0_v = (uint64_t)rec1.y < e0 ? A.slot_prev[rec1.y] : own(rec1.y);
+            n0_v = (uint64_t)rec1.y < ew ? A.slot_prev[rec1.y] : own(rec1.y);
         if ((rec1.x & F_C) && (uint64_t)rec1.z < base)
-            n1_v = (uint64_t)rec1.z < e0 ? A.slot_prev[rec1.z] : own(rec1.z);
+            n1_v = (uint64_t)rec1.z < ew ? A.slot_prev[rec1.z] : own(rec1.z);
         // ---- parallel part: this lane's event ----------------------------------------
-        const bool have_prev = base > e0;    // previous batch of this chunk is in prev_v
+        const bool have_prev = base > ew;    // previous batch of this chunk is in prev_v
         const uint64_t pbase = base - 64;
         const uint32_t g0 = (uint32_t)__shfl((int)prev_v, (int)(t0_v & 63u), 64);
         const uint32_t g1 = (uint32_t)__shfl((int)prev_v, (int)(t1_v & 63u), 64);
@@ -355,10 +368,10 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
             uint32_t s;
             if (f & F_A) {
                 s = occ.lowest_free();
-                alloc_or = alloc_or | M::bit(s);
+                if (counted) alloc_or = alloc_or | M::bit(s);
                 if (f & F_O) {
                     occ = occ | M::bit(s);
-                    occ_or = occ_or | occ;
+                    if (counted) occ_or = occ_or | occ;
                 }
             } else {
                 // tokens born in this batch, or more than two waiters
@@ -379,7 +392,7 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
                         uint32_t ts;
                         if (t >= base) ts = rl(cur_v, (uint32_t)(t - base));
                         else if (have_prev && t >= pbase) ts = rl(prev_v, (uint32_t)(t - pbase));
-                        else ts = ufl(t < e0 ? A.slot_prev[t] : own(t));
+                        else ts = ufl(t < ew ? A.slot_prev[t] : own(t));
                         clr = clr | M::bit(ts);
                         m = ts < m ? ts : m;
                     }
@@ -400,9 +413,11 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         if (!(sm >> 63)) occ = occ & q.readlane(63);
         if (base + lid < e1) {
             const uint16_t nv = (uint16_t)cur_v;
-            diff |= gp_v != nv;
-            A.slot_next[base + lid] = nv;
-            if (lds) lslot[base - e0 + lid] = nv;
+            if (counted) {
+                diff |= gp_v != nv;
+                A.slot_next[base + lid] = nv;
+            }
+            if (lds) lslot[base - ew + lid] = nv;
         }
         gp_v = gp_next;
         // same-wave vector memory ops to one address complete in order; only keep
@@ -429,7 +444,9 @@ __global__ void __launch_bounds__(64) k_lf_replay(ReplayArgs A) {
         A.chunk_stats[2 * c] = occ_or.highest();          // max_lane
         A.chunk_stats[2 * c + 1] = alloc_or.highest();    // max slot
     }
-    if (__any(diff) || occ_changed) A.changed[A.iter] = 1u;
+    // a warm-started first iteration is not the replay from iteration 0's
+    // outputs, so it can never be the fixed point: it always counts as a change
+    if (__any(diff) || occ_changed || ew < e0) A.changed[A.iter] = 1u;
 #ifdef WG_REPLAY_PROFILE
     if (lid == 0) {
         RP_ADD(0, 1); RP_ADD(1, rp_batches); RP_ADD(2, rp_fast); RP_ADD(3, rp_sev); RP_ADD(4, rp_fm);
@@ -544,7 +561,8 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
     if (blind > R.max_iters) blind = R.max_iters;
     for (uint32_t k = 0; k < blind; k++) {
         R.it++;
-        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr};
+        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr,
+                     R.warm};
         launch_replay(R, a, s);
         // after a fixed point later iterations do nothing; the converged slots are
         // in both buffers, so either pointer is final
@@ -589,7 +607,7 @@ hipError_t wg_replay_iterate_spec(hipStream_t s, ReplayRun &R, uint32_t blind) {
     for (uint32_t k = 0; k < blind; k++) {
         R.it++;
         ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, R.nev_dev,
-                     R.gate};
+                     R.gate, R.warm};
         launch_replay(R, a, s);
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);
@@ -613,7 +631,8 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
     uint32_t next_poll = R.it + 3;
     while (!*converged && R.it < R.max_iters) {
         R.it++;
-        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr};
+        ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr,
+                     R.warm};
         launch_replay(R, a, s);
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);

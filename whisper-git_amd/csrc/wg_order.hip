@@ -123,6 +123,7 @@ extern "C" {
 int wg_order_rows(wg_ctx *c, const int64_t *walk_time, uint64_t n_walk, const int64_t *orphan_time, uint64_t n_orphans,
                   const int64_t *syn_time, uint64_t n_syn, int32_t residency, uint32_t *perm_out, int32_t out_residency) {
     if (!c) return WG_E_INVALID;
+    WG_SETTLE(c);
     if ((n_walk && !walk_time) || (n_orphans && !orphan_time) || (n_syn && !syn_time)) return WG_E_INVALID;
     if (residency != WG_HOST && residency != WG_DEVICE) return wg_fail(c, WG_E_INVALID, "bad residency %d", residency);
     if (out_residency != WG_HOST && out_residency != WG_DEVICE)

@@ -268,6 +268,7 @@ extern "C" {
 
 int wg_render(wg_ctx *c, const wg_render_params *p, uint8_t *rgba, int32_t out_residency) {
     if (!c || !p || !rgba) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (out_residency != WG_HOST && out_residency != WG_DEVICE) return wg_fail(c, WG_E_INVALID, "bad residency");
     if (!p->width || !p->height || p->width > 16384 || p->height > 16384)
         return wg_fail(c, WG_E_INVALID, "image %ux%u outside 1..16384", p->width, p->height);

@@ -49,7 +49,7 @@ struct RtChunk {
     float    start;   // exact f32 acc at chunk start (MODE_TABLE / MODE_EXACT)
     int32_t  kstart;  // binade of start (MODE_TABLE)
     uint32_t integral;// every step of the chunk is an integer < 2^24
-    uint32_t pad;
+    uint32_t bad;     // a negative or non-finite step (the walk replays every row)
 };
 
 // 2-state transducer: parity p -> (d[p] ulps, o[p]); bit2 of f = valid
@@ -129,7 +129,7 @@ __global__ void k_heights(uint64_t m, uint64_t n, const int64_t *__restrict__ ti
 // row_top scan
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(RT_T) k_rt_sum(uint64_t n, const float *__restrict__ h, const float *__restrict__ band,
-                                                 RtChunk *__restrict__ ch, uint32_t *__restrict__ flags) {
+                                                 RtChunk *__restrict__ ch) {
     const uint64_t c = blockIdx.x;
     const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
     double sum = 0.0;
@@ -144,19 +144,22 @@ __global__ void __launch_bounds__(RT_T) k_rt_sum(uint64_t n, const float *__rest
             sum += (double)s;
         }
     }
-    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1u);
     __shared__ double ws[RT_T / 64];
     __shared__ uint32_t wf[RT_T / 64];
     for (int d = 32; d >= 1; d >>= 1) sum += __shfl_down(sum, d, 64);
-    const bool anyfrac = __any(frac);
-    if ((threadIdx.x & 63) == 0) { ws[threadIdx.x >> 6] = sum; wf[threadIdx.x >> 6] = anyfrac ? 1u : 0u; }
+    const bool anyfrac = __any(frac), anybad = __any(bad);
+    if ((threadIdx.x & 63) == 0) {
+        ws[threadIdx.x >> 6] = sum;
+        wf[threadIdx.x >> 6] = (anyfrac ? 1u : 0u) | (anybad ? 2u : 0u);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
         uint32_t fr = 0;
         for (int w = 0; w < RT_T / 64; w++) { t += ws[w]; fr |= wf[w]; }
         ch[c].sum = t;
-        ch[c].integral = fr ? 0u : 1u;
+        ch[c].integral = (fr & 1u) ? 0u : 1u;
+        ch[c].bad = (fr >> 1) & 1u;
     }
 }
 
@@ -170,7 +173,16 @@ __global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__res
     __shared__ double carry;
     __shared__ uint32_t carry_int;   // all chunks so far integral
     __shared__ uint32_t n_exact;     // the exact regime is a prefix of the chunks: its length
+    // the flag words (no fill before the pass): [0] a negative / non-finite
+    // step anywhere, [1] replayed chunks and [2] all-serial (the walk), [3] the
+    // exact-regime length (below)
+    uint32_t anybad = 0;
+    for (uint64_t c = threadIdx.x; c < nch; c += 1024) anybad |= ch[c].bad;
+    anybad = __syncthreads_or((int)anybad) ? 1u : 0u;
     if (threadIdx.x == 0) {
+        flags[0] = anybad;
+        flags[1] = 0u;
+        flags[2] = 0u;
         // an exact start: a finite integer within 2^24 (row_top there is the exact sum)
         const float A0 = a0 ? *a0 : 0.0f;
         carry = (double)A0;
@@ -198,7 +210,7 @@ __global__ void __launch_bounds__(1024) k_rt_prefix(uint64_t nch, RtChunk *__res
         const double pre = carry + wb + inc - v;
         const uint32_t nonint_incl = nb + ninc;   // non-integral chunks in [base, c]
         // exact regime: every chunk up to c integral and the sum after c <= 2^24
-        const bool exact = c < nch && carry_int && nonint_incl == 0 && pre + v <= TWO24 && !flags[0];
+        const bool exact = c < nch && carry_int && nonint_incl == 0 && pre + v <= TWO24 && !anybad;
         if (c < nch) {
             ch[c].prefix = pre;
             ch[c].kguess = pre > 0.0 ? ilogb(pre) : -1000;
@@ -249,7 +261,8 @@ __device__ __forceinline__ Td td_reduce64(Td t) {   // ordered: lane 63 gets T_0
 }
 
 __global__ void __launch_bounds__(64) k_rt_super(uint64_t nch, const RtChunk *__restrict__ ch, const uint4 *__restrict__ tables,
-                                                 uint4 *__restrict__ stab, int32_t *__restrict__ skbase) {
+                                                 uint4 *__restrict__ stab, int32_t *__restrict__ skbase,
+                                                 SupState *__restrict__ sup) {
     const uint64_t S = blockIdx.x, c0 = S * RT_SUP, cc = c0 + (threadIdx.x & 63);
     const bool full = c0 + RT_SUP <= nch;
     double sm = full ? ch[cc].sum : 0.0;
@@ -268,27 +281,10 @@ __global__ void __launch_bounds__(64) k_rt_super(uint64_t nch, const RtChunk *__
         const bool fits = full && k >= 24 && k < 120 && sm < ldexp(1.0, k - 23) * 2147483648.0;
         if ((threadIdx.x & 63) == 63) stab[S * WG_RT_NBIN + j] = fits ? make_uint4(t.d0, t.d1, t.f, 0u) : make_uint4(0u, 0u, 2u, 0u);
     }
-    if ((threadIdx.x & 63) == 0) skbase[S] = k0;
-}
-
-// chunk starts inside the super-chunks the walk consumed whole
-__global__ void __launch_bounds__(64) k_rt_fill(uint64_t nch, const SupState *__restrict__ sup, RtChunk *__restrict__ ch,
-                                                const uint4 *__restrict__ tables) {
-    const uint64_t S = blockIdx.x;
-    const SupState st = sup[S];
-    if (st.mode != 1u) return;
-    const int lid = threadIdx.x & 63;
-    const uint64_t cc = S * RT_SUP + lid;
-    const float u = ldexpf(1.0f, st.k - 23);
-    const uint32_t p0 = parity_at(st.start, st.k);
-    const int b = st.k - ch[cc].kguess + 1;
-    const uint4 q = tables[cc * WG_RT_NBIN + b];   // valid: the super table was composed from these
-    const Td t = td_scan(Td{q.x, q.y, q.z});
-    const Td ex = wg_wave_shr1(t, td_identity());
-    const uint32_t D = p0 ? ex.d1 : ex.d0;
-    ch[cc].start = st.start + (float)D * u;
-    ch[cc].kstart = st.k;
-    ch[cc].mode = MODE_TABLE;
+    if ((threadIdx.x & 63) == 0) {
+        skbase[S] = k0;
+        sup[S] = SupState{0.0f, 0, 0u, 0u};   // (the walk marks the super-chunks it consumes whole)
+    }
 }
 
 // Replay rows [r0, r1) from acc one by one (negative / non-finite steps).
@@ -534,15 +530,44 @@ __global__ void __launch_bounds__(64) k_rt_walk(uint64_t n, uint64_t nch, const 
     }
 }
 
+// A chunk inside a super-chunk the walk consumed whole: its start from the
+// super-chunk's start and the scan of its chunks' tables up to it
+__device__ __forceinline__ void super_start(const SupState &st, uint64_t S, uint64_t c, const RtChunk *__restrict__ ch,
+                                            const uint4 *__restrict__ tables, float *start, int *kstart) {
+    __shared__ float s_start;
+    if (threadIdx.x < 64) {
+        const int lid = threadIdx.x & 63;
+        const uint64_t cc = S * RT_SUP + lid;
+        const float u = ldexpf(1.0f, st.k - 23);
+        const uint32_t p0 = parity_at(st.start, st.k);
+        const int b = st.k - ch[cc].kguess + 1;
+        const uint4 q = tables[cc * WG_RT_NBIN + b];   // valid: the super table was composed from these
+        const Td t = td_scan(Td{q.x, q.y, q.z});
+        const Td ex = wg_wave_shr1(t, td_identity());
+        const uint32_t D = p0 ? ex.d1 : ex.d0;
+        if ((uint64_t)lid == c - S * RT_SUP) s_start = st.start + (float)D * u;
+    }
+    __syncthreads();
+    *start = s_start;
+    *kstart = st.k;
+}
+
 __global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, uint64_t c_lo, const float *__restrict__ h,
                                                   const float *__restrict__ band, const RtChunk *__restrict__ ch,
-                                                  float *__restrict__ row_top) {
+                                                  float *__restrict__ row_top, uint64_t nsup,
+                                                  const SupState *__restrict__ sup, const uint4 *__restrict__ tables) {
     const uint64_t c = c_lo + blockIdx.x;
-    const uint32_t mode = ch[c].mode;
-    if (mode == MODE_REPLAYED) return;
+    uint32_t mode = ch[c].mode;
+    float A = ch[c].start;
+    int kst = ch[c].kstart;
+    if (mode == MODE_REPLAYED) {
+        const uint64_t S = c / RT_SUP;
+        if (S >= nsup || sup[S].mode != 1u) return;   // replayed by the walk
+        super_start(sup[S], S, c, ch, tables, &A, &kst);
+        mode = MODE_TABLE;
+    }
     const int lid = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t r0 = c * WG_RT_CHUNK + (uint64_t)threadIdx.x * RT_Q;
-    const float A = ch[c].start;
     if (mode == MODE_EXACT) {
         // every partial sum is an integer <= 2^24: the f32 scan is exact
         float s[RT_Q], t = 0.0f;
@@ -562,7 +587,7 @@ __global__ void __launch_bounds__(RT_T) k_rt_rows(uint64_t n, uint64_t c_lo, con
         }
         return;   // row_top[n] is written by the walk
     }
-    const int k = ch[c].kstart;
+    const int k = kst;
     const float u = ldexpf(1.0f, k - 23);
     const uint32_t p0 = parity_at(A, k);
     Td tr[RT_Q];
@@ -665,15 +690,15 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
     WG_ALLOC(c, c->rt_tables, (nch + 1) * WG_RT_NBIN * sizeof(uint4));
     WG_ALLOC(c, c->rt_flags, 64);
     wg_stage_begin(c, "row_top");
-    WG_HIP(c, hipMemsetAsync(c->rt_flags.p, 0, 64, c->stream));
     if (n == 0) {
+        WG_HIP(c, hipMemsetAsync(c->rt_flags.p, 0, 64, c->stream));
         if (!a0) WG_HIP(c, hipMemsetAsync(row_top, 0, 4, c->stream));
         wg_stage_end(c);
         return WG_OK;
     }
     RtChunk *ch = c->rt_chunk.as<RtChunk>();
     uint32_t *fl = c->rt_flags.as<uint32_t>();
-    hipLaunchKernelGGL(k_rt_sum, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, ch, fl);
+    hipLaunchKernelGGL(k_rt_sum, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, ch);
     hipLaunchKernelGGL(k_rt_prefix, dim3(1), dim3(1024), 0, c->stream, nch, ch, fl, a0);
     hipLaunchKernelGGL(k_rt_tables, dim3(nch), dim3(RT_T), 0, c->stream, n, h, d_band, (const RtChunk *)ch,
                        c->rt_tables.as<uint4>());
@@ -682,20 +707,15 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
     uint4 *stab = c->rt_sup.as<uint4>();
     int32_t *skb = reinterpret_cast<int32_t *>(stab + nsup * WG_RT_NBIN);
     SupState *sup = reinterpret_cast<SupState *>(c->rt_sup.as<uint8_t>() + ((nsup * (WG_RT_NBIN * 16 + 4) + 15) / 16) * 16);
-    if (nsup) {
-        WG_HIP(c, hipMemsetAsync(sup, 0, nsup * sizeof(SupState), c->stream));
+    if (nsup)
         hipLaunchKernelGGL(k_rt_super, dim3(nsup), dim3(64), 0, c->stream, nch, (const RtChunk *)ch,
-                           c->rt_tables.as<const uint4>(), stab, skb);
-    }
+                           c->rt_tables.as<const uint4>(), stab, skb, sup);
     hipLaunchKernelGGL(k_rt_walk, dim3(1), dim3(64), 0, c->stream, n, nch, h, d_band, ch,
                        c->rt_tables.as<const uint4>(), fl, row_top, nsup, (const uint4 *)stab, (const int32_t *)skb, sup, a0);
-    if (nsup)
-        hipLaunchKernelGGL(k_rt_fill, dim3(nsup), dim3(64), 0, c->stream, nch, (const SupState *)sup, ch,
-                           c->rt_tables.as<const uint4>());
     const uint64_t c_lo = (row_lo < n ? row_lo : n) / WG_RT_CHUNK;
     if (c_lo < nch)
         hipLaunchKernelGGL(k_rt_rows, dim3(nch - c_lo), dim3(RT_T), 0, c->stream, n, c_lo, h, d_band, (const RtChunk *)ch,
-                           row_top);
+                           row_top, nsup, (const SupState *)sup, c->rt_tables.as<const uint4>());
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;

@@ -11,6 +11,36 @@ constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ITEMS = 8;
 constexpr uint64_t SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
 
+// The 8 items of a thread: two 16-byte loads / stores when in bounds and
+// aligned (uniform: every thread's base is a multiple of 8 items), else one
+// item at a time
+template <class TI, class TO>
+__device__ __forceinline__ void load8(const TI *in, uint64_t base, uint64_t n, TO (&v)[SCAN_ITEMS]) {
+    if constexpr (sizeof(TI) == 4) {
+        if (base + SCAN_ITEMS <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
+            const uint4 a = reinterpret_cast<const uint4 *>(in + base)[0], b = reinterpret_cast<const uint4 *>(in + base)[1];
+            v[0] = (TO)a.x; v[1] = (TO)a.y; v[2] = (TO)a.z; v[3] = (TO)a.w;
+            v[4] = (TO)b.x; v[5] = (TO)b.y; v[6] = (TO)b.z; v[7] = (TO)b.w;
+            return;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) v[k] = (base + k < n) ? (TO)in[base + k] : (TO)0;
+}
+template <class TO>
+__device__ __forceinline__ void store8(TO *out, uint64_t base, uint64_t n, const TO (&v)[SCAN_ITEMS]) {
+    if constexpr (sizeof(TO) == 4) {
+        if (base + SCAN_ITEMS <= n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+            reinterpret_cast<uint4 *>(out + base)[0] = make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
+            reinterpret_cast<uint4 *>(out + base)[1] = make_uint4((uint32_t)v[4], (uint32_t)v[5], (uint32_t)v[6], (uint32_t)v[7]);
+            return;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++)
+        if (base + k < n) out[base + k] = v[k];
+}
+
 template <class T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
     const int lane = threadIdx.x & 63;
@@ -45,10 +75,11 @@ __device__ __forceinline__ T block_excl_scan(T v, T &total) {
 template <class TI, class TO>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(const TI *__restrict__ in, TO *__restrict__ bsum, uint64_t n) {
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    TO v[SCAN_ITEMS];
+    load8<TI, TO>(in, base, n, v);
     TO s = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; k++)
-        if (base + k < n) s += (TO)in[base + k];
+    for (int k = 0; k < SCAN_ITEMS; k++) s += v[k];
     TO tot;
     (void)block_excl_scan<TO>(s, tot);
     if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
@@ -58,19 +89,19 @@ template <class TI, class TO>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_down(const TI *in, TO *out, const TO *__restrict__ boff, uint64_t n) {
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
     TO v[SCAN_ITEMS];
+    load8<TI, TO>(in, base, n, v);
     TO s = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; k++) {
-        v[k] = (base + k < n) ? (TO)in[base + k] : (TO)0;
-        s += v[k];
-    }
+    for (int k = 0; k < SCAN_ITEMS; k++) s += v[k];
     TO tot;
     TO run = block_excl_scan<TO>(s, tot) + (boff ? boff[blockIdx.x] : (TO)0);
+    TO o[SCAN_ITEMS];
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; k++) {
-        if (base + k < n) out[base + k] = run;
+        o[k] = run;
         run += v[k];
     }
+    store8<TO>(out, base, n, o);
     // the thread holding the last element writes the grand total to out[n]
     if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
     if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
@@ -87,19 +118,19 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_down2(const TI *in, TO *o
     (void)block_excl_scan<TO>(pre, ptot);
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
     TO v[SCAN_ITEMS];
+    load8<TI, TO>(in, base, n, v);
     TO s = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; k++) {
-        v[k] = (base + k < n) ? (TO)in[base + k] : (TO)0;
-        s += v[k];
-    }
+    for (int k = 0; k < SCAN_ITEMS; k++) s += v[k];
     TO tot;
     TO run = block_excl_scan<TO>(s, tot) + ptot;
+    TO o[SCAN_ITEMS];
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; k++) {
-        if (base + k < n) out[base + k] = run;
+        o[k] = run;
         run += v[k];
     }
+    store8<TO>(out, base, n, o);
     if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
 }
 
@@ -109,10 +140,11 @@ struct Pair32 { const uint32_t *in[2]; uint32_t *out[2]; uint32_t *bsum[2]; };
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan2_reduce(Pair32 P, uint64_t n) {
     const uint32_t *in = P.in[blockIdx.y];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    load8<uint32_t, uint32_t>(in, base, n, v);
     uint32_t s = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; k++)
-        if (base + k < n) s += in[base + k];
+    for (int k = 0; k < SCAN_ITEMS; k++) s += v[k];
     uint32_t tot;
     (void)block_excl_scan<uint32_t>(s, tot);
     if (threadIdx.x == 0) P.bsum[blockIdx.y][blockIdx.x] = tot;
@@ -128,19 +160,19 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan2_down(Pair32 P, uint64_t 
     (void)block_excl_scan<uint32_t>(pre, ptot);
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
     uint32_t v[SCAN_ITEMS];
+    load8<uint32_t, uint32_t>(in, base, n, v);
     uint32_t s = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; k++) {
-        v[k] = (base + k < n) ? in[base + k] : 0u;
-        s += v[k];
-    }
+    for (int k = 0; k < SCAN_ITEMS; k++) s += v[k];
     uint32_t tot;
     uint32_t run = block_excl_scan<uint32_t>(s, tot) + ptot;
+    uint32_t o[SCAN_ITEMS];
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; k++) {
-        if (base + k < n) out[base + k] = run;
+        o[k] = run;
         run += v[k];
     }
+    store8<uint32_t>(out, base, n, o);
     if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
 }
 
@@ -171,19 +203,19 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_bs_down(ScanBsArgs P, uin
     }
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
     uint32_t v[SCAN_ITEMS];
+    load8<uint32_t, uint32_t>(in, base, n, v);
     uint32_t s = 0;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; k++) {
-        v[k] = (base + k < n) ? in[base + k] : 0u;
-        s += v[k];
-    }
+    for (int k = 0; k < SCAN_ITEMS; k++) s += v[k];
     uint32_t tot;
     uint32_t run = block_excl_scan<uint32_t>(s, tot) + ptot;
+    uint32_t o[SCAN_ITEMS];
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; k++) {
-        if (base + k < n) out[base + k] = run;
+        o[k] = run;
         run += v[k];
     }
+    store8<uint32_t>(out, base, n, o);
     if (n > 0 && base <= n - 1 && n - 1 < base + SCAN_ITEMS) out[n] = run;
     if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
 }
@@ -268,6 +300,15 @@ hipError_t wg_scan_bs_u32(const WgScanBs &S, uint64_t n, void *tmp, hipStream_t 
     if (nbs > WG_BS_SELF && (size_t)(t - (char *)tmp) + tmp_bytes_rec<uint64_t>(nbs) > wg_scan_tmp_bytes(n))
         return hipErrorInvalidValue;   // (cannot happen: 3 (n/256 + 65) u32 + the recursion fit the reserve)
     hipLaunchKernelGGL(k_scan_bs_down, dim3((uint32_t)nblocks(n), (uint32_t)S.na), dim3(SCAN_THREADS), 0, s, P, n);
+    return hipGetLastError();
+}
+
+hipError_t wg_tile_sums2_u32(const uint32_t *in0, const uint32_t *in1, uint64_t n, uint32_t *ts0, uint32_t *ts1,
+                             hipStream_t s) {
+    Pair32 P;
+    P.in[0] = in0; P.in[1] = in1; P.out[0] = nullptr; P.out[1] = nullptr;
+    P.bsum[0] = ts0; P.bsum[1] = ts1;
+    hipLaunchKernelGGL(k_scan2_reduce, dim3((uint32_t)nblocks(n), 2), dim3(SCAN_THREADS), 0, s, P, n);
     return hipGetLastError();
 }
 

@@ -227,6 +227,7 @@ extern "C" {
 int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t rb, uint64_t re, const wg_row_text *text,
                   uint64_t *match_count) {
     if (!c || (query_len && !query)) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
     const ShardState &S = c->sh;
     const uint64_t N = S.N;
@@ -329,6 +330,7 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
 
 int wg_copy_match_flags(wg_ctx *c, uint8_t *dst) {
     if (!c) return WG_E_INVALID;
+    WG_SETTLE(c);
     const uint64_t rows = c->match_re - c->match_rb;
     if (!c->match_flags.p) return wg_fail(c, WG_E_STATE, "no match flags computed");
     if (rows && !dst) return WG_E_INVALID;

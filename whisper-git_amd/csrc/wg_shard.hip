@@ -766,6 +766,7 @@ extern "C" {
 int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, uint64_t row_begin, uint64_t row_end,
                          wg_shard_msg *out) {
     if (!c || !in || !out) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (world < 1 || world > 16 || rank < 0 || rank >= world) return wg_fail(c, WG_E_INVALID, "bad world/rank %d/%d", world, rank);
     if (in->residency != WG_DEVICE) return wg_fail(c, WG_E_INVALID, "sharded builds take device-resident commits");
     const uint64_t N = in->n_commits;
@@ -879,6 +880,7 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
 
 int wg_shard_msg_bytes(wg_ctx *c, uint64_t *out) {
     if (!c || !out) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->sh.msg_dev) { *out = c->sh.msg_bytes; return WG_OK; }
     (void)hipSetDevice(c->device);
     uint64_t b = 0;
@@ -890,6 +892,7 @@ int wg_shard_msg_bytes(wg_ctx *c, uint64_t *out) {
 
 int wg_shard_copy_msg(wg_ctx *c, void *dst) {
     if (!c) return WG_E_INVALID;
+    WG_SETTLE(c);
     uint64_t b = 0;
     if (const int rc = wg_shard_msg_bytes(c, &b)) return rc;
     if (!dst && b) return WG_E_INVALID;
@@ -902,6 +905,7 @@ int wg_shard_pack_slot(wg_ctx *c, void *slot, uint64_t cap) {
     // k_sh_slot_head writes 32 bytes (slot header + the first 16 message bytes, zero when the message is
     // longer than the slot) and the receivers read 16-byte vectors: cap is a multiple of 16, >= 16
     if (!c || !slot || (reinterpret_cast<uintptr_t>(slot) & 15u) || cap < 16 || (cap & 15u)) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->sh.on || c->sh.step == SH_IDLE) return wg_fail(c, WG_E_STATE, "no sharded call in progress");
     (void)hipSetDevice(c->device);
     if (c->sh.msg_dev) {   // length on the device: one kernel writes the header and copies what fits
@@ -927,6 +931,7 @@ int wg_shard_slot_heads(wg_ctx *c, const void *gathered, uint64_t stride, int wo
     if (!c || !gathered || !out || world < 1 || 3 * world > 64 || (reinterpret_cast<uintptr_t>(gathered) & 15u) ||
         stride < 32 || (stride & 15u))
         return WG_E_INVALID;
+        WG_SETTLE(c);
     (void)hipSetDevice(c->device);
     WgFetch it[64];
     const uint8_t *g = static_cast<const uint8_t *>(gathered);
@@ -941,6 +946,7 @@ int wg_shard_slot_heads(wg_ctx *c, const void *gathered, uint64_t stride, int wo
 int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const uint64_t *sizes, const uint32_t *heads,
                       wg_shard_msg *out) {
     if (!c || !out || !sizes) return WG_E_INVALID;
+    WG_SETTLE(c);
     ShardState &S = c->sh;
     S.heads = heads;   // valid for this call only
     S.sizes = sizes;
@@ -1135,6 +1141,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
 
 int wg_shard_geometry_begin(wg_ctx *c, const float *band, int32_t residency, wg_shard_msg *out) {
     if (!c || !out) return WG_E_INVALID;
+    WG_SETTLE(c);
     ShardState &S = c->sh;
     if (!S.on || !c->have_layout) return wg_fail(c, WG_E_STATE, "no sharded layout built");
     if (S.step != SH_IDLE) return wg_fail(c, WG_E_STATE, "a sharded call is in progress");

@@ -304,6 +304,7 @@ extern "C" {
 int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, const uint64_t *summary_off,
                    int32_t residency, const wg_text_params *p) {
     if (!c || !p) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (p->slot < 0 || p->slot >= WG_FONT_SLOTS || !c->fonts[p->slot].built)
         return wg_fail(c, WG_E_STATE, "font atlas slot %d not built", p->slot);
     if (!c->have_geom) return wg_fail(c, WG_E_STATE, "no geometry");
@@ -414,6 +415,7 @@ int wg_emit_glyphs(wg_ctx *c, uint64_t rb, uint64_t re, const uint8_t *summary, 
 
 int wg_glyph_summary_get(wg_ctx *c, wg_glyph_summary *out) {
     if (!c || !out) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_text) return wg_fail(c, WG_E_STATE, "no glyphs emitted");
     out->row_begin = c->text_rb;
     out->row_end = c->text_re;
@@ -428,6 +430,7 @@ int wg_glyph_summary_get(wg_ctx *c, wg_glyph_summary *out) {
 
 int wg_copy_glyph_vertices(wg_ctx *c, uint64_t first, uint64_t count, wg_text_vertex *dst) {
     if (!c || (!dst && count)) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_text) return wg_fail(c, WG_E_STATE, "no glyphs emitted");
     const uint64_t nv = c->n_quads * 6;
     if (first > nv || count > nv - first) return wg_fail(c, WG_E_INVALID, "vertex range out of bounds");
@@ -440,6 +443,7 @@ int wg_copy_glyph_vertices(wg_ctx *c, uint64_t first, uint64_t count, wg_text_ve
 
 int wg_copy_glyph_offsets(wg_ctx *c, uint64_t *dst) {
     if (!c || !dst) return WG_E_INVALID;
+    WG_SETTLE(c);
     if (!c->have_text) return wg_fail(c, WG_E_STATE, "no glyphs emitted");
     WG_HIP(c, hipMemcpyAsync(dst, c->text_off.p, (c->text_re - c->text_rb + 1) * 8, hipMemcpyDeviceToHost, c->stream));
     WG_HIP(c, hipStreamSynchronize(c->stream));

@@ -72,11 +72,15 @@ __device__ __forceinline__ uint64_t vtx_at(uint64_t rb, uint64_t j, int64_t sel,
 // closes the range.  tcap: tile records the buffer holds (the launch may
 // precede the host's knowledge of the total; a list that does not fit writes
 // no records).
+// gate: a build awaiting its validation (WG_OPT_DEFER_VALIDATION) whose
+// geometry lists did not fit (its error words [0] / [8]): nothing is read or
+// written (the validation redoes the build and this emission)
 __global__ void k_vtx_prep(uint64_t rb, uint64_t rows, int64_t sel, const uint32_t *__restrict__ voff,
                            const uint32_t *__restrict__ coff, uint64_t *__restrict__ vtx_off, uint64_t tcap,
-                           uint4 *__restrict__ info) {
+                           uint4 *__restrict__ info, const uint32_t *__restrict__ gate) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j > rows) return;
+    if (gate && (gate[0] | gate[8])) return;
     const uint32_t v0 = voff[rb], c0 = coff[rb];
     const uint64_t s = vtx_at(rb, j, sel, voff, coff, v0, c0);
     vtx_off[j] = s;
@@ -134,7 +138,8 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         const float *__restrict__ height, const float *__restrict__ node_y, const uint32_t *__restrict__ lane_out,
         const uint8_t *__restrict__ color_out, const float4 *__restrict__ palette,
         const uint4 *__restrict__ tinfo, const uint8_t *__restrict__ match, int64_t mlo, int64_t mhi,
-        float4 *__restrict__ out, uint64_t ntl) {
+        float4 *__restrict__ out, uint64_t ntl, const uint32_t *__restrict__ max_lane_dev,
+        const uint32_t *__restrict__ gate) {
     __shared__ RowInfo rows[MAXR];
     __shared__ __attribute__((aligned(4))) uint8_t pair_row[PAIRS];   // row (within the tile) of every vertex pair
     __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
@@ -145,6 +150,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     __shared__ float4 pal[2 * WG_PALETTE_SIZE];    // palette, then the same at WG_DIM_ALPHA
     __shared__ float2 circ[3][WG_TESS_NODE_SEGMENTS + 2];   // r*(cos, sin) for node, ring inner, ring outer radius
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (gate && (gate[0] | gate[8])) return;   // (see k_vtx_prep)
     // the grid may be sized by the buffer's capacity (ntl tiles): workgroups
     // past the total's tiles exit, and a total beyond the capacity writes
     // nothing (the host relaunches)
@@ -164,6 +170,11 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     const uint4 ti = tinfo[tile], tn = tinfo[tile + 1];   // everything below hangs on these
     const uint64_t v1 = (v0 + TILE < total) ? v0 + TILE : total;
     const uint64_t nrows = re - rb;
+    if (max_lane_dev) {   // a build not validated yet (WG_OPT_DEFER_VALIDATION): graph_width (:353-354) from its max_lane
+        const uint32_t ml = *max_lane_dev;
+        vis = ml + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? ml + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
+        if (vis < 1) vis = 1;   // (a build that will not validate: any value, the emission is redone)
+    }
     const float visf = (float)(vis - 1);
     const uint64_t first = ti.x;
     const uint32_t A = ti.y, K0 = ti.z;
@@ -424,10 +435,11 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     }
     wg_stage_begin(c, "vtx_counts");
     uint64_t *off = c->vtx_off.as<uint64_t>();
+    const uint32_t *gate = c->pend.build ? c->geom_err : nullptr;   // a build awaiting its validation
     auto prep = [&](uint64_t tcap) {   // vtx_off + tile records (none when tcap is too small)
         hipLaunchKernelGGL(k_vtx_prep, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
                            c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
-                           c->tile_first.as<uint4>());
+                           c->tile_first.as<uint4>(), gate);
     };
     const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;
     const uint64_t tcap = c->tile_first.cap / sizeof(uint4);
@@ -440,7 +452,13 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     // launched right away into the buffers as they are (steady-state frames
     // fit the last frame's capacity; the kernels exit past the total and
     // write nothing when it does not fit), and relaunched only if needed.
-    if (const int rc = wg_fetch_begin(c, {{off + rows, true}})) return rc;
+    // a build awaiting its validation (WG_OPT_DEFER_VALIDATION): its words ride on this read
+    WgFetch fi[1 + WG_PENDING_ITEMS];
+    fi[0] = WgFetch{off + rows, true};
+    const int npend = c->pend.build ? c->pend.k : 0;
+    for (int i = 0; i < npend; i++) fi[1 + i] = c->pend.it[i];
+    if (const int rc = wg_fetch_begin_n(c, 1 + npend, fi)) return rc;
+    const uint32_t *ml_dev = npend ? c->lane_scalars.as<const uint32_t>() : nullptr;
     // search-match flags of global rows [match_rb, match_re) -> context rows [mlo, mhi)
     const uint8_t *match = c->match_on ? c->match_flags.as<const uint8_t>() : nullptr;
     const int64_t mlo = (int64_t)c->match_rb - (int64_t)c->sh.s + (int64_t)c->sh.row_base;
@@ -454,12 +472,18 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
                            c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
                            c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
                            c->palette.as<const float4>(), c->tile_first.as<const uint4>(), match, mlo, mhi,
-                           c->vtx.as<float4>(), grid);
+                           c->vtx.as<float4>(), grid, ml_dev, gate);
         wg_stage_end(c);
     };
     if (early) launch(vcap, std::min((vcap + TILE - 1) / TILE, tcap - 1));
-    uint64_t total = 0;
-    if (const int rc = wg_fetch_end(c, &total)) return rc;
+    uint64_t fv[1 + WG_PENDING_ITEMS] = {0};
+    if (const int rc = wg_fetch_end(c, fv)) return rc;
+    if (npend) {   // validate the build; one that did not hold is redone here, with this frame and emission
+        bool redone = false;
+        if (const int rc = wg_validate_pending(c, fv + 1, &redone)) return rc;
+        if (redone) return WG_OK;
+    }
+    const uint64_t total = fv[0];
     c->n_vtx = total;
     const uint64_t ntiles = (total + TILE - 1) / TILE;
     if (!early || total > vcap || ntiles + 1 > tcap) {   // did not fit: size the buffers and launch again

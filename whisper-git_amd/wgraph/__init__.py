@@ -182,6 +182,12 @@ class Engine:
         """Force the general lane walk (True) or auto-select (False)."""
         self._check(lib().wg_set_option(self._ctx, 1, 1 if general else 0))
 
+    def set_defer_validation(self, on: bool):
+        """WG_OPT_DEFER_VALIDATION: a speculative build is validated with the
+        next emission's vertex-total read instead of before build() returns
+        (results identical; a build that does not hold is redone there)."""
+        self._check(lib().wg_set_option(self._ctx, 5, 1 if on else 0))
+
     # -- layout ----------------------------------------------------------------------
     def build(self, dag=None, commits: abi.Commits | None = None):
         """GraphLayout::build on a wgraph.synth.Dag (host) or a prepared wg_commits."""
