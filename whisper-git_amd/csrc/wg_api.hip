@@ -416,11 +416,13 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
     case WG_OPT_REPLAY_CHUNK:
         if (value < 64 || value > (1 << 20) || (value & 63)) return wg_fail(c, WG_E_INVALID, "replay chunk must be a multiple of 64");
         c->replay_chunk = (uint32_t)value;
+        c->replay_auto = false;
         return WG_OK;
     case WG_OPT_TIMING_EMIT_ONLY: c->timing_emit_only = value != 0; return WG_OK;
     case WG_OPT_REPLAY_WARMUP:
         if (value < 0 || value > 3584 || (value & 63)) return wg_fail(c, WG_E_INVALID, "replay warm-up must be a multiple of 64 in 0..3584");
         c->replay_warm = (uint32_t)value;
+        c->replay_auto = false;
         return WG_OK;
     case WG_OPT_DEFER_VALIDATION:
         WG_SETTLE(c);

@@ -204,6 +204,9 @@ __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, co
     }
 }
 
+constexpr int GO_T = 256, GO_Q = 8;
+constexpr uint64_t GO_TILE = (uint64_t)GO_T * GO_Q;
+
 // 8 consecutive words at a 32-byte aligned address
 __device__ __forceinline__ void ld8(const uint32_t *p, uint32_t (&v)[8]) {
     const uint4 a = reinterpret_cast<const uint4 *>(p)[0], b = reinterpret_cast<const uint4 *>(p)[1];
@@ -214,64 +217,79 @@ __device__ __forceinline__ void st8(uint32_t *p, const uint32_t (&v)[8]) {
     reinterpret_cast<uint4 *>(p)[1] = make_uint4(v[4], v[5], v[6], v[7]);
 }
 
-// The sweep's carry-in offsets from the chunk difference counts (nch + 1
-// entries) in one single-block launch: their exclusive scan (the edges alive
-// across each chunk start), then the exclusive scan of those counts
-constexpr int CO_T = 1024;
-constexpr uint64_t CO_MAX = 32 * (uint64_t)CO_T;
-__device__ __forceinline__ uint32_t co_block_excl(uint32_t v, uint32_t *ws) {
-    const uint32_t inc = wg_wave_scan(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
-    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = inc;
+// Tile sums (GO_TILE entries) of the three difference arrays the offsets
+// kernel scans: the full-vertical and curve spans per row (n + 1 entries) and
+// the sweep's carry-in counts per 64-row chunk (nch + 1 entries; tiles past
+// its end sum to 0)
+__global__ void __launch_bounds__(GO_T) k_tile_sums3(const uint32_t *__restrict__ F, const uint32_t *__restrict__ C,
+                                                    const uint32_t *__restrict__ D, uint64_t n1, uint64_t nd1,
+                                                    uint32_t *__restrict__ tsF, uint32_t *__restrict__ tsC,
+                                                    uint32_t *__restrict__ tsD) {
+    __shared__ uint32_t ws[GO_T / 64];
+    const int a = blockIdx.y;
+    const uint32_t *in = a == 0 ? F : (a == 1 ? C : D);
+    const uint64_t len = a == 2 ? nd1 : n1;
+    const uint64_t base = (uint64_t)blockIdx.x * GO_TILE + (uint64_t)threadIdx.x * GO_Q;
+    uint32_t v[GO_Q];
+    if (base + GO_Q <= len) ld8(in + base, v);
+    else
+#pragma unroll
+        for (int k = 0; k < GO_Q; k++) v[k] = base + k < len ? in[base + k] : 0u;
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < GO_Q; k++) t += v[k];
+    t = wg_wave_scan(t, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = t;
     __syncthreads();
-    uint32_t base = 0;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) base += ws[w];
-    __syncthreads();
-    return base + inc - v;
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < GO_T / 64; w++) tot += ws[w];
+        (a == 0 ? tsF : (a == 1 ? tsC : tsD))[blockIdx.x] = tot;
+    }
 }
-// each thread owns a run of q <= 32 consecutive entries, held in registers:
-// both scans cost one load round and one block scan each
-__global__ void __launch_bounds__(CO_T) k_carry_offsets(uint64_t nch, uint32_t *__restrict__ diff, uint32_t *__restrict__ off) {
-    __shared__ uint32_t ws[CO_T / 64];
-    const uint32_t q = (uint32_t)((nch + 1 + CO_T - 1) / CO_T);
-    const uint64_t a = (uint64_t)threadIdx.x * q;
-    uint32_t v[32];
+
+// ordered exclusive block scan (GO_T threads) of two values at once (defined below)
+__device__ __forceinline__ uint2 go_block_excl(uint2 v, uint2 &tot);
+
+// The sweep's carry-in counts of chunks [base, base + 8) from the chunk
+// difference array D (nch + 1 entries, the tile's exclusive offset pre): the
+// count of chunk k is the exclusive scan of D at k + 1; written over D[k]
+// (each thread reads its entries before it writes them), with their 256-entry
+// sums for the carry offsets' scan (wg_scan_bs_u32)
+__device__ __forceinline__ void carry_counts(uint32_t *D, uint64_t nch, uint64_t base, uint32_t pre, uint32_t *bsD,
+                                             uint64_t nbsD) {
+    uint32_t v[GO_Q];
+    if (base + GO_Q <= nch + 1) ld8(D + base, v);
+    else
+#pragma unroll
+        for (int k = 0; k < GO_Q; k++) v[k] = base + k <= nch ? D[base + k] : 0u;
     uint32_t s = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 32; j++) {
-        v[j] = (j < q && a + j <= nch) ? diff[a + j] : 0u;
-        s += v[j];
-    }
-    // pass 1: exclusive scan of diff[0..nch]; entry k + 1 is the count of chunk k
-    uint32_t run = co_block_excl(s, ws);
+    for (int k = 0; k < GO_Q; k++) s += v[k];
+    uint2 tot;
+    uint32_t run = go_block_excl(make_uint2(s, 0u), tot).x + pre;
+    uint32_t ex[GO_Q + 1];
 #pragma unroll
-    for (uint32_t j = 0; j < 32; j++) {
-        const uint32_t t = v[j];
-        v[j] = run;
-        run += t;
-    }
-    // run = the exclusive value one past this thread's run (the next thread's
-    // first): pass 2 scans the counts off[k] <- scan(ex[k + 1]), k < nch
-    uint32_t w[32];
-    s = 0;
+    for (int k = 0; k < GO_Q; k++) { ex[k] = run; run += v[k]; }
+    ex[GO_Q] = run;   // the next entry's exclusive value
+    uint32_t cnt[GO_Q], t = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 32; j++) {
-        const uint32_t nxt = (j + 1 < 32 && j + 1 < q) ? v[(j + 1) & 31] : run;   // ex[a + j + 1]
-        w[j] = (j < q && a + j < nch) ? nxt : 0u;
-        s += w[j];
+    for (int k = 0; k < GO_Q; k++) {
+        cnt[k] = base + k < nch ? ex[k + 1] : 0u;
+        t += cnt[k];
     }
-    run = co_block_excl(s, ws);
+    if (base + GO_Q <= nch) st8(D + base, cnt);
+    else
 #pragma unroll
-    for (uint32_t j = 0; j < 32; j++) {
-        if (j < q && a + j < nch) off[a + j] = run;
-        run += w[j];
-    }
-    if (a < nch && a + q >= nch) off[nch] = run;   // the thread owning the last count
-    if (nch == 0 && threadIdx.x == 0) off[0] = 0u;
+        for (int k = 0; k < GO_Q; k++)
+            if (base + k < nch) D[base + k] = cnt[k];
+#pragma unroll
+    for (int d = 16; d >= 1; d >>= 1) t += (uint32_t)__shfl_xor((int)t, d, 64);
+    const uint64_t sub = base / WG_BS_THREADS;
+    if ((threadIdx.x & 31) == 0 && sub < nbsD) bsD[sub] = t;
 }
 
 // ordered exclusive block scan (GO_T threads) of two values at once
-constexpr int GO_T = 256, GO_Q = 8;
-constexpr uint64_t GO_TILE = (uint64_t)GO_T * GO_Q;
 __device__ __forceinline__ uint2 go_block_excl(uint2 v, uint2 &tot) {
     __shared__ uint2 ws[GO_T / 64];
     const uint32_t a = wg_wave_scan(v.x, 0u, [](uint32_t x, uint32_t y) { return x + y; });
@@ -300,10 +318,15 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
                                                       const uint32_t *__restrict__ tsC, const uint32_t *__restrict__ cntT,
                                                       const uint32_t *__restrict__ cntB, const uint32_t *__restrict__ cntCend,
                                                       uint32_t *__restrict__ nV, uint32_t *__restrict__ nC,
-                                                      uint32_t *__restrict__ bsV, uint32_t *__restrict__ bsC, uint64_t nbs) {
+                                                      uint32_t *__restrict__ bsV, uint32_t *__restrict__ bsC, uint64_t nbs,
+                                                      uint32_t *D, const uint32_t *__restrict__ tsD, uint64_t nch,
+                                                      uint32_t *__restrict__ bsD, uint64_t nbsD) {
     uint2 pre = make_uint2(0u, 0u), ptot;
-    for (uint64_t b = threadIdx.x; b < blockIdx.x; b += GO_T) { pre.x += tsF[b]; pre.y += tsC[b]; }
+    uint2 preD = make_uint2(0u, 0u), ptotD;
+    for (uint64_t b = threadIdx.x; b < blockIdx.x; b += GO_T) { pre.x += tsF[b]; pre.y += tsC[b]; preD.x += tsD[b]; }
     (void)go_block_excl(pre, ptot);
+    (void)go_block_excl(preD, ptotD);
+    carry_counts(D, nch, (uint64_t)blockIdx.x * GO_TILE + (uint64_t)threadIdx.x * GO_Q, ptotD.x, bsD, nbsD);
     const uint64_t base = (uint64_t)blockIdx.x * GO_TILE + (uint64_t)threadIdx.x * GO_Q;
     uint32_t vF[GO_Q], vC[GO_Q], vT[GO_Q], vB[GO_Q], vE[GO_Q];
     const bool full = base + GO_Q <= n;   // every item a row (and within the n + 1 entries): 16-byte accesses
@@ -1041,26 +1064,25 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     // of the per-chunk counts it holds one entry later
     WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
     uint32_t *carry_off = c->carry_off.as<uint32_t>();
-    if (nch + 1 <= CO_MAX) {
-        hipLaunchKernelGGL(k_carry_offsets, dim3(1), dim3(CO_T), 0, s, nch, carry_cnt, carry_off);
-    } else {   // (more than 2M rows: two scans)
-        WG_HIP(c, wg_exclusive_scan_u32(carry_cnt, carry_cnt, nch + 1, c->scan_tmp.p, s));
-        WG_HIP(c, wg_exclusive_scan_u32(carry_cnt + 1, carry_off, nch, c->scan_tmp.p, s));
-    }
-    // row offsets: tile sums of the two difference arrays, one kernel for their
-    // scans + the per-row list totals (+ 256-row sums), one for the offsets
-    const uint64_t nbs = wg_bs_blocks(n), nt2 = (n + 1 + 2047) / 2048;
-    WG_ALLOC(c, c->bsum, (2 * nbs + 2 * nt2 + 256) * 4);
-    uint32_t *bsV = c->bsum.as<uint32_t>(), *bsC = bsV + nbs, *tsF = bsC + nbs, *tsC = tsF + nt2 + 64;
-    WG_HIP(c, wg_tile_sums2_u32(cntF, cntC, n + 1, tsF, tsC, s));
+
+    // offsets: tile sums of the three difference arrays; one kernel for their
+    // scans, the per-row list totals and the per-chunk carry counts (+ their
+    // 256-entry sums); one launch for the three offset arrays
+    const uint64_t nbs = wg_bs_blocks(n), nbsD = wg_bs_blocks(nch), nt2 = (n + 1 + GO_TILE - 1) / GO_TILE;
+    WG_ALLOC(c, c->bsum, (2 * nbs + nbsD + 3 * nt2 + 512) * 4);
+    uint32_t *bsV = c->bsum.as<uint32_t>(), *bsC = bsV + nbs, *bsD = bsC + nbs;
+    uint32_t *tsF = bsD + nbsD + 64, *tsC = tsF + nt2 + 64, *tsD = tsC + nt2 + 64;
+    hipLaunchKernelGGL(k_tile_sums3, dim3((uint32_t)nt2, 3), dim3(GO_T), 0, s, (const uint32_t *)cntF, (const uint32_t *)cntC,
+                       (const uint32_t *)carry_cnt, n + 1, nch + 1, tsF, tsC, tsD);
     hipLaunchKernelGGL(k_geom_offsets, dim3((uint32_t)nt2), dim3(GO_T), 0, s, n, cntF, cntC, (const uint32_t *)tsF,
                        (const uint32_t *)tsC, (const uint32_t *)cntT, (const uint32_t *)cntB, (const uint32_t *)cntCend,
-                       voff, soff, bsV, bsC, nbs);
+                       voff, soff, bsV, bsC, nbs, carry_cnt, (const uint32_t *)tsD, nch, bsD, nbsD);
     {
         WgScanBs S;
-        S.na = 2;
+        S.na = 3;
         S.in[0] = voff; S.out[0] = voff; S.bsum[0] = bsV;
         S.in[1] = soff; S.out[1] = soff; S.bsum[1] = bsC;
+        S.in[2] = carry_cnt; S.out[2] = carry_off; S.bsum[2] = bsD; S.len[2] = nch;
         WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, s));
     }
     // list capacities: exact from the totals, or (speculative build) the

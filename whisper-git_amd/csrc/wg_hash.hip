@@ -10,6 +10,7 @@
 //   prow[k]   = canonical row of parent reference k, or -1 if not in the list
 #include "wg_internal.h"
 #include "wg_hashfn.h"
+#include "wg_lanes_refs.h"
 
 namespace {
 
@@ -26,10 +27,13 @@ namespace {
 // Two tables alternate between builds: the place pass also empties the other
 // one (and its duplicate word) for the next build, so no fill launch precedes
 // the join.
+// (lf.first_ref set: the lane stage's initial state too, LfClear)
 __global__ void k_hash_place(const uint8_t *__restrict__ oid, uint64_t n, unsigned long long *table, uint64_t mask,
-                             unsigned long long *next_table, uint64_t next_words) {
+                             unsigned long long *next_table, uint64_t next_words, LfClear lf) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t w = i; w < next_words; w += (uint64_t)gridDim.x * blockDim.x) next_table[w] = HEMPTY;
+    if (lf.first_ref)
+        for (uint64_t w = i; w < n + 16; w += (uint64_t)gridDim.x * blockDim.x) lf_clear_at(lf, n, w);
     if (i >= n) return;
     const Key k = load_key(oid + i * 20);
     table[key_hash(k) & mask] = ((unsigned long long)key_fp(k) << 32) | (uint32_t)i;
@@ -65,13 +69,16 @@ __global__ void k_hash_settle(const uint8_t *__restrict__ oid, uint64_t n, unsig
 // key: ids all distinct), prow of the row's parent references (-1: not in
 // the list, :306-311) and the row's edge count (parents found, lane-
 // independent, so the edge offsets are ready before the lanes are) with the
-// block's sum of it for the offsets' scan (wg_scan_bs_u32).
+// block's sum of it for the offsets' scan (wg_scan_bs_u32).  first_ref set:
+// then the lane fast path's reference pass of the row (lf_refs_row, the
+// k_lf_refs of a single-GPU build) on the parents just resolved.
 __global__ void __launch_bounds__(WG_BS_THREADS) k_probe_rows(const uint8_t *__restrict__ oid, uint64_t n,
                                                              const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
                                                              const unsigned long long *__restrict__ table, uint64_t mask,
                                                              const uint32_t *__restrict__ dup, uint32_t *__restrict__ canon,
                                                              int32_t *__restrict__ prow, uint32_t *__restrict__ edge_cnt,
-                                                             uint32_t *__restrict__ bsum) {
+                                                             uint32_t *__restrict__ bsum, LfRange R,
+                                                             unsigned long long *first_ref, uint32_t *fpc, uint32_t *viol) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t cnt = 0;
     if (i < n) {
@@ -87,6 +94,7 @@ __global__ void __launch_bounds__(WG_BS_THREADS) k_probe_rows(const uint8_t *__r
             cnt += p >= 0;
         }
         edge_cnt[i] = cnt;
+        if (first_ref && lf_refs_row(R, i, first_ref, fpc)) atomicOr(viol, 1u);
     }
     wg_bsum_store(cnt, bsum);
 }
@@ -115,14 +123,43 @@ int wg_stage_hash_join(wg_ctx *c) {
     uint32_t *dup = reinterpret_cast<uint32_t *>(table + cap);
     const int T = WG_BS_THREADS;
     const uint32_t g = (uint32_t)((n + T - 1) / T);
+    c->lf_refs_done = false;
     if (n) {
+        // the lane fast path's clear and reference pass ride on these kernels
+        // (wg_lf_refs skips its own: lf_refs_done)
+        LfClear L;
+        LfRange R;
+        const bool lanes = !c->force_general_lanes;
+        if (lanes) {
+            WG_ALLOC(c, c->lf[LF_FIRST], n * 8 + 8);
+            WG_ALLOC(c, c->lf[LF_LFIRST], n * 8 + 8);
+            WG_ALLOC(c, c->lf[LF_FPC], (n + 2) * 4);
+            WG_ALLOC(c, c->lf[LF_CHFILL], (n + 2) * 4);
+            WG_ALLOC(c, c->lf[LF_FLAGS], 64);
+            WG_ALLOC(c, c->lane_scalars, 64);
+            L.first_ref = c->lf[LF_FIRST].as<unsigned long long>();
+            L.lfirst = c->lf[LF_LFIRST].as<unsigned long long>();
+            L.fpc = c->lf[LF_FPC].as<uint32_t>();
+            L.ch_fill = c->lf[LF_CHFILL].as<uint32_t>();
+            L.flags = c->lf[LF_FLAGS].as<uint32_t>();
+            L.scal = c->lane_scalars.as<uint32_t>();
+            R.s = 0;
+            R.nl = n;
+            R.e = n;
+            R.poff = c->d_poff;
+            R.prow = c->prow.as<const int32_t>();
+            R.canon = c->canon.as<const uint32_t>();
+            R.lfirst = L.lfirst;
+        }
         hipLaunchKernelGGL(k_hash_place, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1,
-                           c->htab[o].as<unsigned long long>(), words);
+                           c->htab[o].as<unsigned long long>(), words, L);
         c->htab_clean[o] = words;
         hipLaunchKernelGGL(k_hash_settle, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1, dup);
         hipLaunchKernelGGL(k_probe_rows, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
                            (const unsigned long long *)table, cap - 1, (const uint32_t *)dup, c->canon.as<uint32_t>(),
-                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->bsum.as<uint32_t>());
+                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->bsum.as<uint32_t>(), R, L.first_ref,
+                           L.fpc, L.flags);
+        c->lf_refs_done = lanes;
         WgScanBs S;
         S.na = 1;
         S.in[0] = c->edge_cnt.as<const uint32_t>();

@@ -256,6 +256,14 @@ struct wg_ctx {
     DevBuf lf[LF_COUNT];    // event-compressed lane path workspaces (wg_lanes_fast.hip), indexed by LF_*
     uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
     uint32_t replay_warm = 0;      // iteration 1's warm-up events before each chunk (WG_OPT_REPLAY_WARMUP)
+    bool replay_auto = true;       // neither option set: chunk / warm-up follow the last build's event count
+    // (profiles/r03i tune: 512 / 0 is best from ~40k events up; below ~25k
+    // events — random13 100k, 13.9k events: 0.163 -> 0.117 ms — 256 / 256)
+    void replay_geometry(uint32_t *chunk, uint32_t *warm) const {
+        *chunk = replay_chunk;
+        *warm = replay_warm;
+        if (replay_auto && n_events > 0 && n_events < 24576) { *chunk = 256; *warm = 256; }
+    }
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
     uint32_t replay_nw = 1;        // occupancy words of the next replay (from the last build's slot count)
@@ -274,6 +282,7 @@ struct wg_ctx {
     uint64_t e_refs_own = 0;   // parent references of the rows this context owns
     bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])
     bool lane_out_fused = false;
+    bool lf_refs_done = false;     // the hash join's kernels did the lane stage's clear + reference pass (single GPU)
     bool edges_pending = false;    // the edge list is written by the next full geometry pass (k_edges_rows)   // the lane kernel wrote lane_out / color_out (speculative fast path)
     bool force_general_lanes = false;   // WG_LANES=general (testing the general walk)
     ReplayRun spec_run;     // the speculative build's replay (its iteration count and flag words)
@@ -508,6 +517,7 @@ struct WgScanBs {
     const uint32_t *in[3] = {nullptr, nullptr, nullptr};
     uint32_t *out[3] = {nullptr, nullptr, nullptr};
     const uint32_t *bsum[3] = {nullptr, nullptr, nullptr};   // [ceil(n / WG_BS_THREADS)] each
+    uint64_t len[3] = {0, 0, 0};   // an array shorter than n (0: n)
 };
 // out[a][0..n] = exclusive scan of in[a] (out[a][n] = total); in may alias out.
 // tmp: c->scan_tmp after wg_scan_reserve(c, n).

@@ -45,11 +45,11 @@
 // crossing entries.  A waiter created before s is a crossing token (WG_TOK_X)
 // until the other shards report which event started its chain.
 #include "wg_internal.h"
+#include "wg_lanes_refs.h"
 
 namespace {
 
 constexpr int T = 256;
-constexpr uint64_t REF_NONE = ~0ull;
 constexpr uint32_t TAGS = WG_TOK_EV | WG_TOK_X;
 
 // event record flags (uint4.x): A = takes the lowest free slot, O = occupies
@@ -67,17 +67,6 @@ __device__ __forceinline__ uint32_t token_bits(uint64_t e, uint32_t t0, uint32_t
 
 inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
 
-__device__ __forceinline__ unsigned long long ref_key(uint64_t row, uint32_t kidx) {
-    return ((unsigned long long)row << 16) | kidx;
-}
-
-// is parent ref k of a row (refs from pa) the first occurrence of that parent in the row's in-list refs?
-__device__ __forceinline__ bool first_in_row(const int32_t *__restrict__ prow, uint32_t pa, uint32_t k, int32_t p) {
-    for (uint32_t q = pa; q < k; q++)
-        if (prow[q] == p) return false;
-    return true;
-}
-
 // is ref k (row gi, index kidx, target p) the first in-list reference to p?
 __device__ __forceinline__ bool is_first_ref(const LfRange &R, const unsigned long long *__restrict__ first_ref,
                                              uint64_t gi, uint32_t k, uint32_t kidx, uint64_t p) {
@@ -90,24 +79,7 @@ __device__ __forceinline__ bool is_first_ref(const LfRange &R, const unsigned lo
 __global__ void k_lf_refs(LfRange R, unsigned long long *first_ref, uint32_t *fpc, uint32_t *viol) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R.nl) return;
-    const uint64_t gi = R.s + i;
-    bool bad = R.canon && R.canon[gi] != (uint32_t)gi;
-    const uint32_t pa = R.poff[gi], pb = R.poff[gi + 1];
-    for (uint32_t k = pa; k < pb; k++) {
-        const int32_t p = R.prow[k];
-        if (p < 0) continue;
-        if (k - pa > 0xFFFFu) { bad = true; continue; }
-        if ((uint64_t)p <= gi) {                     // leaky: target at this row or earlier
-            if (!R.lfirst || (uint64_t)p < R.s) { bad = true; continue; }
-            if (first_in_row(R.prow, pa, k, p)) atomicMin(&R.lfirst[p - R.s], ref_key(gi, k - pa));
-            continue;
-        }
-        if ((uint64_t)p >= R.e) continue;            // beyond the shard: crossing entry
-        if (!first_in_row(R.prow, pa, k, p)) continue;
-        atomicMin(&first_ref[p - R.s], ref_key(gi, k - pa));
-        if (k == pa) atomicAdd(&fpc[p - R.s], 1u);
-    }
-    if (bad) atomicOr(viol, 1u);
+    if (lf_refs_row(R, R.s + i, first_ref, fpc)) atomicOr(viol, 1u);
 }
 
 // references from earlier shards into this one
@@ -383,15 +355,8 @@ __global__ void k_lf_lanes(uint64_t nl, const uint32_t *__restrict__ sp, const u
 // the lane stage's initial state in one launch (instead of four fills):
 // first references "none", per-row counters and the chain fill counters 0,
 // the flag words 0
-__global__ void k_lf_clear(uint64_t n, unsigned long long *__restrict__ first_ref, uint32_t *__restrict__ fpc,
-                           uint32_t *__restrict__ ch_fill, uint32_t *__restrict__ flags,
-                           unsigned long long *__restrict__ lfirst, uint32_t *__restrict__ scal) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) first_ref[i] = REF_NONE;
-    if (lfirst && i < n) lfirst[i] = REF_NONE;
-    if (i < n + 2) { fpc[i] = 0u; ch_fill[i] = 0u; }
-    if (i < 16) flags[i] = 0u;
-    if (scal && i < 16) scal[i] = 0u;   // the lane scalars (max_lane, slots, overflow, ...)
+__global__ void k_lf_clear(uint64_t n, LfClear L) {
+    lf_clear_at(L, n, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x);   // (+ the lane scalars: max_lane, slots, ...)
 }
 
 // gathered shard-local records (k_lf_events<true> of every rank, rank r's at
@@ -447,10 +412,20 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back, uint32_t *scal) {
     WG_ALLOC(c, c->bsum, 3 * (nbs + 64) * 4);
     { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "lf_refs");
-    hipLaunchKernelGGL(k_lf_clear, dim3(blocks(n + 16)), dim3(T), 0, s, n, first_ref.as<unsigned long long>(),
-                       fpc.as<uint32_t>(), ch_fill.as<uint32_t>(), flags.as<uint32_t>(), R.lfirst, scal);
-    if (n) hipLaunchKernelGGL(k_lf_refs, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<unsigned long long>(),
-                              fpc.as<uint32_t>(), flags.as<uint32_t>());
+    if (c->lf_refs_done) {   // cleared by the hash join's place pass, references taken by its per-row probe
+        c->lf_refs_done = false;
+    } else {
+        LfClear L;
+        L.first_ref = first_ref.as<unsigned long long>();
+        L.lfirst = R.lfirst;
+        L.fpc = fpc.as<uint32_t>();
+        L.ch_fill = ch_fill.as<uint32_t>();
+        L.flags = flags.as<uint32_t>();
+        L.scal = scal;
+        hipLaunchKernelGGL(k_lf_clear, dim3(blocks(n + 16)), dim3(T), 0, s, n, L);
+        if (n) hipLaunchKernelGGL(k_lf_refs, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<unsigned long long>(),
+                                  fpc.as<uint32_t>(), flags.as<uint32_t>());
+    }
     if (R.xin_end)
         hipLaunchKernelGGL(k_lf_xin, dim3(blocks(R.xin_end)), dim3(T), 0, s, R, first_ref.as<unsigned long long>(),
                            fpc.as<uint32_t>());
@@ -616,8 +591,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
     ReplayRun run;
     run.nev = nev;
     run.nw = nw;
-    run.chunk = c->replay_chunk;
-    run.warm = c->replay_warm;
+    c->replay_geometry(&run.chunk, &run.warm);
     const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
@@ -696,8 +670,7 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     run = ReplayRun{};
     run.nev = nev_cap;
     run.nw = c->replay_nw;
-    run.chunk = c->replay_chunk;
-    run.warm = c->replay_warm;
+    c->replay_geometry(&run.chunk, &run.warm);
     const uint64_t nch = (nev_cap + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];

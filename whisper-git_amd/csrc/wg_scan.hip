@@ -187,11 +187,14 @@ struct ScanBsArgs {
     uint32_t *out[3];
     const uint32_t *bsum[3];
     const uint32_t *bpre[3];   // exclusive scan of bsum, or null
+    uint64_t n[3];
 };
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_bs_down(ScanBsArgs P, uint64_t n) {
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_bs_down(ScanBsArgs P) {
     const int a = blockIdx.y;
     const uint32_t *in = P.in[a];
     uint32_t *out = P.out[a];
+    const uint64_t n = P.n[a];
+    if ((uint64_t)blockIdx.x * SCAN_TILE > n) return;   // (a shorter array: its tiles end earlier)
     const uint64_t b0 = (uint64_t)blockIdx.x * BS_PER_TILE;
     uint32_t ptot;
     if (P.bpre[a]) {
@@ -282,13 +285,14 @@ hipError_t wg_exclusive_scan2_u32(const uint32_t *in0, uint32_t *out0, const uin
 
 hipError_t wg_scan_bs_u32(const WgScanBs &S, uint64_t n, void *tmp, hipStream_t s) {
     ScanBsArgs P{};
-    const uint64_t nbs = wg_bs_blocks(n);
     char *t = (char *)tmp;
     for (int a = 0; a < S.na; a++) {
         P.in[a] = S.in[a];
         P.out[a] = S.out[a];
         P.bsum[a] = S.bsum[a];
         P.bpre[a] = nullptr;
+        P.n[a] = S.len[a] ? S.len[a] : n;
+        const uint64_t nbs = wg_bs_blocks(P.n[a]);
         if (nbs > WG_BS_SELF) {   // many tiles: scan the producer sums first (one array of the tmp at a time)
             uint32_t *pre = reinterpret_cast<uint32_t *>(t);
             t += ((nbs + 1) * 4 + 255) & ~size_t(255);
@@ -297,9 +301,9 @@ hipError_t wg_scan_bs_u32(const WgScanBs &S, uint64_t n, void *tmp, hipStream_t 
             P.bpre[a] = pre;
         }
     }
-    if (nbs > WG_BS_SELF && (size_t)(t - (char *)tmp) + tmp_bytes_rec<uint64_t>(nbs) > wg_scan_tmp_bytes(n))
+    if ((size_t)(t - (char *)tmp) + tmp_bytes_rec<uint64_t>(wg_bs_blocks(n)) > wg_scan_tmp_bytes(n))
         return hipErrorInvalidValue;   // (cannot happen: 3 (n/256 + 65) u32 + the recursion fit the reserve)
-    hipLaunchKernelGGL(k_scan_bs_down, dim3((uint32_t)nblocks(n), (uint32_t)S.na), dim3(SCAN_THREADS), 0, s, P, n);
+    hipLaunchKernelGGL(k_scan_bs_down, dim3((uint32_t)nblocks(n), (uint32_t)S.na), dim3(SCAN_THREADS), 0, s, P);
     return hipGetLastError();
 }
 
