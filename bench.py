@@ -52,6 +52,8 @@ def parse():
                     help="gloo rehearsal: move HIP-resident slots through gloo (the stream-ordered slot path of RCCL)")
     ap.add_argument("--no-defer", action="store_true",
                     help="validate every speculative build before build() returns (WG_OPT_DEFER_VALIDATION off)")
+    ap.add_argument("--no-build-frame", action="store_true",
+                    help="separate build() and row_geometry() calls instead of wg_layout_build_frame")
     ap.add_argument("--all-stage-events", action="store_true",
                     help="record every stage's HIP events inside the timed region (default: only the emission "
                          "kernel's, for the roofline; the stage breakdown comes from a separate pass)")
@@ -498,9 +500,11 @@ def main():
         comm = ShardComm(dev, device_transport=True if args.device_transport else None)
 
     def step():
-        if comm is None:
+        if comm is None and args.no_build_frame:
             eng.build(commits=commits)
             eng.row_geometry(device_ptr=t_band.data_ptr())
+        elif comm is None:   # the same two calls, the frame's row_top beside the build
+            eng.build_frame(commits=commits, device_ptr=t_band.data_ptr())
         else:
             eng.shard_build(commits, world, rank, shard0, shard1, comm)
             eng.shard_geometry(comm, device_ptr=t_band.data_ptr())

@@ -243,6 +243,11 @@ int wg_compute_row_heights(wg_ctx *ctx, const int64_t *time, uint64_t n, int32_t
  * band == NULL reproduces GraphLayout::row_geometry from build (:322-346);
  * otherwise band[N] (residency as given) is the per-row pills band.      */
 int wg_row_geometry(wg_ctx *ctx, const float *band, int32_t band_residency);
+/* wg_layout_build then wg_row_geometry(band) — history_view's first frame
+ * after a refresh (commit_graph.rs:1419-1421) — in one call: the frame's
+ * banded row_top (heights and band only) is computed on the engine's side
+ * stream beside the build.  Results identical to the two calls. */
+int wg_layout_build_frame(wg_ctx *ctx, const wg_commits *commits, const float *band, int32_t band_residency);
 int wg_geometry_summary_get(wg_ctx *ctx, wg_geometry_summary *out);
 int wg_copy_geometry(wg_ctx *ctx, const wg_geometry_host *dst);
 

@@ -118,3 +118,62 @@ def test_deferred_validation_sequence():
         assert int(last[8]) >= 2              # and some were redone (capacity, well-formedness)
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("defer", [False, True])
+def test_build_frame_sequence(defer):
+    """wg_layout_build_frame = wg_layout_build + wg_row_geometry(band), the
+    frame's row_top computed beside the build: bit-exact against the oracle's
+    build + row_geometry_with_bands over a sequence of lists (host and device
+    bands, repeats, a redone speculative build), with plain builds and
+    frame passes interleaved; an empty list too."""
+    import torch
+    import wgraph
+    from oracle import oracle_c
+    eng = wgraph.Engine(0)
+    try:
+        eng.set_defer_validation(defer)
+        seq = [("wide16", 3000, 1), ("wide16", 3000, 1), ("wide16", 40000, 3), ("anomaly", 2000, 4),
+               ("random13", 20000, 5), ("linux", 60000, 6), ("linear", 500, 7), ("skew", 30000, 8),
+               ("linuxwide", 20000, 9)]
+        for i, (kind, n, seed) in enumerate(seq):
+            d = synth.generate(kind, n, seed=seed)
+            o = oracle_c.OracleLayout(d)
+            tag = f"#{i} {kind}/{n} defer={defer}"
+            keep = None
+            if i % 3 == 0:
+                eng.build_frame(d, band=d.band)
+            elif i % 3 == 1:
+                keep = torch.from_numpy(d.band).to("cuda:0")
+                torch.cuda.synchronize()
+                eng.build_frame(d, device_ptr=keep.data_ptr())
+            else:
+                eng.build(d)
+                eng.row_geometry(d.band)
+            sel = d.n // 3
+            eng.emit_vertices(0, d.n, selected=sel)
+            og = o.row_geometry(d.band)
+            ov, _ = o.emit_vertices(0, d.n, selected=sel)
+            assert eng.vertex_summary().checksum == oracle_c.vertex_checksum(ov), tag
+            got = eng.geometry()
+            for k, v in og.items():
+                assert_bits(f"{tag} band_{k}", got[k], v)
+            lane, color = eng.lanes()
+            assert_bits(tag + " lane", lane, o.lane)
+            assert_bits(tag + " color", color, o.color)
+            # the next frame with other bands goes through the normal frame pass
+            b2 = d.band.copy()
+            b2[d.n // 2:] += 7.0
+            eng.row_geometry(b2)
+            og2 = o.row_geometry(b2)
+            got = eng.geometry()
+            assert_bits(tag + " reband row_top", got["row_top"], og2["row_top"])
+            assert_bits(tag + " reband node_y", got["node_y"], og2["node_y"])
+            o.close()
+            del keep
+        e = synth.generate("linear", 0, seed=1)
+        eng.build_frame(e, band=e.band)
+        assert eng.geometry_summary().n_rows == 0
+    finally:
+        eng.close()

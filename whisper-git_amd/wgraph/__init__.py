@@ -65,6 +65,7 @@ def lib():
             "wg_copy_row_heights": ([vp, vp], ctypes.c_int),
             "wg_compute_row_heights": ([vp, vp, u64, i32, vp], ctypes.c_int),
             "wg_row_geometry": ([vp, vp, i32], ctypes.c_int),
+            "wg_layout_build_frame": ([vp, ctypes.POINTER(abi.Commits), vp, i32], ctypes.c_int),
             "wg_geometry_summary_get": ([vp, ctypes.POINTER(abi.GeometrySummary)], ctypes.c_int),
             "wg_copy_geometry": ([vp, ctypes.POINTER(abi.GeometryHost)], ctypes.c_int),
             "wg_emit_vertices": ([vp, u64, u64, i64, vp], ctypes.c_int),
@@ -111,7 +112,7 @@ def lib():
 EXPORTED_SYMBOLS = (
     "wg_abi_version", "wg_create", "wg_destroy", "wg_last_error", "wg_set_stream", "wg_synchronize", "wg_set_option",
     "wg_layout_build", "wg_layout_summary_get", "wg_copy_lanes", "wg_copy_edges", "wg_copy_row_heights",
-    "wg_compute_row_heights",    "wg_row_geometry", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
+    "wg_compute_row_heights", "wg_row_geometry", "wg_layout_build_frame", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
     "wg_shard_copy_msg", "wg_shard_msg_bytes", "wg_shard_pack_slot", "wg_shard_slot_heads", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
@@ -196,6 +197,20 @@ class Engine:
             self._keep = [dag]
         self._commits = commits
         self._check(lib().wg_layout_build(self._ctx, ctypes.byref(commits)))
+
+    def build_frame(self, dag=None, commits: abi.Commits | None = None, band=None, device_ptr: int | None = None):
+        """build() then row_geometry(band) in one call (wg_layout_build_frame):
+        the frame's banded row_top runs on the side stream beside the build."""
+        if commits is None:
+            commits = abi.commits_struct(dag)
+            self._keep = [dag]
+        self._commits = commits
+        if device_ptr is not None:
+            self._check(lib().wg_layout_build_frame(self._ctx, ctypes.byref(commits), device_ptr, abi.WG_DEVICE))
+        else:
+            b = np.ascontiguousarray(band, np.float32)
+            self._band = b
+            self._check(lib().wg_layout_build_frame(self._ctx, ctypes.byref(commits), b.ctypes.data, abi.WG_HOST))
 
     # -- row-sharded build (one rank per GPU; see wgraph.shard.ShardComm) ------------------
     def shard_build(self, commits: abi.Commits, world: int, rank: int, row_begin: int, row_end: int, comm):
