@@ -342,8 +342,11 @@ def config_rates(eng, dev, torch, args):
         c.residency = abi.WG_DEVICE
 
         def step():
-            eng.build(commits=c)
-            eng.row_geometry(device_ptr=keep[5].data_ptr())
+            if args.no_build_frame:
+                eng.build(commits=c)
+                eng.row_geometry(device_ptr=keep[5].data_ptr())
+            else:
+                eng.build_frame(commits=c, device_ptr=keep[5].data_ptr())
             eng.emit_vertices(0, d.n, selected=7)
         for _ in range(2):
             step()
@@ -402,8 +405,11 @@ def build_lifecycle(dag, dev, torch, args, pal):
     def step(k, c, n):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        eng.build(commits=c)
-        eng.row_geometry(device_ptr=k[5].data_ptr())
+        if args.no_build_frame:
+            eng.build(commits=c)
+            eng.row_geometry(device_ptr=k[5].data_ptr())
+        else:
+            eng.build_frame(commits=c, device_ptr=k[5].data_ptr())
         eng.emit_vertices(0, n, selected=7, palette=pal)
         torch.cuda.synchronize()
         return round((time.perf_counter() - t0) * 1e3, 4)

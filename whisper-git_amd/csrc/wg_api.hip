@@ -125,18 +125,16 @@ int wg_side_join(wg_ctx *c) {
     return WG_OK;
 }
 
-int wg_side_zero_rowtop(wg_ctx *c, uint64_t m, float *h, float *rt, uint64_t row_lo, const float *band, float *rt_band,
+int wg_side_zero_rowtop(wg_ctx *c, uint64_t m, float *h, float *rt, uint64_t row_lo, const float *band,
                         const float *band_host, float *band_dev) {
     int rc = wg_side_fork(c);
     if (rc != WG_OK) return rc;
-    rc = wg_heights_run(c, m, c->n_list, h);
-    if (rc == WG_OK) rc = wg_rowtop_run(c, m, h, nullptr, rt, row_lo);
-    // the frame's banded row_top right after it (same scan buffers, same stream)
-    if (rc == WG_OK && band_host && m) {
+    if (band_host && m) {   // (build_frame's host band, copied on this stream)
         const hipError_t e = hipMemcpyAsync(band_dev, band_host, m * 4, hipMemcpyHostToDevice, c->stream);
         if (e != hipSuccess) rc = wg_fail(c, WG_E_HIP, "band copy: %s", hipGetErrorString(e));
     }
-    if (rc == WG_OK && band && rt_band) rc = wg_rowtop_run(c, m, h, band, rt_band, row_lo);
+    if (rc == WG_OK) rc = wg_heights_run(c, m, c->n_list, h);
+    if (rc == WG_OK) rc = wg_rowtop_run(c, m, h, band, rt, row_lo);
     wg_side_done(c);
     return rc;
 }
@@ -262,14 +260,16 @@ static int build_check(wg_ctx *c, const uint64_t *v, int kl, int k, bool *redo) 
         c->spec_redo_geom++;
         c->lists_gen = ~0ull;
         c->spec = false;
-        // (the zero-band row_top again: a frame pass may have swapped in its own, build_frame)
-        if ((rc = wg_stage_rowtop(c, nullptr)) != WG_OK) return rc;
-        if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
+        // (the row_top again with the build's bands: a frame pass queued since
+        // may have rescanned it with its own)
+        const float *bb = c->build_banded ? c->band_prev.as<const float>() : nullptr;
+        if ((rc = wg_stage_rowtop(c, bb)) != WG_OK) return rc;
+        if ((rc = wg_stage_geometry(c, bb)) != WG_OK) return rc;
     }
     c->spec_ready = c->lists_gen == c->layout_gen;   // an exact or validated build: the buffers are sized
     c->have_geom = true;
-    c->geom_key_gen = c->layout_gen;   // the geometry of (this layout, no bands)
-    c->geom_key_band = false;
+    c->geom_key_gen = c->layout_gen;   // the geometry of (this layout, the build's bands)
+    c->geom_key_band = c->build_banded;
     return WG_OK;
 }
 
@@ -464,24 +464,17 @@ int wg_layout_build(wg_ctx *c, const wg_commits *in) {
 }
 
 // GraphLayout::build followed by row_geometry_with_bands(band) (history_view's
-// first frame after a refresh, commit_graph.rs:1419-1421): the frame's banded
-// row_top depends on the heights and bands only, so it runs on the side stream
-// beside the build's hash join and lanes instead of after the build.
+// first frame after a refresh, commit_graph.rs:1419-1421).  build's own
+// row_geometry (:322-346) is replaced by the frame's before anyone can read
+// it, so the build's geometry pass takes the bands itself: the banded row_top
+// on the side stream beside the hash join and lanes, and no second pass.
 int wg_layout_build_frame(wg_ctx *c, const wg_commits *in, const float *band, int32_t residency) {
     if (c) WG_SETTLE(c);
     if (!c || !in || !band) return WG_E_INVALID;
     if (residency != WG_HOST && residency != WG_DEVICE) return wg_fail(c, WG_E_INVALID, "bad residency %d", residency);
-    int rc = layout_build_impl(c, in, band, residency);
-    if (rc != WG_OK) return rc;
-    if (c->pend.build) {   // a deferred build: this frame is redone with it if it does not hold
-        c->pend.frame = true;
-        c->pend.frame_band = true;
-        c->pend.emit = false;
-    }
-    // the band now lives on the device (c->band for a host band) unless the
-    // list was empty
-    if (!c->rt_band_ready) return row_geometry_impl(c, band, residency);
-    return row_geometry_impl(c, c->rt_band_ptr, WG_DEVICE);
+    const int rc = layout_build_impl(c, in, band, residency);
+    if (rc != WG_OK || c->build_banded) return rc;
+    return row_geometry_impl(c, band, residency);   // (an empty list)
 }
 
 static int layout_build_impl(wg_ctx *c, const wg_commits *in, const float *fband, int32_t fres) {
@@ -550,23 +543,21 @@ static int layout_build_impl(wg_ctx *c, const wg_commits *in, const float *fband
     c->n_list = n;
     WG_ALLOC(c, c->heights, n * 4 + 4);
     WG_ALLOC(c, c->g_row_top, (n + 1) * 4);
-    c->rt_band_ready = false;
-    if (fband && n) {   // wg_layout_build_frame: the frame's banded row_top on the side stream as well
-        WG_ALLOC(c, c->g_row_top_b, (n + 1) * 4);
-        const float *db = fband;
+    // wg_layout_build_frame: the frame's bands instead (a host band is
+    // copied on the side stream first)
+    c->build_banded = fband && n;
+    const float *db = nullptr;
+    if (c->build_banded) {
+        db = fband;
         if (fres == WG_HOST) {
             WG_ALLOC(c, c->band, n * 4 + 4);
             db = c->band.as<const float>();
         }
-        if ((rc = wg_side_zero_rowtop(c, n, c->heights.as<float>(), c->g_row_top.as<float>(), 0, db,
-                                      c->g_row_top_b.as<float>(), fres == WG_HOST ? fband : nullptr,
-                                      c->band.as<float>())) != WG_OK)
-            return rc;
-        c->rt_band_ready = true;
-        c->rt_band_ptr = db;
-    } else if ((rc = wg_side_zero_rowtop(c, n, c->heights.as<float>(), c->g_row_top.as<float>(), 0)) != WG_OK) {
-        return rc;
+        WG_ALLOC(c, c->band_prev, n * 4 + 4);   // the bands kept for the next frame's compare
     }
+    if ((rc = wg_side_zero_rowtop(c, n, c->heights.as<float>(), c->g_row_top.as<float>(), 0, db,
+                                  db && fres == WG_HOST ? fband : nullptr, c->band.as<float>())) != WG_OK)
+        return rc;
     // Speculative build (once an exact build has sized this context's
     // buffers): no host read until the end — event records and edges sized by
     // upper bounds, the replay run for the last build's iteration count, the
@@ -582,10 +573,14 @@ static int layout_build_impl(wg_ctx *c, const wg_commits *in, const float *fband
     if ((rc = wg_stage_edges(c, spec)) != WG_OK) return rc;
     c->have_layout = true;
     c->layout_gen++;
-    c->rt_band_gen = c->layout_gen;
-    // self.row_geometry with the default node_y / zero bands (:322-346)
+    // self.row_geometry with the default node_y / zero bands (:322-346), or
+    // the frame's (build_frame; its bands copied to band_prev as they are read)
     if ((rc = wg_side_join(c)) != WG_OK) return rc;
-    if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
+    {
+        struct KeepOff { wg_ctx *c; ~KeepOff() { c->band_keep = nullptr; } } keep_off{c};
+        c->band_keep = db ? c->band_prev.as<float>() : nullptr;
+        if ((rc = wg_stage_geometry(c, db)) != WG_OK) return rc;
+    }
     if (spec) {
         constexpr int K = WG_PENDING_ITEMS;
         static_assert(K + 1 <= FETCH_MAX, "validation words exceed one fetch");
@@ -613,7 +608,7 @@ static int layout_build_impl(wg_ctx *c, const wg_commits *in, const float *fband
             c->geom_sum_stale = false;
             c->have_geom = true;
             c->geom_key_gen = c->layout_gen;
-            c->geom_key_band = false;
+            c->geom_key_band = c->build_banded;
             return WG_OK;
         }
         uint64_t v[K] = {0};
@@ -623,8 +618,8 @@ static int layout_build_impl(wg_ctx *c, const wg_commits *in, const float *fband
     }
     c->spec_ready = c->lists_gen == c->layout_gen;   // an exact or validated build: the buffers are sized
     c->have_geom = true;
-    c->geom_key_gen = c->layout_gen;   // the geometry of (this layout, no bands)
-    c->geom_key_band = false;
+    c->geom_key_gen = c->layout_gen;   // the geometry of (this layout, the build's bands)
+    c->geom_key_band = c->build_banded;
     return WG_OK;
 }
 
@@ -783,16 +778,8 @@ static int row_geometry_impl(wg_ctx *c, const float *band, int32_t residency) {
         c->band_keep = c->band_prev.as<float>();
     }
     struct KeepOff { wg_ctx *c; ~KeepOff() { c->band_keep = nullptr; } } keep_off{c};
-    // bands equal below geom_r0: row_top is rescanned from there.  After
-    // wg_layout_build_frame the frame's row_top was computed beside the build.
-    if (c->rt_band_ready && d_band && d_band == c->rt_band_ptr && c->rt_band_gen == c->layout_gen && c->geom_r0 == 0) {
-        c->rt_band_ready = false;
-        if ((rc = wg_side_join(c)) != WG_OK) return rc;
-        std::swap(c->g_row_top, c->g_row_top_b);
-    } else if ((rc = wg_stage_rowtop(c, d_band, c->geom_r0)) != WG_OK) {
-        return rc;
-    }
-    c->rt_band_ready = false;
+    // bands equal below geom_r0: row_top is rescanned from there
+    if ((rc = wg_stage_rowtop(c, d_band, c->geom_r0)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, d_band)) != WG_OK) return rc;
     c->have_geom = true;
     c->geom_key_gen = c->layout_gen;

@@ -307,13 +307,9 @@ struct wg_ctx {
     float    total_height = 0.0f;
     DevBuf band;            // float [N] device copy of caller bands
     DevBuf g_height, g_node_y, g_row_top;   // float [N], [N], [N+1]
-    // wg_layout_build_frame: the frame's banded row_top, computed on the side
-    // stream beside the build (heights and bands only), swapped into
-    // g_row_top by the frame pass
-    DevBuf g_row_top_b;
-    bool rt_band_ready = false;
-    uint64_t rt_band_gen = 0;
-    const float *rt_band_ptr = nullptr;
+    // wg_layout_build_frame: the build's own geometry pass took the frame's
+    // bands (the band copy in band_prev); a redone build redoes it with them
+    bool build_banded = false;
     DevBuf rt_chunk;        // per-chunk scan state
     DevBuf rt_tables;       // per-chunk transducer tables
     DevBuf rt_sup;          // super-chunk tables, binade bases and walk states
@@ -594,7 +590,7 @@ void wg_side_done(wg_ctx *c);
 int wg_side_join(wg_ctx *c);
 // heights of rows [0, m) of the list + zero-band row_top into (h, rt), on the side stream
 int wg_side_zero_rowtop(wg_ctx *c, uint64_t m, float *h, float *rt, uint64_t row_lo,
-                        const float *band = nullptr, float *rt_band = nullptr,   // + the banded row_top (build_frame)
+                        const float *band = nullptr,   // banded row_top (build_frame)
                         const float *band_host = nullptr, float *band_dev = nullptr);   // (a host band copied there first)
 int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, float *row_top,
                   uint64_t row_lo,    // rows below row_lo: walked, not written

@@ -768,6 +768,7 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     if (!c || !in || !out) return WG_E_INVALID;
     WG_SETTLE(c);
     c->lf_refs_done = false;   // (only a single-GPU hash join does the lane references)
+    c->build_banded = false;
     if (world < 1 || world > 16 || rank < 0 || rank >= world) return wg_fail(c, WG_E_INVALID, "bad world/rank %d/%d", world, rank);
     if (in->residency != WG_DEVICE) return wg_fail(c, WG_E_INVALID, "sharded builds take device-resident commits");
     const uint64_t N = in->n_commits;
