@@ -1,19 +1,22 @@
 """Benchmark: commit-rows/s to vertex buffers (BASELINE.json metric).
 
 One step = the whole hot path over one batch of device-resident commits:
-GraphLayout::build (hash join, lane assignment, edges, heights, default
-row geometry) -> row_geometry_with_bands (pills bands) -> graph_cell vertex
-emission for every row of this rank's shard (WG-TESS-1 SplineVertex buffers
-written to HBM).  Workload: the WIDE16 synthetic DAG (C5 shape, <= 16
-lanes), 1M commit-rows per GPU (weak scaling: N GPUs = an N-million-row
-DAG, each rank emits its contiguous 1M-row shard).
+GraphLayout::build (hash join, lane assignment, edges, heights) and the
+frame's row_geometry_with_bands (pills bands) in one call
+(wg_layout_build_frame: the build's geometry pass takes the bands, which is
+what history_view's first frame after a refresh computes) -> graph_cell
+vertex emission for every row of this rank's shard (WG-TESS-1 SplineVertex
+buffers written to HBM).  Workload: the WIDE16 synthetic DAG (C5 shape,
+<= 16 lanes), 1M commit-rows per GPU (weak scaling: N GPUs = an
+N-million-row DAG, each rank emits its contiguous 1M-row shard);
+--total-rows T gives strong scaling instead (one T-row DAG over N GPUs).
 
-Multi-GPU: every rank holds the whole N-million-row DAG in
-HBM and builds only its contiguous 1M-row shard (wg_shard_* C ABI): parent
-ids, crossing references, chain tokens and the lane-event stream are
-all-gathered over RCCL (torch.distributed "nccl" group) at the exchange
-points of DESIGN.md §6 (five per step), then each rank emits its own rows'
-vertex buffers.
+Multi-GPU: every rank holds the whole DAG in HBM and builds
+only its contiguous shard (wg_shard_* C ABI): parent ids, crossing
+references, chain tokens and the lane-event stream are all-gathered over
+RCCL (torch.distributed "nccl" group) at the exchange points of DESIGN.md
+§6 (four per step with wg_shard_build_frame_begin), then each rank emits
+its own rows' vertex buffers.
 Launched per the driver contract:
   python bench.py --gpus 1 --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -40,7 +43,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--rows-per-gpu", type=int, default=1_000_000,
+                    help="weak scaling (the default): each GPU builds and emits this many rows of an N x that DAG")
+    ap.add_argument("--total-rows", type=int, default=0,
+                    help="strong scaling: one DAG of this many rows split over the N GPUs (e.g. 1000000 at "
+                         "--gpus 8 = 125000 rows per GPU); overrides --rows-per-gpu")
     ap.add_argument("--kind", default="wide16")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000, help="rows of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -463,9 +470,16 @@ def main():
     import wgraph
     from wgraph import abi, synth
 
-    rows_total = args.rows_per_gpu * world
-    workload = (f"{args.kind} synthetic DAG (C5 shape), {args.rows_per_gpu} commit-rows per GPU, "
-                f"full path: layout build + banded geometry + SplineVertex emission")
+    strong = args.total_rows > 0
+    if strong:   # a fixed DAG over the N GPUs (the last shard may be shorter)
+        args.rows_per_gpu = (args.total_rows + world - 1) // world
+        rows_total = args.total_rows
+    else:
+        rows_total = args.rows_per_gpu * world
+    workload = (f"{args.kind} synthetic DAG (C5 shape), "
+                + (f"{rows_total} commit-rows over {world} GPU(s) (strong scaling)" if strong
+                   else f"{args.rows_per_gpu} commit-rows per GPU")
+                + ", full path: layout build + banded geometry + SplineVertex emission")
     t0 = time.perf_counter()
     dag = synth.generate(args.kind, rows_total)
     log(f"generated {args.kind} DAG: {dag.n} rows, {dag.e} parent refs in {time.perf_counter() - t0:.1f}s")
@@ -509,8 +523,10 @@ def main():
         if comm is None and args.no_build_frame:
             eng.build(commits=commits)
             eng.row_geometry(device_ptr=t_band.data_ptr())
-        elif comm is None:   # the same two calls, the frame's row_top beside the build
+        elif comm is None:   # the same two calls, the build's geometry pass taking the bands
             eng.build_frame(commits=commits, device_ptr=t_band.data_ptr())
+        elif not args.no_build_frame:   # sharded: 4 exchanges instead of 5
+            eng.shard_build_frame(commits, world, rank, shard0, shard1, comm, device_ptr=t_band.data_ptr())
         else:
             eng.shard_build(commits, world, rank, shard0, shard1, comm)
             eng.shard_geometry(comm, device_ptr=t_band.data_ptr())
@@ -642,7 +658,7 @@ def main():
         out = {"metric": "commit-rows/sec to vertex buffers, 1M-commit synthetic DAG per GPU",
                "value": round(value, 1), "unit": "commit-rows/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+               "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
                "config": {"workload": workload,
                           "rows_total": rows_total, "rows_per_gpu": args.rows_per_gpu,
                           "vertices_per_gpu": int(vs.n_vertices), "parallelism": f"row-shard x{world}"},

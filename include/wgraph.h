@@ -296,6 +296,14 @@ typedef struct wg_shard_msg {
 /* GraphLayout::build (:265-355) of a row shard (+ zero-band geometry). */
 int wg_shard_build_begin(wg_ctx *ctx, const wg_commits *commits, int world, int rank,
                          uint64_t row_begin, uint64_t row_end, wg_shard_msg *out);
+/* wg_shard_build_begin then wg_shard_geometry_begin(band) in one sharded
+ * call (history_view's first frame after a refresh, commit_graph.rs:1419-
+ * 1421): the build's own geometry pass takes the bands — one exchange and one
+ * geometry pass fewer per step; the banded row_top runs on the side stream
+ * beside the build.  band = the whole [N] array; a device band must stay
+ * valid until the call is done (done = 1).  Results identical to the two calls. */
+int wg_shard_build_frame_begin(wg_ctx *ctx, const wg_commits *commits, int world, int rank, uint64_t row_begin,
+                               uint64_t row_end, const float *band, int32_t band_residency, wg_shard_msg *out);
 /* row_geometry_with_bands (:367-399) of the shard; band = the whole [N] array. */
 int wg_shard_geometry_begin(wg_ctx *ctx, const float *band, int32_t band_residency, wg_shard_msg *out);
 #define WG_SHARD_BYTES_ON_DEVICE UINT64_MAX

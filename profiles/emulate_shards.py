@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--stage-events", action="store_true", help="record every stage's HIP events (stages_ms)")
+    ap.add_argument("--two-calls", action="store_true",
+                    help="shard_build + shard_geometry (5 exchanges) instead of shard_build_frame (4)")
     args = ap.parse_args()
 
     import torch
@@ -172,10 +174,13 @@ def main():
                     wgraph.lib().wg_set_option(eng._ctx, 4, 0 if args.stage_events else 1)
                     eng.enable_timing(True, reserve=64 * (args.steps + 1))
                 comm.start("build")
-                eng.shard_build(commits, W, r, s0, s1, comm)
-                comm.stop()
-                comm.start("geometry")
-                eng.shard_geometry(comm, device_ptr=band_ptr)
+                if args.two_calls:
+                    eng.shard_build(commits, W, r, s0, s1, comm)
+                    comm.stop()
+                    comm.start("geometry")
+                    eng.shard_geometry(comm, device_ptr=band_ptr)
+                else:
+                    eng.shard_build_frame(commits, W, r, s0, s1, comm, device_ptr=band_ptr)
                 comm.stop()
                 comm.start("emit")
                 eng.emit_vertices(s0, s1, selected=s0 + 7, palette=pal)
@@ -224,6 +229,7 @@ def main():
 
     # the single-GPU step on an R-row list of the same kind, for comparison
     single = wgraph.Engine(0)
+    single.set_defer_validation(True)   # as bench.py
     dag1 = synth.generate(args.kind, R)
     k1 = [torch.from_numpy(a).to(dev) for a in (dag1.oid.reshape(-1), dag1.time, dag1.parent_off.view(np.int32),
                                                  dag1.parent_oid.reshape(-1), dag1.flags, dag1.band)]
@@ -234,8 +240,11 @@ def main():
 
     def one(eng=None):
         eng = eng or single
-        eng.build(commits=c1)
-        eng.row_geometry(device_ptr=k1[5].data_ptr())
+        if args.two_calls:
+            eng.build(commits=c1)
+            eng.row_geometry(device_ptr=k1[5].data_ptr())
+        else:
+            eng.build_frame(commits=c1, device_ptr=k1[5].data_ptr())
         eng.emit_vertices(0, R, selected=7, palette=pal)
         eng.synchronize()
     one()

@@ -101,6 +101,22 @@ def run_case(eng, comm, torch, kind, n, seed, world, rank, errors):
         errors.append(f"{kind}/{n}/w{world} rank {rank}: vertex checksum; {len(bad)} vertices differ, first {i} "
                       f"(row {row}, sel {sel}): got {gw[i].view(np.float32) if i >= 0 else None} "
                       f"want {ow[i].view(np.float32) if i >= 0 else None}")
+    # build + banded frame in one sharded call (wg_shard_build_frame_begin): one exchange fewer
+    x0 = comm.exchanges
+    eng.shard_build_frame(c, world, rank, s, e, comm, band=d.band)
+    frame_x = comm.exchanges - x0
+    if world > 1 and want_mode == 1 and frame_x != 4:
+        errors.append(f"{kind}/{n}/w{world} rank {rank}: build_frame took {frame_x} exchanges, expected 4")
+    lane, color = eng.lanes()
+    same("frame lane", lane, o.lane[s:e])
+    same("frame color", color, o.color[s:e])
+    same("frame edges", u32rows(eng.edges()), oe[(oe[:, 0] >= s) & (oe[:, 0] < e)])
+    got = eng.geometry()
+    for k, v in geometry_slice(og, s, e).items():
+        same("frame_" + k, got[k], v)
+    eng.emit_vertices(s, e, selected=sel)
+    if eng.vertex_summary().checksum != oracle_c.vertex_checksum(ov):
+        errors.append(f"{kind}/{n}/w{world} rank {rank}: build_frame vertex checksum")
     o.close()
     del keep
 

@@ -146,10 +146,14 @@ def _lockstep(engines, begin):
     return rounds
 
 
-@pytest.mark.parametrize("world,kind,n", [(2, "wide16", 40000), (3, "random13", 20000), (4, "linux", 30000)])
-def test_packed_slots_in_one_process(world, kind, n):
+@pytest.mark.parametrize("world,kind,n,frame", [(2, "wide16", 40000, False), (3, "random13", 20000, False),
+                                                (4, "linux", 30000, False), (2, "wide16", 40000, True),
+                                                (4, "random13", 30000, True)])
+def test_packed_slots_in_one_process(world, kind, n, frame):
     """wg_shard_pack_slot: every rank's slot packed on the shared stream, no
-    host synchronisation before the gather; shards equal the oracle."""
+    host synchronisation before the gather; shards equal the oracle.  frame:
+    wg_shard_build_frame_begin with the device bands (4 exchanges instead of
+    the two calls' 5)."""
     import ctypes
     import sys as _sys
 
@@ -183,9 +187,14 @@ def test_packed_slots_in_one_process(world, kind, n):
         for e in engines:
             e.set_stream(ts.cuda_stream)
         rng = [shard_rows(d.n, world, r) for r in range(world)]
-        _lockstep(engines, lambda e, r, m: lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), world, r,
-                                                                       rng[r][0], rng[r][1], m))
-        _lockstep(engines, lambda e, r, m: lib().wg_shard_geometry_begin(e._ctx, keep[5].data_ptr(), abi.WG_DEVICE, m))
+        if frame:
+            rounds = _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
+                e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
+            assert rounds == 4
+        else:
+            _lockstep(engines, lambda e, r, m: lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), world, r,
+                                                                           rng[r][0], rng[r][1], m))
+            _lockstep(engines, lambda e, r, m: lib().wg_shard_geometry_begin(e._ctx, keep[5].data_ptr(), abi.WG_DEVICE, m))
         og = o.row_geometry(d.band)
         for r, e in enumerate(engines):
             s, t = rng[r]

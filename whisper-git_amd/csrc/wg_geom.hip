@@ -839,23 +839,32 @@ __device__ __forceinline__ bool curve_kept(uint32_t r, const wg_edge &e, uint32_
 
 // cond (the frame pass): only when *cond (the row flags changed); otherwise
 // the current offsets' per-row counts, so the scan that follows reproduces them
-__global__ void k_curve_keep(uint64_t n, const uint32_t *__restrict__ soff, const uint32_t *__restrict__ sref,
-                             const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
-                             uint32_t *__restrict__ cnt, const uint32_t *__restrict__ cond,
-                             const uint32_t *__restrict__ cur_off, Cap sc, uint32_t *ovf,
-                             uint8_t *__restrict__ flags_kept) {
+// (+ the block's sum of the counts for the offsets' scan, wg_scan_bs_u32)
+__global__ void __launch_bounds__(WG_BS_THREADS) k_curve_keep(uint64_t n, const uint32_t *__restrict__ soff,
+                                                             const uint32_t *__restrict__ sref,
+                                                             const wg_edge *__restrict__ edges,
+                                                             const uint8_t *__restrict__ rowflags, uint32_t *__restrict__ cnt,
+                                                             const uint32_t *__restrict__ cond,
+                                                             const uint32_t *__restrict__ cur_off, Cap sc, uint32_t *ovf,
+                                                             uint8_t *__restrict__ flags_kept, uint32_t *__restrict__ bsum) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (over(sc, ovf) || r >= n) return;
-    const uint32_t f = rowflags[r];
-    flags_kept[r] = (uint8_t)f;   // the flags the curve lists are filtered with (equal when cond is 0)
-    if (cond && !*cond) { cnt[r] = cur_off[r + 1] - cur_off[r]; return; }
-    const uint32_t a = soff[r], b = soff[r + 1];
-    uint32_t k = b - a;
-    if (f) {
-        k = 0;
-        for (uint32_t j = a; j < b; j++) k += curve_kept((uint32_t)r, edges[sref[j]], f) ? 1u : 0u;
+    uint32_t k = 0;
+    if (!over(sc, ovf) && r < n) {
+        const uint32_t f = rowflags[r];
+        flags_kept[r] = (uint8_t)f;   // the flags the curve lists are filtered with (equal when cond is 0)
+        if (cond && !*cond) {
+            k = cur_off[r + 1] - cur_off[r];
+        } else {
+            const uint32_t a = soff[r], b = soff[r + 1];
+            k = b - a;
+            if (f) {
+                k = 0;
+                for (uint32_t j = a; j < b; j++) k += curve_kept((uint32_t)r, edges[sref[j]], f) ? 1u : 0u;
+            }
+        }
+        cnt[r] = k;
     }
-    cnt[r] = k;
+    wg_bsum_store(k, bsum);
 }
 
 __global__ void k_curve_compact(uint64_t n, const uint32_t *__restrict__ soff, const uint32_t *__restrict__ sref,
@@ -887,10 +896,20 @@ static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *c
     WG_ALLOC(c, c->curve_cnt, (n + 2) * 4);
     WG_ALLOC(c, c->rowflags_lists, n + 4);
     uint32_t *cnt = c->curve_cnt.as<uint32_t>();
+    // (the geometry pass's other tile sums are consumed by now: the same words)
+    WG_ALLOC(c, c->bsum, (wg_bs_blocks(n) + 64) * 4);
+    static_assert(T == WG_BS_THREADS, "k_curve_keep is a wg_scan_bs_u32 producer");
     hipLaunchKernelGGL(k_curve_keep, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
                        c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
-                       cnt, cond, (const uint32_t *)coff, sc, ovf, c->rowflags_lists.as<uint8_t>());
-    WG_HIP(c, wg_exclusive_scan_u32(cnt, coff, n, c->scan_tmp.p, s));
+                       cnt, cond, (const uint32_t *)coff, sc, ovf, c->rowflags_lists.as<uint8_t>(), c->bsum.as<uint32_t>());
+    {
+        WgScanBs S;
+        S.na = 1;
+        S.in[0] = cnt;
+        S.out[0] = coff;
+        S.bsum[0] = c->bsum.as<const uint32_t>();
+        WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, s));
+    }
     hipLaunchKernelGGL(k_curve_compact, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
                        c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
                        (const uint32_t *)coff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), cond, sc, ovf);

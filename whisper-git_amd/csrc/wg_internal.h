@@ -148,7 +148,9 @@ struct ShardState {
     DevBuf xtok, xt;          // chain token per crossing entry: shard-local / global
     DevBuf dev_small;
     DevBuf h_g, rt_g;         // heights of rows [0, e) / row_top of rows [s, e] (below s: unspecified)
-    bool rt_zero = false;     // rt_g holds the zero-band row_top (computed at build begin, side stream)
+    bool rt_fresh = false;        // rt_g was computed at build begin (side stream) with the bands rt_band
+    const float *rt_band = nullptr;
+    const float *build_band = nullptr;   // wg_shard_build_frame_begin: the build's geometry takes these bands
     uint64_t local_gen = ~0ull;           // layout_gen of the local edges (c->edges / edge_cnt / in_scan)
     uint64_t local_ne = 0, local_nin = 0; // local edges, of which incoming
     DevBuf band_host;         // device copy of a host band array [N]
@@ -187,7 +189,17 @@ struct ReplayRun {
     uint32_t *stats = nullptr, *flags = nullptr, *scal = nullptr;
     const uint32_t *nev_dev = nullptr;   // speculative build: event count on the device (nev = upper bound)
     const uint32_t *gate = nullptr;      // speculative build: nonzero = not well formed, replay nothing
+    uint32_t switch_it = 0;              // exact replay at a short chunk: still moving at this iteration ->
+    bool switched = false;               // stop; the caller replays at WG_REPLAY_CHUNK_LONG (wg_replay_resume)
 };
+// The replay's chunk lengths (events).  Short chunks make iteration 1 short
+// (its chunks replay serially, one wave each) and suit lists whose greedy
+// state forgets a wrong entry within a chunk; on others (long-lived lanes
+// carrying a wrong guess across many chunks: the Linux shape) the fixed point
+// turns linear in the chunk count, and the list is replayed at the long chunk.
+constexpr uint32_t WG_REPLAY_CHUNK_SHORT = 128, WG_REPLAY_CHUNK_LONG = 512;
+constexpr uint32_t WG_REPLAY_SHORT_MAX_FP = 6;   // a short-chunk replay needing more iterations: long chunks next
+constexpr uint32_t WG_REPLAY_SWITCH_IT = 12;     // exact replay: iterations at the short chunk before the switch
 
 // small device -> host reads (wg_api.hip): one tiny kernel writes the values
 // into mapped pinned host memory, then the stream is synchronised — instead of
@@ -257,12 +269,20 @@ struct wg_ctx {
     uint32_t replay_chunk = 512;   // events per replay chunk (WG_OPT_REPLAY_CHUNK)
     uint32_t replay_warm = 0;      // iteration 1's warm-up events before each chunk (WG_OPT_REPLAY_WARMUP)
     bool replay_auto = true;       // neither option set: chunk / warm-up follow the last build's event count
-    // (profiles/r03i tune: 512 / 0 is best from ~40k events up; below ~25k
-    // events — random13 100k, 13.9k events: 0.163 -> 0.117 ms — 256 / 256)
+    // Auto: the short chunk with a warm-up first, the long chunk once a list
+    // needed more than WG_REPLAY_SHORT_MAX_FP iterations at the short one
+    // (replay_long; an exact replay still moving at WG_REPLAY_SWITCH_IT starts
+    // over at the long chunk).  profiles/r03l_replay_tune.jsonl: wide16 1M
+    // (46k events) 128 + 512 warm-up 0.160 ms (5 iterations) against 512 / 0
+    // 0.203 (4); random13 100k (13.9k events) 128 + 256 0.092 against 0.117;
+    // the Linux shape (93k events) needs 21+ iterations below 512: long.
+    bool replay_long = false;
     void replay_geometry(uint32_t *chunk, uint32_t *warm) const {
         *chunk = replay_chunk;
         *warm = replay_warm;
-        if (replay_auto && n_events > 0 && n_events < 24576) { *chunk = 256; *warm = 256; }
+        if (!replay_auto) return;
+        if (!replay_long) { *chunk = WG_REPLAY_CHUNK_SHORT; *warm = n_events >= 24576 ? 512u : 256u; }
+        else { *chunk = WG_REPLAY_CHUNK_LONG; *warm = 0; }
     }
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
@@ -273,8 +293,13 @@ struct wg_ctx {
     // changed nothing), the next build's blind count: up at once, down by half
     // the excess per build (it used to fall by one per build: after a list that
     // needed hundreds of iterations, later builds launched hundreds of empty ones).
-    void replay_adapt(uint32_t fp) {
+    void replay_adapt(uint32_t fp, uint32_t chunk = 0) {
         if (fp == 0) return;
+        if (replay_auto && chunk == WG_REPLAY_CHUNK_SHORT && fp > WG_REPLAY_SHORT_MAX_FP) {
+            replay_long = true;   // this list shape wants the long chunk (its own blind count from the next build on)
+            replay_blind = 4;
+            return;
+        }
         replay_blind = fp >= replay_blind ? fp : (fp > (replay_blind + fp) / 2 ? fp : (replay_blind + fp) / 2);
         if (replay_blind < 2) replay_blind = 2;
     }

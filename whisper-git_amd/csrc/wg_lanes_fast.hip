@@ -594,6 +594,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
     c->replay_geometry(&run.chunk, &run.warm);
     const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
+    if (run.chunk < WG_REPLAY_CHUNK_LONG && c->replay_auto) run.switch_it = WG_REPLAY_SWITCH_IT;
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
     DevBuf &rflags = c->lf[LF_RFLAGS];
     WG_ALLOC(c, slot_a, (nev + 64) * sizeof(uint16_t));
@@ -632,11 +633,16 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
         if (!conv) break;
     }
     wg_stage_end(c);
+    if (run.switched) {   // still moving at the short chunk: this list shape replays at the long one
+        c->replay_long = true;
+        c->replay_blind = 4;
+        return replay_lanes_at(c, R, nev, ev, aux, lane, nw, ok, overflow);
+    }
     c->replay_iters = run.it;
     // next build: the iterations this one needed — up to the first iteration
     // that changed nothing (k_lf_replay_finish) — at once if more, halving the
     // excess if fewer (a list that needed many must not hold later ones for long)
-    if (sc[5] >= 1) c->replay_adapt((uint32_t)sc[5]);
+    if (sc[5] >= 1) c->replay_adapt((uint32_t)sc[5], run.chunk);
     else if (run.it > blind) c->replay_blind = run.it;
     if (conv && sc[2]) *overflow = true;            // more than 64 nw - 1 slots: the caller widens
     if (!conv || sc[2]) return WG_OK;               // no fixed point / overflow
@@ -743,7 +749,7 @@ bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v) {
     c->n_slots = (uint32_t)v[4];
     c->replay_nw = wg_ctx::nw_for_slots(c->n_slots);
     c->replay_iters = c->spec_run.it;
-    c->replay_adapt((uint32_t)v[8]);   // blind count and chunk size from the iterations it took
+    c->replay_adapt((uint32_t)v[8], c->spec_run.chunk);   // blind count and chunk length from the iterations it took
     c->lane_path = 0;
     return true;
 }

@@ -624,11 +624,15 @@ hipError_t wg_replay_finish_lanes(hipStream_t s, const ReplayRun &R, uint64_t nl
     return hipGetLastError();
 }
 
-// Continue with polls (every 3rd iteration, then doubling) until a fixed
-// point or max_iters; *converged tells which.
+// Continue with polls (every 3rd iteration, then every 6th) until a fixed
+// point or max_iters; *converged tells which.  A replay at a short chunk that
+// is still moving at R.switch_it stops there (R.switched: the caller replays
+// at WG_REPLAY_CHUNK_LONG from the start, so its iteration count is the long
+// chunk's own and the next builds' blind count follows it).
 hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged) {
     *converged = R.nev == 0;
     uint32_t next_poll = R.it + 3;
+    if (R.switch_it && R.chunk < WG_REPLAY_CHUNK_LONG && next_poll > R.switch_it) next_poll = R.switch_it > R.it ? R.switch_it : R.it + 1;
     while (!*converged && R.it < R.max_iters) {
         R.it++;
         ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr,
@@ -637,10 +641,14 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
         std::swap(R.sp_prev, R.sp_next);
         std::swap(R.op, R.on);
         if (R.it == next_poll || R.it == R.max_iters) {
-            next_poll = R.it + (next_poll - R.it + 3) * 2;
+            next_poll = R.it + 6;
             uint64_t fl[2] = {1, 1};
             if (wg_fetch(c, {{R.flags + R.it - 1, false}, {R.flags + R.it, false}}, fl) != WG_OK) return hipErrorUnknown;
             *converged = fl[0] == 0 || fl[1] == 0;
+            if (!*converged && R.switch_it && R.it >= R.switch_it && R.chunk < WG_REPLAY_CHUNK_LONG) {
+                R.switched = true;
+                return hipSuccess;
+            }
         }
     }
     if (R.nev)

@@ -526,6 +526,7 @@ static int sh_send_dev(wg_ctx *c, uint64_t cap_bytes, wg_shard_msg *out) {
 }
 static void sh_done(wg_ctx *c, wg_shard_msg *out) {
     c->sh.step = SH_IDLE;
+    c->sh.build_band = nullptr;   // (build_frame's bands are the caller's: not kept past the call)
     out->send = nullptr;
     out->bytes = 0;
     out->done = 1;
@@ -606,6 +607,7 @@ static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
     c->have_geom = true;
     S.row_base = S.s;
+    if (S.build_band && (rc = wg_row_geometry(c, S.build_band, WG_DEVICE)) != WG_OK) return rc;   // (build_frame)
     sh_done(c, out);
     return WG_OK;
 }
@@ -616,11 +618,13 @@ static int sh_geometry_begin(wg_ctx *c, const float *band_g, wg_shard_msg *out) 
     const uint64_t e = S.e;
     int rc = wg_side_join(c);
     if (rc != WG_OK) return rc;
-    if (band_g || !S.rt_zero) {   // the zero-band row_top may be left from the build's side stream
+    // the build's first pass takes the row_top the build began on the side
+    // stream (its bands: none, or build_frame's); any later pass rescans
+    if (!(S.rt_fresh && band_g == S.rt_band)) {
         WG_ALLOC(c, S.rt_g, (e + 1) * 4);
         if ((rc = wg_rowtop_run(c, e, S.h_g.as<const float>(), band_g, S.rt_g.as<float>(), S.s)) != WG_OK) return rc;
-        S.rt_zero = band_g == nullptr;
     }
+    S.rt_fresh = false;
     S.band_g = band_g;
     const uint64_t nown = S.xoff[S.rank + 1] - S.xoff[S.rank], xin = S.xoff[S.rank];
     S.step = SH_X6;
@@ -763,10 +767,26 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
 
 extern "C" {
 
+static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank, uint64_t row_begin, uint64_t row_end,
+                            const float *band, int32_t band_res, wg_shard_msg *out);
+
 int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, uint64_t row_begin, uint64_t row_end,
                          wg_shard_msg *out) {
     if (!c || !in || !out) return WG_E_INVALID;
     WG_SETTLE(c);
+    return shard_build_impl(c, in, world, rank, row_begin, row_end, nullptr, WG_DEVICE, out);
+}
+
+int wg_shard_build_frame_begin(wg_ctx *c, const wg_commits *in, int world, int rank, uint64_t row_begin, uint64_t row_end,
+                               const float *band, int32_t band_res, wg_shard_msg *out) {
+    if (!c || !in || !out || !band) return WG_E_INVALID;
+    WG_SETTLE(c);
+    if (band_res != WG_HOST && band_res != WG_DEVICE) return wg_fail(c, WG_E_INVALID, "bad residency %d", band_res);
+    return shard_build_impl(c, in, world, rank, row_begin, row_end, band, band_res, out);
+}
+
+static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank, uint64_t row_begin, uint64_t row_end,
+                            const float *band, int32_t band_res, wg_shard_msg *out) {
     c->lf_refs_done = false;   // (only a single-GPU hash join does the lane references)
     c->build_banded = false;
     if (world < 1 || world > 16 || rank < 0 || rank >= world) return wg_fail(c, WG_E_INVALID, "bad world/rank %d/%d", world, rank);
@@ -801,7 +821,17 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     c->n = N;
     c->e_refs = S.Etot;
     hipStream_t st = c->stream;
-    S.rt_zero = false;
+    S.rt_fresh = false;
+    S.build_band = nullptr;
+    if (band && N) {   // build_frame: the bands, on the device (a host band copied before the side fork)
+        if (band_res == WG_HOST) {
+            WG_ALLOC(c, S.band_host, N * 4 + 4);
+            WG_HIP(c, hipMemcpyAsync(S.band_host.p, band, N * 4, hipMemcpyHostToDevice, st));
+            S.build_band = S.band_host.as<const float>();
+        } else {
+            S.build_band = band;
+        }
+    }
     if (world == 1) {
         uint64_t eo[2] = {0, 0};
         if (N) {
@@ -821,13 +851,15 @@ int wg_shard_build_begin(wg_ctx *c, const wg_commits *in, int world, int rank, u
     // the device.
     const uint64_t nl = row_end - row_begin, El = S.Etot;
     // heights of rows [0, e) (the last row of the LIST is ROW_HEIGHT) and the
-    // zero-band row_top of the own rows: side stream, overlapping the exchanges
+    // row_top of the own rows (zero bands, or build_frame's): side stream,
+    // overlapping the exchanges
     c->n_list = N;
     WG_ALLOC(c, S.h_g, row_end * 4 + 4);
     WG_ALLOC(c, S.rt_g, (row_end + 1) * 4);
-    int rc = wg_side_zero_rowtop(c, row_end, S.h_g.as<float>(), S.rt_g.as<float>(), row_begin);
+    int rc = wg_side_zero_rowtop(c, row_end, S.h_g.as<float>(), S.rt_g.as<float>(), row_begin, S.build_band);
     if (rc != WG_OK) return rc;
-    S.rt_zero = true;
+    S.rt_fresh = true;
+    S.rt_band = S.build_band;
     // ---- local table, probes, global duplicate scan -------------------------------------
     uint64_t cap = 1024;
     while (cap < 2 * nl) cap <<= 1;
@@ -1132,7 +1164,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
                            c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>());
         c->have_layout = true;
         c->layout_gen++;
-        return sh_geometry_begin(c, nullptr, out);
+        return sh_geometry_begin(c, S.build_band, out);   // the default geometry, or build_frame's
     }
     case SH_X6:
         return sh_geometry_finish(c, gathered, stride, out);

@@ -87,6 +87,8 @@ def lib():
             "wg_shard_build_begin": ([vp, ctypes.POINTER(abi.Commits), ctypes.c_int, ctypes.c_int, u64, u64,
                                       ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_geometry_begin": ([vp, vp, i32, ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
+            "wg_shard_build_frame_begin": ([vp, ctypes.POINTER(abi.Commits), ctypes.c_int, ctypes.c_int, u64, u64, vp, i32,
+                                            ctypes.POINTER(abi.ShardMsg)], ctypes.c_int),
             "wg_shard_copy_msg": ([vp, vp], ctypes.c_int),
             "wg_shard_pack_slot": ([vp, vp, u64], ctypes.c_int),
             "wg_shard_slot_heads": ([vp, vp, u64, ctypes.c_int, vp], ctypes.c_int),
@@ -114,7 +116,7 @@ EXPORTED_SYMBOLS = (
     "wg_layout_build", "wg_layout_summary_get", "wg_copy_lanes", "wg_copy_edges", "wg_copy_row_heights",
     "wg_compute_row_heights", "wg_row_geometry", "wg_layout_build_frame", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
-    "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_geometry_begin",
+    "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_build_frame_begin", "wg_shard_geometry_begin",
     "wg_shard_copy_msg", "wg_shard_msg_bytes", "wg_shard_pack_slot", "wg_shard_slot_heads", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
     "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets",
     "wg_match_rows", "wg_copy_match_flags", "wg_lower_utf8", "wg_order_rows", "wg_render", "wg_write_png")
@@ -220,6 +222,22 @@ class Engine:
         msg = abi.ShardMsg()
         self._check(lib().wg_shard_build_begin(self._ctx, ctypes.byref(commits), world, rank, row_begin, row_end,
                                                ctypes.byref(msg)))
+        self._shard_loop(msg, comm)
+
+    def shard_build_frame(self, commits: abi.Commits, world: int, rank: int, row_begin: int, row_end: int, comm,
+                          band=None, device_ptr: int | None = None):
+        """shard_build then shard_geometry(band) in one sharded call
+        (wg_shard_build_frame_begin): one exchange and one geometry pass fewer."""
+        self._commits = commits
+        msg = abi.ShardMsg()
+        if device_ptr is not None:
+            ptr, res = device_ptr, abi.WG_DEVICE
+        else:
+            b = np.ascontiguousarray(band, np.float32)
+            self._band = b
+            ptr, res = b.ctypes.data, abi.WG_HOST
+        self._check(lib().wg_shard_build_frame_begin(self._ctx, ctypes.byref(commits), world, rank, row_begin, row_end,
+                                                     ptr, res, ctypes.byref(msg)))
         self._shard_loop(msg, comm)
 
     def shard_geometry(self, comm, band=None, device_ptr: int | None = None):
