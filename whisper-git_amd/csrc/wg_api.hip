@@ -24,6 +24,11 @@ int wg_fail(wg_ctx *c, int code, const char *fmt, ...) {
     return code;
 }
 
+// Stage timing events: a device-scope release (the default system-scope
+// fence writes back and invalidates the caches between the kernels they
+// bracket: ~10 us before and after the emission kernel in a timed step).
+static hipError_t wg_timing_event(hipEvent_t *e) { return hipEventCreateWithFlags(e, hipEventReleaseToDevice); }
+
 // Stages nest: begin takes the next slot and pushes it, end closes the top.
 void wg_stage_begin(wg_ctx *c, const char *name) {
     if (!c->timing) return;
@@ -33,7 +38,7 @@ void wg_stage_begin(wg_ctx *c, const char *name) {
         return;
     }
     StageTimer &t = c->stages[c->n_stages];
-    if (!t.a) { (void)hipEventCreate(&t.a); (void)hipEventCreate(&t.b); }
+    if (!t.a) { (void)wg_timing_event(&t.a); (void)wg_timing_event(&t.b); }
     t.name = name;
     (void)hipEventRecord(t.a, c->stream);
     c->stage_stack[c->stage_depth++] = c->n_stages++;
@@ -98,8 +103,9 @@ int wg_copy_batch(wg_ctx *c, const WgCopies &cp, hipStream_t s) {
 int wg_side_fork(wg_ctx *c) {
     if (!c->side) {
         WG_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-        WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-        WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+        // stream-to-stream order on one device: a device-scope release suffices
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventReleaseToDevice));
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventReleaseToDevice));
     }
     if (const int rc = wg_side_join(c)) return rc;
     WG_HIP(c, hipEventRecord(c->ev_fork, c->stream));
@@ -979,7 +985,7 @@ int wg_enable_timing(wg_ctx *c, int on) {
     if (!c) return WG_E_INVALID;
     c->timing = on != 0;
     for (int i = 0; i < on && i < WG_STAGE_MAX; i++)
-        if (!c->stages[i].a) { WG_HIP(c, hipEventCreate(&c->stages[i].a)); WG_HIP(c, hipEventCreate(&c->stages[i].b)); }
+        if (!c->stages[i].a) { WG_HIP(c, wg_timing_event(&c->stages[i].a)); WG_HIP(c, wg_timing_event(&c->stages[i].b)); }
     c->n_stages = 0;
     c->stage_depth = 0;
     return WG_OK;
