@@ -626,6 +626,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
             conv = sc[3] == 0 || sc[4] == 0;
         } else {
             int rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc);
+            if (rc == WG_OK && nev) rc = wg_fetch(c, {{ls + 3, false}}, sc + 5);   // (the resumed replay's first no-change iteration)
             if (rc != WG_OK) return rc;
         }
         if (conv) break;
