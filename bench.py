@@ -589,6 +589,17 @@ def main():
             stage_ms[name] = stage_ms.get(name, 0.0) + ms / nb
         eng.enable_timing(False)
 
+    # the emission alone, back to back with no timing events, by the host's
+    # clock (each call: the offsets kernel, the total's read, the launch):
+    # a check on the event-timed launch duration the roofline uses
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ne = min(args.steps, 10)
+    for _ in range(ne):
+        eng.emit_vertices(shard0, shard1, selected=selected, palette=pal)
+    torch.cuda.synchronize()
+    emit_only_ms = (time.perf_counter() - t1) * 1e3 / ne
+
     ms_per_step = elapsed * 1e3 / args.steps
     rows_done = rows_total  # all ranks together emit every row once per step
     value = rows_done * args.steps / elapsed
@@ -609,7 +620,9 @@ def main():
     roofline = {"kernel": "k_vtx_tile (vtx_emit)", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None, "algorithmic_bytes_per_launch": int(bytes_w + bytes_r),
-                "avg_launch_ms": round(vtx_ms, 4)}
+                "avg_launch_ms": round(vtx_ms, 4),
+                # the host clock over emission-only calls (no events): launch + offsets kernel + the total's read
+                "emit_only_wall_ms_per_call": round(emit_only_ms, 4)}
     pmc = pmc_traffic(args, workload)
     if pmc is not None:
         # HBM bytes per launch from the committed PMC passes of this same command

@@ -24,6 +24,8 @@ timeout -k 10 300 rocprofv3 --kernel-include-regex k_vtx_tile --pmc WRITE_SIZE -
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/side" -o run -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu > "$OUT/side.json" 2> "$OUT/side.err"
 if [ -x "$ROOT/profiles/microbench/store_ceiling" ]; then
     timeout -k 10 120 "$ROOT/profiles/microbench/store_ceiling" > "$OUT/store_ceiling.jsonl" 2> "$OUT/store_ceiling.err"
+    # the same timed with device-scope events, as bench.py times the emission
+    STORE_EVENTS=device timeout -k 10 120 "$ROOT/profiles/microbench/store_ceiling" > "$OUT/store_ceiling_devev.jsonl" 2>> "$OUT/store_ceiling.err"
 fi
 if [ -x "$ROOT/profiles/microbench/store_sweep" ]; then
     timeout -k 10 200 "$ROOT/profiles/microbench/store_sweep" > "$OUT/store_sweep.jsonl" 2> "$OUT/store_sweep.err"

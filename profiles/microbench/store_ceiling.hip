@@ -5,6 +5,7 @@
 // workgroup (k_vtx_tile's shape), 256 threads per workgroup.
 //   hipcc --offload-arch=gfx950 -O3 -o store_ceiling store_ceiling.hip && ./store_ceiling
 #include <hip/hip_runtime.h>
+#include <cstring>
 
 #include <cstdio>
 #include <cstdlib>
@@ -44,8 +45,12 @@ int main() {
     v4f *out;
     CHECK(hipMalloc(&out, bytes));
     hipEvent_t a, b;
-    CHECK(hipEventCreate(&a));
-    CHECK(hipEventCreate(&b));
+    // STORE_EVENTS=device: timing events with a device-scope release (as
+    // bench.py's since r03n); default: HIP's system-scope fence
+    const char *ev_env = getenv("STORE_EVENTS");
+    const unsigned ev_flags = (ev_env && !strcmp(ev_env, "device")) ? hipEventReleaseToDevice : hipEventDefault;
+    CHECK(hipEventCreateWithFlags(&a, ev_flags));
+    CHECK(hipEventCreateWithFlags(&b, ev_flags));
     struct V { const char *name; void (*launch)(v4f *, size_t); };
     auto run = [&](const char *name, auto launch) {
         for (int w = 0; w < 2; w++) launch();

@@ -11,6 +11,7 @@
 // with 256 / 512 threads and 12 / 24 / 48 KiB tiles, plain and non-temporal.
 //   hipcc --offload-arch=gfx950 -O3 -o store_sweep store_sweep.hip && ./store_sweep
 #include <hip/hip_runtime.h>
+#include <cstring>
 
 #include <cstdio>
 #include <cstdlib>
@@ -85,8 +86,12 @@ int main(int argc, char **argv) {
     unsigned *ctr;
     CHECK(hipMalloc(&ctr, 8 * 32 * 4));
     hipEvent_t a, b;
-    CHECK(hipEventCreate(&a));
-    CHECK(hipEventCreate(&b));
+    // STORE_EVENTS=device: timing events with a device-scope release (as
+    // bench.py's since r03n); default: HIP's system-scope fence
+    const char *ev_env = getenv("STORE_EVENTS");
+    const unsigned ev_flags = (ev_env && !strcmp(ev_env, "device")) ? hipEventReleaseToDevice : hipEventDefault;
+    CHECK(hipEventCreateWithFlags(&a, ev_flags));
+    CHECK(hipEventCreateWithFlags(&b, ev_flags));
     auto run = [&](const char *name, auto launch) {
         for (int w = 0; w < 2; w++) launch();
         CHECK(hipDeviceSynchronize());
