@@ -27,7 +27,15 @@ int wg_fail(wg_ctx *c, int code, const char *fmt, ...) {
 // Stage timing events: a device-scope release (the default system-scope
 // fence writes back and invalidates the caches between the kernels they
 // bracket: ~10 us before and after the emission kernel in a timed step).
-static hipError_t wg_timing_event(hipEvent_t *e) { return hipEventCreateWithFlags(e, hipEventReleaseToDevice); }
+// WG_EVENT_SCOPE=system (diagnostic): HIP's default fence for these events
+// and the side stream's, for same-box comparisons.
+static bool wg_system_events() {
+    static const bool sys = [] { const char *v = std::getenv("WG_EVENT_SCOPE"); return v && !std::strcmp(v, "system"); }();
+    return sys;
+}
+static hipError_t wg_timing_event(hipEvent_t *e) {
+    return hipEventCreateWithFlags(e, wg_system_events() ? hipEventDefault : hipEventReleaseToDevice);
+}
 
 // Stages nest: begin takes the next slot and pushes it, end closes the top.
 void wg_stage_begin(wg_ctx *c, const char *name) {
@@ -104,8 +112,9 @@ int wg_side_fork(wg_ctx *c) {
     if (!c->side) {
         WG_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         // stream-to-stream order on one device: a device-scope release suffices
-        WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventReleaseToDevice));
-        WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventReleaseToDevice));
+        const unsigned scope = wg_system_events() ? 0u : hipEventReleaseToDevice;
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | scope));
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | scope));
     }
     if (const int rc = wg_side_join(c)) return rc;
     WG_HIP(c, hipEventRecord(c->ev_fork, c->stream));
