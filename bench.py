@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the side measurements (host-input rate, glyph quads, font atlas)")
+    ap.add_argument("--no-events", action="store_true",
+                    help="diagnostic: no HIP timing events inside the timed region (no roofline launch time)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (host rehearsal)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--device-transport", action="store_true",
@@ -541,7 +543,7 @@ def main():
     # stage's; the stage breakdown is otherwise a separate pass below
     lib_opt = wgraph.lib().wg_set_option
     eng._check(lib_opt(eng._ctx, 4, 0 if args.all_stage_events else 1))   # WG_OPT_TIMING_EMIT_ONLY
-    eng.enable_timing(True, reserve=64 * (args.steps + 1))
+    eng.enable_timing(not args.no_events, reserve=64 * (args.steps + 1))
 
     if comm is not None:
         comm.set_timing(True)

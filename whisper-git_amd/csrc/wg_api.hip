@@ -33,6 +33,7 @@ static bool wg_system_events() {
     static const bool sys = [] { const char *v = std::getenv("WG_EVENT_SCOPE"); return v && !std::strcmp(v, "system"); }();
     return sys;
 }
+static unsigned wg_event_scope() { return wg_system_events() ? 0u : hipEventReleaseToDevice; }
 static hipError_t wg_timing_event(hipEvent_t *e) {
     return hipEventCreateWithFlags(e, wg_system_events() ? hipEventDefault : hipEventReleaseToDevice);
 }
@@ -112,9 +113,8 @@ int wg_side_fork(wg_ctx *c) {
     if (!c->side) {
         WG_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         // stream-to-stream order on one device: a device-scope release suffices
-        const unsigned scope = wg_system_events() ? 0u : hipEventReleaseToDevice;
-        WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | scope));
-        WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | scope));
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | wg_event_scope()));
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | wg_event_scope()));
     }
     if (const int rc = wg_side_join(c)) return rc;
     WG_HIP(c, hipEventRecord(c->ev_fork, c->stream));
@@ -234,7 +234,9 @@ int wg_fetch_begin_n(wg_ctx *c, int n, const WgFetch *items) {
         c->fetch_pending = 0;
     }
     if (const int rc = fetch_launch(c, n, items, FETCH_MAX)) return rc;
-    if (!c->ev_fetch) WG_HIP(c, hipEventCreateWithFlags(&c->ev_fetch, hipEventDisableTiming));
+    // (a device-scope release: the words reach the host by k_fetch's own
+    // system-scope stores; the event only backs the host's fallback wait)
+    if (!c->ev_fetch) WG_HIP(c, hipEventCreateWithFlags(&c->ev_fetch, hipEventDisableTiming | wg_event_scope()));
     WG_HIP(c, hipEventRecord(c->ev_fetch, c->stream));
     c->fetch_pending = n;
     return WG_OK;
@@ -316,7 +318,7 @@ int wg_validate_pending(wg_ctx *c, const uint64_t *v, bool *redone) {
 // stage needed anyway — a value the host needs only later costs no stall.
 int wg_fetch_defer(wg_ctx *c, std::initializer_list<WgFetch> items) {
     if (const int rc = fetch_launch(c, (int)items.size(), items.begin(), 2 * FETCH_MAX)) return rc;
-    if (!c->ev_defer) WG_HIP(c, hipEventCreateWithFlags(&c->ev_defer, hipEventDisableTiming));
+    if (!c->ev_defer) WG_HIP(c, hipEventCreateWithFlags(&c->ev_defer, hipEventDisableTiming | wg_event_scope()));
     WG_HIP(c, hipEventRecord(c->ev_defer, c->stream));
     c->defer_pending = (int)items.size();
     return WG_OK;
