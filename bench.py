@@ -340,8 +340,14 @@ def config_rates(eng, dev, torch, args):
         c1.update({"cpu_ms_per_step": round(cms, 3), "cpu_rows_per_s": round(d1.n / cms * 1e3, 1), "cpu_cores": 1,
                    "cpu_kind": "port (oracle/wg_oracle.c, 1 thread)"})
     res["C1"] = c1
+    import wgraph
     for cid, kind, n in (("C1", "linear", 10_000), ("C3", "random13", 100_000), ("C4", "linux", 1_300_000),
                          ("skew", "skew", 1_000_000), ("linuxwide", "linuxwide", 1_000_000)):
+        # a context of its own per list (a repository tab's GraphLayout): the
+        # bench list's buffers would size the speculative grids (capacities)
+        eng = wgraph.Engine(dev.index)
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        eng.set_defer_validation(not args.no_defer)
         d = synth.generate(kind, n)
         keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
                                                        d.parent_oid.reshape(-1), d.flags, d.band)]
@@ -357,7 +363,7 @@ def config_rates(eng, dev, torch, args):
             else:
                 eng.build_frame(commits=c, device_ptr=keep[5].data_ptr())
             eng.emit_vertices(0, d.n, selected=7)
-        for _ in range(2):
+        for _ in range(5):   # (the replay's blind count adapts over the first builds)
             step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -379,6 +385,7 @@ def config_rates(eng, dev, torch, args):
                          "parents at earlier rows, leaked slots")
         if cid == "linuxwide":
             r["note"] = "LINUX shape with > 100 concurrent lanes (4-word replay occupancy)"
+        eng.close()
         del keep
     return res
 

@@ -281,7 +281,10 @@ struct wg_ctx {
         *chunk = replay_chunk;
         *warm = replay_warm;
         if (!replay_auto) return;
-        if (!replay_long) { *chunk = WG_REPLAY_CHUNK_SHORT; *warm = n_events >= 24576 ? 512u : 256u; }
+        if (!replay_long) {   // (short lists: 64-event chunks — random13 100k 0.093 -> 0.085 ms, r03l / r03q)
+            *chunk = n_events >= 24576 ? WG_REPLAY_CHUNK_SHORT : WG_REPLAY_CHUNK_SHORT / 2;
+            *warm = n_events >= 24576 ? 512u : 256u;
+        }
         else { *chunk = WG_REPLAY_CHUNK_LONG; *warm = 0; }
     }
     uint32_t replay_iters = 0;     // iterations the last replay needed
@@ -295,7 +298,7 @@ struct wg_ctx {
     // needed hundreds of iterations, later builds launched hundreds of empty ones).
     void replay_adapt(uint32_t fp, uint32_t chunk = 0) {
         if (fp == 0) return;
-        if (replay_auto && chunk == WG_REPLAY_CHUNK_SHORT && fp > WG_REPLAY_SHORT_MAX_FP) {
+        if (replay_auto && chunk < WG_REPLAY_CHUNK_LONG && fp > WG_REPLAY_SHORT_MAX_FP) {
             replay_long = true;   // this list shape wants the long chunk (its own blind count from the next build on)
             replay_blind = 4;
             return;
