@@ -76,7 +76,11 @@ def main():
         if cur_e is not None:
             busy += cur_e - cur_s
         windows.append((b - a, busy, nk))
-    timed = windows[-5:] if len(windows) >= 5 else windows
+    # whole steps only (bench.py ends with emission-only calls: windows of a few
+    # launches), and the timed ones: the last five whole steps are the
+    # stage-breakdown pass, whose per-stage events add gaps
+    full = [w for w in windows if w[2] >= 20]
+    timed = full[-10:-5] if len(full) >= 10 else (full[-5:] if len(full) >= 5 else full)
 
     vtx = next((r for r in stats if short(r["Name"]) == KERNEL), None)
     lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py --steps 5 --warmup 2 --no-cpu --no-extras`", ""]
@@ -87,7 +91,7 @@ def main():
         span = sum(w[0] for w in timed) / len(timed) / 1e6
         busy = sum(w[1] for w in timed) / len(timed) / 1e6
         nk = sum(w[2] for w in timed) / len(timed)
-        lines += [f"Per step (k_vtx_tile end to k_vtx_tile end, last {len(timed)} steps): span {span:.3f} ms, "
+        lines += [f"Per step (k_vtx_tile end to k_vtx_tile end, {len(timed)} timed steps): span {span:.3f} ms, "
                   f"GPU busy {busy:.3f} ms ({100 * busy / span:.1f}%), idle {span - busy:.3f} ms, "
                   f"{nk:.0f} kernel launches.", ""]
     lines += ["| kernel | calls | total ms | avg us | % |", "|---|---:|---:|---:|---:|"]
