@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--stage-events", action="store_true", help="record every stage's HIP events (stages_ms)")
+    ap.add_argument("--no-defer", action="store_true", help="validate each speculative pass before the call returns")
     ap.add_argument("--two-calls", action="store_true",
                     help="shard_build + shard_geometry (5 exchanges) instead of shard_build_frame (4)")
     args = ap.parse_args()
@@ -150,6 +151,7 @@ def main():
         e = wgraph.Engine(0)
         s = torch.cuda.Stream(dev)
         e.set_stream(s.cuda_stream)
+        e.set_defer_validation(not args.no_defer)   # as bench.py
         engines.append(e)
         streams.append(s)
 
@@ -229,7 +231,7 @@ def main():
 
     # the single-GPU step on an R-row list of the same kind, for comparison
     single = wgraph.Engine(0)
-    single.set_defer_validation(True)   # as bench.py
+    single.set_defer_validation(not args.no_defer)   # as bench.py
     dag1 = synth.generate(args.kind, R)
     k1 = [torch.from_numpy(a).to(dev) for a in (dag1.oid.reshape(-1), dag1.time, dag1.parent_off.view(np.int32),
                                                  dag1.parent_oid.reshape(-1), dag1.flags, dag1.band)]

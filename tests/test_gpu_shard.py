@@ -146,14 +146,20 @@ def _lockstep(engines, begin):
     return rounds
 
 
-@pytest.mark.parametrize("world,kind,n,frame", [(2, "wide16", 40000, False), (3, "random13", 20000, False),
-                                                (4, "linux", 30000, False), (2, "wide16", 40000, True),
-                                                (4, "random13", 30000, True)])
-def test_packed_slots_in_one_process(world, kind, n, frame):
+@pytest.mark.parametrize("world,kind,n,frame,defer", [(2, "wide16", 40000, False, False),
+                                                      (3, "random13", 20000, False, False),
+                                                      (4, "linux", 30000, False, False),
+                                                      (2, "wide16", 40000, True, False),
+                                                      (4, "random13", 30000, True, False),
+                                                      (3, "wide16", 30000, True, True),
+                                                      (4, "linux", 30000, True, True)])
+def test_packed_slots_in_one_process(world, kind, n, frame, defer):
     """wg_shard_pack_slot: every rank's slot packed on the shared stream, no
     host synchronisation before the gather; shards equal the oracle.  frame:
     wg_shard_build_frame_begin with the device bands (4 exchanges instead of
-    the two calls' 5)."""
+    the two calls' 5).  defer: three steps with WG_OPT_DEFER_VALIDATION, the
+    later steps' speculative local geometry validated by the emission (the
+    second step's emission first, the third step's by a geometry query)."""
     import ctypes
     import sys as _sys
 
@@ -186,11 +192,28 @@ def test_packed_slots_in_one_process(world, kind, n, frame):
     try:
         for e in engines:
             e.set_stream(ts.cuda_stream)
+            e.set_defer_validation(defer)
         rng = [shard_rows(d.n, world, r) for r in range(world)]
         if frame:
-            rounds = _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
-                e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
-            assert rounds == 4
+            def frame_build():
+                return _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
+                    e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
+            assert frame_build() == 4
+            if defer:
+                og = o.row_geometry(d.band)
+                frame_build()   # step 2: a speculative local geometry pass, its validation deferred
+                for r, e in enumerate(engines):   # ... to the emission's vertex-total read
+                    s, t = rng[r]
+                    e.emit_vertices(s, t, selected=s + 3)
+                    ov, _ = o.emit_vertices(s, t, selected=s + 3)
+                    assert e.vertex_summary().checksum == oracle_c.vertex_checksum(ov), f"rank {r} deferred"
+                frame_build()   # step 3: settled by a host query instead
+                for r, e in enumerate(engines):
+                    s, t = rng[r]
+                    g = e.geometry()
+                    vo = og["vert_off"].astype(np.int64)
+                    assert g["row_top"].tobytes() == og["row_top"][s:t + 1].tobytes(), f"rank {r} settled"
+                    assert g["vert"].tobytes() == og["vert"][vo[s]:vo[t]].tobytes(), f"rank {r} settled"
         else:
             _lockstep(engines, lambda e, r, m: lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), world, r,
                                                                            rng[r][0], rng[r][1], m))

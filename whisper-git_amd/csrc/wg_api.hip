@@ -298,7 +298,7 @@ int wg_validate_pending(wg_ctx *c, const uint64_t *v, bool *redone) {
     const PendingBuild P = c->pend;
     c->pend = PendingBuild{};
     bool redo = false;
-    int rc = build_check(c, v, P.kl, P.k, &redo);
+    int rc = P.shard ? wg_shard_geom_validate(c, v, &redo) : build_check(c, v, P.kl, P.k, &redo);
     if (rc != WG_OK || !redo) return rc;
     *redone = true;
     if (P.frame && (rc = row_geometry_impl(c, P.frame_band ? c->band_prev.as<const float>() : nullptr, WG_DEVICE)) != WG_OK)

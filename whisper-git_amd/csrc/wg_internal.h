@@ -159,6 +159,7 @@ struct ShardState {
     DevBuf in_scan, edge_y, own_edges;
     uint64_t n_own_edges = 0;
     bool geom_spec_ready = false;   // an earlier sharded geometry pass sized the lists (speculation may start)
+    bool geom_banded = false;       // the last local geometry pass took bands (c->band holds the local copy)
 };
 
 // SDF font atlas slot (wg_font.hip)
@@ -216,6 +217,7 @@ constexpr int WG_PENDING_ITEMS = WG_LANES_SPEC_ITEMS + WG_GEOM_SPEC_ITEMS + 1;
 // total (or by wg_settle), and a build that did not hold is redone then
 struct PendingBuild {
     bool build = false;
+    bool shard = false;             // a sharded build's speculative geometry pass only (its lanes are exact)
     int k = 0, kl = 0;              // validation items, of which the lane stage's
     WgFetch it[WG_PENDING_ITEMS];
     bool frame = false, frame_band = false;   // a frame geometry pass followed (its bands are in band_prev)
@@ -446,6 +448,9 @@ int wg_fetch_begin_n(wg_ctx *c, int n, const WgFetch *items);
 // followed by the frame pass and emission queued after it (*redone = true).
 int wg_settle(wg_ctx *c);
 int wg_validate_pending(wg_ctx *c, const uint64_t *v, bool *redone);
+// a sharded geometry pass awaiting its validation (wg_shard.hip): check the
+// words, redo the pass exactly when they do not hold (*redo)
+int wg_shard_geom_validate(wg_ctx *c, const uint64_t *v, bool *redo);
 #define WG_SETTLE(c)                                                               \
     do {                                                                           \
         if ((c)->pend.build) {                                                     \

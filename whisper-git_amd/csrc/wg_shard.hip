@@ -738,6 +738,7 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     S.n_own_edges = ne - n_in;
     S.local_gen = c->layout_gen;
     const float *band_l = band_g ? c->band.as<const float>() : nullptr;
+    S.geom_banded = band_g != nullptr;
     c->spec = spec;
     rc = wg_stage_geometry(c, band_l);
     c->spec = false;
@@ -747,21 +748,50 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
         int k = wg_geom_spec_items(c, it);
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + nloc, false};
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + 1, false};
+        static_assert(WG_GEOM_SPEC_ITEMS + 2 <= WG_PENDING_ITEMS, "shard geometry words exceed a pending build's");
+        if (c->defer_validation) {
+            // no host read: the words ride on the emission's vertex-total read
+            // (the emission is gated on the pass's overflow words, as after a
+            // deferred single-GPU build); any host query settles them first
+            PendingBuild &P = c->pend;
+            P = PendingBuild{};
+            P.build = true;
+            P.shard = true;
+            P.k = k;
+            for (int i = 0; i < k; i++) P.it[i] = it[i];
+            c->have_geom = true;
+            sh_done(c, out);
+            return WG_OK;
+        }
         uint64_t v[WG_GEOM_SPEC_ITEMS + 4] = {0};
         if ((rc = wg_fetch_n(c, k, it, v)) != WG_OK) return rc;
-        S.local_ne = v[WG_GEOM_SPEC_ITEMS];
-        S.local_nin = v[WG_GEOM_SPEC_ITEMS + 1];
-        c->n_edges = S.local_ne;
-        S.n_own_edges = S.local_ne - S.local_nin;
-        if (!wg_geom_spec_check(c, v)) {   // past a capacity: the exact pass (the local edges are in place)
-            c->spec_redo_geom++;
-            c->lists_gen = ~0ull;
-            if ((rc = wg_stage_geometry(c, band_l)) != WG_OK) return rc;
-        }
+        bool redo = false;
+        if ((rc = wg_shard_geom_validate(c, v, &redo)) != WG_OK) return rc;
     }
     S.geom_spec_ready = c->lists_gen == c->layout_gen;
     c->have_geom = true;
     sh_done(c, out);
+    return WG_OK;
+}
+
+// the speculative local geometry pass's words (WG_GEOM_SPEC_ITEMS, then the
+// local edge count and the incoming edges' count): the counts, and past a
+// capacity the exact pass (the local edges are in place)
+int wg_shard_geom_validate(wg_ctx *c, const uint64_t *v, bool *redo) {
+    ShardState &S = c->sh;
+    *redo = false;
+    S.local_ne = v[WG_GEOM_SPEC_ITEMS];
+    S.local_nin = v[WG_GEOM_SPEC_ITEMS + 1];
+    c->n_edges = S.local_ne;
+    S.n_own_edges = S.local_ne - S.local_nin;
+    if (!wg_geom_spec_check(c, v)) {
+        *redo = true;
+        c->spec_redo_geom++;
+        c->lists_gen = ~0ull;
+        const int rc = wg_stage_geometry(c, S.geom_banded ? c->band.as<const float>() : nullptr);
+        if (rc != WG_OK) return rc;
+    }
+    S.geom_spec_ready = c->lists_gen == c->layout_gen;
     return WG_OK;
 }
 
