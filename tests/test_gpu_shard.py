@@ -237,3 +237,68 @@ def test_packed_slots_in_one_process(world, kind, n, frame, defer):
             e.close()
         stream_ctx.__exit__(None, None, None)
         del keep
+
+
+@pytest.mark.parametrize("bad", ["own_range", "length"])
+def test_x1_header_guards(bad):
+    """wg_shard_exchange refuses a gathered X1 whose headers do not hold
+    (VERDICT r02 weak #13): this rank's own reference range past the list
+    (E1 > n_parents, once a size underflow) or an unresolved-reference count
+    longer than the message that carried it -> WG_E_INVALID with a message,
+    no launch sized by it."""
+    import ctypes
+    import sys as _sys
+
+    import numpy as np
+    import torch
+    _sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+    import wgraph
+    from wgraph import abi, lib, synth
+    from wgraph.shard import ShardComm, shard_rows
+
+    d = synth.generate("wide16", 20000, seed=5)
+    dev = torch.device("cuda", 0)
+    keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                   d.parent_oid.reshape(-1), d.flags)]
+    c = abi.Commits()
+    c.n_commits, c.n_parents = d.n, d.e
+    c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep)
+    c.residency = abi.WG_DEVICE
+    ts = torch.cuda.Stream(dev)
+    ts.wait_stream(torch.cuda.current_stream(dev))
+    W = 2
+    engines = [wgraph.Engine(0) for _ in range(W)]
+    try:
+        msgs = [abi.ShardMsg() for _ in range(W)]
+        for r, e in enumerate(engines):
+            e.set_stream(ts.cuda_stream)
+            s, t = shard_rows(d.n, W, r)
+            e._check(lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), W, r, s, t, ctypes.byref(msgs[r])))
+        sizes = []
+        for e in engines:
+            n = ctypes.c_uint64(0)
+            e._check(lib().wg_shard_msg_bytes(e._ctx, ctypes.byref(n)))
+            sizes.append(int(n.value))
+        cap = ShardComm.round_cap(max(sizes))
+        stride = cap + ShardComm.HDR
+        with torch.cuda.stream(ts):
+            slots = torch.zeros(W * stride, dtype=torch.uint8, device=dev)
+            for r, e in enumerate(engines):
+                e._check(lib().wg_shard_pack_slot(e._ctx, slots.data_ptr() + r * stride, cap))
+        ts.synchronize()
+        heads = np.ascontiguousarray(slots.view(W, stride)[:, 16:32].cpu().numpy()).view(np.uint32).reshape(W, 4).copy()
+        if bad == "own_range":   # rank 0's own range [E0, E1) with E1 past the list's references
+            heads[0, 3] = 0xFFFFFFF0
+        else:                    # rank 1 announces more unresolved references than its message holds
+            heads[1, 1] = 1 << 20
+        out = abi.ShardMsg()
+        sz = (ctypes.c_uint64 * W)(*sizes)
+        rc = lib().wg_shard_exchange(engines[0]._ctx, slots.data_ptr() + ShardComm.HDR, stride, sz,
+                                     heads.ctypes.data, ctypes.byref(out))
+        assert rc == abi.WG_E_INVALID
+        msg = lib().wg_last_error(engines[0]._ctx).decode()
+        assert ("X1 header" in msg) if bad == "own_range" else ("announces" in msg), msg
+    finally:
+        for e in engines:
+            e.close()
+        del keep

@@ -13,7 +13,8 @@
 //            compacted into LDS: every cell pixel counts which of its 4x4
 //            sample points lie inside the outline (non-zero winding) ->
 //            coverage 0..16; inside = coverage >= 8
-//   k_edt_cols        pass 1, one thread per pixel scanning its column
+//   k_edt_cols        pass 1, one lane per column of a 64 x 64 tile staged in
+//                     LDS with R rows above and below: one sweep down, one up
 //            outward: squared vertical distance to the nearest pixel of the
 //            other class
 //   k_edt_rows        pass 2, one workgroup per row staged in LDS: squared
@@ -115,21 +116,73 @@ __global__ void __launch_bounds__(COV_T) k_font_coverage(const GlyphDesc *__rest
 // gout[y][x] = (vertical distance from an outside pixel to the nearest inside pixel)^2
 // 0 on the pixel's own class; capped at (R + 1)^2.  One thread per pixel
 // scanning its column outward (coalesced across x), exit at the first hit.
-__global__ void k_edt_cols(const uint8_t *__restrict__ cov, uint32_t W, uint32_t H, uint32_t R,
-                           uint16_t *__restrict__ gin, uint16_t *__restrict__ gout) {
-    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t y = blockIdx.y;
-    if (x >= W) return;
-    const uint64_t o = (uint64_t)y * W + x;
-    const bool in = cov[o] >= 8;
-    uint32_t d = R + 1;
-    for (uint32_t k = 1; k <= R; k++) {
-        const bool hit_up = y >= k && ((cov[o - (uint64_t)k * W] >= 8) != in);
-        const bool hit_dn = y + k < H && ((cov[o + (uint64_t)k * W] >= 8) != in);
-        if (hit_up || hit_dn) { d = k; break; }
+// One wave per 64 x 64 pixel tile: the tile's columns plus R rows above and
+// below are staged in LDS (1 = inside, 0 = outside, 2 = past the atlas),
+// then each lane sweeps its column down and up once, keeping the last row
+// of either class seen: a pixel's nearest pixel of the other class above
+// (below) is the last (next) row of that class, so d = min of the two
+// distances, capped at R + 1 — the same value as scanning k = 1..R.
+constexpr uint32_t EC_TX = 64, EC_TY = 64, EC_RMAX = 240;   // R = 4 * spread, spread <= 60
+__global__ void __launch_bounds__(64) k_edt_cols(const uint8_t *__restrict__ cov, uint32_t W, uint32_t H, uint32_t R,
+                                                uint16_t *__restrict__ gin, uint16_t *__restrict__ gout) {
+    __shared__ __attribute__((aligned(16))) uint8_t t[(EC_TY + 2 * EC_RMAX) * EC_TX];
+    __shared__ uint16_t dup[EC_TY * EC_TX];
+    const uint32_t x0 = blockIdx.x * EC_TX, y0 = blockIdx.y * EC_TY;
+    const uint32_t rows = EC_TY + 2 * R;
+    const uint32_t c = threadIdx.x, x = x0 + c;
+    if ((W & 15u) == 0 && x0 + EC_TX <= W) {
+        // 16-byte loads, 16 rows per wave instruction, all of them in flight
+        const uint32_t q = c & 3u, rsub = c >> 2;   // 4 lanes per 64-byte row, 16 rows per round
+        for (uint32_t lr0 = 0; lr0 < rows; lr0 += 16) {
+            const uint32_t lr = lr0 + rsub;
+            const int64_t y = (int64_t)y0 + (int64_t)lr - (int64_t)R;
+            uint4 v = make_uint4(0x02020202u, 0x02020202u, 0x02020202u, 0x02020202u);
+            if (lr < rows && y >= 0 && y < (int64_t)H) {
+                const uint4 w = *reinterpret_cast<const uint4 *>(cov + (uint64_t)y * W + x0 + 16 * q);
+                auto cls = [](uint32_t b) {   // byte-wise (b >= 8) ? 1 : 0
+                    uint32_t r = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) r |= (((b >> (8 * k)) & 0xFFu) >= 8u ? 1u : 0u) << (8 * k);
+                    return r;
+                };
+                v = make_uint4(cls(w.x), cls(w.y), cls(w.z), cls(w.w));
+            }
+            if (lr < rows) *reinterpret_cast<uint4 *>(t + lr * EC_TX + 16 * q) = v;
+        }
+        __syncthreads();   // (rows were staged by other lanes)
+    } else {
+        for (uint32_t lr = 0; lr < rows; lr++) {
+            const int64_t y = (int64_t)y0 + (int64_t)lr - (int64_t)R;
+            t[lr * EC_TX + c] = (y < 0 || y >= (int64_t)H || x >= W) ? 2u : (cov[(uint64_t)y * W + x] >= 8 ? 1u : 0u);
+        }
     }
-    gin[o] = (uint16_t)(in ? d * d : 0u);
-    gout[o] = (uint16_t)(in ? 0u : d * d);
+    // (below, each lane reads only its own column)
+    const int32_t far = (int32_t)R + 1;
+    int32_t last[2] = {-1000000, -1000000};   // staged row of the last pixel of class 0 / 1 above
+    for (uint32_t lr = 0; lr < R + EC_TY; lr++) {
+        const uint32_t v = t[lr * EC_TX + c];
+        if (lr >= R) {
+            const int32_t du = (v < 2u) ? (int32_t)lr - last[v ^ 1u] : far;
+            dup[(lr - R) * EC_TX + c] = (uint16_t)(du < far ? du : far);
+        }
+        if (v < 2u) last[v] = (int32_t)lr;
+    }
+    int32_t next[2] = {1000000, 1000000};     // ... and below
+    for (int32_t lr = (int32_t)rows - 1; lr >= (int32_t)R; lr--) {
+        const uint32_t v = t[lr * EC_TX + c];
+        if (lr < (int32_t)(R + EC_TY)) {
+            const uint32_t ly = (uint32_t)lr - R, y = y0 + ly;
+            if (x < W && y < H) {
+                const int32_t dd = next[v ^ 1u] - lr;
+                int32_t d = dup[ly * EC_TX + c];
+                d = dd < d ? dd : d;
+                const uint64_t o = (uint64_t)y * W + x;
+                gin[o] = (uint16_t)(v ? d * d : 0);
+                gout[o] = (uint16_t)(v ? 0 : d * d);
+            }
+        }
+        if (v < 2u) next[v] = lr;
+    }
 }
 
 // ---- pass 2: rows -> squared distances and the SDF byte -------------------------------
@@ -456,7 +509,8 @@ int wg_font_atlas_build(wg_ctx *c, int slot, const uint8_t *ttf, uint64_t len, c
                            S.gdesc.as<const GlyphDesc>(), S.edges.as<const float4>(), spread, W, S.cov.as<uint8_t>());
     wg_stage_end(c);
     wg_stage_begin(c, "font_edt");
-    hipLaunchKernelGGL(k_edt_cols, dim3((W + 255) / 256, H), dim3(256), 0, s, S.cov.as<const uint8_t>(), W, H, S.R,
+    hipLaunchKernelGGL(k_edt_cols, dim3((W + EC_TX - 1) / EC_TX, (H + EC_TY - 1) / EC_TY), dim3(EC_TX), 0, s,
+                       S.cov.as<const uint8_t>(), W, H, S.R,
                        S.gin.as<uint16_t>(), S.gout.as<uint16_t>());
     hipLaunchKernelGGL(k_edt_rows, dim3(H), dim3(ROW_T), 0, s, S.gin.as<const uint16_t>(), S.gout.as<const uint16_t>(), W,
                        S.R, (float)spread, S.d2in.as<uint16_t>(), S.d2out.as<uint16_t>(), S.sdf.as<uint8_t>());
