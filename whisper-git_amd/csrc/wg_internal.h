@@ -144,7 +144,6 @@ struct ShardState {
     DevBuf dlist;   // the partition's rows {home slot, fingerprint, row} for the duplicate scan's settle pass
     DevBuf xall;              // WgXEnt [nx]: crossing entries of every rank
     std::vector<uint64_t> xoff, evoff, auxoff;   // per-rank prefixes (world + 1)
-    uint64_t nev_own = 0, naux_own = 0;
     DevBuf xtok, xt;          // chain token per crossing entry: shard-local / global
     DevBuf dev_small;
     DevBuf h_g, rt_g;         // heights of rows [0, e) / row_top of rows [s, e] (below s: unspecified)

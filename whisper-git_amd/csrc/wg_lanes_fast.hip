@@ -287,8 +287,10 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
                             const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
                             const uint32_t *__restrict__ secev, const uint32_t *__restrict__ sp,
                             uint4 *__restrict__ ev, uint32_t *__restrict__ aux, const uint32_t *__restrict__ gate = nullptr,
-                            WgReplayInit RI = WgReplayInit{}) {
+                            WgReplayInit RI = WgReplayInit{}, const uint32_t *__restrict__ aux_after = nullptr) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // (a message whose merge-token lists follow its records: the event count is on the device)
+    if (aux_after) aux = reinterpret_cast<uint32_t *>(ev + *aux_after);
     // speculative build: the replay's initial state (wg_replay_prepare_spec)
     for (uint64_t i = j; i < RI.total; i += (uint64_t)gridDim.x * blockDim.x) {
         if (i < RI.occ_words) RI.occ[i] = 0ull;
@@ -537,11 +539,16 @@ int wg_lf_events_local(wg_ctx *c, const LfRange &R, uint4 *ev_out, uint32_t *aux
     const uint64_t n = R.nl;
     if (!n) return WG_OK;
     wg_stage_begin(c, "lf_events");
+    // aux_out == nullptr: the merge-token lists right after the records, at the
+    // device event count; nothing is written when the list is not well formed
+    const bool after = aux_out == nullptr;
     hipLaunchKernelGGL(k_lf_events<true>, dim3(blocks(n)), dim3(T), 0, c->stream, R, 0u, 0u, (const uint32_t *)nullptr,
                        c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
                        c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
                        c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
-                       c->lf[LF_SECEV].as<const uint32_t>(), lf_sp(c), ev_out, aux_out);
+                       c->lf[LF_SECEV].as<const uint32_t>(), lf_sp(c), ev_out, aux_out,
+                       after ? c->lf[LF_FLAGS].as<const uint32_t>() : (const uint32_t *)nullptr, WgReplayInit{},
+                       after ? c->lf[LF_EVOFF].as<const uint32_t>() + n : (const uint32_t *)nullptr);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;

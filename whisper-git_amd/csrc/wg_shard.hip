@@ -462,6 +462,14 @@ __global__ void k_sh_x1_head(uint4 *__restrict__ dst, unsigned long long *__rest
     *dst = make_uint4(flags[0] | flags[1], nu, poff[s], poff[e]);
     *len = 16ull + (unsigned long long)nu * 32ull;
 }
+// X3's header and length from the lane prelude's device words: {events,
+// merge words, not well formed} (no records when not well formed)
+__global__ void k_sh_x3_head(uint4 *__restrict__ dst, unsigned long long *__restrict__ len, const uint32_t *__restrict__ flags,
+                             const uint32_t *__restrict__ nev, const uint32_t *__restrict__ naux, uint64_t tok_b) {
+    const uint32_t viol = flags[0], ne = nev[0], na = naux[0];
+    *dst = make_uint4(ne, na, viol, 0u);
+    *len = 16ull + tok_b + (viol ? 0ull : (unsigned long long)ne * 16ull + (unsigned long long)na * 4ull);
+}
 // transport slot of a message whose length is on the device: header, then the
 // payload when it fits (its first 16 bytes zero otherwise); 16-byte moves
 __global__ void __launch_bounds__(256) k_sh_pack_dev(uint4 *__restrict__ slot, uint64_t cap, const uint4 *__restrict__ msg,
@@ -1098,29 +1106,27 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, st));
         LfRange R = sh_range(c);
         wg_stage_begin(c, "lanes");
-        uint32_t viol = 0;
-        uint64_t nev = 0, naux = 0;
-        if ((rc = wg_lf_refs(c, R, true)) != WG_OK) return rc;
-        rc = wg_lf_chain(c, R);                   // queued before the flags are back
-        const int rc2 = wg_lf_refs_end(c, &viol, &nev, &naux);
-        if (rc != WG_OK) return rc;
-        if (rc2 != WG_OK) return rc2;
+        // No host read: the message (header, tokens, then the event records
+        // and merge-token lists) is bounded by the rows' references (a row
+        // makes at most max(1, parents) events; merge lists hold at most
+        // 2 (n + E) + 16 words) and its header and length are written on the
+        // device, as X1's are; every rank learns the counts from the gathered
+        // heads.  Not well formed: no records, every rank falls back at X3.
+        if ((rc = wg_lf_refs(c, R, false)) != WG_OK) return rc;
+        if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
         wg_stage_end(c);
-        S.nev_own = nev;
-        S.naux_own = naux;
         const uint64_t nown = R.xown_end - R.xown_begin;
         const uint64_t tok_b = (nown * 4 + 15) & ~15ull;          // records start 16-byte aligned
-        const uint64_t rec_b = viol ? 0 : nev * 16 + naux * 4;    // not well formed: every rank falls back at X3
+        const uint64_t ev_cap = nl + El, aux_cap = 2 * (nl + El) + 16;
         S.step = SH_X3;
-        if ((rc = sh_send(c, 16 + tok_b + rec_b, out)) != WG_OK) return rc;
-        uint32_t h4[4] = {(uint32_t)nev, (uint32_t)naux, viol, 0};
-        hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), make_uint4(h4[0], h4[1], h4[2], h4[3]));
+        if ((rc = sh_send_dev(c, 16 + tok_b + ev_cap * 16 + aux_cap * 4, out)) != WG_OK) return rc;
+        hipLaunchKernelGGL(k_sh_x3_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), S.msg_len.as<unsigned long long>(),
+                           c->lf[LF_FLAGS].as<const uint32_t>(), c->lf[LF_EVOFF].as<const uint32_t>() + nl,
+                           c->lf[LF_AUXOFF].as<const uint32_t>() + nl, tok_b);
         uint8_t *m = S.msg.as<uint8_t>() + 16;
         if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(m))) != WG_OK) return rc;
         // the event records travel in the same message, with shard-local tokens
-        if (!viol && (rc = wg_lf_events_local(c, R, reinterpret_cast<uint4 *>(m + tok_b),
-                                              reinterpret_cast<uint32_t *>(m + tok_b + nev * 16))) != WG_OK)
-            return rc;
+        if ((rc = wg_lf_events_local(c, R, reinterpret_cast<uint4 *>(m + tok_b), nullptr)) != WG_OK) return rc;
         return WG_OK;
     }
     case SH_X3: {   // global event ids; replay the global event stream; lanes of own rows; default geometry
