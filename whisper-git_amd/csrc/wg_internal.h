@@ -384,6 +384,7 @@ struct wg_ctx {
     // ---- vertices -------------------------------------------------------------
     bool     have_vtx = false;
     uint64_t vrow_begin = 0, vrow_end = 0, n_vtx = 0;
+    uint64_t vtx_tiles_last = 0;   // tiles of the last emission (bounds the next one's early grid)
     int64_t  selected = -1;
     DevBuf vtx_off;         // uint64 [rows+1]
     DevBuf vtx;             // wg_vertex [n_vtx]

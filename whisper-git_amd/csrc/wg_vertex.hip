@@ -477,7 +477,13 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
                            c->vtx.as<float4>(), grid, ml_dev, gate);
         wg_stage_end(c);
     };
-    if (early) launch(vcap, std::min((vcap + TILE - 1) / TILE, tcap - 1));
+    // the early grid: the buffers' capacity, bounded by twice the last
+    // emission's tiles (a context whose lists shrank would otherwise launch
+    // its largest list's grid every frame); a list that outgrows it is
+    // launched again whole below
+    uint64_t early_grid = std::min((vcap + TILE - 1) / TILE, tcap - 1);
+    if (c->vtx_tiles_last) early_grid = std::min(early_grid, 2 * c->vtx_tiles_last + 64);
+    if (early) launch(vcap, early_grid);
     uint64_t fv[1 + WG_PENDING_ITEMS] = {0};
     if (const int rc = wg_fetch_end(c, fv)) return rc;
     if (npend) {   // validate the build; one that did not hold is redone here, with this frame and emission
@@ -488,7 +494,8 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const uint64_t total = fv[0];
     c->n_vtx = total;
     const uint64_t ntiles = (total + TILE - 1) / TILE;
-    if (!early || total > vcap || ntiles + 1 > tcap) {   // did not fit: size the buffers and launch again
+    c->vtx_tiles_last = ntiles;
+    if (!early || total > vcap || ntiles + 1 > tcap || ntiles > early_grid) {   // did not fit: size the buffers and launch again
         if (early) wg_stage_begin(c, "vtx_counts");
         WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
         WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
