@@ -221,6 +221,13 @@ int         wg_synchronize(wg_ctx *ctx);
  * states are mostly right before the second iteration.  Speed only, never
  * results. */
 #define WG_OPT_REPLAY_WARMUP 6
+/* WG_OPT_SHARD_SPEC_REPLAY: 1 (default) = once a sharded build sized the
+ * context, the X3 step replays the global lane events for the blind
+ * iteration count without a host read; the replay's convergence and width
+ * words travel in the X6 headers, and a replay that did not reach its fixed
+ * point is redone exactly at X6 (whose message is then sent again: one more
+ * exchange round, same results).  0 = the replay is checked before X3 returns. */
+#define WG_OPT_SHARD_SPEC_REPLAY 7
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------

@@ -302,3 +302,84 @@ def test_x1_header_guards(bad):
         for e in engines:
             e.close()
         del keep
+
+
+@pytest.mark.parametrize("spec", [True, False])
+def test_spec_replay_sequence(spec):
+    """WG_OPT_SHARD_SPEC_REPLAY: after the first sharded build, X3 replays the
+    global events blind and the X6 headers carry the replay's words.  A list
+    shape change (wide16 -> linux) leaves the blind count short: every rank
+    redoes the replay exactly at X6 and sends X6 again (5 exchange rounds
+    instead of 4); lanes, geometry and vertices equal the oracle every step.
+    spec=False: the replay is checked before X3 returns, 4 rounds always."""
+    import ctypes
+    import sys as _sys
+
+    import numpy as np
+    import torch
+    _sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+    _sys.path.insert(0, ROOT)
+    import wgraph
+    from oracle import oracle_c
+    from wgraph import abi, lib, synth
+    from wgraph.shard import shard_rows
+
+    world = 3
+    dev = torch.device("cuda", 0)
+    ts = torch.cuda.Stream(dev)
+    ts.wait_stream(torch.cuda.current_stream(dev))
+    stream_ctx = torch.cuda.stream(ts)
+    stream_ctx.__enter__()
+    engines = [wgraph.Engine(0) for _ in range(world)]
+    redo_steps = []
+    try:
+        for e in engines:
+            e.set_stream(ts.cuda_stream)
+            e.set_shard_spec_replay(spec)
+        for step, (kind, n, seed) in enumerate([("wide16", 20000, 3), ("wide16", 20000, 4), ("linux", 30000, 5),
+                                                 ("linux", 30000, 6), ("random13", 25000, 7)]):
+            d = synth.generate(kind, n, seed=seed)
+            keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                           d.parent_oid.reshape(-1), d.flags, d.band)]
+            c = abi.Commits()
+            c.n_commits, c.n_parents = d.n, d.e
+            c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
+            c.residency = abi.WG_DEVICE
+            rng = [shard_rows(d.n, world, r) for r in range(world)]
+            before = [int(e.debug_counters()[7]) if step else 0 for e in engines]
+            rounds = _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
+                e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
+            redo = [int(e.debug_counters()[7]) - b for e, b in zip(engines, before)]
+            assert len(set(redo)) == 1, f"step {step}: ranks disagree on the redo {redo}"
+            assert rounds == 4 + redo[0], f"step {step}: {rounds} rounds, {redo[0]} redone"
+            if not spec or step == 0:
+                assert redo[0] == 0
+            redo_steps.append(redo[0])
+            o = oracle_c.OracleLayout(d)
+            try:
+                og = o.row_geometry(d.band)
+                vo = og["vert_off"].astype(np.int64)
+                for r, e in enumerate(engines):
+                    s, t = rng[r]
+                    assert int(e.debug_counters()[5]) == 1, "sharded path expected"
+                    lane, color = e.lanes()
+                    assert lane.tobytes() == o.lane[s:t].tobytes() and color.tobytes() == o.color[s:t].tobytes(), \
+                        f"step {step} rank {r} lanes"
+                    ls_ = e.layout_summary()
+                    assert ls_.max_lane == o.max_lane and ls_.n_slots == o.n_slots, f"step {step} rank {r} max_lane"
+                    g = e.geometry()
+                    assert g["row_top"].tobytes() == og["row_top"][s:t + 1].tobytes(), f"step {step} rank {r}"
+                    assert g["vert"].tobytes() == og["vert"][vo[s]:vo[t]].tobytes(), f"step {step} rank {r}"
+                    e.emit_vertices(s, t, selected=s + 3)
+                    ov, _ = o.emit_vertices(s, t, selected=s + 3)
+                    assert e.vertex_summary().checksum == oracle_c.vertex_checksum(ov), f"step {step} rank {r} vertices"
+            finally:
+                o.close()
+            torch.cuda.synchronize()
+            del keep
+        if spec:
+            assert sum(redo_steps) >= 1, f"no step exercised the X6 redo: {redo_steps}"
+    finally:
+        for e in engines:
+            e.close()
+        stream_ctx.__exit__(None, None, None)

@@ -453,6 +453,9 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         WG_SETTLE(c);
         c->defer_validation = value != 0;
         return WG_OK;
+    case WG_OPT_SHARD_SPEC_REPLAY:
+        c->spec_replay_shard = value != 0;
+        return WG_OK;
     case WG_OPT_SWEEP_REG:
         if (value < 0 || value > 512) return wg_fail(c, WG_E_INVALID, "sweep register capacity must be 0..512");
         c->sweep_reg_cap = (uint32_t)value;

@@ -159,6 +159,9 @@ struct ShardState {
     uint64_t n_own_edges = 0;
     bool geom_spec_ready = false;   // an earlier sharded geometry pass sized the lists (speculation may start)
     bool geom_banded = false;       // the last local geometry pass took bands (c->band holds the local copy)
+    bool replay_pending = false;    // X3 replayed speculatively: its words ride on the X6 headers
+    uint32_t rp_it = 0, rp_chunk = 0;
+    const uint32_t *rp_flags = nullptr, *rp_scal = nullptr;
 };
 
 // SDF font atlas slot (wg_font.hip)
@@ -321,6 +324,7 @@ struct wg_ctx {
     bool spec = false;          // the build in progress is speculative
     bool spec_ready = false;    // an exact build sized this context's buffers (speculation may start)
     bool defer_validation = false;   // WG_OPT_DEFER_VALIDATION
+    bool spec_replay_shard = true;   // WG_OPT_SHARD_SPEC_REPLAY
     PendingBuild pend;
     uint64_t spec_nsuper_grid = 0;   // the speculative geometry pass's curve-record grid (its capacity)
     uint32_t spec_builds = 0, spec_redo_lanes = 0, spec_redo_geom = 0;   // speculative builds, of which lanes / geometry redone
@@ -612,6 +616,9 @@ int wg_lf_events_finish(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uin
 // more than 63 slots (the caller takes its fallback)
 int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
                        bool *ok);
+int wg_lf_replay_lanes_spec(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                            ReplayRun &run);
+void wg_lf_replay_spec_commit(wg_ctx *c, uint32_t it, uint32_t chunk, uint32_t max_lane, uint32_t n_slots, uint32_t first_still);
 int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
 int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out,
                    const int64_t *time = nullptr);   // rows [0,m) of an n-row list (time: the layout's)

@@ -589,19 +589,13 @@ int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *e
     }
 }
 
-static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
-                           uint32_t nw, bool *ok, bool *overflow) {
-    hipStream_t s = c->stream;
-    *ok = false;
-    *overflow = false;
-    wg_stage_begin(c, "lf_loop");
-    ReplayRun run;
+// the run's buffers and geometry at occupancy width nw (exact and speculative sharded replays)
+static int replay_setup(wg_ctx *c, ReplayRun &run, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t nw) {
     run.nev = nev;
     run.nw = nw;
     c->replay_geometry(&run.chunk, &run.warm);
     const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
-    if (run.chunk < WG_REPLAY_CHUNK_LONG && c->replay_auto) run.switch_it = WG_REPLAY_SWITCH_IT;
     DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
     DevBuf &rflags = c->lf[LF_RFLAGS];
     WG_ALLOC(c, slot_a, (nev + 64) * sizeof(uint16_t));
@@ -618,6 +612,47 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
     run.stats = stats.as<uint32_t>();
     run.flags = rflags.as<uint32_t>();
     run.scal = c->lane_scalars.as<uint32_t>();
+    return WG_OK;
+}
+
+// Speculative form (the sharded build's X3 step, wg_shard.hip): the blind
+// iterations and the lanes of the range with no host read.  The convergence
+// and width words (run.flags[it - 1], run.flags[it], the lane scalars) travel
+// in the X6 header (k_sh_x6_head); a replay that was no fixed point is redone
+// by wg_lf_replay_lanes then, and wg_lf_replay_spec_commit applies the words.
+int wg_lf_replay_lanes_spec(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                            ReplayRun &run) {
+    run = ReplayRun{};
+    int rc = replay_setup(c, run, nev, ev, aux, c->replay_nw);
+    if (rc != WG_OK) return rc;
+    hipStream_t s = c->stream;
+    wg_stage_begin(c, "lf_loop");
+    WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind < 2 ? 2u : c->replay_blind));
+    if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    return WG_OK;
+}
+
+void wg_lf_replay_spec_commit(wg_ctx *c, uint32_t it, uint32_t chunk, uint32_t max_lane, uint32_t n_slots, uint32_t first_still) {
+    c->max_lane = max_lane;
+    c->n_slots = n_slots;
+    c->replay_nw = wg_ctx::nw_for_slots(n_slots);
+    c->replay_iters = it;
+    c->replay_adapt(first_still, chunk);
+    c->lane_path = 0;
+}
+
+static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                           uint32_t nw, bool *ok, bool *overflow) {
+    hipStream_t s = c->stream;
+    *ok = false;
+    *overflow = false;
+    ReplayRun run;
+    int src = replay_setup(c, run, nev, ev, aux, nw);
+    if (src != WG_OK) return src;
+    if (run.chunk < WG_REPLAY_CHUNK_LONG && c->replay_auto) run.switch_it = WG_REPLAY_SWITCH_IT;
+    wg_stage_begin(c, "lf_loop");
     WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind));
     const uint32_t blind = run.it;
     const uint32_t *ls = c->lane_scalars.as<const uint32_t>();

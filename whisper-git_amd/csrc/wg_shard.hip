@@ -452,7 +452,20 @@ __global__ void k_sh_edges_own(LocalEdgeArgs A) {
 }
 
 // a message's 16-byte header (kernel arguments: no host buffer outlives the call)
-__global__ void k_sh_put_head(uint4 *__restrict__ dst, uint4 v) { *dst = v; }
+// X6 header from the device: {own entries, incoming entries, replay words,
+// max_lane | first iteration that changed nothing << 16}.  Replay words (a
+// speculative X3 replay, else 0): bit 0 = no fixed point within the blind
+// iterations, bit 1 = past the occupancy width, slots << 2.
+__global__ void k_sh_x6_head(uint4 *__restrict__ dst, uint32_t nown, uint32_t xin, const uint32_t *__restrict__ flags,
+                             uint32_t it, const uint32_t *__restrict__ scal) {
+    uint32_t w2 = 0, w3 = 0;
+    if (flags) {
+        const bool conv = it == 0 || flags[it - 1] == 0 || flags[it] == 0;
+        w2 = (conv ? 0u : 1u) | (scal[2] ? 2u : 0u) | (min(scal[1], 0x3fffffffu) << 2);
+        w3 = min(scal[0], 0xffffu) | (min(scal[3], 0xffffu) << 16);
+    }
+    *dst = make_uint4(nown, xin, w2, w3);
+}
 // X1 header from the device: {violation | duplicate, unresolved references,
 // E0 = parent_off[s], E1 = parent_off[e]} and the message length
 __global__ void k_sh_x1_head(uint4 *__restrict__ dst, unsigned long long *__restrict__ len, const uint32_t *__restrict__ flags,
@@ -597,10 +610,25 @@ static LfRange sh_range(wg_ctx *c) {
     return R;
 }
 
+static void sh_graph_width(wg_ctx *c) {
+    const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
+    const float gw = (float)vis * WG_LANE_W;
+    c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
+}
+
+// lanes of the local rows (+ the two boundary rows) from the replay's lane assignment
+static void sh_lane_out(wg_ctx *c) {
+    ShardState &S = c->sh;
+    const uint64_t nl = S.e - S.s, nloc = nl + 2;
+    hipLaunchKernelGGL(k_sh_lane_out, dim3(blocks(nloc)), dim3(T), 0, c->stream, S.s, nl, c->lane_asg.as<const uint32_t>(),
+                       c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>());
+}
+
 // whole-list build on every rank (inputs that the sharded path does not take)
 static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
     ShardState &S = c->sh;
     S.replicated = true;
+    S.replay_pending = false;
     c->n = S.N;
     c->e_refs = S.Etot;
     c->edge_y = nullptr;
@@ -637,8 +665,8 @@ static int sh_geometry_begin(wg_ctx *c, const float *band_g, wg_shard_msg *out) 
     const uint64_t nown = S.xoff[S.rank + 1] - S.xoff[S.rank], xin = S.xoff[S.rank];
     S.step = SH_X6;
     if ((rc = sh_send(c, 16 + (nown + xin) * 16, out)) != WG_OK) return rc;
-    uint32_t hdr[4] = {(uint32_t)nown, (uint32_t)xin, 0, 0};
-    hipLaunchKernelGGL(k_sh_put_head, dim3(1), dim3(1), 0, c->stream, S.msg.as<uint4>(), make_uint4(hdr[0], hdr[1], hdr[2], hdr[3]));
+    hipLaunchKernelGGL(k_sh_x6_head, dim3(1), dim3(1), 0, c->stream, S.msg.as<uint4>(), (uint32_t)nown, (uint32_t)xin,
+                       S.replay_pending ? S.rp_flags : nullptr, S.rp_it, S.rp_scal);
     if (nown + xin)
         hipLaunchKernelGGL(k_sh_pack_ends, dim3(blocks(nown + xin)), dim3(T), 0, c->stream, S.s, S.e,
                            S.xall.as<const WgXEnt>(), S.xoff[S.rank], nown, xin, c->lane_out.as<const uint32_t>(),
@@ -657,6 +685,30 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     std::vector<uint32_t> hdr;
     int rc = read_headers(c, gathered, stride, hdr);
     if (rc != WG_OK) return rc;
+    if (S.replay_pending) {
+        // the speculative X3 replay's words (every rank replayed the same
+        // stream; the OR keeps the decision common): no fixed point or past the
+        // width -> the exact replay, then this step's message again
+        S.replay_pending = false;
+        uint32_t redo = 0;
+        for (int r = 0; r < W; r++) redo |= hdr[4 * r + 2] & 3u;
+        if (redo) {
+            c->spec_redo_lanes++;
+            bool ok = false;
+            if ((rc = wg_lf_replay_lanes(c, sh_range(c), c->n_events, c->lf[LF_EVREC].as<const uint4>(),
+                                         c->lf[LF_AUX].as<const uint32_t>(), c->lane_asg.as<uint32_t>(), &ok)) != WG_OK)
+                return rc;
+            if (!ok) return sh_fallback(c, out);
+            sh_graph_width(c);
+            sh_lane_out(c);
+            S.rt_fresh = true;   // row_top does not depend on the lanes
+            S.rt_band = S.band_g;
+            return sh_geometry_begin(c, S.band_g, out);
+        }
+        const uint32_t w2 = hdr[4 * S.rank + 2], w3 = hdr[4 * S.rank + 3];
+        wg_lf_replay_spec_commit(c, S.rp_it, S.rp_chunk, w3 & 0xffffu, w2 >> 2, w3 >> 16);
+        sh_graph_width(c);
+    }
     std::vector<uint64_t> cnt(W);
     RankCounts nown{};
     for (int r = 0; r < W; r++) {
@@ -1184,20 +1236,32 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
             return rc;
         c->n_events = nev;
         WG_ALLOC(c, c->lane_asg, nl * 4 + 4);
-        bool ok = false;
-        if ((rc = wg_lf_replay_lanes(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
-                                     c->lane_asg.as<uint32_t>(), &ok)) != WG_OK)
-            return rc;
-        if (!ok) return sh_fallback(c, out);        // no fixed point / > 63 slots: same decision on every rank
-        c->lane_path = 0;
-        const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
-        const float gw = (float)vis * WG_LANE_W;
-        c->graph_width = gw > WG_LANE_W ? gw : WG_LANE_W;
         const uint64_t nloc = nl + 2;
         WG_ALLOC(c, c->lane_out, nloc * 4 + 4);
         WG_ALLOC(c, c->color_out, nloc + 4);
-        hipLaunchKernelGGL(k_sh_lane_out, dim3(blocks(nloc)), dim3(T), 0, st, s, nl, c->lane_asg.as<const uint32_t>(),
-                           c->d_flags, c->lane_out.as<uint32_t>(), c->color_out.as<uint8_t>());
+        S.replay_pending = false;
+        if (nev && S.geom_spec_ready && c->spec_replay_shard) {
+            // after a sharded build sized this context: the blind iterations
+            // with no host read, the words checked with the X6 headers
+            ReplayRun run;
+            if ((rc = wg_lf_replay_lanes_spec(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
+                                              c->lane_asg.as<uint32_t>(), run)) != WG_OK)
+                return rc;
+            S.replay_pending = true;
+            S.rp_it = run.it;
+            S.rp_chunk = run.chunk;
+            S.rp_flags = run.flags;
+            S.rp_scal = run.scal;
+        } else {
+            bool ok = false;
+            if ((rc = wg_lf_replay_lanes(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
+                                         c->lane_asg.as<uint32_t>(), &ok)) != WG_OK)
+                return rc;
+            if (!ok) return sh_fallback(c, out);        // no fixed point / > 63 slots: same decision on every rank
+            c->lane_path = 0;
+            sh_graph_width(c);
+        }
+        sh_lane_out(c);
         c->have_layout = true;
         c->layout_gen++;
         return sh_geometry_begin(c, S.build_band, out);   // the default geometry, or build_frame's

@@ -191,6 +191,12 @@ class Engine:
         (results identical; a build that does not hold is redone there)."""
         self._check(lib().wg_set_option(self._ctx, 5, 1 if on else 0))
 
+    def set_shard_spec_replay(self, on: bool):
+        """WG_OPT_SHARD_SPEC_REPLAY: the sharded build's X3 step replays the
+        global lane events without a host read, the replay checked with the X6
+        headers (default on; a replay that misses is redone there)."""
+        self._check(lib().wg_set_option(self._ctx, 7, 1 if on else 0))
+
     # -- layout ----------------------------------------------------------------------
     def build(self, dag=None, commits: abi.Commits | None = None):
         """GraphLayout::build on a wgraph.synth.Dag (host) or a prepared wg_commits."""
