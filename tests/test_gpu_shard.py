@@ -87,10 +87,12 @@ def test_eight_shards_device_transport(tmp_path):
     assert all(r["on_device"] for r in res)
 
 
-def _lockstep(engines, begin):
+def _lockstep(engines, begin, tamper=None):
     """Drive every rank's exchange protocol in one thread: slots written by
     wg_shard_pack_slot in stream order (the device-transport path ShardComm
-    takes over RCCL), gathered by placing the slots side by side."""
+    takes over RCCL), gathered by placing the slots side by side.  tamper(step,
+    heads): may rewrite the gathered heads; when it returns True, rank 0's
+    exchange of them is returned as (rc, error message) instead."""
     import ctypes
 
     import numpy as np
@@ -137,6 +139,11 @@ def _lockstep(engines, begin):
         ph = np.ascontiguousarray(polled[:, 1:3]).view(np.uint32).reshape(W, 4)
         assert np.array_equal(ph, heads), f"round {rounds} step {int(msgs[0].step)} sizes {sizes}: polled {ph.tolist()} heads {heads.tolist()}"
         sz = (ctypes.c_uint64 * W)(*sizes)
+        if tamper is not None and tamper(int(msgs[0].step), heads):
+            heads = np.ascontiguousarray(heads)
+            rc = lib().wg_shard_exchange(engines[0]._ctx, slots.data_ptr() + ShardComm.HDR, stride, sz,
+                                         heads.ctypes.data, ctypes.byref(msgs[0]))
+            return rc, lib().wg_last_error(engines[0]._ctx).decode()
         for r, e in enumerate(engines):
             e._check(lib().wg_shard_exchange(e._ctx, slots.data_ptr() + ShardComm.HDR, stride, sz,
                                               heads.ctypes.data, ctypes.byref(msgs[r])))
@@ -298,6 +305,57 @@ def test_x1_header_guards(bad):
         assert rc == abi.WG_E_INVALID
         msg = lib().wg_last_error(engines[0]._ctx).decode()
         assert ("X1 header" in msg) if bad == "own_range" else ("announces" in msg), msg
+    finally:
+        for e in engines:
+            e.close()
+        del keep
+
+
+def test_x3_crossing_count_guard():
+    """X3's heads carry each rank's own crossing-entry count (X2 leaves the
+    crossing offsets on the device): counts summing past the X1 records are
+    refused with WG_E_INVALID before any launch is sized by them."""
+    import ctypes
+    import sys as _sys
+
+    import numpy as np
+    import torch
+    _sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+    import wgraph
+    from wgraph import abi, lib, synth
+    from wgraph.shard import shard_rows
+
+    d = synth.generate("wide16", 20000, seed=5)
+    dev = torch.device("cuda", 0)
+    keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                   d.parent_oid.reshape(-1), d.flags)]
+    c = abi.Commits()
+    c.n_commits, c.n_parents = d.n, d.e
+    c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep)
+    c.residency = abi.WG_DEVICE
+    ts = torch.cuda.Stream(dev)
+    ts.wait_stream(torch.cuda.current_stream(dev))
+    W = 2
+    engines = [wgraph.Engine(0) for _ in range(W)]
+    seen = []
+    try:
+        with torch.cuda.stream(ts):
+            for e in engines:
+                e.set_stream(ts.cuda_stream)
+            rng = [shard_rows(d.n, W, r) for r in range(W)]
+
+            def tamper(step, heads):
+                if step != 3:   # SH_X3
+                    return False
+                seen.append(heads[:, 3].copy())
+                heads[1, 3] = 0x7FFFFFFF
+                return True
+
+            rc, msg = _lockstep(engines, lambda e, r, m: lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), W, r,
+                                                                                      rng[r][0], rng[r][1], m), tamper)
+        assert seen and int(seen[0][1]) == 0 and int(seen[0][0]) > 0, seen   # rank 0's rows cross into rank 1's
+        assert rc == abi.WG_E_INVALID, (rc, msg)
+        assert "crossing entries" in msg, msg
     finally:
         for e in engines:
             e.close()

@@ -101,6 +101,10 @@ struct LfRange {
     const WgXEnt *xall = nullptr;     // crossing entries of every shard, shard-major
     uint64_t xin_end = 0;             // [0, xin_end): entries of earlier shards
     uint64_t xown_begin = 0, xown_end = 0;   // this shard's own entries
+    // device-resident bounds (the sharded X2 step, before any host read): when
+    // set, xin_end = xown_begin = *xb_dev and xown_end = *xe_dev, and the host
+    // fields above are upper bounds (grids, sizes) with xown_begin = 0
+    const uint32_t *xb_dev = nullptr, *xe_dev = nullptr;
     uint8_t *isfb = nullptr;          // by global ref index: target beyond e and first reference to it
     uint32_t *xsec = nullptr;         // by global ref index: SECALLOC token of such a secondary reference
     // by target row - s: the first (row, parent index) reference to the target

@@ -67,6 +67,11 @@ __device__ __forceinline__ uint32_t token_bits(uint64_t e, uint32_t t0, uint32_t
 
 inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
 
+// crossing-entry bounds, from the device when the range carries them (LfRange::xb_dev)
+__device__ __forceinline__ uint64_t lf_xin_end(const LfRange &R) { return R.xb_dev ? (uint64_t)*R.xb_dev : R.xin_end; }
+__device__ __forceinline__ uint64_t lf_xown_begin(const LfRange &R) { return R.xb_dev ? (uint64_t)*R.xb_dev : R.xown_begin; }
+__device__ __forceinline__ uint64_t lf_xown_end(const LfRange &R) { return R.xe_dev ? (uint64_t)*R.xe_dev : R.xown_end; }
+
 // is ref k (row gi, index kidx, target p) the first in-list reference to p?
 __device__ __forceinline__ bool is_first_ref(const LfRange &R, const unsigned long long *__restrict__ first_ref,
                                              uint64_t gi, uint32_t k, uint32_t kidx, uint64_t p) {
@@ -85,7 +90,7 @@ __global__ void k_lf_refs(LfRange R, unsigned long long *first_ref, uint32_t *fp
 // references from earlier shards into this one
 __global__ void k_lf_xin(LfRange R, unsigned long long *first_ref, uint32_t *fpc) {
     const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= R.xin_end) return;
+    if (x >= lf_xin_end(R)) return;
     const WgXEnt en = R.xall[x];
     if (!(en.kf & WG_XF_FIRST_IN_ROW) || en.p < R.s || en.p >= R.e) return;
     const uint32_t kidx = en.kf & 0xFFFFu;
@@ -95,15 +100,16 @@ __global__ void k_lf_xin(LfRange R, unsigned long long *first_ref, uint32_t *fpc
 
 // own references beyond the shard: first reference to their target?
 __global__ void k_lf_xfirst(LfRange R) {
-    const uint64_t x = R.xown_begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= R.xown_end) return;
+    const uint64_t xe = lf_xown_end(R);
+    const uint64_t x = lf_xown_begin(R) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= xe) return;
     const WgXEnt en = R.xall[x];
     const uint32_t kidx = en.kf & 0xFFFFu;
     const uint32_t k = R.poff[en.c] + kidx;
     if (!(en.kf & WG_XF_FIRST_IN_ROW)) { R.isfb[k] = 0; return; }
     const unsigned long long key = ref_key(en.c, kidx);
     bool first = true;
-    for (uint64_t y = 0; y < R.xown_end && first; y++) {
+    for (uint64_t y = 0; y < xe && first; y++) {
         const WgXEnt o = R.xall[y];
         if (o.p == en.p && (o.kf & WG_XF_FIRST_IN_ROW) && ref_key(o.c, o.kf & 0xFFFFu) < key) first = false;
     }
@@ -176,7 +182,7 @@ __global__ void k_lf_secev_children(LfRange R, const unsigned long long *__restr
 // first references into this shard through a secondary parent of an earlier shard
 __global__ void k_lf_xin_secev(LfRange R, const unsigned long long *__restrict__ first_ref, uint32_t *__restrict__ secev) {
     const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= R.xin_end) return;
+    if (x >= lf_xin_end(R)) return;
     const WgXEnt en = R.xall[x];
     const uint32_t kidx = en.kf & 0xFFFFu;
     if (!(en.kf & WG_XF_FIRST_IN_ROW) || kidx == 0 || en.p < R.s || en.p >= R.e) return;
@@ -185,7 +191,7 @@ __global__ void k_lf_xin_secev(LfRange R, const unsigned long long *__restrict__
 
 __global__ void k_lf_xin_children(LfRange R, const uint32_t *__restrict__ ch_off, uint32_t *ch_fill, uint32_t *ch) {
     const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= R.xin_end) return;
+    if (x >= lf_xin_end(R)) return;
     const WgXEnt en = R.xall[x];
     if ((en.kf & 0xFFFFu) != 0 || en.p < R.s || en.p >= R.e) return;
     const uint64_t pl = en.p - R.s;
@@ -252,14 +258,15 @@ __global__ void k_lf_jump4(uint64_t nl, const uint32_t *__restrict__ in, uint32_
 // token of every own crossing entry: the chain of its child row (first
 // parent) or its SECALLOC event (first reference through a secondary parent)
 __global__ void k_lf_export(LfRange R, const uint32_t *__restrict__ sp, uint32_t *__restrict__ tok) {
-    const uint64_t x = R.xown_begin + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x >= R.xown_end) return;
+    const uint64_t xb = lf_xown_begin(R);
+    const uint64_t x = xb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= lf_xown_end(R)) return;
     const WgXEnt en = R.xall[x];
     const uint32_t kidx = en.kf & 0xFFFFu;
     uint32_t t = WG_TOK_NONE;
     if (kidx == 0) t = sp[en.c - R.s];
     else if ((en.kf & WG_XF_FIRST_IN_ROW) && R.isfb[R.poff[en.c] + kidx]) t = R.xsec[R.poff[en.c] + kidx];
-    tok[x - R.xown_begin] = t;
+    tok[x - xb] = t;
 }
 
 __device__ __forceinline__ uint32_t globalize(uint32_t v, uint32_t ev_base, const uint32_t *__restrict__ xt) {

@@ -477,10 +477,13 @@ __global__ void k_sh_x1_head(uint4 *__restrict__ dst, unsigned long long *__rest
 }
 // X3's header and length from the lane prelude's device words: {events,
 // merge words, not well formed} (no records when not well formed)
+// (+ the rank's own crossing entries [*xb, *xe) and the crossing table's
+// earlier-row flag, both known only on the device at X2)
 __global__ void k_sh_x3_head(uint4 *__restrict__ dst, unsigned long long *__restrict__ len, const uint32_t *__restrict__ flags,
-                             const uint32_t *__restrict__ nev, const uint32_t *__restrict__ naux, uint64_t tok_b) {
-    const uint32_t viol = flags[0], ne = nev[0], na = naux[0];
-    *dst = make_uint4(ne, na, viol, 0u);
+                             const uint32_t *__restrict__ nev, const uint32_t *__restrict__ naux, uint64_t tok_b,
+                             const uint32_t *__restrict__ early, const uint32_t *__restrict__ xb, const uint32_t *__restrict__ xe) {
+    const uint32_t viol = flags[0] | (early[0] ? 2u : 0u), ne = nev[0], na = naux[0];
+    *dst = make_uint4(ne, na, viol, xe[0] - xb[0]);
     *len = 16ull + tok_b + (viol ? 0ull : (unsigned long long)ne * 16ull + (unsigned long long)na * 4ull);
 }
 // transport slot of a message whose length is on the device: header, then the
@@ -1136,18 +1139,12 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         if (L) hipLaunchKernelGGL(k_sh_combine, dim3(blocks(L)), dim3(T), 0, st, SF, L, S.unres.as<const uint32_t>(),
                                   S.xt.as<int32_t>(), S.xtok.as<uint32_t>(), S.flags.as<uint32_t>() + 4);
         WG_HIP(c, wg_exclusive_scan_u32(S.xtok.as<uint32_t>(), S.xtok.as<uint32_t>(), L, c->scan_tmp.p, st));
-        uint64_t xb[20] = {0};
-        {
-            WgFetch it[20];
-            for (int r = 0; r <= W; r++) it[r] = WgFetch{S.xtok.as<uint32_t>() + S.uoffs[r], false};
-            it[W + 1] = WgFetch{S.flags.as<uint32_t>() + 4, false};
-            if ((rc = wg_fetch_n(c, W + 2, it, xb)) != WG_OK) return rc;
-        }
-        if (xb[W + 1]) return sh_fallback(c, out);   // a parent at an earlier row: every rank sees it
-        S.xoff.assign(W + 1, 0);
-        for (int r = 0; r <= W; r++) S.xoff[r] = xb[r];
-        const uint64_t nx = S.xoff[W];
-        WG_ALLOC(c, S.xall, nx * sizeof(WgXEnt) + 16);
+        // No host read: the crossing table is sized by the L records, the
+        // rank's own entries [xtok[uoffs[rank]], xtok[uoffs[rank + 1]]) stay on
+        // the device (LfRange::xb_dev), and their count and the earlier-row
+        // flag travel in X3's header (every rank learns xoff from the heads
+        // and falls back at X3 on the flag)
+        WG_ALLOC(c, S.xall, L * sizeof(WgXEnt) + 16);
         if (L) hipLaunchKernelGGL(k_sh_xbuild, dim3(blocks(L)), dim3(T), 0, st, L, S.unres.as<const uint32_t>(),
                                   S.xt.as<const int32_t>(), S.xtok.as<const uint32_t>(), S.uoffs[S.rank], S.uoffs[S.rank + 1],
                                   c->d_poff, S.E0, S.xall.as<WgXEnt>(), S.prow.as<int32_t>(), S.refx.as<uint32_t>());
@@ -1156,25 +1153,32 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_HIP(c, hipMemsetAsync(S.isfb.p, 0, El + 16, st));
         WG_ALLOC(c, c->lane_scalars, 64);
         WG_HIP(c, hipMemsetAsync(c->lane_scalars.p, 0, 64, st));
+        S.xoff.assign(W + 1, 0);   // known from X3's heads
         LfRange R = sh_range(c);
+        R.xin_end = L;          // bounds; the kernels read the device values
+        R.xown_begin = 0;
+        R.xown_end = L;
+        R.xb_dev = S.xtok.as<const uint32_t>() + S.uoffs[S.rank];
+        R.xe_dev = S.xtok.as<const uint32_t>() + S.uoffs[S.rank + 1];
         wg_stage_begin(c, "lanes");
-        // No host read: the message (header, tokens, then the event records
-        // and merge-token lists) is bounded by the rows' references (a row
-        // makes at most max(1, parents) events; merge lists hold at most
-        // 2 (n + E) + 16 words) and its header and length are written on the
-        // device, as X1's are; every rank learns the counts from the gathered
-        // heads.  Not well formed: no records, every rank falls back at X3.
+        // The message (header, tokens, then the event records and merge-token
+        // lists) is bounded by the rows' references (a row makes at most
+        // max(1, parents) events; merge lists hold at most 2 (n + E) + 16
+        // words) and by the L records (tokens), and its header and length are
+        // written on the device, as X1's are; every rank learns the counts from
+        // the gathered heads.  Not well formed: no records, every rank falls
+        // back at X3.
         if ((rc = wg_lf_refs(c, R, false)) != WG_OK) return rc;
         if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
         wg_stage_end(c);
-        const uint64_t nown = R.xown_end - R.xown_begin;
-        const uint64_t tok_b = (nown * 4 + 15) & ~15ull;          // records start 16-byte aligned
+        const uint64_t tok_b = (L * 4 + 15) & ~15ull;          // records start 16-byte aligned (same on every rank)
         const uint64_t ev_cap = nl + El, aux_cap = 2 * (nl + El) + 16;
         S.step = SH_X3;
         if ((rc = sh_send_dev(c, 16 + tok_b + ev_cap * 16 + aux_cap * 4, out)) != WG_OK) return rc;
         hipLaunchKernelGGL(k_sh_x3_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), S.msg_len.as<unsigned long long>(),
                            c->lf[LF_FLAGS].as<const uint32_t>(), c->lf[LF_EVOFF].as<const uint32_t>() + nl,
-                           c->lf[LF_AUXOFF].as<const uint32_t>() + nl, tok_b);
+                           c->lf[LF_AUXOFF].as<const uint32_t>() + nl, tok_b, S.flags.as<const uint32_t>() + 4, R.xb_dev,
+                           R.xe_dev);
         uint8_t *m = S.msg.as<uint8_t>() + 16;
         if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(m))) != WG_OK) return rc;
         // the event records travel in the same message, with shard-local tokens
@@ -1186,16 +1190,21 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         if ((rc = read_headers(c, gathered, stride, hdr)) != WG_OK) return rc;
         S.evoff.assign(W + 1, 0);
         S.auxoff.assign(W + 1, 0);
+        S.xoff.assign(W + 1, 0);
         bool bad = false;
+        const uint64_t L = S.uoffs[W], tok_b = (L * 4 + 15) & ~15ull;
         for (int r = 0; r < W; r++) {
             S.evoff[r + 1] = S.evoff[r] + hdr[4 * r];
             S.auxoff[r + 1] = S.auxoff[r] + hdr[4 * r + 1];
-            bad |= hdr[4 * r + 2] != 0;
+            S.xoff[r + 1] = S.xoff[r] + hdr[4 * r + 3];   // own crossing entries (X2 left them on the device)
+            bad |= hdr[4 * r + 2] != 0;                   // not well formed, or a parent at an earlier row
         }
+        if (S.xoff[W] > L)
+            return wg_fail(c, WG_E_INVALID, "X3 headers: %llu crossing entries of %llu records",
+                           (unsigned long long)S.xoff[W], (unsigned long long)L);
         if (bad || S.evoff[W] >= (1ull << 30)) return sh_fallback(c, out);
         const uint64_t nx = S.xoff[W];
         for (int r = 0; r < W; r++) {
-            const uint64_t tok_b = ((S.xoff[r + 1] - S.xoff[r]) * 4 + 15) & ~15ull;
             if ((rc = check_len(c, r, 16 + tok_b + (uint64_t)hdr[4 * r] * 16 + (uint64_t)hdr[4 * r + 1] * 4,
                                 "X3 tokens and event records")) != WG_OK)
                 return rc;
@@ -1216,7 +1225,6 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
             for (int r = 0; r < W; r++) {
                 const uint64_t n = S.xoff[r + 1] - S.xoff[r];
                 const uint64_t ne_r = S.evoff[r + 1] - S.evoff[r], na_r = S.auxoff[r + 1] - S.auxoff[r];
-                const uint64_t tok_b = (n * 4 + 15) & ~15ull;
                 const uint8_t *src = (const uint8_t *)gathered + r * stride + 16;
                 cp.add(S.xtok.as<uint32_t>() + S.xoff[r], src, n * 4);
                 cp.add(evrec.as<uint4>() + S.evoff[r], src + tok_b, ne_r * 16);
