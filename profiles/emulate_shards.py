@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--stage-events", action="store_true", help="record every stage's HIP events (stages_ms)")
     ap.add_argument("--no-defer", action="store_true", help="validate each speculative pass before the call returns")
+    ap.add_argument("--replay", default=None, help="CHUNK:WARM: fixed replay chunk / warm-up (options 2 and 6)")
     ap.add_argument("--no-spec-replay", action="store_true", help="WG_OPT_SHARD_SPEC_REPLAY 0: X3 checks its replay")
     ap.add_argument("--two-calls", action="store_true",
                     help="shard_build + shard_geometry (5 exchanges) instead of shard_build_frame (4)")
@@ -154,6 +155,10 @@ def main():
         e.set_stream(s.cuda_stream)
         e.set_defer_validation(not args.no_defer)   # as bench.py
         e.set_shard_spec_replay(not args.no_spec_replay)
+        if args.replay:
+            ch, wm = (int(x) for x in args.replay.split(":"))
+            e._check(wgraph.lib().wg_set_option(e._ctx, 2, ch))
+            e._check(wgraph.lib().wg_set_option(e._ctx, 6, wm))
         engines.append(e)
         streams.append(s)
 

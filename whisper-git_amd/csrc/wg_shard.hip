@@ -916,6 +916,7 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
     hipStream_t st = c->stream;
     S.rt_fresh = false;
     S.build_band = nullptr;
+    S.replay_pending = false;
     if (band && N) {   // build_frame: the bands, on the device (a host band copied before the side fork)
         if (band_res == WG_HOST) {
             WG_ALLOC(c, S.band_host, N * 4 + 4);
