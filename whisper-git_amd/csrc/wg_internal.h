@@ -207,6 +207,7 @@ struct ReplayRun {
 constexpr uint32_t WG_REPLAY_CHUNK_SHORT = 128, WG_REPLAY_CHUNK_LONG = 512;
 constexpr uint32_t WG_REPLAY_SHORT_MAX_FP = 6;   // a short-chunk replay needing more iterations: long chunks next
 constexpr uint32_t WG_REPLAY_SWITCH_IT = 12;     // exact replay: iterations at the short chunk before the switch
+constexpr uint64_t WG_REPLAY_WIDE_EVENTS = 131072;   // 1024 short chunks: above, short chunks of twice the length
 
 // small device -> host reads (wg_api.hip): one tiny kernel writes the values
 // into mapped pinned host memory, then the stream is synchronised — instead of
@@ -292,6 +293,11 @@ struct wg_ctx {
         if (!replay_long) {   // (short lists: 64-event chunks — random13 100k 0.093 -> 0.085 ms, r03l / r03q)
             *chunk = n_events >= 24576 ? WG_REPLAY_CHUNK_SHORT : WG_REPLAY_CHUNK_SHORT / 2;
             *warm = n_events >= 24576 ? 512u : 256u;
+            // More chunks than SIMDs (a sharded build's global replay: 368k
+            // events at 8 x 1M rows): iteration 1 turns throughput-bound on
+            // the scalar units, and the warm-up is paid per chunk — double
+            // chunks halve it (r03 emulation: 235 -> 207 us per step)
+            if (n_events >= WG_REPLAY_WIDE_EVENTS) *chunk = 2 * WG_REPLAY_CHUNK_SHORT;
         }
         else { *chunk = WG_REPLAY_CHUNK_LONG; *warm = 0; }
     }
