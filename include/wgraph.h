@@ -30,7 +30,9 @@ extern "C" {
  * first build exchange of a multi-rank build always is; ask
  * wg_shard_msg_bytes); wg_shard_pack_slot / wg_shard_slot_heads take caps
  * and strides that are multiples of 16 only; wg_shard_exchange fails when a
- * message header announces more than that rank's sizes[] entry. */
+ * message header announces more than that rank's sizes[] entry; an
+ * exchange step may be sent again (msg.step repeats on every rank alike:
+ * WG_OPT_SHARD_SPEC_REPLAY), so transports loop until msg.done. */
 #define WGRAPH_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
