@@ -441,3 +441,69 @@ def test_spec_replay_sequence(spec):
         for e in engines:
             e.close()
         stream_ctx.__exit__(None, None, None)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_earlier_row_parent_across_shards(world):
+    """A parent at an earlier row in another shard (clock skew: the
+    reference leaks the waiter, commit_graph.rs:441-446, and skips the edge,
+    :526-528).  The crossing table's earlier-row flag is raised on the device
+    at X2 and travels in X3's header: every rank falls back to the whole-list
+    build at X3 (mode 2) with the oracle's lanes, geometry and vertices."""
+    import ctypes
+    import sys as _sys
+
+    import numpy as np
+    import torch
+    _sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+    _sys.path.insert(0, ROOT)
+    import wgraph
+    from oracle import oracle_c
+    from wgraph import abi, lib, synth
+    from wgraph.shard import shard_rows
+
+    d = synth.generate("wide16", 24000, seed=17)
+    r_late = shard_rows(d.n, world, world - 1)[0] + 100      # a row of the last shard
+    pa = int(d.parent_off[r_late])
+    assert int(d.parent_off[r_late + 1]) > pa
+    d.parent_oid[pa] = d.oid[10]                            # its first parent: row 10 (shard 0, earlier)
+    dev = torch.device("cuda", 0)
+    keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                   d.parent_oid.reshape(-1), d.flags, d.band)]
+    c = abi.Commits()
+    c.n_commits, c.n_parents = d.n, d.e
+    c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
+    c.residency = abi.WG_DEVICE
+    ts = torch.cuda.Stream(dev)
+    ts.wait_stream(torch.cuda.current_stream(dev))
+    stream_ctx = torch.cuda.stream(ts)
+    stream_ctx.__enter__()
+    engines = [wgraph.Engine(0) for _ in range(world)]
+    o = oracle_c.OracleLayout(d)
+    try:
+        for e in engines:
+            e.set_stream(ts.cuda_stream)
+        rng = [shard_rows(d.n, world, r) for r in range(world)]
+        rounds = _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
+            e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
+        assert rounds == 3, rounds   # X1, X2, X3 (the fallback decided there)
+        og = o.row_geometry(d.band)
+        vo = og["vert_off"].astype(np.int64)
+        for r, e in enumerate(engines):
+            s, t = rng[r]
+            assert int(e.debug_counters()[5]) == 2, "whole-list fallback expected"
+            lane, color = e.lanes()
+            assert lane.tobytes() == o.lane[s:t].tobytes() and color.tobytes() == o.color[s:t].tobytes(), f"rank {r}"
+            assert e.layout_summary().max_lane == o.max_lane
+            g = e.geometry()
+            assert g["row_top"].tobytes() == og["row_top"][s:t + 1].tobytes(), f"rank {r}"
+            assert g["vert"].tobytes() == og["vert"][vo[s]:vo[t]].tobytes(), f"rank {r}"
+            e.emit_vertices(s, t, selected=s + 3)
+            ov, _ = o.emit_vertices(s, t, selected=s + 3)
+            assert e.vertex_summary().checksum == oracle_c.vertex_checksum(ov), f"rank {r} vertices"
+    finally:
+        o.close()
+        for e in engines:
+            e.close()
+        stream_ctx.__exit__(None, None, None)
+        del keep
