@@ -511,7 +511,9 @@ int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
  * iterations of the lane-event replay, [4] lane events, [5] build mode
  * (0 single, 1 row-sharded, 2 row-sharded request built whole), [6]
  * speculative builds (one host read per build) on this context, [7] of
- * which the lanes and [8] the geometry were redone by the exact stages.  */
+ * which the lanes and [8] the geometry were redone by the exact stages
+ * (a sharded build's blind global replay redone at X6 counts in [7]), [9]
+ * sharded builds whose global lane replay ran blind (WG_OPT_SHARD_SPEC_REPLAY). */
 int wg_debug_counters(wg_ctx *ctx, uint32_t *out, int n);
 
 #ifdef __cplusplus

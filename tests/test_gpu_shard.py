@@ -507,3 +507,78 @@ def test_earlier_row_parent_across_shards(world):
             e.close()
         stream_ctx.__exit__(None, None, None)
         del keep
+
+
+def test_spec_replay_mixed_history():
+    """The speculative replay is a decision every rank takes alike: each X3
+    header says whether its rank may speculate and all ranks replay blind
+    only when every one may.  A rank whose context is fresh (no earlier
+    sharded build) next to warmed ones: every rank replays exactly at X3,
+    four exchange rounds, the oracle's results; the next build speculates."""
+    import ctypes
+    import sys as _sys
+
+    import numpy as np
+    import torch
+    _sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+    _sys.path.insert(0, ROOT)
+    import wgraph
+    from oracle import oracle_c
+    from wgraph import abi, lib, synth
+    from wgraph.shard import shard_rows
+
+    world = 3
+    d = synth.generate("random13", 30000, seed=9)
+    dev = torch.device("cuda", 0)
+    keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                   d.parent_oid.reshape(-1), d.flags, d.band)]
+    c = abi.Commits()
+    c.n_commits, c.n_parents = d.n, d.e
+    c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
+    c.residency = abi.WG_DEVICE
+    ts = torch.cuda.Stream(dev)
+    ts.wait_stream(torch.cuda.current_stream(dev))
+    stream_ctx = torch.cuda.stream(ts)
+    stream_ctx.__enter__()
+    engines = [wgraph.Engine(0) for _ in range(world)]
+    o = oracle_c.OracleLayout(d)
+    rng = [shard_rows(d.n, world, r) for r in range(world)]
+
+    def build():
+        return _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
+            e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
+
+    def check(tag):
+        og = o.row_geometry(d.band)
+        vo = og["vert_off"].astype(np.int64)
+        for r, e in enumerate(engines):
+            s, t = rng[r]
+            assert int(e.debug_counters()[5]) == 1, f"{tag}: sharded path expected"
+            lane, color = e.lanes()
+            assert lane.tobytes() == o.lane[s:t].tobytes() and color.tobytes() == o.color[s:t].tobytes(), f"{tag} {r}"
+            g = e.geometry()
+            assert g["vert"].tobytes() == og["vert"][vo[s]:vo[t]].tobytes(), f"{tag} rank {r}"
+
+    try:
+        for e in engines:
+            e.set_stream(ts.cuda_stream)
+        assert build() == 4
+        assert build() == 4          # warmed: speculative (the same list: no redo)
+        check("warm")
+        engines[1].close()
+        engines[1] = wgraph.Engine(0)   # a fresh context beside two warmed ones
+        engines[1].set_stream(ts.cuda_stream)
+        warm = [int(e.debug_counters()[9]) for e in (engines[0], engines[2])]
+        assert min(warm) >= 1, warm   # the second build speculated
+        assert build() == 4          # exact on every rank (no X6 words to disagree on)
+        assert [int(e.debug_counters()[9]) for e in (engines[0], engines[2])] == warm
+        check("mixed")
+        assert build() == 4
+        assert [int(e.debug_counters()[9]) for e in engines] == [warm[0] + 1, 1, warm[1] + 1]
+        check("after")
+    finally:
+        o.close()
+        for e in engines:
+            e.close()
+        stream_ctx.__exit__(None, None, None)
+        del keep

@@ -992,6 +992,7 @@ int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
     if (n > 6) out[6] = c->spec_builds;
     if (n > 7) out[7] = c->spec_redo_lanes;
     if (n > 8) out[8] = c->spec_redo_geom;
+    if (n > 9) out[9] = c->spec_replays_shard;
     return WG_OK;
 }
 

@@ -338,6 +338,7 @@ struct wg_ctx {
     PendingBuild pend;
     uint64_t spec_nsuper_grid = 0;   // the speculative geometry pass's curve-record grid (its capacity)
     uint32_t spec_builds = 0, spec_redo_lanes = 0, spec_redo_geom = 0;   // speculative builds, of which lanes / geometry redone
+    uint32_t spec_replays_shard = 0;   // sharded builds whose global replay ran blind (WG_OPT_SHARD_SPEC_REPLAY)
     // edges
     DevBuf edge_cnt;        // uint32 [N+1] -> edge_off after scan
     DevBuf edges;           // wg_edge [n_edges]

@@ -481,9 +481,10 @@ __global__ void k_sh_x1_head(uint4 *__restrict__ dst, unsigned long long *__rest
 // earlier-row flag, both known only on the device at X2)
 __global__ void k_sh_x3_head(uint4 *__restrict__ dst, unsigned long long *__restrict__ len, const uint32_t *__restrict__ flags,
                              const uint32_t *__restrict__ nev, const uint32_t *__restrict__ naux, uint64_t tok_b,
-                             const uint32_t *__restrict__ early, const uint32_t *__restrict__ xb, const uint32_t *__restrict__ xe) {
-    const uint32_t viol = flags[0] | (early[0] ? 2u : 0u), ne = nev[0], na = naux[0];
-    *dst = make_uint4(ne, na, viol, xe[0] - xb[0]);
+                             const uint32_t *__restrict__ early, const uint32_t *__restrict__ xb, const uint32_t *__restrict__ xe,
+                             uint32_t spec_bit) {
+    const uint32_t viol = (flags[0] ? 1u : 0u) | (early[0] ? 2u : 0u), ne = nev[0], na = naux[0];
+    *dst = make_uint4(ne, na, viol | spec_bit, xe[0] - xb[0]);
     *len = 16ull + tok_b + (viol ? 0ull : (unsigned long long)ne * 16ull + (unsigned long long)na * 4ull);
 }
 // transport slot of a message whose length is on the device: header, then the
@@ -1179,7 +1180,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         hipLaunchKernelGGL(k_sh_x3_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), S.msg_len.as<unsigned long long>(),
                            c->lf[LF_FLAGS].as<const uint32_t>(), c->lf[LF_EVOFF].as<const uint32_t>() + nl,
                            c->lf[LF_AUXOFF].as<const uint32_t>() + nl, tok_b, S.flags.as<const uint32_t>() + 4, R.xb_dev,
-                           R.xe_dev);
+                           R.xe_dev, (S.geom_spec_ready && c->spec_replay_shard) ? 4u : 0u);
         uint8_t *m = S.msg.as<uint8_t>() + 16;
         if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(m))) != WG_OK) return rc;
         // the event records travel in the same message, with shard-local tokens
@@ -1192,13 +1193,14 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         S.evoff.assign(W + 1, 0);
         S.auxoff.assign(W + 1, 0);
         S.xoff.assign(W + 1, 0);
-        bool bad = false;
+        bool bad = false, spec_all = true;
         const uint64_t L = S.uoffs[W], tok_b = (L * 4 + 15) & ~15ull;
         for (int r = 0; r < W; r++) {
             S.evoff[r + 1] = S.evoff[r] + hdr[4 * r];
             S.auxoff[r + 1] = S.auxoff[r] + hdr[4 * r + 1];
             S.xoff[r + 1] = S.xoff[r] + hdr[4 * r + 3];   // own crossing entries (X2 left them on the device)
-            bad |= hdr[4 * r + 2] != 0;                   // not well formed, or a parent at an earlier row
+            bad |= (hdr[4 * r + 2] & 3u) != 0;            // not well formed, or a parent at an earlier row
+            spec_all &= (hdr[4 * r + 2] & 4u) != 0;       // every rank may replay speculatively
         }
         if (S.xoff[W] > L)
             return wg_fail(c, WG_E_INVALID, "X3 headers: %llu crossing entries of %llu records",
@@ -1249,14 +1251,16 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         WG_ALLOC(c, c->lane_out, nloc * 4 + 4);
         WG_ALLOC(c, c->color_out, nloc + 4);
         S.replay_pending = false;
-        if (nev && S.geom_spec_ready && c->spec_replay_shard) {
-            // after a sharded build sized this context: the blind iterations
-            // with no host read, the words checked with the X6 headers
+        if (nev && spec_all) {
+            // after a sharded build sized every rank's context (a decision all
+            // ranks take alike, from the X3 heads): the blind iterations with
+            // no host read, the words checked with the X6 headers
             ReplayRun run;
             if ((rc = wg_lf_replay_lanes_spec(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
                                               c->lane_asg.as<uint32_t>(), run)) != WG_OK)
                 return rc;
             S.replay_pending = true;
+            c->spec_replays_shard++;
             S.rp_it = run.it;
             S.rp_chunk = run.chunk;
             S.rp_flags = run.flags;
