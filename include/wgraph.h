@@ -230,6 +230,12 @@ int         wg_synchronize(wg_ctx *ctx);
  * point is redone exactly at X6 (whose message is then sent again: one more
  * exchange round, same results).  0 = the replay is checked before X3 returns. */
 #define WG_OPT_SHARD_SPEC_REPLAY 7
+/* WG_OPT_REPLAY_MODE: how the lane events are replayed.  0 (default) = auto:
+ * the chunked fixed point, and for lists on which it needs more iterations
+ * than an exact single-wave pass costs (parents at earlier rows, long-lived
+ * lanes) that pass; 1 = always the chunked fixed point; 2 = always the
+ * single-wave pass.  Speed only, never results. */
+#define WG_OPT_REPLAY_MODE 8
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------
@@ -513,7 +519,9 @@ int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
  * speculative builds (one host read per build) on this context, [7] of
  * which the lanes and [8] the geometry were redone by the exact stages
  * (a sharded build's blind global replay redone at X6 counts in [7]), [9]
- * sharded builds whose global lane replay ran blind (WG_OPT_SHARD_SPEC_REPLAY). */
+ * sharded builds whose global lane replay ran blind (WG_OPT_SHARD_SPEC_REPLAY),
+ * [10] 1 if the last lane replay was the single-wave serial pass
+ * (WG_OPT_REPLAY_MODE). */
 int wg_debug_counters(wg_ctx *ctx, uint32_t *out, int n);
 
 #ifdef __cplusplus

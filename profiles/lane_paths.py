@@ -2,10 +2,12 @@
 the serial walk at 1M rows first").
 
 For each list: a fresh engine builds it `steps` times on the parallel
-(event-compressed) path and `steps` times forced onto the general single-wave
-walk (WG_OPT_LANE_PATH = 1); prints one JSON line per (list, path) with the
-mean ms of the "lanes" stage and of the whole build, the path taken and the
-slot count.  python3 profiles/lane_paths.py [steps]
+(event-compressed) path — the replay in auto mode, held on the chunked fixed
+point, and held on the single-wave serial pass (WG_OPT_REPLAY_MODE 0 / 1 / 2)
+— and `steps` times forced onto the general single-wave walk
+(WG_OPT_LANE_PATH = 1); prints one JSON line per (list, path, replay) with
+the mean ms of the "lanes" stage and of the whole build, the path taken, the
+replay used and the slot count.  python3 profiles/lane_paths.py [steps] [lists]
 """
 import json
 import os
@@ -24,11 +26,17 @@ def main():
     import wgraph
     from wgraph import synth
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     for kind, n, over in LISTS:
+        if only and kind not in only:
+            continue
         d = synth.generate(kind, n, **over)
-        for general in (False, True):
+        for general, mode in ((False, 0), (False, 1), (False, 2), (True, 0)):
+            if general and only:
+                continue
             eng = wgraph.Engine(0)
             eng.set_lane_path(general)
+            eng.set_replay_mode(mode)
             eng.build(d)                      # sizes the buffers (cold build, not timed here)
             eng.synchronize()
             eng.enable_timing(True, reserve=64 * (steps + 1))
@@ -42,7 +50,8 @@ def main():
                 st[name] = st.get(name, 0.0) + ms / steps
             s = eng.layout_summary()
             dc = eng.debug_counters()
-            print(json.dumps({"list": kind, "rows": d.n, "forced_general": general, "lane_path": int(s.lane_path),
+            print(json.dumps({"list": kind, "rows": d.n, "forced_general": general, "replay_mode": mode,
+                              "serial": int(dc[10]), "lane_path": int(s.lane_path),
                               "replay_iterations": int(dc[3]), "events": int(dc[4]),
                               "n_slots": int(s.n_slots), "max_lane": int(s.max_lane),
                               "lanes_ms": round(st.get("lanes", 0.0), 4), "build_wall_ms": round(wall, 4),

@@ -6,8 +6,14 @@ took no scalar special event, scalar special events, of which merges with
 more than two waiters, and the mean cycles per chunk spent in total / in the
 scalar loop / in those merges.
 
-usage: WGRAPH_LIB=build/rp.so python3 profiles/replay_profile.py [kind rows]...
-(build/rp.so: hipcc ... -DWG_REPLAY_PROFILE -shared -o build/rp.so whisper-git_amd/csrc/*.hip)
+usage: WGRAPH_LIB=profiles/librp_profile.so python3 profiles/replay_profile.py [kind rows]...
+(profiles/librp_profile.so: hipcc ... -DWG_REPLAY_PROFILE -shared whisper-git_amd/csrc/*.hip)
+
+The engine is held on the chunked replay (WG_OPT_REPLAY_MODE 1) at the long
+chunk the auto mode would reach; the counters are per iteration modulo 64
+(a replay of more iterations adds up in the same rows), so the totals over
+all rows are what a long replay is judged by: events per chunk, scalar events
+and cycles per replayed event, iterations (debug counter [3]).
 """
 import ctypes
 import json
@@ -39,6 +45,7 @@ def main():
         c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep)
         c.residency = abi.WG_DEVICE
         eng = wgraph.Engine(0)
+        eng.set_replay_mode(1)
         for _ in range(3):
             eng.build(commits=c)
         eng.synchronize()
@@ -57,8 +64,18 @@ def main():
                          "scalar_events": int(a[it, 3]), "merges_gt2": int(a[it, 4]),
                          "cycles_per_chunk": int(a[it, 5]) // ch, "scalar_cycles_per_chunk": int(a[it, 6]) // ch,
                          "merge_cycles_per_chunk": int(a[it, 7]) // ch})
-        out[f"{kind}/{n}"] = {"events": int(eng.debug_counters()[4]), "iterations": rows}
-        print(kind, n, json.dumps(out[f"{kind}/{n}"], indent=1), flush=True)
+        dc = eng.debug_counters()
+        tot = a.sum(axis=0)
+        ev = int(dc[4])
+        out[f"{kind}/{n}"] = rec = {
+            "list": kind, "rows": int(n), "events": ev, "replay_iterations": int(dc[3]), "n_slots": int(eng.layout_summary().n_slots),
+            "chunks_run": int(tot[0]), "events_per_chunk": round(ev / max(1, int(rows[0]["chunks"]) if rows else 1), 1),
+            "batches": int(tot[1]), "batches_without_scalar_events": int(tot[2]),
+            "scalar_events": int(tot[3]), "merges_gt2": int(tot[4]),
+            "cycles_total": int(tot[5]), "scalar_loop_cycles": int(tot[6]), "merge_cycles": int(tot[7]),
+            "cycles_per_scalar_event": round(int(tot[6]) / max(1, int(tot[3])), 1),
+            "iterations_first64": rows}
+        print(json.dumps(rec), flush=True)
         eng.close()
         del keep
 

@@ -107,3 +107,75 @@ def test_speculative_builds_across_widths(engine):
             o.close()
     c1 = engine.debug_counters()
     assert int(c1[6]) > int(c0[6]), "no speculative build in the sequence"
+
+
+# ---- the single-wave serial replay (wg_lanes_serial.hip, WG_OPT_REPLAY_MODE) ----
+SERIAL_CASES = [
+    ("wide16", 200_000, {}), ("random13", 100_000, {}), ("linux", 200_000, {}), ("skew", 300_000, {}),
+    ("linuxwide", 200_000, {}),                          # 160 slots: 4-word occupancy
+    ("linux", 100_000, {"max_lines": 400}),              # > 255 slots: 16 words
+    ("anomaly", 10_000, {"p_dup_oid": 0.0}),             # skewed / self / repeated / outside parents, octopus merges
+    ("linear", 5_000, {}),
+]
+
+
+@pytest.mark.parametrize("kind,n,over", SERIAL_CASES, ids=[f"{k}-{n}" for k, n, _ in SERIAL_CASES])
+def test_serial_replay_is_exact(kind, n, over):
+    """WG_OPT_REPLAY_MODE 2: the exact build and the speculative build after it
+    both replay serially and equal the oracle (lanes, colours, edges, max_lane,
+    slot count)."""
+    import wgraph
+    d = synth.generate(kind, n, seed=97, **over)
+    o = _oracle(d)
+    eng = wgraph.Engine(0)
+    try:
+        eng.set_replay_mode(2)
+        for _ in range(2):
+            eng.build(d)
+            _check_lanes(eng, d, o)
+            assert int(eng.debug_counters()[10]) == 1, "not the serial replay"
+    finally:
+        eng.close()
+        o.close()
+
+
+def test_auto_replay_mode_picks_by_list_shape():
+    """Auto mode: the skewed list (parents at earlier rows leak slots for good,
+    so the chunked fixed point needs about one iteration per chunk) moves to
+    the serial replay; wide16 (forgets a wrong guess within a chunk) stays on
+    the chunked one; both bit-exact at every build."""
+    import wgraph
+    for kind, n, want in (("skew", 1_000_000, 1), ("wide16", 1_000_000, 0)):
+        d = synth.generate(kind, n)
+        o = _oracle(d)
+        eng = wgraph.Engine(0)
+        try:
+            for _ in range(3):
+                eng.build(d)
+                _check_lanes(eng, d, o)
+            assert int(eng.debug_counters()[10]) == want, kind
+        finally:
+            eng.close()
+            o.close()
+
+
+def test_replay_mode_follows_the_list_on_one_context():
+    """One context (a repository tab) alternates list shapes: every build is
+    exact whatever replay the context last chose, and a list of a very
+    different length starts the auto choice over (replay_long
+    never cleared)."""
+    import wgraph
+    eng = wgraph.Engine(0)
+    try:
+        seq = [("skew", 200_000), ("skew", 200_000), ("wide16", 200_000), ("random13", 50_000), ("skew", 200_000),
+               ("wide16", 200_000), ("linuxwide", 100_000), ("random13", 50_000)]
+        for kind, n in seq:
+            d = synth.generate(kind, n)
+            o = _oracle(d)
+            try:
+                eng.build(d)
+                _check_lanes(eng, d, o)
+            finally:
+                o.close()
+    finally:
+        eng.close()

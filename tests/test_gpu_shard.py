@@ -582,3 +582,68 @@ def test_spec_replay_mixed_history():
             e.close()
         stream_ctx.__exit__(None, None, None)
         del keep
+
+
+def test_high_fan_in_root_in_a_small_last_shard():
+    """a root with 300 first-parent children in a last
+    shard of 20 rows.  Every reference into it arrives from earlier shards, so
+    its merge list (301 tokens) far exceeds the 2 (n + E) + 16 words the last
+    rank's X3 message used to hold; the message is now sized with the crossing
+    records (k_sh_x3_head refuses counts past it), and every rank's lanes
+    equal the oracle's (300+ concurrent slots)."""
+    import ctypes
+    import sys as _sys
+
+    import numpy as np
+    import torch
+    _sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+    _sys.path.insert(0, ROOT)
+    import wgraph
+    from oracle import oracle_c
+    from wgraph import abi, lib
+    from wgraph.synth import Dag
+
+    n, fan = 1200, 300
+    rng_ = np.random.default_rng(5)
+    oid = rng_.integers(0, 256, (n, 20), dtype=np.uint8)
+    root = n - 1
+    par = []
+    poff = [0]
+    for i in range(n - 1):
+        par.append(root if i < fan or i == n - 2 else i + 1)   # rows < fan: children of the root; the rest a chain into it
+        poff.append(len(par))
+    poff.append(len(par))
+    d = Dag(oid, (1_700_000_000 - 60 * np.arange(n)).astype(np.int64), np.array(poff, np.uint32),
+            oid[np.array(par)].copy(), np.zeros(n, np.uint8), np.zeros(n, np.float32))
+    ranges = [(0, 400), (400, 800), (800, n - 20), (n - 20, n)]
+    world = len(ranges)
+    dev = torch.device("cuda", 0)
+    keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                   d.parent_oid.reshape(-1), d.flags, d.band)]
+    c = abi.Commits()
+    c.n_commits, c.n_parents = d.n, d.e
+    c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep[:5])
+    c.residency = abi.WG_DEVICE
+    ts = torch.cuda.Stream(dev)
+    ts.wait_stream(torch.cuda.current_stream(dev))
+    stream_ctx = torch.cuda.stream(ts)
+    stream_ctx.__enter__()
+    engines = [wgraph.Engine(0) for _ in range(world)]
+    o = oracle_c.OracleLayout(d)
+    try:
+        assert o.n_slots > fan
+        for e in engines:
+            e.set_stream(ts.cuda_stream)
+        _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
+            e._ctx, ctypes.byref(c), world, r, ranges[r][0], ranges[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
+        for r, e in enumerate(engines):
+            s, t = ranges[r]
+            lane, color = e.lanes()
+            assert lane.tobytes() == o.lane[s:t].tobytes() and color.tobytes() == o.color[s:t].tobytes(), f"rank {r}"
+            assert e.layout_summary().max_lane == o.max_lane
+    finally:
+        o.close()
+        for e in engines:
+            e.close()
+        stream_ctx.__exit__(None, None, None)
+        del keep

@@ -456,6 +456,10 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
     case WG_OPT_SHARD_SPEC_REPLAY:
         c->spec_replay_shard = value != 0;
         return WG_OK;
+    case WG_OPT_REPLAY_MODE:
+        if (value < 0 || value > 2) return wg_fail(c, WG_E_INVALID, "replay mode must be 0 (auto), 1 (chunked) or 2 (serial)");
+        c->replay_mode = (uint32_t)value;
+        return WG_OK;
     case WG_OPT_SWEEP_REG:
         if (value < 0 || value > 512) return wg_fail(c, WG_E_INVALID, "sweep register capacity must be 0..512");
         c->sweep_reg_cap = (uint32_t)value;
@@ -993,6 +997,7 @@ int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
     if (n > 7) out[7] = c->spec_redo_lanes;
     if (n > 8) out[8] = c->spec_redo_geom;
     if (n > 9) out[9] = c->spec_replays_shard;
+    if (n > 10) out[10] = c->last_serial ? 1u : 0u;
     return WG_OK;
 }
 

@@ -181,7 +181,7 @@ struct FontSlot {
 // workspace slots in wg_ctx::lf (wg_lanes_fast.hip; the sharded build reuses LF_EVREC / LF_AUX for the
 // gathered event records)
 enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_CH, LF_SPA, LF_SPB, LF_EVREC,
-       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_LFIRST, LF_COUNT };
+       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_LFIRST, LF_SERREC, LF_COUNT };
 
 // event replay to a fixed point (wg_lanes_replay.hip)
 struct ReplayRun {
@@ -198,6 +198,8 @@ struct ReplayRun {
     const uint32_t *gate = nullptr;      // speculative build: nonzero = not well formed, replay nothing
     uint32_t switch_it = 0;              // exact replay at a short chunk: still moving at this iteration ->
     bool switched = false;               // stop; the caller replays at WG_REPLAY_CHUNK_LONG (wg_replay_resume)
+    uint32_t serial_it = 0;              // exact replay at the long chunk: still moving at this iteration ->
+    bool to_serial = false;              // stop; the caller replays serially (wg_replay_resume)
 };
 // The replay's chunk lengths (events).  Short chunks make iteration 1 short
 // (its chunks replay serially, one wave each) and suit lists whose greedy
@@ -301,6 +303,32 @@ struct wg_ctx {
         }
         else { *chunk = WG_REPLAY_CHUNK_LONG; *warm = 0; }
     }
+    // Serial replay (wg_lanes_serial.hip): lists whose greedy state does not
+    // forget a wrong guess (parents at earlier rows leak slots for good,
+    // long-lived lanes) need about one chunked fixed-point iteration per chunk;
+    // their lanes come from one exact single-wave pass instead.  Auto: a replay
+    // at the long chunk still moving after the iterations the serial pass
+    // would cost (serial_cost_us) switches the context to it; a list of a very
+    // different length (mode_rows) starts over with the chunked replay.
+    uint32_t replay_mode = 0;      // WG_OPT_REPLAY_MODE: 0 auto, 1 chunked fixed point, 2 serial
+    bool replay_serial = false;    // auto: this list shape replays serially
+    bool last_serial = false;      // the last lane replay was the serial pass (wg_debug_counters [10])
+    uint64_t mode_rows = 0;        // rows of the list the auto choices (replay_long, replay_serial) were made on
+    bool use_serial() const { return replay_mode == 2 || (replay_mode == 0 && replay_serial); }
+    // estimated cost of the serial pass (us) against one chunked iteration at the long chunk
+    static double serial_cost_us(uint64_t nev, uint32_t nw) {
+        return (double)nev * (nw <= 1 ? 0.016 : nw <= 2 ? 0.04 : nw <= 4 ? 0.07 : 0.3);
+    }
+    static constexpr double WG_CHUNKED_ITER_US = 60.0;
+    // a list of a very different length: the auto choices start over
+    void replay_shape(uint64_t rows) {
+        if (mode_rows && (rows > 2 * mode_rows || 2 * rows < mode_rows)) {
+            replay_long = false;
+            replay_serial = false;
+            replay_blind = 4;
+        }
+        if (!mode_rows || rows > 2 * mode_rows || 2 * rows < mode_rows) mode_rows = rows;
+    }
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
     uint32_t replay_nw = 1;        // occupancy words of the next replay (from the last build's slot count)
@@ -312,6 +340,11 @@ struct wg_ctx {
     // needed hundreds of iterations, later builds launched hundreds of empty ones).
     void replay_adapt(uint32_t fp, uint32_t chunk = 0) {
         if (fp == 0) return;
+        // auto: a long-chunk replay that needed more iterations than the serial pass costs
+        if (replay_mode == 0 && chunk == WG_REPLAY_CHUNK_LONG && fp * WG_CHUNKED_ITER_US > serial_cost_us(n_events, replay_nw)) {
+            replay_serial = true;
+            return;
+        }
         if (replay_auto && chunk < WG_REPLAY_CHUNK_LONG && fp > WG_REPLAY_SHORT_MAX_FP) {
             replay_long = true;   // this list shape wants the long chunk (its own blind count from the next build on)
             replay_blind = 4;
@@ -604,6 +637,12 @@ hipError_t wg_replay_iterate_spec(hipStream_t s, ReplayRun &R, uint32_t blind);
 hipError_t wg_replay_finish_lanes(hipStream_t s, const ReplayRun &R, uint64_t nl, const uint32_t *sp, uint32_t *lane,
                                   uint32_t *lane_out, uint8_t *color_out, const uint8_t *flags);
 hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *converged);
+// the serial replay (wg_lanes_serial.hip): R's buffers as for the chunked
+// replay (R.nev, R.nw, R.ev, R.aux, R.slots_a/b, R.stats, R.flags, R.nev_dev,
+// R.gate); rec: wg_replay_serial_rec_bytes(R.nev) of workspace.  Leaves R as a
+// one-chunk replay that converged at iteration 1.
+hipError_t wg_replay_serial(hipStream_t s, ReplayRun &R, uint4 *rec);
+uint64_t wg_replay_serial_rec_bytes(uint64_t nev);
 int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known = -1);   // wg_lanes.hip
 // speculative build (wg_layout_build): validation words of the lane build
 // (fills WG_LANES_SPEC_ITEMS items) and their check (wg_lanes_fast.hip)

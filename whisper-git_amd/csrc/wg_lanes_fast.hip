@@ -634,7 +634,15 @@ int wg_lf_replay_lanes_spec(wg_ctx *c, const LfRange &R, uint64_t nev, const uin
     if (rc != WG_OK) return rc;
     hipStream_t s = c->stream;
     wg_stage_begin(c, "lf_loop");
-    WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind < 2 ? 2u : c->replay_blind));
+    if (c->use_serial()) {
+        DevBuf &rec = c->lf[LF_SERREC];
+        WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev));
+        WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));
+        c->last_serial = true;
+    } else {
+        WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind < 2 ? 2u : c->replay_blind));
+        c->last_serial = false;
+    }
     if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
@@ -658,8 +666,34 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
     ReplayRun run;
     int src = replay_setup(c, run, nev, ev, aux, nw);
     if (src != WG_OK) return src;
+    if (c->use_serial()) {   // one exact pass: the scalars come with it
+        DevBuf &rec = c->lf[LF_SERREC];
+        WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev));
+        wg_stage_begin(c, "lf_loop");
+        WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));
+        c->last_serial = true;
+        if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
+        WG_HIP(c, hipGetLastError());
+        const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
+        uint64_t sc[3] = {0, 0, 0};
+        const int rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}}, sc);
+        wg_stage_end(c);
+        if (rc != WG_OK) return rc;
+        c->replay_iters = 1;
+        if (sc[2]) { *overflow = true; return WG_OK; }   // more than 64 nw - 1 slots: the caller widens
+        c->max_lane = (uint32_t)sc[0];
+        c->n_slots = (uint32_t)sc[1];
+        c->replay_nw = wg_ctx::nw_for_slots(c->n_slots);
+        *ok = true;
+        return WG_OK;
+    }
     if (run.chunk < WG_REPLAY_CHUNK_LONG && c->replay_auto) run.switch_it = WG_REPLAY_SWITCH_IT;
+    // auto: a replay at the long chunk still moving once its iterations cost
+    // what the serial pass would stops there and replays serially
+    if (c->replay_mode == 0)
+        run.serial_it = 1u + (uint32_t)(wg_ctx::serial_cost_us(nev, nw) / wg_ctx::WG_CHUNKED_ITER_US);
     wg_stage_begin(c, "lf_loop");
+    c->last_serial = false;
     WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind));
     const uint32_t blind = run.it;
     const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
@@ -686,6 +720,10 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
     if (run.switched) {   // still moving at the short chunk: this list shape replays at the long one
         c->replay_long = true;
         c->replay_blind = 4;
+        return replay_lanes_at(c, R, nev, ev, aux, lane, nw, ok, overflow);
+    }
+    if (run.to_serial) {  // still moving at the long chunk: this list shape replays serially
+        c->replay_serial = true;
         return replay_lanes_at(c, R, nev, ev, aux, lane, nw, ok, overflow);
     }
     c->replay_iters = run.it;
@@ -758,7 +796,15 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     wg_stage_begin(c, "lf_loop");
-    WG_HIP(c, wg_replay_iterate_spec(s, run, blind));
+    if (c->use_serial()) {   // exact in one pass (the run then reads as converged at iteration 1)
+        DevBuf &rec = c->lf[LF_SERREC];
+        WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev_cap));
+        WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));
+        c->last_serial = true;
+    } else {
+        WG_HIP(c, wg_replay_iterate_spec(s, run, blind));
+        c->last_serial = false;
+    }
     // scalars + lanes + lane_out / colours in one launch (wg_stage_edges skips k_lane_out)
     WG_ALLOC(c, c->lane_out, n * 4 + 4);
     WG_ALLOC(c, c->color_out, n + 4);
@@ -819,6 +865,7 @@ int wg_lanes_fast(wg_ctx *c, bool *used, bool spec) {
     WG_ALLOC(c, c->lf[LF_LFIRST], c->n * 8 + 8);
     R.lfirst = c->lf[LF_LFIRST].as<unsigned long long>();   // parents at earlier rows stay on this path
     c->e_refs_own = c->e_refs;
+    c->replay_shape(c->n);
     if (spec) {
         const int rc = lanes_fast_spec(c, R);
         *used = rc == WG_OK;

@@ -633,6 +633,7 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
     *converged = R.nev == 0;
     uint32_t next_poll = R.it + 3;
     if (R.switch_it && R.chunk < WG_REPLAY_CHUNK_LONG && next_poll > R.switch_it) next_poll = R.switch_it > R.it ? R.switch_it : R.it + 1;
+    if (R.serial_it && R.chunk >= WG_REPLAY_CHUNK_LONG && next_poll > R.serial_it) next_poll = R.serial_it > R.it ? R.serial_it : R.it + 1;
     while (!*converged && R.it < R.max_iters) {
         R.it++;
         ReplayArgs a{R.nev, R.chunk, R.it, R.ev, R.aux, R.sp_prev, R.sp_next, R.op, R.on, R.stats, R.flags, nullptr, nullptr,
@@ -647,6 +648,10 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
             *converged = fl[0] == 0 || fl[1] == 0;
             if (!*converged && R.switch_it && R.it >= R.switch_it && R.chunk < WG_REPLAY_CHUNK_LONG) {
                 R.switched = true;
+                return hipSuccess;
+            }
+            if (!*converged && R.serial_it && R.it >= R.serial_it && R.chunk >= WG_REPLAY_CHUNK_LONG) {
+                R.to_serial = true;
                 return hipSuccess;
             }
         }

@@ -27,7 +27,7 @@
 // :329-335 / :374-381) is computed for rows [0, e) on every rank.
 //
 // Lists that are not well formed (duplicate ids anywhere, parents at earlier
-// rows), that need more than 63 lane slots or whose replay does not converge
+// rows), that need more than 1023 lane slots or whose replay does not converge
 // fall back, on every rank alike, to the single-GPU build over the whole list.
 #include <cstring>
 #include <vector>
@@ -479,10 +479,14 @@ __global__ void k_sh_x1_head(uint4 *__restrict__ dst, unsigned long long *__rest
 // merge words, not well formed} (no records when not well formed)
 // (+ the rank's own crossing entries [*xb, *xe) and the crossing table's
 // earlier-row flag, both known only on the device at X2)
-__global__ void k_sh_x3_head(uint4 *__restrict__ dst, unsigned long long *__restrict__ len, const uint32_t *__restrict__ flags,
+// Counts past the message's capacity (ev_cap records, aux_cap merge words)
+// mark the list not well formed before the event kernel runs: it writes
+// nothing (gated on flags[0]) and every rank falls back at X3.
+__global__ void k_sh_x3_head(uint4 *__restrict__ dst, unsigned long long *__restrict__ len, uint32_t *__restrict__ flags,
                              const uint32_t *__restrict__ nev, const uint32_t *__restrict__ naux, uint64_t tok_b,
                              const uint32_t *__restrict__ early, const uint32_t *__restrict__ xb, const uint32_t *__restrict__ xe,
-                             uint32_t spec_bit) {
+                             uint32_t spec_bit, uint64_t ev_cap, uint64_t aux_cap) {
+    if ((uint64_t)nev[0] > ev_cap || (uint64_t)naux[0] > aux_cap) flags[0] |= 4u;
     const uint32_t viol = (flags[0] ? 1u : 0u) | (early[0] ? 2u : 0u), ne = nev[0], na = naux[0];
     *dst = make_uint4(ne, na, viol | spec_bit, xe[0] - xb[0]);
     *len = 16ull + tok_b + (viol ? 0ull : (unsigned long long)ne * 16ull + (unsigned long long)na * 4ull);
@@ -1060,7 +1064,7 @@ int wg_shard_slot_heads(wg_ctx *c, const void *gathered, uint64_t stride, int wo
     if (!c || !gathered || !out || world < 1 || 3 * world > 64 || (reinterpret_cast<uintptr_t>(gathered) & 15u) ||
         stride < 32 || (stride & 15u))
         return WG_E_INVALID;
-        WG_SETTLE(c);
+    WG_SETTLE(c);
     (void)hipSetDevice(c->device);
     WgFetch it[64];
     const uint8_t *g = static_cast<const uint8_t *>(gathered);
@@ -1165,22 +1169,25 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         wg_stage_begin(c, "lanes");
         // The message (header, tokens, then the event records and merge-token
         // lists) is bounded by the rows' references (a row makes at most
-        // max(1, parents) events; merge lists hold at most 2 (n + E) + 16
-        // words) and by the L records (tokens), and its header and length are
-        // written on the device, as X1's are; every rank learns the counts from
-        // the gathered heads.  Not well formed: no records, every rank falls
-        // back at X3.
+        // max(1, parents) events) and by the L records (tokens; every
+        // reference arriving from an earlier shard is one of them and adds a
+        // waiter to a merge here, so the merge lists hold at most
+        // 2 (n + E + L) + 16 words — ADVICE r03: without L a high fan-in
+        // root in a small last shard overran the message), and its header and
+        // length are written on the device, as X1's are; every rank learns the
+        // counts from the gathered heads.  Not well formed (or past those
+        // bounds: k_sh_x3_head): no records, every rank falls back at X3.
         if ((rc = wg_lf_refs(c, R, false)) != WG_OK) return rc;
         if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
         wg_stage_end(c);
         const uint64_t tok_b = (L * 4 + 15) & ~15ull;          // records start 16-byte aligned (same on every rank)
-        const uint64_t ev_cap = nl + El, aux_cap = 2 * (nl + El) + 16;
+        const uint64_t ev_cap = nl + El, aux_cap = 2 * (nl + El + L) + 16;
         S.step = SH_X3;
         if ((rc = sh_send_dev(c, 16 + tok_b + ev_cap * 16 + aux_cap * 4, out)) != WG_OK) return rc;
         hipLaunchKernelGGL(k_sh_x3_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), S.msg_len.as<unsigned long long>(),
-                           c->lf[LF_FLAGS].as<const uint32_t>(), c->lf[LF_EVOFF].as<const uint32_t>() + nl,
+                           c->lf[LF_FLAGS].as<uint32_t>(), c->lf[LF_EVOFF].as<const uint32_t>() + nl,
                            c->lf[LF_AUXOFF].as<const uint32_t>() + nl, tok_b, S.flags.as<const uint32_t>() + 4, R.xb_dev,
-                           R.xe_dev, (S.geom_spec_ready && c->spec_replay_shard) ? 4u : 0u);
+                           R.xe_dev, (S.geom_spec_ready && c->spec_replay_shard) ? 4u : 0u, ev_cap, aux_cap);
         uint8_t *m = S.msg.as<uint8_t>() + 16;
         if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(m))) != WG_OK) return rc;
         // the event records travel in the same message, with shard-local tokens

@@ -191,6 +191,11 @@ class Engine:
         (results identical; a build that does not hold is redone there)."""
         self._check(lib().wg_set_option(self._ctx, 5, 1 if on else 0))
 
+    def set_replay_mode(self, mode: int):
+        """WG_OPT_REPLAY_MODE: 0 auto, 1 the chunked fixed-point replay, 2 the
+        single-wave serial replay (speed only; results identical)."""
+        self._check(lib().wg_set_option(self._ctx, 8, int(mode)))
+
     def set_shard_spec_replay(self, on: bool):
         """WG_OPT_SHARD_SPEC_REPLAY: the sharded build's X3 step replays the
         global lane events without a host read, the replay checked with the X6
