@@ -49,7 +49,7 @@ __device__ __forceinline__ void step(uint32_t (&D)[NW], uint32_t lane, uint32_t 
             "v_writelane_b32 %[o], m0, %[j]"
             : [D] "+v"(D[0]), [o] "+v"(o), [t] "=&v"(t), [m] "=&s"(m)
             : [lo] "s"(r.x), [wid] "s"(r.y), [dv] "s"(r.z), [j] "n"(J)
-            : "m0");
+            : "m0", "scc");
         return;
     }
     int x = -1;
@@ -67,7 +67,7 @@ __device__ __forceinline__ void step(uint32_t (&D)[NW], uint32_t lane, uint32_t 
         const int w = x >> 6;
 #pragma unroll
         for (int q = 0; q < NW; q++)
-            if (w == q) asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(D[q]) : "s"(x & 63), "s"(r.z) : "m0");
+            if (w == q) asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(D[q]) : "s"(x & 63), "s"(r.z) : "m0", "scc");
     }
     wlc<J>(o, x);
 }
@@ -93,7 +93,7 @@ __device__ __forceinline__ void pstep(uint32_t &D, uint32_t &o, uint64_t &M, uin
             "v_cmp_gt_u32_e64 %[Mn], %[wid1], %[T]"
             : [D] "+v"(D), [o] "+v"(o), [M] "+s"(M), [Mn] "=s"(Mn), [y] "=&s"(y), [T] "=&v"(T)
             : [Y] "s"(Y), [dvp] "s"(dvp), [lo1] "s"(lo1), [wid1] "s"(wid1), [j] "n"(J)
-            : "m0");
+            : "m0", "scc");
     else
         asm volatile(
             "v_writelane_b32 %[D], %[dvp], m0\n\t"
@@ -106,7 +106,7 @@ __device__ __forceinline__ void pstep(uint32_t &D, uint32_t &o, uint64_t &M, uin
             "v_writelane_b32 %[o], m0, %[j]"
             : [D] "+v"(D), [o] "+v"(o), [M] "+s"(M), [Mn] "=s"(Mn), [y] "=&s"(y), [T] "=&v"(T)
             : [Y] "s"(Y), [dvp] "s"(dvp), [lo1] "s"(lo1), [wid1] "s"(wid1), [j] "n"(J)
-            : "m0");
+            : "m0", "scc");
 }
 template <int G, int PIPE>
 __device__ __forceinline__ void pgroup(uint32_t &D, uint32_t &o, uint64_t &Ma, uint64_t &Mb, uint32_t &dvp,
@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(64) k_pipe(const uint4 *__restrict__ rec, uint
     {
         uint32_t T;
         asm volatile("s_mov_b32 m0, 63\n\tv_subrev_u32 %[T], %[lo], %[D]\n\tv_cmp_gt_u32_e64 %[M], %[wid], %[T]"
-                     : [M] "=s"(Ma), [T] "=&v"(T) : [D] "v"(D), [lo] "s"(cur[0].x), [wid] "s"(cur[0].y) : "m0");
+                     : [M] "=s"(Ma), [T] "=&v"(T) : [D] "v"(D), [lo] "s"(cur[0].x), [wid] "s"(cur[0].y) : "m0", "scc");
     }
     for (uint64_t base = 0; base < n; base += 64) {
         uint32_t o = 0xFFFFu;

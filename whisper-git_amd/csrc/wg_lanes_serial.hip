@@ -28,11 +28,8 @@
 // took (every occupied slot was taken by an occupying allocation first);
 // n_slots the highest slot any allocation took, plus one.
 //
-// The one-wave kernel is latency-bound; per event it runs 8 instructions in a
-// software pipeline: event j+1's compare is issued on D before event j's lane
-// write, and event j's lane is patched into it on the scalar unit (a per-event
-// word says whether that lane is selected with its new D: the tokens event
-// j+1 consumes are known) — profiles/microbench/serial_replay.hip.
+// The one-wave kernel is bound by its instruction issue: 8 instructions per
+// event (profiles/microbench/chain_latency.hip, serial_replay.hip).
 #include "wg_internal.h"
 
 namespace {
@@ -41,55 +38,34 @@ enum : uint32_t { F_A = 1u, F_O = 2u, F_C = 4u, F_M = 8u };
 constexpr uint32_t WG_SER_INF = 0x7FFFFFFFu;
 constexpr int SER_PAD = 128;   // no-op records after the last event (the last batch and the prefetch)
 
-// Per event record, shifted to what the one-wave step for event k reads:
-//   srec[k] = {lo_{k+1}, wid_{k+1}, dv_{k-1}, Y_k}
-// lanes with D - lo < wid are selected by an event (ALLOC: lo 0, wid its time
-// = free before it; MIN / FREE: lo its time, wid 1 = consumed at it); the
-// selected lane's D becomes dv (an occupying event: the time of the event that
-// consumes its token, filled in by k_ser_death; otherwise its own time: free
-// after it); Y_k = 0 when event k selects event k-1's lane with its new D,
-// else the sentinel slot (patched in instead).  Past the last event: no-ops
-// (select nothing; the sentinel patched in takes them, its lane stays leaked).
+// Per event record rec[k] = {lo, wid, dv, 0}: lanes with D - lo < wid are
+// selected (ALLOC: lo 0, wid its time k + 1 = free before it; MIN / FREE: lo
+// its time, wid 1 = consumed at it); the lowest selected lane's D becomes dv
+// (an occupying event: the time of the event that consumes its token, filled
+// in by k_ser_death; otherwise its own time: free after it).  Past the last
+// event: no-ops (select nothing; the sentinel slot takes them, its lane stays
+// leaked).
 __global__ void k_ser_rec(uint64_t nev_cap, const uint32_t *__restrict__ nev_dev, const uint32_t *__restrict__ gate,
-                          const uint4 *__restrict__ ev, const uint32_t *__restrict__ aux, uint4 *__restrict__ srec,
-                          uint32_t sentinel) {
+                          const uint4 *__restrict__ ev, uint4 *__restrict__ rec) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nev_cap + SER_PAD) return;
     if (gate && *gate) return;   // not well formed: nothing is replayed
     const uint64_t nev = nev_dev ? (uint64_t)*nev_dev : nev_cap;
-    uint4 o = make_uint4(0u, 0u, WG_SER_INF, sentinel);
-    if (k + 1 < nev) {   // event k+1's selection
-        const uint32_t t1 = (uint32_t)k + 2u;
-        if (ev[k + 1].x & F_A) { o.x = 0u; o.y = t1; }
-        else { o.x = t1; o.y = 1u; }
+    uint4 o = make_uint4(0u, 0u, WG_SER_INF, 0u);
+    if (k < nev) {
+        const uint32_t f = ev[k].x, t = (uint32_t)k + 1u;
+        if (f & F_A) { o.x = 0u; o.y = t; }
+        else { o.x = t; o.y = 1u; }
+        o.z = (f & F_O) ? WG_SER_INF : t;
     }
-    if (k >= 1 && k <= nev) {   // event k-1's new D (occupying: its consumption time, k_ser_death)
-        const uint32_t fp = ev[k - 1].x;
-        o.z = (fp & F_O) ? WG_SER_INF : (uint32_t)k;
-    }
-    if (k < nev && k > 0) {     // does event k select event k-1's lane with that D?
-        const uint4 r = ev[k];
-        const uint32_t p = (uint32_t)k - 1u;
-        bool sel;
-        if (r.x & F_A) {
-            sel = !(ev[p].x & F_O);                     // a probe's lane is free again
-        } else if (r.x & F_M) {
-            sel = false;
-            const uint32_t n = aux[r.w];
-            for (uint32_t q = 0; q < n && !sel; q++) sel = aux[r.w + 1 + q] == p;
-        } else {
-            sel = r.y == p || r.z == p;                 // it consumes event k-1's token
-        }
-        o.w = sel ? 0u : sentinel;
-    }
-    srec[k] = o;
+    rec[k] = o;
 }
 
-// consumption times: every MIN / FREE event k writes its time k+1 as the new
-// D of the tokens it consumes (field dv_t of srec[t + 1]; after k_ser_rec;
-// tokens never consumed keep WG_SER_INF: leaked)
+// consumption times: every MIN / FREE event k writes its time k + 1 as the
+// new D of the tokens it consumes (after k_ser_rec; tokens never consumed
+// keep WG_SER_INF: leaked)
 __global__ void k_ser_death(uint64_t nev_cap, const uint32_t *__restrict__ nev_dev, const uint32_t *__restrict__ gate,
-                            const uint4 *__restrict__ ev, const uint32_t *__restrict__ aux, uint4 *__restrict__ srec) {
+                            const uint4 *__restrict__ ev, const uint32_t *__restrict__ aux, uint4 *__restrict__ rec) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gate && *gate) return;
     const uint64_t nev = nev_dev ? (uint64_t)*nev_dev : nev_cap;
@@ -99,50 +75,44 @@ __global__ void k_ser_death(uint64_t nev_cap, const uint32_t *__restrict__ nev_d
     const uint32_t t = (uint32_t)k + 1u;
     if (r.x & F_M) {
         const uint32_t n = aux[r.w];
-        for (uint32_t q = 0; q < n; q++) srec[aux[r.w + 1 + q] + 1].z = t;
+        for (uint32_t q = 0; q < n; q++) rec[aux[r.w + 1 + q]].z = t;
     } else {
-        srec[r.y + 1].z = t;
-        srec[r.z + 1].z = t;
+        rec[r.y].z = t;
+        rec[r.z].z = t;
     }
 }
 
 // ---- the one-wave replay, up to 63 slots (slot 63 is the sentinel) --------
-// Event j's step (x_{j-1} in M0, M = event j's compare on D without x_{j-1}'s
-// write): write D[x_{j-1}], event j+1's compare (D has x_{j-1}, not x_j),
-// patch lane x_{j-1} into M (cleared, then the sentinel or x_{j-1} itself
-// set by Y_j), x_j = the lowest selected lane into M0, the output lane j.
-// (In-order issue: the lane write and the next compare go first, so they
-// never wait behind the scalar patch.)  M0 carries x from one step to the
-// next: nothing between the steps touches it (the steps' asm is all that
-// writes M0 in this kernel).
+// One event: T = D - lo, the lanes with T < wid, the lowest into M0, its D :=
+// dv, the output lane j := it.  A single wave issues about one instruction
+// per 6-9 cycles (profiles/microbench/chain_latency.hip), so the step is its
+// instruction count: these five plus the three v_readlane of the record (the
+// batch's records sit one per lane, loaded a batch ahead: scalar loads return
+// out of order and any wait for one waits for all).  Software-pipelining the
+// next event's compare ahead of this lane write needs a scalar patch and a
+// fourth record word: 12 instructions, slower (profiles/r04_serial_variants.md).
 template <int J>
-__device__ __forceinline__ void ser_step1(uint32_t &D, uint32_t &out, uint64_t &M, uint64_t &Mn, uint32_t lo1, uint32_t wid1,
-                                          uint32_t dvp, uint32_t Y) {
-    uint32_t y, T;
+__device__ __forceinline__ void ser_step1(uint32_t &D, uint32_t &out, uint32_t lo, uint32_t wid, uint32_t dv) {
+    uint32_t T;
+    uint64_t M;
     asm volatile(
-        "v_writelane_b32 %[D], %[dvp], m0\n\t"
-        "v_subrev_u32 %[T], %[lo1], %[D]\n\t"
-        "v_cmp_gt_u32_e64 %[Mn], %[wid1], %[T]\n\t"
-        "s_or_b32 %[y], m0, %[Y]\n\t"
-        "s_bitset0_b64 %[M], m0\n\t"
-        "s_bitset1_b64 %[M], %[y]\n\t"
+        "v_subrev_u32 %[T], %[lo], %[D]\n\t"
+        "v_cmp_gt_u32_e64 %[M], %[wid], %[T]\n\t"
         "s_ff1_i32_b64 m0, %[M]\n\t"
+        "v_writelane_b32 %[D], %[dv], m0\n\t"
         "v_writelane_b32 %[o], m0, %[j]"
-        : [D] "+v"(D), [o] "+v"(out), [M] "+s"(M), [Mn] "=s"(Mn), [y] "=&s"(y), [T] "=&v"(T)
-        : [Y] "s"(Y), [dvp] "s"(dvp), [lo1] "s"(lo1), [wid1] "s"(wid1), [j] "n"(J)
-        : "m0");
+        : [D] "+v"(D), [o] "+v"(out), [M] "=&s"(M), [T] "=&v"(T)
+        : [lo] "s"(lo), [wid] "s"(wid), [dv] "s"(dv), [j] "n"(J)
+        : "m0", "scc");
 }
 
-// four steps: the batch's records sit one per lane (lane j = srec[base + j]),
-// read out with v_readlane (vector loads a batch ahead instead of scalar
-// loads: those return out of order, and any wait for one waits for all)
 template <int J>
-__device__ __forceinline__ void ser_quad1(uint32_t &D, uint32_t &out, uint64_t &Ma, uint64_t &Mb, const uint4 &R) {
+__device__ __forceinline__ void ser_quad1(uint32_t &D, uint32_t &out, const uint4 &R) {
 #define WG_SER_RL(v, j) (uint32_t)__builtin_amdgcn_readlane((int)(v), (j))
-    ser_step1<J + 0>(D, out, Ma, Mb, WG_SER_RL(R.x, J + 0), WG_SER_RL(R.y, J + 0), WG_SER_RL(R.z, J + 0), WG_SER_RL(R.w, J + 0));
-    ser_step1<J + 1>(D, out, Mb, Ma, WG_SER_RL(R.x, J + 1), WG_SER_RL(R.y, J + 1), WG_SER_RL(R.z, J + 1), WG_SER_RL(R.w, J + 1));
-    ser_step1<J + 2>(D, out, Ma, Mb, WG_SER_RL(R.x, J + 2), WG_SER_RL(R.y, J + 2), WG_SER_RL(R.z, J + 2), WG_SER_RL(R.w, J + 2));
-    ser_step1<J + 3>(D, out, Mb, Ma, WG_SER_RL(R.x, J + 3), WG_SER_RL(R.y, J + 3), WG_SER_RL(R.z, J + 3), WG_SER_RL(R.w, J + 3));
+    ser_step1<J + 0>(D, out, WG_SER_RL(R.x, J + 0), WG_SER_RL(R.y, J + 0), WG_SER_RL(R.z, J + 0));
+    ser_step1<J + 1>(D, out, WG_SER_RL(R.x, J + 1), WG_SER_RL(R.y, J + 1), WG_SER_RL(R.z, J + 1));
+    ser_step1<J + 2>(D, out, WG_SER_RL(R.x, J + 2), WG_SER_RL(R.y, J + 2), WG_SER_RL(R.z, J + 2));
+    ser_step1<J + 3>(D, out, WG_SER_RL(R.x, J + 3), WG_SER_RL(R.y, J + 3), WG_SER_RL(R.z, J + 3));
 #undef WG_SER_RL
 }
 
@@ -184,7 +154,7 @@ __device__ __forceinline__ void ser_finish(uint32_t lane, uint32_t ml, uint32_t 
     }
 }
 
-__global__ void __launch_bounds__(64) k_ser_replay1(const uint4 *__restrict__ srec, const uint4 *__restrict__ ev,
+__global__ void __launch_bounds__(64) k_ser_replay1(const uint4 *__restrict__ rec, const uint4 *__restrict__ ev,
                                                     uint64_t nev_cap, const uint32_t *__restrict__ nev_dev,
                                                     const uint32_t *__restrict__ gate, uint16_t *__restrict__ slot,
                                                     uint32_t *__restrict__ stats, uint32_t *__restrict__ flags,
@@ -194,42 +164,86 @@ __global__ void __launch_bounds__(64) k_ser_replay1(const uint4 *__restrict__ sr
     const uint64_t nev = nev_dev ? (uint64_t)*nev_dev : nev_cap;
     uint32_t ml = 0, ms = 0, ovf = 0;
     uint32_t D = lane == 63 ? WG_SER_INF : 0u;   // the sentinel slot is held for good
-    uint64_t Ma, Mb;
-    // before event 0: "x_{-1}" = the sentinel, event 0's compare (event 0 is an
-    // allocation — no token exists before it: lo 0, wid 1)
-    {
-        uint32_t T;
-        asm volatile("s_mov_b32 m0, 63\n\t"
-                     "v_subrev_u32 %[T], 0, %[D]\n\t"
-                     "v_cmp_gt_u32_e64 %[M], 1, %[T]"
-                     : [M] "=s"(Ma), [T] "=&v"(T)
-                     : [D] "v"(D)
-                     : "m0");
-    }
-    uint4 R = srec[lane];
+    uint4 R = rec[lane];
     for (uint64_t base = 0; base < nev; base += 64) {
-        const uint4 Rn = srec[base + 64 + lane];   // the next batch (no-ops past the last event)
+        const uint4 Rn = rec[base + 64 + lane];   // the next batch (no-ops past the last event)
         uint32_t out = 0xFFFFu;
-        ser_quad1<0>(D, out, Ma, Mb, R);   ser_quad1<4>(D, out, Ma, Mb, R);
-        ser_quad1<8>(D, out, Ma, Mb, R);   ser_quad1<12>(D, out, Ma, Mb, R);
-        ser_quad1<16>(D, out, Ma, Mb, R);  ser_quad1<20>(D, out, Ma, Mb, R);
-        ser_quad1<24>(D, out, Ma, Mb, R);  ser_quad1<28>(D, out, Ma, Mb, R);
-        ser_quad1<32>(D, out, Ma, Mb, R);  ser_quad1<36>(D, out, Ma, Mb, R);
-        ser_quad1<40>(D, out, Ma, Mb, R);  ser_quad1<44>(D, out, Ma, Mb, R);
-        ser_quad1<48>(D, out, Ma, Mb, R);  ser_quad1<52>(D, out, Ma, Mb, R);
-        ser_quad1<56>(D, out, Ma, Mb, R);  ser_quad1<60>(D, out, Ma, Mb, R);
+        ser_quad1<0>(D, out, R);   ser_quad1<4>(D, out, R);   ser_quad1<8>(D, out, R);   ser_quad1<12>(D, out, R);
+        ser_quad1<16>(D, out, R);  ser_quad1<20>(D, out, R);  ser_quad1<24>(D, out, R);  ser_quad1<28>(D, out, R);
+        ser_quad1<32>(D, out, R);  ser_quad1<36>(D, out, R);  ser_quad1<40>(D, out, R);  ser_quad1<44>(D, out, R);
+        ser_quad1<48>(D, out, R);  ser_quad1<52>(D, out, R);  ser_quad1<56>(D, out, R);  ser_quad1<60>(D, out, R);
         ser_flush(base, nev, lane, out, ev, slot, 63u, ml, ms, ovf);
         R = Rn;
     }
     ser_finish(lane, ml, ms, ovf, 63u, stats, flags, scal);
 }
 
-// ---- wider occupancies (64 NW - 1 slots, NW = 2, 4 or 16): one compare per
-// word, the lowest selected slot over the words, the write by compare + select
-// (no pipelining; profiles/microbench/serial_replay.hip "cnd").  Event j's
-// selection is in srec[j - 1] (event 0: an allocation), its new D in srec[j + 1].
+// ---- wider occupancies (64 NW - 1 slots, NW = 4 or 16): slot 64 w + l is
+// lane l of word w; per event one compare per word, the lowest selected slot
+// over the words (s_ff1 of each word, tagged with the word, unsigned minimum:
+// an empty word's -1 stays the largest), the lane write by compare + select on
+// every word (its word is not a compile-time register).  Records as the
+// one-word kernel's: a batch per lane, read out with v_readlane.
 template <int NW>
-__global__ void __launch_bounds__(64) k_ser_replay_w(const uint4 *__restrict__ srec, const uint4 *__restrict__ ev,
+__device__ __forceinline__ uint32_t ser_first_w(const uint64_t (&m)[NW]);
+template <>
+__device__ __forceinline__ uint32_t ser_first_w<4>(const uint64_t (&m)[4]) {
+    uint32_t x, f1, f2, f3;   // (wave-uniform scalar arithmetic kept in one asm block: the
+                              // compiler takes asm results for divergent and would move it to VALU)
+    asm volatile(
+        "s_ff1_i32_b64 %[x], %[m0]\n\t"
+        "s_ff1_i32_b64 %[f1], %[m1]\n\t"
+        "s_ff1_i32_b64 %[f2], %[m2]\n\t"
+        "s_ff1_i32_b64 %[f3], %[m3]\n\t"
+        "s_or_b32 %[f1], %[f1], 64\n\t"
+        "s_or_b32 %[f2], %[f2], 0x80\n\t"
+        "s_or_b32 %[f3], %[f3], 0xc0\n\t"
+        "s_min_u32 %[x], %[x], %[f1]\n\t"
+        "s_min_u32 %[f2], %[f2], %[f3]\n\t"
+        "s_min_u32 %[x], %[x], %[f2]"
+        : [x] "=&s"(x), [f1] "=&s"(f1), [f2] "=&s"(f2), [f3] "=&s"(f3)
+        : [m0] "s"(m[0]), [m1] "s"(m[1]), [m2] "s"(m[2]), [m3] "s"(m[3])
+        : "scc");
+    return x;
+}
+template <>
+__device__ __forceinline__ uint32_t ser_first_w<16>(const uint64_t (&m)[16]) {
+    uint32_t x = 0xFFFFFFFFu;
+#pragma unroll
+    for (int w = 15; w >= 0; w--) {
+        uint32_t f;
+        asm volatile("s_ff1_i32_b64 %[f], %[m]\n\t"
+                     "s_or_b32 %[f], %[f], %[tag]\n\t"
+                     "s_min_u32 %[x], %[x], %[f]"
+                     : [x] "+s"(x), [f] "=&s"(f) : [m] "s"(m[w]), [tag] "n"(64 * w) : "scc");
+    }
+    return x;
+}
+
+template <int NW, int J>
+__device__ __forceinline__ void ser_step_w(uint32_t (&D)[NW], uint32_t &out, uint32_t lane, uint32_t lo, uint32_t wid,
+                                           uint32_t dv) {
+    uint64_t m[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) m[w] = __ballot(D[w] - lo < wid);
+    const uint32_t x = ser_first_w<NW>(m);   // 0xFFFFFFFF: nothing selected (an overflow)
+#pragma unroll
+    for (int w = 0; w < NW; w++) D[w] = (lane + 64u * w == x) ? dv : D[w];
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(out) : "s"(x), "n"(J));
+}
+
+template <int NW, int J>
+__device__ __forceinline__ void ser_quad_w(uint32_t (&D)[NW], uint32_t &out, uint32_t lane, const uint4 &R) {
+#define WG_SER_RL(v, j) (uint32_t)__builtin_amdgcn_readlane((int)(v), (j))
+    ser_step_w<NW, J + 0>(D, out, lane, WG_SER_RL(R.x, J + 0), WG_SER_RL(R.y, J + 0), WG_SER_RL(R.z, J + 0));
+    ser_step_w<NW, J + 1>(D, out, lane, WG_SER_RL(R.x, J + 1), WG_SER_RL(R.y, J + 1), WG_SER_RL(R.z, J + 1));
+    ser_step_w<NW, J + 2>(D, out, lane, WG_SER_RL(R.x, J + 2), WG_SER_RL(R.y, J + 2), WG_SER_RL(R.z, J + 2));
+    ser_step_w<NW, J + 3>(D, out, lane, WG_SER_RL(R.x, J + 3), WG_SER_RL(R.y, J + 3), WG_SER_RL(R.z, J + 3));
+#undef WG_SER_RL
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64) k_ser_replay_w(const uint4 *__restrict__ rec, const uint4 *__restrict__ ev,
                                                      uint64_t nev_cap, const uint32_t *__restrict__ nev_dev,
                                                      const uint32_t *__restrict__ gate, uint16_t *__restrict__ slot,
                                                      uint32_t *__restrict__ stats, uint32_t *__restrict__ flags,
@@ -242,24 +256,20 @@ __global__ void __launch_bounds__(64) k_ser_replay_w(const uint4 *__restrict__ s
     uint32_t D[NW];
 #pragma unroll
     for (int w = 0; w < NW; w++) D[w] = (w == NW - 1 && lane == 63) ? WG_SER_INF : 0u;
-    uint32_t lo = 0u, wid = 1u;   // event 0: an allocation
+    uint4 R = rec[lane];
     for (uint64_t base = 0; base < nev; base += 64) {
+        const uint4 Rn = rec[base + 64 + lane];
         uint32_t out = 0xFFFFu;
-        for (int j = 0; j < 64; j++) {
-            const uint4 r = srec[base + j], rn = srec[base + j + 1];
-            uint32_t x = cap;   // nothing selected: an overflow (the sentinel)
-#pragma unroll
-            for (int w = NW - 1; w >= 0; w--) {
-                const uint64_t m = __ballot(D[w] - lo < wid);
-                if (m) x = 64u * w + (uint32_t)__builtin_ctzll(m);
-            }
-#pragma unroll
-            for (int w = 0; w < NW; w++) D[w] = (lane + 64u * w == x) ? rn.z : D[w];
-            out = (lane == (uint32_t)j) ? x : out;
-            lo = r.x;
-            wid = r.y;
-        }
+        ser_quad_w<NW, 0>(D, out, lane, R);   ser_quad_w<NW, 4>(D, out, lane, R);
+        ser_quad_w<NW, 8>(D, out, lane, R);   ser_quad_w<NW, 12>(D, out, lane, R);
+        ser_quad_w<NW, 16>(D, out, lane, R);  ser_quad_w<NW, 20>(D, out, lane, R);
+        ser_quad_w<NW, 24>(D, out, lane, R);  ser_quad_w<NW, 28>(D, out, lane, R);
+        ser_quad_w<NW, 32>(D, out, lane, R);  ser_quad_w<NW, 36>(D, out, lane, R);
+        ser_quad_w<NW, 40>(D, out, lane, R);  ser_quad_w<NW, 44>(D, out, lane, R);
+        ser_quad_w<NW, 48>(D, out, lane, R);  ser_quad_w<NW, 52>(D, out, lane, R);
+        ser_quad_w<NW, 56>(D, out, lane, R);  ser_quad_w<NW, 60>(D, out, lane, R);
         ser_flush(base, nev, lane, out, ev, slot, cap, ml, ms, ovf);
+        R = Rn;
     }
     ser_finish(lane, ml, ms, ovf, cap, stats, flags, scal);
 }
@@ -268,7 +278,7 @@ __global__ void __launch_bounds__(64) k_ser_replay_w(const uint4 *__restrict__ s
 
 // Serial replay of nev events (nev_dev: the count on the device, nev its
 // upper bound; gate: nonzero = not well formed, nothing replayed) at
-// occupancy width nw (1, 2, 4 or 16 words); slots into R.slots_a, which becomes
+// occupancy width nw (1, 4 or 16 words); slots into R.slots_a, which becomes
 // the run's result (R.sp_prev); the run looks like a one-chunk replay that
 // converged at iteration 1 (stats / flags / it), so the lane and scalar
 // kernels of wg_lanes_replay.hip finish it unchanged.
@@ -278,10 +288,8 @@ hipError_t wg_replay_serial(hipStream_t s, ReplayRun &R, uint4 *rec) {
     R.it = 1;
     R.sp_prev = R.slots_a;
     R.sp_next = R.slots_b;
-    const uint32_t sentinel = 64u * R.nw - 1u;
     const uint64_t n = R.nev + SER_PAD;
-    hipLaunchKernelGGL(k_ser_rec, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, R.nev, R.nev_dev, R.gate, R.ev, R.aux,
-                       rec, sentinel);
+    hipLaunchKernelGGL(k_ser_rec, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, R.nev, R.nev_dev, R.gate, R.ev, rec);
     if (R.nev)
         hipLaunchKernelGGL(k_ser_death, dim3((uint32_t)((R.nev + 255) / 256)), dim3(256), 0, s, R.nev, R.nev_dev, R.gate, R.ev,
                            R.aux, rec);
@@ -289,9 +297,6 @@ hipError_t wg_replay_serial(hipStream_t s, ReplayRun &R, uint4 *rec) {
     if (R.nw <= 1)
         hipLaunchKernelGGL(k_ser_replay1, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats, R.flags,
                            R.scal);
-    else if (R.nw <= 2)
-        hipLaunchKernelGGL(k_ser_replay_w<2>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
-                           R.flags, R.scal);
     else if (R.nw <= 4)
         hipLaunchKernelGGL(k_ser_replay_w<4>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
                            R.flags, R.scal);
