@@ -258,6 +258,13 @@ int wg_compute_row_heights(wg_ctx *ctx, const int64_t *time, uint64_t n, int32_t
  * band == NULL reproduces GraphLayout::row_geometry from build (:322-346);
  * otherwise band[N] (residency as given) is the per-row pills band.      */
 int wg_row_geometry(wg_ctx *ctx, const float *band, int32_t band_residency);
+/* row_geometry_with_bands(&self, commits, band_heights) (:367-399) with its
+ * commits argument: the heights are compute_row_heights(commits) (:372) of
+ * the list passed (only n_commits, time and residency are read), the edges and
+ * lanes the built layout's.  commits must have the built list's length
+ * (WG_E_INVALID otherwise: the engine keeps one geometry row per built row);
+ * the built list itself (same times) takes wg_row_geometry's per-frame path. */
+int wg_row_geometry_list(wg_ctx *ctx, const wg_commits *commits, const float *band, int32_t band_residency);
 /* wg_layout_build then wg_row_geometry(band) — history_view's first frame
  * after a refresh (commit_graph.rs:1419-1421) — in one call: the frame's
  * banded row_top (heights and band only) is computed on the engine's side

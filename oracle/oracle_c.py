@@ -99,14 +99,17 @@ class OracleLayout:
         self.geometry = _geom_to_dict(L.geom)   # build()'s row_geometry
         self._g = None
 
-    def row_geometry(self, band=None) -> dict:
-        """row_geometry_with_bands(commits, band) (None -> zero bands)."""
+    def row_geometry(self, band=None, time=None) -> dict:
+        """row_geometry_with_bands(commits, band) (None -> zero bands); time:
+        the commits argument's times when it is not the built list."""
         if self._g is not None:
             lib().wgo_geometry_free(ctypes.byref(self._g))
         self._g = _Geom()
         b = None if band is None else np.ascontiguousarray(band, np.float32)
         self._band = b
-        rc = lib().wgo_row_geometry(ctypes.byref(self._L), self.dag.time.ctypes.data,
+        t = self.dag.time if time is None else np.ascontiguousarray(time, np.int64)
+        self._time = t
+        rc = lib().wgo_row_geometry(ctypes.byref(self._L), t.ctypes.data,
                                     None if b is None else b.ctypes.data, ctypes.byref(self._g))
         if rc != 0:
             raise MemoryError("wgo_row_geometry failed")

@@ -284,10 +284,29 @@ TEST(row_geometry_with_short_band_list) {
         CHECK_EQ(g0[r].node_y, NODE_Y);
         CHECK_EQ(g0[r].curves.size(), layout.row_geometry[r].curves.size());
     }
+    // :372 — heights come from the list passed in: the same rows with a month
+    // between two commits give that gap's height, as a layout built on it does
+    std::vector<CommitInfo> gap = commits;
+    for (size_t r = 2; r < gap.size(); r++) gap[r].time -= 30 * 86400;
+    GraphLayout other;
+    other.build(gap);
+    const auto gg = layout.row_geometry_with_bands(gap, {});
+    CHECK_EQ(gg.size(), other.row_geometry.size());
+    bool differs = false;
+    for (size_t r = 0; r < gg.size(); r++) {
+        CHECK_EQ(gg[r].height, other.row_geometry[r].height);
+        CHECK_EQ(gg[r].node_y, other.row_geometry[r].node_y);
+        differs |= gg[r].height != layout.row_geometry[r].height;
+    }
+    CHECK(differs);
+    // the next call without the gap is back on the build's heights
+    const auto g1 = layout.row_geometry_with_bands(commits, {});
+    for (size_t r = 0; r < g1.size(); r++) CHECK_EQ(g1[r].height, layout.row_geometry[r].height);
+    // a list of another length: the edges index the built rows, refused
     bool threw = false;
     try {
         (void)layout.row_geometry_with_bands(uniform_list(3), {});
-    } catch (const std::invalid_argument &) {
+    } catch (const wgraph::Error &) {
         threw = true;
     }
     CHECK(threw);

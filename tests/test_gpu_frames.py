@@ -100,3 +100,33 @@ def test_frames_rescan_row_top_beyond_2_24(engine):
         assert g["row_top"].tobytes() == og["row_top"].tobytes(), r0
         assert g["curve"].tobytes() == og["curve"].tobytes(), r0
     o.close()
+
+
+def test_row_geometry_with_another_list(engine):
+    """row_geometry_with_bands(commits, band) with a commits argument that is
+    not the built list: the heights come from the passed
+    list's times (compute_row_heights(commits), commit_graph.rs:372), the
+    edges from the built layout; the built list again restores its own
+    heights; a list of another length is refused with WG_E_INVALID."""
+    import numpy as np
+    import pytest
+    from oracle import oracle_c
+    from wgraph import WgError, synth
+    d = synth.generate("random13", 20_000, seed=61)
+    other = synth.generate("linux", 20_000, seed=62)          # same length, other times
+    o = oracle_c.OracleLayout(d)
+    try:
+        engine.build(d)
+        for times_of, dag in (("other", other), ("built", d), ("other", other)):
+            engine.row_geometry_list(dag, d.band)
+            og = o.row_geometry(d.band, time=dag.time)
+            got = engine.geometry()
+            for k, v in og.items():
+                assert got[k].tobytes() == v.tobytes(), (times_of, k)
+        engine.row_geometry(d.band)                          # the built list's per-frame path
+        og = o.row_geometry(d.band)
+        assert engine.geometry()["row_top"].tobytes() == og["row_top"].tobytes()
+        with pytest.raises(WgError, match="commits for a layout built on"):
+            engine.row_geometry_list(d.slice_rows(d.n - 1), d.band[:-1])
+    finally:
+        o.close()

@@ -264,6 +264,7 @@ static int build_check(wg_ctx *c, const uint64_t *v, int kl, int k, bool *redo) 
         if ((rc = wg_stage_lanes(c, false)) != WG_OK) return rc;
         if ((rc = wg_stage_edges(c, false, (int64_t)ne)) != WG_OK) return rc;
         c->layout_gen++;
+        c->alt_heights_on = false;   // (a new built list: its own heights)
     } else {
         c->n_edges = ne;
         const uint32_t vis = c->max_lane + 1 < (uint32_t)WG_LANE_COUNT_VISUAL ? c->max_lane + 1 : (uint32_t)WG_LANE_COUNT_VISUAL;
@@ -597,6 +598,7 @@ static int layout_build_impl(wg_ctx *c, const wg_commits *in, const float *fband
     if ((rc = wg_stage_edges(c, spec)) != WG_OK) return rc;
     c->have_layout = true;
     c->layout_gen++;
+    c->alt_heights_on = false;   // (a new built list: its own heights)
     // self.row_geometry with the default node_y / zero bands (:322-346), or
     // the frame's (build_frame; its bands copied to band_prev as they are read)
     if ((rc = wg_side_join(c)) != WG_OK) return rc;
@@ -749,8 +751,67 @@ __global__ void k_band_diff(const uint32_t *__restrict__ a, const uint32_t *__re
         if (a[i] != b[i]) { atomicMin(first, (unsigned long long)i); return; }
 }
 
+// first row whose commit time differs from the built list's (atomicMin)
+__global__ void k_time_diff(const int64_t *__restrict__ a, const int64_t *__restrict__ b, uint64_t n,
+                            unsigned long long *first) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (a[i] != b[i]) { atomicMin(first, (unsigned long long)i); return; }
+}
+
+// row_geometry_with_bands(&self, commits, band_heights) (:367-399) with its
+// commits argument: heights from the passed list's times (compute_row_heights
+// (commits), :372), the geometry from the built edges; the built list itself
+// (same times) is the per-frame path of wg_row_geometry.  One row per built
+// row: a list of another length is refused (WG_E_INVALID), never replaced by
+// the built list.
+int wg_row_geometry_list(wg_ctx *c, const wg_commits *cm, const float *band, int32_t band_residency) {
+    if (!c || !cm) return WG_E_INVALID;
+    WG_SETTLE(c);
+    if (!c->have_layout) return wg_fail(c, WG_E_STATE, "no layout built");
+    if (c->sh.on && !c->sh.replicated) return wg_fail(c, WG_E_STATE, "sharded layout: use wg_shard_geometry_begin");
+    if (cm->n_commits != c->n)
+        return wg_fail(c, WG_E_INVALID, "row_geometry_with_bands: %llu commits for a layout built on %llu (one row per built row)",
+                       (unsigned long long)cm->n_commits, (unsigned long long)c->n);
+    const uint64_t n = c->n;
+    if (n && !cm->time) return wg_fail(c, WG_E_INVALID, "row_geometry_with_bands: commits without times");
+    (void)hipSetDevice(c->device);
+    const int64_t *t = cm->time;
+    if (n && cm->residency == WG_HOST) {
+        WG_ALLOC(c, c->alt_time, n * 8 + 8);
+        WG_HIP(c, hipMemcpyAsync(c->alt_time.p, cm->time, n * 8, hipMemcpyHostToDevice, c->stream));
+        t = c->alt_time.as<const int64_t>();
+    } else if (n && cm->residency != WG_DEVICE) {
+        return wg_fail(c, WG_E_INVALID, "bad residency %d", cm->residency);
+    }
+    bool same = !n || t == c->d_time;
+    if (!same) {
+        WG_ALLOC(c, c->geom_diff_first, 16);
+        WG_HIP(c, hipMemsetAsync(c->geom_diff_first.p, 0xFF, 8, c->stream));
+        const uint64_t g = std::min<uint64_t>((n + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_time_diff, dim3((uint32_t)g), dim3(256), 0, c->stream, t, c->d_time, n,
+                           c->geom_diff_first.as<unsigned long long>());
+        uint64_t first = 0;
+        if (const int frc = wg_fetch(c, {{c->geom_diff_first.p, true}}, &first)) return frc;
+        same = first == ~0ull;
+    }
+    if (same) {
+        if (c->alt_heights_on) { c->alt_heights_on = false; c->geom_key_gen = ~0ull; }
+    } else {
+        WG_ALLOC(c, c->alt_heights, n * 4 + 4);
+        if (const int rc = wg_heights_run(c, n, n, c->alt_heights.as<float>(), t)) return rc;
+        c->alt_heights_on = true;
+        c->geom_key_gen = ~0ull;   // (no per-frame reuse across height sets)
+    }
+    return row_geometry_impl(c, band, band_residency);
+}
+
 int wg_row_geometry(wg_ctx *c, const float *band, int32_t residency) {
     if (!c) return WG_E_INVALID;
+    if (c->alt_heights_on) {   // the built list again: its own heights
+        WG_SETTLE(c);
+        c->alt_heights_on = false;
+        c->geom_key_gen = ~0ull;
+    }
     if (c->pend.build) {   // a deferred build: this pass is redone with it if it does not hold
         c->pend.frame = true;
         c->pend.frame_band = band != nullptr;

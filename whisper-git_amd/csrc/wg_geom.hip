@@ -987,7 +987,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     WG_ALLOC(c, c->curve_off, (n + 2) * 4);
     WG_ALLOC(c, c->scurve_off, (n + 2) * 4);
     { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
-    const float *h = c->heights.as<const float>();
+    const float *h = c->geom_heights();
     const float *rt = c->g_row_top.as<const float>();
     if (n && c->lists_gen == c->layout_gen && c->lists_n == n && c->lists_ne == ne) {
         // same layout: the lists stand; only the curve filter can change with the flags

@@ -181,7 +181,7 @@ struct FontSlot {
 // workspace slots in wg_ctx::lf (wg_lanes_fast.hip; the sharded build reuses LF_EVREC / LF_AUX for the
 // gathered event records)
 enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_CH, LF_SPA, LF_SPB, LF_EVREC,
-       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_LFIRST, LF_SERREC, LF_COUNT };
+       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_LFIRST, LF_SERREC, LF_DEATH, LF_COUNT };
 
 // event replay to a fixed point (wg_lanes_replay.hip)
 struct ReplayRun {
@@ -198,6 +198,8 @@ struct ReplayRun {
     const uint32_t *gate = nullptr;      // speculative build: nonzero = not well formed, replay nothing
     uint32_t switch_it = 0;              // exact replay at a short chunk: still moving at this iteration ->
     bool switched = false;               // stop; the caller replays at WG_REPLAY_CHUNK_LONG (wg_replay_resume)
+    const uint32_t *death = nullptr;     // per event the time of the event consuming its token (0xFFFFFFFF: none),
+                                         // or null: the first iteration then runs the general replay kernel
     uint32_t serial_it = 0;              // exact replay at the long chunk: still moving at this iteration ->
     bool to_serial = false;              // stop; the caller replays serially (wg_replay_resume)
 };
@@ -356,6 +358,8 @@ struct wg_ctx {
     uint64_t n_events = 0;  // events of the last fast-path lane build
     uint64_t e_refs_own = 0;   // parent references of the rows this context owns
     bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])
+    uint32_t *lf_death = nullptr;              // lf[LF_DEATH] when the last wg_lf_chain was a single-GPU one
+    const uint32_t *replay_death = nullptr;    // the exact single-GPU replay's consumption times (replay_setup)
     bool lane_out_fused = false;
     bool lf_refs_done = false;     // the hash join's kernels did the lane stage's clear + reference pass (single GPU)
     bool edges_pending = false;    // the edge list is written by the next full geometry pass (k_edges_rows)   // the lane kernel wrote lane_out / color_out (speculative fast path)
@@ -377,6 +381,11 @@ struct wg_ctx {
     DevBuf edges;           // wg_edge [n_edges]
     // heights
     DevBuf heights;         // float [N]
+    // row_geometry_with_bands on a list other than the built one (wg_row_geometry_list):
+    // the frame passes take the heights of that list's times until the built list comes back
+    DevBuf alt_heights, alt_time;
+    bool alt_heights_on = false;
+    const float *geom_heights() const { return alt_heights_on ? alt_heights.as<const float>() : heights.as<const float>(); }
     // ---- geometry ------------------------------------------------------------
     bool     have_geom = false;
     uint64_t n_vert = 0, n_curve = 0;
@@ -642,6 +651,10 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
 // R.gate); rec: wg_replay_serial_rec_bytes(R.nev) of workspace.  Leaves R as a
 // one-chunk replay that converged at iteration 1.
 hipError_t wg_replay_serial(hipStream_t s, ReplayRun &R, uint4 *rec);
+// the chunked replay's first iteration from R.death (one wave per chunk, the
+// serial step from an empty table `warm` events ahead): slots and exit
+// occupancies as k_lf_replay's iteration 1 would write them (NW = 1)
+hipError_t wg_replay_first(hipStream_t s, const ReplayRun &R, uint16_t *slot_next, unsigned long long *occ_next);
 uint64_t wg_replay_serial_rec_bytes(uint64_t nev);
 int wg_stage_edges(wg_ctx *c, bool spec, int64_t ne_known = -1);   // wg_lanes.hip
 // speculative build (wg_layout_build): validation words of the lane build

@@ -156,10 +156,13 @@ __global__ void __launch_bounds__(WG_BS_THREADS) k_lf_rows(LfRange R, const unsi
 __global__ void k_lf_secev_children(LfRange R, const unsigned long long *__restrict__ first_ref,
                                     const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
                                     uint32_t *__restrict__ secev, const uint32_t *__restrict__ ch_off, uint32_t *ch_fill,
-                                    uint32_t *ch) {
+                                    uint32_t *ch, uint32_t *__restrict__ death) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= R.nl) return;
     const uint64_t gj = R.s + j;
+    // the consumption time of the row's events: none yet (k_lf_events writes the consumers')
+    if (death)
+        for (uint32_t e = ev_off[j]; e < ev_off[j + 1]; e++) death[e] = 0xFFFFFFFFu;
     const uint32_t wi = winfo[j], w = wi & 0x3FFFFFFFu;
     const bool fp_in = wi & 0x40000000u;
     uint32_t e = ev_off[j] + ((w != 1) ? 1u : 0u) + ((w == 1 && !fp_in) ? 1u : 0u);
@@ -294,7 +297,8 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
                             const uint32_t *__restrict__ ch_off, const uint32_t *__restrict__ ch,
                             const uint32_t *__restrict__ secev, const uint32_t *__restrict__ sp,
                             uint4 *__restrict__ ev, uint32_t *__restrict__ aux, const uint32_t *__restrict__ gate = nullptr,
-                            WgReplayInit RI = WgReplayInit{}, const uint32_t *__restrict__ aux_after = nullptr) {
+                            WgReplayInit RI = WgReplayInit{}, const uint32_t *__restrict__ aux_after = nullptr,
+                            uint32_t *__restrict__ death = nullptr) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // (a message whose merge-token lists follow its records: the event count is on the device)
     if (aux_after) aux = reinterpret_cast<uint32_t *>(ev + *aux_after);
@@ -337,10 +341,19 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
         const uint32_t f = F_C | (fp_in ? F_O : 0u) | ((w > 2) ? F_M : 0u);
         ev[e] = make_uint4(f | (LOCAL ? 0u : token_bits(ev_base + e, t[0], t[1])), t[0], t[1],
                            (w > 2) ? aux_base + aux_off[j] : (uint32_t)gj);
+        if (death) {   // (single GPU: tokens are event ids) this event consumes every waiter's token
+            if (list)
+                for (uint32_t q = 1; q <= w; q++) death[list[q]] = e + 1u;
+            else {
+                death[t[0]] = e + 1u;
+                death[t[1]] = e + 1u;
+            }
+        }
         e++;
     } else if (!fp_in) {
         const uint32_t t0 = LOCAL ? sp[j] : sp[j] & ~WG_TOK_EV;
         ev[e] = make_uint4(F_C | (LOCAL ? 0u : token_bits(ev_base + e, t0, t0)), t0, t0, (uint32_t)gj);
+        if (death) death[t0] = e + 1u;
         e++;
     }
     const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
@@ -488,9 +501,18 @@ int wg_lf_chain(wg_ctx *c, const LfRange &R) {
     wg_stage_begin(c, "lf_chain");
     // ch_fill was cleared with the stage's other state (k_lf_clear), ch_off
     // scanned with the event offsets (wg_lf_refs)
+    // single-GPU builds (no crossing entries): the events' consumption times for
+    // the replay's first iteration (wg_replay_first), set by k_lf_events
+    uint32_t *death = nullptr;
+    if (!R.xall) {
+        const uint64_t nev_cap = n + c->e_refs_own;   // a row makes at most max(1, parents) events
+        WG_ALLOC(c, c->lf[LF_DEATH], (nev_cap + 256) * 4);
+        death = c->lf[LF_DEATH].as<uint32_t>();
+    }
+    c->lf_death = death;
     if (n) hipLaunchKernelGGL(k_lf_secev_children, dim3(blocks(n)), dim3(T), 0, s, R, first_ref.as<const unsigned long long>(),
                               winfo.as<const uint32_t>(), ev_off.as<const uint32_t>(), secev.as<uint32_t>(),
-                              ch_off.as<const uint32_t>(), ch_fill.as<uint32_t>(), ch.as<uint32_t>());
+                              ch_off.as<const uint32_t>(), ch_fill.as<uint32_t>(), ch.as<uint32_t>(), death);
     if (R.xin_end)
         hipLaunchKernelGGL(k_lf_xin_secev, dim3(blocks(R.xin_end)), dim3(T), 0, s, R,
                            first_ref.as<const unsigned long long>(), secev.as<uint32_t>());
@@ -536,7 +558,8 @@ int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *
                        c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
                        c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
                        c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
-                       c->lf[LF_SECEV].as<const uint32_t>(), (const uint32_t *)sp, ev_out, aux_out);
+                       c->lf[LF_SECEV].as<const uint32_t>(), (const uint32_t *)sp, ev_out, aux_out, nullptr, WgReplayInit{},
+                       nullptr, (ev_base == 0 && !xt) ? c->lf_death : nullptr);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;
@@ -619,6 +642,7 @@ static int replay_setup(wg_ctx *c, ReplayRun &run, uint64_t nev, const uint4 *ev
     run.stats = stats.as<uint32_t>();
     run.flags = rflags.as<uint32_t>();
     run.scal = c->lane_scalars.as<uint32_t>();
+    run.death = c->replay_death;
     return WG_OK;
 }
 
@@ -785,6 +809,7 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     run.scal = c->lane_scalars.as<uint32_t>();
     run.nev_dev = nev_dev;
     run.gate = gate;
+    run.death = c->lf_death;
     uint32_t blind = c->replay_blind < 2 ? 2u : c->replay_blind;
     const WgReplayInit RI = wg_replay_prepare_spec(run, blind);
     wg_stage_begin(c, "lf_events");
@@ -792,7 +817,8 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
                        c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
                        c->lf[LF_EVOFF].as<const uint32_t>(), c->lf[LF_AUXOFF].as<const uint32_t>(),
                        c->lf[LF_CHOFF].as<const uint32_t>(), c->lf[LF_CH].as<const uint32_t>(),
-                       c->lf[LF_SECEV].as<const uint32_t>(), lf_sp(c), evrec.as<uint4>(), aux.as<uint32_t>(), gate, RI);
+                       c->lf[LF_SECEV].as<const uint32_t>(), lf_sp(c), evrec.as<uint4>(), aux.as<uint32_t>(), gate, RI,
+                       nullptr, c->lf_death);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     wg_stage_begin(c, "lf_loop");
@@ -887,7 +913,9 @@ int wg_lanes_fast(wg_ctx *c, bool *used, bool spec) {
     WG_HIP(c, hipMemsetAsync(evrec.as<uint4>() + nev, 0, 256 * 16, c->stream));   // no-op padding for the replay prefetch
     if ((rc = wg_lf_events(c, R, 0, nullptr, evrec.as<uint4>(), aux.as<uint32_t>(), 0)) != WG_OK) return rc;
     bool ok = false;
+    c->replay_death = c->lf_death;   // (the whole list's events: the first iteration may use them)
     rc = wg_lf_replay_lanes(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(), c->lane_asg.as<uint32_t>(), &ok);
+    c->replay_death = nullptr;
     if (rc != WG_OK) return rc;
     if (!ok) return WG_OK;                           // no fixed point / more than 63 slots: general walk
     c->lane_path = 0;

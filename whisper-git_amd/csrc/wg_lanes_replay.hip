@@ -528,6 +528,13 @@ __global__ void __launch_bounds__(256) k_lf_finish_lanes(uint64_t nchunks, const
 
 // one iteration at the run's occupancy width (R.nw words: up to 64 R.nw - 1 slots)
 static void launch_replay(const ReplayRun &R, const ReplayArgs &a, hipStream_t s) {
+    // iteration 1 restarts every chunk from an empty table: the serial step
+    // (wg_lanes_serial.hip) does that at 8 instructions per event against
+    // the scalar loop's ~320 cycles (r03: 97 of wide16's 156 us of replay)
+    if (a.iter == 1 && R.death && R.nw <= 1 && R.chunk < 0xFFFFFFFFu) {
+        (void)wg_replay_first(s, R, a.slot_next, a.occ_next);
+        return;
+    }
     if (R.nw <= 1) hipLaunchKernelGGL(k_lf_replay<1>, dim3(R.nch), dim3(64), 0, s, a);
     else if (R.nw <= 4) hipLaunchKernelGGL(k_lf_replay<4>, dim3(R.nch), dim3(64), 0, s, a);
     else hipLaunchKernelGGL(k_lf_replay<16>, dim3(R.nch), dim3(64), 0, s, a);

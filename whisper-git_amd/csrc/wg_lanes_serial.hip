@@ -274,6 +274,52 @@ __global__ void __launch_bounds__(64) k_ser_replay_w(const uint4 *__restrict__ r
     ser_finish(lane, ml, ms, ovf, cap, stats, flags, scal);
 }
 
+// ---- the chunked replay's first iteration (wg_lanes_replay.hip) -----------
+// Every chunk restarts `warm` events early from an empty table, so its replay
+// is the serial step over [ew, e1) with this wave's own table: one wave per
+// chunk, the records built in registers from the event flags and the
+// consumption times (R.death).  A merge whose waiters were allocated before
+// the warm-up finds fewer of them (none: x = -1, whose lane write lands on the
+// sentinel): a guess, as the general kernel's zero-filled one is; iteration 1
+// is never a fixed point.  Writes the chunk's slots and its exit occupancy
+// (the lanes alive after it, the sentinel excluded).
+__global__ void __launch_bounds__(64) k_lf_replay_first(const uint4 *__restrict__ ev, const uint32_t *__restrict__ death,
+                                                        uint64_t nev_cap, const uint32_t *__restrict__ nev_dev,
+                                                        const uint32_t *__restrict__ gate, uint32_t chunk, uint32_t warm,
+                                                        uint16_t *__restrict__ slot_next,
+                                                        unsigned long long *__restrict__ occ_next, uint32_t *__restrict__ changed) {
+    if (gate && *gate) return;
+    const uint64_t nev = nev_dev ? (uint64_t)*nev_dev : nev_cap;
+    const uint64_t c = blockIdx.x, e0 = c * chunk;
+    if (e0 >= nev) return;
+    const uint64_t e1 = e0 + chunk < nev ? e0 + chunk : nev;
+    const uint64_t ew = e0 > warm ? e0 - warm : 0;
+    const uint32_t lane = threadIdx.x;
+    uint32_t D = lane == 63 ? WG_SER_INF : 0u;
+    for (uint64_t base = ew; base < e1; base += 64) {
+        const uint64_t k = base + lane;
+        const uint32_t t = (uint32_t)k + 1u;
+        uint4 R = make_uint4(0u, 0u, WG_SER_INF, 0u);   // past the chunk: selects nothing
+        if (k < e1) {
+            const uint32_t f = ev[k].x;
+            R.x = (f & F_A) ? 0u : t;
+            R.y = (f & F_A) ? t : 1u;
+            R.z = (f & F_O) ? death[k] : t;
+        }
+        uint32_t out = 0xFFFFu;
+        ser_quad1<0>(D, out, R);   ser_quad1<4>(D, out, R);   ser_quad1<8>(D, out, R);   ser_quad1<12>(D, out, R);
+        ser_quad1<16>(D, out, R);  ser_quad1<20>(D, out, R);  ser_quad1<24>(D, out, R);  ser_quad1<28>(D, out, R);
+        ser_quad1<32>(D, out, R);  ser_quad1<36>(D, out, R);  ser_quad1<40>(D, out, R);  ser_quad1<44>(D, out, R);
+        ser_quad1<48>(D, out, R);  ser_quad1<52>(D, out, R);  ser_quad1<56>(D, out, R);  ser_quad1<60>(D, out, R);
+        if (base >= e0 && k < e1) slot_next[k] = (uint16_t)out;
+    }
+    const uint64_t alive = __ballot(lane != 63 && D > (uint32_t)e1);   // consumed after the chunk, or never
+    if (lane == 0) {
+        occ_next[c] = alive;
+        changed[1] = 1u;   // a warm-started iteration is never the fixed point
+    }
+}
+
 }  // namespace
 
 // Serial replay of nev events (nev_dev: the count on the device, nev its
@@ -307,3 +353,9 @@ hipError_t wg_replay_serial(hipStream_t s, ReplayRun &R, uint4 *rec) {
 }
 
 uint64_t wg_replay_serial_rec_bytes(uint64_t nev) { return (nev + SER_PAD + 64) * sizeof(uint4); }
+
+hipError_t wg_replay_first(hipStream_t s, const ReplayRun &R, uint16_t *slot_next, unsigned long long *occ_next) {
+    hipLaunchKernelGGL(k_lf_replay_first, dim3((uint32_t)R.nch), dim3(64), 0, s, R.ev, R.death, R.nev, R.nev_dev, R.gate,
+                       R.chunk, R.warm, slot_next, occ_next, R.flags);
+    return hipGetLastError();
+}

@@ -724,5 +724,5 @@ int wg_rowtop_run(wg_ctx *c, uint64_t n, const float *h, const float *d_band, fl
 int wg_stage_rowtop(wg_ctx *c, const float *d_band, uint64_t r_from) {
     if (const int rc = wg_side_join(c)) return rc;   // the side stream's row_top shares the scan buffers
     WG_ALLOC(c, c->g_row_top, (c->n + 1) * 4);
-    return wg_rowtop_run(c, c->n, c->heights.as<const float>(), d_band, c->g_row_top.as<float>(), 0, r_from);
+    return wg_rowtop_run(c, c->n, c->geom_heights(), d_band, c->g_row_top.as<float>(), 0, r_from);
 }

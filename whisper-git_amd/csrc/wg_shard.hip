@@ -647,6 +647,7 @@ static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
     if ((rc = wg_stage_heights(c)) != WG_OK) return rc;
     c->have_layout = true;
     c->layout_gen++;
+    c->alt_heights_on = false;   // (a new built list: its own heights)
     if ((rc = wg_stage_rowtop(c, nullptr)) != WG_OK) return rc;
     if ((rc = wg_stage_geometry(c, nullptr)) != WG_OK) return rc;
     c->have_geom = true;
@@ -1284,6 +1285,7 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         sh_lane_out(c);
         c->have_layout = true;
         c->layout_gen++;
+        c->alt_heights_on = false;   // (a new built list: its own heights)
         return sh_geometry_begin(c, S.build_band, out);   // the default geometry, or build_frame's
     }
     case SH_X6:

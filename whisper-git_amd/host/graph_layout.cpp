@@ -97,15 +97,19 @@ const CommitLayout *GraphLayout::get(const Oid &id) const {
 
 std::vector<RowGeometry> GraphLayout::row_geometry_with_bands(const std::vector<CommitInfo> &commits,
                                                               const std::vector<float> &band_heights) {
-    if (commits.size() != time_.size())
-        throw std::invalid_argument("row_geometry_with_bands: commits is not the list of the last build");
-    for (size_t i = 0; i < commits.size(); i++)
-        if (commits[i].time != time_[i])
-            throw std::invalid_argument("row_geometry_with_bands: commits is not the list of the last build");
+    // heights from the passed list (compute_row_heights(commits), :372), edges from
+    // the built layout: wg_row_geometry_list; a list of another length is refused
+    // by the engine (WG_E_INVALID, thrown as Error), never replaced by the built list
+    std::vector<int64_t> t(commits.size());
+    for (size_t i = 0; i < commits.size(); i++) t[i] = commits[i].time;
+    wg_commits in{};
+    in.n_commits = commits.size();
+    in.time = t.data();
+    in.residency = WG_HOST;
     // band_heights.get(i).copied().unwrap_or(0.0) (:375, :386)
     std::vector<float> band(commits.size(), 0.0f);
     std::memcpy(band.data(), band_heights.data(), std::min(band.size(), band_heights.size()) * sizeof(float));
-    eng_.check(wg_row_geometry(eng_.get(), band.data(), WG_HOST), "wg_row_geometry");
+    eng_.check(wg_row_geometry_list(eng_.get(), &in, band.data(), WG_HOST), "wg_row_geometry_list");
     return copy_geometry();
 }
 

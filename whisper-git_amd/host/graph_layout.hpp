@@ -178,7 +178,7 @@ private:
 
     Engine eng_;
     std::unordered_map<Oid, CommitLayout, OidHash> layouts_;
-    std::vector<int64_t> time_;   // the built list's times (row_geometry_with_bands contract)
+    std::vector<int64_t> time_;   // the built list's times
     mutable uint64_t n_vtx_ = 0;
 };
 

@@ -65,6 +65,7 @@ def lib():
             "wg_copy_row_heights": ([vp, vp], ctypes.c_int),
             "wg_compute_row_heights": ([vp, vp, u64, i32, vp], ctypes.c_int),
             "wg_row_geometry": ([vp, vp, i32], ctypes.c_int),
+            "wg_row_geometry_list": ([vp, ctypes.POINTER(abi.Commits), vp, i32], ctypes.c_int),
             "wg_layout_build_frame": ([vp, ctypes.POINTER(abi.Commits), vp, i32], ctypes.c_int),
             "wg_geometry_summary_get": ([vp, ctypes.POINTER(abi.GeometrySummary)], ctypes.c_int),
             "wg_copy_geometry": ([vp, ctypes.POINTER(abi.GeometryHost)], ctypes.c_int),
@@ -114,7 +115,7 @@ def lib():
 EXPORTED_SYMBOLS = (
     "wg_abi_version", "wg_create", "wg_destroy", "wg_last_error", "wg_set_stream", "wg_synchronize", "wg_set_option",
     "wg_layout_build", "wg_layout_summary_get", "wg_copy_lanes", "wg_copy_edges", "wg_copy_row_heights",
-    "wg_compute_row_heights", "wg_row_geometry", "wg_layout_build_frame", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
+    "wg_compute_row_heights", "wg_row_geometry", "wg_row_geometry_list", "wg_layout_build_frame", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
     "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_build_frame_begin", "wg_shard_geometry_begin",
     "wg_shard_copy_msg", "wg_shard_msg_bytes", "wg_shard_pack_slot", "wg_shard_slot_heads", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
@@ -337,6 +338,19 @@ class Engine:
             b = np.ascontiguousarray(band, np.float32)
             self._band = b
             self._check(lib().wg_row_geometry(self._ctx, b.ctypes.data, abi.WG_HOST))
+
+    def row_geometry_list(self, dag, band=None):
+        """row_geometry_with_bands(commits, band_heights) with its commits
+        argument (wg_row_geometry_list): heights from dag's times, geometry
+        from the built edges; dag must have the built list's length."""
+        c = abi.commits_struct(dag)
+        self._keep_list = [dag, c]
+        b = None
+        if band is not None:
+            b = np.ascontiguousarray(band, np.float32)
+            self._band = b
+        self._check(lib().wg_row_geometry_list(self._ctx, ctypes.byref(c), b.ctypes.data if b is not None else None,
+                                                abi.WG_HOST))
 
     def geometry_summary(self) -> abi.GeometrySummary:
         s = abi.GeometrySummary()
@@ -655,11 +669,13 @@ class GraphLayout:
         return self._ids.get(bytes(oid))
 
     def row_geometry_with_bands(self, commits, band_heights):
-        n = len(commits) if not hasattr(commits, "parent_off") else commits.n
-        band = np.zeros(n, np.float32)
-        m = min(n, len(band_heights))
+        """Heights from `commits` (compute_row_heights(commits), :372), edges
+        from the built layout; commits must have the built list's length."""
+        dag = commits if hasattr(commits, "parent_off") else commits_to_soa(commits)
+        band = np.zeros(dag.n, np.float32)
+        m = min(dag.n, len(band_heights))
         band[:m] = np.asarray(band_heights[:m], np.float32)
-        self.engine.row_geometry(band)
+        self.engine.row_geometry_list(dag, band)
         return geometry_rows(self.engine.geometry())
 
 
