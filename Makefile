@@ -21,7 +21,7 @@ CXXFLAGS_HOST := -O2 -std=c++17 -fPIC -Wall -Wextra -Iinclude
 # and runs on the GPU box's host, whose CPU model differs.  No FMA contraction.
 CFLAGS_ORACLE := -O3 -march=x86-64-v3 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 
-all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgraph_host.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so oracle/libedt_cpu.so \
+all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgraph_host.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so oracle/libedt_cpu.so oracle/libcpu_mt.so \
      tests/cpp/test_graph_layout profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost
 
 # one object per source (parallel, incremental); device code is per translation
@@ -62,7 +62,11 @@ profiles/microbench/launch_cost: profiles/microbench/launch_cost.hip
 oracle/libedt_cpu.so: oracle/edt_cpu.c
 	gcc $(CFLAGS_ORACLE) -fopenmp -shared -o $@ $< -lm
 
-oracle: oracle/liboracle.so oracle/libedt_cpu.so
+# bench.py's multi-threaded CPU baseline (cpu_baseline_threads): OpenMP port, bit-exact with the oracle
+oracle/libcpu_mt.so: oracle/cpu_mt.c oracle/wg_oracle.h include/wgraph.h include/wgraph_tess.h
+	gcc $(CFLAGS_ORACLE) -fopenmp -shared -o $@ oracle/cpu_mt.c -lm
+
+oracle: oracle/liboracle.so oracle/libedt_cpu.so oracle/libcpu_mt.so
 synth: $(PKG)/wgraph/libwgsynth.so
 engine: $(PKG)/wgraph/libwgraph.so
 host: $(PKG)/wgraph/libwgraph_host.so tests/cpp/test_graph_layout
