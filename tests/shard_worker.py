@@ -101,12 +101,12 @@ def run_case(eng, comm, torch, kind, n, seed, world, rank, errors):
         errors.append(f"{kind}/{n}/w{world} rank {rank}: vertex checksum; {len(bad)} vertices differ, first {i} "
                       f"(row {row}, sel {sel}): got {gw[i].view(np.float32) if i >= 0 else None} "
                       f"want {ow[i].view(np.float32) if i >= 0 else None}")
-    # build + banded frame in one sharded call (wg_shard_build_frame_begin): one exchange fewer
+    # build + banded frame in one sharded call (wg_shard_build_frame_begin): X1, X2, X3
     x0 = comm.exchanges
     eng.shard_build_frame(c, world, rank, s, e, comm, band=d.band)
     frame_x = comm.exchanges - x0
-    if world > 1 and want_mode == 1 and frame_x != 4:
-        errors.append(f"{kind}/{n}/w{world} rank {rank}: build_frame took {frame_x} exchanges, expected 4")
+    if world > 1 and want_mode == 1 and frame_x != 3:
+        errors.append(f"{kind}/{n}/w{world} rank {rank}: build_frame took {frame_x} exchanges, expected 3")
     lane, color = eng.lanes()
     same("frame lane", lane, o.lane[s:e])
     same("frame color", color, o.color[s:e])

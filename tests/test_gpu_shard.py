@@ -163,8 +163,8 @@ def _lockstep(engines, begin, tamper=None):
 def test_packed_slots_in_one_process(world, kind, n, frame, defer):
     """wg_shard_pack_slot: every rank's slot packed on the shared stream, no
     host synchronisation before the gather; shards equal the oracle.  frame:
-    wg_shard_build_frame_begin with the device bands (4 exchanges instead of
-    the two calls' 5).  defer: three steps with WG_OPT_DEFER_VALIDATION, the
+    wg_shard_build_frame_begin with the device bands (3 exchanges: X1, X2,
+    X3; the geometry passes exchange nothing).  defer: three steps with WG_OPT_DEFER_VALIDATION, the
     later steps' speculative local geometry validated by the emission (the
     second step's emission first, the third step's by a geometry query)."""
     import ctypes
@@ -205,7 +205,7 @@ def test_packed_slots_in_one_process(world, kind, n, frame, defer):
             def frame_build():
                 return _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
                     e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
-            assert frame_build() == 4
+            assert frame_build() == 3
             if defer:
                 og = o.row_geometry(d.band)
                 frame_build()   # step 2: a speculative local geometry pass, its validation deferred
@@ -365,11 +365,11 @@ def test_x3_crossing_count_guard():
 @pytest.mark.parametrize("spec", [True, False])
 def test_spec_replay_sequence(spec):
     """WG_OPT_SHARD_SPEC_REPLAY: after the first sharded build, X3 replays the
-    global events blind and the X6 headers carry the replay's words.  A list
-    shape change (wide16 -> linux) leaves the blind count short: every rank
-    redoes the replay exactly at X6 and sends X6 again (5 exchange rounds
-    instead of 4); lanes, geometry and vertices equal the oracle every step.
-    spec=False: the replay is checked before X3 returns, 4 rounds always."""
+    global events blind and its words are checked with the local geometry's
+    validation read.  A list shape change (wide16 -> linux) leaves the blind
+    count short: every rank redoes the replay exactly and its local geometry
+    (no exchange: 3 rounds either way); lanes, geometry and vertices equal the
+    oracle every step.  spec=False: the replay is exact before the geometry."""
     import ctypes
     import sys as _sys
 
@@ -409,7 +409,7 @@ def test_spec_replay_sequence(spec):
                 e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
             redo = [int(e.debug_counters()[7]) - b for e, b in zip(engines, before)]
             assert len(set(redo)) == 1, f"step {step}: ranks disagree on the redo {redo}"
-            assert rounds == 4 + redo[0], f"step {step}: {rounds} rounds, {redo[0]} redone"
+            assert rounds == 3, f"step {step}: {rounds} rounds, {redo[0]} redone"
             if not spec or step == 0:
                 assert redo[0] == 0
             redo_steps.append(redo[0])
@@ -436,20 +436,18 @@ def test_spec_replay_sequence(spec):
             torch.cuda.synchronize()
             del keep
         if spec:
-            assert sum(redo_steps) >= 1, f"no step exercised the X6 redo: {redo_steps}"
+            assert sum(redo_steps) >= 1, f"no step exercised the replay redo: {redo_steps}"
     finally:
         for e in engines:
             e.close()
         stream_ctx.__exit__(None, None, None)
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_earlier_row_parent_across_shards(world):
-    """A parent at an earlier row in another shard (clock skew: the
-    reference leaks the waiter, commit_graph.rs:441-446, and skips the edge,
-    :526-528).  The crossing table's earlier-row flag is raised on the device
-    at X2 and travels in X3's header: every rank falls back to the whole-list
-    build at X3 (mode 2) with the oracle's lanes, geometry and vertices."""
+def _lockstep_build_check(d, world, expect_mode, frame=True):
+    """Build d on `world` engines in lockstep (build_frame with the bands, or
+    the two calls) and check every rank against the oracle: build mode
+    (debug counter 5), lanes, colours, max_lane, slots, own edges, heights,
+    row_top, the banded geometry's lists and the vertex checksum."""
     import ctypes
     import sys as _sys
 
@@ -459,14 +457,9 @@ def test_earlier_row_parent_across_shards(world):
     _sys.path.insert(0, ROOT)
     import wgraph
     from oracle import oracle_c
-    from wgraph import abi, lib, synth
+    from wgraph import abi, lib
     from wgraph.shard import shard_rows
 
-    d = synth.generate("wide16", 24000, seed=17)
-    r_late = shard_rows(d.n, world, world - 1)[0] + 100      # a row of the last shard
-    pa = int(d.parent_off[r_late])
-    assert int(d.parent_off[r_late + 1]) > pa
-    d.parent_oid[pa] = d.oid[10]                            # its first parent: row 10 (shard 0, earlier)
     dev = torch.device("cuda", 0)
     keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
                                                    d.parent_oid.reshape(-1), d.flags, d.band)]
@@ -484,20 +477,35 @@ def test_earlier_row_parent_across_shards(world):
         for e in engines:
             e.set_stream(ts.cuda_stream)
         rng = [shard_rows(d.n, world, r) for r in range(world)]
-        rounds = _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
-            e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
-        assert rounds == 3, rounds   # X1, X2, X3 (the fallback decided there)
+        if frame:
+            rounds = _lockstep(engines, lambda e, r, m: lib().wg_shard_build_frame_begin(
+                e._ctx, ctypes.byref(c), world, r, rng[r][0], rng[r][1], keep[5].data_ptr(), abi.WG_DEVICE, m))
+        else:
+            rounds = _lockstep(engines, lambda e, r, m: lib().wg_shard_build_begin(e._ctx, ctypes.byref(c), world, r,
+                                                                                    rng[r][0], rng[r][1], m))
+            rounds += _lockstep(engines, lambda e, r, m: lib().wg_shard_geometry_begin(e._ctx, keep[5].data_ptr(),
+                                                                                        abi.WG_DEVICE, m))
+        assert rounds == 3, rounds   # X1, X2, X3; the geometry passes exchange nothing
         og = o.row_geometry(d.band)
         vo = og["vert_off"].astype(np.int64)
+        oe = o.edges.view(np.uint32).reshape(-1, 5)
         for r, e in enumerate(engines):
             s, t = rng[r]
-            assert int(e.debug_counters()[5]) == 2, "whole-list fallback expected"
+            assert int(e.debug_counters()[5]) == expect_mode, f"rank {r}: build mode {int(e.debug_counters()[5])}"
             lane, color = e.lanes()
-            assert lane.tobytes() == o.lane[s:t].tobytes() and color.tobytes() == o.color[s:t].tobytes(), f"rank {r}"
-            assert e.layout_summary().max_lane == o.max_lane
+            assert lane.tobytes() == o.lane[s:t].tobytes(), (r, np.nonzero(lane != o.lane[s:t])[0][:5])
+            assert color.tobytes() == o.color[s:t].tobytes(), f"rank {r} colours"
+            ls_ = e.layout_summary()
+            assert (ls_.max_lane, ls_.n_slots) == (o.max_lane, o.n_slots), f"rank {r}"
+            ge = np.ascontiguousarray(e.edges()).view(np.uint32).reshape(-1, 5)
+            want = oe[(oe[:, 0] >= s) & (oe[:, 0] < t)]
+            assert ge.tobytes() == want.tobytes(), f"rank {r} edges"
             g = e.geometry()
-            assert g["row_top"].tobytes() == og["row_top"][s:t + 1].tobytes(), f"rank {r}"
-            assert g["vert"].tobytes() == og["vert"][vo[s]:vo[t]].tobytes(), f"rank {r}"
+            assert g["height"].tobytes() == og["height"][s:t].tobytes(), f"rank {r} heights"
+            assert g["row_top"].tobytes() == og["row_top"][s:t + 1].tobytes(), f"rank {r} row_top"
+            assert g["vert"].tobytes() == og["vert"][vo[s]:vo[t]].tobytes(), f"rank {r} verticals"
+            co = og["curve_off"].astype(np.int64)
+            assert g["curve"].tobytes() == og["curve"][co[s]:co[t]].tobytes(), f"rank {r} curves"
             e.emit_vertices(s, t, selected=s + 3)
             ov, _ = o.emit_vertices(s, t, selected=s + 3)
             assert e.vertex_summary().checksum == oracle_c.vertex_checksum(ov), f"rank {r} vertices"
@@ -509,12 +517,76 @@ def test_earlier_row_parent_across_shards(world):
         del keep
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_earlier_row_parent_across_shards(world):
+    """A first parent at an earlier row in another shard (clock skew: the
+    reference leaks the waiter, commit_graph.rs:441-446, and skips the edge,
+    :526-528) stays on the sharded path (mode 1): the child's chain holds its
+    slot for good, the edge takes the far row's lane from X3's row tokens."""
+    from wgraph import synth
+    from wgraph.shard import shard_rows
+
+    d = synth.generate("wide16", 24000, seed=17)
+    r_late = shard_rows(d.n, world, world - 1)[0] + 100      # a row of the last shard
+    pa = int(d.parent_off[r_late])
+    assert int(d.parent_off[r_late + 1]) > pa
+    d.parent_oid[pa] = d.oid[10]                            # its first parent: row 10 (shard 0, earlier)
+    _lockstep_build_check(d, world, 1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_earlier_row_secondary_parents_across_shards(world):
+    """Secondary parents at earlier rows: the first leaky reference to a row
+    allocates a slot that is never freed (:447-459 with the target already
+    processed), later ones find it present.  Three references to row 10 from
+    two later shards (the second shard's first, then the last shard's two),
+    one to row 20 whose own shard already holds a leaky reference to it (so
+    no later reference allocates), and one within a shard."""
+    import numpy as np
+    from wgraph import synth
+    from wgraph.shard import shard_rows
+
+    d = synth.generate("random13", 30000, seed=23)
+    multi = [i for i in range(d.n) if int(d.parent_off[i + 1]) - int(d.parent_off[i]) >= 2]
+    s1 = shard_rows(d.n, world, 1)[0]
+    sl = shard_rows(d.n, world, world - 1)[0]
+    s0e = shard_rows(d.n, world, 0)[1]
+
+    def sec(lo, k=0):
+        rows = [i for i in multi if i >= lo + 50]
+        return rows[k]
+
+    for row, target in [(sec(s1), 10), (sec(sl, 3), 10), (sec(sl, 9), 10), (sec(s0e - 200), 20), (sec(sl, 15), 20),
+                        (sec(sl, 30), sec(sl, 20))]:
+        d.parent_oid[int(d.parent_off[row]) + 1] = d.oid[target]
+    d.parent_oid = np.ascontiguousarray(d.parent_oid)
+    _lockstep_build_check(d, world, 1)
+
+
+@pytest.mark.parametrize("world,kind,n,over", [
+    (8, "skew", 120_000, {}),                          # clock skew + reflog orphans, time-sorted
+    (3, "skew", 60_000, {"p_clock_skew": 2e-3}),       # heavy skew (~200 slots)
+    (4, "linuxwide", 40_000, {}),                      # > 100 concurrent lanes
+], ids=["skew-w8", "skew-heavy-w3", "linuxwide-w4"])
+def test_leaky_lists_stay_sharded(world, kind, n, over):
+    """lists with parents at earlier rows build on the row
+    shards (debug counter 5 == 1), every rank bit-exact against the oracle."""
+    from wgraph import synth
+    _lockstep_build_check(synth.generate(kind, n, **over), world, 1)
+
+
+def test_leaky_list_two_calls():
+    """The same through wg_shard_build_begin + wg_shard_geometry_begin."""
+    from wgraph import synth
+    _lockstep_build_check(synth.generate("skew", 50_000, seed=5), 3, 1, frame=False)
+
+
 def test_spec_replay_mixed_history():
     """The speculative replay is a decision every rank takes alike: each X3
     header says whether its rank may speculate and all ranks replay blind
     only when every one may.  A rank whose context is fresh (no earlier
     sharded build) next to warmed ones: every rank replays exactly at X3,
-    four exchange rounds, the oracle's results; the next build speculates."""
+    three exchange rounds, the oracle's results; the next build speculates."""
     import ctypes
     import sys as _sys
 
@@ -562,18 +634,18 @@ def test_spec_replay_mixed_history():
     try:
         for e in engines:
             e.set_stream(ts.cuda_stream)
-        assert build() == 4
-        assert build() == 4          # warmed: speculative (the same list: no redo)
+        assert build() == 3
+        assert build() == 3          # warmed: speculative (the same list: no redo)
         check("warm")
         engines[1].close()
         engines[1] = wgraph.Engine(0)   # a fresh context beside two warmed ones
         engines[1].set_stream(ts.cuda_stream)
         warm = [int(e.debug_counters()[9]) for e in (engines[0], engines[2])]
         assert min(warm) >= 1, warm   # the second build speculated
-        assert build() == 4          # exact on every rank (no X6 words to disagree on)
+        assert build() == 3          # exact on every rank (no speculative words to disagree on)
         assert [int(e.debug_counters()[9]) for e in (engines[0], engines[2])] == warm
         check("mixed")
-        assert build() == 4
+        assert build() == 3
         assert [int(e.debug_counters()[9]) for e in engines] == [warm[0] + 1, 1, warm[1] + 1]
         check("after")
     finally:

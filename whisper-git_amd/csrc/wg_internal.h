@@ -84,6 +84,7 @@ struct StageTimer {
 // in-list parents" (the greedy ignores repeated parents, :435-459).
 struct WgXEnt { uint32_t c, p, kf, pad; };
 #define WG_XF_FIRST_IN_ROW 0x10000u
+#define WG_XF_LLEAKY       0x20000u   // (a reference to an earlier row) the target's shard holds a leaky reference to it
 // chain tokens of the lane fast path: an event id, a crossing entry (resolved
 // once the other shards have reported), a row (pointer jumping) or nothing
 #define WG_TOK_EV   0x80000000u
@@ -150,7 +151,7 @@ struct ShardState {
     std::vector<uint64_t> xoff, evoff, auxoff;   // per-rank prefixes (world + 1)
     DevBuf xtok, xt;          // chain token per crossing entry: shard-local / global
     DevBuf dev_small;
-    DevBuf h_g, rt_g;         // heights of rows [0, e) / row_top of rows [s, e] (below s: unspecified)
+    DevBuf h_g, rt_g;         // heights / row_top of every row of the list (the crossing edges' far endpoints)
     bool rt_fresh = false;        // rt_g was computed at build begin (side stream) with the bands rt_band
     const float *rt_band = nullptr;
     const float *build_band = nullptr;   // wg_shard_build_frame_begin: the build's geometry takes these bands
@@ -158,12 +159,16 @@ struct ShardState {
     uint64_t local_ne = 0, local_nin = 0; // local edges, of which incoming
     DevBuf band_host;         // device copy of a host band array [N]
     const float *band_g = nullptr;
-    DevBuf xchild, xpar;      // per crossing entry: child lane/colour, parent lane/y
+    DevBuf xchild, xpar;      // per crossing entry: child lane/colour/y, parent lane/y (built locally from etok)
+    DevBuf lk;                // uint8 [nl]: an own row some own row at or after it references (a leaky reference)
+    DevBuf etok;              // uint32 [2 nx]: per crossing entry the global token of its child row / parent row
+    DevBuf elane;             // uint32 [2 nx]: ... and their lanes, after the replay
+    DevBuf death;             // uint32 [nev]: consumption time of every global event's token (the replay's first iteration)
     DevBuf in_scan, edge_y, own_edges;
     uint64_t n_own_edges = 0;
     bool geom_spec_ready = false;   // an earlier sharded geometry pass sized the lists (speculation may start)
     bool geom_banded = false;       // the last local geometry pass took bands (c->band holds the local copy)
-    bool replay_pending = false;    // X3 replayed speculatively: its words ride on the X6 headers
+    bool replay_pending = false;    // X3 replayed speculatively: its words are checked with the local geometry's
     uint32_t rp_it = 0, rp_chunk = 0;
     const uint32_t *rp_flags = nullptr, *rp_scal = nullptr;
 };
@@ -358,6 +363,7 @@ struct wg_ctx {
     uint64_t n_events = 0;  // events of the last fast-path lane build
     uint64_t e_refs_own = 0;   // parent references of the rows this context owns
     bool lf_sp_b = false;   // chain sources ended in lf[LF_SPB] (else lf[LF_SPA])
+    const uint16_t *lf_slot_of = nullptr;      // the last lane replay's slot per event (valid until the next replay)
     uint32_t *lf_death = nullptr;              // lf[LF_DEATH] when the last wg_lf_chain was a single-GPU one
     const uint32_t *replay_death = nullptr;    // the exact single-GPU replay's consumption times (replay_setup)
     bool lane_out_fused = false;
@@ -667,6 +673,12 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back, uint32_t *scal = nul
 int wg_lf_refs_end(wg_ctx *c, uint32_t *viol, uint64_t *nev, uint64_t *naux);
 int wg_lf_chain(wg_ctx *c, const LfRange &R);
 int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok);
+// sharded X3: the row token of every own crossing entry's child row (ctok, by
+// own entry) and of every crossing entry's parent row in this shard (ptok, by
+// global entry; WG_TOK_NONE elsewhere), xcap entries at most, *xtot on the device
+int wg_lf_export_ends(wg_ctx *c, const LfRange &R, uint32_t *ctok, uint32_t *ptok, const uint32_t *xtot, uint64_t xcap);
+// consumption time (event index + 1) of every token the nev global records consume; 0xFFFFFFFF: never
+int wg_lf_death_from_records(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *death);
 int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint4 *ev_out, uint32_t *aux_out,
                  uint32_t aux_base);
 // sharded form: records with shard-local tokens / aux offsets (before the

@@ -75,8 +75,10 @@ __device__ __forceinline__ uint64_t lf_xown_end(const LfRange &R) { return R.xe_
 // is ref k (row gi, index kidx, target p) the first in-list reference to p?
 __device__ __forceinline__ bool is_first_ref(const LfRange &R, const unsigned long long *__restrict__ first_ref,
                                              uint64_t gi, uint32_t k, uint32_t kidx, uint64_t p) {
-    if (p <= gi)   // leaky; without lfirst (or before s) k_lf_refs flagged the list and nothing here is used
-        return R.lfirst && p >= R.s && R.lfirst[p - R.s] == ref_key(gi, kidx);
+    if (p <= gi) {   // leaky; without lfirst k_lf_refs flagged the list and nothing here is used
+        if (p < R.s) return R.isfb[k] != 0;   // target in an earlier shard: k_lf_xfirst decided
+        return R.lfirst && R.lfirst[p - R.s] == ref_key(gi, kidx);
+    }
     if (p >= R.e) return R.isfb[k] != 0;
     return first_ref[p - R.s] == ref_key(gi, kidx);
 }
@@ -98,7 +100,11 @@ __global__ void k_lf_xin(LfRange R, unsigned long long *first_ref, uint32_t *fpc
     if (kidx == 0) atomicAdd(&fpc[en.p - R.s], 1u);
 }
 
-// own references beyond the shard: first reference to their target?
+// own references beyond the shard: first reference to their target?  A
+// reference to an earlier shard's row is leaky (:441-446): first among the
+// leaky references to that row, i.e. its own shard holds none (WG_XF_LLEAKY:
+// every row of that shard precedes this one) and no crossing entry of a row
+// between them, or an earlier one of this row, refers to it
 __global__ void k_lf_xfirst(LfRange R) {
     const uint64_t xe = lf_xown_end(R);
     const uint64_t x = lf_xown_begin(R) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -107,11 +113,14 @@ __global__ void k_lf_xfirst(LfRange R) {
     const uint32_t kidx = en.kf & 0xFFFFu;
     const uint32_t k = R.poff[en.c] + kidx;
     if (!(en.kf & WG_XF_FIRST_IN_ROW)) { R.isfb[k] = 0; return; }
+    const bool leaky = en.p <= en.c;
     const unsigned long long key = ref_key(en.c, kidx);
-    bool first = true;
+    bool first = !(leaky && (en.kf & WG_XF_LLEAKY));
     for (uint64_t y = 0; y < xe && first; y++) {
         const WgXEnt o = R.xall[y];
-        if (o.p == en.p && (o.kf & WG_XF_FIRST_IN_ROW) && ref_key(o.c, o.kf & 0xFFFFu) < key) first = false;
+        // (a forward reference never precedes a leaky one to the same row in key order)
+        if (o.p == en.p && (o.kf & WG_XF_FIRST_IN_ROW) && ref_key(o.c, o.kf & 0xFFFFu) < key && (!leaky || o.p <= o.c))
+            first = false;
     }
     R.isfb[k] = first ? 1 : 0;
 }
@@ -272,6 +281,23 @@ __global__ void k_lf_export(LfRange R, const uint32_t *__restrict__ sp, uint32_t
     tok[x - xb] = t;
 }
 
+// X3 (no X6): the row token of every own entry's child row, and of the parent
+// row of every entry (of any shard) whose parent is in this one — after the
+// replay every rank reads the far endpoints' lanes from them
+__global__ void k_lf_export_ends(LfRange R, const uint32_t *__restrict__ sp, uint32_t *__restrict__ ctok,
+                                 uint32_t *__restrict__ ptok, const uint32_t *__restrict__ xtot, uint64_t xcap) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= xcap) return;
+    const uint64_t nx = *xtot, xb = lf_xown_begin(R), xe = lf_xown_end(R);
+    uint32_t pt = WG_TOK_NONE;
+    if (x < nx) {
+        const WgXEnt en = R.xall[x];
+        if (en.p >= R.s && en.p < R.e) pt = sp[en.p - R.s];
+        if (x >= xb && x < xe) ctok[x - xb] = sp[en.c - R.s];
+    }
+    ptok[x] = pt;
+}
+
 __device__ __forceinline__ uint32_t globalize(uint32_t v, uint32_t ev_base, const uint32_t *__restrict__ xt) {
     if (v & WG_TOK_EV) return WG_TOK_EV | ((v & ~WG_TOK_EV) + ev_base);
     if (v & WG_TOK_X) return xt[v & ~WG_TOK_X];
@@ -363,6 +389,29 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
             ev[e] = make_uint4(F_A | F_O, 0u, 0u, (uint32_t)gj);
             e++;
         }
+    }
+}
+
+// consumption times from global records (the sharded build's gathered
+// stream; a single-GPU build writes them in k_lf_events): tokens never
+// consumed keep 0xFFFFFFFF
+__global__ void k_lf_death_fill(uint64_t nev, uint32_t *__restrict__ death) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nev) death[k] = 0xFFFFFFFFu;
+}
+__global__ void k_lf_death_scatter(uint64_t nev, const uint4 *__restrict__ ev, const uint32_t *__restrict__ aux,
+                                   uint32_t *__restrict__ death) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nev) return;
+    const uint4 r = ev[k];
+    if (!(r.x & F_C)) return;
+    const uint32_t t = (uint32_t)k + 1u;
+    if (r.x & F_M) {
+        const uint32_t n = aux[r.w];
+        for (uint32_t q = 0; q < n; q++) death[aux[r.w + 1 + q]] = t;
+    } else {
+        death[r.y] = t;
+        death[r.z] = t;
     }
 }
 
@@ -544,6 +593,20 @@ int wg_lf_export_tokens(wg_ctx *c, const LfRange &R, uint32_t *tok) {
     return WG_OK;
 }
 
+int wg_lf_export_ends(wg_ctx *c, const LfRange &R, uint32_t *ctok, uint32_t *ptok, const uint32_t *xtot, uint64_t xcap) {
+    if (xcap) hipLaunchKernelGGL(k_lf_export_ends, dim3(blocks(xcap)), dim3(T), 0, c->stream, R, lf_sp(c), ctok, ptok, xtot, xcap);
+    WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+int wg_lf_death_from_records(wg_ctx *c, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *death) {
+    if (!nev) return WG_OK;
+    hipLaunchKernelGGL(k_lf_death_fill, dim3(blocks(nev)), dim3(T), 0, c->stream, nev, death);
+    hipLaunchKernelGGL(k_lf_death_scatter, dim3(blocks(nev)), dim3(T), 0, c->stream, nev, ev, aux, death);
+    WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
 int wg_lf_events(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uint32_t *xt, uint4 *ev_out, uint32_t *aux_out,
                  uint32_t aux_base) {
     const uint64_t n = R.nl;
@@ -668,6 +731,7 @@ int wg_lf_replay_lanes_spec(wg_ctx *c, const LfRange &R, uint64_t nev, const uin
         c->last_serial = false;
     }
     if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
+    c->lf_slot_of = run.sp_prev;
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;
@@ -697,6 +761,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
         WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));
         c->last_serial = true;
         if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
+        c->lf_slot_of = run.sp_prev;
         WG_HIP(c, hipGetLastError());
         const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
         uint64_t sc[3] = {0, 0, 0};
@@ -725,6 +790,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
     bool conv = nev == 0;
     for (int pass = 0; pass < 2; pass++) {
         if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
+        c->lf_slot_of = run.sp_prev;
         WG_HIP(c, hipGetLastError());
         if (nev && !conv) {
             int rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}, {run.flags + run.it - 1, false},

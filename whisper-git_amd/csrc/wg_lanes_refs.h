@@ -32,7 +32,8 @@ __device__ __forceinline__ bool lf_refs_row(const LfRange &R, uint64_t gi, unsig
         if (p < 0) continue;
         if (k - pa > 0xFFFFu) { bad = true; continue; }
         if ((uint64_t)p <= gi) {                     // leaky: target at this row or earlier
-            if (!R.lfirst || (uint64_t)p < R.s) { bad = true; continue; }
+            if (!R.lfirst) { bad = true; continue; }
+            if ((uint64_t)p < R.s) continue;         // in an earlier shard: a crossing entry (LfRange::isfb)
             if (first_in_row(R.prow, pa, k, p)) atomicMin(&R.lfirst[p - R.s], ref_key(gi, k - pa));
             continue;
         }

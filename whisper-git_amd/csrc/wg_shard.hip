@@ -19,16 +19,25 @@
 //       event ids, rewrites the records in place, replays the global event
 //       stream (latency-bound, ~the same cost at 8M rows as at 1M) and reads
 //       its own rows' lanes from it
-//   X6  per geometry pass: lanes, colours and endpoint y of crossing edges
-// Geometry then runs unchanged on a local problem: the shard's rows between a
-// zero-height head row (child of every edge coming from earlier shards) and a
-// zero-height tail row (parent of every edge leaving it), with the true
-// endpoint y of every edge supplied per edge.  row_top (sequential f32,
-// :329-335 / :374-381) is computed for rows [0, e) on every rank.
+//       X3 also carries, per crossing entry, the row token of its child row
+//       (from the child's shard) and of its parent row (from the parent's), so
+//       after the replay every rank reads the far endpoints' lanes itself.
+// Geometry then runs unchanged on a local problem with no exchange: the
+// shard's rows between a zero-height head row (child of every edge coming from
+// earlier shards) and a zero-height tail row (parent of every edge leaving
+// it), with the true endpoint y of every edge supplied per edge.  row_top
+// (sequential f32, :329-335 / :374-381) is computed for every row of the list
+// on every rank (side stream), so a far endpoint's y is local too, and a later
+// frame's geometry (new bands) takes no exchange at all.
 //
-// Lists that are not well formed (duplicate ids anywhere, parents at earlier
-// rows), that need more than 1023 lane slots or whose replay does not converge
-// fall back, on every rank alike, to the single-GPU build over the whole list.
+// Parents at earlier rows (clock skew, orphans re-sorted by time,
+// git/mod.rs:767-772) stay on this path as the single-GPU replay keeps them:
+// leaky references (:441-446) whose "first" decision (LfRange::lfirst, and
+// for a target in an earlier shard k_lf_xfirst with the target shard's
+// WG_XF_LLEAKY bit from X2) is the same on every rank.
+// Lists with duplicate ids, more than 1023 lane slots or a replay without
+// fixed point fall back, on every rank alike, to the single-GPU build over the
+// whole list.
 #include <cstring>
 #include <vector>
 
@@ -163,10 +172,11 @@ __global__ void k_sh_probe(uint64_t s, uint64_t e, const uint32_t *__restrict__ 
         prow_l[k - E0] = (int32_t)hash_find(load_key(poid + k * 20), oid, table, mask);
 }
 
-// per own row: count of the unresolved references; a parent at an earlier row
-// (or the row itself) or more than 2^16 parents flags a violation
+// per own row: count of the unresolved references; more than 2^16 parents
+// flags a violation.  A parent at this row or an earlier own row is leaky: its
+// row is marked in lk (its shard answers X2 with WG_XF_LLEAKY for it)
 __global__ void k_sh_ucnt(uint64_t s, uint64_t nl, const uint32_t *__restrict__ poff, const int32_t *__restrict__ prow_l,
-                          uint32_t *__restrict__ ucnt, uint32_t *flags) {
+                          uint32_t *__restrict__ ucnt, uint32_t *flags, uint8_t *__restrict__ lk) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nl) return;
     const uint64_t E0 = poff[s];
@@ -177,7 +187,7 @@ __global__ void k_sh_ucnt(uint64_t s, uint64_t nl, const uint32_t *__restrict__ 
     for (uint32_t k = pa; k < pb; k++) {
         const int32_t r = prow_l[k - E0];
         if (r < 0) nu++;
-        else if ((uint64_t)r <= gi) bad = true;
+        else if ((uint64_t)r <= gi) lk[(uint64_t)r - s] = 1;
     }
     ucnt[i] = nu;
     if (bad) atomicOr(&flags[0], 1u);
@@ -219,11 +229,16 @@ __device__ __forceinline__ uint32_t section_of(const Sections &S, uint64_t g) {
     return r;
 }
 
+// found row (bit 30: an own row at or after it references it: a leaky reference)
+constexpr int32_t SH_FOUND_LLEAKY = 0x40000000;
 __global__ void k_sh_probe_gathered(uint64_t L, const uint32_t *__restrict__ rec, const uint8_t *__restrict__ oid,
-                                    const unsigned long long *__restrict__ table, uint64_t mask, int32_t *__restrict__ found) {
+                                    const unsigned long long *__restrict__ table, uint64_t mask, uint64_t s,
+                                    const uint8_t *__restrict__ lk, int32_t *__restrict__ found) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= L) return;
-    found[g] = (int32_t)hash_find(load_key(reinterpret_cast<const uint8_t *>(rec + g * 8 + 2)), oid, table, mask);
+    int32_t r = (int32_t)hash_find(load_key(reinterpret_cast<const uint8_t *>(rec + g * 8 + 2)), oid, table, mask);
+    if (r >= 0 && lk[(uint64_t)r - s]) r |= SH_FOUND_LLEAKY;
+    found[g] = r;
 }
 
 // row of every unresolved reference of every rank: the shard that owns the id found it
@@ -236,9 +251,9 @@ __global__ void k_sh_combine(Sections F, uint64_t L, const uint32_t *__restrict_
         const int32_t v = reinterpret_cast<const int32_t *>(F.base + r * F.stride)[g];
         best = v > best ? v : best;
     }
-    row[g] = best;
+    row[g] = best;   // (ids are distinct when the build goes on: one rank found it)
     xflag[g] = best >= 0 ? 1u : 0u;
-    if (best >= 0 && (uint32_t)best <= rec[g * 8]) atomicOr(&flags[0], 1u);   // parent at an earlier row
+    (void)flags;
 }
 
 // crossing entries (every rank's resolved-elsewhere references, rank-major, row order)
@@ -253,15 +268,16 @@ __global__ void k_sh_xbuild(uint64_t L, const uint32_t *__restrict__ rec, const 
     for (uint64_t h = g; h > 0 && rec[(h - 1) * 8] == c; h--)
         if (row[h - 1] == row[g]) first = false;
     const uint32_t x = xpos[g];
+    const int32_t p = row[g] & ~SH_FOUND_LLEAKY;
     WgXEnt en;
     en.c = c;
-    en.p = (uint32_t)row[g];
-    en.kf = kidx | (first ? WG_XF_FIRST_IN_ROW : 0u);
+    en.p = (uint32_t)p;
+    en.kf = kidx | (first ? WG_XF_FIRST_IN_ROW : 0u) | ((row[g] & SH_FOUND_LLEAKY) ? WG_XF_LLEAKY : 0u);
     en.pad = 0;
     xall[x] = en;
     if (g >= own_lo && g < own_hi) {
         const uint64_t k = (uint64_t)poff[c] + kidx;
-        prow_l[k - E0] = row[g];
+        prow_l[k - E0] = p;
         refx[k - E0] = x - xpos[own_lo];
     }
 }
@@ -291,48 +307,61 @@ __global__ void k_sh_resolve(uint64_t nx, uint32_t world, const uint64_t *__rest
     }
 }
 
-// ---- X6: crossing-edge endpoints -----------------------------------------------------------
+// ---- crossing-edge endpoints (no exchange) ------------------------------------------------
 __device__ __forceinline__ float node_y_of(const float *__restrict__ band, uint64_t row) {
     return band ? roundf(band[row] + WG_NODE_Y) : WG_NODE_Y;   // (:390) / build default (:341)
 }
 
-// child records for own crossing entries, parent records for earlier entries into this shard
-__global__ void k_sh_pack_ends(uint64_t s, uint64_t e, const WgXEnt *__restrict__ xall, uint64_t xown_begin,
-                               uint64_t nown, uint64_t xin_end, const uint32_t *__restrict__ lane_l,
-                               const uint8_t *__restrict__ color_l, const float *__restrict__ rt_g,
-                               const float *__restrict__ band, uint4 *__restrict__ out) {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // child record {entry, lane, colour, y}; parent record {entry, lane, y, 0};
-    // entry ~0 = no record (row_top below the shard is not known here)
-    if (q < nown) {
-        const uint64_t x = xown_begin + q;
-        const uint64_t c = xall[x].c;
-        const float y = rt_g[c] + node_y_of(band, c);
-        out[q] = make_uint4((uint32_t)x, lane_l[c - s + 1], color_l[c - s + 1], __float_as_uint(y));
-    } else if (q < nown + xin_end) {
-        const uint64_t x = q - nown;
-        const uint64_t p = xall[x].p;
-        if (p >= s && p < e) {
-            const float y = rt_g[p] + node_y_of(band, p);
-            out[q] = make_uint4((uint32_t)x, lane_l[p - s + 1], __float_as_uint(y), 0u);
-        } else {
-            out[q] = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
-        }
+// the global tokens of every entry's child row and parent row (X3: the child's
+// shard sent the first, the parent's shard the second; NONE elsewhere)
+struct EndToks {
+    const uint8_t *base;
+    uint64_t stride, tok_a;   // rank r's ctok region at base + r stride + 16 + tok_a, its ptok region tok_a later
+    uint32_t world;
+};
+__device__ __forceinline__ uint32_t sh_globalize(uint32_t v, uint64_t ev_base, const uint32_t *__restrict__ xt) {
+    if (v == WG_TOK_NONE) return v;
+    if (v & WG_TOK_EV) return WG_TOK_EV | ((v & ~WG_TOK_EV) + (uint32_t)ev_base);
+    if (v & WG_TOK_X) return xt[v & ~WG_TOK_X];
+    return v;
+}
+__global__ void k_sh_etok(EndToks E, uint64_t nx, const uint64_t *__restrict__ xoff, const uint64_t *__restrict__ evoff,
+                          const uint32_t *__restrict__ xt, uint32_t *__restrict__ etok) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= nx) return;
+    uint32_t r = 0;
+    while (r + 1 < E.world && xoff[r + 1] <= x) r++;
+    const uint8_t *reg = E.base + r * E.stride + 16 + E.tok_a;
+    const uint32_t ct = sh_globalize(reinterpret_cast<const uint32_t *>(reg)[x - xoff[r]], evoff[r], xt);
+    uint32_t pt = WG_TOK_NONE;
+    for (uint32_t q = 0; q < E.world; q++) {
+        const uint32_t v = reinterpret_cast<const uint32_t *>(E.base + q * E.stride + 16 + 2 * E.tok_a)[x];
+        if (v != WG_TOK_NONE) pt = sh_globalize(v, evoff[q], xt);
     }
+    etok[2 * x] = ct;
+    etok[2 * x + 1] = pt;
 }
 
-// scatter every rank's endpoint records into per-entry tables
-struct RankCounts { uint64_t v[16]; };   // by value: no host buffer outlives the launch
+// after the replay: the lanes of both endpoints of every entry
+__global__ void k_sh_end_lanes(uint64_t n2, const uint32_t *__restrict__ etok, const uint16_t *__restrict__ slot_of,
+                               uint32_t *__restrict__ elane) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n2) return;
+    const uint32_t t = etok[i];
+    elane[i] = t == WG_TOK_NONE ? 0u : (uint32_t)slot_of[t & ~WG_TOK_EV];
+}
 
-__global__ void k_sh_unpack_ends(Sections S, RankCounts nown, uint4 *__restrict__ xchild, uint4 *__restrict__ xpar) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= S.off[S.world]) return;
-    const uint32_t r = section_of(S, g);
-    const uint64_t q = g - S.off[r];
-    const uint4 v = reinterpret_cast<const uint4 *>(S.base + r * S.stride + 16)[q];
-    if (v.x == 0xFFFFFFFFu) return;
-    if (q < nown.v[r]) xchild[v.x] = v;
-    else xpar[v.x] = v;
+// per entry: child record {entry, lane, colour, y}, parent record {entry, lane, y, 0}
+__global__ void k_sh_ends(uint64_t nx, const WgXEnt *__restrict__ xall, const uint32_t *__restrict__ elane,
+                          const uint8_t *__restrict__ flags, const float *__restrict__ rt_g, const float *__restrict__ band,
+                          uint4 *__restrict__ xchild, uint4 *__restrict__ xpar) {
+    const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= nx) return;
+    const WgXEnt en = xall[x];
+    const uint32_t lc = elane[2 * x], lp = elane[2 * x + 1];
+    const uint32_t col = (flags[en.c] & WG_FLAG_ORPHAN) ? (uint32_t)WG_COLOR_ORPHAN : lc % 6u;
+    xchild[x] = make_uint4((uint32_t)x, lc, col, __float_as_uint(rt_g[en.c] + node_y_of(band, en.c)));
+    xpar[x] = make_uint4((uint32_t)x, lp, __float_as_uint(rt_g[en.p] + node_y_of(band, en.p)), 0u);
 }
 
 // the local problem's rows: head (0), own rows (1..nl), tail (nl+1)
@@ -390,7 +419,11 @@ struct LocalEdgeArgs {
 
 __device__ __forceinline__ void far_parent(const LocalEdgeArgs &A, uint64_t p, uint64_t x, uint32_t *pl, uint32_t *plane,
                                            float *py) {
-    if (p < A.e) {
+    if (p < A.s) {   // an earlier shard's row (a leaky reference): the head row, skipped by the decomposition (:526-528)
+        *pl = 0;
+        *plane = A.xpar[x].y;
+        *py = 0.0f;
+    } else if (p < A.e) {
         *pl = (uint32_t)(p - A.s + 1);
         *plane = A.lane_l[p - A.s + 1];
         *py = A.rt_g[p] + node_y_of(A.band, p);
@@ -434,7 +467,8 @@ __global__ void k_sh_edges_own(LocalEdgeArgs A) {
         if (p < 0) continue;
         uint32_t pl, plane;
         float py;
-        far_parent(A, (uint64_t)p, (uint64_t)p >= A.e ? A.xown_begin + A.refx[k] : 0, &pl, &plane, &py);
+        far_parent(A, (uint64_t)p, ((uint64_t)p >= A.e || (uint64_t)p < A.s) ? A.xown_begin + A.refx[k] : 0, &pl, &plane,
+                   &py);
         A.edge_y[o] = make_float2(cy, py);
         if (A.y_only) { o++; continue; }
         wg_edge ed;
@@ -451,21 +485,6 @@ __global__ void k_sh_edges_own(LocalEdgeArgs A) {
     }
 }
 
-// a message's 16-byte header (kernel arguments: no host buffer outlives the call)
-// X6 header from the device: {own entries, incoming entries, replay words,
-// max_lane | first iteration that changed nothing << 16}.  Replay words (a
-// speculative X3 replay, else 0): bit 0 = no fixed point within the blind
-// iterations, bit 1 = past the occupancy width, slots << 2.
-__global__ void k_sh_x6_head(uint4 *__restrict__ dst, uint32_t nown, uint32_t xin, const uint32_t *__restrict__ flags,
-                             uint32_t it, const uint32_t *__restrict__ scal) {
-    uint32_t w2 = 0, w3 = 0;
-    if (flags) {
-        const bool conv = it == 0 || flags[it - 1] == 0 || flags[it] == 0;
-        w2 = (conv ? 0u : 1u) | (scal[2] ? 2u : 0u) | (min(scal[1], 0x3fffffffu) << 2);
-        w3 = min(scal[0], 0xffffu) | (min(scal[3], 0xffffu) << 16);
-    }
-    *dst = make_uint4(nown, xin, w2, w3);
-}
 // X1 header from the device: {violation | duplicate, unresolved references,
 // E0 = parent_off[s], E1 = parent_off[e]} and the message length
 __global__ void k_sh_x1_head(uint4 *__restrict__ dst, unsigned long long *__restrict__ len, const uint32_t *__restrict__ flags,
@@ -526,9 +545,9 @@ __global__ void k_sh_lane_out(uint64_t s, uint64_t nl, const uint32_t *__restric
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// exchange points: X1 unresolved references, X2 their rows, X3 chain tokens
-// and event records, X6 crossing-edge endpoints (per geometry pass)
-enum { SH_IDLE = 0, SH_X1, SH_X2, SH_X3, SH_X6 = 6 };
+// exchange points: X1 unresolved references, X2 their rows, X3 chain tokens,
+// endpoint row tokens and event records (geometry passes take none)
+enum { SH_IDLE = 0, SH_X1, SH_X2, SH_X3 };
 
 static int sh_send(wg_ctx *c, uint64_t bytes, wg_shard_msg *out) {
     WG_ALLOC(c, c->sh.msg, bytes + 64);
@@ -556,6 +575,7 @@ static int sh_send_dev(wg_ctx *c, uint64_t cap_bytes, wg_shard_msg *out) {
 static void sh_done(wg_ctx *c, wg_shard_msg *out) {
     c->sh.step = SH_IDLE;
     c->sh.build_band = nullptr;   // (build_frame's bands are the caller's: not kept past the call)
+    if (!out) return;             // (a deferred check settling after the call)
     out->send = nullptr;
     out->bytes = 0;
     out->done = 1;
@@ -657,82 +677,88 @@ static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
     return WG_OK;
 }
 
-// geometry pass, part 1: row_top of rows [s, e] (walked from row 0), endpoint records (X6)
-static int sh_geometry_begin(wg_ctx *c, const float *band_g, wg_shard_msg *out) {
+// the speculative X3 replay's words, checked with the local geometry's
+// validation read: {flags[it - 1], flags[it], max_lane, slots, overflow, first
+// iteration that changed nothing}
+constexpr int SH_REPLAY_ITEMS = 6;
+static int sh_replay_items(wg_ctx *c, WgFetch *it) {
+    const ShardState &S = c->sh;
+    it[0] = WgFetch{S.rp_it ? S.rp_flags + S.rp_it - 1 : S.rp_flags, false};
+    it[1] = WgFetch{S.rp_flags + S.rp_it, false};
+    for (int k = 0; k < 4; k++) it[2 + k] = WgFetch{S.rp_scal + k, false};
+    return SH_REPLAY_ITEMS;
+}
+
+static int sh_local_geometry(wg_ctx *c, const float *band_g, wg_shard_msg *out, bool allow_spec);
+
+// the lanes of both endpoints of every crossing entry, from the replay that just ran
+static void sh_end_lanes(wg_ctx *c) {
     ShardState &S = c->sh;
-    const uint64_t e = S.e;
+    const uint64_t n2 = 2 * S.xoff[S.world];
+    if (n2)
+        hipLaunchKernelGGL(k_sh_end_lanes, dim3(blocks(n2)), dim3(T), 0, c->stream, n2, S.etok.as<const uint32_t>(),
+                           c->lf_slot_of, S.elane.as<uint32_t>());
+}
+
+// the exact replay of the gathered global events (its lanes, the endpoints' lanes)
+static int sh_replay_exact(wg_ctx *c, bool *ok) {
+    ShardState &S = c->sh;
+    c->replay_death = S.death.as<const uint32_t>();
+    const int rc = wg_lf_replay_lanes(c, sh_range(c), c->n_events, c->lf[LF_EVREC].as<const uint4>(),
+                                      c->lf[LF_AUX].as<const uint32_t>(), c->lane_asg.as<uint32_t>(), ok);
+    c->replay_death = nullptr;
+    if (rc != WG_OK || !*ok) return rc;
+    c->lane_path = 0;
+    sh_graph_width(c);
+    sh_lane_out(c);
+    sh_end_lanes(c);
+    return WG_OK;
+}
+
+// A speculative replay's words: past its blind iterations or its width -> the
+// exact replay (*redo); else they are committed
+static int sh_replay_check(wg_ctx *c, const uint64_t *w, bool *redo, bool *fallback) {
+    ShardState &S = c->sh;
+    *redo = *fallback = false;
+    S.replay_pending = false;
+    const bool conv = S.rp_it == 0 || w[0] == 0 || w[1] == 0;
+    if (conv && !w[4]) {
+        wg_lf_replay_spec_commit(c, S.rp_it, S.rp_chunk, (uint32_t)w[2], (uint32_t)w[3], (uint32_t)w[5]);
+        sh_graph_width(c);
+        return WG_OK;
+    }
+    *redo = true;
+    c->spec_redo_lanes++;
+    bool ok = false;
+    const int rc = sh_replay_exact(c, &ok);
+    if (rc == WG_OK && !ok) *fallback = true;
+    return rc;
+}
+
+// The local geometry problem, with no exchange: the far endpoints' lanes from
+// the replay (etok -> elane), their y from the whole list's row_top; the
+// shard's rows between a head and a tail row; the unchanged geometry stages.
+static int sh_local_geometry(wg_ctx *c, const float *band_g, wg_shard_msg *out, bool allow_spec) {
+    ShardState &S = c->sh;
+    const uint64_t s = S.s, e = S.e, nl = e - s, nloc = nl + 2, nx = S.xoff[S.world];
+    hipStream_t st = c->stream;
     int rc = wg_side_join(c);
     if (rc != WG_OK) return rc;
     // the build's first pass takes the row_top the build began on the side
     // stream (its bands: none, or build_frame's); any later pass rescans
     if (!(S.rt_fresh && band_g == S.rt_band)) {
-        WG_ALLOC(c, S.rt_g, (e + 1) * 4);
-        if ((rc = wg_rowtop_run(c, e, S.h_g.as<const float>(), band_g, S.rt_g.as<float>(), S.s)) != WG_OK) return rc;
+        WG_ALLOC(c, S.rt_g, (S.N + 1) * 4);
+        if ((rc = wg_rowtop_run(c, S.N, S.h_g.as<const float>(), band_g, S.rt_g.as<float>(), 0)) != WG_OK) return rc;
     }
     S.rt_fresh = false;
     S.band_g = band_g;
-    const uint64_t nown = S.xoff[S.rank + 1] - S.xoff[S.rank], xin = S.xoff[S.rank];
-    S.step = SH_X6;
-    if ((rc = sh_send(c, 16 + (nown + xin) * 16, out)) != WG_OK) return rc;
-    hipLaunchKernelGGL(k_sh_x6_head, dim3(1), dim3(1), 0, c->stream, S.msg.as<uint4>(), (uint32_t)nown, (uint32_t)xin,
-                       S.replay_pending ? S.rp_flags : nullptr, S.rp_it, S.rp_scal);
-    if (nown + xin)
-        hipLaunchKernelGGL(k_sh_pack_ends, dim3(blocks(nown + xin)), dim3(T), 0, c->stream, S.s, S.e,
-                           S.xall.as<const WgXEnt>(), S.xoff[S.rank], nown, xin, c->lane_out.as<const uint32_t>(),
-                           c->color_out.as<const uint8_t>(), S.rt_g.as<const float>(), band_g,
-                           reinterpret_cast<uint4 *>(S.msg.as<uint8_t>() + 16));
-    WG_HIP(c, hipGetLastError());
-    return WG_OK;   // wg_shard_copy_msg orders the copy after these kernels
-}
-
-// geometry pass, part 2: the local problem and the unchanged geometry stages
-static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, wg_shard_msg *out) {
-    ShardState &S = c->sh;
-    const int W = S.world;
-    const uint64_t s = S.s, e = S.e, nl = e - s, nloc = nl + 2, nx = S.xoff[W];
-    hipStream_t st = c->stream;
-    std::vector<uint32_t> hdr;
-    int rc = read_headers(c, gathered, stride, hdr);
-    if (rc != WG_OK) return rc;
-    if (S.replay_pending) {
-        // the speculative X3 replay's words (every rank replayed the same
-        // stream; the OR keeps the decision common): no fixed point or past the
-        // width -> the exact replay, then this step's message again
-        S.replay_pending = false;
-        uint32_t redo = 0;
-        for (int r = 0; r < W; r++) redo |= hdr[4 * r + 2] & 3u;
-        if (redo) {
-            c->spec_redo_lanes++;
-            bool ok = false;
-            if ((rc = wg_lf_replay_lanes(c, sh_range(c), c->n_events, c->lf[LF_EVREC].as<const uint4>(),
-                                         c->lf[LF_AUX].as<const uint32_t>(), c->lane_asg.as<uint32_t>(), &ok)) != WG_OK)
-                return rc;
-            if (!ok) return sh_fallback(c, out);
-            sh_graph_width(c);
-            sh_lane_out(c);
-            S.rt_fresh = true;   // row_top does not depend on the lanes
-            S.rt_band = S.band_g;
-            return sh_geometry_begin(c, S.band_g, out);
-        }
-        const uint32_t w2 = hdr[4 * S.rank + 2], w3 = hdr[4 * S.rank + 3];
-        wg_lf_replay_spec_commit(c, S.rp_it, S.rp_chunk, w3 & 0xffffu, w2 >> 2, w3 >> 16);
-        sh_graph_width(c);
-    }
-    std::vector<uint64_t> cnt(W);
-    RankCounts nown{};
-    for (int r = 0; r < W; r++) {
-        nown.v[r] = hdr[4 * r];
-        cnt[r] = (uint64_t)hdr[4 * r] + hdr[4 * r + 1];
-        if ((rc = check_len(c, r, 16 + cnt[r] * 16, "X6 endpoint records")) != WG_OK) return rc;
-    }
     WG_ALLOC(c, S.xchild, nx * 16 + 16);
     WG_ALLOC(c, S.xpar, nx * 16 + 16);
-    Sections SX = make_sections(gathered, stride, W, cnt);
-    if (SX.off[W])
-        hipLaunchKernelGGL(k_sh_unpack_ends, dim3(blocks(SX.off[W])), dim3(T), 0, st, SX, nown, S.xchild.as<uint4>(),
+    if (nx)
+        hipLaunchKernelGGL(k_sh_ends, dim3(blocks(nx)), dim3(T), 0, st, nx, S.xall.as<const WgXEnt>(),
+                           S.elane.as<const uint32_t>(), c->d_flags, S.rt_g.as<const float>(), band_g, S.xchild.as<uint4>(),
                            S.xpar.as<uint4>());
     // local rows
-    const float *band_g = S.band_g;
     WG_ALLOC(c, c->heights, nloc * 4 + 4);
     WG_ALLOC(c, c->g_row_top, (nloc + 1) * 4);
     if (band_g) WG_ALLOC(c, c->band, nloc * 4 + 4);
@@ -748,8 +774,19 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     // speculatively once an earlier pass sized the buffers: local edges sized
     // by their bounds (incoming <= the earlier shards' crossing entries, own <=
     // the shard's references), the geometry lists by capacity, one read at
-    // the end (wg_layout_build's scheme).
-    const bool spec = !same_layout && S.geom_spec_ready;
+    // the end (wg_layout_build's scheme).  A speculative
+    // replay (X3) is checked with the same read.
+    const bool spec = allow_spec && !same_layout && S.geom_spec_ready;
+    if (S.replay_pending && !spec) {   // (nothing to ride on: its words now)
+        WgFetch it[SH_REPLAY_ITEMS];
+        uint64_t w[SH_REPLAY_ITEMS] = {0};
+        sh_replay_items(c, it);
+        if ((rc = wg_fetch_n(c, SH_REPLAY_ITEMS, it, w)) != WG_OK) return rc;
+        bool redo = false, fb = false;
+        if ((rc = sh_replay_check(c, w, &redo, &fb)) != WG_OK) return rc;
+        if (fb) return sh_fallback(c, out);
+        if (redo) return sh_local_geometry(c, band_g, out, false);
+    }
     if (!same_layout) {
         WG_ALLOC(c, S.in_scan, (xin + 2) * 4);
         WG_ALLOC(c, c->edge_cnt, (nloc + 2) * 4);
@@ -813,15 +850,17 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
     c->spec = false;
     if (rc != WG_OK) return rc;
     if (spec) {
-        WgFetch it[WG_GEOM_SPEC_ITEMS + 4];
+        WgFetch it[WG_GEOM_SPEC_ITEMS + 2 + SH_REPLAY_ITEMS];
         int k = wg_geom_spec_items(c, it);
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + nloc, false};
         it[k++] = WgFetch{c->edge_cnt.as<uint32_t>() + 1, false};
-        static_assert(WG_GEOM_SPEC_ITEMS + 2 <= WG_PENDING_ITEMS, "shard geometry words exceed a pending build's");
+        if (S.replay_pending) k += sh_replay_items(c, it + k);
+        static_assert(WG_GEOM_SPEC_ITEMS + 2 + SH_REPLAY_ITEMS <= WG_PENDING_ITEMS, "shard geometry words exceed a pending build's");
         if (c->defer_validation) {
             // no host read: the words ride on the emission's vertex-total read
             // (the emission is gated on the pass's overflow words, as after a
-            // deferred single-GPU build); any host query settles them first
+            // deferred single-GPU build; graph_width from the device while the
+            // replay is unchecked); any host query settles them first
             PendingBuild &P = c->pend;
             P = PendingBuild{};
             P.build = true;
@@ -829,17 +868,18 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
             P.k = k;
             for (int i = 0; i < k; i++) P.it[i] = it[i];
             c->have_geom = true;
-            sh_done(c, out);
+            if (out) sh_done(c, out);
             return WG_OK;
         }
-        uint64_t v[WG_GEOM_SPEC_ITEMS + 4] = {0};
+        uint64_t v[WG_GEOM_SPEC_ITEMS + 2 + SH_REPLAY_ITEMS] = {0};
         if ((rc = wg_fetch_n(c, k, it, v)) != WG_OK) return rc;
         bool redo = false;
         if ((rc = wg_shard_geom_validate(c, v, &redo)) != WG_OK) return rc;
+        if (c->sh.replicated) { if (out) sh_done(c, out); return WG_OK; }   // (the replay fell back)
     }
     S.geom_spec_ready = c->lists_gen == c->layout_gen;
     c->have_geom = true;
-    sh_done(c, out);
+    if (out) sh_done(c, out);
     return WG_OK;
 }
 
@@ -849,6 +889,24 @@ static int sh_geometry_finish(wg_ctx *c, const void *gathered, uint64_t stride, 
 int wg_shard_geom_validate(wg_ctx *c, const uint64_t *v, bool *redo) {
     ShardState &S = c->sh;
     *redo = false;
+    if (S.replay_pending) {   // the speculative replay first: new lanes redo the local geometry exactly
+        bool rr = false, fb = false;
+        int rc = sh_replay_check(c, v + WG_GEOM_SPEC_ITEMS + 2, &rr, &fb);
+        if (rc != WG_OK) return rc;
+        if (fb) {
+            *redo = true;
+            return sh_fallback(c, nullptr);
+        }
+        if (rr) {
+            *redo = true;
+            c->spec_redo_geom++;
+            c->lists_gen = ~0ull;
+            S.local_gen = ~0ull;
+            S.rt_fresh = true;   // (row_top does not depend on the lanes)
+            S.rt_band = S.band_g;
+            return sh_local_geometry(c, S.band_g, nullptr, false);
+        }
+    }
     S.local_ne = v[WG_GEOM_SPEC_ITEMS];
     S.local_nin = v[WG_GEOM_SPEC_ITEMS + 1];
     c->n_edges = S.local_ne;
@@ -950,13 +1008,13 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
     // sized by the list's reference count and indexed from parent_off[s] on
     // the device.
     const uint64_t nl = row_end - row_begin, El = S.Etot;
-    // heights of rows [0, e) (the last row of the LIST is ROW_HEIGHT) and the
-    // row_top of the own rows (zero bands, or build_frame's): side stream,
-    // overlapping the exchanges
+    // heights and row_top of every row of the list (zero bands, or
+    // build_frame's): side stream, overlapping the exchanges; the crossing
+    // edges' far endpoints read their y from it
     c->n_list = N;
-    WG_ALLOC(c, S.h_g, row_end * 4 + 4);
-    WG_ALLOC(c, S.rt_g, (row_end + 1) * 4);
-    int rc = wg_side_zero_rowtop(c, row_end, S.h_g.as<float>(), S.rt_g.as<float>(), row_begin, S.build_band);
+    WG_ALLOC(c, S.h_g, N * 4 + 4);
+    WG_ALLOC(c, S.rt_g, (N + 1) * 4);
+    int rc = wg_side_zero_rowtop(c, N, S.h_g.as<float>(), S.rt_g.as<float>(), 0, S.build_band);
     if (rc != WG_OK) return rc;
     S.rt_fresh = true;
     S.rt_band = S.build_band;
@@ -970,12 +1028,14 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
     WG_ALLOC(c, S.dlist, (uint64_t)dup_blocks(N) * (T * DUP_R * 16 + 4) + 16);
     WG_ALLOC(c, S.prow, El * 4 + 4);
     WG_ALLOC(c, S.xcnt, (nl + 2) * 4);
+    WG_ALLOC(c, S.lk, nl + 16);
     WG_ALLOC(c, S.flags, 64);
     { const int _sr = wg_scan_reserve(c, nl + 2); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "hash_join");
     WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8, st));
     WG_HIP(c, hipMemsetAsync(S.ptable.p, 0xFF, pcap * 8, st));
     WG_HIP(c, hipMemsetAsync(S.flags.p, 0, 64, st));
+    WG_HIP(c, hipMemsetAsync(S.lk.p, 0, nl + 16, st));
     if (nl) hipLaunchKernelGGL(k_sh_place, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
                                c->hash.as<unsigned long long>(), cap - 1);
     const uint32_t nbd = dup_blocks(N);
@@ -990,7 +1050,7 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
         hipLaunchKernelGGL(k_sh_probe, dim3(blocks(nl + nl / 2)), dim3(T), 0, st, row_begin, row_end, c->d_poff, c->d_poid,
                            c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>());
         hipLaunchKernelGGL(k_sh_ucnt, dim3(blocks(nl)), dim3(T), 0, st, row_begin, nl, c->d_poff,
-                           S.prow.as<const int32_t>(), S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>());
+                           S.prow.as<const int32_t>(), S.xcnt.as<uint32_t>(), S.flags.as<uint32_t>(), S.lk.as<uint8_t>());
     }
     WG_HIP(c, wg_exclusive_scan_u32(S.xcnt.as<uint32_t>(), S.xcnt.as<uint32_t>(), nl, c->scan_tmp.p, st));
     c->hcap = cap;
@@ -1128,7 +1188,8 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         S.step = SH_X2;
         if ((rc = sh_send(c, L * 4, out)) != WG_OK) return rc;
         if (L) hipLaunchKernelGGL(k_sh_probe_gathered, dim3(blocks(L)), dim3(T), 0, st, L, S.unres.as<const uint32_t>(),
-                                  c->d_oid, c->hash.as<const unsigned long long>(), c->hcap - 1, S.msg.as<int32_t>());
+                                  c->d_oid, c->hash.as<const unsigned long long>(), c->hcap - 1, S.s,
+                                  (const uint8_t *)S.lk.as<uint8_t>(), S.msg.as<int32_t>());
         WG_HIP(c, hipGetLastError());
         return WG_OK;
     }
@@ -1167,6 +1228,8 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         R.xown_end = L;
         R.xb_dev = S.xtok.as<const uint32_t>() + S.uoffs[S.rank];
         R.xe_dev = S.xtok.as<const uint32_t>() + S.uoffs[S.rank + 1];
+        WG_ALLOC(c, c->lf[LF_LFIRST], nl * 8 + 8);
+        R.lfirst = c->lf[LF_LFIRST].as<unsigned long long>();   // parents at earlier own rows (leaky)
         wg_stage_begin(c, "lanes");
         // The message (header, tokens, then the event records and merge-token
         // lists) is bounded by the rows' references (a row makes at most
@@ -1181,7 +1244,10 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         if ((rc = wg_lf_refs(c, R, false)) != WG_OK) return rc;
         if ((rc = wg_lf_chain(c, R)) != WG_OK) return rc;
         wg_stage_end(c);
-        const uint64_t tok_b = (L * 4 + 15) & ~15ull;          // records start 16-byte aligned (same on every rank)
+        // token regions (each L words, 16-byte aligned, the same on every rank):
+        // own entries' chain tokens, own entries' child row tokens, parent row
+        // tokens by global entry; then the records
+        const uint64_t tok_a = (L * 4 + 15) & ~15ull, tok_b = 3 * tok_a;
         const uint64_t ev_cap = nl + El, aux_cap = 2 * (nl + El + L) + 16;
         S.step = SH_X3;
         if ((rc = sh_send_dev(c, 16 + tok_b + ev_cap * 16 + aux_cap * 4, out)) != WG_OK) return rc;
@@ -1191,6 +1257,9 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
                            R.xe_dev, (S.geom_spec_ready && c->spec_replay_shard) ? 4u : 0u, ev_cap, aux_cap);
         uint8_t *m = S.msg.as<uint8_t>() + 16;
         if ((rc = wg_lf_export_tokens(c, R, reinterpret_cast<uint32_t *>(m))) != WG_OK) return rc;
+        if ((rc = wg_lf_export_ends(c, R, reinterpret_cast<uint32_t *>(m + tok_a), reinterpret_cast<uint32_t *>(m + 2 * tok_a),
+                                    S.xtok.as<const uint32_t>() + L, L)) != WG_OK)
+            return rc;
         // the event records travel in the same message, with shard-local tokens
         if ((rc = wg_lf_events_local(c, R, reinterpret_cast<uint4 *>(m + tok_b), nullptr)) != WG_OK) return rc;
         return WG_OK;
@@ -1202,12 +1271,12 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         S.auxoff.assign(W + 1, 0);
         S.xoff.assign(W + 1, 0);
         bool bad = false, spec_all = true;
-        const uint64_t L = S.uoffs[W], tok_b = (L * 4 + 15) & ~15ull;
+        const uint64_t L = S.uoffs[W], tok_a = (L * 4 + 15) & ~15ull, tok_b = 3 * tok_a;
         for (int r = 0; r < W; r++) {
             S.evoff[r + 1] = S.evoff[r] + hdr[4 * r];
             S.auxoff[r + 1] = S.auxoff[r] + hdr[4 * r + 1];
             S.xoff[r + 1] = S.xoff[r] + hdr[4 * r + 3];   // own crossing entries (X2 left them on the device)
-            bad |= (hdr[4 * r + 2] & 3u) != 0;            // not well formed, or a parent at an earlier row
+            bad |= (hdr[4 * r + 2] & 3u) != 0;            // not well formed
             spec_all &= (hdr[4 * r + 2] & 4u) != 0;       // every rank may replay speculatively
         }
         if (S.xoff[W] > L)
@@ -1254,6 +1323,18 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
                                       evrec.as<uint4>(), aux.as<uint32_t>())) != WG_OK)
             return rc;
         c->n_events = nev;
+        // the endpoints' row tokens (global), and every token's consumption time
+        WG_ALLOC(c, S.etok, nx * 8 + 16);
+        WG_ALLOC(c, S.elane, nx * 8 + 16);
+        if (nx) {
+            EndToks E{(const uint8_t *)gathered, stride, tok_a, (uint32_t)W};
+            hipLaunchKernelGGL(k_sh_etok, dim3(blocks(nx)), dim3(T), 0, st, E, nx, S.dev_small.as<const uint64_t>(),
+                               S.dev_small.as<const uint64_t>() + 20, S.xt.as<const uint32_t>(), S.etok.as<uint32_t>());
+        }
+        WG_ALLOC(c, S.death, (nev + 256) * 4);
+        if ((rc = wg_lf_death_from_records(c, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(), S.death.as<uint32_t>())) !=
+            WG_OK)
+            return rc;
         WG_ALLOC(c, c->lane_asg, nl * 4 + 4);
         const uint64_t nloc = nl + 2;
         WG_ALLOC(c, c->lane_out, nloc * 4 + 4);
@@ -1262,34 +1343,31 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
         if (nev && spec_all) {
             // after a sharded build sized every rank's context (a decision all
             // ranks take alike, from the X3 heads): the blind iterations with
-            // no host read, the words checked with the X6 headers
+            // no host read, the words checked with the local geometry's
             ReplayRun run;
-            if ((rc = wg_lf_replay_lanes_spec(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
-                                              c->lane_asg.as<uint32_t>(), run)) != WG_OK)
-                return rc;
+            c->replay_death = S.death.as<const uint32_t>();
+            rc = wg_lf_replay_lanes_spec(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
+                                         c->lane_asg.as<uint32_t>(), run);
+            c->replay_death = nullptr;
+            if (rc != WG_OK) return rc;
             S.replay_pending = true;
             c->spec_replays_shard++;
             S.rp_it = run.it;
             S.rp_chunk = run.chunk;
             S.rp_flags = run.flags;
             S.rp_scal = run.scal;
+            sh_lane_out(c);
+            sh_end_lanes(c);
         } else {
             bool ok = false;
-            if ((rc = wg_lf_replay_lanes(c, R, nev, evrec.as<const uint4>(), aux.as<const uint32_t>(),
-                                         c->lane_asg.as<uint32_t>(), &ok)) != WG_OK)
-                return rc;
-            if (!ok) return sh_fallback(c, out);        // no fixed point / > 63 slots: same decision on every rank
-            c->lane_path = 0;
-            sh_graph_width(c);
+            if ((rc = sh_replay_exact(c, &ok)) != WG_OK) return rc;
+            if (!ok) return sh_fallback(c, out);        // no fixed point / > 1023 slots: same decision on every rank
         }
-        sh_lane_out(c);
         c->have_layout = true;
         c->layout_gen++;
         c->alt_heights_on = false;   // (a new built list: its own heights)
-        return sh_geometry_begin(c, S.build_band, out);   // the default geometry, or build_frame's
+        return sh_local_geometry(c, S.build_band, out, true);   // the default geometry, or build_frame's
     }
-    case SH_X6:
-        return sh_geometry_finish(c, gathered, stride, out);
     default:
         return wg_fail(c, WG_E_STATE, "bad shard step %d", S.step);
     }
@@ -1323,7 +1401,7 @@ int wg_shard_geometry_begin(wg_ctx *c, const float *band, int32_t residency, wg_
         return WG_OK;
     }
     c->have_geom = false;
-    return sh_geometry_begin(c, d_band, out);
+    return sh_local_geometry(c, d_band, out, true);
 }
 
 }  // extern "C"

@@ -458,9 +458,10 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const int npend = c->pend.build ? c->pend.k : 0;
     for (int i = 0; i < npend; i++) fi[1 + i] = c->pend.it[i];
     if (const int rc = wg_fetch_begin_n(c, 1 + npend, fi)) return rc;
-    // (a pending single-GPU build: graph_width from the device's lane scalars;
-    // a sharded build's lanes are exact already)
-    const uint32_t *ml_dev = npend && !c->pend.shard ? c->lane_scalars.as<const uint32_t>() : nullptr;
+    // (a pending single-GPU build, or a sharded one whose replay is unchecked:
+    // graph_width from the device's lane scalars)
+    const uint32_t *ml_dev =
+        npend && (!c->pend.shard || c->sh.replay_pending) ? c->lane_scalars.as<const uint32_t>() : nullptr;
     // search-match flags of global rows [match_rb, match_re) -> context rows [mlo, mhi)
     const uint8_t *match = c->match_on ? c->match_flags.as<const uint8_t>() : nullptr;
     const int64_t mlo = (int64_t)c->match_rb - (int64_t)c->sh.s + (int64_t)c->sh.row_base;
