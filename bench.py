@@ -545,7 +545,7 @@ def main():
             eng.row_geometry(device_ptr=t_band.data_ptr())
         elif comm is None:   # the same two calls, the build's geometry pass taking the bands
             eng.build_frame(commits=commits, device_ptr=t_band.data_ptr())
-        elif not args.no_build_frame:   # sharded: 4 exchanges instead of 5
+        elif not args.no_build_frame:   # sharded: 3 exchanges (X1-X3), one geometry pass instead of two
             eng.shard_build_frame(commits, world, rank, shard0, shard1, comm, device_ptr=t_band.data_ptr())
         else:
             eng.shard_build(commits, world, rank, shard0, shard1, comm)

@@ -226,9 +226,10 @@ int         wg_synchronize(wg_ctx *ctx);
 /* WG_OPT_SHARD_SPEC_REPLAY: 1 (default) = once a sharded build sized the
  * context, the X3 step replays the global lane events for the blind
  * iteration count without a host read; the replay's convergence and width
- * words travel in the X6 headers, and a replay that did not reach its fixed
- * point is redone exactly at X6 (whose message is then sent again: one more
- * exchange round, same results).  0 = the replay is checked before X3 returns. */
+ * words are read with the local geometry pass's validation words, and a
+ * replay that did not reach its fixed point is redone exactly with that
+ * pass (no extra exchange, same results).  0 = the replay is checked before
+ * the geometry pass. */
 #define WG_OPT_SHARD_SPEC_REPLAY 7
 /* WG_OPT_REPLAY_MODE: how the lane events are replayed.  0 (default) = auto:
  * the chunked fixed point, and for lists on which it needs more iterations
@@ -320,13 +321,16 @@ int wg_shard_build_begin(wg_ctx *ctx, const wg_commits *commits, int world, int 
                          uint64_t row_begin, uint64_t row_end, wg_shard_msg *out);
 /* wg_shard_build_begin then wg_shard_geometry_begin(band) in one sharded
  * call (history_view's first frame after a refresh, commit_graph.rs:1419-
- * 1421): the build's own geometry pass takes the bands — one exchange and one
- * geometry pass fewer per step; the banded row_top runs on the side stream
- * beside the build.  band = the whole [N] array; a device band must stay
- * valid until the call is done (done = 1).  Results identical to the two calls. */
+ * 1421): the build's own geometry pass takes the bands — one geometry pass
+ * fewer per step; the banded row_top runs on the side stream beside the
+ * build.  Three exchanges (X1, X2, X3) either way.  band = the whole [N]
+ * array; a device band must stay valid until the call is done (done = 1).
+ * Results identical to the two calls. */
 int wg_shard_build_frame_begin(wg_ctx *ctx, const wg_commits *commits, int world, int rank, uint64_t row_begin,
                                uint64_t row_end, const float *band, int32_t band_residency, wg_shard_msg *out);
-/* row_geometry_with_bands (:367-399) of the shard; band = the whole [N] array. */
+/* row_geometry_with_bands (:367-399) of the shard; band = the whole [N]
+ * array.  No exchange: the crossing edges' far endpoints (lanes from the
+ * build's X3, y from the whole list's row_top) are local; done = 1 on return. */
 int wg_shard_geometry_begin(wg_ctx *ctx, const float *band, int32_t band_residency, wg_shard_msg *out);
 #define WG_SHARD_BYTES_ON_DEVICE UINT64_MAX
 /* Copy this rank's current message (device or host destination). */
@@ -525,7 +529,7 @@ int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
  * (0 single, 1 row-sharded, 2 row-sharded request built whole), [6]
  * speculative builds (one host read per build) on this context, [7] of
  * which the lanes and [8] the geometry were redone by the exact stages
- * (a sharded build's blind global replay redone at X6 counts in [7]), [9]
+ * (a sharded build's blind global replay redone exactly counts in [7]), [9]
  * sharded builds whose global lane replay ran blind (WG_OPT_SHARD_SPEC_REPLAY),
  * [10] 1 if the last lane replay was the single-wave serial pass
  * (WG_OPT_REPLAY_MODE). */

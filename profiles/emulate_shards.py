@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--replay", default=None, help="CHUNK:WARM: fixed replay chunk / warm-up (options 2 and 6)")
     ap.add_argument("--no-spec-replay", action="store_true", help="WG_OPT_SHARD_SPEC_REPLAY 0: X3 checks its replay")
     ap.add_argument("--two-calls", action="store_true",
-                    help="shard_build + shard_geometry (5 exchanges) instead of shard_build_frame (4)")
+                    help="shard_build + shard_geometry (two geometry passes) instead of shard_build_frame (3 exchanges either way)")
     args = ap.parse_args()
 
     import torch

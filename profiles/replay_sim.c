@@ -212,7 +212,7 @@ static void run(const char *name, int scheme, uint32_t CH, uint32_t warm) {
                 }
             }
             xnext[c] = o;
-            if (cc || (scheme == S_EXIT && !occ_eq(&xnext[c], &xprev[c])) || ew < e0) changed = 1;
+            if (cc || (scheme == S_EXIT && !occ_eq(&xnext[c], &xprev[c])) || (ew < e0 && scheme != S_LIVEWARM && it == 1)) changed = 1;
             nchg += cc;
             if (cc > maxchg) maxchg = cc;
             if (wrong) { wrong_chunks++; if (c < first_wrong) first_wrong = c; }
@@ -229,6 +229,136 @@ static void run(const char *name, int scheme, uint32_t CH, uint32_t warm) {
     printf("], \"fixed_point_at\": %d, \"wrong_at_end\": %lu}\n", it, (unsigned long)bad);
     fflush(stdout);
     free(prev); free(next); free(own); free(xprev); free(xnext); free(death); free(lcnt); free(live); free(fill);
+}
+
+/* longseed: the tokens whose life exceeds `warm` events (or that leak) get
+ * their slots first, one after the other, each from a replay of the `warm`
+ * events before its allocation seeded with the long tokens alive there
+ * (level A); then iteration 1 replays every chunk from `warm` events early
+ * seeded the same way, and later iterations take the exit scheme. */
+static occ_t LAST_OCC;
+static uint32_t replay_window(uint64_t ew, uint64_t e1, const uint32_t *seed_tok, const uint16_t *seed_slot, uint32_t nseed,
+                              uint16_t *own, const uint16_t *prev) {
+    occ_t o;
+    memset(&o, 0, sizeof(o));
+    static uint16_t *sslot = NULL;
+    static uint64_t cap = 0;
+    if (cap < NEV) { free(sslot); sslot = malloc(NEV * 2); cap = NEV; }
+    for (uint32_t q = 0; q < nseed; q++) { occ_set(&o, seed_slot[q]); sslot[seed_tok[q]] = seed_slot[q]; }
+    uint32_t s = 0;
+    for (uint64_t k = ew; k < e1; k++) {
+        if (EV[k].a) {
+            s = occ_lowest_free(&o);
+            if (EV[k].o) occ_set(&o, s);
+        } else {
+            uint32_t m = 0xFFFFu;
+            for (uint32_t q = 0; q < EV[k].ntok; q++) {
+                const uint32_t t = TOK[EV[k].tok0 + q];
+                uint32_t ts;
+                if (t >= ew) ts = own[t];
+                else {
+                    int seeded = 0;
+                    for (uint32_t z = 0; z < nseed; z++) if (seed_tok[z] == t) { seeded = 1; break; }
+                    if (!seeded) continue;   /* a ghost: its slot is not in the table */
+                    ts = sslot[t];
+                }
+                occ_clr(&o, ts);
+                if (ts < m) m = ts;
+            }
+            if (EV[k].o && m != 0xFFFFu) occ_set(&o, m);
+            s = m;
+        }
+        own[k] = (uint16_t)s;
+    }
+    (void)prev;
+    LAST_OCC = o;
+    return s;
+}
+
+static void run_longseed(uint32_t CH, uint32_t warm) {
+    uint64_t *death = malloc(NEV * 8);
+    for (uint64_t k = 0; k < NEV; k++) death[k] = NEV;   /* never */
+    for (uint64_t k = 0; k < NEV; k++)
+        for (uint32_t q = 0; q < EV[k].ntok; q++) death[TOK[EV[k].tok0 + q]] = k;
+    uint32_t *lt = malloc(NEV * 4), nl = 0;
+    for (uint64_t k = 0; k < NEV; k++)
+        if (EV[k].o && death[k] - k > warm) lt[nl++] = (uint32_t)k;
+    uint16_t *ls = malloc((nl + 1) * 2), *own = calloc(NEV, 2);
+    uint32_t *stok = malloc((nl + 1) * 4);
+    uint16_t *sslot = malloc((nl + 1) * 2);
+    uint64_t wrongA = 0, replayed = 0;
+    for (uint32_t j = 0; j < nl; j++) {
+        const uint64_t a = lt[j], ew = a > warm ? a - warm : 0;
+        uint32_t ns = 0;
+        for (uint32_t i = 0; i < j; i++)
+            if (lt[i] < ew && death[lt[i]] >= ew) { stok[ns] = lt[i]; sslot[ns] = ls[i]; ns++; }
+        ls[j] = (uint16_t)replay_window(ew, a + 1, stok, sslot, ns, own, NULL);
+        replayed += a + 1 - ew;
+        if (ls[j] != EV[a].slot) wrongA++;
+    }
+    /* iteration 1: every chunk from warm early, seeded with the long tokens alive there */
+    const uint64_t nch = (NEV + CH - 1) / CH;
+    occ_t *XP = calloc(nch, sizeof(occ_t)), *XN = calloc(nch, sizeof(occ_t));
+    uint16_t *PV = calloc(NEV, 2), *NX = calloc(NEV, 2);
+    uint64_t wrong_chunks = 0, wrong_ev = 0, first_wrong = nch;
+    for (uint64_t c = 0; c < nch; c++) {
+        const uint64_t e0 = c * CH, e1 = e0 + CH < NEV ? e0 + CH : NEV, ew = e0 > warm ? e0 - warm : 0;
+        uint32_t ns = 0;
+        for (uint32_t i = 0; i < nl; i++)
+            if (lt[i] < ew && death[lt[i]] >= ew) { stok[ns] = lt[i]; sslot[ns] = ls[i]; ns++; }
+        replay_window(ew, e1, stok, sslot, ns, own, NULL);
+        XP[c] = LAST_OCC;
+        for (uint64_t k = e0; k < e1; k++) PV[k] = own[k];
+        uint64_t w = 0;
+        for (uint64_t k = e0; k < e1; k++) w += own[k] != EV[k].slot;
+        if (w) { wrong_chunks++; if (c < first_wrong) first_wrong = c; }
+        wrong_ev += w;
+    }
+    printf("{\"scheme\": \"longseed\", \"chunk\": %u, \"warm\": %u, \"events\": %lu, \"long_tokens\": %u, "
+           "\"level_a_events\": %lu, \"level_a_wrong\": %lu, \"it1_wrong_chunks\": %lu, \"it1_first_wrong\": %lu, "
+           "\"it1_wrong_events\": %lu, \"chunks\": %lu}\n",
+           CH, warm, (unsigned long)NEV, nl, (unsigned long)replayed, (unsigned long)wrongA, (unsigned long)wrong_chunks,
+           (unsigned long)first_wrong, (unsigned long)wrong_ev, (unsigned long)nch);
+    /* then the exit scheme to the fixed point */
+    int it;
+    for (it = 2; it <= 100000; it++) {
+        int changed = 0;
+        for (uint64_t c = 0; c < nch; c++) {
+            const uint64_t e0 = c * CH, e1 = e0 + CH < NEV ? e0 + CH : NEV;
+            occ_t o;
+            memset(&o, 0, sizeof(o));
+            if (c) o = XP[c - 1];
+            uint64_t cc = 0;
+            for (uint64_t k = e0; k < e1; k++) {
+                uint32_t sl;
+                if (EV[k].a) { sl = occ_lowest_free(&o); if (EV[k].o) occ_set(&o, sl); }
+                else {
+                    uint32_t m = 0xFFFFu;
+                    for (uint32_t q = 0; q < EV[k].ntok; q++) {
+                        const uint32_t t = TOK[EV[k].tok0 + q];
+                        const uint32_t ts = t < e0 ? PV[t] : own[t];
+                        occ_clr(&o, ts);
+                        if (ts < m) m = ts;
+                    }
+                    if (EV[k].o) occ_set(&o, m);
+                    sl = m;
+                }
+                own[k] = (uint16_t)sl;
+                NX[k] = (uint16_t)sl;
+                cc += NX[k] != PV[k];
+            }
+            XN[c] = o;
+            if (cc || !occ_eq(&XN[c], &XP[c])) changed = 1;
+        }
+        uint16_t *t = PV; PV = NX; NX = t;
+        occ_t *x = XP; XP = XN; XN = x;
+        if (!changed) break;
+    }
+    uint64_t bad = 0;
+    for (uint64_t k = 0; k < NEV; k++) bad += PV[k] != EV[k].slot;
+    printf("{\"longseed_then_exit_fixed_point_at\": %d, \"wrong_at_end\": %lu}\n", it, (unsigned long)bad);
+    free(XP); free(XN); free(PV); free(NX);
+    free(death); free(lt); free(ls); free(own); free(stok); free(sslot);
 }
 
 int main(int argc, char **argv) {
@@ -259,6 +389,7 @@ int main(int argc, char **argv) {
                (unsigned long)NEV, (unsigned long)cev, (unsigned long)occupying, (unsigned long)leaked, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
         return 0;
     }
+    if (argc > 5 && !strcmp(argv[5], "longseed")) { run_longseed(CH, warm); wgs_free(d); return 0; }
     for (int a = 5; a < argc || a == 5; a++) {
         const char *s = a < argc ? argv[a] : "exit";
         run(s, !strcmp(s, "live") ? S_LIVE : !strcmp(s, "livewarm") ? S_LIVEWARM : S_EXIT, CH, warm);

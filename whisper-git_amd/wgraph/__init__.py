@@ -199,8 +199,9 @@ class Engine:
 
     def set_shard_spec_replay(self, on: bool):
         """WG_OPT_SHARD_SPEC_REPLAY: the sharded build's X3 step replays the
-        global lane events without a host read, the replay checked with the X6
-        headers (default on; a replay that misses is redone there)."""
+        global lane events without a host read, the replay checked with the
+        local geometry pass's validation words (default on; a replay that
+        misses is redone there, no extra exchange)."""
         self._check(lib().wg_set_option(self._ctx, 7, 1 if on else 0))
 
     # -- layout ----------------------------------------------------------------------
