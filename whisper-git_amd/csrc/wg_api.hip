@@ -154,6 +154,31 @@ int wg_side_zero_rowtop(wg_ctx *c, uint64_t m, float *h, float *rt, uint64_t row
     return rc;
 }
 
+int wg_side_build_begin(wg_ctx *c, uint64_t m, float *h, float *rt, const float *band, const float *band_host,
+                        float *band_dev) {
+    int rc = wg_side_fork(c);
+    if (rc != WG_OK) return rc;
+    if (!c->ev_hash) {
+        const hipError_t e = hipEventCreateWithFlags(&c->ev_hash, hipEventDisableTiming | wg_event_scope());
+        if (e != hipSuccess) rc = wg_fail(c, WG_E_HIP, "event: %s", hipGetErrorString(e));
+    }
+    if (rc == WG_OK) rc = wg_hash_table_launch(c);
+    if (rc == WG_OK) {
+        const hipError_t e = hipEventRecord(c->ev_hash, c->stream);
+        if (e != hipSuccess) rc = wg_fail(c, WG_E_HIP, "event: %s", hipGetErrorString(e));
+        c->hash_on_side = true;
+    }
+    if (rc == WG_OK && band_host && m) {   // (build_frame's host band, copied on this stream)
+        const hipError_t e = hipMemcpyAsync(band_dev, band_host, m * 4, hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) rc = wg_fail(c, WG_E_HIP, "band copy: %s", hipGetErrorString(e));
+    }
+    if (rc == WG_OK) rc = wg_heights_run(c, m, c->n_list, h);
+    if (rc == WG_OK) rc = wg_rowtop_run(c, m, h, band, rt, 0);
+    wg_side_done(c);
+    if (rc != WG_OK) c->hash_built = c->hash_on_side = false;
+    return rc;
+}
+
 int wg_fetch(wg_ctx *c, std::initializer_list<WgFetch> items, uint64_t *out) {
     return wg_fetch_n(c, (int)items.size(), items.begin(), out);
 }
@@ -412,6 +437,7 @@ void wg_destroy(wg_ctx *c) {
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_hash) (void)hipEventDestroy(c->ev_hash);
     if (c->ev_fetch) (void)hipEventDestroy(c->ev_fetch);
     if (c->ev_defer) (void)hipEventDestroy(c->ev_defer);
     delete c;
@@ -580,7 +606,10 @@ static int layout_build_impl(wg_ctx *c, const wg_commits *in, const float *fband
         }
         WG_ALLOC(c, c->band_prev, n * 4 + 4);   // the bands kept for the next frame's compare
     }
-    if ((rc = wg_side_zero_rowtop(c, n, c->heights.as<float>(), c->g_row_top.as<float>(), 0, db,
+    // the hash table's build goes first on the side stream: the window probe
+    // of the parent references runs beside it (wg_stage_hash_join)
+    c->hash_built = c->hash_on_side = false;
+    if ((rc = wg_side_build_begin(c, n, c->heights.as<float>(), c->g_row_top.as<float>(), db,
                                   db && fres == WG_HOST ? fband : nullptr, c->band.as<float>())) != WG_OK)
         return rc;
     // Speculative build (once an exact build has sized this context's

@@ -457,7 +457,8 @@ __global__ void __launch_bounds__(64) k_carry_sort(uint64_t nch, const uint32_t 
 
 // ---- the sweep ---------------------------------------------------------------------
 constexpr int SW_WAVES = 4;
-constexpr int SW_CAP = 384;   // edges alive across one row (per wave)
+constexpr int SW_CAP = 1024;  // edges alive across one row (per wave of the LDS sweep)
+constexpr int SW_CAP_BLOCK = SW_WAVES * SW_CAP;   // ... a chunk past that: one wave with the block's whole pool
 constexpr int SW_NE = 192;    // edges starting inside the 64-row chunk, staged in LDS
 
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
@@ -465,8 +466,11 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
 }
 
 // Fallback sweep for chunks with more edges than the register sweep holds:
-// active list in LDS, appended / compacted row by row.
-__device__ void sweep_chunk_lds(uint64_t q, uint64_t n, const wg_edge *__restrict__ edges,
+// active list in LDS (cap entries), appended / compacted row by row.  False
+// when more than cap edges are alive across a row: the chunk's entries
+// written so far sit at their final offsets, and the sweep with a larger
+// list rewrites all of them.
+__device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_edge *__restrict__ edges,
         const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
         const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
@@ -489,7 +493,7 @@ __device__ void sweep_chunk_lds(uint64_t q, uint64_t n, const wg_edge *__restric
     uint32_t cnt = 0;
     {
         const uint32_t a = carry_off[q], b = carry_off[q + 1];
-        if (b - a > (uint32_t)SW_CAP) { if (lid == 0) atomicOr(&err[0], 1u); return; }
+        if (b - a > cap) return false;
         for (uint32_t i = lid; i < b - a; i += 64) {
             const uint32_t k = carry_sorted[a + i];
             const wg_edge e = edges[k];
@@ -528,7 +532,7 @@ __device__ void sweep_chunk_lds(uint64_t q, uint64_t n, const wg_edge *__restric
                 take = c < p;
             }
             const uint64_t m = __ballot(take);
-            if (cnt + __builtin_popcountll(m) > (uint32_t)SW_CAP) { if (lid == 0) atomicOr(&err[0], 1u); return; }
+            if (cnt + __builtin_popcountll(m) > cap) return false;
             if (take) {
                 const uint32_t pos = cnt + mbcnt(m);
                 E[pos] = k; C[pos] = c; P[pos] = p; I[pos] = info;
@@ -567,6 +571,7 @@ __device__ void sweep_chunk_lds(uint64_t q, uint64_t n, const wg_edge *__restric
         }
         cnt = kept;
     }
+    return true;
 }
 
 __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const uint32_t *__restrict__ list,
@@ -576,19 +581,41 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         uint32_t *__restrict__ err, Cap vc, Cap sc, uint32_t *ovf) {
-    if (over(vc, ovf) || over(sc, ovf)) return;
-    __shared__ uint32_t s_eid[SW_WAVES][SW_CAP];
-    __shared__ uint32_t s_c[SW_WAVES][SW_CAP];
-    __shared__ uint32_t s_p[SW_WAVES][SW_CAP];
-    __shared__ uint32_t s_info[SW_WAVES][SW_CAP];
+    if (over(vc, ovf) || over(sc, ovf)) return;   // (uniform over the grid)
+    __shared__ uint32_t s_eid[SW_CAP_BLOCK];
+    __shared__ uint32_t s_c[SW_CAP_BLOCK];
+    __shared__ uint32_t s_p[SW_CAP_BLOCK];
+    __shared__ uint32_t s_info[SW_CAP_BLOCK];
     __shared__ uint32_t n_c[SW_WAVES][SW_NE];
     __shared__ uint32_t n_p[SW_WAVES][SW_NE];
     __shared__ uint32_t n_info[SW_WAVES][SW_NE];
+    __shared__ uint32_t wide[64], n_wide;   // this block's chunks past one wave's list
     const int w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) n_wide = 0;
+    __syncthreads();
     const uint32_t cnt = *list_n;
-    for (uint32_t i = blockIdx.x * SW_WAVES + w; i < cnt; i += gridDim.x * SW_WAVES)
-        sweep_chunk_lds(list[i], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off, curve_off, vert,
-                        curve_ref, curve_row, err, s_eid[w], s_c[w], s_p[w], s_info[w], n_c[w], n_p[w], n_info[w]);
+    for (uint32_t i = blockIdx.x * SW_WAVES + w; i < cnt; i += gridDim.x * SW_WAVES) {
+        const uint32_t o = (uint32_t)w * SW_CAP;
+        const bool ok = sweep_chunk_lds(SW_CAP, list[i], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
+                                        curve_off, vert, curve_ref, curve_row, err, s_eid + o, s_c + o, s_p + o,
+                                        s_info + o, n_c[w], n_p[w], n_info[w]);
+        if (!ok && (threadIdx.x & 63) == 0) {
+            const uint32_t at = atomicAdd(&n_wide, 1u);
+            if (at < 64u) wide[at] = list[i];
+            else atomicOr(&err[0], 1u);
+        }
+    }
+    __syncthreads();
+    // the wide chunks: wave 0 with every wave's list (a few rows of a list
+    // with more than a thousand lanes; more than SW_CAP_BLOCK alive: error)
+    const uint32_t nw = n_wide < 64u ? n_wide : 64u;
+    if (w == 0)
+        for (uint32_t j = 0; j < nw; j++)
+            if (!sweep_chunk_lds(SW_CAP_BLOCK, wide[j], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
+                                 curve_off, vert, curve_ref, curve_row, err, s_eid, s_c, s_p, s_info, n_c[0], n_p[0],
+                                 n_info[0]) &&
+                (threadIdx.x & 63) == 0)
+                atomicOr(&err[0], 1u);
 }
 
 // The sweep: one wave per 64-row chunk.  A chunk's edge set is fixed — the
@@ -1182,7 +1209,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
                                     {c->curve_off.as<uint32_t>() + n, false}}, fin);
         if (rc != WG_OK) return rc;
     }
-    if (fin[0]) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP);
+    if (fin[0]) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP_BLOCK);
     c->n_curve = fin[3];
     c->lists_nsuper = n_super_grid;
     c->lists_gen = c->layout_gen;

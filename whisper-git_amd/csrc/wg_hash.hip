@@ -65,44 +65,171 @@ __global__ void k_hash_settle(const uint8_t *__restrict__ oid, uint64_t n, unsig
     }
 }
 
-// One thread per row: canon[i] (the row itself when no insert met its own
-// key: ids all distinct), prow of the row's parent references (-1: not in
-// the list, :306-311) and the row's edge count (parents found, lane-
-// independent, so the edge offsets are ready before the lanes are) with the
-// block's sum of it for the offsets' scan (wg_scan_bs_u32).  first_ref set:
-// then the lane fast path's reference pass of the row (lf_refs_row, the
-// k_lf_refs of a single-GPU build) on the parents just resolved.
-__global__ void __launch_bounds__(WG_BS_THREADS) k_probe_rows(const uint8_t *__restrict__ oid, uint64_t n,
-                                                             const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
-                                                             const unsigned long long *__restrict__ table, uint64_t mask,
-                                                             const uint32_t *__restrict__ dup, uint32_t *__restrict__ canon,
-                                                             int32_t *__restrict__ prow, uint32_t *__restrict__ edge_cnt,
-                                                             uint32_t *__restrict__ bsum, LfRange R,
-                                                             unsigned long long *first_ref, uint32_t *fpc, uint32_t *viol) {
+// Parents sit a few rows below their children in a history listing (86% of
+// the wide16 list's references within 16 rows, 99.9% within 64).  With every
+// id distinct the row holding an id is THE row for it, so the reference pass
+// runs in three kernels around the table build (which runs on the side
+// stream meanwhile):
+//   k_probe_window  one thread per row: each reference looks through the next
+//                   PROBE_WIN rows' ids (staged in LDS by the block); a miss
+//                   (farther, earlier, or not in the list) is marked PROW_MISS
+//   k_probe_gather  one block per 256 target rows: the first (row, index)
+//                   reference and first-parent child count of every target
+//                   (LfRange first_ref / fpc) from the window hits of the rows
+//                   that can reach it, LDS atomics, one plain store per target
+//                   (which is also the lane stage's clear)
+//   k_probe_fix     after the table: the misses through the table (two
+//                   dependent random reads each), their share of the lane
+//                   pass with global atomics (as lf_refs_row), canon, the
+//                   edge counts and their block sums.  Duplicate ids: the
+//                   table decides every reference (the last row wins) and the
+//                   list is flagged for the general lane walk.
+constexpr int PROBE_WIN = 64;
+constexpr int32_t PROW_MISS = -2;
+constexpr int T = WG_BS_THREADS;
+
+__global__ void __launch_bounds__(WG_BS_THREADS) k_probe_window(const uint8_t *__restrict__ oid, uint64_t n,
+                                                               const uint32_t *__restrict__ poff,
+                                                               const uint8_t *__restrict__ poid, int32_t *__restrict__ prow,
+                                                               uint32_t *__restrict__ edge_cnt, uint8_t *__restrict__ rowmiss) {
+    constexpr int NW = WG_BS_THREADS + PROBE_WIN;
+    __shared__ uint32_t wkey[NW * 5];   // ids of rows b + 1 .. b + NW
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x;
+    const uint64_t i = b + threadIdx.x;
+    for (int t = threadIdx.x; t < NW; t += WG_BS_THREADS) {
+        const uint64_t r = b + 1 + (uint64_t)t;
+        const Key k = r < n ? load_key(oid + r * 20) : Key{{0u, 0u, 0u, 0u, 0u}};
+#pragma unroll
+        for (int w = 0; w < 5; w++) wkey[t * 5 + w] = k.w[w];
+    }
+    __syncthreads();
+    if (i >= n) return;
+    const uint32_t pa = poff[i], pb = poff[i + 1];
+    const uint32_t lim = n - 1 - i < (uint64_t)PROBE_WIN ? (uint32_t)(n - 1 - i) : (uint32_t)PROBE_WIN;
+    uint32_t cnt = 0;
+    bool miss = false;
+    for (uint32_t k = pa; k < pb; k++) {
+        int32_t p = PROW_MISS;
+        if (k - pa < 64u) {   // (k_probe_fix tracks a row's misses in a 64-bit mask: later refs always miss)
+            const Key key = load_key(poid + (uint64_t)k * 20);
+            for (uint32_t j = 1; j <= lim; j++) {
+                const uint32_t *q = wkey + (threadIdx.x + j - 1) * 5;
+                if (q[0] == key.w[0] && q[1] == key.w[1] && q[2] == key.w[2] && q[3] == key.w[3] && q[4] == key.w[4]) {
+                    p = (int32_t)(i + j);
+                    break;
+                }
+            }
+        }
+        prow[k] = p;
+        cnt += p >= 0;
+        miss |= p < 0;
+    }
+    edge_cnt[i] = cnt;
+    rowmiss[i] = miss ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(WG_BS_THREADS) k_probe_gather(uint64_t n, const uint32_t *__restrict__ poff,
+                                                               const int32_t *__restrict__ prow, LfClear L) {
+    __shared__ unsigned long long fr[WG_BS_THREADS];
+    __shared__ uint32_t fc[WG_BS_THREADS];
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x;
+    fr[threadIdx.x] = REF_NONE;
+    fc[threadIdx.x] = 0u;
+    __syncthreads();
+    // rows b - PROBE_WIN .. b + 255 can reach targets b .. b + 255 through the window
+    for (int t = threadIdx.x; t < WG_BS_THREADS + PROBE_WIN; t += WG_BS_THREADS) {
+        if ((uint64_t)t + b < (uint64_t)PROBE_WIN) continue;
+        const uint64_t i = b + (uint64_t)t - PROBE_WIN;
+        if (i >= n) continue;
+        const uint32_t pa = poff[i], pb = poff[i + 1];
+        for (uint32_t k = pa; k < pb && k - pa < 64u; k++) {
+            const int32_t p = prow[k];
+            if (p < 0 || (uint64_t)p < b || (uint64_t)p >= b + WG_BS_THREADS) continue;   // (window hits are forward)
+            if (!first_in_row(prow, pa, k, p)) continue;
+            atomicMin(&fr[(uint64_t)p - b], ref_key(i, k - pa));
+            if (k == pa) atomicAdd(&fc[(uint64_t)p - b], 1u);
+        }
+    }
+    __syncthreads();
+    const uint64_t r = b + threadIdx.x;
+    if (r < n) {
+        L.first_ref[r] = fr[threadIdx.x];
+        L.lfirst[r] = REF_NONE;
+    }
+    if (r < n + 2) {
+        L.fpc[r] = r < n ? fc[threadIdx.x] : 0u;
+        L.ch_fill[r] = 0u;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < 2 && n + threadIdx.x >= b + WG_BS_THREADS) {
+        L.fpc[n + threadIdx.x] = 0u;    // (the last block covers n, n + 1 unless n is a multiple of 256)
+        L.ch_fill[n + threadIdx.x] = 0u;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 16) {
+        L.flags[threadIdx.x] = 0u;
+        if (L.scal) L.scal[threadIdx.x] = 0u;
+    }
+}
+
+__global__ void __launch_bounds__(WG_BS_THREADS) k_probe_fix(const uint8_t *__restrict__ oid, uint64_t n,
+                                                            const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
+                                                            const unsigned long long *__restrict__ table, uint64_t mask,
+                                                            const uint32_t *__restrict__ dup, uint32_t *__restrict__ canon,
+                                                            int32_t *__restrict__ prow, uint32_t *__restrict__ edge_cnt,
+                                                            const uint8_t *__restrict__ rowmiss, uint32_t *__restrict__ bsum,
+                                                            LfClear L) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t cnt = 0;
     if (i < n) {
-        if (*dup == 0xFFFFFFFFu) canon[i] = (uint32_t)i;
-        else {
+        const uint32_t pa = poff[i], pb = poff[i + 1];
+        if (*dup != 0xFFFFFFFFu) {
+            // duplicate ids (:273-274 last write wins): the table decides every
+            // reference; such a list takes the general lane walk
             const int64_t r = hash_find(load_key(oid + i * 20), oid, table, mask);
             canon[i] = r < 0 ? (uint32_t)i : (uint32_t)r;
-        }
-        const uint32_t pa = poff[i], pb = poff[i + 1];
-        for (uint32_t k = pa; k < pb; k++) {
-            const int32_t p = (int32_t)hash_find(load_key(poid + (uint64_t)k * 20), oid, table, mask);
-            prow[k] = p;
-            cnt += p >= 0;
+            for (uint32_t k = pa; k < pb; k++) {
+                const int32_t p = (int32_t)hash_find(load_key(poid + (uint64_t)k * 20), oid, table, mask);
+                prow[k] = p;
+                cnt += p >= 0;
+            }
+            if (L.flags && canon[i] != (uint32_t)i) atomicOr(&L.flags[0], 1u);
+        } else {
+            canon[i] = (uint32_t)i;
+            cnt = edge_cnt[i];
+            if (L.flags && pb - pa > 0x10000u) atomicOr(&L.flags[0], 1u);   // (lf_refs_row's bound)
+            if (rowmiss[i]) {
+                uint64_t mm = 0;   // the row's misses among its first 64 references
+                for (uint32_t k = pa; k < pb; k++) {
+                    if (prow[k] != PROW_MISS) continue;
+                    const int32_t p = (int32_t)hash_find(load_key(poid + (uint64_t)k * 20), oid, table, mask);
+                    prow[k] = p;
+                    cnt += p >= 0;
+                    if (k - pa < 64u) mm |= 1ull << (k - pa);
+                }
+                // their share of the lane pass (lf_refs_row on these references)
+                if (L.first_ref)
+                    for (uint32_t k = pa; k < pb; k++) {
+                        if (k - pa < 64u && !(mm >> (k - pa) & 1ull)) continue;
+                        const int32_t p = prow[k];
+                        if (p < 0 || k - pa > 0xFFFFu || !first_in_row(prow, pa, k, p)) continue;
+                        if ((uint64_t)p <= i) atomicMin(&L.lfirst[p], ref_key(i, k - pa));   // leaky
+                        else {
+                            atomicMin(&L.first_ref[p], ref_key(i, k - pa));
+                            if (k == pa) atomicAdd(&L.fpc[p], 1u);
+                        }
+                    }
+            }
         }
         edge_cnt[i] = cnt;
-        if (first_ref && lf_refs_row(R, i, first_ref, fpc)) atomicOr(viol, 1u);
     }
     wg_bsum_store(cnt, bsum);
 }
 
 }  // namespace
 
-int wg_stage_hash_join(wg_ctx *c) {
-    const uint64_t n = c->n, e = c->e_refs;
+// The table build (place + settle): on the side stream when the build
+// forks one (wg_side_build_begin: it overlaps the window probe), else inline
+int wg_hash_table_launch(wg_ctx *c) {
+    const uint64_t n = c->n;
     uint64_t cap = 1024;
     while (cap < 2 * n) cap <<= 1;
     c->hcap = cap;
@@ -112,23 +239,49 @@ int wg_stage_hash_join(wg_ctx *c) {
         if (c->htab[k].cap < words * 8 + 64) c->htab_clean[k] = 0;   // (re)allocated below: not known empty
         WG_ALLOC(c, c->htab[k], words * 8 + 64);
     }
-    WG_ALLOC(c, c->canon, n * 4 + 4);
-    WG_ALLOC(c, c->prow, e * 4 + 4);
-    WG_ALLOC(c, c->edge_cnt, (n + 1) * 4);
-    WG_ALLOC(c, c->bsum, 3 * (wg_bs_blocks(n) + 64) * 4);
-    { const int _sr = wg_scan_reserve(c, n + 1); if (_sr != WG_OK) return _sr; }
-    wg_stage_begin(c, "hash_join");
     unsigned long long *table = c->htab[t].as<unsigned long long>();
     if (c->htab_clean[t] < words) WG_HIP(c, hipMemsetAsync(table, 0xFF, words * 8, c->stream));
     uint32_t *dup = reinterpret_cast<uint32_t *>(table + cap);
-    const int T = WG_BS_THREADS;
+    if (n) {
+        const uint32_t g = (uint32_t)((n + T - 1) / T);
+        hipLaunchKernelGGL(k_hash_place, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1,
+                           c->htab[o].as<unsigned long long>(), words, LfClear{});
+        c->htab_clean[o] = words;
+        hipLaunchKernelGGL(k_hash_settle, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1, dup);
+    }
+    c->htab_clean[t] = 0;
+    c->htab_cur = o;
+    c->htab_last = table;
+    c->hash_table = table;
+    c->hash_built = true;
+    WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+int wg_stage_hash_join(wg_ctx *c) {
+    const uint64_t n = c->n, e = c->e_refs;
+    WG_ALLOC(c, c->canon, n * 4 + 4);
+    WG_ALLOC(c, c->prow, e * 4 + 4);
+    WG_ALLOC(c, c->edge_cnt, (n + 1) * 4);
+    WG_ALLOC(c, c->rowmiss, n + 4);
+    WG_ALLOC(c, c->bsum, 3 * (wg_bs_blocks(n) + 64) * 4);
+    { const int _sr = wg_scan_reserve(c, n + 1); if (_sr != WG_OK) return _sr; }
+    wg_stage_begin(c, "hash_join");
+    // the table: built on the side stream already (joined below), or here
+    const bool side = c->hash_built && c->hash_on_side;
+    if (!c->hash_built)
+        if (const int rc = wg_hash_table_launch(c)) return rc;
+    c->hash_built = false;
+    c->hash_on_side = false;
+    const uint64_t cap = c->hcap;
+    unsigned long long *table = c->hash_table;
+    const uint32_t *dup = reinterpret_cast<const uint32_t *>(table + cap);
     const uint32_t g = (uint32_t)((n + T - 1) / T);
     c->lf_refs_done = false;
     if (n) {
         // the lane fast path's clear and reference pass ride on these kernels
         // (wg_lf_refs skips its own: lf_refs_done)
         LfClear L;
-        LfRange R;
         const bool lanes = !c->force_general_lanes;
         if (lanes) {
             WG_ALLOC(c, c->lf[LF_FIRST], n * 8 + 8);
@@ -143,22 +296,16 @@ int wg_stage_hash_join(wg_ctx *c) {
             L.ch_fill = c->lf[LF_CHFILL].as<uint32_t>();
             L.flags = c->lf[LF_FLAGS].as<uint32_t>();
             L.scal = c->lane_scalars.as<uint32_t>();
-            R.s = 0;
-            R.nl = n;
-            R.e = n;
-            R.poff = c->d_poff;
-            R.prow = c->prow.as<const int32_t>();
-            R.canon = c->canon.as<const uint32_t>();
-            R.lfirst = L.lfirst;
         }
-        hipLaunchKernelGGL(k_hash_place, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1,
-                           c->htab[o].as<unsigned long long>(), words, L);
-        c->htab_clean[o] = words;
-        hipLaunchKernelGGL(k_hash_settle, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1, dup);
-        hipLaunchKernelGGL(k_probe_rows, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
-                           (const unsigned long long *)table, cap - 1, (const uint32_t *)dup, c->canon.as<uint32_t>(),
-                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->bsum.as<uint32_t>(), R, L.first_ref,
-                           L.fpc, L.flags);
+        hipLaunchKernelGGL(k_probe_window, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
+                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->rowmiss.as<uint8_t>());
+        if (lanes)
+            hipLaunchKernelGGL(k_probe_gather, dim3(g), dim3(T), 0, c->stream, n, c->d_poff,
+                               (const int32_t *)c->prow.as<int32_t>(), L);
+        if (side) WG_HIP(c, hipStreamWaitEvent(c->stream, c->ev_hash, 0));
+        hipLaunchKernelGGL(k_probe_fix, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
+                           (const unsigned long long *)table, cap - 1, dup, c->canon.as<uint32_t>(), c->prow.as<int32_t>(),
+                           c->edge_cnt.as<uint32_t>(), (const uint8_t *)c->rowmiss.as<uint8_t>(), c->bsum.as<uint32_t>(), L);
         c->lf_refs_done = lanes;
         WgScanBs S;
         S.na = 1;
@@ -171,11 +318,9 @@ int wg_stage_hash_join(wg_ctx *c) {
         if (!c->spec)
             if (const int rc = wg_fetch_defer(c, {{c->edge_cnt.as<uint32_t>() + n, false}})) return rc;
     } else {
+        if (side) WG_HIP(c, hipStreamWaitEvent(c->stream, c->ev_hash, 0));
         WG_HIP(c, hipMemsetAsync(c->edge_cnt.p, 0, 4, c->stream));
     }
-    c->htab_clean[t] = 0;
-    c->htab_cur = o;
-    c->htab_last = table;
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     return WG_OK;

@@ -250,6 +250,7 @@ struct wg_ctx {
     // times only) runs there, overlapping the latency-bound lane phases
     hipStream_t side = nullptr, side_main = nullptr;
     hipEvent_t  ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t  ev_hash = nullptr;   // the side stream's hash table is built (wg_side_build_begin)
     bool        side_pending = false;
     std::string err;
 
@@ -277,6 +278,9 @@ struct wg_ctx {
     int htab_cur = 0;
     const unsigned long long *htab_last = nullptr;   // the last join's table (hcap slots)
     DevBuf canon;           // uint32 [N]  last row holding the same id
+    DevBuf rowmiss;         // uint8  [N]  a reference of the row missed the window probe (wg_hash.hip)
+    unsigned long long *hash_table = nullptr;   // the table of this build (wg_hash_table_launch)
+    bool hash_built = false, hash_on_side = false;   // ... launched already (on the side stream)
     DevBuf prow;            // int32  [E]  canonical parent row or -1
     // lanes
     DevBuf lane_asg;        // uint32 [N]  lane assigned while processing row
@@ -324,7 +328,7 @@ struct wg_ctx {
     bool use_serial() const { return replay_mode == 2 || (replay_mode == 0 && replay_serial); }
     // estimated cost of the serial pass (us) against one chunked iteration at the long chunk
     static double serial_cost_us(uint64_t nev, uint32_t nw) {
-        return (double)nev * (nw <= 1 ? 0.016 : nw <= 2 ? 0.04 : nw <= 4 ? 0.07 : 0.3);
+        return (double)nev * (nw <= 1 ? 0.016 : nw <= 2 ? 0.04 : nw <= 4 ? 0.07 : nw <= 16 ? 0.3 : 1.0);
     }
     static constexpr double WG_CHUNKED_ITER_US = 60.0;
     // a list of a very different length: the auto choices start over
@@ -340,7 +344,9 @@ struct wg_ctx {
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
     uint32_t replay_nw = 1;        // occupancy words of the next replay (from the last build's slot count)
     // the narrowest occupancy (1, 4, 16 words) holding n_slots slots below the sentinel
-    static uint32_t nw_for_slots(uint32_t slots) { return slots < 64 ? 1u : (slots < 256 ? 4u : 16u); }
+    static uint32_t nw_for_slots(uint32_t slots) {
+        return slots < 64 ? 1u : (slots < 256 ? 4u : (slots < 1024 ? 16u : 64u));   // (64: the serial workgroup, 4095 slots)
+    }
     // After a replay that reached its fixed point at iteration fp (the first that
     // changed nothing), the next build's blind count: up at once, down by half
     // the excess per build (it used to fall by one per build: after a list that
@@ -628,6 +634,11 @@ inline uint64_t wg_bs_blocks(uint64_t n) { return (n + WG_BS_THREADS - 1) / WG_B
 
 // stages -------------------------------------------------------------------------
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
+int wg_hash_table_launch(wg_ctx *c);          // wg_hash.hip: place + settle on c->stream
+// the build's side stream: the hash table (joined by the hash join's fix-up
+// kernel), then the heights and the row_top (joined by the geometry)
+int wg_side_build_begin(wg_ctx *c, uint64_t m, float *h, float *rt, const float *band, const float *band_host,
+                        float *band_dev);
 int wg_stage_lanes(wg_ctx *c, bool spec);     // wg_lanes.hip
 int wg_lanes_fast(wg_ctx *c, bool *used, bool spec);   // wg_lanes_fast.hip
 

@@ -188,7 +188,12 @@ __global__ void k_lf_secev_children(LfRange R, const unsigned long long *__restr
     const int32_t p = R.prow[pa];
     if (p < 0 || (uint64_t)p >= R.e || (uint64_t)p <= gj) return;   // beyond the range / leaky
     const uint64_t pl = (uint64_t)p - R.s;
-    ch[ch_off[pl] + atomicAdd(&ch_fill[pl], 1u)] = (uint32_t)j;
+    // (bounded on any input: this kernel is queued before the host knows the
+    // list is well formed, and with duplicate ids the first-parent counts the
+    // lists were sized by and the parent rows differ — the general walk
+    // replaces these results then)
+    const uint32_t at = atomicAdd(&ch_fill[pl], 1u);
+    if (at < ch_off[pl + 1] - ch_off[pl]) ch[ch_off[pl] + at] = (uint32_t)j;
 }
 
 // first references into this shard through a secondary parent of an earlier shard
@@ -207,7 +212,8 @@ __global__ void k_lf_xin_children(LfRange R, const uint32_t *__restrict__ ch_off
     const WgXEnt en = R.xall[x];
     if ((en.kf & 0xFFFFu) != 0 || en.p < R.s || en.p >= R.e) return;
     const uint64_t pl = en.p - R.s;
-    ch[ch_off[pl] + atomicAdd(&ch_fill[pl], 1u)] = WG_TOK_X | (uint32_t)x;
+    const uint32_t at = atomicAdd(&ch_fill[pl], 1u);
+    if (at < ch_off[pl + 1] - ch_off[pl]) ch[ch_off[pl] + at] = WG_TOK_X | (uint32_t)x;
 }
 
 // the chain source pointer of row j before jumping
@@ -226,7 +232,7 @@ __device__ __forceinline__ uint32_t sp_init(uint64_t j, const uint32_t *__restri
 //                   afterwards every pointer leaves its tile (or is a token);
 //   k_lf_jump4      each pass follows up to 4 links, so P becomes P^4: every
 //                   link crosses a tile, and ceil(log4(tiles)) passes finish.
-constexpr int JT_THREADS = 1024, JT_ROWS = 4096;
+constexpr int JT_THREADS = 1024, JT_ROWS = 16384;   // 64 KiB of LDS: 1M rows in 62 tiles, 3 passes of k_lf_jump4
 
 __global__ void __launch_bounds__(JT_THREADS) k_lf_jump_tile(uint64_t nl, uint32_t *__restrict__ sp,
                                                               const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
@@ -239,7 +245,7 @@ __global__ void __launch_bounds__(JT_THREADS) k_lf_jump_tile(uint64_t nl, uint32
     __syncthreads();
     // in place: a stored value is always a later link of the same chain, so a
     // racing read only skips further; stop once no pointer stays in the tile.
-    // Pointers lead to earlier rows on the inputs this path accepts, so 13
+    // Pointers lead to earlier rows on the inputs this path accepts, so 15
     // rounds always suffice; the bound keeps any other input finite.
     for (int round = 0; round < 32; round++) {
         int moved = 0;
@@ -261,7 +267,7 @@ __global__ void k_lf_jump4(uint64_t nl, const uint32_t *__restrict__ in, uint32_
     uint32_t v = in[j];
 #pragma unroll
     for (int h = 0; h < 4; h++) {
-        if (v & TAGS) break;
+        if ((v & TAGS) || (uint64_t)v >= nl) break;   // (a pointer past the rows: only on inputs the path rejects)
         v = in[v];
     }
     out[j] = v;
@@ -674,11 +680,11 @@ int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *e
                        bool *ok) {
     *ok = false;
     // the occupancy width of the last build first; a replay that overflowed
-    // it is redone wider (63 -> 255 -> 1023 slots)
-    for (uint32_t nw = c->replay_nw;; nw = nw < 4 ? 4u : 16u) {
+    // it is redone wider (63 -> 255 -> 1023 slots; 4095 on the serial workgroup)
+    for (uint32_t nw = c->replay_nw;; nw = nw < 4 ? 4u : (nw < 16 ? 16u : 64u)) {
         bool overflow = false;
         const int rc = replay_lanes_at(c, R, nev, ev, aux, lane, nw, ok, &overflow);
-        if (rc != WG_OK || !overflow || nw >= 16) return rc;
+        if (rc != WG_OK || !overflow || nw >= 64) return rc;
     }
 }
 
@@ -721,7 +727,7 @@ int wg_lf_replay_lanes_spec(wg_ctx *c, const LfRange &R, uint64_t nev, const uin
     if (rc != WG_OK) return rc;
     hipStream_t s = c->stream;
     wg_stage_begin(c, "lf_loop");
-    if (c->use_serial()) {
+    if (c->use_serial() || run.nw > 16) {   // (past 1023 slots only the serial workgroup replays)
         DevBuf &rec = c->lf[LF_SERREC];
         WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev));
         WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));
@@ -754,7 +760,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
     ReplayRun run;
     int src = replay_setup(c, run, nev, ev, aux, nw);
     if (src != WG_OK) return src;
-    if (c->use_serial()) {   // one exact pass: the scalars come with it
+    if (c->use_serial() || nw > 16) {   // one exact pass: the scalars come with it (past 1023 slots: the only one)
         DevBuf &rec = c->lf[LF_SERREC];
         WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev));
         wg_stage_begin(c, "lf_loop");
@@ -888,7 +894,7 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     wg_stage_begin(c, "lf_loop");
-    if (c->use_serial()) {   // exact in one pass (the run then reads as converged at iteration 1)
+    if (c->use_serial() || run.nw > 16) {   // exact in one pass (the run then reads as converged at iteration 1)
         DevBuf &rec = c->lf[LF_SERREC];
         WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev_cap));
         WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));

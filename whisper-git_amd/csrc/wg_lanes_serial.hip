@@ -274,6 +274,62 @@ __global__ void __launch_bounds__(64) k_ser_replay_w(const uint4 *__restrict__ r
     ser_finish(lane, ml, ms, ovf, cap, stats, flags, scal);
 }
 
+// ---- more than 1023 slots: a workgroup of MW_WAVES waves ------------------
+// Wave v holds slots [256 v, 256 v + 256) as four words (the four-word step's
+// compare and scalar selection); per event every wave offers its lowest
+// selected slot to one LDS word (ds_min), a barrier, every wave reads the
+// winner, its owner writes the lane's D and wave 0 the output lane.  Three
+// words in turn: event k's winner word is read by every wave before barrier
+// k + 1, and thread 0 resets it for event k + 3 after barrier k + 1.
+constexpr int MW_WAVES = 16, MW_NW = 4;   // 4096 slots, the last one the sentinel
+__global__ void __launch_bounds__(64 * MW_WAVES) k_ser_replay_mw(const uint4 *__restrict__ rec, const uint4 *__restrict__ ev,
+                                                                uint64_t nev_cap, const uint32_t *__restrict__ nev_dev,
+                                                                const uint32_t *__restrict__ gate, uint16_t *__restrict__ slot,
+                                                                uint32_t *__restrict__ stats, uint32_t *__restrict__ flags,
+                                                                uint32_t *__restrict__ scal) {
+    __shared__ uint32_t cb[3];
+    if (gate && *gate) return;   // (uniform over the block)
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t nev = nev_dev ? (uint64_t)*nev_dev : nev_cap;
+    constexpr uint32_t cap = 64u * MW_NW * MW_WAVES - 1u;
+    uint32_t ml = 0, ms = 0, ovf = 0;
+    uint32_t D[MW_NW];
+#pragma unroll
+    for (int w = 0; w < MW_NW; w++) D[w] = (wv == MW_WAVES - 1 && w == MW_NW - 1 && lane == 63) ? WG_SER_INF : 0u;
+    if (threadIdx.x < 3) cb[threadIdx.x] = 0xFFFFFFFFu;
+    __syncthreads();
+    uint4 R = rec[lane];
+    uint32_t k3 = 0;
+    for (uint64_t base = 0; base < nev; base += 64) {
+        const uint4 Rn = rec[base + 64 + lane];
+        uint32_t out = 0xFFFFu;
+        for (uint32_t J = 0; J < 64; J++) {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)R.x, (int)J);
+            const uint32_t wid = (uint32_t)__builtin_amdgcn_readlane((int)R.y, (int)J);
+            const uint32_t dv = (uint32_t)__builtin_amdgcn_readlane((int)R.z, (int)J);
+            uint64_t m[MW_NW];
+#pragma unroll
+            for (int w = 0; w < MW_NW; w++) m[w] = __ballot(D[w] - lo < wid);
+            const uint32_t x = ser_first_w<MW_NW>(m);
+            if (x != 0xFFFFFFFFu && lane == 0) atomicMin(&cb[k3], x + 256u * wv);
+            __syncthreads();
+            uint32_t g = (uint32_t)__builtin_amdgcn_readfirstlane((int)cb[k3]);
+            if (threadIdx.x == 0) cb[k3 == 0 ? 2u : k3 - 1u] = 0xFFFFFFFFu;   // event k - 1's word, for event k + 2
+            if (g == 0xFFFFFFFFu) g = cap;   // nothing selected: the sentinel (an overflow, or a padding no-op)
+            if ((g >> 8) == wv) {
+                const uint32_t l = g & 255u;
+#pragma unroll
+                for (int w = 0; w < MW_NW; w++) D[w] = (lane + 64u * (uint32_t)w == l) ? dv : D[w];
+            }
+            asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(out) : "s"(g), "s"(J) : "m0");
+            k3 = k3 == 2u ? 0u : k3 + 1u;
+        }
+        if (wv == 0) ser_flush(base, nev, lane, out, ev, slot, cap, ml, ms, ovf);
+        R = Rn;
+    }
+    if (wv == 0) ser_finish(lane, ml, ms, ovf, cap, stats, flags, scal);
+}
+
 // ---- the chunked replay's first iteration (wg_lanes_replay.hip) -----------
 // Every chunk restarts `warm` events early from an empty table, so its replay
 // is the serial step over [ew, e1) with this wave's own table: one wave per
@@ -324,7 +380,7 @@ __global__ void __launch_bounds__(64) k_lf_replay_first(const uint4 *__restrict_
 
 // Serial replay of nev events (nev_dev: the count on the device, nev its
 // upper bound; gate: nonzero = not well formed, nothing replayed) at
-// occupancy width nw (1, 4 or 16 words); slots into R.slots_a, which becomes
+// occupancy width nw (1, 4, 16 words; 64: the 16-wave workgroup); slots into R.slots_a, which becomes
 // the run's result (R.sp_prev); the run looks like a one-chunk replay that
 // converged at iteration 1 (stats / flags / it), so the lane and scalar
 // kernels of wg_lanes_replay.hip finish it unchanged.
@@ -346,9 +402,12 @@ hipError_t wg_replay_serial(hipStream_t s, ReplayRun &R, uint4 *rec) {
     else if (R.nw <= 4)
         hipLaunchKernelGGL(k_ser_replay_w<4>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
                            R.flags, R.scal);
-    else
+    else if (R.nw <= 16)
         hipLaunchKernelGGL(k_ser_replay_w<16>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
                            R.flags, R.scal);
+    else
+        hipLaunchKernelGGL(k_ser_replay_mw, dim3(1), dim3(64 * MW_WAVES), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a,
+                           R.stats, R.flags, R.scal);
     return hipGetLastError();
 }
 
