@@ -70,14 +70,14 @@ __global__ void k_hash_settle(const uint8_t *__restrict__ oid, uint64_t n, unsig
 // id distinct the row holding an id is THE row for it, so the reference pass
 // runs in three kernels around the table build (which runs on the side
 // stream meanwhile):
-//   k_probe_window  one thread per row: each reference looks through the next
-//                   PROBE_WIN rows' ids (staged in LDS by the block); a miss
-//                   (farther, earlier, or not in the list) is marked PROW_MISS
-//   k_probe_gather  one block per 256 target rows: the first (row, index)
-//                   reference and first-parent child count of every target
-//                   (LfRange first_ref / fpc) from the window hits of the rows
-//                   that can reach it, LDS atomics, one plain store per target
-//                   (which is also the lane stage's clear)
+//   k_probe_near    one block per 256 rows: each reference looks for its id
+//                   among the next PROBE_WIN rows' ids (staged in LDS with a
+//                   fingerprint table); a miss (farther, earlier, or not in
+//                   the list) is marked PROW_MISS; the first (row, index)
+//                   reference and first-parent child count of every target of
+//                   the block (LfRange first_ref / fpc) from the hits of the
+//                   rows that can reach it, LDS atomics, one plain store per
+//                   target (which is also the lane stage's clear)
 //   k_probe_fix     after the table: the misses through the table (two
 //                   dependent random reads each), their share of the lane
 //                   pass with global atomics (as lf_refs_row), canon, the
@@ -88,69 +88,90 @@ constexpr int PROBE_WIN = 64;
 constexpr int32_t PROW_MISS = -2;
 constexpr int T = WG_BS_THREADS;
 
-__global__ void __launch_bounds__(WG_BS_THREADS) k_probe_window(const uint8_t *__restrict__ oid, uint64_t n,
-                                                               const uint32_t *__restrict__ poff,
-                                                               const uint8_t *__restrict__ poid, int32_t *__restrict__ prow,
-                                                               uint32_t *__restrict__ edge_cnt, uint8_t *__restrict__ rowmiss) {
-    constexpr int NW = WG_BS_THREADS + PROBE_WIN;
-    __shared__ uint32_t wkey[NW * 5];   // ids of rows b + 1 .. b + NW
-    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x;
-    const uint64_t i = b + threadIdx.x;
-    for (int t = threadIdx.x; t < NW; t += WG_BS_THREADS) {
-        const uint64_t r = b + 1 + (uint64_t)t;
-        const Key k = r < n ? load_key(oid + r * 20) : Key{{0u, 0u, 0u, 0u, 0u}};
-#pragma unroll
-        for (int w = 0; w < 5; w++) wkey[t * 5 + w] = k.w[w];
-    }
-    __syncthreads();
-    if (i >= n) return;
-    const uint32_t pa = poff[i], pb = poff[i + 1];
-    const uint32_t lim = n - 1 - i < (uint64_t)PROBE_WIN ? (uint32_t)(n - 1 - i) : (uint32_t)PROBE_WIN;
-    uint32_t cnt = 0;
-    bool miss = false;
-    for (uint32_t k = pa; k < pb; k++) {
-        int32_t p = PROW_MISS;
-        if (k - pa < 64u) {   // (k_probe_fix tracks a row's misses in a 64-bit mask: later refs always miss)
-            const Key key = load_key(poid + (uint64_t)k * 20);
-            for (uint32_t j = 1; j <= lim; j++) {
-                const uint32_t *q = wkey + (threadIdx.x + j - 1) * 5;
-                if (q[0] == key.w[0] && q[1] == key.w[1] && q[2] == key.w[2] && q[3] == key.w[3] && q[4] == key.w[4]) {
-                    p = (int32_t)(i + j);
-                    break;
-                }
-            }
-        }
-        prow[k] = p;
-        cnt += p >= 0;
-        miss |= p < 0;
-    }
-    edge_cnt[i] = cnt;
-    rowmiss[i] = miss ? 1 : 0;
-}
+// k_probe_near: block b owns rows [b, b + 256) and targets [b, b + 256).
+// The ids of rows [b - 63, b + 320] go to LDS with a small open-addressing
+// table over their fingerprints; every row of [b - 64, b + 256) resolves its
+// references against it (a hit must lie within PROBE_WIN rows below the
+// child: the rows that can reach a target of this block), the block's own
+// rows write prow / their hit count / the miss flag, and the hits into the
+// block's targets feed the first-reference and first-parent-child counts
+// with LDS atomics (rows [b - 64, b) are resolved again for that: 25% more
+// lookups instead of a second kernel over prow).  A reference is first in
+// its row when no earlier reference of the row has the same id.
+constexpr int NR_LO = PROBE_WIN - 1;                 // rows staged below b
+constexpr int NR = NR_LO + T + PROBE_WIN + 1;        // rows b - 63 .. b + 320
+constexpr int NH = 1024;                             // LDS table slots (>= 2.5 x NR)
+__device__ __forceinline__ uint32_t near_slot(uint32_t fp) { return (fp * 0x9E3779B1u) >> 22; }
 
-__global__ void __launch_bounds__(WG_BS_THREADS) k_probe_gather(uint64_t n, const uint32_t *__restrict__ poff,
-                                                               const int32_t *__restrict__ prow, LfClear L) {
-    __shared__ unsigned long long fr[WG_BS_THREADS];
-    __shared__ uint32_t fc[WG_BS_THREADS];
+__global__ void __launch_bounds__(T) k_probe_near(const uint8_t *__restrict__ oid, uint64_t n,
+                                                  const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
+                                                  int32_t *__restrict__ prow, uint32_t *__restrict__ edge_cnt,
+                                                  uint8_t *__restrict__ rowmiss, LfClear L) {
+    __shared__ uint32_t wkey[NR * 5];
+    __shared__ uint32_t htab[NH];                    // staged row index + 1, 0 empty
+    __shared__ unsigned long long fr[T];
+    __shared__ uint32_t fc[T];
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x;
+    const int64_t r0 = (int64_t)b - NR_LO;           // staged row 0
+    for (int t = threadIdx.x; t < NH; t += T) htab[t] = 0u;
     fr[threadIdx.x] = REF_NONE;
     fc[threadIdx.x] = 0u;
     __syncthreads();
-    // rows b - PROBE_WIN .. b + 255 can reach targets b .. b + 255 through the window
-    for (int t = threadIdx.x; t < WG_BS_THREADS + PROBE_WIN; t += WG_BS_THREADS) {
-        if ((uint64_t)t + b < (uint64_t)PROBE_WIN) continue;
-        const uint64_t i = b + (uint64_t)t - PROBE_WIN;
-        if (i >= n) continue;
+    for (int t = threadIdx.x; t < NR; t += T) {
+        const int64_t r = r0 + t;
+        if (r < 0 || (uint64_t)r >= n) continue;
+        const Key k = load_key(oid + (uint64_t)r * 20);
+#pragma unroll
+        for (int w = 0; w < 5; w++) wkey[t * 5 + w] = k.w[w];
+        uint32_t h = near_slot(key_fp(k));
+        while (atomicCAS(&htab[h], 0u, (uint32_t)t + 1u) != 0u) h = (h + 1u) & (NH - 1u);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < T + PROBE_WIN; t += T) {
+        const int64_t is = (int64_t)b - PROBE_WIN + t;
+        if (is < 0 || (uint64_t)is >= n) continue;
+        const uint64_t i = (uint64_t)is;
+        const bool own = i >= b;
         const uint32_t pa = poff[i], pb = poff[i + 1];
-        for (uint32_t k = pa; k < pb && k - pa < 64u; k++) {
-            const int32_t p = prow[k];
-            if (p < 0 || (uint64_t)p < b || (uint64_t)p >= b + WG_BS_THREADS) continue;   // (window hits are forward)
-            if (!first_in_row(prow, pa, k, p)) continue;
-            atomicMin(&fr[(uint64_t)p - b], ref_key(i, k - pa));
-            if (k == pa) atomicAdd(&fc[(uint64_t)p - b], 1u);
+        uint32_t cnt = 0;
+        bool miss = false;
+        for (uint32_t k = pa; k < pb; k++) {
+            int32_t p = PROW_MISS;
+            Key key{};
+            if (k - pa < 64u) {
+                key = load_key(poid + (uint64_t)k * 20);
+                uint32_t h = near_slot(key_fp(key));
+                for (uint32_t e = htab[h]; e != 0u; h = (h + 1u) & (NH - 1u), e = htab[h]) {
+                    const uint32_t *q = wkey + (e - 1u) * 5;
+                    if (q[0] == key.w[0] && q[1] == key.w[1] && q[2] == key.w[2] && q[3] == key.w[3] && q[4] == key.w[4]) {
+                        const int64_t r = r0 + (int64_t)(e - 1u);
+                        if (r > (int64_t)i && r <= (int64_t)i + PROBE_WIN) p = (int32_t)r;
+                        break;
+                    }
+                }
+            }
+            if (own) {
+                prow[k] = p;
+                cnt += p >= 0;
+                miss |= p < 0;
+            }
+            // the lane pass's counts for hits into this block's targets
+            if (L.first_ref && p >= 0 && (uint64_t)p >= b && (uint64_t)p < b + T) {
+                bool first = true;
+                for (uint32_t q = pa; q < k && first; q++) first = !key_eq(key, poid + (uint64_t)q * 20);
+                if (first) {
+                    atomicMin(&fr[(uint64_t)p - b], ref_key(i, k - pa));
+                    if (k == pa) atomicAdd(&fc[(uint64_t)p - b], 1u);
+                }
+            }
+        }
+        if (own) {
+            edge_cnt[i] = cnt;
+            rowmiss[i] = miss ? 1 : 0;
         }
     }
     __syncthreads();
+    if (!L.first_ref) return;
     const uint64_t r = b + threadIdx.x;
     if (r < n) {
         L.first_ref[r] = fr[threadIdx.x];
@@ -160,8 +181,8 @@ __global__ void __launch_bounds__(WG_BS_THREADS) k_probe_gather(uint64_t n, cons
         L.fpc[r] = r < n ? fc[threadIdx.x] : 0u;
         L.ch_fill[r] = 0u;
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < 2 && n + threadIdx.x >= b + WG_BS_THREADS) {
-        L.fpc[n + threadIdx.x] = 0u;    // (the last block covers n, n + 1 unless n is a multiple of 256)
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < 2 && n + threadIdx.x >= b + T) {
+        L.fpc[n + threadIdx.x] = 0u;   // (the last block covers n, n + 1 unless n is a multiple of 256)
         L.ch_fill[n + threadIdx.x] = 0u;
     }
     if (blockIdx.x == 0 && threadIdx.x < 16) {
@@ -297,11 +318,8 @@ int wg_stage_hash_join(wg_ctx *c) {
             L.flags = c->lf[LF_FLAGS].as<uint32_t>();
             L.scal = c->lane_scalars.as<uint32_t>();
         }
-        hipLaunchKernelGGL(k_probe_window, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
-                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->rowmiss.as<uint8_t>());
-        if (lanes)
-            hipLaunchKernelGGL(k_probe_gather, dim3(g), dim3(T), 0, c->stream, n, c->d_poff,
-                               (const int32_t *)c->prow.as<int32_t>(), L);
+        hipLaunchKernelGGL(k_probe_near, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
+                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->rowmiss.as<uint8_t>(), L);
         if (side) WG_HIP(c, hipStreamWaitEvent(c->stream, c->ev_hash, 0));
         hipLaunchKernelGGL(k_probe_fix, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
                            (const unsigned long long *)table, cap - 1, dup, c->canon.as<uint32_t>(), c->prow.as<int32_t>(),

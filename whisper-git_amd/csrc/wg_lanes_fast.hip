@@ -232,7 +232,7 @@ __device__ __forceinline__ uint32_t sp_init(uint64_t j, const uint32_t *__restri
 //                   afterwards every pointer leaves its tile (or is a token);
 //   k_lf_jump4      each pass follows up to 4 links, so P becomes P^4: every
 //                   link crosses a tile, and ceil(log4(tiles)) passes finish.
-constexpr int JT_THREADS = 1024, JT_ROWS = 16384;   // 64 KiB of LDS: 1M rows in 62 tiles, 3 passes of k_lf_jump4
+constexpr int JT_THREADS = 1024, JT_ROWS = 4096;   // (16384: one jump4 pass fewer, the tile pass 18 -> 50 us)
 
 __global__ void __launch_bounds__(JT_THREADS) k_lf_jump_tile(uint64_t nl, uint32_t *__restrict__ sp,
                                                               const uint32_t *__restrict__ winfo, const uint32_t *__restrict__ ev_off,
@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(JT_THREADS) k_lf_jump_tile(uint64_t nl, uint32
     __syncthreads();
     // in place: a stored value is always a later link of the same chain, so a
     // racing read only skips further; stop once no pointer stays in the tile.
-    // Pointers lead to earlier rows on the inputs this path accepts, so 15
+    // Pointers lead to earlier rows on the inputs this path accepts, so 13
     // rounds always suffice; the bound keeps any other input finite.
     for (int round = 0; round < 32; round++) {
         int moved = 0;
