@@ -61,6 +61,8 @@ def parse():
                     help="gloo rehearsal: move HIP-resident slots through gloo (the stream-ordered slot path of RCCL)")
     ap.add_argument("--no-defer", action="store_true",
                     help="validate every speculative build before build() returns (WG_OPT_DEFER_VALIDATION off)")
+    ap.add_argument("--no-slice", action="store_true",
+                    help="build the geometry lists in the geometry pass, not row-sliced under the emission (WG_OPT_SLICE_LISTS 0)")
     ap.add_argument("--no-build-frame", action="store_true",
                     help="separate build() and row_geometry() calls instead of wg_layout_build_frame")
     ap.add_argument("--all-stage-events", action="store_true",
@@ -359,6 +361,7 @@ def config_rates(eng, dev, torch, args):
         eng = wgraph.Engine(dev.index)
         eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         eng.set_defer_validation(not args.no_defer)
+        eng.set_slice_lists(0 if args.no_slice else 1)
         d = synth.generate(kind, n)
         keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
                                                        d.parent_oid.reshape(-1), d.flags, d.band)]
@@ -428,6 +431,7 @@ def build_lifecycle(dag, dev, torch, args, pal):
     eng = wgraph.Engine(dev.index)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     eng.set_defer_validation(not args.no_defer)
+    eng.set_slice_lists(0 if args.no_slice else 1)
 
     def step(k, c, n):
         torch.cuda.synchronize()
@@ -532,6 +536,7 @@ def main():
     # a step's build is validated with its emission's vertex-total read (one
     # host wait per step, while the emission runs) instead of mid-step
     eng.set_defer_validation(not args.no_defer)
+    eng.set_slice_lists(0 if args.no_slice else 1)
     pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
     selected = shard0 + 7
     comm = None
@@ -627,8 +632,12 @@ def main():
     # roofline of the dominant kernel (vertex emission), from live HIP events
     vs = eng.vertex_summary()
     gs = eng.geometry_summary()
+    sliced_emits = int(eng.debug_counters()[11])
     n_rows_shard = shard1 - shard0
-    vtx_ms = float(np.mean(launches.get("vtx_emit", [float("nan")])))   # one launch per step
+    # one emission per step: one k_vtx_tile launch, or two when the geometry
+    # lists are row-sliced under it (WG_OPT_SLICE_LISTS) — then
+    # the span from part 1's start to the end of both parts
+    vtx_ms = float(np.mean(launches.get("vtx_emit", [float("nan")])))
     g = eng.geometry()   # this rank's rows (the whole list at N=1)
     r0, r1 = (shard0, shard1) if world == 1 else (0, shard1 - shard0)
     nvert_shard = int(g["vert_off"][r1]) - int(g["vert_off"][r0])
@@ -641,6 +650,7 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None, "algorithmic_bytes_per_launch": int(bytes_w + bytes_r),
                 "avg_launch_ms": round(vtx_ms, 4),
+                "launches_per_emission": 2 if sliced_emits else 1,
                 # the host clock over emission-only calls (no events): launch + offsets kernel + the total's read
                 "emit_only_wall_ms_per_call": round(emit_only_ms, 4)}
     pmc = pmc_traffic(args, workload)

@@ -1,10 +1,10 @@
 """Per-step kernel timeline from a rocprofv3 --kernel-trace CSV: kernels of
-the last step (k_vtx_tile end to k_vtx_tile end), their durations and the
-idle gap before each one (host synchronisations show up as gaps).
+one step (from a build's first kernel to the next build's; t = 0 at the end
+of the previous step's last kernel), their durations and the idle gap
+before each one (host synchronisations show up as gaps).
 
 usage: python3 profiles/gaps.py <run_kernel_trace.csv> [min_gap_us] [step]
-  step: which step (between the step-th and step+1-th k_vtx_tile, from 0);
-        default the last one.  bench.py's last steps are its stage-breakdown
+  step: which step (from 0); default the last complete one.  bench.py's last steps are its stage-breakdown
         pass, whose per-stage HIP events show up as ~10 us gaps: pick a step
         of the timed region (after the warmup) to see the timed step.
 """
@@ -18,14 +18,17 @@ def main():
     min_gap = float(sys.argv[2]) if len(sys.argv) > 2 else 3.0
     ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                   re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))) for r in rows))
-    ends = [i for i, k in enumerate(ks) if k[2] == "k_vtx_tile"]
+    # a step starts at its build's first kernel (the near probe; the hash
+    # place on lists built another way); the emission may be two launches
+    first = "k_probe_near" if any(k[2] == "k_probe_near" for k in ks) else "k_hash_place"
+    starts = [i for i, k in enumerate(ks) if k[2] == first] + [len(ks)]
     if len(sys.argv) > 3:
         st = int(sys.argv[3])
-        a, b = ends[st], ends[st + 1]
     else:
-        a, b = ends[-2], ends[-1]
-    step = ks[a + 1:b + 1]
-    t0 = ks[a][1]
+        st = len(starts) - 3
+    a, b = starts[st], starts[st + 1]
+    step = ks[a:b]
+    t0 = max(e for _, e, _ in ks[:a]) if a else step[0][0]
     busy = sum(e - s for s, e, _ in step)
     span = step[-1][1] - t0
     print(f"step span {span / 1e3:.1f} us, busy {busy / 1e3:.1f} us, {len(step)} kernels")

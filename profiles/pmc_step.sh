@@ -12,7 +12,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/pmc_step_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-RX=${PMC_KERNELS:-"k_hash_place|k_hash_settle|k_probe_rows|k_lf_rows|k_lf_jump_tile|k_lf_replay|k_rt_walk|k_rt_tables|k_edges_rows|k_edge_counts|k_top_carry|k_top_finish|k_sweep|k_curves_tb|k_curves"}
+RX=${PMC_KERNELS:-"k_probe_near|k_probe_fix|k_hash_place|k_hash_settle|k_lf_rows|k_lf_jump_tile|k_lf_replay|k_rt_walk|k_edges_rows|k_edge_counts|k_geom_offsets|k_top_carry|k_top_finish|k_sweep|k_curves_tb|k_curves|k_vtx_prep"}
 BENCH="$ROOT/bench.py --steps 3 --warmup 1 --no-cpu --no-extras"
 timeout -s KILL 120 rocprofv3 --kernel-include-regex "$RX" --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH > "$OUT/fetch.json" 2> "$OUT/fetch.err"
 timeout -s KILL 120 rocprofv3 --kernel-include-regex "$RX" --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $BENCH > "$OUT/write.json" 2> "$OUT/write.err"

@@ -183,3 +183,44 @@ def test_build_frame_sequence(defer):
         assert eng.geometry_summary().n_rows == 0
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("kind,n", [("wide16", 120000), ("linuxwide", 40000), ("skew", 60000), ("random13", 100000)])
+def test_sliced_lists_emission(kind, n):
+    """WG_OPT_SLICE_LISTS: a deferred-validation build_frame leaves its
+    geometry lists to the whole-list emission, which builds rows [0, h) and
+    emits their tiles while rows [h, N) are built beside them.  Three steps
+    (the exact first build, then speculative ones: the split's first guess,
+    then the last frame's split tile) and the same steps with slicing off:
+    every vertex buffer and the frame's geometry bit-exact against the
+    oracle."""
+    import wgraph
+    from oracle import oracle_c
+    d = synth.generate(kind, n, seed=11)
+    o = oracle_c.OracleLayout(d)
+    og = o.row_geometry(d.band)
+    sel = n // 5
+    ov, _ = o.emit_vertices(0, n, selected=sel)
+    want = oracle_c.vertex_checksum(ov)
+    try:
+        for sliced in (2, 0):
+            eng = wgraph.Engine(0)
+            try:
+                eng.set_defer_validation(True)
+                eng.set_slice_lists(sliced)
+                for step in range(3):
+                    tag = f"{kind}/{n} sliced={sliced} step {step}"
+                    eng.build_frame(d, band=d.band)
+                    eng.emit_vertices(0, n, selected=sel)
+                    vs = eng.vertex_summary()
+                    assert vs.n_vertices == len(ov) and vs.checksum == want, tag
+                got = eng.geometry()
+                for k, v in og.items():
+                    assert_bits(f"{kind} sliced={sliced} {k}", got[k], v)
+                dc = eng.debug_counters()
+                assert int(dc[6]) == 2   # the later builds speculated
+                assert int(dc[11]) == (2 if sliced else 0)   # and their emissions sliced the lists
+            finally:
+                eng.close()
+    finally:
+        o.close()

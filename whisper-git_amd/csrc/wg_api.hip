@@ -111,10 +111,18 @@ int wg_copy_batch(wg_ctx *c, const WgCopies &cp, hipStream_t s) {
 
 int wg_side_fork(wg_ctx *c) {
     if (!c->side) {
-        WG_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        // the side stream at the device's highest priority: its kernels are
+        // short latency-bound ones (the hash table, row_top, the second list
+        // slice) running beside a long main-stream kernel (the probe, the
+        // emission's first part) whose workgroups would otherwise take every
+        // slot as it frees
+        int lo_prio = 0, hi_prio = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) hi_prio = 0;
+        WG_HIP(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi_prio));
         // stream-to-stream order on one device: a device-scope release suffices
         WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | wg_event_scope()));
         WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | wg_event_scope()));
+        WG_HIP(c, hipEventCreateWithFlags(&c->ev_slice, hipEventDisableTiming | wg_event_scope()));
     }
     if (const int rc = wg_side_join(c)) return rc;
     WG_HIP(c, hipEventRecord(c->ev_fork, c->stream));
@@ -271,6 +279,7 @@ int wg_fetch_begin_n(wg_ctx *c, int n, const WgFetch *items) {
 // Deferred validation of a speculative build (WG_OPT_DEFER_VALIDATION)
 // ---------------------------------------------------------------------------
 int wg_settle(wg_ctx *c) {
+    if (const int rc = wg_geom_lists_flush(c)) return rc;   // (the words below include the lists' flags)
     if (!c->pend.build) return WG_OK;
     uint64_t v[WG_PENDING_ITEMS] = {0};
     if (const int rc = wg_fetch_n(c, c->pend.k, c->pend.it, v)) return rc;
@@ -438,6 +447,7 @@ void wg_destroy(wg_ctx *c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->ev_hash) (void)hipEventDestroy(c->ev_hash);
+    if (c->ev_slice) (void)hipEventDestroy(c->ev_slice);
     if (c->ev_fetch) (void)hipEventDestroy(c->ev_fetch);
     if (c->ev_defer) (void)hipEventDestroy(c->ev_defer);
     delete c;
@@ -486,6 +496,12 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
     case WG_OPT_REPLAY_MODE:
         if (value < 0 || value > 2) return wg_fail(c, WG_E_INVALID, "replay mode must be 0 (auto), 1 (chunked) or 2 (serial)");
         c->replay_mode = (uint32_t)value;
+        return WG_OK;
+    case WG_OPT_SLICE_LISTS:
+        if (value < 0 || value > 2) return wg_fail(c, WG_E_INVALID, "slice lists must be 0, 1 or 2");
+        WG_SETTLE(c);
+        c->slice_on = value != 0;
+        c->slice_min_rows = value == 2 ? 4 * WG_SWEEP_CH : 1ull << 18;
         return WG_OK;
     case WG_OPT_SWEEP_REG:
         if (value < 0 || value > 512) return wg_fail(c, WG_E_INVALID, "sweep register capacity must be 0..512");
@@ -1088,6 +1104,7 @@ int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
     if (n > 8) out[8] = c->spec_redo_geom;
     if (n > 9) out[9] = c->spec_replays_shard;
     if (n > 10) out[10] = c->last_serial ? 1u : 0u;
+    if (n > 11) out[11] = c->sliced_emits;
     return WG_OK;
 }
 

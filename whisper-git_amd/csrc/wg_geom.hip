@@ -112,7 +112,8 @@ struct EdgeRowsArgs {
     const float *h, *band, *row_top;
     float *height, *node_y, *band_keep;
     uint8_t *rowflags, *zflags;
-    uint32_t *cntB, *diffF, *diffC, *cntCend, *carry_diff, *cntT, *top_fill, *carry_fill, *misc;
+    uint8_t *flags_kept;       // the flags the curve lists are filtered with (rowflags_lists)
+    uint32_t *cntB, *diffF, *diffC, *cntCend, *cntPend, *carry_diff, *cntT, *top_fill, *carry_fill, *misc;
 };
 __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) {
     static_assert(WG_SWEEP_CH == 64, "a wave's rows are one sweep chunk");
@@ -152,6 +153,7 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
         A.diffF[r + 1] = f;
         A.diffC[r + 1] = cc;
         A.cntCend[r] = ce;
+        A.cntPend[r] = 0u;
         A.cntT[r] = 0u;
         A.top_fill[r] = 0u;
         A.zflags[r] = 0;
@@ -175,6 +177,7 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
         if (bot - node_abs < 1e-4f) fl |= RF_CHILD;
         if (node_abs - top < 1e-4f) fl |= RF_PARENT;
         A.rowflags[r] = fl;
+        A.flags_kept[r] = fl;
     }
     if (r == 0) { A.diffF[0] = 0u; A.diffC[0] = 0u; A.carry_diff[0] = 0u; }
     if (r < 64) A.misc[r] = 0u;
@@ -187,7 +190,7 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
 
 __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, const uint8_t *__restrict__ rowflags,
                               uint32_t *cntT, uint32_t *diffF, uint32_t *diffC, uint32_t *cntCend,
-                              uint32_t *carry_diff, const uint32_t *__restrict__ ne_dev) {
+                              uint32_t *cntPend, uint32_t *carry_diff, const uint32_t *__restrict__ ne_dev) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ne || (ne_dev && k >= *ne_dev)) return;
     const wg_edge e = edges[k];
@@ -201,6 +204,7 @@ __global__ void k_edge_counts(uint64_t ne, const wg_edge *__restrict__ edges, co
     } else {
         if (c + 1 < p) atomicAdd(&diffC[p], 0xFFFFFFFFu);
         if (!(rowflags[p] & RF_PARENT)) atomicAdd(&cntCend[p], 1u);
+        atomicAdd(&cntPend[p], 1u);   // (the parent-end share, for the filtered count)
     }
 }
 
@@ -311,16 +315,21 @@ __device__ __forceinline__ uint2 go_block_excl(uint2 v, uint2 &tot) {
 
 // One launch after the tile sums of the two difference arrays (scanned
 // over n + 1 entries, in place): the per-row span counts, the per-row list
-// totals nV = nF + nT + nB (-> vert_off) and nC (-> curve_off, the superset:
-// the flag row is all zero) and their 256-row sums for the offsets' scan
-// (wg_scan_bs_u32).
+// totals nV = nF + nT + nB (-> vert_off), nC (-> scurve_off, the superset:
+// the flag row is all zero) and nK (-> curve_off, the superset filtered by
+// the pass's strip flags, :577: a row's crossing, child-end and parent-end
+// segments each dropped as a group by its flag) and their 256-row sums for
+// the offsets' scan (wg_scan_bs_u32).
 __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, uint32_t *C, const uint32_t *__restrict__ tsF,
                                                       const uint32_t *__restrict__ tsC, const uint32_t *__restrict__ cntT,
                                                       const uint32_t *__restrict__ cntB, const uint32_t *__restrict__ cntCend,
                                                       uint32_t *__restrict__ nV, uint32_t *__restrict__ nC,
                                                       uint32_t *__restrict__ bsV, uint32_t *__restrict__ bsC, uint64_t nbs,
                                                       uint32_t *D, const uint32_t *__restrict__ tsD, uint64_t nch,
-                                                      uint32_t *__restrict__ bsD, uint64_t nbsD) {
+                                                      uint32_t *__restrict__ bsD, uint64_t nbsD,
+                                                      const uint32_t *__restrict__ cntPend,
+                                                      const uint8_t *__restrict__ rowflags, uint32_t *__restrict__ nK,
+                                                      uint32_t *__restrict__ bsK) {
     uint2 pre = make_uint2(0u, 0u), ptot;
     uint2 preD = make_uint2(0u, 0u), ptotD;
     for (uint64_t b = threadIdx.x; b < blockIdx.x; b += GO_T) { pre.x += tsF[b]; pre.y += tsC[b]; preD.x += tsD[b]; }
@@ -328,10 +337,14 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
     (void)go_block_excl(preD, ptotD);
     carry_counts(D, nch, (uint64_t)blockIdx.x * GO_TILE + (uint64_t)threadIdx.x * GO_Q, ptotD.x, bsD, nbsD);
     const uint64_t base = (uint64_t)blockIdx.x * GO_TILE + (uint64_t)threadIdx.x * GO_Q;
-    uint32_t vF[GO_Q], vC[GO_Q], vT[GO_Q], vB[GO_Q], vE[GO_Q];
+    uint32_t vF[GO_Q], vC[GO_Q], vT[GO_Q], vB[GO_Q], vE[GO_Q], vP[GO_Q], vR[GO_Q];
     const bool full = base + GO_Q <= n;   // every item a row (and within the n + 1 entries): 16-byte accesses
     if (full) {
         ld8(F + base, vF); ld8(C + base, vC); ld8(cntT + base, vT); ld8(cntB + base, vB); ld8(cntCend + base, vE);
+        ld8(cntPend + base, vP);
+        const uint2 f8 = *reinterpret_cast<const uint2 *>(rowflags + base);
+#pragma unroll
+        for (int k = 0; k < 4; k++) { vR[k] = (f8.x >> (8 * k)) & 0xFFu; vR[k + 4] = (f8.y >> (8 * k)) & 0xFFu; }
     } else {
 #pragma unroll
         for (int k = 0; k < GO_Q; k++) {
@@ -342,6 +355,8 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
             vT[k] = row ? cntT[base + k] : 0u;
             vB[k] = row ? cntB[base + k] : 0u;
             vE[k] = row ? cntCend[base + k] : 0u;
+            vP[k] = row ? cntPend[base + k] : 0u;
+            vR[k] = row ? rowflags[base + k] : 0u;
         }
     }
     uint2 sum = make_uint2(0u, 0u);
@@ -354,8 +369,8 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
     uint2 run = go_block_excl(sum, tot);
     run.x += ptot.x;
     run.y += ptot.y;
-    uint32_t tV = 0, tC = 0;
-    uint32_t oF[GO_Q], oC[GO_Q], oV[GO_Q], oN[GO_Q];
+    uint32_t tV = 0, tC = 0, tK = 0;
+    uint32_t oF[GO_Q], oC[GO_Q], oV[GO_Q], oN[GO_Q], oK[GO_Q];
 #pragma unroll
     for (int k = 0; k < GO_Q; k++) {
         oF[k] = run.x;
@@ -365,16 +380,20 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
         // run = the exclusive value at row + 1: the edges alive across the row
         oV[k] = run.x + vT[k] + vB[k];
         oN[k] = run.y + vE[k];
-        if (base + k < n) { tV += oV[k]; tC += oN[k]; }
+        // kept: crossing (c < r < p) unless RF_ZERO, child-end (r == c) unless
+        // RF_CHILD, parent-end (r == p) unless RF_PARENT (curve_kept)
+        const uint32_t f = vR[k];
+        oK[k] = ((f & RF_ZERO) ? 0u : run.y) + ((f & RF_CHILD) ? 0u : vE[k] - vP[k]) + ((f & RF_PARENT) ? 0u : vP[k]);
+        if (base + k < n) { tV += oV[k]; tC += oN[k]; tK += oK[k]; }
     }
     if (full) {
-        st8(F + base, oF); st8(C + base, oC); st8(nV + base, oV); st8(nC + base, oN);
+        st8(F + base, oF); st8(C + base, oC); st8(nV + base, oV); st8(nC + base, oN); st8(nK + base, oK);
     } else {
 #pragma unroll
         for (int k = 0; k < GO_Q; k++) {
             const uint64_t i = base + k;
             if (i <= n) { F[i] = oF[k]; C[i] = oC[k]; }
-            if (i < n) { nV[i] = oV[k]; nC[i] = oN[k]; }
+            if (i < n) { nV[i] = oV[k]; nC[i] = oN[k]; nK[i] = oK[k]; }
         }
     }
     // 256-row sums: 32 threads x 8 rows
@@ -382,9 +401,10 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
     for (int d = 16; d >= 1; d >>= 1) {
         tV += (uint32_t)__shfl_xor((int)tV, d, 64);
         tC += (uint32_t)__shfl_xor((int)tC, d, 64);
+        tK += (uint32_t)__shfl_xor((int)tK, d, 64);
     }
     const uint64_t sub = (uint64_t)blockIdx.x * (GO_TILE / WG_BS_THREADS) + threadIdx.x / 32;
-    if ((threadIdx.x & 31) == 0 && sub < nbs) { bsV[sub] = tV; bsC[sub] = tC; }
+    if ((threadIdx.x & 31) == 0 && sub < nbs) { bsV[sub] = tV; bsC[sub] = tC; bsK[sub] = tK; }
 }
 
 // one pass over the edges: same-lane edges' ids into their parent row's
@@ -414,11 +434,12 @@ __global__ void k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges, cons
 // per row: the top-half entries (edge ids placed by k_top_carry) sorted by
 // edge id and packed, then the bottom halves (same-lane edges of child r, in
 // parent order) after them
-__global__ void k_top_finish(uint64_t n, const uint32_t *__restrict__ edge_off, const wg_edge *__restrict__ edges,
-                             const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ scanF,
-                             const uint32_t *__restrict__ cntT, uint32_t *vert, Cap vc, uint32_t *ovf) {
-    uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (over(vc, ovf) || r >= n) return;
+__global__ void k_top_finish(uint64_t r0, uint64_t r1, const uint32_t *__restrict__ edge_off,
+                             const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
+                             const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT, uint32_t *vert, Cap vc,
+                             uint32_t *ovf) {
+    uint64_t r = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // rows [r0, r1)
+    if (over(vc, ovf) || r >= r1) return;
     const uint32_t nt = cntT[r];
     uint32_t *v = vert + vert_off[r] + scanF[r + 1];
     for (uint32_t i = 1; i < nt; i++) {   // insertion sort by edge id (in-degree is small)
@@ -460,6 +481,7 @@ constexpr int SW_WAVES = 4;
 constexpr int SW_CAP = 1024;  // edges alive across one row (per wave of the LDS sweep)
 constexpr int SW_CAP_BLOCK = SW_WAVES * SW_CAP;   // ... a chunk past that: one wave with the block's whole pool
 constexpr int SW_NE = 192;    // edges starting inside the 64-row chunk, staged in LDS
+constexpr int SW_LDS_BLOCKS = 512;
 
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -475,6 +497,7 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
         const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
+        const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ err, uint32_t *E, uint32_t *C, uint32_t *P, uint32_t *I, uint32_t *NC, uint32_t *NP,
         uint32_t *NI) {
     const uint32_t lid = threadIdx.x & 63;
@@ -486,6 +509,7 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
     const uint32_t rf_v = lid < nr ? rowflags[rr] : 0u;
     const uint32_t voff_v = lid < nr ? vert_off[rr] : 0u;
     const uint32_t coff_v = lid < nr ? curve_off[rr] : 0u;
+    const uint32_t koff_v = lid < nr ? kept_off[rr] : 0u;
     const uint32_t E1 = edge_off[R1];
     const uint32_t E0 = (uint32_t)__builtin_amdgcn_readlane((int)eoff_v, 0);
     const bool staged = E1 - E0 <= (uint32_t)SW_NE;
@@ -544,6 +568,7 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
         const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)rf_v, (int)j);
         uint32_t fbase = (uint32_t)__builtin_amdgcn_readlane((int)voff_v, (int)j);
         uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
+        uint32_t kbase = (uint32_t)__builtin_amdgcn_readlane((int)koff_v, (int)j);
         uint32_t kept = 0;
         for (uint32_t base = 0; base < cnt; base += 64) {
             const uint32_t idx = base + lid;
@@ -554,17 +579,20 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
             const bool same = (info & 0x10000000u) != 0;
             const bool full = act && same && c < r && r < p;
             const bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
-            const bool curv = act && !same && c <= r && r <= p && !skip;
+            const bool curv = act && !same && c <= r && r <= p;   // the superset (no strip flag)
+            const bool kcur = curv && !skip;                       // this pass's filtered list
             const bool keep = act && p > r;
-            const uint64_t mf = __ballot(full), mc = __ballot(curv), mk = __ballot(keep);
+            const uint64_t mf = __ballot(full), mc = __ballot(curv), mk = __ballot(keep), mq = __ballot(kcur);
             if (full) vert[fbase + mbcnt(mf)] = pack_vert(info & 0xFFFFFFu, WG_VERT_FULL, (info >> 24) & 0xFu);
             if (curv) { const uint32_t o = cbase + mbcnt(mc); curve_ref[o] = eid; curve_row[o] = (uint32_t)r; }
+            if (kcur) { const uint32_t o = kbase + mbcnt(mq); kept_ref[o] = eid; kept_row[o] = (uint32_t)r; }
             if (keep) {
                 const uint32_t o = kept + mbcnt(mk);
                 E[o] = eid; C[o] = c; P[o] = p; I[o] = info;
             }
             fbase += __builtin_popcountll(mf);
             cbase += __builtin_popcountll(mc);
+            kbase += __builtin_popcountll(mq);
             kept += __builtin_popcountll(mk);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -580,6 +608,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         const uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
+        const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ err, Cap vc, Cap sc, uint32_t *ovf) {
     if (over(vc, ovf) || over(sc, ovf)) return;   // (uniform over the grid)
     __shared__ uint32_t s_eid[SW_CAP_BLOCK];
@@ -597,7 +626,8 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
     for (uint32_t i = blockIdx.x * SW_WAVES + w; i < cnt; i += gridDim.x * SW_WAVES) {
         const uint32_t o = (uint32_t)w * SW_CAP;
         const bool ok = sweep_chunk_lds(SW_CAP, list[i], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
-                                        curve_off, vert, curve_ref, curve_row, err, s_eid + o, s_c + o, s_p + o,
+                                        curve_off, vert, curve_ref, curve_row, kept_off, kept_ref, kept_row, err,
+                                        s_eid + o, s_c + o, s_p + o,
                                         s_info + o, n_c[w], n_p[w], n_info[w]);
         if (!ok && (threadIdx.x & 63) == 0) {
             const uint32_t at = atomicAdd(&n_wide, 1u);
@@ -612,7 +642,8 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
     if (w == 0)
         for (uint32_t j = 0; j < nw; j++)
             if (!sweep_chunk_lds(SW_CAP_BLOCK, wide[j], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
-                                 curve_off, vert, curve_ref, curve_row, err, s_eid, s_c, s_p, s_info, n_c[0], n_p[0],
+                                 curve_off, vert, curve_ref, curve_row, kept_off, kept_ref, kept_row, err, s_eid, s_c,
+                                 s_p, s_info, n_c[0], n_p[0],
                                  n_info[0]) &&
                 (threadIdx.x & 63) == 0)
                 atomicOr(&err[0], 1u);
@@ -628,38 +659,63 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
 constexpr int SW_SLOTS = 8;
 
 // The chunk's carry-in list (registration order) ranked into edge order:
-// edge ids are distinct, so rank = the number of smaller ids
-__device__ __forceinline__ void carry_rank(const uint32_t *__restrict__ carry, uint32_t len, uint32_t *out) {
-    for (uint32_t i = threadIdx.x & 63; i < len; i += 64) {
-        const uint32_t x = carry[i];
+// edge ids are distinct, so rank = the number of smaller ids.  The list is
+// staged once in the wave's LDS (padded with ~0, which no id exceeds) and
+// ranked from there, four ids per broadcast read — a rank loop over HBM
+// waits one load latency per id (a 160-lane list: 80 waits per lane).
+constexpr uint32_t SW_STAGE = 64u * SW_SLOTS;   // ids staged per wave
+__device__ __forceinline__ void carry_rank(const uint32_t *__restrict__ carry, uint32_t len, uint32_t *stage,
+                                           uint32_t *out) {
+    const uint32_t lid = threadIdx.x & 63;
+    if (len > SW_STAGE) {   // (the LDS-sweep chunks only: ranked from HBM)
+        for (uint32_t i = lid; i < len; i += 64) {
+            const uint32_t x = carry[i];
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < len; j++) rank += carry[j] < x;
+            out[rank] = x;
+        }
+        return;
+    }
+    for (uint32_t i = lid; i < ((len + 3) & ~3u); i += 64) stage[i] = i < len ? carry[i] : ~0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(stage);
+    for (uint32_t i = lid; i < len; i += 64) {
+        const uint32_t x = stage[i];
         uint32_t rank = 0;
-        for (uint32_t j = 0; j < len; j++) rank += carry[j] < x;
+        for (uint32_t j = 0; j < (len + 3) / 4; j++) {
+            const uint4 v = s4[j];
+            rank += (v.x < x) + (v.y < x) + (v.z < x) + (v.w < x);
+        }
         out[rank] = x;
     }
 }
 
-__global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nch, const wg_edge *__restrict__ edges,
+__global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0, uint64_t q1, const wg_edge *__restrict__ edges,
         const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
         const uint32_t *__restrict__ carry, uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
+        const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, Cap cc, uint32_t *ovf) {
     __shared__ uint32_t s_car[SW_WAVES][64 * SW_SLOTS];
+    __shared__ __attribute__((aligned(16))) uint32_t s_stage[SW_WAVES][SW_STAGE];
     const uint32_t lid = threadIdx.x & 63;
-    const uint64_t q = (uint64_t)blockIdx.x * SW_WAVES + (threadIdx.x >> 6);
-    if (over(vc, ovf) || over(sc, ovf) || over(cc, ovf) || q >= nch) return;
+    const uint64_t q = q0 + (uint64_t)blockIdx.x * SW_WAVES + (threadIdx.x >> 6);   // chunks [q0, q1)
+    if (over(vc, ovf) || over(sc, ovf) || over(cc, ovf) || q >= q1) return;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
     const uint32_t a = carry_off[q], ncar = carry_off[q + 1] - a;
     const uint32_t E0 = edge_off[R0], E1 = edge_off[R1];
     const uint32_t total = ncar + (E1 - E0);
     if (total > reg_cap || total > 64u * SW_SLOTS) {   // the LDS sweep (k_sweep_lds) reads the ranked list from HBM
-        carry_rank(carry + a, ncar, carry_sorted + a);
+        carry_rank(carry + a, ncar, s_stage[threadIdx.x >> 6], carry_sorted + a);
         if (lid == 0) big[atomicAdd(big_n, 1u)] = (uint32_t)q;
         return;
     }
     uint32_t *sorted = s_car[threadIdx.x >> 6];
-    carry_rank(carry + a, ncar, sorted);
+    carry_rank(carry + a, ncar, s_stage[threadIdx.x >> 6], sorted);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -667,12 +723,15 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
     const uint64_t rr = R0 + lid;
     const uint32_t voff_v = lid < nr ? vert_off[rr] : 0u;
     const uint32_t coff_v = lid < nr ? curve_off[rr] : 0u;
+    const uint32_t koff_v = lid < nr ? kept_off[rr] : 0u;
+    const uint32_t rf_v = lid < nr ? rowflags[rr] : 0u;
     // per slot: the edge id, the packed full-vertical entry and two row windows
     // as (first row, length - 1) for an unsigned compare: full verticals on
     // rows c < r < p of same-lane edges, curve segments on rows c <= r <= p of
-    // cross-lane edges; an empty window has first row ~0.  The sweep always runs
-    // on the all-zero flag row (the curve lists are a superset, filtered per
-    // pass), so no strip flag enters the row loop.
+    // cross-lane edges; an empty window has first row ~0.  The curve lists are
+    // written twice: the superset (no strip flag: refiltered by later frame
+    // passes) and this pass's list filtered by the row's strip flags (the same
+    // entries when the row has none).
     uint32_t ek[SW_SLOTS], fb[SW_SLOTS], fl[SW_SLOTS], cb[SW_SLOTS], cl[SW_SLOTS], pv[SW_SLOTS];
     const uint32_t nslots = (total + 63) / 64;
 #pragma unroll
@@ -695,11 +754,12 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
             }
         }
     }
-    (void)rowflags;
     for (uint32_t j = 0; j < nr; j++) {
         const uint32_t r = (uint32_t)(R0 + j);
         uint32_t fbase = (uint32_t)__builtin_amdgcn_readlane((int)voff_v, (int)j);
         uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
+        uint32_t kbase = (uint32_t)__builtin_amdgcn_readlane((int)koff_v, (int)j);
+        const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)rf_v, (int)j);
 #pragma unroll
         for (int sl = 0; sl < SW_SLOTS; sl++) {
             if ((uint32_t)sl >= nslots) break;
@@ -713,6 +773,14 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t nc
             if (mc) {
                 if (curv) { const uint32_t o = cbase + mbcnt(mc); curve_ref[o] = ek[sl]; curve_row[o] = r; }
                 cbase += __builtin_popcountll(mc);
+                uint64_t mk = mc;
+                if (rf) {   // (uniform) curve_kept: r == c -> RF_CHILD, r == p -> RF_PARENT, else RF_ZERO
+                    const uint32_t d = r - cb[sl];
+                    const uint32_t skip = d == 0 ? (rf & RF_CHILD) : (d == cl[sl] ? (rf & RF_PARENT) : (rf & RF_ZERO));
+                    mk = __ballot(curv && !skip);
+                }
+                if ((mk >> lid) & 1ull) { const uint32_t o = kbase + mbcnt(mk); kept_ref[o] = ek[sl]; kept_row[o] = r; }
+                kbase += __builtin_popcountll(mk);
             }
         }
     }
@@ -802,47 +870,64 @@ __device__ __forceinline__ Cubic edge_cubic(const wg_edge &e, uint32_t ref, cons
 // are (a frame whose bands and row_top are unchanged above row pmin)
 // refilt (the frame pass): nonzero = the curve lists were refiltered by this
 // pass (every record moved: all are recomputed)
-__global__ void k_curves_tb(const uint32_t *__restrict__ nc, const uint32_t *__restrict__ curve_ref,
+// records [*lo (0 when null), *hi): the counts live on the device; grid-stride
+// (a row slice's grid is sized by a guess)
+__global__ void k_curves_tb(const uint32_t *__restrict__ lo, const uint32_t *__restrict__ hi,
+                            const uint32_t *__restrict__ curve_ref,
                             const uint32_t *__restrict__ curve_row, const wg_edge *__restrict__ edges,
                             const float *__restrict__ row_top, const float *__restrict__ node_y,
                             const float2 *__restrict__ edge_y, float *__restrict__ tb, uint32_t pmin, Cap sc,
                             uint32_t *ovf, const uint32_t *__restrict__ refilt) {
-    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (over(sc, ovf) || k >= *nc) return;   // grid sized by an upper bound; the count lives on the device
+    if (over(sc, ovf)) return;
     if (refilt && *refilt) pmin = 0;
-    const uint32_t ref = curve_ref[k];
-    const wg_edge e = edges[ref];
-    if (e.parent_row < pmin) return;
-    const uint32_t row = curve_row[k];
-    if (row == e.parent_row) return;         // t_b = 1 (:589-593)
-    float child_y, parent_y;
-    const Cubic cv = edge_cubic(e, ref, row_top, node_y, edge_y, &child_y, &parent_y);
-    tb[k] = t_at_y(cv, row_top[row + 1]);    // strip_bot = row bottom (:574-578)
+    const uint32_t k1 = *hi;
+    for (uint64_t k = (lo ? *lo : 0u) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < k1;
+         k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t ref = curve_ref[k];
+        const wg_edge e = edges[ref];
+        if (e.parent_row < pmin) continue;
+        const uint32_t row = curve_row[k];
+        if (row == e.parent_row) continue;       // t_b = 1 (:589-593)
+        float child_y, parent_y;
+        const Cubic cv = edge_cubic(e, ref, row_top, node_y, edge_y, &child_y, &parent_y);
+        tb[k] = t_at_y(cv, row_top[row + 1]);    // strip_bot = row bottom (:574-578)
+    }
 }
 
-__global__ void k_curves(const uint32_t *__restrict__ nc, const uint32_t *__restrict__ curve_ref,
+// row_lo: the first row of the slice; the row above it belongs to another
+// slice (its t_b may not be computed yet): bisected here
+__global__ void k_curves(const uint32_t *__restrict__ lo, const uint32_t *__restrict__ hi, uint32_t row_lo,
+                         const uint32_t *__restrict__ curve_ref,
                          const uint32_t *__restrict__ curve_row, const uint32_t *__restrict__ curve_off,
                          const wg_edge *__restrict__ edges, const float *__restrict__ row_top,
                          const float *__restrict__ node_y, const float2 *__restrict__ edge_y,
                          const float *__restrict__ tb, wg_curve *__restrict__ out, uint8_t *__restrict__ out_color,
                          uint32_t pmin, Cap sc, uint32_t *ovf, const uint32_t *__restrict__ refilt) {
-    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (over(sc, ovf) || k >= *nc) return;
+    if (over(sc, ovf)) return;
     if (refilt && *refilt) pmin = 0;
+    const uint32_t k1 = *hi;
+    for (uint64_t k = (lo ? *lo : 0u) + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < k1;
+         k += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t ref = curve_ref[k];
     const wg_edge e = edges[ref];
-    if (e.parent_row < pmin) return;
+    if (e.parent_row < pmin) continue;
     const uint32_t row = curve_row[k];
     float child_y, parent_y;
     const Cubic cv = edge_cubic(e, ref, row_top, node_y, edge_y, &child_y, &parent_y);
     const float rtop = row_top[row];
     const float strip_top = (row == e.child_row) ? child_y : rtop;
     float t_a = 0.0f;
-    if (row != e.child_row) {
+    if (row != e.child_row && row == row_lo) {
+        t_a = t_at_y(cv, strip_top);   // (the same value the row above's record holds as its t_b)
+    } else if (row != e.child_row) {
         // the same edge's record in row - 1 holds t_at_y(row_top[row]) as its t_b
-        const uint32_t a0 = curve_off[row - 1], a1 = curve_off[row];
-        uint32_t j = a0;
-        while (j < a1 && curve_ref[j] < ref) j++;   // edge order
+        // (lower bound by bisection: the list is in edge order; a wide row
+        // holds hundreds of records)
+        uint32_t j = curve_off[row - 1], a1 = curve_off[row], hi = a1;
+        while (j < hi) {
+            const uint32_t mid = j + (hi - j) / 2;
+            if (curve_ref[mid] < ref) j = mid + 1; else hi = mid;
+        }
         t_a = (j < a1 && curve_ref[j] == ref) ? tb[j] : t_at_y(cv, strip_top);
     }
     const float t_b = (row == e.parent_row) ? 1.0f : tb[k];
@@ -851,6 +936,7 @@ __global__ void k_curves(const uint32_t *__restrict__ nc, const uint32_t *__rest
     o[0] = make_float4(s.p0.x, s.p0.y - rtop, s.p1.x, s.p1.y - rtop);
     o[1] = make_float4(s.p2.x, s.p2.y - rtop, s.p3.x, s.p3.y - rtop);
     out_color[k] = (uint8_t)e.color;
+    }
 }
 
 inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
@@ -858,7 +944,9 @@ inline uint32_t blocks(uint64_t n) { return (uint32_t)((n + T - 1) / T); }
 // Curve lists are swept once per layout as a superset (every cross-lane
 // segment c <= r <= p, strip flags ignored) and filtered per geometry pass by
 // the row's own flags (:577): r == c needs a child strip, r == p a parent
-// strip, c < r < p a non-zero-height row.
+// strip, c < r < p a non-zero-height row.  The full pass's sweep writes its
+// own filtered lists beside the superset (counts from k_geom_offsets); the
+// frame pass refilters the superset here.
 __device__ __forceinline__ bool curve_kept(uint32_t r, const wg_edge &e, uint32_t f) {
     const uint32_t skip = (r == e.child_row) ? (f & RF_CHILD) : (r == e.parent_row) ? (f & RF_PARENT) : (f & RF_ZERO);
     return skip == 0;
@@ -914,8 +1002,8 @@ __global__ void k_curve_compact(uint64_t n, const uint32_t *__restrict__ soff, c
 
 }  // namespace
 
-// filter the curve superset by this pass's row flags -> curve_off / curve_ref / curve_row.
-// cond (the frame pass, on the device): refilter only if the flags changed —
+// filter the curve superset by a frame pass's row flags -> curve_off / curve_ref / curve_row.
+// cond (on the device): refilter only if the flags changed —
 // otherwise the same offsets are rescanned and the lists stand, no host read.
 static Cap no_cap() { return Cap{nullptr, ~0u, nullptr}; }
 static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *cond, Cap sc, uint32_t *ovf) {
@@ -944,15 +1032,18 @@ static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *c
     return WG_OK;
 }
 
-static void launch_curves(wg_ctx *c, uint64_t n, uint64_t n_upper, hipStream_t s, uint32_t pmin, Cap sc, uint32_t *ovf,
-                          const uint32_t *refilt) {
-    if (!n_upper) return;
-    hipLaunchKernelGGL(k_curves_tb, dim3(blocks(n_upper)), dim3(T), 0, s, c->curve_off.as<const uint32_t>() + n,
+// curve records of rows [r0, r1) (their range read on the device); grid: an
+// upper bound of the records, or a guess (the kernels stride)
+static void launch_curves(wg_ctx *c, uint64_t r0, uint64_t r1, uint64_t grid_recs, hipStream_t s, uint32_t pmin, Cap sc,
+                          uint32_t *ovf, const uint32_t *refilt) {
+    if (!grid_recs || r1 <= r0) return;
+    const uint32_t *lo = r0 ? c->curve_off.as<const uint32_t>() + r0 : nullptr;
+    hipLaunchKernelGGL(k_curves_tb, dim3(blocks(grid_recs)), dim3(T), 0, s, lo, c->curve_off.as<const uint32_t>() + r1,
                        c->curve_ref.as<const uint32_t>(), c->curve_row.as<const uint32_t>(), c->edges.as<const wg_edge>(),
                        c->g_row_top.as<const float>(), c->g_node_y.as<const float>(),
                        reinterpret_cast<const float2 *>(c->edge_y), c->curve_tb.as<float>(), pmin, sc, ovf, refilt);
-    hipLaunchKernelGGL(k_curves, dim3(blocks(n_upper)), dim3(T), 0, s, c->curve_off.as<const uint32_t>() + n,
-                       c->curve_ref.as<const uint32_t>(), c->curve_row.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
+    hipLaunchKernelGGL(k_curves, dim3(blocks(grid_recs)), dim3(T), 0, s, lo, c->curve_off.as<const uint32_t>() + r1,
+                       (uint32_t)r0, c->curve_ref.as<const uint32_t>(), c->curve_row.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
                        c->edges.as<const wg_edge>(), c->g_row_top.as<const float>(), c->g_node_y.as<const float>(),
                        reinterpret_cast<const float2 *>(c->edge_y), c->curve_tb.as<const float>(), c->curve.as<wg_curve>(),
                        c->curve_color.as<uint8_t>(), pmin, sc, ovf, refilt);
@@ -1003,7 +1094,61 @@ bool wg_geom_spec_check(wg_ctx *c, const uint64_t *v) {
     return true;
 }
 
+int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s) {
+    const wg_ctx::ListsDef &L = c->glist;
+    const uint64_t n = L.n;
+    if (r1 > n || r0 >= r1 || (r0 % WG_SWEEP_CH) || (r1 != n && (r1 % WG_SWEEP_CH)))
+        return wg_fail(c, WG_E_INVALID, "list slice [%llu,%llu) of %llu rows", (unsigned long long)r0, (unsigned long long)r1,
+                       (unsigned long long)n);
+    const wg_edge *E = c->edges.as<const wg_edge>();
+    const uint32_t *edge_off = c->edge_cnt.as<const uint32_t>();
+    const uint32_t *voff = c->vert_off.as<const uint32_t>(), *soff = c->scurve_off.as<const uint32_t>();
+    const uint32_t *koff = c->curve_off.as<const uint32_t>(), *carry_off = c->carry_off.as<const uint32_t>();
+    const Cap vc{L.vtot, L.vcap, nullptr}, sc{L.stot, L.scap, nullptr}, cc{L.ctot, L.ccap, nullptr};
+    uint32_t *err = L.err, *ovf = err + 8;
+    uint32_t *vert = c->vert.as<uint32_t>();
+    hipLaunchKernelGGL(k_top_finish, dim3(blocks(r1 - r0)), dim3(T), 0, s, r0, r1, edge_off, E, voff, L.cntF, L.cntT, vert,
+                       vc, ovf);
+    // chunks too wide for the register sweep: listed per slice (counts in
+    // err[1] / err[4]) and swept through LDS
+    const uint64_t q0 = r0 / WG_SWEEP_CH, q1 = (r1 + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
+    uint32_t *big = c->sweep_big.as<uint32_t>() + q0, *big_n = err + (slice ? 4 : 1);
+    uint32_t *carry_sorted = c->carry_sorted.as<uint32_t>();
+    hipLaunchKernelGGL(k_sweep, dim3((uint32_t)((q1 - q0 + SW_WAVES - 1) / SW_WAVES)), dim3(64 * SW_WAVES), 0, s, n, q0, q1, E,
+                       edge_off, carry_off, (const uint32_t *)c->carry.as<uint32_t>(), carry_sorted,
+                       c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
+                       c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), big,
+                       big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, vc, sc, cc, ovf);
+    // (one wave per wide chunk, ~73 KB of LDS per block: two blocks per CU,
+    // the whole chip for lists whose every chunk is wide; sized by the last
+    // pass's count of wide chunks; 64 blocks for a list that had none, as
+    // many as before r04: a block lists at most 64 chunks past one wave's
+    // pool for its whole-block pass)
+    const uint64_t lds_want = 64 + (uint64_t)c->sweep_wide_last / SW_WAVES;
+    const uint64_t lds_grid = std::min<uint64_t>(std::min<uint64_t>(SW_LDS_BLOCKS, lds_want),
+                                                 (q1 - q0 + SW_WAVES - 1) / SW_WAVES);
+    hipLaunchKernelGGL(k_sweep_lds, dim3((uint32_t)lds_grid), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)big,
+                       (const uint32_t *)big_n, E, edge_off, carry_off, (const uint32_t *)carry_sorted,
+                       c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
+                       c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), err,
+                       vc, sc, ovf);
+    // the records of the slice's rows: a grid for its share of the records
+    // (+ a quarter), the kernels stride over the rest
+    uint64_t grid_recs = L.n_super_grid;
+    if (r1 - r0 < n) grid_recs = std::min<uint64_t>(L.n_super_grid, L.n_super_grid * (r1 - r0) / n * 5 / 4 + 64 * T);
+    launch_curves(c, r0, r1, grid_recs, s, 0u, sc, ovf, nullptr);
+    WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+int wg_geom_lists_flush(wg_ctx *c) {
+    if (!c->glist.deferred) return WG_OK;
+    c->glist.deferred = false;
+    return wg_geom_lists(c, 0, c->glist.n, 0, c->stream);
+}
+
 int wg_stage_geometry(wg_ctx *c, const float *d_band) {
+    if (const int rc = wg_geom_lists_flush(c)) return rc;   // (a deferred pass's lists, before anything reuses them)
     if (const int rc = wg_side_join(c)) return rc;
     const uint64_t n = c->n, ne = c->n_edges;
     hipStream_t s = c->stream;
@@ -1046,7 +1191,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         wg_stage_end(c);
         wg_stage_begin(c, "geom_curves");
         // re-filtered lists move every record: all of them are recomputed then
-        launch_curves(c, n, c->lists_nsuper, s, (uint32_t)r0, bg, diff + 8, diff);
+        launch_curves(c, 0, n, c->lists_nsuper, s, (uint32_t)r0, bg, diff + 8, diff);
         WG_HIP(c, hipGetLastError());
         wg_stage_end(c);
         c->geom_sum_at[0] = rt + n;
@@ -1074,15 +1219,17 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     // are swept as a superset.
     const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
     const uint64_t rowa = (n + 2 + 63) & ~63ull, cha = (nch + 2 + 63) & ~63ull;
-    const uint64_t zwords = (6 * rowa + 2 * cha + 64 + rowa / 4 + 3) & ~3ull;   // cleared in 16-byte units
+    const uint64_t zwords = (7 * rowa + 2 * cha + 64 + rowa / 4 + 3) & ~3ull;   // cleared in 16-byte units
     WG_ALLOC(c, c->geom_zero, zwords * 4);
+    WG_ALLOC(c, c->rowflags_lists, n + 4);
     uint32_t *cntF = c->geom_zero.as<uint32_t>(), *cntT = cntF + rowa, *cntB = cntT + rowa;
-    uint32_t *cntC = cntB + rowa, *cntCend = cntC + rowa, *top_fill = cntCend + rowa;
+    uint32_t *cntC = cntB + rowa, *cntCend = cntC + rowa, *cntPend = cntCend + rowa, *top_fill = cntPend + rowa;
     uint32_t *carry_cnt = top_fill + rowa, *carry_fill = carry_cnt + cha, *sweep_err = carry_fill + cha;
     uint32_t *ovf = sweep_err + 8;   // capacity overflow of a speculative pass
     c->geom_err = sweep_err;
     const uint8_t *zflags = reinterpret_cast<const uint8_t *>(sweep_err + 64);
     uint32_t *voff = c->vert_off.as<uint32_t>(), *soff = c->scurve_off.as<uint32_t>();
+    uint32_t *koff = c->curve_off.as<uint32_t>();
 
     wg_stage_begin(c, "geom_counts");
     {
@@ -1098,14 +1245,15 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         A.h = h; A.band = d_band; A.row_top = rt;
         A.height = c->g_height.as<float>(); A.node_y = c->g_node_y.as<float>(); A.band_keep = c->band_keep;
         A.rowflags = c->rowflags.as<uint8_t>(); A.zflags = const_cast<uint8_t *>(zflags);
-        A.cntB = cntB; A.diffF = cntF; A.diffC = cntC; A.cntCend = cntCend; A.carry_diff = carry_cnt;
+        A.flags_kept = c->rowflags_lists.as<uint8_t>();
+        A.cntB = cntB; A.diffF = cntF; A.diffC = cntC; A.cntCend = cntCend; A.cntPend = cntPend; A.carry_diff = carry_cnt;
         A.cntT = cntT; A.top_fill = top_fill; A.carry_fill = carry_fill; A.misc = sweep_err;
         hipLaunchKernelGGL(k_edges_rows, dim3(blocks(n)), dim3(256), 0, s, n, A);
         c->edges_pending = false;
     }
     if (ne)
         hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntT, cntF, cntC, cntCend,
-                           carry_cnt, ne_dev);
+                           cntPend, carry_cnt, ne_dev);
     // carry-in offsets: the exclusive scan of the chunk difference counts, then
     // of the per-chunk counts it holds one entry later
     WG_ALLOC(c, c->carry_off, (nch + 2) * 4);
@@ -1115,20 +1263,22 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     // scans, the per-row list totals and the per-chunk carry counts (+ their
     // 256-entry sums); one launch for the three offset arrays
     const uint64_t nbs = wg_bs_blocks(n), nbsD = wg_bs_blocks(nch), nt2 = (n + 1 + GO_TILE - 1) / GO_TILE;
-    WG_ALLOC(c, c->bsum, (2 * nbs + nbsD + 3 * nt2 + 512) * 4);
-    uint32_t *bsV = c->bsum.as<uint32_t>(), *bsC = bsV + nbs, *bsD = bsC + nbs;
+    WG_ALLOC(c, c->bsum, (3 * nbs + nbsD + 3 * nt2 + 512) * 4);
+    uint32_t *bsV = c->bsum.as<uint32_t>(), *bsC = bsV + nbs, *bsK = bsC + nbs, *bsD = bsK + nbs;
     uint32_t *tsF = bsD + nbsD + 64, *tsC = tsF + nt2 + 64, *tsD = tsC + nt2 + 64;
     hipLaunchKernelGGL(k_tile_sums3, dim3((uint32_t)nt2, 3), dim3(GO_T), 0, s, (const uint32_t *)cntF, (const uint32_t *)cntC,
                        (const uint32_t *)carry_cnt, n + 1, nch + 1, tsF, tsC, tsD);
     hipLaunchKernelGGL(k_geom_offsets, dim3((uint32_t)nt2), dim3(GO_T), 0, s, n, cntF, cntC, (const uint32_t *)tsF,
                        (const uint32_t *)tsC, (const uint32_t *)cntT, (const uint32_t *)cntB, (const uint32_t *)cntCend,
-                       voff, soff, bsV, bsC, nbs, carry_cnt, (const uint32_t *)tsD, nch, bsD, nbsD);
+                       voff, soff, bsV, bsC, nbs, carry_cnt, (const uint32_t *)tsD, nch, bsD, nbsD,
+                       (const uint32_t *)cntPend, c->rowflags.as<const uint8_t>(), koff, bsK);
     {
         WgScanBs S;
-        S.na = 3;
+        S.na = 4;
         S.in[0] = voff; S.out[0] = voff; S.bsum[0] = bsV;
         S.in[1] = soff; S.out[1] = soff; S.bsum[1] = bsC;
         S.in[2] = carry_cnt; S.out[2] = carry_off; S.bsum[2] = bsD; S.len[2] = nch;
+        S.in[3] = koff; S.out[3] = koff; S.bsum[3] = bsK;
         WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, s));
     }
     // list capacities: exact from the totals, or (speculative build) the
@@ -1178,37 +1328,37 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     if (ne)
         hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, vert,
                            (const uint32_t *)carry_off, carry_fill, c->carry.as<uint32_t>(), ne_dev, vc, cc, ovf);
-    hipLaunchKernelGGL(k_top_finish, dim3(blocks(n)), dim3(T), 0, s, n, edge_off, E, voff, cntF, cntT, vert, vc, ovf);
-    uint32_t *carry_sorted = c->carry_sorted.as<uint32_t>();
-    // chunks too wide for the register sweep are listed in sweep_err[2..] and swept through LDS
-    uint32_t *big_n = sweep_err + 1;
     WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
-    hipLaunchKernelGGL(k_sweep, dim3((nch + SW_WAVES - 1) / SW_WAVES), dim3(64 * SW_WAVES), 0, s, n, nch, E, edge_off,
-                       (const uint32_t *)carry_off, (const uint32_t *)c->carry.as<uint32_t>(), carry_sorted, zflags,
-                       voff, (const uint32_t *)soff, vert, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
-                       c->sweep_big.as<uint32_t>(), big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS,
-                       vc, sc, cc, ovf);
-    hipLaunchKernelGGL(k_sweep_lds, dim3(64), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)c->sweep_big.as<uint32_t>(),
-                       (const uint32_t *)big_n, E, edge_off, (const uint32_t *)carry_off,
-                       (const uint32_t *)carry_sorted, zflags, voff, (const uint32_t *)soff, vert,
-                       c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(), sweep_err, vc, sc, ovf);
-    WG_HIP(c, hipGetLastError());
-    {
-        const int rc = filter_curves(c, n, s, nullptr, sc, ovf);
-        if (rc != WG_OK) return rc;
+    wg_ctx::ListsDef &L = c->glist;
+    L = wg_ctx::ListsDef{};
+    L.n = n;
+    L.n_super_grid = n_super_grid;
+    L.cntF = cntF;
+    L.cntT = cntT;
+    L.vtot = vc.total; L.vcap = vc.cap;
+    L.stot = sc.total; L.scap = sc.cap;
+    L.ctot = cc.total; L.ccap = cc.cap;
+    L.err = sweep_err;
+    // a speculative pass validated with the emission's read: the lists are
+    // left to the emission (row-sliced under its first tiles).  Below ~256K
+    // rows the list kernels sit at the launch floor: slicing would only add
+    // five launches.
+    if (spec && c->defer_validation && c->slice_on && !c->sh.on && n >= c->slice_min_rows) {
+        L.deferred = true;
+        WG_HIP(c, hipGetLastError());
+        wg_stage_end(c);
+        return WG_OK;
     }
-    wg_stage_end(c);
-    wg_stage_begin(c, "geom_curves");
-    launch_curves(c, n, n_super_grid, s, 0u, sc, ovf, nullptr);
-    WG_HIP(c, hipGetLastError());
+    if (const int rc = wg_geom_lists(c, 0, n, 0, s)) return rc;
     wg_stage_end(c);
     if (spec) return WG_OK;   // validated at the end of the build (wg_geom_spec_items / wg_geom_spec_check)
-    uint64_t fin[4] = {0, 0, 0, 0};
+    uint64_t fin[5] = {0, 0, 0, 0, 0};
     {
         const int rc = wg_fetch(c, {{sweep_err, false}, {rt + n, false}, {c->rt_flags.as<uint32_t>() + 2, false},
-                                    {c->curve_off.as<uint32_t>() + n, false}}, fin);
+                                    {c->curve_off.as<uint32_t>() + n, false}, {sweep_err + 1, false}}, fin);
         if (rc != WG_OK) return rc;
     }
+    c->sweep_wide_last = (uint32_t)fin[4];
     if (fin[0]) return wg_fail(c, WG_E_UNSUPPORTED, "more than %d edges alive across one row", SW_CAP_BLOCK);
     c->n_curve = fin[3];
     c->lists_nsuper = n_super_grid;

@@ -450,6 +450,26 @@ struct wg_ctx {
     DevBuf sweep_big;       // uint32 [nch] chunks too wide for the register sweep
     uint32_t sweep_reg_cap = 512;   // edges per chunk the register sweep holds (WG_OPT_SWEEP_REG)
     const float *edge_y = nullptr;   // per edge {child_y, parent_y} override (row-sharded geometry), or null
+    // Row-sliced lists (wg_geom_lists): a speculative full pass whose
+    // validation rides on the emission leaves its list kernels (top halves,
+    // sweep, curve clipping) to wg_stage_vertices, which runs rows [0, h) first
+    // and rows [h, n) on the side stream beside the emission of the first
+    // slice's tiles.  Any other call runs them whole first (WG_SETTLE).
+    struct ListsDef {
+        bool deferred = false;
+        uint64_t n = 0, n_super_grid = 0;
+        const uint32_t *cntF = nullptr, *cntT = nullptr;
+        const uint32_t *vtot = nullptr, *stot = nullptr, *ctot = nullptr;   // the lists' scanned totals (capacity checks)
+        uint32_t vcap = ~0u, scap = ~0u, ccap = ~0u;
+        uint32_t *err = nullptr;   // the pass's flag words (geom_err)
+    } glist;
+    bool     slice_on = true;      // WG_OPT_SLICE_LISTS
+    double   slice_frac = 0.25;
+    uint64_t slice_min_rows = 1ull << 18;   // (WG_OPT_SLICE_LISTS = 2: every list of >= 4 chunks, for the tests)
+    uint64_t vtx_t1_last = 0;      // the last sliced emission's first second-slice tile (part 1's grid)
+    uint32_t sliced_emits = 0;     // emissions that ran row-sliced lists (wg_debug_counters [11])
+    uint32_t sweep_wide_last = 0;  // the last read pass's chunks past the register sweep (sizes the LDS sweep's grid)
+    hipEvent_t ev_slice = nullptr;
     // ---- vertices -------------------------------------------------------------
     bool     have_vtx = false;
     uint64_t vrow_begin = 0, vrow_end = 0, n_vtx = 0;
@@ -522,7 +542,7 @@ int wg_validate_pending(wg_ctx *c, const uint64_t *v, bool *redone);
 int wg_shard_geom_validate(wg_ctx *c, const uint64_t *v, bool *redo);
 #define WG_SETTLE(c)                                                               \
     do {                                                                           \
-        if ((c)->pend.build) {                                                     \
+        if ((c)->pend.build || (c)->glist.deferred) {                              \
             const int _sr = wg_settle(c);                                          \
             if (_sr != WG_OK) return _sr;                                          \
         }                                                                          \
@@ -601,7 +621,7 @@ hipError_t wg_exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, 
 // wg_bsum_store(v, bsum) with every thread of the block (it synchronises the
 // block) and so leaves bsum[blockIdx.x] = the block's sum.  The down-sweep
 // then needs one launch (up to WG_BS_SELF tile sums; more add a scan of the
-// sums first).  Up to three arrays of the same length share the launches.
+// sums first).  Up to four arrays of the same length share the launches.
 constexpr int WG_BS_THREADS = 256;
 constexpr uint64_t WG_BS_SELF = 8192;
 __device__ __forceinline__ void wg_bsum_store(uint32_t v, uint32_t *__restrict__ bsum) {
@@ -619,10 +639,10 @@ __device__ __forceinline__ void wg_bsum_store(uint32_t v, uint32_t *__restrict__
 }
 struct WgScanBs {
     int na = 0;
-    const uint32_t *in[3] = {nullptr, nullptr, nullptr};
-    uint32_t *out[3] = {nullptr, nullptr, nullptr};
-    const uint32_t *bsum[3] = {nullptr, nullptr, nullptr};   // [ceil(n / WG_BS_THREADS)] each
-    uint64_t len[3] = {0, 0, 0};   // an array shorter than n (0: n)
+    const uint32_t *in[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint32_t *out[4] = {nullptr, nullptr, nullptr, nullptr};
+    const uint32_t *bsum[4] = {nullptr, nullptr, nullptr, nullptr};   // [ceil(n / WG_BS_THREADS)] each
+    uint64_t len[4] = {0, 0, 0, 0};   // an array shorter than n (0: n)
 };
 // out[a][0..n] = exclusive scan of in[a] (out[a][n] = total); in may alias out.
 // tmp: c->scan_tmp after wg_scan_reserve(c, n).
@@ -727,6 +747,10 @@ int wg_geom_summary_sync(wg_ctx *c);                   // read a frame pass's su
 int wg_geom_spec_items(wg_ctx *c, WgFetch *it);        // speculative full pass: WG_GEOM_SPEC_ITEMS validation words
 bool wg_geom_spec_check(wg_ctx *c, const uint64_t *v);
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel);  // wg_vertex.hip
+// the full pass's list kernels for rows [r0, r1) (r0 a multiple of WG_SWEEP_CH;
+// slice 0 or 1: its own wide-chunk list), and all of them when deferred
+int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s);
+int wg_geom_lists_flush(wg_ctx *c);
 int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out);  // wg_vertex.hip
 int wg_words_checksum(wg_ctx *c, const uint32_t *w, uint64_t nwords, uint64_t *out);  // wg_vertex.hip
 void wg_init_height_thresholds(uint32_t *th);  // wg_rowtop.hip

@@ -183,11 +183,11 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan2_down(Pair32 P, uint64_t 
 constexpr uint64_t BS_PER_TILE = SCAN_TILE / WG_BS_THREADS;
 static_assert(SCAN_TILE % WG_BS_THREADS == 0, "producer blocks tile the scan tiles");
 struct ScanBsArgs {
-    const uint32_t *in[3];
-    uint32_t *out[3];
-    const uint32_t *bsum[3];
-    const uint32_t *bpre[3];   // exclusive scan of bsum, or null
-    uint64_t n[3];
+    const uint32_t *in[4];
+    uint32_t *out[4];
+    const uint32_t *bsum[4];
+    const uint32_t *bpre[4];   // exclusive scan of bsum, or null
+    uint64_t n[4];
 };
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_bs_down(ScanBsArgs P) {
     const int a = blockIdx.y;
@@ -255,9 +255,9 @@ hipError_t scan_rec(const TI *in, TO *out, uint64_t n, char *tmp, hipStream_t s)
 }  // namespace
 
 size_t wg_scan_tmp_bytes(uint64_t n) {
-    // + wg_scan_bs_u32's scanned producer sums (three arrays) and their recursion
+    // + wg_scan_bs_u32's scanned producer sums (four arrays) and their recursion
     const uint64_t nbs = wg_bs_blocks(n);
-    return tmp_bytes_rec<uint64_t>(n) + 3 * (((nbs + 1) * 4 + 255) & ~size_t(255)) + tmp_bytes_rec<uint64_t>(nbs) + 1024;
+    return tmp_bytes_rec<uint64_t>(n) + 4 * (((nbs + 1) * 4 + 255) & ~size_t(255)) + tmp_bytes_rec<uint64_t>(nbs) + 1024;
 }
 
 hipError_t wg_exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, void *tmp, hipStream_t s) {
@@ -284,6 +284,7 @@ hipError_t wg_exclusive_scan2_u32(const uint32_t *in0, uint32_t *out0, const uin
 }
 
 hipError_t wg_scan_bs_u32(const WgScanBs &S, uint64_t n, void *tmp, hipStream_t s) {
+    if (S.na < 1 || S.na > 4) return hipErrorInvalidValue;
     ScanBsArgs P{};
     char *t = (char *)tmp;
     for (int a = 0; a < S.na; a++) {
@@ -302,7 +303,7 @@ hipError_t wg_scan_bs_u32(const WgScanBs &S, uint64_t n, void *tmp, hipStream_t 
         }
     }
     if ((size_t)(t - (char *)tmp) + tmp_bytes_rec<uint64_t>(wg_bs_blocks(n)) > wg_scan_tmp_bytes(n))
-        return hipErrorInvalidValue;   // (cannot happen: 3 (n/256 + 65) u32 + the recursion fit the reserve)
+        return hipErrorInvalidValue;   // (cannot happen: 4 (n/256 + 65) u32 + the recursion fit the reserve)
     hipLaunchKernelGGL(k_scan_bs_down, dim3((uint32_t)nblocks(n), (uint32_t)S.na), dim3(SCAN_THREADS), 0, s, P);
     return hipGetLastError();
 }

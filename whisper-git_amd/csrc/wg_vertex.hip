@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         const uint8_t *__restrict__ color_out, const float4 *__restrict__ palette,
         const uint4 *__restrict__ tinfo, const uint8_t *__restrict__ match, int64_t mlo, int64_t mhi,
         float4 *__restrict__ out, uint64_t ntl, const uint32_t *__restrict__ max_lane_dev,
-        const uint32_t *__restrict__ gate) {
+        const uint32_t *__restrict__ gate, int part, uint64_t split_row, uint64_t p1) {
     __shared__ RowInfo rows[MAXR];
     __shared__ __attribute__((aligned(4))) uint8_t pair_row[PAIRS];   // row (within the tile) of every vertex pair
     __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
@@ -163,9 +163,19 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
     // shape: 5.6 -> 6.1-6.3 TB/s (profiles/microbench/store_sweep.hip).  The
     // split follows the device's total, so the working workgroups are the
     // first 8 * per of the grid, on all eight XCDs, whatever the capacity.
-    const uint64_t per = (nt + 7) / 8;
-    const uint64_t tile = (uint64_t)(blockIdx.x % 8u) * per + blockIdx.x / 8u;
-    if (blockIdx.x / 8u >= per || tile >= nt) return;
+    // part 1 / 2 (a row-sliced emission): the tiles before / from tile t1,
+    // the first tile that may hold a vertex of row split_row or later (its
+    // lists are the second slice's, built while part 1 runs); t1 is capped
+    // by part 1's grid p1
+    uint64_t lo = 0, hi = nt;
+    if (part) {
+        uint64_t t1 = vtx_off[split_row] / TILE;
+        t1 = t1 < p1 ? t1 : p1;
+        if (part == 1) hi = t1; else lo = t1;
+    }
+    const uint64_t per = (hi - lo + 7) / 8;
+    const uint64_t tile = lo + (uint64_t)(blockIdx.x % 8u) * per + blockIdx.x / 8u;
+    if (blockIdx.x / 8u >= per || tile >= hi) return;
     const uint64_t v0 = tile * TILE;
     const uint4 ti = tinfo[tile], tn = tinfo[tile + 1];   // everything below hangs on these
     const uint64_t v1 = (v0 + TILE < total) ? v0 + TILE : total;
@@ -444,6 +454,11 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;
     const uint64_t tcap = c->tile_first.cap / sizeof(uint4);
     const bool early = vcap > 0 && tcap > 1;
+    // a full pass's deferred lists (wg_geom_lists): row-sliced under the
+    // emission of the whole list, else run whole here
+    const bool sliced = c->glist.deferred && early && rb == 0 && rows == c->glist.n;
+    if (!sliced)
+        if (const int rc = wg_geom_lists_flush(c)) return rc;
     prep(early ? tcap : 0);
     float q = roundf(c->graph_width / WG_LANE_W);
     uint32_t vis = q <= 0.0f ? 0u : (uint32_t)q;
@@ -453,11 +468,35 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     // fit the last frame's capacity; the kernels exit past the total and
     // write nothing when it does not fit), and relaunched only if needed.
     // a build awaiting its validation (WG_OPT_DEFER_VALIDATION): its words ride on this read
-    WgFetch fi[1 + WG_PENDING_ITEMS];
+    WgFetch fi[4 + WG_PENDING_ITEMS];
     fi[0] = WgFetch{off + rows, true};
     const int npend = c->pend.build ? c->pend.k : 0;
     for (int i = 0; i < npend; i++) fi[1 + i] = c->pend.it[i];
-    if (const int rc = wg_fetch_begin_n(c, 1 + npend, fi)) return rc;
+    // the split row h (a chunk boundary, about slice_frac of the rows): its
+    // vertex offset rides on the read (part 1's grid for the next frame)
+    uint64_t h = 0;
+    if (sliced) {
+        h = (uint64_t)((double)rows * c->slice_frac) / WG_SWEEP_CH * WG_SWEEP_CH;
+        const uint64_t hmax = (rows - 1) / WG_SWEEP_CH * WG_SWEEP_CH;
+        h = h < WG_SWEEP_CH ? WG_SWEEP_CH : (h > hmax ? hmax : h);
+        fi[1 + npend] = WgFetch{off + h, true};
+        fi[2 + npend] = WgFetch{c->glist.err + 1, false};   // the slices' wide chunks
+        fi[3 + npend] = WgFetch{c->glist.err + 4, false};
+    }
+    const int nfi = 1 + npend + (sliced ? 3 : 0);
+    if (sliced) {
+        // (launched below, with the tiles)
+    } else if (early) {
+        // the read on the side stream: the tiles start right after the prep
+        // instead of behind the read's system-scope release (~10 us of L2
+        // write-back on the step's critical path)
+        if (const int rc = wg_side_fork(c)) return rc;
+        const int rc = wg_fetch_begin_n(c, nfi, fi);
+        wg_side_done(c);
+        if (rc) return rc;
+    } else if (const int rc = wg_fetch_begin_n(c, nfi, fi)) {
+        return rc;
+    }
     // (a pending single-GPU build, or a sharded one whose replay is unchecked:
     // graph_width from the device's lane scalars)
     const uint32_t *ml_dev =
@@ -466,17 +505,26 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const uint8_t *match = c->match_on ? c->match_flags.as<const uint8_t>() : nullptr;
     const int64_t mlo = (int64_t)c->match_rb - (int64_t)c->sh.s + (int64_t)c->sh.row_base;
     const int64_t mhi = mlo + (int64_t)(c->match_re - c->match_rb);
-    auto launch = [&](uint64_t vcap, uint64_t grid) {
-        wg_stage_end(c);
-        wg_stage_begin(c, "vtx_emit");
+    // part 0: every tile; 1 / 2: the tiles before / from the split (see
+    // k_vtx_tile); ntl: the tile bound of the fit check, the same for both parts
+    // mark: the launch is the "vtx_emit" stage (the sliced emission marks its
+    // two parts together: from part 1's start to the side's join)
+    auto launch_on = [&](hipStream_t st, uint64_t vcap, uint64_t grid, uint64_t ntl, int part, uint64_t p1, bool mark) {
+        if (mark) {
+            wg_stage_end(c);
+            wg_stage_begin(c, "vtx_emit");
+        }
         // (grid rounded up to whole XCD rounds: k_vtx_tile's tile order)
-        hipLaunchKernelGGL(k_vtx_tile, dim3((uint32_t)((grid + 7) / 8 * 8)), dim3(VT), 0, s, rb, re, vcap, vis, (const uint64_t *)off,
+        hipLaunchKernelGGL(k_vtx_tile, dim3((uint32_t)((grid + 7) / 8 * 8)), dim3(VT), 0, st, rb, re, vcap, vis, (const uint64_t *)off,
                            c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
                            c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
                            c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
                            c->palette.as<const float4>(), c->tile_first.as<const uint4>(), match, mlo, mhi,
-                           c->vtx.as<float4>(), grid, ml_dev, gate);
-        wg_stage_end(c);
+                           c->vtx.as<float4>(), ntl, ml_dev, gate, part, h, p1);
+        if (mark) wg_stage_end(c);
+    };
+    auto launch = [&](uint64_t vcap, uint64_t grid, uint64_t ntl, int part, uint64_t p1) {
+        launch_on(s, vcap, grid, ntl, part, p1, true);
     };
     // the early grid: the buffers' capacity, bounded by twice the last
     // emission's tiles (a context whose lists shrank would otherwise launch
@@ -484,8 +532,36 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     // launched again whole below
     uint64_t early_grid = std::min((vcap + TILE - 1) / TILE, tcap - 1);
     if (c->vtx_tiles_last) early_grid = std::min(early_grid, 2 * c->vtx_tiles_last + 64);
-    if (early) launch(vcap, early_grid);
-    uint64_t fv[1 + WG_PENDING_ITEMS] = {0};
+    // part 1's grid: the last sliced frame's split tile (a guess the first
+    // time); part 2 covers the rest of the early grid, checked below
+    uint64_t g1 = 0, g2 = 0;
+    if (sliced) {
+        // main: rows [0, h)'s lists, then their tiles (part 1); the side
+        // stream, after those lists: rows [h, n)'s lists beside part 1, the
+        // read (the validation words include both slices' flags), the other
+        // tiles (part 2); main then waits for the side (every later call and
+        // the next build are ordered after part 2)
+        c->glist.deferred = false;
+        c->sliced_emits++;
+        g1 = c->vtx_t1_last ? c->vtx_t1_last : (uint64_t)((double)early_grid * c->slice_frac);
+        g1 = (std::min(g1, early_grid) + 7) / 8 * 8;
+        g2 = early_grid > g1 ? early_grid - g1 + 64 : 64;
+        if (const int rc = wg_geom_lists(c, 0, h, 0, s)) return rc;
+        if (const int rc = wg_side_fork(c)) return rc;
+        int rc = wg_geom_lists(c, h, rows, 1, c->stream);
+        if (rc == WG_OK) rc = wg_fetch_begin_n(c, nfi, fi);
+        if (rc == WG_OK) launch_on(c->stream, vcap, g2, early_grid, 2, g1, false);
+        wg_side_done(c);
+        if (rc) return rc;
+        wg_stage_end(c);
+        wg_stage_begin(c, "vtx_emit");
+        launch_on(s, vcap, g1, early_grid, 1, g1, false);
+        if ((rc = wg_side_join(c)) != WG_OK) return rc;
+        wg_stage_end(c);
+    } else if (early) {
+        launch(vcap, early_grid, early_grid, 0, 0);
+    }
+    uint64_t fv[4 + WG_PENDING_ITEMS] = {0};
     if (const int rc = wg_fetch_end(c, fv)) return rc;
     if (npend) {   // validate the build; one that did not hold is redone here, with this frame and emission
         bool redone = false;
@@ -501,7 +577,13 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
         WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
         prep(ntiles + 1);
-        launch(total, ntiles);
+        launch(total, ntiles, ntiles, 0, 0);
+    } else if (sliced) {
+        const uint64_t t1 = fv[1 + npend] / TILE;
+        c->vtx_t1_last = t1;
+        c->sweep_wide_last = (uint32_t)(fv[2 + npend] + fv[3 + npend]);
+        const uint64_t need2 = ntiles - std::min(t1, g1);
+        if (need2 > (g2 + 7) / 8 * 8) launch(vcap, need2, early_grid, 2, g1);   // part 2 short of tiles: again, whole
     }
     WG_HIP(c, hipGetLastError());
     return WG_OK;
