@@ -61,8 +61,8 @@ def parse():
                     help="gloo rehearsal: move HIP-resident slots through gloo (the stream-ordered slot path of RCCL)")
     ap.add_argument("--no-defer", action="store_true",
                     help="validate every speculative build before build() returns (WG_OPT_DEFER_VALIDATION off)")
-    ap.add_argument("--no-slice", action="store_true",
-                    help="build the geometry lists in the geometry pass, not row-sliced under the emission (WG_OPT_SLICE_LISTS 0)")
+    ap.add_argument("--slice", action="store_true",
+                    help="row-slice the geometry lists under the emission (WG_OPT_SLICE_LISTS 1; default off)")
     ap.add_argument("--no-build-frame", action="store_true",
                     help="separate build() and row_geometry() calls instead of wg_layout_build_frame")
     ap.add_argument("--all-stage-events", action="store_true",
@@ -361,7 +361,7 @@ def config_rates(eng, dev, torch, args):
         eng = wgraph.Engine(dev.index)
         eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         eng.set_defer_validation(not args.no_defer)
-        eng.set_slice_lists(0 if args.no_slice else 1)
+        eng.set_slice_lists(1 if args.slice else 0)
         d = synth.generate(kind, n)
         keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
                                                        d.parent_oid.reshape(-1), d.flags, d.band)]
@@ -431,7 +431,7 @@ def build_lifecycle(dag, dev, torch, args, pal):
     eng = wgraph.Engine(dev.index)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     eng.set_defer_validation(not args.no_defer)
-    eng.set_slice_lists(0 if args.no_slice else 1)
+    eng.set_slice_lists(1 if args.slice else 0)
 
     def step(k, c, n):
         torch.cuda.synchronize()
@@ -469,6 +469,8 @@ def pmc_traffic(args, workload):
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload and "hbm_bytes_per_launch" in d:
+            if "hbm_bytes_per_emission" in d:   # (a two-part emission: both parts)
+                d["hbm_bytes_per_launch"] = d["hbm_bytes_per_emission"]
             d["_file"] = os.path.relpath(f, ROOT)
             best = d
     return best
@@ -536,7 +538,7 @@ def main():
     # a step's build is validated with its emission's vertex-total read (one
     # host wait per step, while the emission runs) instead of mid-step
     eng.set_defer_validation(not args.no_defer)
-    eng.set_slice_lists(0 if args.no_slice else 1)
+    eng.set_slice_lists(1 if args.slice else 0)
     pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
     selected = shard0 + 7
     comm = None

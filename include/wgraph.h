@@ -237,13 +237,15 @@ int         wg_synchronize(wg_ctx *ctx);
  * lanes) that pass; 1 = always the chunked fixed point; 2 = always the
  * single-wave pass.  Speed only, never results. */
 #define WG_OPT_REPLAY_MODE 8
-/* WG_OPT_SLICE_LISTS: 1 (default) = a speculative full geometry pass whose
+/* WG_OPT_SLICE_LISTS: 1 = a speculative full geometry pass whose
  * validation rides on the emission (WG_OPT_DEFER_VALIDATION) leaves its list
  * kernels to the next wg_emit_vertices of the whole list, which builds rows
  * [0, h) first and rows [h, N) beside the emission of the first rows' tiles
  * (h about N / 6), for lists of at least 2^18 rows (2 = of any length past
- * four 64-row chunks); 0 = the lists are built in the geometry pass.  Any
- * other call builds deferred lists whole first.  Speed only, never results. */
+ * four 64-row chunks); 0 (default: measured slower, the second slice's
+ * kernels wait for slots beside the emission) = the lists are built in the
+ * geometry pass.  Any other call builds deferred lists whole first.  Speed
+ * only, never results. */
 #define WG_OPT_SLICE_LISTS 9
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 

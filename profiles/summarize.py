@@ -58,9 +58,11 @@ def main():
             w.writerow([short(r["Name"]), r["Calls"], r["TotalDurationNs"], r["AverageNs"], r["Percentage"],
                         r["MinNs"], r["MaxNs"]])
 
-    # per-step windows: one k_vtx_tile launch closes every step
+    # per-step windows: from one build's first kernel to the next (the
+    # emission may be two k_vtx_tile launches: row-sliced geometry lists)
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in trace)
-    ends = [e for s, e, n in ev if n == KERNEL]
+    first = "k_probe_near" if any(n == "k_probe_near" for _, _, n in ev) else "k_hash_place"
+    ends = [s for s, e, n in ev if n == first]
     windows = []
     for a, b in zip(ends[:-1], ends[1:]):
         iv = sorted((max(s, a), min(e, b)) for s, e, n in ev if e > a and s < b)
@@ -91,7 +93,7 @@ def main():
         span = sum(w[0] for w in timed) / len(timed) / 1e6
         busy = sum(w[1] for w in timed) / len(timed) / 1e6
         nk = sum(w[2] for w in timed) / len(timed)
-        lines += [f"Per step (k_vtx_tile end to k_vtx_tile end, {len(timed)} timed steps): span {span:.3f} ms, "
+        lines += [f"Per step (build start to build start, {len(timed)} timed steps): span {span:.3f} ms, "
                   f"GPU busy {busy:.3f} ms ({100 * busy / span:.1f}%), idle {span - busy:.3f} ms, "
                   f"{nk:.0f} kernel launches.", ""]
     lines += ["| kernel | calls | total ms | avg us | % |", "|---|---:|---:|---:|---:|"]
@@ -123,6 +125,11 @@ def main():
             pmc["workload"] = bench["config"]["workload"]
             pmc["rows_per_gpu"] = bench["config"]["rows_per_gpu"]
             pmc["algorithmic_bytes_per_launch"] = bench["roofline"]["algorithmic_bytes_per_launch"]
+            # one emission = launches_per_emission k_vtx_tile launches (two
+            # when the geometry lists are row-sliced): its HBM bytes
+            lpe = int(bench["roofline"].get("launches_per_emission", 1))
+            pmc["launches_per_emission"] = lpe
+            pmc["hbm_bytes_per_emission"] = (rd + wr) * lpe
         lines += ["", f"PMC ({KERNEL}, per launch): FETCH_SIZE {pmc['fetch_size_kib_per_launch']:.0f} KiB "
                       f"(x2 gfx950 correction -> {rd / 1e9:.3f} GB read), WRITE_SIZE "
                       f"{pmc['write_size_kib_per_launch']:.0f} KiB ({wr / 1e9:.3f} GB written)"

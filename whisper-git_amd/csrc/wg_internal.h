@@ -463,7 +463,7 @@ struct wg_ctx {
         uint32_t vcap = ~0u, scap = ~0u, ccap = ~0u;
         uint32_t *err = nullptr;   // the pass's flag words (geom_err)
     } glist;
-    bool     slice_on = true;      // WG_OPT_SLICE_LISTS
+    bool     slice_on = false;     // WG_OPT_SLICE_LISTS (measured slower on wide16 1M: DESIGN §3.2a)
     double   slice_frac = 0.25;
     uint64_t slice_min_rows = 1ull << 18;   // (WG_OPT_SLICE_LISTS = 2: every list of >= 4 chunks, for the tests)
     uint64_t vtx_t1_last = 0;      // the last sliced emission's first second-slice tile (part 1's grid)

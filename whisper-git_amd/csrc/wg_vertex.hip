@@ -486,10 +486,12 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const int nfi = 1 + npend + (sliced ? 3 : 0);
     if (sliced) {
         // (launched below, with the tiles)
-    } else if (early) {
+    } else if (early && rows >= c->slice_min_rows) {
         // the read on the side stream: the tiles start right after the prep
         // instead of behind the read's system-scope release (~10 us of L2
-        // write-back on the step's critical path)
+        // write-back on the step's critical path).  Not for short lists:
+        // there the host's launches are the step's pace, and the fork and
+        // join cost it four more runtime calls
         if (const int rc = wg_side_fork(c)) return rc;
         const int rc = wg_fetch_begin_n(c, nfi, fi);
         wg_side_done(c);

@@ -201,7 +201,7 @@ class Engine:
         """WG_OPT_SLICE_LISTS: a deferred-validation build leaves its geometry
         lists to the next whole-list emission, which builds them in two row
         slices, the second beside the first slice's tiles (speed only).
-        0 off, 1 lists of >= 2^18 rows (default), 2 any list past 256 rows."""
+        0 off (default), 1 lists of >= 2^18 rows, 2 any list past 256 rows."""
         self._check(lib().wg_set_option(self._ctx, 9, int(mode)))
 
     def set_shard_spec_replay(self, on: bool):
