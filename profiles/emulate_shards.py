@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--no-defer", action="store_true", help="validate each speculative pass before the call returns")
     ap.add_argument("--replay", default=None, help="CHUNK:WARM: fixed replay chunk / warm-up (options 2 and 6)")
     ap.add_argument("--no-spec-replay", action="store_true", help="WG_OPT_SHARD_SPEC_REPLAY 0: X3 checks its replay")
+    ap.add_argument("--replay-mode", type=int, default=None, help="WG_OPT_REPLAY_MODE (0 auto, 1 chunked, 2 serial)")
     ap.add_argument("--two-calls", action="store_true",
                     help="shard_build + shard_geometry (two geometry passes) instead of shard_build_frame (3 exchanges either way)")
     args = ap.parse_args()
@@ -155,6 +156,8 @@ def main():
         e.set_stream(s.cuda_stream)
         e.set_defer_validation(not args.no_defer)   # as bench.py
         e.set_shard_spec_replay(not args.no_spec_replay)
+        if args.replay_mode is not None:
+            e.set_replay_mode(args.replay_mode)
         if args.replay:
             ch, wm = (int(x) for x in args.replay.split(":"))
             e._check(wgraph.lib().wg_set_option(e._ctx, 2, ch))
