@@ -499,7 +499,7 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ err, uint32_t *E, uint32_t *C, uint32_t *P, uint32_t *I, uint32_t *NC, uint32_t *NP,
-        uint32_t *NI) {
+        uint32_t *NI, bool super) {
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
@@ -507,9 +507,9 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
     const uint64_t rr = R0 + lid;
     const uint32_t eoff_v = lid < nr ? edge_off[rr] : 0u;
     const uint32_t rf_v = lid < nr ? rowflags[rr] : 0u;
-    const uint32_t voff_v = lid < nr ? vert_off[rr] : 0u;
-    const uint32_t coff_v = lid < nr ? curve_off[rr] : 0u;
-    const uint32_t koff_v = lid < nr ? kept_off[rr] : 0u;
+    const uint32_t voff_v = (!super && lid < nr) ? vert_off[rr] : 0u;
+    const uint32_t coff_v = (super && lid < nr) ? curve_off[rr] : 0u;
+    const uint32_t koff_v = (!super && lid < nr) ? kept_off[rr] : 0u;
     const uint32_t E1 = edge_off[R1];
     const uint32_t E0 = (uint32_t)__builtin_amdgcn_readlane((int)eoff_v, 0);
     const bool staged = E1 - E0 <= (uint32_t)SW_NE;
@@ -577,10 +577,11 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
             if (act) { eid = E[idx]; c = C[idx]; p = P[idx]; info = I[idx]; }
             __builtin_amdgcn_wave_barrier();
             const bool same = (info & 0x10000000u) != 0;
-            const bool full = act && same && c < r && r < p;
+            const bool full = !super && act && same && c < r && r < p;
             const bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
-            const bool curv = act && !same && c <= r && r <= p;   // the superset (no strip flag)
-            const bool kcur = curv && !skip;                       // this pass's filtered list
+            const bool seg = act && !same && c <= r && r <= p;
+            const bool curv = super && seg;           // the superset (no strip flag)
+            const bool kcur = !super && seg && !skip; // this pass's filtered list
             const bool keep = act && p > r;
             const uint64_t mf = __ballot(full), mc = __ballot(curv), mk = __ballot(keep), mq = __ballot(kcur);
             if (full) vert[fbase + mbcnt(mf)] = pack_vert(info & 0xFFFFFFu, WG_VERT_FULL, (info >> 24) & 0xFu);
@@ -609,8 +610,10 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
-        uint32_t *__restrict__ err, Cap vc, Cap sc, uint32_t *ovf) {
-    if (over(vc, ovf) || over(sc, ovf)) return;   // (uniform over the grid)
+        uint32_t *__restrict__ err, Cap vc, Cap sc, uint32_t *ovf, bool super, const uint32_t *__restrict__ run_if,
+        const uint32_t *__restrict__ done) {
+    if (super && (*run_if == 0 || *done != 0)) return;   // (uniform over the grid)
+    if (over(vc, ovf) || over(sc, ovf)) return;
     __shared__ uint32_t s_eid[SW_CAP_BLOCK];
     __shared__ uint32_t s_c[SW_CAP_BLOCK];
     __shared__ uint32_t s_p[SW_CAP_BLOCK];
@@ -628,7 +631,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         const bool ok = sweep_chunk_lds(SW_CAP, list[i], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
                                         curve_off, vert, curve_ref, curve_row, kept_off, kept_ref, kept_row, err,
                                         s_eid + o, s_c + o, s_p + o,
-                                        s_info + o, n_c[w], n_p[w], n_info[w]);
+                                        s_info + o, n_c[w], n_p[w], n_info[w], super);
         if (!ok && (threadIdx.x & 63) == 0) {
             const uint32_t at = atomicAdd(&n_wide, 1u);
             if (at < 64u) wide[at] = list[i];
@@ -644,7 +647,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
             if (!sweep_chunk_lds(SW_CAP_BLOCK, wide[j], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
                                  curve_off, vert, curve_ref, curve_row, kept_off, kept_ref, kept_row, err, s_eid, s_c,
                                  s_p, s_info, n_c[0], n_p[0],
-                                 n_info[0]) &&
+                                 n_info[0], super) &&
                 (threadIdx.x & 63) == 0)
                 atomicOr(&err[0], 1u);
 }
@@ -692,17 +695,24 @@ __device__ __forceinline__ void carry_rank(const uint32_t *__restrict__ carry, u
     }
 }
 
+// SUPER = false (a full pass): the full verticals and this pass's curve lists
+// filtered by the rows' strip flags; true (a frame pass whose flags differ
+// from the full pass's, run_if != 0, once per layout: done): the flag-free
+// curve superset the frame filter takes (k_curve_keep / k_curve_compact)
+template <bool SUPER>
 __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0, uint64_t q1, const wg_edge *__restrict__ edges,
         const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
         const uint32_t *__restrict__ carry, uint32_t *__restrict__ carry_sorted, const uint8_t *__restrict__ rowflags,
         const uint32_t *__restrict__ vert_off, const uint32_t *__restrict__ curve_off,
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
-        uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, Cap cc, uint32_t *ovf) {
+        uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, Cap cc, uint32_t *ovf,
+        const uint32_t *__restrict__ run_if, const uint32_t *__restrict__ done) {
     __shared__ uint32_t s_car[SW_WAVES][64 * SW_SLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[SW_WAVES][SW_STAGE];
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t q = q0 + (uint64_t)blockIdx.x * SW_WAVES + (threadIdx.x >> 6);   // chunks [q0, q1)
+    if (SUPER && (*run_if == 0 || *done != 0)) return;
     if (over(vc, ovf) || over(sc, ovf) || over(cc, ovf) || q >= q1) return;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
@@ -721,17 +731,17 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // per-row scalars of the chunk, one row per lane
     const uint64_t rr = R0 + lid;
-    const uint32_t voff_v = lid < nr ? vert_off[rr] : 0u;
-    const uint32_t coff_v = lid < nr ? curve_off[rr] : 0u;
-    const uint32_t koff_v = lid < nr ? kept_off[rr] : 0u;
-    const uint32_t rf_v = lid < nr ? rowflags[rr] : 0u;
+    const uint32_t voff_v = (!SUPER && lid < nr) ? vert_off[rr] : 0u;
+    const uint32_t coff_v = (SUPER && lid < nr) ? curve_off[rr] : 0u;
+    const uint32_t koff_v = (!SUPER && lid < nr) ? kept_off[rr] : 0u;
+    const uint32_t rf_v = (!SUPER && lid < nr) ? rowflags[rr] : 0u;
     // per slot: the edge id, the packed full-vertical entry and two row windows
     // as (first row, length - 1) for an unsigned compare: full verticals on
     // rows c < r < p of same-lane edges, curve segments on rows c <= r <= p of
-    // cross-lane edges; an empty window has first row ~0.  The curve lists are
-    // written twice: the superset (no strip flag: refiltered by later frame
-    // passes) and this pass's list filtered by the row's strip flags (the same
-    // entries when the row has none).
+    // cross-lane edges; an empty window has first row ~0.  A full pass writes
+    // the curve list filtered by the row's strip flags (every segment of a row
+    // without flags); the flag-free superset is swept only for a frame pass
+    // whose flags differ (SUPER).
     uint32_t ek[SW_SLOTS], fb[SW_SLOTS], fl[SW_SLOTS], cb[SW_SLOTS], cl[SW_SLOTS], pv[SW_SLOTS];
     const uint32_t nslots = (total + 63) / 64;
 #pragma unroll
@@ -763,16 +773,21 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
 #pragma unroll
         for (int sl = 0; sl < SW_SLOTS; sl++) {
             if ((uint32_t)sl >= nslots) break;
-            const bool full = r - fb[sl] <= fl[sl];
-            const bool curv = r - cb[sl] <= cl[sl];
-            const uint64_t mf = __ballot(full), mc = __ballot(curv);
-            if (mf) {
-                if (full) vert[fbase + mbcnt(mf)] = pv[sl];
-                fbase += __builtin_popcountll(mf);
+            if (!SUPER) {
+                const bool full = r - fb[sl] <= fl[sl];
+                const uint64_t mf = __ballot(full);
+                if (mf) {
+                    if (full) vert[fbase + mbcnt(mf)] = pv[sl];
+                    fbase += __builtin_popcountll(mf);
+                }
             }
-            if (mc) {
+            const bool curv = r - cb[sl] <= cl[sl];
+            const uint64_t mc = __ballot(curv);
+            if (SUPER && mc) {
                 if (curv) { const uint32_t o = cbase + mbcnt(mc); curve_ref[o] = ek[sl]; curve_row[o] = r; }
                 cbase += __builtin_popcountll(mc);
+            }
+            if (!SUPER && mc) {
                 uint64_t mk = mc;
                 if (rf) {   // (uniform) curve_kept: r == c -> RF_CHILD, r == p -> RF_PARENT, else RF_ZERO
                     const uint32_t d = r - cb[sl];
@@ -961,8 +976,11 @@ __global__ void __launch_bounds__(WG_BS_THREADS) k_curve_keep(uint64_t n, const 
                                                              const uint8_t *__restrict__ rowflags, uint32_t *__restrict__ cnt,
                                                              const uint32_t *__restrict__ cond,
                                                              const uint32_t *__restrict__ cur_off, Cap sc, uint32_t *ovf,
-                                                             uint8_t *__restrict__ flags_kept, uint32_t *__restrict__ bsum) {
+                                                             uint8_t *__restrict__ flags_kept, uint32_t *__restrict__ bsum,
+                                                             uint32_t *__restrict__ super_done) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // (the superset this refilter reads stands for the layout's later frames)
+    if (super_done && cond && *cond && r == 0) *super_done = 1u;
     uint32_t k = 0;
     if (!over(sc, ovf) && r < n) {
         const uint32_t f = rowflags[r];
@@ -1016,7 +1034,8 @@ static int filter_curves(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *c
     static_assert(T == WG_BS_THREADS, "k_curve_keep is a wg_scan_bs_u32 producer");
     hipLaunchKernelGGL(k_curve_keep, dim3(blocks(n)), dim3(T), 0, s, n, c->scurve_off.as<const uint32_t>(),
                        c->scurve_ref.as<const uint32_t>(), c->edges.as<const wg_edge>(), c->rowflags.as<const uint8_t>(),
-                       cnt, cond, (const uint32_t *)coff, sc, ovf, c->rowflags_lists.as<uint8_t>(), c->bsum.as<uint32_t>());
+                       cnt, cond, (const uint32_t *)coff, sc, ovf, c->rowflags_lists.as<uint8_t>(), c->bsum.as<uint32_t>(),
+                       c->geom_err ? c->geom_err + 5 : nullptr);
     {
         WgScanBs S;
         S.na = 1;
@@ -1114,11 +1133,12 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
     const uint64_t q0 = r0 / WG_SWEEP_CH, q1 = (r1 + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
     uint32_t *big = c->sweep_big.as<uint32_t>() + q0, *big_n = err + (slice ? 4 : 1);
     uint32_t *carry_sorted = c->carry_sorted.as<uint32_t>();
-    hipLaunchKernelGGL(k_sweep, dim3((uint32_t)((q1 - q0 + SW_WAVES - 1) / SW_WAVES)), dim3(64 * SW_WAVES), 0, s, n, q0, q1, E,
-                       edge_off, carry_off, (const uint32_t *)c->carry.as<uint32_t>(), carry_sorted,
+    hipLaunchKernelGGL(k_sweep<false>, dim3((uint32_t)((q1 - q0 + SW_WAVES - 1) / SW_WAVES)), dim3(64 * SW_WAVES), 0, s, n,
+                       q0, q1, E, edge_off, carry_off, (const uint32_t *)c->carry.as<uint32_t>(), carry_sorted,
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), big,
-                       big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, vc, sc, cc, ovf);
+                       big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, vc, sc, cc, ovf,
+                       (const uint32_t *)nullptr, (const uint32_t *)nullptr);
     // (one wave per wide chunk, ~73 KB of LDS per block: two blocks per CU,
     // the whole chip for lists whose every chunk is wide; sized by the last
     // pass's count of wide chunks; 64 blocks for a list that had none, as
@@ -1131,7 +1151,7 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
                        (const uint32_t *)big_n, E, edge_off, carry_off, (const uint32_t *)carry_sorted,
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), err,
-                       vc, sc, ovf);
+                       vc, sc, ovf, false, (const uint32_t *)nullptr, (const uint32_t *)nullptr);
     // the records of the slice's rows: a grid for its share of the records
     // (+ a quarter), the kernels stride over the rest
     uint64_t grid_recs = L.n_super_grid;
@@ -1139,6 +1159,35 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
     launch_curves(c, r0, r1, grid_recs, s, 0u, sc, ovf, nullptr);
     WG_HIP(c, hipGetLastError());
     return WG_OK;
+}
+
+// The flag-free curve superset of the last full pass's layout, for a frame
+// pass whose row flags differ from the full pass's (run_if: its flag-change
+// word, on the device): swept once per layout (done: the full pass's error
+// word 5, raised by the first refilter); a frame pass whose flags equal the
+// full pass's keeps the full pass's lists and skips both kernels.
+static void launch_superset(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t *run_if, Cap g, uint32_t *ovf) {
+    if (!n || !c->geom_err) return;
+    const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
+    uint32_t *err = c->geom_err;
+    const wg_edge *E = c->edges.as<const wg_edge>();
+    const uint32_t *edge_off = c->edge_cnt.as<const uint32_t>(), *carry_off = c->carry_off.as<const uint32_t>();
+    const uint32_t *soff = c->scurve_off.as<const uint32_t>();
+    uint32_t *big = c->sweep_big.as<uint32_t>(), *big_n = err + 6;
+    hipLaunchKernelGGL(k_sweep<true>, dim3((uint32_t)((nch + SW_WAVES - 1) / SW_WAVES)), dim3(64 * SW_WAVES), 0, s, n,
+                       (uint64_t)0, nch, E, edge_off, carry_off, (const uint32_t *)c->carry.as<uint32_t>(),
+                       c->carry_sorted.as<uint32_t>(), (const uint8_t *)nullptr, (const uint32_t *)nullptr, soff,
+                       (uint32_t *)nullptr, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
+                       (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, big, big_n,
+                       c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, g, g, g, ovf, run_if,
+                       (const uint32_t *)(err + 5));
+    const uint64_t lds_grid = std::min<uint64_t>(std::min<uint64_t>(SW_LDS_BLOCKS, 64 + (uint64_t)c->sweep_wide_last / SW_WAVES),
+                                                 (nch + SW_WAVES - 1) / SW_WAVES);
+    hipLaunchKernelGGL(k_sweep_lds, dim3((uint32_t)lds_grid), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)big,
+                       (const uint32_t *)big_n, E, edge_off, carry_off, (const uint32_t *)c->carry_sorted.as<uint32_t>(),
+                       c->rowflags.as<const uint8_t>(), (const uint32_t *)nullptr, soff, (uint32_t *)nullptr,
+                       c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(), (const uint32_t *)nullptr,
+                       (uint32_t *)nullptr, (uint32_t *)nullptr, err, g, g, ovf, true, run_if, (const uint32_t *)(err + 5));
 }
 
 int wg_geom_lists_flush(wg_ctx *c) {
@@ -1186,6 +1235,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
                            c->band_keep, c->rowflags_lists.as<const uint8_t>(), diff);
         // (a build awaiting its validation whose lists did not fit: no reads of them)
         const Cap bg = Cap{nullptr, ~0u, c->pend.build ? c->geom_err : nullptr};
+        launch_superset(c, n, s, diff, bg, diff + 8);
         int rc = filter_curves(c, n, s, diff, bg, diff + 8);
         if (rc != WG_OK) return rc;
         wg_stage_end(c);
