@@ -17,7 +17,3 @@ cd /tmp && export TMPDIR=/tmp
 BENCH="$ROOT/bench.py --steps 5 --warmup 2 --no-cpu --no-extras"
 timeout -s KILL 120 rocprofv3 --kernel-include-regex k_vtx_tile --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH > "$OUT/fetch.json" 2> "$OUT/fetch.err"
 timeout -s KILL 120 rocprofv3 --kernel-include-regex k_vtx_tile --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $BENCH > "$OUT/write.json" 2> "$OUT/write.err"
-# the sharded skew step's X3 segment (global replay) with the serial replay forced
-cd "$ROOT"
-timeout -k 10 300 python -u profiles/emulate_shards.py --world 8 --steps 3 --kind skew --replay-mode 2 \
-    --out "$ROOT/gpurun_out/${TAG}_shard_emulation_skew_serial.json" > "$ROOT/gpurun_out/${TAG}_emu_skew_serial.log" 2>&1
