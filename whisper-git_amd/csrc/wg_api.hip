@@ -111,14 +111,9 @@ int wg_copy_batch(wg_ctx *c, const WgCopies &cp, hipStream_t s) {
 
 int wg_side_fork(wg_ctx *c) {
     if (!c->side) {
-        // the side stream at the device's highest priority: its kernels are
-        // short latency-bound ones (the hash table, row_top, the second list
-        // slice) running beside a long main-stream kernel (the probe, the
-        // emission's first part) whose workgroups would otherwise take every
-        // slot as it frees
-        int lo_prio = 0, hi_prio = 0;
-        if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) hi_prio = 0;
-        WG_HIP(c, hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi_prio));
+        // (normal priority: at the highest, the hash table's kernels starved
+        // the near probe beside them, 58 -> 81 us, r04f/r04g traces)
+        WG_HIP(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         // stream-to-stream order on one device: a device-scope release suffices
         WG_HIP(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | wg_event_scope()));
         WG_HIP(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | wg_event_scope()));

@@ -411,21 +411,45 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
 // top-half slots (sorted and packed by k_top_finish), and every edge into
 // the carry-in list of each 64-row chunk it is alive across (sorted by
 // k_carry_sort)
-__global__ void k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
+// The (edge, chunk) registrations of a wave's 64 edges are dealt to its
+// lanes in turn: an edge alive across thousands of chunks (a long-lived
+// branch of a wide list) no longer loops alone while its wave waits
+// (linuxwide: 344 us with one lane per edge)
+__global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges,
+                            const uint32_t *__restrict__ vert_off,
                             const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert,
                             const uint32_t *__restrict__ carry_off, uint32_t *carry_fill, uint32_t *carry,
                             const uint32_t *__restrict__ ne_dev, Cap vc, Cap cc, uint32_t *ovf) {
-    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (over(vc, ovf) || over(cc, ovf)) return;
-    if (k >= ne || (ne_dev && k >= *ne_dev)) return;
-    const wg_edge e = edges[k];
-    if (e.child_row >= e.parent_row) return;
+    __shared__ uint32_t s_pre[256 / 64][64], s_k0[256 / 64][64];
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lid = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (over(vc, ovf) || over(cc, ovf)) return;   // (uniform)
+    const bool valid = k < ne && !(ne_dev && k >= *ne_dev);
+    wg_edge e{};
+    if (valid) e = edges[k];
+    const bool live = valid && e.child_row < e.parent_row;
     const uint32_t k0 = e.child_row / WG_SWEEP_CH + 1, k1 = e.parent_row / WG_SWEEP_CH;
-    for (uint32_t q = k0; q <= k1; q++) {
+    const uint32_t span = (live && k1 >= k0) ? k1 - k0 + 1 : 0u;
+    const uint32_t inc = wg_wave_scan(span, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    s_pre[wv][lid] = inc - span;
+    s_k0[wv][lid] = k0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t kbase = k - lid;
+    for (uint32_t t = lid; t < tot; t += 64) {
+        // the edge: the last lane whose exclusive start is <= t (lanes with
+        // no registration share the next lane's start and come before it)
+        uint32_t l = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1)
+            if (s_pre[wv][l + step] <= t) l += step;
+        const uint32_t q = s_k0[wv][l] + (t - s_pre[wv][l]);
         const uint32_t pos = atomicAdd(&carry_fill[q], 1u);
-        carry[carry_off[q] + pos] = (uint32_t)k;
+        carry[carry_off[q] + pos] = (uint32_t)(kbase + l);
     }
-    if (e.child_lane != e.parent_lane) return;
+    if (!live || e.child_lane != e.parent_lane) return;
     const uint32_t p = e.parent_row;
     const uint32_t pos = atomicAdd(&top_fill[p], 1u);
     vert[vert_off[p] + scanF[p + 1] + pos] = (uint32_t)k;   // edge id, packed below

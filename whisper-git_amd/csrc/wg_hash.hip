@@ -265,9 +265,13 @@ int wg_hash_table_launch(wg_ctx *c) {
     uint32_t *dup = reinterpret_cast<uint32_t *>(table + cap);
     if (n) {
         const uint32_t g = (uint32_t)((n + T - 1) / T);
+        // the next build's table is emptied here, unless a long list's
+        // emission will (wg_hash_clear_next, beside its tiles: 8 bytes per
+        // slot off the build's critical path)
+        const bool later = c->defer_validation && !c->sh.on && n >= c->slice_min_rows;
         hipLaunchKernelGGL(k_hash_place, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1,
-                           c->htab[o].as<unsigned long long>(), words, LfClear{});
-        c->htab_clean[o] = words;
+                           c->htab[o].as<unsigned long long>(), later ? 0ull : words, LfClear{});
+        if (!later) c->htab_clean[o] = words;
         hipLaunchKernelGGL(k_hash_settle, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1, dup);
     }
     c->htab_clean[t] = 0;
@@ -276,6 +280,17 @@ int wg_hash_table_launch(wg_ctx *c) {
     c->hash_table = table;
     c->hash_built = true;
     WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+// the next build's table (and its duplicate word) emptied on stream s, if
+// the last build left it to the emission
+int wg_hash_clear_next(wg_ctx *c, hipStream_t s) {
+    const int o = c->htab_cur;
+    const uint64_t words = c->hcap + 1;
+    if (!c->hcap || c->htab_clean[o] >= words || c->htab[o].cap < words * 8) return WG_OK;
+    WG_HIP(c, hipMemsetAsync(c->htab[o].p, 0xFF, words * 8, s));
+    c->htab_clean[o] = words;
     return WG_OK;
 }
 

@@ -654,7 +654,8 @@ inline uint64_t wg_bs_blocks(uint64_t n) { return (n + WG_BS_THREADS - 1) / WG_B
 
 // stages -------------------------------------------------------------------------
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
-int wg_hash_table_launch(wg_ctx *c);          // wg_hash.hip: place + settle on c->stream
+int wg_hash_table_launch(wg_ctx *c);
+int wg_hash_clear_next(wg_ctx *c, hipStream_t s);   // the next build's table, emptied beside an emission          // wg_hash.hip: place + settle on c->stream
 // the build's side stream: the hash table (joined by the hash join's fix-up
 // kernel), then the heights and the row_top (joined by the geometry)
 int wg_side_build_begin(wg_ctx *c, uint64_t m, float *h, float *rt, const float *band, const float *band_host,

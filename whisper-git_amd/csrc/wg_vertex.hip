@@ -493,7 +493,8 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         // there the host's launches are the step's pace, and the fork and
         // join cost it four more runtime calls
         if (const int rc = wg_side_fork(c)) return rc;
-        const int rc = wg_fetch_begin_n(c, nfi, fi);
+        int rc = wg_fetch_begin_n(c, nfi, fi);
+        if (rc == WG_OK && !c->sh.on) rc = wg_hash_clear_next(c, c->stream);
         wg_side_done(c);
         if (rc) return rc;
     } else if (const int rc = wg_fetch_begin_n(c, nfi, fi)) {
