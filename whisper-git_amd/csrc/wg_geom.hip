@@ -408,7 +408,7 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
 }
 
 // one pass over the edges: same-lane edges' ids into their parent row's
-// top-half slots (sorted and packed by k_top_finish), and every edge into
+// top-half slots (sorted and packed by the sweep wave, top_finish_row), and every edge into
 // the carry-in list of each 64-row chunk it is alive across (sorted by
 // k_carry_sort)
 // The (edge, chunk) registrations of a wave's 64 edges are dealt to its
@@ -458,12 +458,12 @@ __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *_
 // per row: the top-half entries (edge ids placed by k_top_carry) sorted by
 // edge id and packed, then the bottom halves (same-lane edges of child r, in
 // parent order) after them
-__global__ void k_top_finish(uint64_t r0, uint64_t r1, const uint32_t *__restrict__ edge_off,
-                             const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
-                             const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT, uint32_t *vert, Cap vc,
-                             uint32_t *ovf) {
-    uint64_t r = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // rows [r0, r1)
-    if (over(vc, ovf) || r >= r1) return;
+// (done by the full pass's sweep wave for its 64 rows, one row per lane,
+// before its row loop: one launch fewer)
+__device__ __forceinline__ void top_finish_row(uint64_t r, const uint32_t *__restrict__ edge_off,
+                                               const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
+                                               const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT,
+                                               uint32_t *vert) {
     const uint32_t nt = cntT[r];
     uint32_t *v = vert + vert_off[r] + scanF[r + 1];
     for (uint32_t i = 1; i < nt; i++) {   // insertion sort by edge id (in-degree is small)
@@ -731,7 +731,8 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, Cap cc, uint32_t *ovf,
-        const uint32_t *__restrict__ run_if, const uint32_t *__restrict__ done) {
+        const uint32_t *__restrict__ run_if, const uint32_t *__restrict__ done, const uint32_t *__restrict__ scanF,
+        const uint32_t *__restrict__ cntT) {
     __shared__ uint32_t s_car[SW_WAVES][64 * SW_SLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[SW_WAVES][SW_STAGE];
     const uint32_t lid = threadIdx.x & 63;
@@ -740,6 +741,8 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
     if (over(vc, ovf) || over(sc, ovf) || over(cc, ovf) || q >= q1) return;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
+    // the chunk's top and bottom halves (their entries follow the full ones)
+    if (!SUPER && lid < nr) top_finish_row(R0 + lid, edge_off, edges, vert_off, scanF, cntT, vert);
     const uint32_t a = carry_off[q], ncar = carry_off[q + 1] - a;
     const uint32_t E0 = edge_off[R0], E1 = edge_off[R1];
     const uint32_t total = ncar + (E1 - E0);
@@ -1150,8 +1153,6 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
     const Cap vc{L.vtot, L.vcap, nullptr}, sc{L.stot, L.scap, nullptr}, cc{L.ctot, L.ccap, nullptr};
     uint32_t *err = L.err, *ovf = err + 8;
     uint32_t *vert = c->vert.as<uint32_t>();
-    hipLaunchKernelGGL(k_top_finish, dim3(blocks(r1 - r0)), dim3(T), 0, s, r0, r1, edge_off, E, voff, L.cntF, L.cntT, vert,
-                       vc, ovf);
     // chunks too wide for the register sweep: listed per slice (counts in
     // err[1] / err[4]) and swept through LDS
     const uint64_t q0 = r0 / WG_SWEEP_CH, q1 = (r1 + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
@@ -1162,7 +1163,7 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), big,
                        big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, vc, sc, cc, ovf,
-                       (const uint32_t *)nullptr, (const uint32_t *)nullptr);
+                       (const uint32_t *)nullptr, (const uint32_t *)nullptr, L.cntF, L.cntT);
     // (one wave per wide chunk, ~73 KB of LDS per block: two blocks per CU,
     // the whole chip for lists whose every chunk is wide; sized by the last
     // pass's count of wide chunks; 64 blocks for a list that had none, as
@@ -1204,7 +1205,7 @@ static void launch_superset(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t
                        (uint32_t *)nullptr, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
                        (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, big, big_n,
                        c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, g, g, g, ovf, run_if,
-                       (const uint32_t *)(err + 5));
+                       (const uint32_t *)(err + 5), (const uint32_t *)nullptr, (const uint32_t *)nullptr);
     const uint64_t lds_grid = std::min<uint64_t>(std::min<uint64_t>(SW_LDS_BLOCKS, 64 + (uint64_t)c->sweep_wide_last / SW_WAVES),
                                                  (nch + SW_WAVES - 1) / SW_WAVES);
     hipLaunchKernelGGL(k_sweep_lds, dim3((uint32_t)lds_grid), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)big,
