@@ -139,6 +139,12 @@ void wg_side_done(wg_ctx *c) {
 int wg_side_join(wg_ctx *c) {
     if (!c->side_pending) return WG_OK;
     c->side_pending = false;
+    // already reached (the host ran behind the device, e.g. the next build
+    // after an emission whose side read it waited for): no wait packet on
+    // the main queue — a cross-queue wait costs ~10 us even when satisfied
+    const hipError_t q = hipEventQuery(c->ev_join);
+    if (q == hipSuccess) return WG_OK;
+    if (q == hipErrorNotReady) (void)hipGetLastError();   // (a status, not a failure: not left as the last error)
     WG_HIP(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     return WG_OK;
 }

@@ -484,19 +484,19 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         fi[3 + npend] = WgFetch{c->glist.err + 4, false};
     }
     const int nfi = 1 + npend + (sliced ? 3 : 0);
+    bool side_read = false;
     if (sliced) {
         // (launched below, with the tiles)
-    } else if (early && rows >= c->slice_min_rows) {
+    } else if (early && rows >= c->slice_min_rows && c->side && c->ev_fork) {
         // the read on the side stream: the tiles start right after the prep
         // instead of behind the read's system-scope release (~10 us of L2
-        // write-back on the step's critical path).  Not for short lists:
-        // there the host's launches are the step's pace, and the fork and
-        // join cost it four more runtime calls
-        if (const int rc = wg_side_fork(c)) return rc;
-        int rc = wg_fetch_begin_n(c, nfi, fi);
-        if (rc == WG_OK && !c->sh.on) rc = wg_hash_clear_next(c, c->stream);
-        wg_side_done(c);
-        if (rc) return rc;
+        // write-back on the step's critical path); one event record between
+        // the prep and the tiles, the side's calls after the tiles' launch
+        // (below).  Not for short lists: there the host's launches are the
+        // step's pace, and the side costs it four more runtime calls
+        if (const int rc = wg_side_join(c)) return rc;
+        WG_HIP(c, hipEventRecord(c->ev_fork, s));
+        side_read = true;
     } else if (const int rc = wg_fetch_begin_n(c, nfi, fi)) {
         return rc;
     }
@@ -563,6 +563,15 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         wg_stage_end(c);
     } else if (early) {
         launch(vcap, early_grid, early_grid, 0, 0);
+    }
+    if (side_read) {   // the side stream after the prep: the read, the next build's empty table
+        WG_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        c->side_main = c->stream;
+        c->stream = c->side;
+        int rc = wg_fetch_begin_n(c, nfi, fi);
+        if (rc == WG_OK && !c->sh.on) rc = wg_hash_clear_next(c, c->stream);
+        wg_side_done(c);
+        if (rc) return rc;
     }
     uint64_t fv[4 + WG_PENDING_ITEMS] = {0};
     if (const int rc = wg_fetch_end(c, fv)) return rc;
