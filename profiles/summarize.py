@@ -81,8 +81,11 @@ def main():
     # whole steps only (bench.py ends with emission-only calls: windows of a few
     # launches), and the timed ones: the last five whole steps are the
     # stage-breakdown pass, whose per-stage events add gaps
-    full = [w for w in windows if w[2] >= 20]
-    timed = full[-10:-5] if len(full) >= 10 else (full[-5:] if len(full) >= 5 else full)
+    # (windows run from one build's first kernel to the next build's: the
+    # timed steps are the five shortest whole ones — the stage-breakdown pass
+    # adds event gaps, the last window holds the emission-only calls)
+    full = [w for w in windows[:-1] if w[2] >= 20]
+    timed = sorted(full)[:5]
 
     vtx = next((r for r in stats if short(r["Name"]) == KERNEL), None)
     lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py --steps 5 --warmup 2 --no-cpu --no-extras`", ""]
