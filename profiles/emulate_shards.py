@@ -223,6 +223,7 @@ def main():
         raise SystemExit(f"emulated rank failed: {errors}")
 
     counters = [int(e.debug_counters()[5]) for e in engines]
+    dcs = [e.debug_counters() for e in engines]   # [1] lane slots of the global replay, [10] serial replay
 
     # rank 0's emission again on its sharded geometry, alone on the GPU (no other
     # rank's segments interleaved): separates the shard data from the emulation
@@ -298,7 +299,8 @@ def main():
                          "segment_ms": [round(1e3 * float(np.median([seg[r][k + j * (len(seg[r]) // args.steps)][1]
                                                                    for j in range(args.steps)])), 4)
                                         for k in range(len(seg[r]) // args.steps)],
-                         "mode": counters[r],
+                         "mode": counters[r], "lane_slots": int(dcs[r][1]), "serial_replay": int(dcs[r][10]),
+                         "replay_iterations": int(dcs[r][3]), "events": int(dcs[r][4]),
                          "stages_ms": {k: round(v, 4) for k, v in sorted(stage_ms[r].items())}})
     n_x = len(xlog) // args.steps
     xbytes = {}
