@@ -692,6 +692,10 @@ int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *e
 static int replay_setup(wg_ctx *c, ReplayRun &run, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t nw) {
     run.nev = nev;
     run.nw = nw;
+    // (the serial pass's cost is its words: 8 instead of 16 when the last
+    // list of this context held at most 448 slots; a list past 511 overflows
+    // and the caller widens, as at any width)
+    run.ser_w8 = nw == 16 && c->n_slots > 0 && c->n_slots <= 448;
     c->replay_geometry(&run.chunk, &run.warm);
     const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point

@@ -207,6 +207,19 @@ __device__ __forceinline__ uint32_t ser_first_w<4>(const uint64_t (&m)[4]) {
     return x;
 }
 template <>
+__device__ __forceinline__ uint32_t ser_first_w<8>(const uint64_t (&m)[8]) {
+    uint32_t x = 0xFFFFFFFFu;
+#pragma unroll
+    for (int w = 7; w >= 0; w--) {
+        uint32_t f;
+        asm volatile("s_ff1_i32_b64 %[f], %[m]\n\t"
+                     "s_or_b32 %[f], %[f], %[tag]\n\t"
+                     "s_min_u32 %[x], %[x], %[f]"
+                     : [x] "+s"(x), [f] "=&s"(f) : [m] "s"(m[w]), [tag] "n"(64 * w) : "scc");
+    }
+    return x;
+}
+template <>
 __device__ __forceinline__ uint32_t ser_first_w<16>(const uint64_t (&m)[16]) {
     uint32_t x = 0xFFFFFFFFu;
 #pragma unroll
@@ -401,6 +414,9 @@ hipError_t wg_replay_serial(hipStream_t s, ReplayRun &R, uint4 *rec) {
                            R.scal);
     else if (R.nw <= 4)
         hipLaunchKernelGGL(k_ser_replay_w<4>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
+                           R.flags, R.scal);
+    else if (R.nw <= 16 && R.ser_w8)
+        hipLaunchKernelGGL(k_ser_replay_w<8>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
                            R.flags, R.scal);
     else if (R.nw <= 16)
         hipLaunchKernelGGL(k_ser_replay_w<16>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
