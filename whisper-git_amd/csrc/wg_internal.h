@@ -197,6 +197,7 @@ struct ReplayRun {
     uint16_t *slots_a = nullptr, *slots_b = nullptr, *sp_prev = nullptr, *sp_next = nullptr;   // sp_prev: last written
     uint32_t nw = 1;                     // occupancy words (1, 4 or 16: up to 63, 255, 1023 slots)
     bool ser_w8 = false;                 // nw 16 on the serial pass with 8 words (511 slots; the last list used <= 448)
+    bool ser_w3 = false;                 // nw 4 on the serial pass with 3 words (191 slots; the last list used <= 170)
     uint32_t warm = 0;                   // iteration 1 starts this many events before each chunk
     unsigned long long *occ_a = nullptr, *occ_b = nullptr, *op = nullptr, *on = nullptr;
     uint32_t *stats = nullptr, *flags = nullptr, *scal = nullptr;

@@ -696,6 +696,7 @@ static int replay_setup(wg_ctx *c, ReplayRun &run, uint64_t nev, const uint4 *ev
     // list of this context held at most 448 slots; a list past 511 overflows
     // and the caller widens, as at any width)
     run.ser_w8 = nw == 16 && c->n_slots > 0 && c->n_slots <= 448;
+    run.ser_w3 = nw == 4 && c->n_slots > 0 && c->n_slots <= 170;
     c->replay_geometry(&run.chunk, &run.warm);
     const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point

@@ -207,6 +207,22 @@ __device__ __forceinline__ uint32_t ser_first_w<4>(const uint64_t (&m)[4]) {
     return x;
 }
 template <>
+__device__ __forceinline__ uint32_t ser_first_w<3>(const uint64_t (&m)[3]) {
+    uint32_t x, f1, f2;   // (as the four-word form)
+    asm volatile(
+        "s_ff1_i32_b64 %[x], %[m0]\n\t"
+        "s_ff1_i32_b64 %[f1], %[m1]\n\t"
+        "s_ff1_i32_b64 %[f2], %[m2]\n\t"
+        "s_or_b32 %[f1], %[f1], 64\n\t"
+        "s_or_b32 %[f2], %[f2], 0x80\n\t"
+        "s_min_u32 %[x], %[x], %[f1]\n\t"
+        "s_min_u32 %[x], %[x], %[f2]"
+        : [x] "=&s"(x), [f1] "=&s"(f1), [f2] "=&s"(f2)
+        : [m0] "s"(m[0]), [m1] "s"(m[1]), [m2] "s"(m[2])
+        : "scc");
+    return x;
+}
+template <>
 __device__ __forceinline__ uint32_t ser_first_w<8>(const uint64_t (&m)[8]) {
     uint32_t x = 0xFFFFFFFFu;
 #pragma unroll
@@ -412,6 +428,9 @@ hipError_t wg_replay_serial(hipStream_t s, ReplayRun &R, uint4 *rec) {
     if (R.nw <= 1)
         hipLaunchKernelGGL(k_ser_replay1, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats, R.flags,
                            R.scal);
+    else if (R.nw <= 4 && R.ser_w3)
+        hipLaunchKernelGGL(k_ser_replay_w<3>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
+                           R.flags, R.scal);
     else if (R.nw <= 4)
         hipLaunchKernelGGL(k_ser_replay_w<4>, dim3(1), dim3(64), 0, s, r, R.ev, R.nev, R.nev_dev, R.gate, R.slots_a, R.stats,
                            R.flags, R.scal);
