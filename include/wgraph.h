@@ -232,10 +232,13 @@ int         wg_synchronize(wg_ctx *ctx);
  * the geometry pass. */
 #define WG_OPT_SHARD_SPEC_REPLAY 7
 /* WG_OPT_REPLAY_MODE: how the lane events are replayed.  0 (default) = auto:
- * the chunked fixed point, and for lists on which it needs more iterations
- * than an exact single-wave pass costs (parents at earlier rows, long-lived
- * lanes) that pass; 1 = always the chunked fixed point; 2 = always the
- * single-wave pass.  Speed only, never results. */
+ * the chunked fixed point; for lists on which it needs many iterations
+ * (parents at earlier rows, the Linux shape) the compacted fixed point (the
+ * slots leaked by parents at earlier rows struck out, D-state chunks with a
+ * long warm-up); for lists on which that still needs more iterations than an
+ * exact single-wave pass costs (long-lived lanes) that pass; 1 = always the
+ * chunked fixed point; 2 = always the single-wave pass; 3 = always the
+ * compacted fixed point.  Speed only, never results. */
 #define WG_OPT_REPLAY_MODE 8
 /* WG_OPT_SLICE_LISTS: 1 = a speculative full geometry pass whose
  * validation rides on the emission (WG_OPT_DEFER_VALIDATION) leaves its list
@@ -247,6 +250,10 @@ int         wg_synchronize(wg_ctx *ctx);
  * geometry pass.  Any other call builds deferred lists whole first.  Speed
  * only, never results. */
 #define WG_OPT_SLICE_LISTS 9
+/* WG_OPT_DC_WARMUP: the compacted replay's first-iteration warm-up in events
+ * (a multiple of 64 in 64..1048576; 0 = auto, the default: 8192, doubled up
+ * to 32768 while the fixed point comes late).  Speed only, never results. */
+#define WG_OPT_DC_WARMUP 10
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------
@@ -543,7 +550,12 @@ int wg_stage_timings(wg_ctx *ctx, int *n_stages, const char **names, float *ms);
  * sharded builds whose global lane replay ran blind (WG_OPT_SHARD_SPEC_REPLAY),
  * [10] 1 if the last lane replay was the single-wave serial pass
  * (WG_OPT_REPLAY_MODE), [11] emissions that built row-sliced geometry lists
- * (WG_OPT_SLICE_LISTS). */
+ * (WG_OPT_SLICE_LISTS), [12] the last lane replay's form: 100 + words for the
+ * chunked fixed point (101, 104, 116), 200 + words for the serial pass (201,
+ * 203, 204, 208, 216; 264 the 16-wave workgroup), 300 + words for the
+ * compacted fixed point (301, 302, 304), 0 none (the general walk), [13]
+ * the slots the last compacted replay struck out as leaked, [14] its
+ * first-iteration warm-up (events). */
 int wg_debug_counters(wg_ctx *ctx, uint32_t *out, int n);
 
 #ifdef __cplusplus

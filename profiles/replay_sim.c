@@ -361,6 +361,102 @@ static void run_longseed(uint32_t CH, uint32_t warm) {
     free(death); free(lt); free(ls); free(own); free(stok); free(sslot);
 }
 
+/* compact: the D-state replay (wg_lanes_serial.hip: a slot holds D = the time
+ * its holder is consumed) with leaked slots removed from the slot order — a
+ * slot whose token is never consumed stays occupied for good, so the lowest
+ * free slot is the lowest free one among the others; positions are ranks among
+ * the non-leaked slots, and a leak removes its position (the ones above shift
+ * down).  Chunked fixed point on the exit D-vectors (iteration 1 warm-started
+ * from empty), then the real slots: S_j = the non-leaked slot indices in order
+ * after j leaks, slot(k) = S_{leaks before k}[pos(k)]. */
+#define CINF 0x7FFFFFFFu
+static uint32_t CWID;   /* compact positions tracked */
+static uint32_t cmaxpos;
+static uint32_t creplay(uint64_t ew, uint64_t e1, const uint32_t *Din, uint32_t *Dout, uint32_t *pos, const uint64_t *death) {
+    static uint32_t *D = NULL;
+    if (!D) D = malloc(CWID * 4);
+    memcpy(D, Din, CWID * 4);
+    uint32_t hi = 0;   /* positions [0, hi) may be nonzero */
+    for (uint32_t p = 0; p < CWID; p++) if (D[p]) hi = p + 1;
+    for (uint64_t k = ew; k < e1; k++) {
+        const uint32_t t = (uint32_t)k + 1;
+        uint32_t x = 0xFFFFFFFFu;
+        if (EV[k].a) { for (x = 0; x < CWID && D[x] >= t; x++) {} if (x == CWID) x = 0xFFFFFFFFu; }
+        else for (uint32_t p = 0; p < hi; p++) if (D[p] == t) { x = p; break; }
+        const uint32_t dv = EV[k].o ? (death[k] >= NEV ? CINF : (uint32_t)death[k] + 1) : t;
+        pos[k] = x;
+        if (x == 0xFFFFFFFFu) continue;
+        if (x + 1 > cmaxpos) cmaxpos = x + 1;
+        if (dv == CINF) { memmove(D + x, D + x + 1, (CWID - 1 - x) * 4); D[CWID - 1] = 0; if (hi) hi--; if (hi < x) hi = x; }
+        else { D[x] = dv; if (x + 1 > hi) hi = x + 1; }
+    }
+    /* free positions (consumed at or before the last event) all read 0, so a
+     * warm-started exit and the exact one compare equal */
+    for (uint32_t p = 0; p < CWID; p++) if (D[p] <= (uint32_t)e1) D[p] = 0;
+    memcpy(Dout, D, CWID * 4);
+    return 0;
+}
+static void run_compact(uint32_t CH, uint32_t warm) {
+    CWID = 1024;
+    uint64_t *death = malloc(NEV * 8);
+    for (uint64_t k = 0; k < NEV; k++) death[k] = NEV;
+    for (uint64_t k = 0; k < NEV; k++)
+        for (uint32_t q = 0; q < EV[k].ntok; q++) death[TOK[EV[k].tok0 + q]] = k;
+    uint64_t nleak = 0;
+    for (uint64_t k = 0; k < NEV; k++) if (EV[k].o && death[k] >= NEV) nleak++;
+    const uint64_t nch = (NEV + CH - 1) / CH;
+    uint32_t *XP = calloc(nch * CWID, 4), *XN = calloc(nch * CWID, 4);
+    uint32_t *PP = malloc(NEV * 4), *PN = malloc(NEV * 4), *zero = calloc(CWID, 4);
+    for (uint64_t k = 0; k < NEV; k++) PP[k] = 0xFFFFFFFEu;
+    /* the sequential compact replay (for the width and the real-slot check) */
+    uint32_t *PS = malloc(NEV * 4), *Dx = malloc(CWID * 4);
+    cmaxpos = 0;
+    creplay(0, NEV, zero, Dx, PS, death);
+    const uint32_t seqw = cmaxpos;
+    printf("{\"scheme\": \"compact\", \"chunk\": %u, \"warm\": %u, \"events\": %lu, \"leaks\": %lu, \"compact_width\": %u, \"iters\": [",
+           CH, warm, (unsigned long)NEV, (unsigned long)nleak, seqw);
+    int it;
+    uint32_t *own = malloc(NEV * 4);
+    for (it = 1; it <= 100000; it++) {
+        int changed = 0;
+        uint64_t wrong_chunks = 0, wrong_ev = 0, first_wrong = nch;
+        for (uint64_t c = 0; c < nch; c++) {
+            const uint64_t e0 = c * CH, e1 = e0 + CH < NEV ? e0 + CH : NEV;
+            uint64_t ew = e0;
+            const uint32_t *Din = zero;
+            if (it == 1) ew = e0 > warm ? e0 - warm : 0;
+            else if (c) Din = XP + (c - 1) * CWID;
+            creplay(ew, e1, Din, XN + c * CWID, own, death);
+            uint64_t w = 0;
+            for (uint64_t k = e0; k < e1; k++) { PN[k] = own[k]; if (PN[k] != PP[k]) changed = 1; w += own[k] != PS[k]; }
+            if (memcmp(XN + c * CWID, XP + c * CWID, CWID * 4)) changed = 1;
+            if (w) { wrong_chunks++; if (c < first_wrong) first_wrong = c; }
+            wrong_ev += w;
+        }
+        printf("%s[%d, %lu, %lu, %lu]", it > 1 ? ", " : "", it, (unsigned long)wrong_chunks, (unsigned long)first_wrong,
+               (unsigned long)wrong_ev);
+        uint32_t *t = PP; PP = PN; PN = t;
+        t = XP; XP = XN; XN = t;
+        if (!changed && it > 1) break;
+    }
+    /* real slots */
+    uint32_t *S = malloc((CWID + nleak + 8) * 4);
+    for (uint32_t p = 0; p < CWID; p++) S[p] = p;
+    uint64_t bad = 0;
+    for (uint64_t k = 0; k < NEV; k++) {
+        const uint32_t x = PP[k];
+        const uint32_t slot = x == 0xFFFFFFFFu ? 0xFFFFu : S[x];
+        if (slot != EV[k].slot) bad++;
+        if (x != 0xFFFFFFFFu && EV[k].o && death[k] >= NEV) {
+            const uint32_t top = S[CWID - 1];
+            memmove(S + x, S + x + 1, (CWID - 1 - x) * 4);
+            S[CWID - 1] = top + 1;
+        }
+    }
+    printf("], \"fixed_point_at\": %d, \"wrong_slots_at_end\": %lu}\n", it, (unsigned long)bad);
+    fflush(stdout);
+}
+
 int main(int argc, char **argv) {
     if (argc < 5) { fprintf(stderr, "usage: %s preset rows chunk warm [exit|live ...]\n", argv[0]); return 2; }
     static const char *names[] = {"linear", "random13", "linux", "wide16", "anomaly", "skew", "linuxwide"};
@@ -389,6 +485,7 @@ int main(int argc, char **argv) {
                (unsigned long)NEV, (unsigned long)cev, (unsigned long)occupying, (unsigned long)leaked, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
         return 0;
     }
+    if (argc > 5 && !strcmp(argv[5], "compact")) { run_compact(CH, warm); wgs_free(d); return 0; }
     if (argc > 5 && !strcmp(argv[5], "longseed")) { run_longseed(CH, warm); wgs_free(d); return 0; }
     for (int a = 5; a < argc || a == 5; a++) {
         const char *s = a < argc ? argv[a] : "exit";

@@ -147,10 +147,11 @@ def test_serial_replay_is_exact(kind, n, over):
 def test_auto_replay_mode_picks_by_list_shape():
     """Auto mode: the skewed list (parents at earlier rows leak slots for good,
     so the chunked fixed point needs about one iteration per chunk) moves to
-    the serial replay; wide16 (forgets a wrong guess within a chunk) stays on
-    the chunked one; both bit-exact at every build."""
+    the compacted replay (r05: the leaked slots struck out, form 301, every
+    leak counted); wide16 (forgets a wrong guess within a chunk) stays on the
+    chunked one (101); both bit-exact at every build."""
     import wgraph
-    for kind, n, want in (("skew", 1_000_000, 1), ("wide16", 1_000_000, 0)):
+    for kind, n, want in (("skew", 1_000_000, 301), ("wide16", 1_000_000, 101)):
         d = synth.generate(kind, n)
         o = _oracle(d)
         eng = wgraph.Engine(0)
@@ -158,7 +159,11 @@ def test_auto_replay_mode_picks_by_list_shape():
             for _ in range(3):
                 eng.build(d)
                 _check_lanes(eng, d, o)
-            assert int(eng.debug_counters()[10]) == want, kind
+            dc = eng.debug_counters()
+            assert int(dc[12]) == want, kind
+            assert int(dc[10]) == 0, kind   # not the serial pass
+            if kind == "skew":
+                assert int(dc[13]) > 0, "no leaked slot struck out"
         finally:
             eng.close()
             o.close()

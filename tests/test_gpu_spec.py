@@ -224,3 +224,39 @@ def test_sliced_lists_emission(kind, n):
                 eng.close()
     finally:
         o.close()
+
+
+def test_duplicate_ids_window_row_differs_from_table_row():
+    """Round 4's illegal memory access: with duplicate ids the
+    window probe's row for an id (the next 64 rows' ids, wg_hash.hip) and the
+    table's (the last occurrence wins, commit_graph.rs:273-274) differ, and
+    the lane-chain kernels queued before the host knows the list is not well
+    formed wrote past a child list.  The list that faulted (anomaly, 5000
+    rows, seed 77) on a fresh context (the exact build) and on a context whose
+    earlier build lets it speculate, twice; every build bit-exact against the
+    oracle through the general walk (lane_path 1), geometry and vertices too."""
+    import wgraph
+    from oracle import oracle_c
+    d = synth.generate("anomaly", 5000, seed=77)
+    o = oracle_c.OracleLayout(d)
+    try:
+        eng = wgraph.Engine(0)
+        try:
+            eng.build(d)
+            assert eng.layout_summary().lane_path == 1
+            full_check(eng, d, o, "fresh")
+        finally:
+            eng.close()
+        eng = wgraph.Engine(0)
+        try:
+            w = synth.generate("wide16", 6000, seed=3)
+            eng.build(w)
+            for k in range(2):
+                eng.build(d)
+                full_check(eng, d, o, f"speculating #{k}")
+                assert eng.layout_summary().lane_path == 1
+            assert int(eng.debug_counters()[7]) >= 1   # the speculative lanes were redone by the exact walk
+        finally:
+            eng.close()
+    finally:
+        o.close()

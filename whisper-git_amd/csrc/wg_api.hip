@@ -495,7 +495,8 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         c->spec_replay_shard = value != 0;
         return WG_OK;
     case WG_OPT_REPLAY_MODE:
-        if (value < 0 || value > 2) return wg_fail(c, WG_E_INVALID, "replay mode must be 0 (auto), 1 (chunked) or 2 (serial)");
+        if (value < 0 || value > 3)
+            return wg_fail(c, WG_E_INVALID, "replay mode must be 0 (auto), 1 (chunked), 2 (serial) or 3 (compacted)");
         c->replay_mode = (uint32_t)value;
         return WG_OK;
     case WG_OPT_SLICE_LISTS:
@@ -503,6 +504,11 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         WG_SETTLE(c);
         c->slice_on = value != 0;
         c->slice_min_rows = value == 2 ? 4 * WG_SWEEP_CH : 1ull << 18;
+        return WG_OK;
+    case WG_OPT_DC_WARMUP:
+        if (value < 0 || value > (1 << 20) || (value & 63)) return wg_fail(c, WG_E_INVALID, "warm-up must be a multiple of 64 in 0..2^20");
+        c->dc_warm_fixed = (uint32_t)value;
+        c->dc_warm = value ? (uint32_t)value : wg_ctx::WG_DC_WARM0;
         return WG_OK;
     case WG_OPT_SWEEP_REG:
         if (value < 0 || value > 512) return wg_fail(c, WG_E_INVALID, "sweep register capacity must be 0..512");
@@ -1106,6 +1112,9 @@ int wg_debug_counters(wg_ctx *c, uint32_t *out, int n) {
     if (n > 9) out[9] = c->spec_replays_shard;
     if (n > 10) out[10] = c->last_serial ? 1u : 0u;
     if (n > 11) out[11] = c->sliced_emits;
+    if (n > 12) out[12] = c->last_form;
+    if (n > 13) out[13] = c->last_leaks;
+    if (n > 14) out[14] = c->last_dc_warm;
     return WG_OK;
 }
 

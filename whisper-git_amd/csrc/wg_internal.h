@@ -171,6 +171,8 @@ struct ShardState {
     bool replay_pending = false;    // X3 replayed speculatively: its words are checked with the local geometry's
     uint32_t rp_it = 0, rp_chunk = 0;
     const uint32_t *rp_flags = nullptr, *rp_scal = nullptr;
+    bool rp_dc = false;       // ... by the compacted replay, at rp_nw words
+    uint32_t rp_nw = 1, rp_warm = 0;
 };
 
 // SDF font atlas slot (wg_font.hip)
@@ -186,7 +188,8 @@ struct FontSlot {
 // workspace slots in wg_ctx::lf (wg_lanes_fast.hip; the sharded build reuses LF_EVREC / LF_AUX for the
 // gathered event records)
 enum { LF_FIRST, LF_FPC, LF_WINFO, LF_EVOFF, LF_SECEV, LF_CHOFF, LF_CHFILL, LF_CH, LF_SPA, LF_SPB, LF_EVREC,
-       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_LFIRST, LF_SERREC, LF_DEATH, LF_COUNT };
+       LF_SLOT, LF_FLAGS, LF_SLOTB, LF_OCC, LF_STATS, LF_RFLAGS, LF_AUXOFF, LF_AUX, LF_LFIRST, LF_SERREC, LF_DEATH,
+       LF_DCVEC, LF_DCMASK, LF_DCPRE, LF_DCLIST, LF_DCSNAP, LF_DCSLOT, LF_COUNT };
 
 // event replay to a fixed point (wg_lanes_replay.hip)
 struct ReplayRun {
@@ -209,7 +212,32 @@ struct ReplayRun {
                                          // or null: the first iteration then runs the general replay kernel
     uint32_t serial_it = 0;              // exact replay at the long chunk: still moving at this iteration ->
     bool to_serial = false;              // stop; the caller replays serially (wg_replay_resume)
+    // compacted D-state chunked replay (wg_lanes_dchunk.hip): nw = words of positions (1, 2, 4)
+    bool dc = false;
+    uint32_t *dc_dvec[2] = {nullptr, nullptr};   // exit D-vectors per chunk, two iterations in turn
+    unsigned long long *dc_lkmask = nullptr;     // per 64-event batch: the leaking events
+    uint32_t *dc_bpre = nullptr;                 // per batch: leaks before it (k_dc_snap)
+    uint32_t *dc_lklist = nullptr;               // the leaking events in order
+    uint16_t *dc_snap = nullptr;                 // the non-leaked slots after each leak, [leak_cap + 1][64 nw]
+    uint32_t dc_leak_cap = 0;
+    uint16_t *dc_pos = nullptr;                  // the final positions (wg_dc_finish)
+    uint16_t *dc_slot = nullptr;                 // the slots (wg_dc_finish; sp_prev points here after it)
+    uint64_t dc_blocks = 0;                      // k_dc_fix blocks = stats records (3 words each)
 };
+// the compacted D-state chunked replay (wg_lanes_dchunk.hip): R.slots_a / b
+// hold positions; wg_dc_init clears the flag words, wg_dc_iterate launches
+// iterations (the first warm-started), wg_dc_finish turns the last positions
+// into slots (R.sp_prev, R.stats per WG_DC_FIX_T events).  lane_scalars [4]
+// the highest allocated position + 1, [5] leaks, [6] more leaks than dc_leak_cap.
+constexpr uint32_t WG_DC_FIX_T = 256;
+uint32_t wg_dc_words(uint32_t positions);   // 1, 2 or 4 words for that many positions below the sentinel; 0: none
+constexpr uint32_t WG_DC_LEAK_CAP = 16384;   // leaks the snapshots hold (more: the serial pass)
+// resets the run (positions in R.slots_a / b); flags: also clear the flag
+// words (a speculative build's event kernel clears them otherwise)
+hipError_t wg_dc_init(hipStream_t s, ReplayRun &R, bool flags);
+hipError_t wg_dc_scalars(hipStream_t s, const ReplayRun &R);   // lane scalars [0..4] after wg_dc_finish (wg_lanes_replay.hip)
+hipError_t wg_dc_iterate(hipStream_t s, ReplayRun &R, uint32_t n);
+hipError_t wg_dc_finish(hipStream_t s, ReplayRun &R);
 // The replay's chunk lengths (events).  Short chunks make iteration 1 short
 // (its chunks replay serially, one wave each) and suit lists whose greedy
 // state forgets a wrong entry within a chunk; on others (long-lived lanes
@@ -226,7 +254,7 @@ constexpr uint64_t WG_REPLAY_WIDE_EVENTS = 131072;   // 1024 short chunks: above
 struct WgFetch { const void *p; bool wide; };   // wide: 8-byte value, else 4-byte
 
 // speculative build validation words: lanes + geometry + the edge count
-constexpr int WG_LANES_SPEC_ITEMS = 9;
+constexpr int WG_LANES_SPEC_ITEMS = 12;
 constexpr int WG_GEOM_SPEC_ITEMS = 8;
 constexpr int WG_PENDING_ITEMS = WG_LANES_SPEC_ITEMS + WG_GEOM_SPEC_ITEMS + 1;
 
@@ -261,6 +289,9 @@ struct wg_ctx {
     uint64_t n_list = 0;      // rows of the whole list (n differs for a row shard)
     bool     have_layout = false;
     uint32_t max_lane = 0, n_slots = 0, lane_path = 1;
+    uint32_t slots_last = 0;  // n_slots of the last completed lane build (a build in progress has cleared n_slots)
+    // the slot count the next replay's width and narrow forms follow
+    uint32_t slots_hint() const { return n_slots ? n_slots : slots_last; }
     float    graph_width = 24.0f;
     // inputs (device copies when the caller passed host memory)
     DevBuf in_oid, in_time, in_poff, in_poid, in_flags;
@@ -317,30 +348,79 @@ struct wg_ctx {
         else { *chunk = WG_REPLAY_CHUNK_LONG; *warm = 0; }
     }
     // Serial replay (wg_lanes_serial.hip): lists whose greedy state does not
-    // forget a wrong guess (parents at earlier rows leak slots for good,
-    // long-lived lanes) need about one chunked fixed-point iteration per chunk;
-    // their lanes come from one exact single-wave pass instead.  Auto: a replay
-    // at the long chunk still moving after the iterations the serial pass
-    // would cost (serial_cost_us) switches the context to it; a list of a very
-    // different length (mode_rows) starts over with the chunked replay.
-    uint32_t replay_mode = 0;      // WG_OPT_REPLAY_MODE: 0 auto, 1 chunked fixed point, 2 serial
+    // forget a wrong guess (long-lived lanes) need about one chunked
+    // fixed-point iteration per chunk; their lanes come from one exact
+    // single-wave pass instead.  Compacted replay (wg_lanes_dchunk.hip, r05):
+    // the D-state chunked fixed point with the leaked slots struck out, for
+    // the lists whose greedy state forgets once the leaks are gone (parents at
+    // earlier rows, the Linux shape).  Auto: a short-chunk replay that needs
+    // more than WG_REPLAY_SHORT_MAX_FP iterations moves the context to the
+    // compacted replay; a compacted replay whose fixed point comes late
+    // doubles its warm-up, and one whose iterations cost more than the serial
+    // pass would moves it to the serial pass; the serial choice expires after
+    // WG_SERIAL_RETRY builds (the compacted replay is tried again), and a list
+    // of a very different length (mode_rows) starts over.
+    uint32_t replay_mode = 0;      // WG_OPT_REPLAY_MODE: 0 auto, 1 chunked fixed point, 2 serial, 3 compacted
     bool replay_serial = false;    // auto: this list shape replays serially
+    bool replay_dc = false;        // auto: this list shape replays by the compacted fixed point
     bool last_serial = false;      // the last lane replay was the serial pass (wg_debug_counters [10])
-    uint64_t mode_rows = 0;        // rows of the list the auto choices (replay_long, replay_serial) were made on
-    bool use_serial() const { return replay_mode == 2 || (replay_mode == 0 && replay_serial); }
+    uint32_t last_form = 0;        // the last replay's form (wg_debug_counters [12], WG_FORM_*)
+    uint32_t last_leaks = 0;       // leaked slots struck out by the last compacted replay ([13])
+    uint32_t last_dc_warm = 0;     // ... and its warm-up ([14])
+    uint32_t serial_builds = 0;    // serial builds since the auto choice was made
+    uint32_t dc_plain_builds = 0;  // compacted builds in a row that struck out no leak (the chunked replay is retried)
+    static constexpr uint32_t WG_SERIAL_RETRY = 16;
+    uint32_t dc_warm = 8192;       // the compacted replay's first-iteration warm-up (events)
+    uint32_t dc_warm_fixed = 0;    // WG_OPT_DC_WARMUP (0: auto)
+    static constexpr uint32_t WG_DC_WARM0 = 8192, WG_DC_WARM_MAX = 32768;
+    uint32_t dc_nw = 1;            // words of positions of the next compacted replay (1, 2, 4)
+    uint32_t dc_blind = 2;         // its iterations before the first check
+    uint64_t mode_rows = 0;        // rows of the list the auto choices were made on
+    // (mode 3: the compacted replay, or the serial pass where it does not apply)
+    bool use_serial() const { return replay_mode == 2 || ((replay_mode == 0 || replay_mode == 3) && replay_serial); }
+    bool use_dc() const { return (replay_mode == 3 || (replay_mode == 0 && replay_dc)) && !replay_serial; }
     // estimated cost of the serial pass (us) against one chunked iteration at the long chunk
     static double serial_cost_us(uint64_t nev, uint32_t nw) {
         return (double)nev * (nw <= 1 ? 0.016 : nw <= 2 ? 0.04 : nw <= 4 ? 0.07 : nw <= 16 ? 0.3 : 1.0);
     }
     static constexpr double WG_CHUNKED_ITER_US = 60.0;
+    static constexpr double WG_DC_ITER_US = 15.0;   // a compacted iteration after the first (128-256 events per chunk)
     // a list of a very different length: the auto choices start over
     void replay_shape(uint64_t rows) {
         if (mode_rows && (rows > 2 * mode_rows || 2 * rows < mode_rows)) {
             replay_long = false;
             replay_serial = false;
+            replay_dc = false;
+            dc_warm = dc_warm_fixed ? dc_warm_fixed : WG_DC_WARM0;
+            dc_blind = 2;
             replay_blind = 4;
         }
         if (!mode_rows || rows > 2 * mode_rows || 2 * rows < mode_rows) mode_rows = rows;
+    }
+    // a serial build done: after WG_SERIAL_RETRY of them the compacted replay is tried again
+    void serial_done() {
+        if ((replay_mode != 0 && replay_mode != 3) || !replay_serial) return;
+        if (++serial_builds >= WG_SERIAL_RETRY) {
+            replay_serial = false;
+            replay_dc = true;
+            dc_warm = dc_warm_fixed ? dc_warm_fixed : WG_DC_WARM_MAX;
+            dc_blind = 2;
+            serial_builds = 0;
+        }
+    }
+    // a compacted replay that reached its fixed point at iteration fp: the
+    // next one's warm-up, blind count, or the serial pass
+    void dc_adapt(uint32_t fp, uint64_t nev, uint32_t positions) {
+        if (fp == 0) return;
+        if (replay_mode == 0 && fp > 2 &&
+            (double)(fp - 1) * WG_DC_ITER_US > serial_cost_us(nev, positions < 64 ? 1u : positions < 256 ? 4u : 16u)) {
+            replay_serial = true;
+            serial_builds = 0;
+            return;
+        }
+        if (fp > 3 && dc_warm < WG_DC_WARM_MAX && !dc_warm_fixed) dc_warm *= 2;
+        dc_blind = fp >= dc_blind ? fp : (dc_blind + fp) / 2;
+        if (dc_blind < 2) dc_blind = 2;
     }
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
@@ -361,7 +441,8 @@ struct wg_ctx {
             return;
         }
         if (replay_auto && chunk < WG_REPLAY_CHUNK_LONG && fp > WG_REPLAY_SHORT_MAX_FP) {
-            replay_long = true;   // this list shape wants the long chunk (its own blind count from the next build on)
+            if (replay_mode == 0) replay_dc = true;   // this list shape wants the compacted replay
+            else replay_long = true;                  // (held on the chunked replay: the long chunk)
             replay_blind = 4;
             return;
         }
@@ -727,7 +808,9 @@ int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *e
                        bool *ok);
 int wg_lf_replay_lanes_spec(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
                             ReplayRun &run);
-void wg_lf_replay_spec_commit(wg_ctx *c, uint32_t it, uint32_t chunk, uint32_t max_lane, uint32_t n_slots, uint32_t first_still);
+// a speculative sharded replay's words hold (run: its it, chunk, dc, nw, warm): the context takes them
+void wg_lf_replay_spec_commit(wg_ctx *c, const ReplayRun &run, uint32_t max_lane, uint32_t n_slots, uint32_t first_still,
+                              uint32_t positions, uint32_t leaks);
 int wg_stage_heights(wg_ctx *c);              // wg_rowtop.hip
 int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out,
                    const int64_t *time = nullptr);   // rows [0,m) of an n-row list (time: the layout's)

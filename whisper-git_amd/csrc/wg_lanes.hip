@@ -174,6 +174,7 @@ int wg_stage_lanes(wg_ctx *c, bool spec) {
     WG_ALLOC(c, c->lane_asg, n * 4 + 4);
     WG_ALLOC(c, c->lane_scalars, 64);
     c->max_lane = 0;
+    if (c->n_slots) c->slots_last = c->n_slots;   // (the replay's narrow forms follow the last list's slots)
     c->n_slots = 0;
     c->lane_path = 1;
     c->graph_width = WG_LANE_W;   // max_lane 0 -> one visible lane (:353-354)

@@ -118,7 +118,10 @@ __global__ void k_lf_xfirst(LfRange R) {
     bool first = !(leaky && (en.kf & WG_XF_LLEAKY));
     for (uint64_t y = 0; y < xe && first; y++) {
         const WgXEnt o = R.xall[y];
-        // (a forward reference never precedes a leaky one to the same row in key order)
+        // For a leaky entry only earlier leaky references count: forward
+        // references to the same row (from rows c' < p, which sort before it)
+        // are consumed at row p (:287-291) and hold nothing afterwards.  For a
+        // forward entry no leaky reference can sort before it.
         if (o.p == en.p && (o.kf & WG_XF_FIRST_IN_ROW) && ref_key(o.c, o.kf & 0xFFFFu) < key && (!leaky || o.p <= o.c))
             first = false;
     }
@@ -374,18 +377,20 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
         ev[e] = make_uint4(f | (LOCAL ? 0u : token_bits(ev_base + e, t[0], t[1])), t[0], t[1],
                            (w > 2) ? aux_base + aux_off[j] : (uint32_t)gj);
         if (death) {   // (single GPU: tokens are event ids) this event consumes every waiter's token
-            if (list)
-                for (uint32_t q = 1; q <= w; q++) death[list[q]] = e + 1u;
-            else {
-                death[t[0]] = e + 1u;
-                death[t[1]] = e + 1u;
+            const uint32_t dn = ev_off[R.nl];   // (a token past the events is never written through)
+            if (list) {
+                for (uint32_t q = 1; q <= w; q++)
+                    if (list[q] < dn) death[list[q]] = e + 1u;
+            } else {
+                if (t[0] < dn) death[t[0]] = e + 1u;
+                if (t[1] < dn) death[t[1]] = e + 1u;
             }
         }
         e++;
     } else if (!fp_in) {
         const uint32_t t0 = LOCAL ? sp[j] : sp[j] & ~WG_TOK_EV;
         ev[e] = make_uint4(F_C | (LOCAL ? 0u : token_bits(ev_base + e, t0, t0)), t0, t0, (uint32_t)gj);
-        if (death) death[t0] = e + 1u;
+        if (death && t0 < ev_off[R.nl]) death[t0] = e + 1u;
         e++;
     }
     const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
@@ -400,7 +405,8 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
 
 // consumption times from global records (the sharded build's gathered
 // stream; a single-GPU build writes them in k_lf_events): tokens never
-// consumed keep 0xFFFFFFFF
+// consumed keep 0xFFFFFFFF.  A token past the events (a crossing entry that
+// resolved to no token, WG_TOK_NONE) is not written through.
 __global__ void k_lf_death_fill(uint64_t nev, uint32_t *__restrict__ death) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < nev) death[k] = 0xFFFFFFFFu;
@@ -414,10 +420,13 @@ __global__ void k_lf_death_scatter(uint64_t nev, const uint4 *__restrict__ ev, c
     const uint32_t t = (uint32_t)k + 1u;
     if (r.x & F_M) {
         const uint32_t n = aux[r.w];
-        for (uint32_t q = 0; q < n; q++) death[aux[r.w + 1 + q]] = t;
+        for (uint32_t q = 0; q < n; q++) {
+            const uint32_t tk = aux[r.w + 1 + q];
+            if (tk < nev) death[tk] = t;
+        }
     } else {
-        death[r.y] = t;
-        death[r.z] = t;
+        if (r.y < nev) death[r.y] = t;
+        if (r.z < nev) death[r.z] = t;
     }
 }
 
@@ -674,29 +683,176 @@ int wg_lf_events_finish(wg_ctx *c, const LfRange &R, uint32_t ev_base, const uin
 // The replay's convergence check rides on the lane-scalar read: steady-state
 // builds launch exactly the iterations they need with one host sync.
 static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
-                           uint32_t nw, bool *ok, bool *overflow);
+                           uint32_t nw, bool *ok, bool *overflow, bool narrow = true, bool *was_narrow = nullptr);
+
+static int replay_lanes_dc(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                           bool *ok, bool *to_serial);
 
 int wg_lf_replay_lanes(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
                        bool *ok) {
     *ok = false;
+    // the compacted replay (it needs the consumption times); past its width,
+    // its leak snapshots or the serial pass's cost it hands over to the serial pass
+    if (c->use_dc() && c->replay_death) {
+        bool to_serial = false;
+        const int rc = replay_lanes_dc(c, R, nev, ev, aux, lane, ok, &to_serial);
+        if (rc != WG_OK || *ok) return rc;
+        c->replay_serial = true;   // (auto and mode 3: the serial pass from here on, until it expires)
+        c->serial_builds = 0;
+    }
     // the occupancy width of the last build first; a replay that overflowed
-    // it is redone wider (63 -> 255 -> 1023 slots; 4095 on the serial workgroup)
-    for (uint32_t nw = c->replay_nw;; nw = nw < 4 ? 4u : (nw < 16 ? 16u : 64u)) {
-        bool overflow = false;
-        const int rc = replay_lanes_at(c, R, nev, ev, aux, lane, nw, ok, &overflow);
-        if (rc != WG_OK || !overflow || nw >= 64) return rc;
+    // it is redone wider (63 -> 255 -> 1023 slots; 4095 on the serial
+    // workgroup); a serial pass in a narrower form (3 of 4 words: 191 slots,
+    // 8 of 16: 511) that overflowed is redone at its full width first
+    bool narrow = true;
+    for (uint32_t nw = c->replay_nw;;) {
+        bool overflow = false, was_narrow = false;
+        const int rc = replay_lanes_at(c, R, nev, ev, aux, lane, nw, ok, &overflow, narrow, &was_narrow);
+        if (rc != WG_OK || !overflow || (nw >= 64 && !was_narrow)) return rc;
+        if (was_narrow) { narrow = false; continue; }
+        nw = nw < 4 ? 4u : (nw < 16 ? 16u : 64u);
+    }
+}
+
+// the form code of a serial pass at nw words (wg_debug_counters [12])
+static uint32_t serial_form(const ReplayRun &run) {
+    if (run.nw <= 1) return 201;
+    if (run.nw <= 4) return run.ser_w3 ? 203 : 204;
+    if (run.nw <= 16) return run.ser_w8 ? 208 : 216;
+    return 264;
+}
+
+// The compacted replay's run and buffers (wg_lanes_dchunk.hip) for nev events
+// (a bound when the run's nev_dev is set) at nw words of positions.
+static int dc_setup(wg_ctx *c, ReplayRun &run, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t nw) {
+    run = ReplayRun{};
+    run.dc = true;
+    run.nev = nev;
+    run.nw = nw;
+    run.chunk = nev >= WG_REPLAY_WIDE_EVENTS ? 2 * WG_REPLAY_CHUNK_SHORT : WG_REPLAY_CHUNK_SHORT;
+    run.warm = c->dc_warm;
+    const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
+    run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
+    const uint64_t nb = nev / 64 + 2, W = 64ull * nw;
+    DevBuf *b = c->lf;
+    WG_ALLOC(c, b[LF_SLOT], (nev + 64) * sizeof(uint16_t));
+    WG_ALLOC(c, b[LF_SLOTB], (nev + 64) * sizeof(uint16_t));
+    WG_ALLOC(c, b[LF_DCVEC], 2 * nch * W * 4);
+    WG_ALLOC(c, b[LF_DCMASK], nb * 8);
+    WG_ALLOC(c, b[LF_DCPRE], nb * 4);
+    WG_ALLOC(c, b[LF_DCLIST], (uint64_t)WG_DC_LEAK_CAP * 4);
+    WG_ALLOC(c, b[LF_DCSNAP], ((uint64_t)WG_DC_LEAK_CAP + 1) * W * 2);
+    WG_ALLOC(c, b[LF_DCSLOT], (nev + 64) * sizeof(uint16_t));
+    WG_ALLOC(c, b[LF_STATS], (nev / WG_DC_FIX_T + 2) * 12);
+    WG_ALLOC(c, b[LF_RFLAGS], (run.max_iters + 2) * 4);
+    run.ev = ev;
+    run.aux = aux;
+    run.slots_a = b[LF_SLOT].as<uint16_t>();
+    run.slots_b = b[LF_SLOTB].as<uint16_t>();
+    run.dc_dvec[0] = b[LF_DCVEC].as<uint32_t>();
+    run.dc_dvec[1] = b[LF_DCVEC].as<uint32_t>() + nch * W;
+    run.dc_lkmask = b[LF_DCMASK].as<unsigned long long>();
+    run.dc_bpre = b[LF_DCPRE].as<uint32_t>();
+    run.dc_lklist = b[LF_DCLIST].as<uint32_t>();
+    run.dc_snap = b[LF_DCSNAP].as<uint16_t>();
+    run.dc_leak_cap = WG_DC_LEAK_CAP;
+    run.dc_slot = b[LF_DCSLOT].as<uint16_t>();
+    run.stats = b[LF_STATS].as<uint32_t>();
+    run.flags = b[LF_RFLAGS].as<uint32_t>();
+    run.scal = c->lane_scalars.as<uint32_t>();
+    run.death = c->replay_death;
+    return WG_OK;
+}
+
+// a compacted replay's outcome: the context's scalars and next choices
+// (w: max_lane, slots, positions + 1, leaks, first iteration that changed nothing)
+static void dc_commit(wg_ctx *c, const ReplayRun &run, uint64_t nev, uint32_t max_lane, uint32_t n_slots, uint32_t positions,
+                      uint32_t leaks, uint32_t first_still) {
+    c->max_lane = max_lane;
+    c->n_slots = n_slots;
+    c->replay_nw = wg_ctx::nw_for_slots(n_slots);
+    c->replay_iters = run.it;
+    const uint32_t w = wg_dc_words(positions);
+    c->dc_nw = w ? w : 4u;
+    c->last_leaks = leaks;
+    c->last_dc_warm = run.warm;
+    c->last_form = 300u + run.nw;
+    c->last_serial = false;
+    c->dc_adapt(first_still, nev, positions);
+    c->lane_path = 0;
+    // (auto) a list shape with no leaks may suit the chunked replay after all:
+    // it is tried again after WG_SERIAL_RETRY such builds (a skewed list's
+    // choice does not hold later lists of the same length)
+    if (c->replay_mode == 0 && c->replay_dc) {
+        c->dc_plain_builds = leaks ? 0u : c->dc_plain_builds + 1u;
+        if (c->dc_plain_builds >= wg_ctx::WG_SERIAL_RETRY) {
+            c->replay_dc = false;
+            c->dc_plain_builds = 0;
+            c->replay_blind = 4;
+        }
+    }
+}
+
+// The exact compacted replay: c->dc_blind iterations, then polls; positions
+// past the width are redone wider (1 -> 2 -> 4 words).  *to_serial: more
+// leaks than the snapshots hold, more than 4 words, or (auto) iterations past
+// what the serial pass costs.
+static int replay_lanes_dc(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
+                           bool *ok, bool *to_serial) {
+    hipStream_t s = c->stream;
+    *ok = *to_serial = false;
+    uint32_t nw = c->dc_nw ? c->dc_nw : 1u;
+    for (;;) {
+        ReplayRun run;
+        int rc = dc_setup(c, run, nev, ev, aux, nw);
+        if (rc != WG_OK) return rc;
+        // (auto) the serial pass's cost in iterations after the first
+        const uint32_t budget = 2u + (uint32_t)(wg_ctx::serial_cost_us(nev, c->replay_nw) / wg_ctx::WG_DC_ITER_US);
+        wg_stage_begin(c, "lf_loop");
+        WG_HIP(c, wg_dc_init(s, run, true));
+        WG_HIP(c, wg_dc_iterate(s, run, c->dc_blind < 2 ? 2u : c->dc_blind));
+        const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
+        uint64_t w[9] = {0, 0, 0, 0, 0, 0, 0, 1, 1};
+        bool conv = false;
+        for (;;) {
+            WG_HIP(c, wg_dc_finish(s, run));
+            WG_HIP(c, wg_dc_scalars(s, run));
+            rc = wg_fetch(c, {{ls, false}, {ls + 1, false}, {ls + 2, false}, {ls + 3, false}, {ls + 4, false}, {ls + 5, false},
+                              {ls + 6, false}, {run.flags + run.it - 1, false}, {run.flags + run.it, false}}, w);
+            if (rc != WG_OK) { wg_stage_end(c); return rc; }
+            conv = nev == 0 || w[7] == 0 || w[8] == 0;
+            if (conv || run.it >= run.max_iters) break;
+            if (c->replay_mode == 0 && run.it >= budget) break;
+            WG_HIP(c, wg_dc_iterate(s, run, 4));
+        }
+        wg_stage_end(c);
+        if (!conv || w[6]) { *to_serial = true; return WG_OK; }   // (auto budget spent / more leaks than the snapshots hold)
+        if (w[2]) {                                                // positions past the width: wider
+            if (nw >= 4) { *to_serial = true; return WG_OK; }
+            nw = nw < 2 ? 2u : 4u;
+            continue;
+        }
+        if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
+        WG_HIP(c, hipGetLastError());
+        c->lf_slot_of = run.sp_prev;
+        dc_commit(c, run, nev, (uint32_t)w[0], (uint32_t)w[1], (uint32_t)w[4], (uint32_t)w[5], (uint32_t)w[3]);
+        *ok = true;
+        return WG_OK;
     }
 }
 
 // the run's buffers and geometry at occupancy width nw (exact and speculative sharded replays)
-static int replay_setup(wg_ctx *c, ReplayRun &run, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t nw) {
+static int replay_setup(wg_ctx *c, ReplayRun &run, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t nw,
+                        bool narrow = true) {
     run.nev = nev;
     run.nw = nw;
     // (the serial pass's cost is its words: 8 instead of 16 when the last
-    // list of this context held at most 448 slots; a list past 511 overflows
-    // and the caller widens, as at any width)
-    run.ser_w8 = nw == 16 && c->n_slots > 0 && c->n_slots <= 448;
-    run.ser_w3 = nw == 4 && c->n_slots > 0 && c->n_slots <= 170;
+    // list of this context held at most 448 slots, 3 instead of 4 at most
+    // 170; a list past 511 / 191 overflows and the caller redoes it at the
+    // full width)
+    const uint32_t hint = c->slots_hint();
+    run.ser_w8 = narrow && nw == 16 && hint > 0 && hint <= 448;
+    run.ser_w3 = narrow && nw == 4 && hint > 0 && hint <= 170;
     c->replay_geometry(&run.chunk, &run.warm);
     const uint64_t nch = (nev + run.chunk - 1) / run.chunk + 1;
     run.max_iters = (uint32_t)nch + 1;   // always enough to reach the fixed point
@@ -728,18 +884,36 @@ static int replay_setup(wg_ctx *c, ReplayRun &run, uint64_t nev, const uint4 *ev
 int wg_lf_replay_lanes_spec(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
                             ReplayRun &run) {
     run = ReplayRun{};
+    hipStream_t s = c->stream;
+    if (c->use_dc() && c->replay_death) {   // the compacted replay: blind iterations, then its slots and scalars
+        int rc = dc_setup(c, run, nev, ev, aux, c->dc_nw ? c->dc_nw : 1u);
+        if (rc != WG_OK) return rc;
+        wg_stage_begin(c, "lf_loop");
+        WG_HIP(c, wg_dc_init(s, run, true));
+        WG_HIP(c, wg_dc_iterate(s, run, c->dc_blind < 2 ? 2u : c->dc_blind));
+        WG_HIP(c, wg_dc_finish(s, run));
+        WG_HIP(c, wg_dc_scalars(s, run));
+        if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
+        c->lf_slot_of = run.sp_prev;
+        c->last_serial = false;
+        WG_HIP(c, hipGetLastError());
+        wg_stage_end(c);
+        return WG_OK;
+    }
     int rc = replay_setup(c, run, nev, ev, aux, c->replay_nw);
     if (rc != WG_OK) return rc;
-    hipStream_t s = c->stream;
     wg_stage_begin(c, "lf_loop");
     if (c->use_serial() || run.nw > 16) {   // (past 1023 slots only the serial workgroup replays)
         DevBuf &rec = c->lf[LF_SERREC];
         WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev));
         WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));
         c->last_serial = true;
+        c->last_form = serial_form(run);
+        c->serial_done();
     } else {
         WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind < 2 ? 2u : c->replay_blind));
         c->last_serial = false;
+        c->last_form = 100u + run.nw;
     }
     if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
     c->lf_slot_of = run.sp_prev;
@@ -748,29 +922,36 @@ int wg_lf_replay_lanes_spec(wg_ctx *c, const LfRange &R, uint64_t nev, const uin
     return WG_OK;
 }
 
-void wg_lf_replay_spec_commit(wg_ctx *c, uint32_t it, uint32_t chunk, uint32_t max_lane, uint32_t n_slots, uint32_t first_still) {
+void wg_lf_replay_spec_commit(wg_ctx *c, const ReplayRun &run, uint32_t max_lane, uint32_t n_slots, uint32_t first_still,
+                              uint32_t positions, uint32_t leaks) {
+    if (run.dc) {
+        dc_commit(c, run, c->n_events, max_lane, n_slots, positions, leaks, first_still);
+        return;
+    }
     c->max_lane = max_lane;
     c->n_slots = n_slots;
     c->replay_nw = wg_ctx::nw_for_slots(n_slots);
-    c->replay_iters = it;
-    c->replay_adapt(first_still, chunk);
+    c->replay_iters = run.it;
+    c->replay_adapt(first_still, run.chunk);
     c->lane_path = 0;
 }
 
 static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint4 *ev, const uint32_t *aux, uint32_t *lane,
-                           uint32_t nw, bool *ok, bool *overflow) {
+                           uint32_t nw, bool *ok, bool *overflow, bool narrow, bool *was_narrow) {
     hipStream_t s = c->stream;
     *ok = false;
     *overflow = false;
     ReplayRun run;
-    int src = replay_setup(c, run, nev, ev, aux, nw);
+    int src = replay_setup(c, run, nev, ev, aux, nw, narrow);
     if (src != WG_OK) return src;
+    if (was_narrow) *was_narrow = c->use_serial() && (run.ser_w3 || run.ser_w8);
     if (c->use_serial() || nw > 16) {   // one exact pass: the scalars come with it (past 1023 slots: the only one)
         DevBuf &rec = c->lf[LF_SERREC];
         WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev));
         wg_stage_begin(c, "lf_loop");
         WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));
         c->last_serial = true;
+        c->last_form = serial_form(run);
         if (R.nl) hipLaunchKernelGGL(k_lf_lanes, dim3(blocks(R.nl)), dim3(T), 0, s, R.nl, lf_sp(c), run.sp_prev, lane);
         c->lf_slot_of = run.sp_prev;
         WG_HIP(c, hipGetLastError());
@@ -784,6 +965,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
         c->max_lane = (uint32_t)sc[0];
         c->n_slots = (uint32_t)sc[1];
         c->replay_nw = wg_ctx::nw_for_slots(c->n_slots);
+        c->serial_done();
         *ok = true;
         return WG_OK;
     }
@@ -794,6 +976,7 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
         run.serial_it = 1u + (uint32_t)(wg_ctx::serial_cost_us(nev, nw) / wg_ctx::WG_CHUNKED_ITER_US);
     wg_stage_begin(c, "lf_loop");
     c->last_serial = false;
+    c->last_form = 100u + nw;
     WG_HIP(c, wg_replay_start(c, s, run, c->replay_blind));
     const uint32_t blind = run.it;
     const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
@@ -818,9 +1001,13 @@ static int replay_lanes_at(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
         if (!conv) break;
     }
     wg_stage_end(c);
-    if (run.switched) {   // still moving at the short chunk: this list shape replays at the long one
-        c->replay_long = true;
+    if (run.switched) {   // still moving at the short chunk: this list shape takes the compacted replay (auto) or the long chunk
         c->replay_blind = 4;
+        if (c->replay_mode == 0 && c->replay_death) {
+            c->replay_dc = true;
+            return wg_lf_replay_lanes(c, R, nev, ev, aux, lane, ok);
+        }
+        c->replay_long = true;
         return replay_lanes_at(c, R, nev, ev, aux, lane, nw, ok, overflow);
     }
     if (run.to_serial) {  // still moving at the long chunk: this list shape replays serially
@@ -862,33 +1049,54 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     WG_ALLOC(c, aux, naux_cap * 4);
     hipStream_t s = c->stream;
     ReplayRun &run = c->spec_run;
-    run = ReplayRun{};
-    run.nev = nev_cap;
-    run.nw = c->replay_nw;
-    c->replay_geometry(&run.chunk, &run.warm);
-    const uint64_t nch = (nev_cap + run.chunk - 1) / run.chunk + 1;
-    run.max_iters = (uint32_t)nch + 1;
-    DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
-    DevBuf &rflags = c->lf[LF_RFLAGS];
-    WG_ALLOC(c, slot_a, (nev_cap + 64) * sizeof(uint16_t));
-    WG_ALLOC(c, slot_b, (nev_cap + 64) * sizeof(uint16_t));
-    WG_ALLOC(c, occ, (nch * 16 + 16) * run.nw);
-    WG_ALLOC(c, stats, nch * 8 + 8);
-    WG_ALLOC(c, rflags, (run.max_iters + 2) * 4);
-    run.ev = evrec.as<const uint4>();
-    run.aux = aux.as<const uint32_t>();
-    run.slots_a = slot_a.as<uint16_t>();
-    run.slots_b = slot_b.as<uint16_t>();
-    run.occ_a = occ.as<unsigned long long>();
-    run.occ_b = occ.as<unsigned long long>() + nch * run.nw;
-    run.stats = stats.as<uint32_t>();
-    run.flags = rflags.as<uint32_t>();
-    run.scal = c->lane_scalars.as<uint32_t>();
-    run.nev_dev = nev_dev;
-    run.gate = gate;
-    run.death = c->lf_death;
-    uint32_t blind = c->replay_blind < 2 ? 2u : c->replay_blind;
-    const WgReplayInit RI = wg_replay_prepare_spec(run, blind);
+    uint32_t blind;
+    WgReplayInit RI;
+    if (c->use_dc()) {   // the compacted replay (the flag words cleared by the event kernel)
+        int rc2 = dc_setup(c, run, nev_cap, evrec.as<const uint4>(), aux.as<const uint32_t>(), c->dc_nw ? c->dc_nw : 1u);
+        if (rc2 != WG_OK) return rc2;
+        run.nev_dev = nev_dev;
+        run.gate = gate;
+        run.death = c->lf_death;
+        blind = c->dc_blind < 2 ? 2u : c->dc_blind;
+        if (blind > run.max_iters) blind = run.max_iters;
+        WG_HIP(c, wg_dc_init(s, run, false));
+        RI.changed = run.flags;
+        RI.nflags = run.max_iters + 2;
+        RI.nev_dev = nev_dev;
+        RI.total = RI.nflags > 256 ? RI.nflags : 256;
+    } else {
+        run = ReplayRun{};
+        run.nev = nev_cap;
+        run.nw = c->replay_nw;
+        // (the serial pass's narrower forms, as replay_setup takes them)
+        const uint32_t hint = c->slots_hint();   // (wg_stage_lanes cleared n_slots)
+        run.ser_w8 = run.nw == 16 && hint > 0 && hint <= 448;
+        run.ser_w3 = run.nw == 4 && hint > 0 && hint <= 170;
+        c->replay_geometry(&run.chunk, &run.warm);
+        const uint64_t nch = (nev_cap + run.chunk - 1) / run.chunk + 1;
+        run.max_iters = (uint32_t)nch + 1;
+        DevBuf &slot_a = c->lf[LF_SLOT], &slot_b = c->lf[LF_SLOTB], &occ = c->lf[LF_OCC], &stats = c->lf[LF_STATS];
+        DevBuf &rflags = c->lf[LF_RFLAGS];
+        WG_ALLOC(c, slot_a, (nev_cap + 64) * sizeof(uint16_t));
+        WG_ALLOC(c, slot_b, (nev_cap + 64) * sizeof(uint16_t));
+        WG_ALLOC(c, occ, (nch * 16 + 16) * run.nw);
+        WG_ALLOC(c, stats, nch * 8 + 8);
+        WG_ALLOC(c, rflags, (run.max_iters + 2) * 4);
+        run.ev = evrec.as<const uint4>();
+        run.aux = aux.as<const uint32_t>();
+        run.slots_a = slot_a.as<uint16_t>();
+        run.slots_b = slot_b.as<uint16_t>();
+        run.occ_a = occ.as<unsigned long long>();
+        run.occ_b = occ.as<unsigned long long>() + nch * run.nw;
+        run.stats = stats.as<uint32_t>();
+        run.flags = rflags.as<uint32_t>();
+        run.scal = c->lane_scalars.as<uint32_t>();
+        run.nev_dev = nev_dev;
+        run.gate = gate;
+        run.death = c->lf_death;
+        blind = c->replay_blind < 2 ? 2u : c->replay_blind;
+        RI = wg_replay_prepare_spec(run, blind);
+    }
     wg_stage_begin(c, "lf_events");
     hipLaunchKernelGGL(k_lf_events<false>, dim3(blocks(n)), dim3(T), 0, s, R, 0u, 0u, (const uint32_t *)nullptr,
                        c->lf[LF_FIRST].as<const unsigned long long>(), c->lf[LF_WINFO].as<const uint32_t>(),
@@ -899,7 +1107,11 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     wg_stage_begin(c, "lf_loop");
-    if (c->use_serial() || run.nw > 16) {   // exact in one pass (the run then reads as converged at iteration 1)
+    if (run.dc) {
+        WG_HIP(c, wg_dc_iterate(s, run, blind));
+        WG_HIP(c, wg_dc_finish(s, run));
+        c->last_serial = false;
+    } else if (c->use_serial() || run.nw > 16) {   // exact in one pass (the run then reads as converged at iteration 1)
         DevBuf &rec = c->lf[LF_SERREC];
         WG_ALLOC(c, rec, wg_replay_serial_rec_bytes(nev_cap));
         WG_HIP(c, wg_replay_serial(s, run, rec.as<uint4>()));
@@ -920,7 +1132,9 @@ static int lanes_fast_spec(wg_ctx *c, const LfRange &R) {
 
 // The speculative lane build's validation words (WG_LANES_SPEC_ITEMS): {not
 // well formed, events, aux words, max_lane, slots, past the occupancy width,
-// changed at it - 1, changed at it, first iteration that changed nothing}.
+// changed at it - 1, changed at it, first iteration that changed nothing, and
+// for the compacted replay its positions + 1, leaks, more leaks than its
+// snapshots hold}.
 int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
     const uint64_t n = c->n;
     const uint32_t *ls = c->lane_scalars.as<const uint32_t>();
@@ -934,6 +1148,9 @@ int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
     it[6] = WgFetch{run.flags + run.it - 1, false};
     it[7] = WgFetch{run.flags + run.it, false};
     it[8] = WgFetch{ls + 3, false};   // first iteration that changed nothing
+    it[9] = WgFetch{ls + 4, false};
+    it[10] = WgFetch{ls + 5, false};
+    it[11] = WgFetch{ls + 6, false};
     return WG_LANES_SPEC_ITEMS;
 }
 
@@ -942,8 +1159,15 @@ int wg_lanes_spec_items(wg_ctx *c, WgFetch *it) {
 // n_slots, n_events, the replay's blind count are updated.
 bool wg_lanes_spec_check(wg_ctx *c, const uint64_t *v) {
     const bool conv = v[6] == 0 || v[7] == 0;
-    if (v[0] || v[5] || !conv) return false;
+    const ReplayRun &run = c->spec_run;
+    if (v[0] || v[5] || !conv || (run.dc && v[11])) return false;   // (the exact stages redo the lanes)
     c->n_events = v[1];
+    if (run.dc) {
+        dc_commit(c, run, v[1], (uint32_t)v[3], (uint32_t)v[4], (uint32_t)v[9], (uint32_t)v[10], (uint32_t)v[8]);
+        return true;
+    }
+    c->last_form = c->last_serial ? serial_form(run) : 100u + run.nw;
+    if (c->last_serial) c->serial_done();
     c->max_lane = (uint32_t)v[3];
     c->n_slots = (uint32_t)v[4];
     c->replay_nw = wg_ctx::nw_for_slots(c->n_slots);

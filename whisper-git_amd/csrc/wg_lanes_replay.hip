@@ -467,7 +467,7 @@ __global__ void k_lf_replay_init(uint64_t nchunks, unsigned long long *occ_prev,
 // the iterations the next build launches before its first check
 __device__ void replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats, uint32_t *__restrict__ scal,
                               const uint32_t *__restrict__ flags, uint32_t iters, uint32_t slot_cap,
-                              const uint32_t *__restrict__ nev_dev, uint32_t chunk) {
+                              const uint32_t *__restrict__ nev_dev, uint32_t chunk, bool dc) {
     const uint32_t lid = threadIdx.x;   // < 64
     uint32_t fp = ~0u;
     for (uint32_t i = 1 + lid; i <= iters; i += 64)
@@ -481,27 +481,34 @@ __device__ void replay_finish(uint64_t nchunks, const uint32_t *__restrict__ sta
         const uint64_t nd = ((uint64_t)*nev_dev + chunk - 1) / chunk;
         nchunks = nd < nchunks ? nd : nchunks;
     }
-    uint32_t ml = 0, ms = 0;
+    // (the compacted replay, wg_lanes_dchunk.hip: three words per record, the
+    // third the highest allocated position; an overflow reads 0xFFFF)
+    const uint32_t st = dc ? 3u : 2u;
+    uint32_t ml = 0, ms = 0, mp = 0;
     for (uint64_t c = lid; c < nchunks; c += 64) {
-        ml = stats[2 * c] > ml ? stats[2 * c] : ml;
-        ms = stats[2 * c + 1] > ms ? stats[2 * c + 1] : ms;
+        ml = stats[st * c] > ml ? stats[st * c] : ml;
+        ms = stats[st * c + 1] > ms ? stats[st * c + 1] : ms;
+        if (dc) mp = stats[st * c + 2] > mp ? stats[st * c + 2] : mp;
     }
     for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t a = (uint32_t)__shfl_down((int)ml, d, 64), b = (uint32_t)__shfl_down((int)ms, d, 64);
+        const uint32_t a = (uint32_t)__shfl_down((int)ml, d, 64), b = (uint32_t)__shfl_down((int)ms, d, 64),
+                       q = (uint32_t)__shfl_down((int)mp, d, 64);
         ml = a > ml ? a : ml;
         ms = b > ms ? b : ms;
+        mp = q > mp ? q : mp;
     }
     if (lid == 0) {
         scal[0] = ml;
         scal[1] = ms + 1;
-        scal[2] = ms >= slot_cap ? 1u : 0u;   // the sentinel slot was handed out: the occupancy overflowed
+        scal[2] = ms >= (dc ? 0xFFFFu : slot_cap) ? 1u : 0u;   // the sentinel slot was handed out: the occupancy overflowed
+        if (dc) scal[4] = mp + 1;
     }
 }
 
 __global__ void __launch_bounds__(64) k_lf_replay_finish(uint64_t nchunks, const uint32_t *__restrict__ stats,
                                                         uint32_t *__restrict__ scal, const uint32_t *__restrict__ flags,
-                                                        uint32_t iters, uint32_t slot_cap) {
-    replay_finish(nchunks, stats, scal, flags, iters, slot_cap, nullptr, 1u);
+                                                        uint32_t iters, uint32_t slot_cap, bool dc) {
+    replay_finish(nchunks, stats, scal, flags, iters, slot_cap, nullptr, 1u, dc);
 }
 
 // speculative fast path: the scalars (first wave of block 0), then per row the
@@ -513,9 +520,10 @@ __global__ void __launch_bounds__(256) k_lf_finish_lanes(uint64_t nchunks, const
                                                         uint32_t chunk, uint64_t nl, const uint32_t *__restrict__ sp,
                                                         const uint16_t *__restrict__ slot_of, uint32_t *__restrict__ lane,
                                                         uint32_t *__restrict__ lane_out, uint8_t *__restrict__ color_out,
-                                                        const uint8_t *__restrict__ flags, const uint32_t *__restrict__ gate) {
+                                                        const uint8_t *__restrict__ flags, const uint32_t *__restrict__ gate,
+                                                        bool dc) {
     if (*gate) return;   // not well formed: the exact stages redo the lanes
-    if (blockIdx.x == 0 && threadIdx.x < 64) replay_finish(nchunks, stats, scal, rflags, iters, slot_cap, nev_dev, chunk);
+    if (blockIdx.x == 0 && threadIdx.x < 64) replay_finish(nchunks, stats, scal, rflags, iters, slot_cap, nev_dev, chunk, dc);
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nl) return;
     const uint32_t l = slot_of[sp[j] & ~WG_TOK_EV];
@@ -556,7 +564,7 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
     if (R.max_iters > R.nch + 1) R.max_iters = (uint32_t)(R.nch + 1);
     if (R.nev == 0) {
         hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, (uint64_t)0, R.stats, R.scal, (const uint32_t *)R.flags, 0u,
-                           64u * R.nw - 1u);
+                           64u * R.nw - 1u, false);
         return hipGetLastError();
     }
     const uint64_t ninit = R.nch > R.max_iters + 1 ? R.nch : R.max_iters + 1;
@@ -577,7 +585,7 @@ hipError_t wg_replay_start(wg_ctx *c, hipStream_t s, ReplayRun &R, uint32_t blin
         std::swap(R.op, R.on);
     }
     hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it,
-                       64u * R.nw - 1u);
+                       64u * R.nw - 1u, false);
     return hipGetLastError();
 }
 
@@ -625,9 +633,9 @@ hipError_t wg_replay_iterate_spec(hipStream_t s, ReplayRun &R, uint32_t blind) {
 hipError_t wg_replay_finish_lanes(hipStream_t s, const ReplayRun &R, uint64_t nl, const uint32_t *sp, uint32_t *lane,
                                   uint32_t *lane_out, uint8_t *color_out, const uint8_t *flags) {
     const uint64_t g = nl ? (nl + 255) / 256 : 1;
-    hipLaunchKernelGGL(k_lf_finish_lanes, dim3((uint32_t)g), dim3(256), 0, s, R.nch, (const uint32_t *)R.stats, R.scal,
-                       (const uint32_t *)R.flags, R.it, 64u * R.nw - 1u, R.nev_dev, R.chunk, nl, sp,
-                       (const uint16_t *)R.sp_prev, lane, lane_out, color_out, flags, R.gate);
+    hipLaunchKernelGGL(k_lf_finish_lanes, dim3((uint32_t)g), dim3(256), 0, s, R.dc ? R.dc_blocks : R.nch, (const uint32_t *)R.stats,
+                       R.scal, (const uint32_t *)R.flags, R.it, 64u * R.nw - 1u, R.nev_dev, R.dc ? WG_DC_FIX_T : R.chunk, nl, sp,
+                       (const uint16_t *)R.sp_prev, lane, lane_out, color_out, flags, R.gate, R.dc);
     return hipGetLastError();
 }
 
@@ -665,7 +673,7 @@ hipError_t wg_replay_resume(wg_ctx *c, hipStream_t s, ReplayRun &R, bool *conver
     }
     if (R.nev)
         hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.nch, R.stats, R.scal, (const uint32_t *)R.flags, R.it,
-                           64u * R.nw - 1u);
+                           64u * R.nw - 1u, false);
     return hipGetLastError();
 }
 
@@ -680,3 +688,10 @@ extern "C" int wg_debug_replay_profile(unsigned long long *out, int reset) {
     return WG_OK;
 }
 #endif
+
+// the scalars of a compacted replay (wg_lanes_dchunk.hip) after wg_dc_finish
+hipError_t wg_dc_scalars(hipStream_t s, const ReplayRun &R) {
+    hipLaunchKernelGGL(k_lf_replay_finish, dim3(1), dim3(64), 0, s, R.dc_blocks, R.stats, R.scal, (const uint32_t *)R.flags, R.it,
+                       0xFFFFu, true);
+    return hipGetLastError();
+}

@@ -31,11 +31,11 @@
 // The one-wave kernel is bound by its instruction issue: 8 instructions per
 // event (profiles/microbench/chain_latency.hip, serial_replay.hip).
 #include "wg_internal.h"
+#include "wg_lanes_dstep.h"
 
 namespace {
 
 enum : uint32_t { F_A = 1u, F_O = 2u, F_C = 4u, F_M = 8u };
-constexpr uint32_t WG_SER_INF = 0x7FFFFFFFu;
 constexpr int SER_PAD = 128;   // no-op records after the last event (the last batch and the prefetch)
 
 // Per event record rec[k] = {lo, wid, dv, 0}: lanes with D - lo < wid are
@@ -73,49 +73,25 @@ __global__ void k_ser_death(uint64_t nev_cap, const uint32_t *__restrict__ nev_d
     const uint4 r = ev[k];
     if (!(r.x & F_C)) return;
     const uint32_t t = (uint32_t)k + 1u;
-    if (r.x & F_M) {
+    if (r.x & F_M) {   // (a token past the events is not written through)
         const uint32_t n = aux[r.w];
-        for (uint32_t q = 0; q < n; q++) rec[aux[r.w + 1 + q]].z = t;
+        for (uint32_t q = 0; q < n; q++) {
+            const uint32_t tk = aux[r.w + 1 + q];
+            if (tk < nev) rec[tk].z = t;
+        }
     } else {
-        rec[r.y].z = t;
-        rec[r.z].z = t;
+        if (r.y < nev) rec[r.y].z = t;
+        if (r.z < nev) rec[r.z].z = t;
     }
 }
 
 // ---- the one-wave replay, up to 63 slots (slot 63 is the sentinel) --------
-// One event: T = D - lo, the lanes with T < wid, the lowest into M0, its D :=
-// dv, the output lane j := it.  A single wave issues about one instruction
-// per 6-9 cycles (profiles/microbench/chain_latency.hip), so the step is its
-// instruction count: these five plus the three v_readlane of the record (the
-// batch's records sit one per lane, loaded a batch ahead: scalar loads return
-// out of order and any wait for one waits for all).  Software-pipelining the
-// next event's compare ahead of this lane write needs a scalar patch and a
-// fourth record word: 12 instructions, slower (profiles/r04_serial_variants.md).
-template <int J>
-__device__ __forceinline__ void ser_step1(uint32_t &D, uint32_t &out, uint32_t lo, uint32_t wid, uint32_t dv) {
-    uint32_t T;
-    uint64_t M;
-    asm volatile(
-        "v_subrev_u32 %[T], %[lo], %[D]\n\t"
-        "v_cmp_gt_u32_e64 %[M], %[wid], %[T]\n\t"
-        "s_ff1_i32_b64 m0, %[M]\n\t"
-        "v_writelane_b32 %[D], %[dv], m0\n\t"
-        "v_writelane_b32 %[o], m0, %[j]"
-        : [D] "+v"(D), [o] "+v"(out), [M] "=&s"(M), [T] "=&v"(T)
-        : [lo] "s"(lo), [wid] "s"(wid), [dv] "s"(dv), [j] "n"(J)
-        : "m0", "scc");
-}
-
-template <int J>
-__device__ __forceinline__ void ser_quad1(uint32_t &D, uint32_t &out, const uint4 &R) {
-#define WG_SER_RL(v, j) (uint32_t)__builtin_amdgcn_readlane((int)(v), (j))
-    ser_step1<J + 0>(D, out, WG_SER_RL(R.x, J + 0), WG_SER_RL(R.y, J + 0), WG_SER_RL(R.z, J + 0));
-    ser_step1<J + 1>(D, out, WG_SER_RL(R.x, J + 1), WG_SER_RL(R.y, J + 1), WG_SER_RL(R.z, J + 1));
-    ser_step1<J + 2>(D, out, WG_SER_RL(R.x, J + 2), WG_SER_RL(R.y, J + 2), WG_SER_RL(R.z, J + 2));
-    ser_step1<J + 3>(D, out, WG_SER_RL(R.x, J + 3), WG_SER_RL(R.y, J + 3), WG_SER_RL(R.z, J + 3));
-#undef WG_SER_RL
-}
-
+// The D-step of wg_lanes_dstep.h: the batch's records sit one per lane, loaded
+// a batch ahead (scalar loads return out of order and any wait for one waits
+// for all).  Software-pipelining the next event's compare ahead of this lane
+// write needs a scalar patch and a fourth record word: 12 instructions,
+// slower (profiles/r04_serial_variants.md).
+//
 // the batch's outputs: slots, and the running maxima (occupying events /
 // allocations; a slot at the sentinel or beyond is an overflow)
 __device__ __forceinline__ void ser_flush(uint64_t base, uint64_t nev, uint32_t lane, uint32_t x, const uint4 *__restrict__ ev,
@@ -178,99 +154,9 @@ __global__ void __launch_bounds__(64) k_ser_replay1(const uint4 *__restrict__ re
     ser_finish(lane, ml, ms, ovf, 63u, stats, flags, scal);
 }
 
-// ---- wider occupancies (64 NW - 1 slots, NW = 4 or 16): slot 64 w + l is
-// lane l of word w; per event one compare per word, the lowest selected slot
-// over the words (s_ff1 of each word, tagged with the word, unsigned minimum:
-// an empty word's -1 stays the largest), the lane write by compare + select on
-// every word (its word is not a compile-time register).  Records as the
+// ---- wider occupancies (64 NW - 1 slots, NW = 3, 4, 8 or 16): slot 64 w + l
+// is lane l of word w (ser_step_w, wg_lanes_dstep.h).  Records as the
 // one-word kernel's: a batch per lane, read out with v_readlane.
-template <int NW>
-__device__ __forceinline__ uint32_t ser_first_w(const uint64_t (&m)[NW]);
-template <>
-__device__ __forceinline__ uint32_t ser_first_w<4>(const uint64_t (&m)[4]) {
-    uint32_t x, f1, f2, f3;   // (wave-uniform scalar arithmetic kept in one asm block: the
-                              // compiler takes asm results for divergent and would move it to VALU)
-    asm volatile(
-        "s_ff1_i32_b64 %[x], %[m0]\n\t"
-        "s_ff1_i32_b64 %[f1], %[m1]\n\t"
-        "s_ff1_i32_b64 %[f2], %[m2]\n\t"
-        "s_ff1_i32_b64 %[f3], %[m3]\n\t"
-        "s_or_b32 %[f1], %[f1], 64\n\t"
-        "s_or_b32 %[f2], %[f2], 0x80\n\t"
-        "s_or_b32 %[f3], %[f3], 0xc0\n\t"
-        "s_min_u32 %[x], %[x], %[f1]\n\t"
-        "s_min_u32 %[f2], %[f2], %[f3]\n\t"
-        "s_min_u32 %[x], %[x], %[f2]"
-        : [x] "=&s"(x), [f1] "=&s"(f1), [f2] "=&s"(f2), [f3] "=&s"(f3)
-        : [m0] "s"(m[0]), [m1] "s"(m[1]), [m2] "s"(m[2]), [m3] "s"(m[3])
-        : "scc");
-    return x;
-}
-template <>
-__device__ __forceinline__ uint32_t ser_first_w<3>(const uint64_t (&m)[3]) {
-    uint32_t x, f1, f2;   // (as the four-word form)
-    asm volatile(
-        "s_ff1_i32_b64 %[x], %[m0]\n\t"
-        "s_ff1_i32_b64 %[f1], %[m1]\n\t"
-        "s_ff1_i32_b64 %[f2], %[m2]\n\t"
-        "s_or_b32 %[f1], %[f1], 64\n\t"
-        "s_or_b32 %[f2], %[f2], 0x80\n\t"
-        "s_min_u32 %[x], %[x], %[f1]\n\t"
-        "s_min_u32 %[x], %[x], %[f2]"
-        : [x] "=&s"(x), [f1] "=&s"(f1), [f2] "=&s"(f2)
-        : [m0] "s"(m[0]), [m1] "s"(m[1]), [m2] "s"(m[2])
-        : "scc");
-    return x;
-}
-template <>
-__device__ __forceinline__ uint32_t ser_first_w<8>(const uint64_t (&m)[8]) {
-    uint32_t x = 0xFFFFFFFFu;
-#pragma unroll
-    for (int w = 7; w >= 0; w--) {
-        uint32_t f;
-        asm volatile("s_ff1_i32_b64 %[f], %[m]\n\t"
-                     "s_or_b32 %[f], %[f], %[tag]\n\t"
-                     "s_min_u32 %[x], %[x], %[f]"
-                     : [x] "+s"(x), [f] "=&s"(f) : [m] "s"(m[w]), [tag] "n"(64 * w) : "scc");
-    }
-    return x;
-}
-template <>
-__device__ __forceinline__ uint32_t ser_first_w<16>(const uint64_t (&m)[16]) {
-    uint32_t x = 0xFFFFFFFFu;
-#pragma unroll
-    for (int w = 15; w >= 0; w--) {
-        uint32_t f;
-        asm volatile("s_ff1_i32_b64 %[f], %[m]\n\t"
-                     "s_or_b32 %[f], %[f], %[tag]\n\t"
-                     "s_min_u32 %[x], %[x], %[f]"
-                     : [x] "+s"(x), [f] "=&s"(f) : [m] "s"(m[w]), [tag] "n"(64 * w) : "scc");
-    }
-    return x;
-}
-
-template <int NW, int J>
-__device__ __forceinline__ void ser_step_w(uint32_t (&D)[NW], uint32_t &out, uint32_t lane, uint32_t lo, uint32_t wid,
-                                           uint32_t dv) {
-    uint64_t m[NW];
-#pragma unroll
-    for (int w = 0; w < NW; w++) m[w] = __ballot(D[w] - lo < wid);
-    const uint32_t x = ser_first_w<NW>(m);   // 0xFFFFFFFF: nothing selected (an overflow)
-#pragma unroll
-    for (int w = 0; w < NW; w++) D[w] = (lane + 64u * w == x) ? dv : D[w];
-    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(out) : "s"(x), "n"(J));
-}
-
-template <int NW, int J>
-__device__ __forceinline__ void ser_quad_w(uint32_t (&D)[NW], uint32_t &out, uint32_t lane, const uint4 &R) {
-#define WG_SER_RL(v, j) (uint32_t)__builtin_amdgcn_readlane((int)(v), (j))
-    ser_step_w<NW, J + 0>(D, out, lane, WG_SER_RL(R.x, J + 0), WG_SER_RL(R.y, J + 0), WG_SER_RL(R.z, J + 0));
-    ser_step_w<NW, J + 1>(D, out, lane, WG_SER_RL(R.x, J + 1), WG_SER_RL(R.y, J + 1), WG_SER_RL(R.z, J + 1));
-    ser_step_w<NW, J + 2>(D, out, lane, WG_SER_RL(R.x, J + 2), WG_SER_RL(R.y, J + 2), WG_SER_RL(R.z, J + 2));
-    ser_step_w<NW, J + 3>(D, out, lane, WG_SER_RL(R.x, J + 3), WG_SER_RL(R.y, J + 3), WG_SER_RL(R.z, J + 3));
-#undef WG_SER_RL
-}
-
 template <int NW>
 __global__ void __launch_bounds__(64) k_ser_replay_w(const uint4 *__restrict__ rec, const uint4 *__restrict__ ev,
                                                      uint64_t nev_cap, const uint32_t *__restrict__ nev_dev,

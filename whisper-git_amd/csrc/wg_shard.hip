@@ -679,13 +679,14 @@ static int sh_fallback(wg_ctx *c, wg_shard_msg *out) {
 
 // the speculative X3 replay's words, checked with the local geometry's
 // validation read: {flags[it - 1], flags[it], max_lane, slots, overflow, first
-// iteration that changed nothing}
-constexpr int SH_REPLAY_ITEMS = 6;
+// iteration that changed nothing, and for the compacted replay the positions
+// + 1, the leaks, more leaks than its snapshots hold}
+constexpr int SH_REPLAY_ITEMS = 9;
 static int sh_replay_items(wg_ctx *c, WgFetch *it) {
     const ShardState &S = c->sh;
     it[0] = WgFetch{S.rp_it ? S.rp_flags + S.rp_it - 1 : S.rp_flags, false};
     it[1] = WgFetch{S.rp_flags + S.rp_it, false};
-    for (int k = 0; k < 4; k++) it[2 + k] = WgFetch{S.rp_scal + k, false};
+    for (int k = 0; k < 7; k++) it[2 + k] = WgFetch{S.rp_scal + k, false};
     return SH_REPLAY_ITEMS;
 }
 
@@ -722,8 +723,14 @@ static int sh_replay_check(wg_ctx *c, const uint64_t *w, bool *redo, bool *fallb
     *redo = *fallback = false;
     S.replay_pending = false;
     const bool conv = S.rp_it == 0 || w[0] == 0 || w[1] == 0;
-    if (conv && !w[4]) {
-        wg_lf_replay_spec_commit(c, S.rp_it, S.rp_chunk, (uint32_t)w[2], (uint32_t)w[3], (uint32_t)w[5]);
+    if (conv && !w[4] && !(S.rp_dc && w[8])) {
+        ReplayRun run;
+        run.it = S.rp_it;
+        run.chunk = S.rp_chunk;
+        run.dc = S.rp_dc;
+        run.nw = S.rp_nw;
+        run.warm = S.rp_warm;
+        wg_lf_replay_spec_commit(c, run, (uint32_t)w[2], (uint32_t)w[3], (uint32_t)w[5], (uint32_t)w[6], (uint32_t)w[7]);
         sh_graph_width(c);
         return WG_OK;
     }
@@ -977,6 +984,7 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
     }
     c->n = N;
     c->e_refs = S.Etot;
+    c->replay_shape(N);   // (the whole list's length: every rank makes the same replay choices)
     hipStream_t st = c->stream;
     S.rt_fresh = false;
     S.build_band = nullptr;
@@ -1356,6 +1364,9 @@ int wg_shard_exchange(wg_ctx *c, const void *gathered, uint64_t stride, const ui
             S.rp_chunk = run.chunk;
             S.rp_flags = run.flags;
             S.rp_scal = run.scal;
+            S.rp_dc = run.dc;
+            S.rp_nw = run.nw;
+            S.rp_warm = run.warm;
             sh_lane_out(c);
             sh_end_lanes(c);
         } else {

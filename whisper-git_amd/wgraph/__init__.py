@@ -194,8 +194,14 @@ class Engine:
 
     def set_replay_mode(self, mode: int):
         """WG_OPT_REPLAY_MODE: 0 auto, 1 the chunked fixed-point replay, 2 the
-        single-wave serial replay (speed only; results identical)."""
+        single-wave serial replay, 3 the compacted fixed point (leaked slots
+        struck out; speed only, results identical)."""
         self._check(lib().wg_set_option(self._ctx, 8, int(mode)))
+
+    def set_dc_warmup(self, events: int):
+        """WG_OPT_DC_WARMUP: the compacted replay's first-iteration warm-up
+        (events, a multiple of 64; 0 = auto)."""
+        self._check(lib().wg_set_option(self._ctx, 10, int(events)))
 
     def set_slice_lists(self, mode: int):
         """WG_OPT_SLICE_LISTS: a deferred-validation build leaves its geometry
@@ -556,6 +562,11 @@ class Engine:
 
     # -- timing ----------------------------------------------------------------------------
     def debug_counters(self) -> np.ndarray:
+        """wg_debug_counters: [3] replay iterations, [4] events, [5] shard mode,
+        [6..8] speculative builds / lanes redone / geometry redone, [9] sharded
+        blind replays, [10] serial pass, [11] sliced emissions, [12] the
+        replay's form (100 + words chunked, 200 + words serial, 300 + words
+        compacted), [13] leaked slots struck out, [14] its warm-up."""
         out = np.zeros(16, np.uint32)
         self._check(lib().wg_debug_counters(self._ctx, out.ctypes.data, 16))
         return out
