@@ -61,6 +61,8 @@ def parse():
                     help="gloo rehearsal: move HIP-resident slots through gloo (the stream-ordered slot path of RCCL)")
     ap.add_argument("--no-defer", action="store_true",
                     help="validate every speculative build before build() returns (WG_OPT_DEFER_VALIDATION off)")
+    ap.add_argument("--join-fused", action="store_true",
+                    help="the id table's place pass inside the window probe, settle on the main stream (A/B; default: beside it)")
     ap.add_argument("--slice", action="store_true",
                     help="row-slice the geometry lists under the emission (WG_OPT_SLICE_LISTS 1; default off)")
     ap.add_argument("--no-build-frame", action="store_true",
@@ -362,6 +364,7 @@ def config_rates(eng, dev, torch, args):
         eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         eng.set_defer_validation(not args.no_defer)
         eng.set_slice_lists(1 if args.slice else 0)
+        eng.set_join_fused(args.join_fused)
         d = synth.generate(kind, n)
         keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
                                                        d.parent_oid.reshape(-1), d.flags, d.band)]
@@ -432,6 +435,7 @@ def build_lifecycle(dag, dev, torch, args, pal):
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     eng.set_defer_validation(not args.no_defer)
     eng.set_slice_lists(1 if args.slice else 0)
+    eng.set_join_fused(args.join_fused)
 
     def step(k, c, n):
         torch.cuda.synchronize()
@@ -539,6 +543,7 @@ def main():
     # host wait per step, while the emission runs) instead of mid-step
     eng.set_defer_validation(not args.no_defer)
     eng.set_slice_lists(1 if args.slice else 0)
+    eng.set_join_fused(args.join_fused)
     pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
     selected = shard0 + 7
     comm = None

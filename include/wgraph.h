@@ -254,6 +254,10 @@ int         wg_synchronize(wg_ctx *ctx);
  * (a multiple of 64 in 64..1048576; 0 = auto, the default: 8192, doubled up
  * to 32768 while the fixed point comes late).  Speed only, never results. */
 #define WG_OPT_DC_WARMUP 10
+/* WG_OPT_JOIN_FUSED: 1 = the id table's place pass rides on the window
+ * probe and its settle pass follows on the build's stream; 0 (default) = the
+ * table is built on the side stream beside the probe.  Speed only. */
+#define WG_OPT_JOIN_FUSED 11
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------

@@ -171,8 +171,9 @@ int wg_side_build_begin(wg_ctx *c, uint64_t m, float *h, float *rt, const float 
         const hipError_t e = hipEventCreateWithFlags(&c->ev_hash, hipEventDisableTiming | wg_event_scope());
         if (e != hipSuccess) rc = wg_fail(c, WG_E_HIP, "event: %s", hipGetErrorString(e));
     }
-    if (rc == WG_OK) rc = wg_hash_table_launch(c);
-    if (rc == WG_OK) {
+    // (the fused join builds its table on the main stream, wg_stage_hash_join)
+    if (rc == WG_OK && !c->join_fused) rc = wg_hash_table_launch(c);
+    if (rc == WG_OK && !c->join_fused) {
         const hipError_t e = hipEventRecord(c->ev_hash, c->stream);
         if (e != hipSuccess) rc = wg_fail(c, WG_E_HIP, "event: %s", hipGetErrorString(e));
         c->hash_on_side = true;
@@ -504,6 +505,9 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         WG_SETTLE(c);
         c->slice_on = value != 0;
         c->slice_min_rows = value == 2 ? 4 * WG_SWEEP_CH : 1ull << 18;
+        return WG_OK;
+    case WG_OPT_JOIN_FUSED:
+        c->join_fused = value != 0;
         return WG_OK;
     case WG_OPT_DC_WARMUP:
         if (value < 0 || value > (1 << 20) || (value & 63)) return wg_fail(c, WG_E_INVALID, "warm-up must be a multiple of 64 in 0..2^20");

@@ -103,10 +103,20 @@ constexpr int NR = NR_LO + T + PROBE_WIN + 1;        // rows b - 63 .. b + 320
 constexpr int NH = 1024;                             // LDS table slots (>= 2.5 x NR)
 __device__ __forceinline__ uint32_t near_slot(uint32_t fp) { return (fp * 0x9E3779B1u) >> 22; }
 
+// (fused join, r05) place: the table's place pass rides on the staging of
+// the block's own rows — their ids are loaded anyway — and the next build's
+// table is emptied here unless a long list's emission does it
+struct NearPlace {
+    unsigned long long *table = nullptr;   // null: the table is built elsewhere (side stream)
+    uint64_t mask = 0;
+    unsigned long long *next_table = nullptr;
+    uint64_t next_words = 0;
+};
+
 __global__ void __launch_bounds__(T) k_probe_near(const uint8_t *__restrict__ oid, uint64_t n,
                                                   const uint32_t *__restrict__ poff, const uint8_t *__restrict__ poid,
                                                   int32_t *__restrict__ prow, uint32_t *__restrict__ edge_cnt,
-                                                  uint8_t *__restrict__ rowmiss, LfClear L) {
+                                                  uint8_t *__restrict__ rowmiss, LfClear L, NearPlace P) {
     __shared__ uint32_t wkey[NR * 5];
     __shared__ uint32_t htab[NH];                    // staged row index + 1, 0 empty
     __shared__ unsigned long long fr[T];
@@ -117,6 +127,8 @@ __global__ void __launch_bounds__(T) k_probe_near(const uint8_t *__restrict__ oi
     fr[threadIdx.x] = REF_NONE;
     fc[threadIdx.x] = 0u;
     __syncthreads();
+    for (uint64_t w = (uint64_t)blockIdx.x * T + threadIdx.x; w < P.next_words; w += (uint64_t)gridDim.x * T)
+        P.next_table[w] = HEMPTY;
     for (int t = threadIdx.x; t < NR; t += T) {
         const int64_t r = r0 + t;
         if (r < 0 || (uint64_t)r >= n) continue;
@@ -125,6 +137,8 @@ __global__ void __launch_bounds__(T) k_probe_near(const uint8_t *__restrict__ oi
         for (int w = 0; w < 5; w++) wkey[t * 5 + w] = k.w[w];
         uint32_t h = near_slot(key_fp(k));
         while (atomicCAS(&htab[h], 0u, (uint32_t)t + 1u) != 0u) h = (h + 1u) & (NH - 1u);
+        if (P.table && (uint64_t)r >= b && (uint64_t)r < b + T)   // the place pass for the block's own rows
+            P.table[key_hash(k) & P.mask] = ((unsigned long long)key_fp(k) << 32) | (uint32_t)r;
     }
     __syncthreads();
     for (int t = threadIdx.x; t < T + PROBE_WIN; t += T) {
@@ -247,37 +261,51 @@ __global__ void __launch_bounds__(WG_BS_THREADS) k_probe_fix(const uint8_t *__re
 
 }  // namespace
 
-// The table build (place + settle): on the side stream when the build
-// forks one (wg_side_build_begin: it overlaps the window probe), else inline
-int wg_hash_table_launch(wg_ctx *c) {
+// The table's buffers for this build: two tables used in turn (the next
+// build's emptied by this build's place pass, or by a long list's emission
+// beside its tiles when `later`); the current one is emptied first if it is
+// not known empty.
+static int hash_table_prepare(wg_ctx *c, unsigned long long **table, unsigned long long **next, uint64_t *words, bool *later) {
     const uint64_t n = c->n;
     uint64_t cap = 1024;
     while (cap < 2 * n) cap <<= 1;
     c->hcap = cap;
-    const uint64_t words = cap + 1;   // the table, then the duplicate flag word (all ones = none)
+    *words = cap + 1;   // the table, then the duplicate flag word (all ones = none)
     const int t = c->htab_cur, o = t ^ 1;
     for (int k : {t, o}) {
-        if (c->htab[k].cap < words * 8 + 64) c->htab_clean[k] = 0;   // (re)allocated below: not known empty
-        WG_ALLOC(c, c->htab[k], words * 8 + 64);
+        if (c->htab[k].cap < *words * 8 + 64) c->htab_clean[k] = 0;   // (re)allocated below: not known empty
+        WG_ALLOC(c, c->htab[k], *words * 8 + 64);
     }
-    unsigned long long *table = c->htab[t].as<unsigned long long>();
-    if (c->htab_clean[t] < words) WG_HIP(c, hipMemsetAsync(table, 0xFF, words * 8, c->stream));
-    uint32_t *dup = reinterpret_cast<uint32_t *>(table + cap);
-    if (n) {
-        const uint32_t g = (uint32_t)((n + T - 1) / T);
-        // the next build's table is emptied here, unless a long list's
-        // emission will (wg_hash_clear_next, beside its tiles: 8 bytes per
-        // slot off the build's critical path)
-        const bool later = c->defer_validation && !c->sh.on && n >= c->slice_min_rows;
-        hipLaunchKernelGGL(k_hash_place, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1,
-                           c->htab[o].as<unsigned long long>(), later ? 0ull : words, LfClear{});
-        if (!later) c->htab_clean[o] = words;
-        hipLaunchKernelGGL(k_hash_settle, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1, dup);
-    }
+    *table = c->htab[t].as<unsigned long long>();
+    *next = c->htab[o].as<unsigned long long>();
+    if (c->htab_clean[t] < *words) WG_HIP(c, hipMemsetAsync(*table, 0xFF, *words * 8, c->stream));
+    // the next build's table is emptied by this build, unless a long list's
+    // emission will (wg_hash_clear_next, beside its tiles: 8 bytes per slot
+    // off the build's critical path)
+    *later = c->defer_validation && !c->sh.on && n >= c->slice_min_rows;
+    if (!*later) c->htab_clean[o] = *words;
     c->htab_clean[t] = 0;
     c->htab_cur = o;
-    c->htab_last = table;
-    c->hash_table = table;
+    c->htab_last = *table;
+    c->hash_table = *table;
+    return WG_OK;
+}
+
+// The table build (place + settle): on the side stream when the build
+// forks one (wg_side_build_begin: it overlaps the window probe), else inline
+int wg_hash_table_launch(wg_ctx *c) {
+    const uint64_t n = c->n;
+    unsigned long long *table = nullptr, *next = nullptr;
+    uint64_t words = 0;
+    bool later = false;
+    if (const int rc = hash_table_prepare(c, &table, &next, &words, &later)) return rc;
+    uint32_t *dup = reinterpret_cast<uint32_t *>(table + c->hcap);
+    if (n) {
+        const uint32_t g = (uint32_t)((n + T - 1) / T);
+        hipLaunchKernelGGL(k_hash_place, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, c->hcap - 1, next,
+                           later ? 0ull : words, LfClear{});
+        hipLaunchKernelGGL(k_hash_settle, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, c->hcap - 1, dup);
+    }
     c->hash_built = true;
     WG_HIP(c, hipGetLastError());
     return WG_OK;
@@ -303,10 +331,26 @@ int wg_stage_hash_join(wg_ctx *c) {
     WG_ALLOC(c, c->bsum, 3 * (wg_bs_blocks(n) + 64) * 4);
     { const int _sr = wg_scan_reserve(c, n + 1); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "hash_join");
-    // the table: built on the side stream already (joined below), or here
+    // the table: built on the side stream already (joined below), or here —
+    // fused (c->join_fused, r05): its place pass inside the window probe, the
+    // settle pass between the probe and the fix-up, all on this stream
     const bool side = c->hash_built && c->hash_on_side;
-    if (!c->hash_built)
-        if (const int rc = wg_hash_table_launch(c)) return rc;
+    NearPlace P;
+    bool fused = false;
+    if (!c->hash_built) {
+        if (c->join_fused && n) {
+            unsigned long long *next = nullptr;
+            uint64_t words = 0;
+            bool later = false;
+            if (const int rc = hash_table_prepare(c, &P.table, &next, &words, &later)) return rc;
+            P.mask = c->hcap - 1;
+            P.next_table = next;
+            P.next_words = later ? 0ull : words;
+            fused = true;
+        } else if (const int rc = wg_hash_table_launch(c)) {
+            return rc;
+        }
+    }
     c->hash_built = false;
     c->hash_on_side = false;
     const uint64_t cap = c->hcap;
@@ -334,7 +378,10 @@ int wg_stage_hash_join(wg_ctx *c) {
             L.scal = c->lane_scalars.as<uint32_t>();
         }
         hipLaunchKernelGGL(k_probe_near, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
-                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->rowmiss.as<uint8_t>(), L);
+                           c->prow.as<int32_t>(), c->edge_cnt.as<uint32_t>(), c->rowmiss.as<uint8_t>(), L, P);
+        if (fused)
+            hipLaunchKernelGGL(k_hash_settle, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, table, cap - 1,
+                               reinterpret_cast<uint32_t *>(table + cap));
         if (side) WG_HIP(c, hipStreamWaitEvent(c->stream, c->ev_hash, 0));
         hipLaunchKernelGGL(k_probe_fix, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
                            (const unsigned long long *)table, cap - 1, dup, c->canon.as<uint32_t>(), c->prow.as<int32_t>(),

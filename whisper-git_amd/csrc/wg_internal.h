@@ -313,6 +313,9 @@ struct wg_ctx {
     DevBuf canon;           // uint32 [N]  last row holding the same id
     DevBuf rowmiss;         // uint8  [N]  a reference of the row missed the window probe (wg_hash.hip)
     unsigned long long *hash_table = nullptr;   // the table of this build (wg_hash_table_launch)
+    // WG_OPT_JOIN_FUSED: the table's place pass in the window probe, settle on the main stream (r05 A/B on
+    // wide16 1M: 1.438 / 1.444 ms/step against 1.434 / 1.434 with the table beside the probe: off)
+    bool join_fused = false;
     bool hash_built = false, hash_on_side = false;   // ... launched already (on the side stream)
     DevBuf prow;            // int32  [E]  canonical parent row or -1
     // lanes
@@ -384,7 +387,15 @@ struct wg_ctx {
         return (double)nev * (nw <= 1 ? 0.016 : nw <= 2 ? 0.04 : nw <= 4 ? 0.07 : nw <= 16 ? 0.3 : 1.0);
     }
     static constexpr double WG_CHUNKED_ITER_US = 60.0;
-    static constexpr double WG_DC_ITER_US = 15.0;   // a compacted iteration after the first (128-256 events per chunk)
+    // The compacted replay's cost model (us): one wave replays an event in
+    // about 25 / 40 / 72 ns at 1 / 2 / 4 words of positions (the D-step's
+    // instruction count, profiles/r05_dc_*); iteration 1 replays warm + chunk
+    // events per wave, every later one chunk events plus a launch.
+    static double dc_step_us(uint32_t nw) { return nw <= 1 ? 0.025 : nw <= 2 ? 0.04 : 0.072; }
+    static double dc_iter_us(uint32_t nw, uint32_t chunk) { return chunk * dc_step_us(nw) + 5.0; }
+    static double dc_cost_us(uint32_t nw, uint32_t warm, uint32_t chunk, uint32_t fp) {
+        return (warm + chunk) * dc_step_us(nw) + (fp > 1 ? fp - 1 : 0) * dc_iter_us(nw, chunk);
+    }
     // a list of a very different length: the auto choices start over
     void replay_shape(uint64_t rows) {
         if (mode_rows && (rows > 2 * mode_rows || 2 * rows < mode_rows)) {
@@ -392,6 +403,8 @@ struct wg_ctx {
             replay_serial = false;
             replay_dc = false;
             dc_warm = dc_warm_fixed ? dc_warm_fixed : WG_DC_WARM0;
+            dc_probe = false;
+            dc_warm_frozen = false;
             dc_blind = 2;
             replay_blind = 4;
         }
@@ -403,22 +416,40 @@ struct wg_ctx {
         if (++serial_builds >= WG_SERIAL_RETRY) {
             replay_serial = false;
             replay_dc = true;
-            dc_warm = dc_warm_fixed ? dc_warm_fixed : WG_DC_WARM_MAX;
+            dc_warm = dc_warm_fixed ? dc_warm_fixed : WG_DC_WARM0;
+            dc_probe = false;
             dc_blind = 2;
             serial_builds = 0;
         }
     }
-    // a compacted replay that reached its fixed point at iteration fp: the
-    // next one's warm-up, blind count, or the serial pass
-    void dc_adapt(uint32_t fp, uint64_t nev, uint32_t positions) {
+    // A compacted replay (nw words, its warm-up and chunk) that reached its
+    // fixed point at iteration fp: the serial pass when the model prices the
+    // serial pass lower (auto); else a fixed point later than iteration 3
+    // tries a doubled warm-up once (kept only if the model prices it lower:
+    // long-lived lanes need more than any affordable warm-up); the blind count.
+    bool dc_probe = false;         // the last compacted replay tried a doubled warm-up
+    bool dc_warm_frozen = false;   // ... and it did not pay
+    double dc_cost_before = 0;     // the modelled cost before that probe
+    void dc_adapt(uint32_t fp, uint64_t nev, uint32_t nw, uint32_t warm, uint32_t chunk, uint32_t serial_nw) {
         if (fp == 0) return;
-        if (replay_mode == 0 && fp > 2 &&
-            (double)(fp - 1) * WG_DC_ITER_US > serial_cost_us(nev, positions < 64 ? 1u : positions < 256 ? 4u : 16u)) {
+        const double cost = dc_cost_us(nw, warm, chunk, fp);
+        if (replay_mode == 0 && fp > 2 && cost > serial_cost_us(nev, serial_nw)) {
             replay_serial = true;
             serial_builds = 0;
+            dc_probe = false;
             return;
         }
-        if (fp > 3 && dc_warm < WG_DC_WARM_MAX && !dc_warm_fixed) dc_warm *= 2;
+        if (dc_probe) {
+            dc_probe = false;
+            if (cost >= dc_cost_before) {   // the longer warm-up did not pay: back, and no more probes
+                dc_warm = warm / 2 >= 64 ? warm / 2 : 64;
+                dc_warm_frozen = true;
+            }
+        } else if (fp > 3 && warm < WG_DC_WARM_MAX && !dc_warm_fixed && !dc_warm_frozen) {
+            dc_cost_before = cost;
+            dc_warm = warm * 2;
+            dc_probe = true;
+        }
         dc_blind = fp >= dc_blind ? fp : (dc_blind + fp) / 2;
         if (dc_blind < 2) dc_blind = 2;
     }

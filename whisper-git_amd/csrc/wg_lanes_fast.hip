@@ -778,7 +778,7 @@ static void dc_commit(wg_ctx *c, const ReplayRun &run, uint64_t nev, uint32_t ma
     c->last_dc_warm = run.warm;
     c->last_form = 300u + run.nw;
     c->last_serial = false;
-    c->dc_adapt(first_still, nev, positions);
+    c->dc_adapt(first_still, nev, run.nw, run.warm, run.chunk, c->replay_nw);
     c->lane_path = 0;
     // (auto) a list shape with no leaks may suit the chunked replay after all:
     // it is tried again after WG_SERIAL_RETRY such builds (a skewed list's
@@ -806,8 +806,10 @@ static int replay_lanes_dc(wg_ctx *c, const LfRange &R, uint64_t nev, const uint
         ReplayRun run;
         int rc = dc_setup(c, run, nev, ev, aux, nw);
         if (rc != WG_OK) return rc;
-        // (auto) the serial pass's cost in iterations after the first
-        const uint32_t budget = 2u + (uint32_t)(wg_ctx::serial_cost_us(nev, c->replay_nw) / wg_ctx::WG_DC_ITER_US);
+        // (auto) the iterations after the first that cost what the serial pass does
+        const double first = wg_ctx::dc_cost_us(nw, run.warm, run.chunk, 1);
+        const double rest = wg_ctx::serial_cost_us(nev, c->replay_nw) - first;
+        const uint32_t budget = 2u + (rest > 0 ? (uint32_t)(rest / wg_ctx::dc_iter_us(nw, run.chunk)) : 0u);
         wg_stage_begin(c, "lf_loop");
         WG_HIP(c, wg_dc_init(s, run, true));
         WG_HIP(c, wg_dc_iterate(s, run, c->dc_blind < 2 ? 2u : c->dc_blind));

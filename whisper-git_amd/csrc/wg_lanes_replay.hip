@@ -633,8 +633,11 @@ hipError_t wg_replay_iterate_spec(hipStream_t s, ReplayRun &R, uint32_t blind) {
 hipError_t wg_replay_finish_lanes(hipStream_t s, const ReplayRun &R, uint64_t nl, const uint32_t *sp, uint32_t *lane,
                                   uint32_t *lane_out, uint8_t *color_out, const uint8_t *flags) {
     const uint64_t g = nl ? (nl + 255) / 256 : 1;
+    // the slot a run reports when its occupancy overflowed: the sentinel of its
+    // width (the serial pass's 3- and 8-word forms: 191 / 511, not 255 / 1023)
+    const uint32_t cap = (R.nw == 4 && R.ser_w3) ? 191u : (R.nw == 16 && R.ser_w8) ? 511u : 64u * R.nw - 1u;
     hipLaunchKernelGGL(k_lf_finish_lanes, dim3((uint32_t)g), dim3(256), 0, s, R.dc ? R.dc_blocks : R.nch, (const uint32_t *)R.stats,
-                       R.scal, (const uint32_t *)R.flags, R.it, 64u * R.nw - 1u, R.nev_dev, R.dc ? WG_DC_FIX_T : R.chunk, nl, sp,
+                       R.scal, (const uint32_t *)R.flags, R.it, cap, R.nev_dev, R.dc ? WG_DC_FIX_T : R.chunk, nl, sp,
                        (const uint16_t *)R.sp_prev, lane, lane_out, color_out, flags, R.gate, R.dc);
     return hipGetLastError();
 }

@@ -203,6 +203,11 @@ class Engine:
         (events, a multiple of 64; 0 = auto)."""
         self._check(lib().wg_set_option(self._ctx, 10, int(events)))
 
+    def set_join_fused(self, on: bool):
+        """WG_OPT_JOIN_FUSED: the id table's place pass inside the window probe,
+        or (default) the table built on the side stream beside it."""
+        self._check(lib().wg_set_option(self._ctx, 11, int(bool(on))))
+
     def set_slice_lists(self, mode: int):
         """WG_OPT_SLICE_LISTS: a deferred-validation build leaves its geometry
         lists to the next whole-list emission, which builds them in two row
