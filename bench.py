@@ -61,6 +61,7 @@ def parse():
                     help="gloo rehearsal: move HIP-resident slots through gloo (the stream-ordered slot path of RCCL)")
     ap.add_argument("--no-defer", action="store_true",
                     help="validate every speculative build before build() returns (WG_OPT_DEFER_VALIDATION off)")
+    ap.add_argument("--vtx-tile", type=int, default=0, help="vertices per emission tile (1024, 2048; 0 = auto)")
     ap.add_argument("--join-fused", action="store_true",
                     help="the id table's place pass inside the window probe, settle on the main stream (A/B; default: beside it)")
     ap.add_argument("--slice", action="store_true",
@@ -365,6 +366,7 @@ def config_rates(eng, dev, torch, args):
         eng.set_defer_validation(not args.no_defer)
         eng.set_slice_lists(1 if args.slice else 0)
         eng.set_join_fused(args.join_fused)
+        eng.set_vtx_tile(args.vtx_tile)
         d = synth.generate(kind, n)
         keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
                                                        d.parent_oid.reshape(-1), d.flags, d.band)]
@@ -436,6 +438,7 @@ def build_lifecycle(dag, dev, torch, args, pal):
     eng.set_defer_validation(not args.no_defer)
     eng.set_slice_lists(1 if args.slice else 0)
     eng.set_join_fused(args.join_fused)
+    eng.set_vtx_tile(args.vtx_tile)
 
     def step(k, c, n):
         torch.cuda.synchronize()
@@ -544,6 +547,7 @@ def main():
     eng.set_defer_validation(not args.no_defer)
     eng.set_slice_lists(1 if args.slice else 0)
     eng.set_join_fused(args.join_fused)
+    eng.set_vtx_tile(args.vtx_tile)
     pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
     selected = shard0 + 7
     comm = None

@@ -258,6 +258,11 @@ int         wg_synchronize(wg_ctx *ctx);
  * probe and its settle pass follows on the build's stream; 0 (default) = the
  * table is built on the side stream beside the probe.  Speed only. */
 #define WG_OPT_JOIN_FUSED 11
+/* WG_OPT_VTX_TILE: vertices per emission workgroup tile: 1024, 2048, 4096,
+ * or 0 (default: auto, 2048 once the last emission wrote more than 4e8
+ * vertices — its geometry no longer sits in the Infinity Cache — and 4096
+ * past 1.6e9).  Speed only. */
+#define WG_OPT_VTX_TILE 12
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------

@@ -485,6 +485,17 @@ int main(int argc, char **argv) {
                (unsigned long)NEV, (unsigned long)cev, (unsigned long)occupying, (unsigned long)leaked, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
         return 0;
     }
+    if (argc > 5 && !strcmp(argv[5], "wordhist")) {   /* which 64-slot word each event's slot lies in */
+        uint64_t h[2][17] = {{0}};
+        for (uint64_t k = 0; k < NEV; k++) { const uint32_t w = EV[k].slot / 64; h[EV[k].a ? 0 : 1][w < 16 ? w : 16]++; }
+        for (int t = 0; t < 2; t++) {
+            printf("%s:", t ? "consume" : "alloc");
+            for (int w = 0; w < 17; w++) if (h[t][w]) printf(" w%d=%lu", w, (unsigned long)h[t][w]);
+            printf("\n");
+        }
+        wgs_free(d);
+        return 0;
+    }
     if (argc > 5 && !strcmp(argv[5], "compact")) { run_compact(CH, warm); wgs_free(d); return 0; }
     if (argc > 5 && !strcmp(argv[5], "longseed")) { run_longseed(CH, warm); wgs_free(d); return 0; }
     for (int a = 5; a < argc || a == 5; a++) {

@@ -220,6 +220,36 @@ def test_baseline_configs_vertex_checksum(engine, kind, n):
         o.close()
 
 
+@pytest.mark.parametrize("tile", [1024, 2048])
+@pytest.mark.parametrize("kind,n", [("wide16", 50_000), ("linuxwide", 20_000), ("random13", 30_000), ("anomaly", 5000)])
+def test_emission_tile_sizes(kind, n, tile):
+    """WG_OPT_VTX_TILE: the emission's workgroup tile (1024 or 2048 vertices,
+    auto picks 2048 for lists past 4e8 vertices) changes nothing: the whole
+    vertex buffer, its row offsets and a partial row range with a selected row
+    bit-exact against the oracle (WG-TESS-1), twice on one context (the
+    second emission launched on the buffers in place)."""
+    import wgraph
+    from oracle import oracle_c
+    d = synth.generate(kind, n, seed=29)
+    o = oracle_c.OracleLayout(d)
+    eng = wgraph.Engine(0)
+    try:
+        eng.set_vtx_tile(tile)
+        eng.build(d)
+        eng.row_geometry(d.band)
+        o.row_geometry(d.band)
+        for rb, re_, sel in ((0, n, n // 3), (n // 5, n // 5 + 777, n // 5 + 10)):
+            for _ in range(2):
+                eng.emit_vertices(rb, re_, selected=sel)
+                ov, ooff = o.emit_vertices(rb, re_, selected=sel)
+                assert eng.vertex_offsets().tobytes() == ooff.tobytes(), (kind, tile, rb)
+                vs = eng.vertex_summary()
+                assert vs.n_vertices == len(ov) and vs.checksum == oracle_c.vertex_checksum(ov), (kind, tile, rb)
+    finally:
+        eng.close()
+        o.close()
+
+
 def test_bands_with_fractional_and_negative_values(engine):
     """Non-integer bands keep the transducer path exact; a negative band forces
     the serial path, which must also be exact."""

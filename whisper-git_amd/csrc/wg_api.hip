@@ -506,6 +506,11 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         c->slice_on = value != 0;
         c->slice_min_rows = value == 2 ? 4 * WG_SWEEP_CH : 1ull << 18;
         return WG_OK;
+    case WG_OPT_VTX_TILE:
+        if (value != 0 && value != 1024 && value != 2048 && value != 4096)
+            return wg_fail(c, WG_E_INVALID, "vertex tile must be 0, 1024, 2048 or 4096");
+        c->vtx_tile_opt = (uint32_t)value;
+        return WG_OK;
     case WG_OPT_JOIN_FUSED:
         c->join_fused = value != 0;
         return WG_OK;

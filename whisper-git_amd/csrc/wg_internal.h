@@ -124,7 +124,6 @@ struct LfRange {
 #define WG_SWEEP_CAP  2048   // active-edge capacity per wave (LDS)
 
 // Vertex tiles (wg_vertex.hip)
-#define WG_VTX_TILE   1536   // vertices per workgroup tile (36 KiB of LDS)
 
 // Row-sharded build state (wg_shard.hip)
 struct ShardState {
@@ -588,6 +587,9 @@ struct wg_ctx {
     bool     have_vtx = false;
     uint64_t vrow_begin = 0, vrow_end = 0, n_vtx = 0;
     uint64_t vtx_tiles_last = 0;   // tiles of the last emission (bounds the next one's early grid)
+    uint32_t vtx_tile_last = 1024; // ... of this many vertices (wg_vertex.hip)
+    uint32_t vtx_tile_opt = 0;     // WG_OPT_VTX_TILE: 0 auto, 1024 or 2048
+    static constexpr uint64_t WG_VTX_BIG_VERTICES = 400000000ull;   // auto: 2048-vertex tiles past this many
     int64_t  selected = -1;
     DevBuf vtx_off;         // uint64 [rows+1]
     DevBuf vtx;             // wg_vertex [n_vtx]

@@ -33,20 +33,24 @@ namespace {
 #ifndef WG_VTX_THREADS
 #define WG_VTX_THREADS 256
 #endif
-#ifndef WG_VTX_TILE_VERTS
-#define WG_VTX_TILE_VERTS 1024   // 24 KiB out per workgroup (tile sweep: 1024 0.98 ms, 1536 1.01, 2048 1.05, 512 1.07)
-#endif
+// Vertices per workgroup tile: 1024 (24 KiB out) by default; 2048 for lists
+// whose geometry outgrows the Infinity Cache (each tile's load round then
+// waits on HBM under the saturated write stream, and a larger tile amortises
+// it: DESIGN.md §3 "one load round per tile"; WG_OPT_VTX_TILE).
+// (tile sweep on wide16 1M: 1024 0.98 ms, 1536 1.01, 2048 1.05, 512 1.07)
 constexpr int VT = WG_VTX_THREADS;
-constexpr int TILE = WG_VTX_TILE_VERTS;     // vertices per workgroup
-constexpr int PAIRS = TILE / 2;             // 512
-constexpr int ROUNDS = PAIRS / VT;          // 2
-static_assert(PAIRS % VT == 0, "a tile is a whole number of rounds of one pair per thread");
+template <int TILE>
+struct TileGeo {
+    static constexpr int PAIRS = TILE / 2;
+    static constexpr int ROUNDS = PAIRS / VT;
+    static constexpr int MAXR = TILE / WG_VTX_PER_NODE + 3;         // rows overlapping a tile
+    static constexpr int MAXC = TILE / WG_VTX_PER_CURVE + 3;        // curve segments overlapping a tile
+    static constexpr int MAXV = TILE / WG_VTX_PER_VERTICAL + 2;     // vertical entries overlapping a tile
+    static_assert(PAIRS % VT == 0, "a tile is a whole number of rounds of one pair per thread");
+    static_assert(MAXR <= 64, "rows of a tile are loaded by one wave");
+};
 typedef float v4f __attribute__((ext_vector_type(4)));
-static_assert(TILE / WG_VTX_PER_NODE + 3 <= 64, "rows of a tile are loaded by one wave");
-constexpr int MAXR = TILE / WG_VTX_PER_NODE + 3;          // rows overlapping a tile
-constexpr int MAXC = TILE / WG_VTX_PER_CURVE + 3;         // curve segments overlapping a tile
 constexpr int NPTS = WG_TESS_CURVE_SEGMENTS + 1;          // 17 strip points per segment
-constexpr int MAXV = TILE / WG_VTX_PER_VERTICAL + 2;      // vertical entries overlapping a tile
 
 __constant__ float c_cos[25] = WG_UNIT_CIRCLE_COS_INIT;
 __constant__ float c_sin[25] = WG_UNIT_CIRCLE_SIN_INIT;
@@ -75,6 +79,7 @@ __device__ __forceinline__ uint64_t vtx_at(uint64_t rb, uint64_t j, int64_t sel,
 // gate: a build awaiting its validation (WG_OPT_DEFER_VALIDATION) whose
 // geometry lists did not fit (its error words [0] / [8]): nothing is read or
 // written (the validation redoes the build and this emission)
+template <int TILE>
 __global__ void k_vtx_prep(uint64_t rb, uint64_t rows, int64_t sel, const uint32_t *__restrict__ voff,
                            const uint32_t *__restrict__ coff, uint64_t *__restrict__ vtx_off, uint64_t tcap,
                            uint4 *__restrict__ info, const uint32_t *__restrict__ gate) {
@@ -132,6 +137,7 @@ __device__ __forceinline__ float clamp_rs(float x, float lo, float hi) {
     return x;
 }
 
+template <int TILE>
 __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint64_t vcap, uint32_t vis,
         const uint64_t *__restrict__ vtx_off, const uint32_t *__restrict__ voff, const uint32_t *__restrict__ vert,
         const uint32_t *__restrict__ coff, const wg_curve *__restrict__ curve, const uint8_t *__restrict__ curve_color,
@@ -140,6 +146,8 @@ __global__ void __launch_bounds__(VT) k_vtx_tile(uint64_t rb, uint64_t re, uint6
         const uint4 *__restrict__ tinfo, const uint8_t *__restrict__ match, int64_t mlo, int64_t mhi,
         float4 *__restrict__ out, uint64_t ntl, const uint32_t *__restrict__ max_lane_dev,
         const uint32_t *__restrict__ gate, int part, uint64_t split_row, uint64_t p1) {
+    using G = TileGeo<TILE>;
+    constexpr int PAIRS = G::PAIRS, ROUNDS = G::ROUNDS, MAXR = G::MAXR, MAXC = G::MAXC, MAXV = G::MAXV;
     __shared__ RowInfo rows[MAXR];
     __shared__ __attribute__((aligned(4))) uint8_t pair_row[PAIRS];   // row (within the tile) of every vertex pair
     __shared__ float4 pts[MAXC * NPTS];            // (L.x, L.y, R.x, R.y) per strip point
@@ -433,6 +441,21 @@ __global__ void k_checksum(const uint32_t *__restrict__ w, uint64_t nwords, unsi
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const uint64_t rows = re - rb;
     hipStream_t s = c->stream;
+    // the tile size: WG_OPT_VTX_TILE, or (auto) from the last emission's
+    // vertex count: past 4e8 (its geometry past the Infinity Cache) 2048, past
+    // 1.6e9 4096, else 1024 (r05 A/B, profiles/r05/r05c_vtx_tile.jsonl:
+    // linuxwide 1M 13.93 / 12.81 / 12.65 ms/step at 1024 / 2048 / 4096,
+    // wide16 3M 4.28 / 4.19 / 4.33, wide16 1M 1.479 / 1.498, C4 3.881 / 3.896)
+    uint32_t TILE = c->vtx_tile_opt;
+    if (!TILE) {
+        const uint64_t last = c->vtx_tiles_last * c->vtx_tile_last;
+        TILE = last > 4 * wg_ctx::WG_VTX_BIG_VERTICES ? 4096u : last > wg_ctx::WG_VTX_BIG_VERTICES ? 2048u : 1024u;
+    }
+    if (TILE != c->vtx_tile_last) {   // (tile indices of the last emission do not carry over)
+        c->vtx_tiles_last = c->vtx_tiles_last * c->vtx_tile_last / TILE;
+        c->vtx_t1_last = 0;
+        c->vtx_tile_last = TILE;
+    }
     WG_ALLOC(c, c->vtx_off, (rows + 2) * 8);
     { const int _sr = wg_scan_reserve(c, rows + 2); if (_sr != WG_OK) return _sr; }
     c->vrow_begin = rb;
@@ -447,9 +470,18 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     uint64_t *off = c->vtx_off.as<uint64_t>();
     const uint32_t *gate = c->pend.build ? c->geom_err : nullptr;   // a build awaiting its validation
     auto prep = [&](uint64_t tcap) {   // vtx_off + tile records (none when tcap is too small)
-        hipLaunchKernelGGL(k_vtx_prep, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
-                           c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
-                           c->tile_first.as<uint4>(), gate);
+        if (TILE == 4096)
+            hipLaunchKernelGGL(k_vtx_prep<4096>, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
+                               c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
+                               c->tile_first.as<uint4>(), gate);
+        else if (TILE == 2048)
+            hipLaunchKernelGGL(k_vtx_prep<2048>, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
+                               c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
+                               c->tile_first.as<uint4>(), gate);
+        else
+            hipLaunchKernelGGL(k_vtx_prep<1024>, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
+                               c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
+                               c->tile_first.as<uint4>(), gate);
     };
     const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;
     const uint64_t tcap = c->tile_first.cap / sizeof(uint4);
@@ -518,12 +550,17 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
             wg_stage_begin(c, "vtx_emit");
         }
         // (grid rounded up to whole XCD rounds: k_vtx_tile's tile order)
-        hipLaunchKernelGGL(k_vtx_tile, dim3((uint32_t)((grid + 7) / 8 * 8)), dim3(VT), 0, st, rb, re, vcap, vis, (const uint64_t *)off,
-                           c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(), c->curve_off.as<const uint32_t>(),
-                           c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(), c->g_height.as<const float>(),
-                           c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(), c->color_out.as<const uint8_t>(),
-                           c->palette.as<const float4>(), c->tile_first.as<const uint4>(), match, mlo, mhi,
-                           c->vtx.as<float4>(), ntl, ml_dev, gate, part, h, p1);
+#define WG_VTX_LAUNCH(TL)                                                                                                     \
+        hipLaunchKernelGGL(k_vtx_tile<TL>, dim3((uint32_t)((grid + 7) / 8 * 8)), dim3(VT), 0, st, rb, re, vcap, vis,          \
+                           (const uint64_t *)off, c->vert_off.as<const uint32_t>(), c->vert.as<const uint32_t>(),             \
+                           c->curve_off.as<const uint32_t>(), c->curve.as<const wg_curve>(), c->curve_color.as<const uint8_t>(),\
+                           c->g_height.as<const float>(), c->g_node_y.as<const float>(), c->lane_out.as<const uint32_t>(),    \
+                           c->color_out.as<const uint8_t>(), c->palette.as<const float4>(), c->tile_first.as<const uint4>(),  \
+                           match, mlo, mhi, c->vtx.as<float4>(), ntl, ml_dev, gate, part, h, p1)
+        if (TILE == 4096) WG_VTX_LAUNCH(4096);
+        else if (TILE == 2048) WG_VTX_LAUNCH(2048);
+        else WG_VTX_LAUNCH(1024);
+#undef WG_VTX_LAUNCH
         if (mark) wg_stage_end(c);
     };
     auto launch = [&](uint64_t vcap, uint64_t grid, uint64_t ntl, int part, uint64_t p1) {

@@ -208,6 +208,10 @@ class Engine:
         or (default) the table built on the side stream beside it."""
         self._check(lib().wg_set_option(self._ctx, 11, int(bool(on))))
 
+    def set_vtx_tile(self, verts: int):
+        """WG_OPT_VTX_TILE: vertices per emission tile (1024, 2048; 0 = auto)."""
+        self._check(lib().wg_set_option(self._ctx, 12, int(verts)))
+
     def set_slice_lists(self, mode: int):
         """WG_OPT_SLICE_LISTS: a deferred-validation build leaves its geometry
         lists to the next whole-list emission, which builds them in two row
