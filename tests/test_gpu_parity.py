@@ -220,7 +220,7 @@ def test_baseline_configs_vertex_checksum(engine, kind, n):
         o.close()
 
 
-@pytest.mark.parametrize("tile", [1024, 2048])
+@pytest.mark.parametrize("tile", [1024, 2048, 4096])
 @pytest.mark.parametrize("kind,n", [("wide16", 50_000), ("linuxwide", 20_000), ("random13", 30_000), ("anomaly", 5000)])
 def test_emission_tile_sizes(kind, n, tile):
     """WG_OPT_VTX_TILE: the emission's workgroup tile (1024 or 2048 vertices,
