@@ -38,7 +38,7 @@ def main():
         eng.enable_timing(False)
         flags = eng.match_flags()
         m = 20_000
-        want = search_oracle.match_rows(dag, query.encode(), (sb, so_), (ab, ao), 0, m)
+        want, _ = search_oracle.match_rows(dag, query.encode(), (sb, so_), (ab, ao), 0, m)
         ok = bool(np.array_equal(np.asarray(flags[:m], np.uint8), np.asarray(want, np.uint8)))
         k = float(np.mean(ms))
         print(json.dumps({"query": query, "rows": n, "matches": int(nm), "kernel_ms": round(k, 4),

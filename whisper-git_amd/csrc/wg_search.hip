@@ -28,7 +28,6 @@
 #include "wg_internal.h"
 #include "wg_unicase.h"
 
-#include <algorithm>
 #include <cstring>
 
 namespace {
@@ -131,6 +130,8 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         reinterpret_cast<uint32_t *>(s_lut2)[i] = reinterpret_cast<const uint32_t *>(A.lut2)[i];
     const WgCaseTables T{s_lower, s_cased, s_ign, s_lut2};
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t r = A.rb + (uint64_t)blockIdx.x * MT + threadIdx.x;
+    const bool live = r < A.re;
     const uint32_t m = A.m;
     const bool qlds = m <= (uint32_t)QLDS;
     if (qlds)
@@ -140,16 +141,8 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         for (uint32_t i = 0; i < m; i++) { qv = (qv << 8) | A.q[i]; qmask = (qmask << 8) | 0xFFu; }
     __syncthreads();   // tables and query
     WgKmp km{qlds ? s_q : A.q, qlds ? s_fail : A.fail, m, 0};
-    uint32_t *col = &s_tt[wv][lane];
-    // persistent blocks (r05): the tables and the query are staged once per
-    // block, which then takes groups of MT rows in turn (a block per group
-    // staged 8 KiB of tables for 256 rows)
-    uint32_t hits = 0;
-    const uint64_t ngroups = (A.re - A.rb + MT - 1) / MT;
-    for (uint64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const uint64_t r = A.rb + grp * MT + threadIdx.x;
-    const bool live = r < A.re;
     bool hit = false;
+    uint32_t *col = &s_tt[wv][lane];
     // summary, then author
     for (int f = 0; f < 2; f++) {
         const uint8_t *text = f ? A.auth : A.sum;
@@ -211,10 +204,8 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         }
     }
     if (live) A.out[r - A.rb] = hit ? 1 : 0;
-    hits += (live && hit) ? 1u : 0u;
-    }
-    for (int d = 32; d >= 1; d >>= 1) hits += (uint32_t)__shfl_xor((int)hits, d, 64);
-    if (lane == 0 && hits) atomicAdd(A.count, (unsigned long long)hits);
+    const int cnt = __syncthreads_count(live && hit);
+    if (threadIdx.x == 0 && cnt) atomicAdd(A.count, (unsigned long long)cnt);
 }
 
 inline uint32_t mblocks(uint64_t n) { return (uint32_t)((n + MT - 1) / MT); }
@@ -325,12 +316,7 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     A.out = c->match_flags.as<uint8_t>();
     A.count = c->match_q.as<unsigned long long>();
     wg_stage_begin(c, "match");
-    if (rows) {   // persistent blocks: a few per CU, each taking groups of MT rows in turn
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0) ncu = 256;
-        const uint32_t g = std::min<uint32_t>(mblocks(rows), (uint32_t)ncu * 4u);
-        hipLaunchKernelGGL(k_match, dim3(g), dim3(MT), 0, s, A);
-    }
+    if (rows) hipLaunchKernelGGL(k_match, dim3(mblocks(rows)), dim3(MT), 0, s, A);
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     uint64_t cnt = 0;
