@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--no-defer", action="store_true",
                     help="validate every speculative build before build() returns (WG_OPT_DEFER_VALIDATION off)")
     ap.add_argument("--vtx-tile", type=int, default=0, help="vertices per emission tile (1024, 2048; 0 = auto)")
+    ap.add_argument("--no-fused-read", action="store_true", help="the emission's host read by a read kernel (A/B)")
     ap.add_argument("--join-fused", action="store_true",
                     help="the id table's place pass inside the window probe, settle on the main stream (A/B; default: beside it)")
     ap.add_argument("--slice", action="store_true",
@@ -367,6 +368,7 @@ def config_rates(eng, dev, torch, args):
         eng.set_slice_lists(1 if args.slice else 0)
         eng.set_join_fused(args.join_fused)
         eng.set_vtx_tile(args.vtx_tile)
+        eng.set_fused_read(not args.no_fused_read)
         d = synth.generate(kind, n)
         keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
                                                        d.parent_oid.reshape(-1), d.flags, d.band)]
@@ -439,6 +441,7 @@ def build_lifecycle(dag, dev, torch, args, pal):
     eng.set_slice_lists(1 if args.slice else 0)
     eng.set_join_fused(args.join_fused)
     eng.set_vtx_tile(args.vtx_tile)
+    eng.set_fused_read(not args.no_fused_read)
 
     def step(k, c, n):
         torch.cuda.synchronize()
@@ -548,6 +551,7 @@ def main():
     eng.set_slice_lists(1 if args.slice else 0)
     eng.set_join_fused(args.join_fused)
     eng.set_vtx_tile(args.vtx_tile)
+    eng.set_fused_read(not args.no_fused_read)
     pal = np.ascontiguousarray(abi.DEFAULT_PALETTE)
     selected = shard0 + 7
     comm = None

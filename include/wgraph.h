@@ -263,6 +263,11 @@ int         wg_synchronize(wg_ctx *ctx);
  * vertices — its geometry no longer sits in the Infinity Cache — and 4096
  * past 1.6e9).  Speed only. */
 #define WG_OPT_VTX_TILE 12
+/* WG_OPT_FUSED_READ: 1 (default) = the emission's one host read (the vertex
+ * total and a deferred build's validation words) is written to the host by
+ * the kernel that computes the total; 0 = a separate read kernel.  Speed
+ * only. */
+#define WG_OPT_FUSED_READ 13
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------

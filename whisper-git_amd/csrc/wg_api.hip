@@ -265,8 +265,9 @@ int wg_fetch_begin(wg_ctx *c, std::initializer_list<WgFetch> items) {
 
 int wg_fetch_begin_n(wg_ctx *c, int n, const WgFetch *items) {
     if (c->fetch_pending) {   // left behind by a failed call: drop it
-        (void)hipEventSynchronize(c->ev_fetch);
+        (void)(c->fetch_fused ? hipStreamSynchronize(c->stream) : hipEventSynchronize(c->ev_fetch));
         c->fetch_pending = 0;
+        c->fetch_fused = false;
     }
     if (const int rc = fetch_launch(c, n, items, FETCH_MAX)) return rc;
     // (a device-scope release: the words reach the host by k_fetch's own
@@ -370,11 +371,40 @@ int wg_fetch_deferred(wg_ctx *c, uint64_t *out) {
     return WG_OK;
 }
 
+int wg_fetch_fused_begin(wg_ctx *c, int n, const WgFetch *items, WgFusedFetch *f) {
+    static_assert(WG_FETCH_MAX == FETCH_MAX, "fused fetch region size");
+    if (n < 0 || n > FETCH_MAX) return wg_fail(c, WG_E_INVALID, "wg_fetch: too many items");
+    if (c->fetch_pending) {   // left behind by a failed call: drop it
+        (void)hipStreamSynchronize(c->stream);
+        c->fetch_pending = 0;
+    }
+    if (!c->h_fetch) {
+        WG_HIP(c, hipHostMalloc((void **)&c->h_fetch, (3 * FETCH_MAX + 8) * sizeof(uint64_t),
+                                hipHostMallocMapped | hipHostMallocCoherent));
+        WG_HIP(c, hipHostGetDevicePointer((void **)&c->d_fetch, c->h_fetch, 0));
+        memset(c->h_fetch, 0, (3 * FETCH_MAX + 8) * sizeof(uint64_t));
+    }
+    *f = WgFusedFetch{};
+    for (int i = 0; i < n; i++) {
+        f->p[i] = items[i].p;
+        if (items[i].wide) f->wide |= 1ull << i;
+    }
+    f->n = (uint32_t)n;
+    f->out = (unsigned long long *)c->d_fetch + FETCH_MAX;
+    f->seq_word = (unsigned long long *)c->d_fetch + 3 * FETCH_MAX + 1;
+    f->seq = c->fetch_want[1] = ++c->fetch_seq;
+    c->fetch_pending = n;
+    c->fetch_fused = true;
+    return WG_OK;
+}
+
 int wg_fetch_end(wg_ctx *c, uint64_t *out) {
     if (!c->fetch_pending) return wg_fail(c, WG_E_STATE, "wg_fetch_end: nothing pending");
     const int n = c->fetch_pending;
     c->fetch_pending = 0;
-    if (!fetch_spin(c, 1)) WG_HIP(c, hipEventSynchronize(c->ev_fetch));
+    const bool fused = c->fetch_fused;
+    c->fetch_fused = false;
+    if (!fetch_spin(c, 1)) WG_HIP(c, fused ? hipStreamSynchronize(c->stream) : hipEventSynchronize(c->ev_fetch));
     for (int i = 0; i < n; i++) out[i] = ((volatile uint64_t *)c->h_fetch)[FETCH_MAX + i];
     return WG_OK;
 }
@@ -505,6 +535,10 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         WG_SETTLE(c);
         c->slice_on = value != 0;
         c->slice_min_rows = value == 2 ? 4 * WG_SWEEP_CH : 1ull << 18;
+        return WG_OK;
+    case WG_OPT_FUSED_READ:
+        WG_SETTLE(c);
+        c->fused_read = value != 0;
         return WG_OK;
     case WG_OPT_VTX_TILE:
         if (value != 0 && value != 1024 && value != 2048 && value != 4096)

@@ -634,6 +634,8 @@ struct wg_ctx {
     uint64_t  *h_fetch = nullptr;   // mapped pinned host memory for wg_fetch / wg_fetch_begin
     hipEvent_t ev_fetch = nullptr;  // completion of the pending wg_fetch_begin
     int        fetch_pending = 0;   // words of the pending wg_fetch_begin
+    bool       fetch_fused = false; // ... written by a producing kernel (wg_fetch_fused_begin): no event behind it
+    bool       fused_read = true;   // WG_OPT_FUSED_READ: the emission's read folded into k_vtx_prep
     hipEvent_t ev_defer = nullptr;  // completion of the last wg_fetch_defer
     int        defer_pending = 0;   // words of the last wg_fetch_defer
     uint64_t  *d_fetch = nullptr;
@@ -664,6 +666,26 @@ int wg_shard_geom_validate(wg_ctx *c, const uint64_t *v, bool *redo);
         }                                                                          \
     } while (0)
 int wg_fetch_end(wg_ctx *c, uint64_t *out);
+// A read folded into a producing kernel instead of a k_fetch launch (and the
+// event between that kernel and the next): wg_fetch_fused_begin fills the
+// arguments for wg_fetch_begin's region, one device thread calls
+// wg_fused_fetch_store after the words are final, wg_fetch_end reads them
+// (its fallback wait is the stream's)
+constexpr int WG_FETCH_MAX = 64;
+struct WgFusedFetch {
+    const void *p[WG_FETCH_MAX];
+    unsigned long long wide;
+    uint32_t n;
+    unsigned long long *out, *seq_word, seq;
+};
+int wg_fetch_fused_begin(wg_ctx *c, int n, const WgFetch *items, WgFusedFetch *f);
+__device__ __forceinline__ void wg_fused_fetch_store(const WgFusedFetch &f) {
+    for (uint32_t i = 0; i < f.n; i++)
+        f.out[i] = ((f.wide >> i) & 1ull) ? *reinterpret_cast<const volatile unsigned long long *>(f.p[i])
+                                          : (unsigned long long)*reinterpret_cast<const volatile uint32_t *>(f.p[i]);
+    __threadfence_system();
+    __hip_atomic_store(f.seq_word, f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 int wg_fetch_defer(wg_ctx *c, std::initializer_list<WgFetch> items);
 int wg_fetch_deferred(wg_ctx *c, uint64_t *out);
 

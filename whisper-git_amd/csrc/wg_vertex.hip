@@ -79,17 +79,27 @@ __device__ __forceinline__ uint64_t vtx_at(uint64_t rb, uint64_t j, int64_t sel,
 // gate: a build awaiting its validation (WG_OPT_DEFER_VALIDATION) whose
 // geometry lists did not fit (its error words [0] / [8]): nothing is read or
 // written (the validation redoes the build and this emission)
+// ff (fused): the vertex total and the pending words are read out to the host
+// by the thread of row `rows` right after it wrote the total — no k_fetch
+// launch and no event between this kernel and the tiles (r05: the event cost
+// ~12 us on the step's critical path)
 template <int TILE>
 __global__ void k_vtx_prep(uint64_t rb, uint64_t rows, int64_t sel, const uint32_t *__restrict__ voff,
                            const uint32_t *__restrict__ coff, uint64_t *__restrict__ vtx_off, uint64_t tcap,
-                           uint4 *__restrict__ info, const uint32_t *__restrict__ gate) {
+                           uint4 *__restrict__ info, const uint32_t *__restrict__ gate, WgFusedFetch ff) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j > rows) return;
-    if (gate && (gate[0] | gate[8])) return;
+    if (gate && (gate[0] | gate[8])) {   // (the host still gets the words: they say the build did not hold)
+        if (j == rows && ff.seq_word) wg_fused_fetch_store(ff);
+        return;
+    }
     const uint32_t v0 = voff[rb], c0 = coff[rb];
     const uint64_t s = vtx_at(rb, j, sel, voff, coff, v0, c0);
     vtx_off[j] = s;
-    if (j == rows) return;
+    if (j == rows) {
+        if (ff.seq_word) wg_fused_fetch_store(ff);
+        return;
+    }
     const uint64_t e = vtx_at(rb, j + 1, sel, voff, coff, v0, c0);
     const uint64_t ntiles = (vtx_at(rb, rows, sel, voff, coff, v0, c0) + TILE - 1) / TILE;
     if (ntiles + 1 > tcap) return;
@@ -469,20 +479,17 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     wg_stage_begin(c, "vtx_counts");
     uint64_t *off = c->vtx_off.as<uint64_t>();
     const uint32_t *gate = c->pend.build ? c->geom_err : nullptr;   // a build awaiting its validation
-    auto prep = [&](uint64_t tcap) {   // vtx_off + tile records (none when tcap is too small)
-        if (TILE == 4096)
-            hipLaunchKernelGGL(k_vtx_prep<4096>, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
-                               c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
-                               c->tile_first.as<uint4>(), gate);
-        else if (TILE == 2048)
-            hipLaunchKernelGGL(k_vtx_prep<2048>, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
-                               c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
-                               c->tile_first.as<uint4>(), gate);
-        else
-            hipLaunchKernelGGL(k_vtx_prep<1024>, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,
-                               c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,
-                               c->tile_first.as<uint4>(), gate);
+    auto prep = [&](uint64_t tcap, const WgFusedFetch &ff) {   // vtx_off + tile records (none when tcap is too small)
+#define WG_PREP_LAUNCH(TL)                                                                                       \
+        hipLaunchKernelGGL(k_vtx_prep<TL>, dim3((rows + 1 + 255) / 256), dim3(256), 0, s, rb, rows, sel,          \
+                           c->vert_off.as<const uint32_t>(), c->curve_off.as<const uint32_t>(), off, tcap,       \
+                           c->tile_first.as<uint4>(), gate, ff)
+        if (TILE == 4096) WG_PREP_LAUNCH(4096);
+        else if (TILE == 2048) WG_PREP_LAUNCH(2048);
+        else WG_PREP_LAUNCH(1024);
+#undef WG_PREP_LAUNCH
     };
+    const WgFusedFetch no_fetch{};
     const uint64_t vcap = c->vtx.cap > 64 ? (c->vtx.cap - 64) / sizeof(wg_vertex) : 0;
     const uint64_t tcap = c->tile_first.cap / sizeof(uint4);
     const bool early = vcap > 0 && tcap > 1;
@@ -491,7 +498,6 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const bool sliced = c->glist.deferred && early && rb == 0 && rows == c->glist.n;
     if (!sliced)
         if (const int rc = wg_geom_lists_flush(c)) return rc;
-    prep(early ? tcap : 0);
     float q = roundf(c->graph_width / WG_LANE_W);
     uint32_t vis = q <= 0.0f ? 0u : (uint32_t)q;
     if (vis < 1) vis = 1;
@@ -516,21 +522,22 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         fi[3 + npend] = WgFetch{c->glist.err + 4, false};
     }
     const int nfi = 1 + npend + (sliced ? 3 : 0);
-    bool side_read = false;
+    bool fused_read = false;
     if (sliced) {
-        // (launched below, with the tiles)
-    } else if (early && rows >= c->slice_min_rows && c->side && c->ev_fork) {
-        // the read on the side stream: the tiles start right after the prep
-        // instead of behind the read's system-scope release (~10 us of L2
-        // write-back on the step's critical path); one event record between
-        // the prep and the tiles, the side's calls after the tiles' launch
-        // (below).  Not for short lists: there the host's launches are the
-        // step's pace, and the side costs it four more runtime calls
-        if (const int rc = wg_side_join(c)) return rc;
-        WG_HIP(c, hipEventRecord(c->ev_fork, s));
-        side_read = true;
-    } else if (const int rc = wg_fetch_begin_n(c, nfi, fi)) {
-        return rc;
+        prep(early ? tcap : 0, no_fetch);   // (the read is launched below, with the tiles)
+    } else if (early && c->fused_read) {
+        // the read folded into the prep kernel (r05): its last thread writes the
+        // total and the pending words to the host right after computing the
+        // total, so the tiles start right after the prep — no k_fetch launch,
+        // no system-scope release and no event record between them (r04 read on
+        // the side stream behind an event record: a ~12 us gap before the tiles)
+        WgFusedFetch ff;
+        if (const int rc = wg_fetch_fused_begin(c, nfi, fi, &ff)) return rc;
+        prep(tcap, ff);
+        fused_read = true;
+    } else {
+        prep(early ? tcap : 0, no_fetch);
+        if (const int rc = wg_fetch_begin_n(c, nfi, fi)) return rc;
     }
     // (a pending single-GPU build, or a sharded one whose replay is unchecked:
     // graph_width from the device's lane scalars)
@@ -601,14 +608,10 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     } else if (early) {
         launch(vcap, early_grid, early_grid, 0, 0);
     }
-    if (side_read) {   // the side stream after the prep: the read, the next build's empty table
-        WG_HIP(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-        c->side_main = c->stream;
-        c->stream = c->side;
-        int rc = wg_fetch_begin_n(c, nfi, fi);
-        if (rc == WG_OK && !c->sh.on) rc = wg_hash_clear_next(c, c->stream);
-        wg_side_done(c);
-        if (rc) return rc;
+    if (fused_read && !c->sh.on && c->side) {
+        // the next build's empty table, on the side stream beside the tiles
+        // (ordered after the previous builds' use of it by this build's fork)
+        if (const int rc = wg_hash_clear_next(c, c->side)) return rc;
     }
     uint64_t fv[4 + WG_PENDING_ITEMS] = {0};
     if (const int rc = wg_fetch_end(c, fv)) return rc;
@@ -625,7 +628,7 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         if (early) wg_stage_begin(c, "vtx_counts");
         WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
         WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
-        prep(ntiles + 1);
+        prep(ntiles + 1, no_fetch);
         launch(total, ntiles, ntiles, 0, 0);
     } else if (sliced) {
         const uint64_t t1 = fv[1 + npend] / TILE;

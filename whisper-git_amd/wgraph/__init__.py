@@ -212,6 +212,11 @@ class Engine:
         """WG_OPT_VTX_TILE: vertices per emission tile (1024, 2048; 0 = auto)."""
         self._check(lib().wg_set_option(self._ctx, 12, int(verts)))
 
+    def set_fused_read(self, on: bool):
+        """WG_OPT_FUSED_READ: the emission's host read written by the kernel
+        that computes the vertex total (default) or by a read kernel."""
+        self._check(lib().wg_set_option(self._ctx, 13, int(bool(on))))
+
     def set_slice_lists(self, mode: int):
         """WG_OPT_SLICE_LISTS: a deferred-validation build leaves its geometry
         lists to the next whole-list emission, which builds them in two row
