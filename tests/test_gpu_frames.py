@@ -130,3 +130,36 @@ def test_row_geometry_with_another_list(engine):
             engine.row_geometry_list(d.slice_rows(d.n - 1), d.band[:-1])
     finally:
         o.close()
+
+
+def test_row_geometry_list_device_times_rewritten_in_place(engine):
+    """A device-resident build whose time buffer the caller rewrites in place,
+    then passes again as the commits argument: the heights follow the times as
+    they stand (no pointer-equality shortcut against a caller's buffer)."""
+    import numpy as np
+    import torch
+    from oracle import oracle_c
+    from wgraph import abi, synth
+    d = synth.generate("random13", 20_000, seed=63)
+    other = synth.generate("linux", 20_000, seed=64)
+    dev = torch.device("cuda", 0)
+    keep = [torch.from_numpy(a).to(dev) for a in (d.oid.reshape(-1), d.time, d.parent_off.view(np.int32),
+                                                   d.parent_oid.reshape(-1), d.flags)]
+    c = abi.Commits()
+    c.n_commits, c.n_parents = d.n, d.e
+    c.oid, c.time, c.parent_off, c.parent_oid, c.flags = (t.data_ptr() for t in keep)
+    c.residency = abi.WG_DEVICE
+    o = oracle_c.OracleLayout(d)
+    try:
+        engine.build(commits=c)
+        engine.row_geometry_list(band=d.band, commits=c)
+        assert engine.geometry()["row_top"].tobytes() == o.row_geometry(d.band)["row_top"].tobytes()
+        keep[1].copy_(torch.from_numpy(other.time).to(dev))   # the caller rewrites its times
+        torch.cuda.synchronize()
+        engine.row_geometry_list(band=d.band, commits=c)
+        og = o.row_geometry(d.band, time=other.time)
+        got = engine.geometry()
+        for k, v in og.items():
+            assert got[k].tobytes() == v.tobytes(), k
+    finally:
+        o.close()

@@ -79,6 +79,76 @@ def test_match_without_text_fields_and_wide_rows(engine):
         engine.match_rows("")
 
 
+def test_match_fuzz_bytes_unaligned(engine):
+    """Rows of random bytes from an alphabet of ASCII letters, lead and
+    continuation bytes of two- to four-byte sequences (valid, truncated,
+    overlong, stray), U+03A3 / U+0130 / U+1E9E / U+212A pieces, with the
+    device text at byte offsets 0-3 (the LDS stage's edge words) and row
+    ranges that start mid-word; queries cut from the lowered rows."""
+    import torch
+    d = synth.generate("random13", 2000, seed=3)
+    engine.build(d)
+    rng = np.random.default_rng(11)
+    alpha = [b"A", b"a", b"Z", b"z", b" ", b".", b"'", b"\xce\xa3", b"\xcf\x83", b"\xc4\xb0", b"\xe1\xba\x9e",
+             b"\xe2\x84\xaa", b"\xce", b"\xa3", b"\x80", b"\xc0\xaf", b"\xe0\x80\x80", b"\xf0\x9f\x9a\x80",
+             b"\xf0\x9f", b"\xd0\x94", b"\xc7\x85", b"\xcc\x87", b"\xff", b"\xe6\x97\xa5", b"\x00", b"\x01"]
+    try:
+        # with raw 0xFF bytes in every 256-row range (specials left in place) and without (specials marked)
+        for alph in (alpha, alpha[:22] + alpha[23:]):
+            rows = [b"".join(alph[i] for i in rng.integers(0, len(alph), int(k))) for k in rng.integers(0, 24, d.n)]
+            rows[50:60] = [b""] * 10
+            off = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.uint64)
+            body = np.frombuffer(b"".join(rows), np.uint8)
+            qs = [b"a", b"\xcf\x83", b"\xcf\x82", b"i\xcc\x87", b"\xc3\x9f", b"k", b"\x80", b"\xce", b"\xff", b"\x00",
+                  b"a\x01", b"\xfe", b"i", b"\xcc\x87a"]
+            for r in rng.integers(0, d.n, 12):
+                lw = so.to_lowercase(rows[r])
+                if len(lw) > 2:
+                    a = int(rng.integers(0, len(lw) - 1))
+                    qs.append(lw[a:a + int(rng.integers(1, 12))])
+            for shift in range(4):
+                buf = torch.zeros(len(body) + 8, dtype=torch.uint8, device="cuda")
+                buf[shift:shift + len(body)] = torch.from_numpy(body.copy()).cuda()
+                ot = torch.from_numpy(off.view(np.int64).copy()).cuda()
+                dev = ((buf.data_ptr() + shift, ot.data_ptr()), None)
+                for q in qs:
+                    for rb, re_ in ((0, d.n), (333, 1501)):
+                        n = engine.match_rows(q, rb, re_, device=dev)
+                        want, wn = so.match_rows(d, q, (body, off), None, rb, re_)
+                        got = engine.match_flags()
+                        assert n == wn and (got == want).all(), (shift, q, rb, np.flatnonzero(got != want)[:5])
+    finally:
+        engine.match_rows("")
+
+
+def test_match_dense_non_ascii_fields(engine):
+    """Fields with more non-ASCII code points per 256 rows than the kernel's
+    lists hold (Cyrillic, Greek with final sigmas) and rows mixing them with
+    length-changing code points: every path gives the oracle's flags."""
+    d = synth.generate("random13", 1200, seed=4)
+    engine.build(d)
+    rng = np.random.default_rng(5)
+    pieces = ["Дa", "Σa", "ΣΣ ", "İ", "ẞ", "σ", "ΟΣ "]
+    rows = []
+    for i in range(d.n):
+        kind = (i // 256) % 3
+        if kind == 0:
+            rows.append(("Дa" * 20).encode())
+        elif kind == 1:
+            rows.append(("Σa" * 12 + ("ΟΣ " if i % 5 == 0 else "")).encode())
+        else:
+            rows.append("".join(pieces[j] for j in rng.integers(0, len(pieces), 9)).encode())
+    off = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.uint64)
+    body = np.frombuffer(b"".join(rows), np.uint8)
+    try:
+        for q in ("да", "σa", "ς", "ας σ", "i̇", "ss", "σσ", "ος", "дaдaдaдaдaд"):
+            n = engine.match_rows(q, summaries=(body, off), authors=(body, off))
+            want, wn = so.match_rows(d, q.encode(), (body, off), (body, off))
+            assert n == wn and (engine.match_flags() == want).all(), q
+    finally:
+        engine.match_rows("")
+
+
 def test_empty_query_matches_all_and_build_clears(engine, data):
     d, summ, auth = data
     engine.build(d)

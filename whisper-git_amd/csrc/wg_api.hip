@@ -461,7 +461,7 @@ void wg_destroy(wg_ctx *c) {
     }
     c->tile_first.release();
     DevBuf *xb[] = {&c->band_prev, &c->geom_diff_first, &c->render_small, &c->render_img, &c->match_flags,
-                    &c->match_q, &c->match_lut2};
+                    &c->match_q, &c->match_flat};
     for (DevBuf *b : xb) b->release();
     for (int f = 0; f < 2; f++) { c->match_txt[f].release(); c->match_off[f].release(); }
     for (DevBuf &b : c->ord) b.release();
@@ -878,8 +878,12 @@ int wg_row_geometry_list(wg_ctx *c, const wg_commits *cm, const float *band, int
     } else if (n && cm->residency != WG_DEVICE) {
         return wg_fail(c, WG_E_INVALID, "bad residency %d", cm->residency);
     }
-    bool same = !n || t == c->d_time;
-    if (!same) {
+    // The built list's times by pointer only when they are the engine's own
+    // copy: a caller's device buffer may have been rewritten since the build
+    // (then the heights are recomputed from it as it stands).
+    const bool own = c->d_time == c->in_time.as<const int64_t>();
+    bool same = !n || (t == c->d_time && own);
+    if (!same && t != c->d_time) {
         WG_ALLOC(c, c->geom_diff_first, 16);
         WG_HIP(c, hipMemsetAsync(c->geom_diff_first.p, 0xFF, 8, c->stream));
         const uint64_t g = std::min<uint64_t>((n + 255) / 256, 2048);

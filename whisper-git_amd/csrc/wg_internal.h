@@ -615,7 +615,7 @@ struct wg_ctx {
     uint64_t match_rb = 0, match_re = 0, match_count = 0;
     DevBuf   match_flags;           // uint8 [match_re - match_rb]
     DevBuf   match_q;               // {count u64, pad} + fail u16[m] + q u8[m]
-    DevBuf match_lut2;      // int16 [WG_LUT2_N] lowercase deltas of U+0080..U+07FF (search)
+    DevBuf match_flat;      // uint32 [WG_FLAT_N] lowercase | case classes of the BMP (search)
     DevBuf   match_txt[2], match_off[2];   // device copies of host summary / author text
     std::vector<uint64_t> match_rel[2];
     std::vector<uint8_t>  match_qhost;

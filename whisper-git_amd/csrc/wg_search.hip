@@ -10,21 +10,35 @@
 // (:1323-1324).  Non-matching rows are drawn at opacity 0.3 (:1467, 1482):
 // wg_emit_vertices / wg_emit_glyphs scale their alpha by WG_DIM_ALPHA.
 //
-// Per-row byte work (~the text bytes + 20 B of id per row).  A lane owns a
-// row: its summary and then its author bytes are copied into the lane's
-// column of a lane-major LDS block (batched aligned loads; the wave then reads
-// consecutive words at every step), and the lane lowers them as a byte
-// stream (ASCII inline; other code points through the Unicode tables in LDS,
-// the two-byte range by a direct delta table, Final_Sigma by a scan of the
-// neighbouring code points in the column) into the matcher: a 64-bit shift
-// register for queries of <= 8 lowered bytes, else Knuth-Morris-Pratt with
-// the query and failure table in LDS.  VALU-bound: a wave runs its longest
-// row, and a lane at a non-ASCII code point holds the others for the whole
-// decode / lower / encode path (measured: ~0.37 ms per 1M rows with ASCII
-// summaries and the name pool's non-ASCII authors, ~0.6 ms with 15%
-// non-ASCII summary words, whatever the byte path: flat or LDS reads, KMP or
-// shift register).  Rows longer than 128 bytes, or queries longer than the
-// LDS copy, take the generic stream from HBM.
+// Per-row byte work (~the text bytes + 20 B of id per row).  A workgroup
+// owns 256 rows and takes their fields one at a time, with every lane busy
+// in each pass (LDS-resident, barrier-separated):
+//  1. stage: the field's bytes of all 256 rows (one contiguous range) into
+//     LDS by coalesced word loads, ASCII lowered on the way in (SWAR), the
+//     lead bytes of non-ASCII code points listed (wave-aggregated appends);
+//  2. Final_Sigma for the listed 0xCE leads that are U+03A3, over the
+//     original bytes (ASCII lowering keeps case classes);
+//  3. the listed code points lowered IN PLACE by the thread holding the list
+//     entry (one flat table load per code point).  A "special" — U+0130 and
+//     the simple mappings whose UTF-8 length differs (U+1E9E, U+212A, ...) —
+//     cannot be lowered in place: it is marked (0xFF, its index, 0xFE...:
+//     bytes the lowered query does not hold) and, if its lowered bytes share
+//     one with the query, listed for a local walk;
+//  4. every byte position holding the query's first byte is tested against
+//     the query's first 8 lowered bytes (a 64-bit window from three LDS words;
+//     the rest of a longer query on a window hit); the row (binary search
+//     over the rows' LDS offsets) must hold the whole window.  A window over
+//     a mark never matches, and windows off the specials are exact;
+//  5. the windows over each listed special: the lowered stream from 3 (m - 1)
+//     buffer bytes before it to as many after, marks expanded, through a
+//     shift-register matcher.
+// Fallbacks, all exact: a query holding 0xFE / 0xFF / bytes < 32 or a field
+// holding raw 0xFE / 0xFF (no marks: the rows with specials are walked whole,
+// decoding), queries over 16 bytes (rows with relevant specials walked whole,
+// KMP), more code points than the lists hold or a field over the LDS buffer
+// (the row's own thread streams it from HBM through wg_lower_stream).  Last,
+// per row, the id's hex digits (short id contains q / id starts with q),
+// only for queries that are all hex digits.
 #include "wg_internal.h"
 #include "wg_unicase.h"
 
@@ -33,7 +47,6 @@
 namespace {
 
 constexpr int MT = 256;                 // rows per workgroup
-constexpr int QLDS = 2048;              // query bytes held in LDS
 
 __constant__ uint32_t c_lower[WG_LOWER_N][3] = WG_LOWER_TABLE_INIT;
 __constant__ uint32_t c_cased[WG_CASED_N][2] = WG_CASED_TABLE_INIT;
@@ -48,169 +61,473 @@ struct MatchArgs {
     const uint64_t *sum_off, *auth_off;    // [N+1] global (or rebased host copies)
     const uint8_t *oid, *flags;
     const uint8_t *q;                      // lowered query [m]
-    const int16_t *lut2;                   // [WG_LUT2_N] simple lowercase deltas of U+0080..U+07FF
+    const uint32_t *flat;                  // [WG_FLAT_N] per BMP code point, then [WG_SPECIAL_N] specials' lowered bytes
     const uint16_t *fail;                  // KMP failure table [m]
     uint32_t m;
+    uint32_t qhex;                         // the query can match the id's hex (m <= 40, all of [0-9a-f])
+    uint32_t marks;                        // the query holds no 0xFE / 0xFF byte: specials can be marked in place
+    uint32_t spec_rel;                     // bit i: special i's lowered bytes share a byte with the query
     uint8_t *out;                          // [re - rb]
     unsigned long long *count;
 };
 
-// Rows of a wave are transposed into LDS lane-major: word j of lane k's row
-// at col[j * 64 + k].  A per-lane walk over its own row then reads
-// consecutive words across the wave at every step — the byte-offset layout
-// put the 64 lanes' reads at effectively random banks (about 5-way
-// conflicts on every read).  Rows longer than TT_W words go through the
-// stream from HBM.
-constexpr uint32_t TT_W = 32;             // words (128 bytes) of a row held in LDS
+constexpr uint32_t MCAP = 24576;           // bytes of one field of a workgroup's rows held in LDS
+constexpr uint32_t MCAPW = MCAP / 4;
+constexpr uint32_t LCAP = 2048;            // listed lead bytes of one field of a workgroup
+constexpr uint32_t CECAP = 512;            // ... 0xCE lead bytes
+constexpr uint32_t SPCAP = 128;            // ... specials walked locally
+// per-row flags (s_rf): matched, and per field the walk it needs
+constexpr uint32_t RF_HIT = 1u;
+__device__ __forceinline__ uint32_t rf_mark(int f) { return 2u << (3 * f); }     // a marked special: walk, fast hits stand
+__device__ __forceinline__ uint32_t rf_decode(int f) { return 4u << (3 * f); }   // an unmarked special: decoding walk, fast hits void
+__device__ __forceinline__ uint32_t rf_hbm(int f) { return 8u << (3 * f); }      // field over the buffer: stream from HBM
 
-// a row's bytes in its lane-major LDS column
-struct LdsCol {
-    const uint32_t *col;
-    __device__ uint8_t operator[](uint32_t i) const { return (uint8_t)(col[(i >> 2) * 64] >> (8u * (i & 3u))); }
+// bytes in LDS
+struct LdsBytes {
+    const uint8_t *b;
+    __device__ uint8_t operator[](uint32_t i) const { return b[i]; }
 };
 
-// the lowered bytes of the non-ASCII unit at g[i] (row g[0, n) in the column), as wg_lower_stream
-__device__ __forceinline__ uint32_t lower_unit(const WgCaseTables &T, const LdsCol &g, uint32_t i, uint32_t n,
-                                               uint32_t *len, uint8_t *buf) {
-    const uint32_t cp = wg_utf8_decode(g, i, n, len);
-    if (cp & 0x80000000u) { buf[0] = (uint8_t)cp; return 1; }
-    if (cp == 0x130) { buf[0] = 'i'; buf[1] = 0xCC; buf[2] = 0x87; return 3; }   // SpecialCasing
-    if (cp == 0x3A3) return wg_utf8_encode(wg_final_sigma(T, g, i, n) ? 0x3C2u : 0x3C3u, buf);
-    return wg_utf8_encode(wg_lower_simple(T, cp), buf);
+// the four bytes of w with 'A'..'Z' lowered (bytes >= 0x80 unchanged)
+__device__ __forceinline__ uint32_t ascii_lower4(uint32_t w) {
+    const uint32_t h = w & 0x7F7F7F7Fu;
+    const uint32_t ge_a = h + 0x3F3F3F3Fu;     // bit 7 set: byte >= 'A'
+    const uint32_t gt_z = h + 0x25252525u;     // bit 7 set: byte > 'Z'
+    const uint32_t up = ge_a & ~gt_z & ~w & 0x80808080u;
+    return w | (up >> 2);
 }
 
-// row's lowered stream against the query: the last <= 8 bytes in a 64-bit
-// shift register (m <= 8), or KMP with q / fail in LDS
-template <bool SHORT>
-__device__ __forceinline__ bool match_row(const WgCaseTables &T, const uint32_t *col, uint32_t n,
-                                          uint64_t qv, uint64_t qmask, const uint8_t *q, const uint16_t *fail, uint32_t m) {
-    uint64_t win = 0;
-    uint32_t fed = 0, k = 0, widx = 0xFFFFFFFFu, w = 0;
-    auto feed = [&](uint32_t c) -> bool {
-        if (SHORT) {
-            win = (win << 8) | c;
-            fed++;
-            return fed >= m && (win & qmask) == qv;
+// bit 7 of each byte of w that equals b
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t b) {
+    const uint32_t x = w ^ (b * 0x01010101u);
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+
+// the largest r < nr with rel[r] <= p (p >= rel[0]): the row holding byte p
+__device__ __forceinline__ uint32_t row_of(const uint32_t *rel, uint32_t nr, uint32_t p) {
+    uint32_t lo = 0, hi = nr;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rel[mid] <= p) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// word k of a field's staged range: bytes [bias, span) of the LDS image hold
+// gp[0, span - bias); aligned words inside by one load, the edge words by bytes
+__device__ __forceinline__ uint32_t stage_word(const uint8_t *gp, uint32_t bias, uint32_t span, uint32_t k) {
+    if (4 * k >= bias && 4 * k + 4 <= span)
+        return __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(gp - bias) + k);
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t pos = 4 * k + j;
+        if (pos >= bias && pos < span) v |= (uint32_t)gp[pos - bias] << (8 * j);
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t hex_char(uint32_t v) { return v < 10 ? '0' + v : 'a' + v - 10; }
+
+// the last <= 16 lowered bytes in two 64-bit shift registers against the query (m <= 16)
+struct FeedShift {
+    uint64_t lo, hi, qlo, qhi, mlo, mhi;
+    uint32_t fed, m;
+    __device__ bool operator()(uint32_t c) {
+        hi = (hi << 8) | (lo >> 56);
+        lo = (lo << 8) | c;
+        fed++;
+        return fed >= m && (lo & mlo) == qlo && (hi & mhi) == qhi;
+    }
+};
+
+// A row of the LDS buffer after the in-place pass: every code point lowered
+// (U+03A3 resolved) except the specials, whose lowering changes the UTF-8
+// length.  A special is either marked — its bytes rewritten as 0xFF, its
+// index, 0xFE... (bytes the lowered query does not hold, and that no raw
+// byte of the workgroup's field is) — or left as it was.  The row's lowered
+// stream: bytes as they stand, a mark expanded to its special's lowered
+// bytes, and with DECODE a raw special lowered again (simple lowercase is
+// idempotent on its image, checked over every code point of the tables, so
+// re-lowering a lowered code point is a no-op; only then is decoding needed).
+// Without marks (the query or the field holds 0xFE / 0xFF) those bytes are
+// the text's own.
+// the matcher the walks feed: the last <= 16 bytes in shift registers
+// (m <= 16), else KMP over the query in HBM
+struct WalkFeed {
+    FeedShift sh;
+    WgKmp km;
+    bool kmp;
+    __device__ bool operator()(uint32_t c) { return kmp ? km((uint8_t)c) : sh(c); }
+};
+
+// the local walk over a marked special (m <= 16): the buffer's bytes as they
+// stand, each mark expanded to its special's lowered bytes
+__device__ __forceinline__ bool walk_marked(const uint8_t *sb, uint32_t a, uint32_t b, const uint32_t *special,
+                                            FeedShift f) {
+    for (uint32_t p = a; p < b; p++) {
+        const uint32_t c = sb[p];
+        if (c < 0xFEu) {
+            if (f(c)) return true;
+        } else if (c == 0xFFu) {
+            const uint32_t x = special[sb[p + 1]];
+            for (uint32_t i = 0; i < (x >> 24); i++)
+                if (f((x >> (8 * i)) & 0xFFu)) return true;
+            p++;
         }
-        while (k && q[k] != c) k = fail[k];
-        if (q[k] == c) k++;
-        return k == m;
-    };
-    for (uint32_t i = 0; i < n;) {
-        if ((i >> 2) != widx) { widx = i >> 2; w = col[widx * 64]; }
-        const uint32_t b0 = (w >> (8u * (i & 3u))) & 0xFFu;
-        if (b0 < 0x80u) {
-            if (feed((b0 - 'A' < 26u) ? b0 + 32 : b0)) return true;
-            i++;
-            continue;
+    }
+    return false;
+}
+
+__device__ bool walk_row(const WgCaseTables &T, const uint32_t *buf, uint32_t rs, uint32_t re, const uint32_t *special,
+                         bool marks, bool decode, WalkFeed feed) {
+    const uint8_t *sb = reinterpret_cast<const uint8_t *>(buf);
+    uint32_t skip = 0;   // bytes still to skip: a mark's index byte, the rest of a decoded code point
+    for (uint32_t k = rs >> 2; 4 * k < re; k++) {
+        const uint32_t w = buf[k];
+        for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t p = 4 * k + j;
+            if (p < rs || p >= re) continue;
+            if (skip) { skip--; continue; }
+            const uint32_t b = (w >> (8 * j)) & 0xFFu;
+            if (b < 0x80u || (!decode && b < 0xFEu)) {
+                if (feed(b)) return true;
+                continue;
+            }
+            if (marks && b == 0xFEu) continue;
+            if (marks && b == 0xFFu) {
+                const uint32_t x = special[sb[p + 1]];
+                for (uint32_t i = 0; i < (x >> 24); i++)
+                    if (feed((x >> (8 * i)) & 0xFFu)) return true;
+                skip = 1;
+                continue;
+            }
+            uint32_t len;   // decode: a raw code point lowered again
+            const uint32_t cp = wg_utf8_decode(LdsBytes{sb + rs}, p - rs, re - rs, &len);
+            uint32_t o, no;
+            if (cp & 0x80000000u) { o = cp & 0xFFu; no = 1; }
+            else if (cp == 0x130u) { o = 'i' | 0xCCu << 8 | 0x87u << 16; no = 3; }
+            else {
+                uint8_t e[4];
+                no = wg_utf8_encode(wg_lower_simple(T, cp), e);
+                o = (uint32_t)e[0] | (uint32_t)e[1] << 8 | (uint32_t)e[2] << 16 | (uint32_t)e[3] << 24;
+            }
+            for (uint32_t i = 0; i < no; i++)
+                if (feed((o >> (8 * i)) & 0xFFu)) return true;
+            skip = len - 1;
         }
-        uint32_t len;
-        uint8_t buf[4];
-        const uint32_t nb = lower_unit(T, LdsCol{col}, i, n, &len, buf);
-        for (uint32_t j = 0; j < nb; j++)
-            if (feed(buf[j])) return true;
-        i += len;
     }
     return false;
 }
 
 __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
-    __shared__ uint32_t s_tt[MT / 64][TT_W * 64];
-    __shared__ uint8_t s_q[QLDS];
-    __shared__ uint16_t s_fail[QLDS];
-    // the case tables (6.5 KiB) and the two-byte range's deltas in LDS
-    __shared__ uint32_t s_lower[WG_LOWER_N][3];
-    __shared__ uint32_t s_cased[WG_CASED_N][2];
-    __shared__ uint32_t s_ign[WG_IGNORABLE_N][2];
-    __shared__ int16_t s_lut2[WG_LUT2_N];
-    for (uint32_t i = threadIdx.x; i < WG_LOWER_N * 3; i += MT) (&s_lower[0][0])[i] = (&c_lower[0][0])[i];
-    for (uint32_t i = threadIdx.x; i < WG_CASED_N * 2; i += MT) (&s_cased[0][0])[i] = (&c_cased[0][0])[i];
-    for (uint32_t i = threadIdx.x; i < WG_IGNORABLE_N * 2; i += MT) (&s_ign[0][0])[i] = (&c_ign[0][0])[i];
-    for (uint32_t i = threadIdx.x; i < WG_LUT2_N / 2; i += MT)
-        reinterpret_cast<uint32_t *>(s_lut2)[i] = reinterpret_cast<const uint32_t *>(A.lut2)[i];
-    const WgCaseTables T{s_lower, s_cased, s_ign, s_lut2};
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t r = A.rb + (uint64_t)blockIdx.x * MT + threadIdx.x;
-    const bool live = r < A.re;
+    __shared__ uint32_t s_buf[MCAPW + 4];
+    __shared__ uint32_t s_rel[MT + 1];
+    __shared__ uint16_t s_lead[LCAP];         // LDS positions of the staged lead bytes (>= 0xC0) other than 0xCE
+    __shared__ uint16_t s_ce[CECAP];          // ... of the 0xCE lead bytes (U+0380..U+03BF; bit 15: a final U+03A3)
+    __shared__ uint32_t s_rf[MT];             // per row: RF_HIT, rf_mark / rf_decode / rf_hbm per field
+    __shared__ uint8_t s_wrow[MT];            // rows to walk whole (this field)
+    __shared__ uint16_t s_spos[SPCAP];        // marked specials the query could overlap: walked locally
+    __shared__ uint32_t s_special[WG_SPECIAL_N];
+    __shared__ uint32_t s_cnt[4];             // leads | 0xCE leads << 16, rows to walk, flags (1: a row starts with a continuation byte, 2: a raw 0xFE / 0xFF byte), specials listed
+    uint8_t *const sb = reinterpret_cast<uint8_t *>(s_buf);
+    const WgCaseTables T{c_lower, c_cased, c_ign, A.flat};
+    const uint32_t *special = s_special;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid < WG_SPECIAL_N) s_special[tid] = A.flat[WG_FLAT_N + tid];
+    const uint64_t r0 = A.rb + (uint64_t)blockIdx.x * MT;
+    const uint32_t nr = (uint32_t)((A.re - r0) < MT ? (A.re - r0) : MT);
     const uint32_t m = A.m;
-    const bool qlds = m <= (uint32_t)QLDS;
-    if (qlds)
-        for (uint32_t i = threadIdx.x; i < m; i += MT) { s_q[i] = A.q[i]; s_fail[i] = A.fail[i]; }
-    uint64_t qv = 0, qmask = 0;   // short queries: the query's bytes as the shift register holds them
-    if (m <= 8)
-        for (uint32_t i = 0; i < m; i++) { qv = (qv << 8) | A.q[i]; qmask = (qmask << 8) | 0xFFu; }
-    __syncthreads();   // tables and query
-    WgKmp km{qlds ? s_q : A.q, qlds ? s_fail : A.fail, m, 0};
-    bool hit = false;
-    uint32_t *col = &s_tt[wv][lane];
-    // summary, then author
+    // the query's first <= 8 bytes little-endian, as an LDS window holds them
+    uint64_t qv = 0, qmask = ~0ull;
+    for (uint32_t i = 0; i < m && i < 8; i++) qv |= (uint64_t)A.q[i] << (8 * i);
+    if (m < 8) qmask = (1ull << (8 * m)) - 1;
+    const uint32_t q0 = (uint32_t)(qv & 0xFFu);
+    // ... and its last <= 16 big-endian, as the walk's shift registers hold them
+    FeedShift sh{0, 0, 0, 0, 0, 0, 0, m};
+    if (m <= 16) {
+        for (uint32_t i = 0; i < m; i++) {
+            if (i + 8 < m) { sh.qhi = (sh.qhi << 8) | A.q[i]; sh.mhi = (sh.mhi << 8) | 0xFFu; }
+            else { sh.qlo = (sh.qlo << 8) | A.q[i]; sh.mlo = (sh.mlo << 8) | 0xFFu; }
+        }
+    }
+    const WalkFeed wf{sh, WgKmp{A.q, A.fail, m, 0}, m > 16};
+    s_rf[tid] = 0;
+    // both fields' row offsets and ranges up front (one round trip)
+    uint64_t orow[2] = {0, 0}, gsf[2] = {0, 0}, gef[2] = {0, 0};
+    for (int f = 0; f < 2; f++) {
+        const uint64_t *off = f ? A.auth_off : A.sum_off;
+        if (!off) continue;
+        gsf[f] = off[r0];
+        gef[f] = off[r0 + nr];
+        if (tid < nr) orow[f] = off[r0 + tid];
+    }
+    constexpr int SB = 4;   // words per thread per staging batch
     for (int f = 0; f < 2; f++) {
         const uint8_t *text = f ? A.auth : A.sum;
         const uint64_t *off = f ? A.auth_off : A.sum_off;
-        if (!off) continue;
-        const uint64_t s = live ? off[r] : 0, n = live ? off[r + 1] - s : 0;
-        const uint8_t *g = text + s;
-        const bool lds = n <= TT_W * 4 && qlds;
-        if (lds && !hit) {
-            // this lane's row into its LDS column: 4-byte windows from aligned words
-            // (a second word only when the window reaches into it: no read past the row)
-            // (only aligned words holding a byte of the row are read; the loads of
-            // a batch are all issued before the first is waited for)
-            const uintptr_t base = reinterpret_cast<uintptr_t>(g);
-            const uint32_t sh = (uint32_t)(base & 3u);
-            const uint32_t *aw = reinterpret_cast<const uint32_t *>(base - sh);
-            const uint32_t nw = (uint32_t)((n + 3) >> 2), naw = (uint32_t)((n + sh + 3) >> 2);
-            for (uint32_t j0 = 0; j0 < nw; j0 += 8) {
-                uint32_t x[9];
-#pragma unroll
-                for (int u = 0; u < 9; u++) x[u] = (j0 + u < naw) ? aw[j0 + u] : 0u;
-#pragma unroll
-                for (int u = 0; u < 8; u++)
-                    if (j0 + u < nw) col[(j0 + u) * 64] = __builtin_amdgcn_alignbyte(x[u + 1], x[u], sh);
-            }
+        if (!off) continue;   // uniform
+        const uint64_t gs = gsf[f], ge = gef[f];
+        const uint8_t *gp = text + gs;
+        const uint32_t bias = (uint32_t)(reinterpret_cast<uintptr_t>(gp) & 3u);
+        const uint64_t span64 = ge - gs + bias;
+        if (span64 > MCAP) {   // uniform: every row of this field takes the stream from HBM
+            if (tid < nr) atomicOr(&s_rf[tid], rf_hbm(f));
+            continue;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (live && !hit && n) {
-            if (lds) {
-                hit = m <= 8 ? match_row<true>(T, col, (uint32_t)n, qv, qmask, s_q, s_fail, m)
-                             : match_row<false>(T, col, (uint32_t)n, qv, qmask, s_q, s_fail, m);
+        const uint32_t span = (uint32_t)span64, nw = (span + 3) >> 2;
+        const uint32_t lo_p = bias, hi_p = span;
+        if (tid < 4) s_cnt[tid] = 0;
+        __syncthreads();   // the previous field's readers are done with the buffer
+        // stage: aligned words inside [gs, ge) by word loads, the (at most two) edge
+        // words by bytes; ASCII lowered on the way in (SWAR; case classes unchanged,
+        // so Final_Sigma below still sees the original's), lead bytes listed
+        // (wave-aggregated: one LDS atomic per wave and batch)
+        {
+            uint32_t raw_ff = 0;
+            for (uint32_t k0 = tid - lane; k0 < nw; k0 += SB * MT) {   // wave-uniform trip count
+                uint32_t v[SB], cnt = 0;
+#pragma unroll
+                for (int u = 0; u < SB; u++) {
+                    const uint32_t k = k0 + lane + u * MT;
+                    v[u] = 0;
+                    if (k < nw) v[u] = stage_word(gp, bias, span, k);
+                }
+#pragma unroll
+                for (int u = 0; u < SB; u++) {
+                    const uint32_t k = k0 + lane + u * MT;
+                    const uint32_t w = v[u];
+                    if (k < nw) s_buf[k] = ascii_lower4(w);
+                    const uint32_t lead = w & (w << 1) & 0x80808080u;   // bytes >= 0xC0
+                    const uint32_t ce = eq_bytes(w, 0xCEu);
+                    cnt += (uint32_t)__builtin_popcount(lead & ~ce) + ((uint32_t)__builtin_popcount(ce) << 16);
+                    raw_ff |= w & (w << 1) & (w << 2) & (w << 3) & (w << 4) & (w << 5) & (w << 6) & 0x80808080u;   // 0xFE / 0xFF
+                }
+                if (__ballot(cnt != 0)) {
+                    uint32_t incl = cnt;
+                    for (uint32_t d = 1; d < 64; d <<= 1) {
+                        const uint32_t t = __shfl_up(incl, d, 64);
+                        if (lane >= d) incl += t;
+                    }
+                    uint32_t base = 0;
+                    if (lane == 63) base = atomicAdd(&s_cnt[0], incl);
+                    base = __shfl(base, 63, 64);
+                    uint32_t il = (base & 0xFFFFu) + ((incl - cnt) & 0xFFFFu), ic = (base >> 16) + ((incl - cnt) >> 16);
+#pragma unroll
+                    for (int u = 0; u < SB; u++) {
+                        const uint32_t w = v[u], k = k0 + lane + u * MT;
+                        const uint32_t lead = w & (w << 1) & 0x80808080u, ce = eq_bytes(w, 0xCEu);
+                        if (!lead) continue;
+                        for (uint32_t j = 0; j < 4; j++) {
+                            if (!((lead >> (8 * j)) & 0x80u)) continue;
+                            if ((ce >> (8 * j)) & 0x80u) {
+                                if (ic < CECAP) s_ce[ic] = (uint16_t)(4 * k + j);
+                                ic++;
+                            } else {
+                                if (il < LCAP) s_lead[il] = (uint16_t)(4 * k + j);
+                                il++;
+                            }
+                        }
+                    }
+                }
+            }
+            if (tid < 4) s_buf[nw + tid] = 0;
+            if (tid < nr) s_rel[tid] = (uint32_t)(orow[f] - gs) + bias;
+            if (tid == 0) s_rel[nr] = span;
+            if (raw_ff) atomicOr(&s_cnt[2], 2u);
+        }
+        __syncthreads();
+        const uint32_t nlead = s_cnt[0] & 0xFFFFu, nce = s_cnt[0] >> 16;
+        if (nlead > LCAP || nce > CECAP) {   // uniform: more code points than the lists hold: the stream from HBM
+            if (tid < nr) atomicOr(&s_rf[tid], rf_hbm(f));
+            continue;
+        }
+        if (tid < nr && s_rel[tid] < s_rel[tid + 1] && (sb[s_rel[tid]] & 0xC0u) == 0x80u) atomicOr(&s_cnt[2], 1u);
+        // Final_Sigma of the U+03A3s, over the original non-ASCII bytes (nothing non-ASCII written yet)
+        for (uint32_t i = tid; i < nce; i += MT) {
+            const uint32_t p = s_ce[i];
+            const uint32_t r = row_of(s_rel, nr, p), rs = s_rel[r], n = s_rel[r + 1] - rs;
+            const LdsBytes g{sb + rs};
+            uint32_t len;
+            if (wg_utf8_decode(g, p - rs, n, &len) == 0x3A3u && wg_final_sigma(T, g, p - rs, n))
+                s_ce[i] = (uint16_t)(p | 0x8000u);
+        }
+        __syncthreads();
+        // lower the listed code points in place (a lead's thread writes its whole
+        // sequence).  Decoded against the end of the staged rows unless a row starts
+        // with a continuation byte (then against their row).  A special is marked
+        // and its row set to walk — unless its lowered bytes share none with the
+        // query: then no match can overlap it; where marks are off it is left
+        // as it was and its row walked by decoding, fast hits void.
+        const uint32_t fl = s_cnt[2];
+        const bool exact = (fl & 1u) != 0, marks = A.marks && !(fl & 2u);
+        for (uint32_t i = tid; i < nlead + nce; i += MT) {
+            const uint32_t e = i < nlead ? s_lead[i] : s_ce[i - nlead];
+            const uint32_t p = e & 0x7FFFu;
+            uint32_t rs = 0, n = hi_p;
+            if (exact) {
+                const uint32_t r = row_of(s_rel, nr, p);
+                rs = s_rel[r];
+                n = s_rel[r + 1] - rs;
+            }
+            uint32_t len;
+            const uint32_t cp = wg_utf8_decode(LdsBytes{sb + rs}, p - rs, n, &len);
+            if (cp & 0x80000000u) continue;   // stands for itself
+            uint32_t lc;
+            if (cp < WG_FLAT_N) {
+                const uint32_t x = A.flat[cp];
+                if (x & WG_FLAT_LENCHG) {   // includes U+0130 -> "i̇"
+                    const uint32_t idx = (x >> WG_FLAT_SPECIAL_SHIFT) & 31u;
+                    if (marks) {
+                        sb[p] = 0xFF;
+                        sb[p + 1] = (uint8_t)idx;
+                        for (uint32_t j = 2; j < len; j++) sb[p + j] = 0xFE;
+                        if ((A.spec_rel >> idx) & 1u) {   // walked locally (windows over it), or the row whole
+                            const uint32_t si = m <= 16 ? atomicAdd(&s_cnt[3], 1u) : SPCAP;
+                            if (si < SPCAP) s_spos[si] = (uint16_t)p;
+                            else atomicOr(&s_rf[row_of(s_rel, nr, p)], rf_mark(f));
+                        }
+                    } else {   // raw bytes stay: no window of the row can be trusted
+                        atomicOr(&s_rf[row_of(s_rel, nr, p)], rf_decode(f));
+                    }
+                    continue;
+                }
+                lc = x & 0xFFFFu;
             } else {
-                km.k = 0;
-                hit = wg_lower_stream(T, g, (uint32_t)n, km);
+                lc = wg_lower_simple(T, cp);
+                if (lc < 0x10000u) {   // none in the tables; walked by decoding if it ever is
+                    atomicOr(&s_rf[row_of(s_rel, nr, p)], rf_decode(f));
+                    continue;
+                }
+            }
+            if (cp == 0x3A3u) lc = (e & 0x8000u) ? 0x3C2u : 0x3C3u;
+            if (lc == cp) continue;
+            uint8_t o[4];
+            wg_utf8_encode(lc, o);
+            for (uint32_t j = 0; j < len; j++) sb[p + j] = o[j];
+        }
+        __syncthreads();
+        if (tid < nr && (s_rf[tid] & (rf_mark(f) | rf_decode(f)))) s_wrow[atomicAdd(&s_cnt[1], 1u)] = (uint8_t)tid;
+        // every byte position holding the query's first byte against its first 8 bytes
+        for (uint32_t k = tid + (lo_p >> 2); 4 * k < hi_p; k += MT) {
+            const uint32_t w0 = s_buf[k];
+            uint32_t cand = eq_bytes(w0, q0);
+            if (!cand) continue;
+            const uint32_t w1 = s_buf[k + 1], w2 = s_buf[k + 2];
+            while (cand) {
+                const uint32_t j = (uint32_t)__builtin_ctz(cand) >> 3;
+                cand &= cand - 1;
+                const uint64_t x = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, j) |
+                                   ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, j) << 32);
+                const uint32_t p = 4 * k + j;
+                if ((x & qmask) != qv || p < lo_p || p + m > hi_p) continue;
+                const uint32_t r = row_of(s_rel, nr, p);
+                if (p + m > s_rel[r + 1] || (s_rf[r] & rf_decode(f))) continue;
+                bool ok = true;
+                for (uint32_t i = 8; i < m && ok; i++) ok = sb[p + i] == A.q[i];
+                if (ok) atomicOr(&s_rf[r], RF_HIT);
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the column is rewritten by the next field
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        // rows with a special the query could overlap, compacted: the row's lowered stream from LDS
+        // ... and the windows over each listed special: the lowered stream from
+        // 3 (m - 1) bytes before it to as many after (each 3 bytes of the buffer
+        // hold at least one lowered byte), entered at a byte outside a mark
+        const uint32_t nwalk = s_cnt[1], nsp = s_cnt[3] < SPCAP ? s_cnt[3] : SPCAP;
+        for (uint32_t i = tid; i < nwalk + nsp; i += MT) {
+            uint32_t row, a, b;
+            bool dec = false;
+            if (i >= nwalk) {
+                const uint32_t p = s_spos[i - nwalk];
+                row = row_of(s_rel, nr, p);
+                const uint32_t rs = s_rel[row], re = s_rel[row + 1], back = 3 * (m - 1);
+                a = p - rs > back ? p - back : rs;
+                while (a < p && (sb[a] == 0xFEu || (a > rs && sb[a - 1] == 0xFFu))) a++;
+                b = re - p > 3 + back ? p + 3 + back : re;
+            } else {
+                row = s_wrow[i];
+                a = s_rel[row];
+                b = s_rel[row + 1];
+                dec = (s_rf[row] & rf_decode(f)) != 0;
+            }
+            if (s_rf[row] & RF_HIT) continue;
+            const bool h = i >= nwalk ? walk_marked(sb, a, b, special, sh) : walk_row(T, s_buf, a, b, special, marks, dec, wf);
+            if (h) atomicOr(&s_rf[row], RF_HIT);
+        }
     }
-    if (live && !hit && m <= 40) {
-        // id hex (lowercase already): short_id contains q (non-synthetic rows), id starts with q
-        uint8_t hex[40];
+    __syncthreads();
+    const bool live = tid < nr;
+    const uint64_t r = r0 + tid;
+    bool hit = live && (s_rf[tid] & RF_HIT);
+    for (int f = 0; f < 2 && live && !hit; f++) {   // fields over the LDS buffer: the stream from HBM
+        const uint8_t *text = f ? A.auth : A.sum;
+        const uint64_t *off = f ? A.auth_off : A.sum_off;
+        if (!off || !(s_rf[tid] & rf_hbm(f))) continue;
+        const uint64_t s = off[r];
+        WgKmp km{A.q, A.fail, m, 0};
+        hit = wg_lower_stream(T, text + s, (uint32_t)(off[r + 1] - s), km);
+    }
+    if (live && !hit && A.qhex) {
+        // the id's hex (lowercase): id starts with q, or short_id (7 digits, non-synthetic rows) contains q
         const uint8_t *id = A.oid + r * 20;
-        for (int i = 0; i < 20; i++) {
-            const uint32_t b = id[i], hi = b >> 4, lo = b & 15;
-            hex[2 * i] = (uint8_t)(hi < 10 ? '0' + hi : 'a' + hi - 10);
-            hex[2 * i + 1] = (uint8_t)(lo < 10 ? '0' + lo : 'a' + lo - 10);
+        const uint32_t w0 = (reinterpret_cast<uintptr_t>(A.oid) & 3u)
+                                ? (uint32_t)id[0] | (uint32_t)id[1] << 8 | (uint32_t)id[2] << 16 | (uint32_t)id[3] << 24
+                                : *reinterpret_cast<const uint32_t *>(id);
+        uint64_t hex8 = 0;
+        for (int i = 0; i < 4; i++) {
+            const uint32_t b = (w0 >> (8 * i)) & 0xFFu;
+            hex8 |= (uint64_t)hex_char(b >> 4) << (16 * i);
+            hex8 |= (uint64_t)hex_char(b & 15u) << (16 * i + 8);
         }
-        const uint8_t *q = km.q;
-        bool pre = true;
-        for (uint32_t i = 0; i < m; i++) pre &= hex[i] == q[i];
-        hit = pre;
-        if (!hit && m <= 7 && !(A.flags[r] & WG_FLAG_SYNTHETIC)) {
-            km.k = 0;
-            for (int i = 0; i < 7 && !hit; i++) hit = km(hex[i]);
+        hit = (hex8 & qmask) == qv;
+        for (uint32_t i = 8; i < m && hit; i++) {
+            const uint32_t b = A.oid[r * 20 + i / 2];
+            hit = hex_char((i & 1) ? (b & 15u) : (b >> 4)) == A.q[i];
         }
+        if (!hit && m <= 7 && !(A.flags[r] & WG_FLAG_SYNTHETIC))
+            for (uint32_t s = 1; s + m <= 7 && !hit; s++) hit = ((hex8 >> (8 * s)) & qmask) == qv;
     }
     if (live) A.out[r - A.rb] = hit ? 1 : 0;
     const int cnt = __syncthreads_count(live && hit);
-    if (threadIdx.x == 0 && cnt) atomicAdd(A.count, (unsigned long long)cnt);
+    if (tid == 0 && cnt) atomicAdd(A.count, (unsigned long long)cnt);
 }
 
 inline uint32_t mblocks(uint64_t n) { return (uint32_t)((n + MT - 1) / MT); }
 
 }  // namespace
+
+// The search kernel's table: per BMP code point its simple lowercase, Cased,
+// Case_Ignorable, and whether lowering changes its UTF-8 length (the
+// "specials": U+0130 -> "i̇" and the simple mappings across a UTF-8 length,
+// each with its index); then per special its lowered bytes | length << 24.
+void wg_match_flat_table(std::vector<uint32_t> &flat) {
+    static std::vector<uint32_t> cache;
+    if (cache.empty()) {
+        const WgCaseTables HT{h_lower, h_cased, h_ign};
+        std::vector<uint32_t> t(WG_FLAT_N + WG_SPECIAL_N, 0);
+        uint32_t ns = 0;
+        auto entry = [&](uint32_t cp) {
+            const uint32_t lc = wg_lower_simple(HT, cp);
+            uint8_t b0[4], b1[4];
+            const uint32_t n0 = wg_utf8_encode(cp, b0), n1 = wg_utf8_encode(lc, b1);
+            uint32_t e = (lc & 0xFFFFu) | (wg_is_cased(HT, cp) ? WG_FLAT_CASED : 0u) | (wg_is_ignorable(HT, cp) ? WG_FLAT_IGN : 0u);
+            if ((cp == 0x130u || lc >= WG_FLAT_N || n0 != n1) && ns < WG_SPECIAL_N) {   // 25 in the tables
+                const uint32_t x = cp == 0x130u ? ('i' | 0xCCu << 8 | 0x87u << 16 | 3u << 24)
+                                                : ((uint32_t)b1[0] | (n1 > 1 ? (uint32_t)b1[1] << 8 : 0u) |
+                                                   (n1 > 2 ? (uint32_t)b1[2] << 16 : 0u) | n1 << 24);
+                t[WG_FLAT_N + ns] = x;
+                e |= WG_FLAT_LENCHG | ns << WG_FLAT_SPECIAL_SHIFT;
+                ns++;
+            }
+            t[cp] = e;
+        };
+        entry(0x130u);   // special 0
+        for (uint32_t cp = 0; cp < WG_FLAT_N; cp++)
+            if (cp != 0x130u) entry(cp);
+        cache.swap(t);
+    }
+    flat = cache;
+}
 
 // Rust `str::to_lowercase` of a byte string on the host (same tables as the device)
 std::vector<uint8_t> wg_lower_host(const uint8_t *p, uint64_t n) {
@@ -285,12 +602,11 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
             }
         }
     }
-    if (!c->match_lut2.p) {   // once per context: the two-byte range's deltas, from the host tables
-        const WgCaseTables HT{h_lower, h_cased, h_ign};
-        std::vector<int16_t> lut(WG_LUT2_N);
-        for (uint32_t cp = 0x80; cp < 0x800; cp++) lut[cp - 0x80] = (int16_t)((int32_t)wg_lower_simple(HT, cp) - (int32_t)cp);
-        WG_ALLOC(c, c->match_lut2, WG_LUT2_N * 2 + 16);
-        WG_HIP(c, hipMemcpyAsync(c->match_lut2.p, lut.data(), WG_LUT2_N * 2, hipMemcpyHostToDevice, s));
+    if (!c->match_flat.p) {   // once per context: the BMP's lowercase and case classes, and the specials
+        std::vector<uint32_t> flat;
+        wg_match_flat_table(flat);
+        WG_ALLOC(c, c->match_flat, flat.size() * 4 + 16);
+        WG_HIP(c, hipMemcpyAsync(c->match_flat.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, s));
         WG_HIP(c, hipStreamSynchronize(s));
     }
     WG_ALLOC(c, c->match_q, 16 + m * 3 + 16);
@@ -312,7 +628,23 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     A.fail = reinterpret_cast<const uint16_t *>(c->match_q.as<uint8_t>() + 16);
     A.q = c->match_q.as<uint8_t>() + 16 + (size_t)m * 2;
     A.m = m;
-    A.lut2 = c->match_lut2.as<const int16_t>();
+    A.qhex = m <= 40;
+    A.marks = 1;
+    for (uint8_t b : q) {
+        A.qhex &= (b - '0' < 10u) || (b - 'a' < 6u);
+        A.marks &= b < 0xFE && b >= WG_SPECIAL_N;   // a mark's bytes never in the query
+    }
+    A.spec_rel = 0;
+    {
+        std::vector<uint32_t> flat;
+        wg_match_flat_table(flat);
+        for (uint32_t i = 0; i < WG_SPECIAL_N; i++) {
+            const uint32_t x = flat[WG_FLAT_N + i];
+            for (uint32_t j = 0; j < (x >> 24); j++)
+                if (std::memchr(q.data(), (int)((x >> (8 * j)) & 0xFFu), q.size())) A.spec_rel |= 1u << i;
+        }
+    }
+    A.flat = c->match_flat.as<const uint32_t>();
     A.out = c->match_flags.as<uint8_t>();
     A.count = c->match_q.as<unsigned long long>();
     wg_stage_begin(c, "match");

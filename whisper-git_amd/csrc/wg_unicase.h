@@ -30,9 +30,17 @@ struct WgCaseTables {
     const uint32_t (*lower)[3];   // WG_LOWER_N    {lo, hi, delta<<2 | step}
     const uint32_t (*cased)[2];   // WG_CASED_N    {lo, hi}
     const uint32_t (*ign)[2];     // WG_IGNORABLE_N
-    const int16_t *lut2 = nullptr;   // optional: simple lowercase delta of U+0080..U+07FF (the two-byte range)
+    // optional: per BMP code point, its simple lowercase | Cased << 16 |
+    // Case_Ignorable << 17 | lowering changes its UTF-8 length << 18 (one
+    // load instead of the range searches; built from the tables above)
+    const uint32_t *flat = nullptr;
 };
-#define WG_LUT2_N (0x800 - 0x80)
+#define WG_FLAT_N 0x10000u
+#define WG_FLAT_CASED (1u << 16)
+#define WG_FLAT_IGN (1u << 17)
+#define WG_FLAT_LENCHG (1u << 18)
+#define WG_FLAT_SPECIAL_SHIFT 19   // bits 19-23: a length-changing code point's index among the specials
+#define WG_SPECIAL_N 32u
 
 // UTF-8 decode at p[i] (i < n).  Returns the code point and its length, or
 // 0x80000000 | byte with length 1 for a byte that starts no well-formed sequence.
@@ -92,7 +100,7 @@ WG_HD inline int wg_range_find(const uint32_t (*tab)[W], int n, uint32_t cp) {
 
 WG_HD inline uint32_t wg_lower_simple(const WgCaseTables &T, uint32_t cp) {
     if (cp < 0x80) return (cp - 'A' < 26u) ? cp + 32 : cp;
-    if (T.lut2 && cp < 0x800) return (uint32_t)((int32_t)cp + T.lut2[cp - 0x80]);
+    if (T.flat && cp < WG_FLAT_N) return T.flat[cp] & 0xFFFFu;
     const int r = wg_range_find<3>(T.lower, WG_LOWER_N, cp);
     if (r < 0 || cp > T.lower[r][1]) return cp;
     const uint32_t step = T.lower[r][2] & 3u;
@@ -107,11 +115,13 @@ WG_HD inline bool wg_in_ranges(const uint32_t (*tab)[2], int n, uint32_t cp) {
 WG_HD inline bool wg_is_cased(const WgCaseTables &T, uint32_t cp) {
     if (cp & 0x80000000u) return false;
     if (cp < 0x80) return (cp | 32u) - 'a' < 26u;
+    if (T.flat && cp < WG_FLAT_N) return (T.flat[cp] & WG_FLAT_CASED) != 0;
     return wg_in_ranges(T.cased, WG_CASED_N, cp);
 }
 WG_HD inline bool wg_is_ignorable(const WgCaseTables &T, uint32_t cp) {
     if (cp & 0x80000000u) return false;
     if (cp < 0x80) return cp == '\'' || cp == '.' || cp == ':' || cp == '^' || cp == '`';
+    if (T.flat && cp < WG_FLAT_N) return (T.flat[cp] & WG_FLAT_IGN) != 0;
     return wg_in_ranges(T.ign, WG_IGNORABLE_N, cp);
 }
 

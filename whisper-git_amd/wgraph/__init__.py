@@ -367,11 +367,12 @@ class Engine:
             self._band = b
             self._check(lib().wg_row_geometry(self._ctx, b.ctypes.data, abi.WG_HOST))
 
-    def row_geometry_list(self, dag, band=None):
+    def row_geometry_list(self, dag=None, band=None, commits: abi.Commits | None = None):
         """row_geometry_with_bands(commits, band_heights) with its commits
-        argument (wg_row_geometry_list): heights from dag's times, geometry
-        from the built edges; dag must have the built list's length."""
-        c = abi.commits_struct(dag)
+        argument (wg_row_geometry_list): heights from dag's times (or a
+        prepared wg_commits, e.g. device-resident), geometry from the built
+        edges; the list must have the built list's length."""
+        c = abi.commits_struct(dag) if commits is None else commits
         self._keep_list = [dag, c]
         b = None
         if band is not None:
