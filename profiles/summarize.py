@@ -27,6 +27,12 @@ def short(name: str) -> str:
     return re.sub(r"\(.*", "", name)
 
 
+def is_kernel(name: str) -> bool:
+    """KERNEL, plain or as a template instance (void k_vtx_tile<1024>, r05)."""
+    s = short(name)
+    return s == KERNEL or re.fullmatch(r"(void )?" + KERNEL + r"<[^>]*>", s) is not None
+
+
 def read_csv(path):
     with open(path, newline="") as f:
         return list(csv.DictReader(f))
@@ -87,7 +93,7 @@ def main():
     full = [w for w in windows[:-1] if w[2] >= 20]
     timed = sorted(full)[:5]
 
-    vtx = next((r for r in stats if short(r["Name"]) == KERNEL), None)
+    vtx = next((r for r in stats if is_kernel(r["Name"])), None)
     lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py --steps 5 --warmup 2 --no-cpu --no-extras`", ""]
     if bench:
         lines += [f"bench line under the profiler: value {bench['value']:.4g} {bench['unit']}, "
@@ -111,7 +117,7 @@ def main():
             continue
         per = defaultdict(float)
         for r in read_csv(p):
-            if r["Counter_Name"] == cname and short(r["Kernel_Name"]) == KERNEL:
+            if r["Counter_Name"] == cname and is_kernel(r["Kernel_Name"]):
                 per[r["Dispatch_Id"]] += float(r["Counter_Value"])
         if per:
             pmc[cname.lower() + "_kib_per_launch"] = sum(per.values()) / len(per)

@@ -121,12 +121,16 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
     uint32_t cd = 0;
     if (r < n) {
         uint32_t b = 0, f = 0, cc = 0, ce = 0;
-        auto count = [&](uint32_t c, uint32_t p, bool same) {
-            if (c >= p) return;
-            cd += c / WG_SWEEP_CH + 1 <= p / WG_SWEEP_CH;
-            if (same) { b++; f += c + 1 < p; }
-            else { cc += c + 1 < p; ce++; }   // (the swept lists' flag row is all zero: no child-end filter)
-        };
+        // (plain accumulation, no by-reference closure: that put the counters in scratch)
+#define WG_EDGE_COUNT(c_, p_, same_)                                                                 \
+    do {                                                                                             \
+        const uint32_t c = (c_), p = (p_);                                                           \
+        if (c < p) {                                                                                 \
+            cd += c / WG_SWEEP_CH + 1 <= p / WG_SWEEP_CH;                                            \
+            if (same_) { b++; f += c + 1 < p; }                                                      \
+            else { cc += c + 1 < p; ce++; }   /* (the swept lists' flag row is all zero: no child-end filter) */ \
+        }                                                                                            \
+    } while (0)
         if (A.prow) {
             uint32_t o = A.edge_off[r];
             const uint32_t cl = A.lane_out[r], col = A.color_out[r];
@@ -141,14 +145,15 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
                 e.color = col;
                 A.edges[o] = e;
                 o++;
-                count(e.child_row, e.parent_row, e.child_lane == e.parent_lane);
+                WG_EDGE_COUNT(e.child_row, e.parent_row, e.child_lane == e.parent_lane);
             }
         } else {
             for (uint32_t k = A.edge_off[r]; k < A.edge_off[r + 1]; k++) {
                 const wg_edge e = A.edges[k];
-                count(e.child_row, e.parent_row, e.child_lane == e.parent_lane);
+                WG_EDGE_COUNT(e.child_row, e.parent_row, e.child_lane == e.parent_lane);
             }
         }
+#undef WG_EDGE_COUNT
         A.cntB[r] = b;
         A.diffF[r + 1] = f;
         A.diffC[r + 1] = cc;
