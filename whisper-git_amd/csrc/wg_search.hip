@@ -11,11 +11,13 @@
 // wg_emit_vertices / wg_emit_glyphs scale their alpha by WG_DIM_ALPHA.
 //
 // Per-row byte work (~the text bytes + 20 B of id per row).  A workgroup
-// owns 256 rows and takes their fields one at a time, with every lane busy
-// in each pass (LDS-resident, barrier-separated):
-//  1. stage: the field's bytes of all 256 rows (one contiguous range) into
+// owns 256 rows and stages both their fields into one LDS image when they fit
+// (else one field per pass), with every lane busy in each phase
+// (LDS-resident, barrier-separated):
+//  1. stage: each field's bytes of the 256 rows (one contiguous range) into
 //     LDS by coalesced word loads, ASCII lowered on the way in (SWAR), the
-//     lead bytes of non-ASCII code points listed (wave-aggregated appends);
+//     lead bytes of non-ASCII code points listed (wave-aggregated appends;
+//     the 0xCE leads from the top of the same list);
 //  2. Final_Sigma for the listed 0xCE leads that are U+03A3, over the
 //     original bytes (ASCII lowering keeps case classes);
 //  3. the listed code points lowered IN PLACE by the thread holding the list
@@ -71,10 +73,9 @@ struct MatchArgs {
     unsigned long long *count;
 };
 
-constexpr uint32_t MCAP = 24576;           // bytes of one field of a workgroup's rows held in LDS
+constexpr uint32_t MCAP = 22528;           // bytes of a workgroup's staged fields held in LDS
 constexpr uint32_t MCAPW = MCAP / 4;
-constexpr uint32_t LCAP = 2048;            // listed lead bytes of one field of a workgroup
-constexpr uint32_t CECAP = 512;            // ... 0xCE lead bytes
+constexpr uint32_t LCAP = 2560;            // listed lead bytes of a pass (the 0xCE leads from the top down, the others from the bottom up)
 constexpr uint32_t SPCAP = 128;            // ... specials walked locally
 // per-row flags (s_rf): matched, and per field the walk it needs
 constexpr uint32_t RF_HIT = 1u;
@@ -222,11 +223,12 @@ __device__ bool walk_row(const WgCaseTables &T, const uint32_t *buf, uint32_t rs
 
 __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     __shared__ uint32_t s_buf[MCAPW + 4];
-    __shared__ uint32_t s_rel[MT + 1];
-    __shared__ uint16_t s_lead[LCAP];         // LDS positions of the staged lead bytes (>= 0xC0) other than 0xCE
-    __shared__ uint16_t s_ce[CECAP];          // ... of the 0xCE lead bytes (U+0380..U+03BF; bit 15: a final U+03A3)
+    __shared__ uint32_t s_rel[2][MT + 1];     // per region of the staged image: its rows' byte offsets in it
+    __shared__ uint16_t s_lead[LCAP];         // LDS positions of the staged lead bytes (>= 0xC0): others at [0, n), 0xCE
+                                              // (U+0380..U+03BF; bit 15: a final U+03A3) at [LCAP - nce, LCAP)
+    uint16_t *const s_ce = s_lead + LCAP;     // (s_ce[-1 - i]: the i-th 0xCE lead)
     __shared__ uint32_t s_rf[MT];             // per row: RF_HIT, rf_mark / rf_decode / rf_hbm per field
-    __shared__ uint8_t s_wrow[MT];            // rows to walk whole (this field)
+    __shared__ uint16_t s_wrow[2 * MT];       // rows to walk whole: row | region << 8
     __shared__ uint16_t s_spos[SPCAP];        // marked specials the query could overlap: walked locally
     __shared__ uint32_t s_special[WG_SPECIAL_N];
     __shared__ uint32_t s_cnt[4];             // leads | 0xCE leads << 16, rows to walk, flags (1: a row starts with a continuation byte, 2: a raw 0xFE / 0xFF byte), specials listed
@@ -262,42 +264,74 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         gef[f] = off[r0 + nr];
         if (tid < nr) orow[f] = off[r0 + tid];
     }
-    constexpr int SB = 4;   // words per thread per staging batch
+    // The fields' images in LDS: both in one pass when they fit together
+    // (summary words, one zero word, author words), else one pass each; a
+    // field past the buffer takes the stream from HBM.  Each staged field is
+    // a region of the pass.
+    uint32_t fspan[2] = {0, 0};
+    bool fst[2] = {false, false};
     for (int f = 0; f < 2; f++) {
-        const uint8_t *text = f ? A.auth : A.sum;
-        const uint64_t *off = f ? A.auth_off : A.sum_off;
-        if (!off) continue;   // uniform
-        const uint64_t gs = gsf[f], ge = gef[f];
-        const uint8_t *gp = text + gs;
-        const uint32_t bias = (uint32_t)(reinterpret_cast<uintptr_t>(gp) & 3u);
-        const uint64_t span64 = ge - gs + bias;
-        if (span64 > MCAP) {   // uniform: every row of this field takes the stream from HBM
-            if (tid < nr) atomicOr(&s_rf[tid], rf_hbm(f));
+        if (!(f ? A.auth_off : A.sum_off)) continue;
+        const uint8_t *gp = (f ? A.auth : A.sum) + gsf[f];
+        const uint64_t span = gef[f] - gsf[f] + (reinterpret_cast<uintptr_t>(gp) & 3u);
+        if (span > MCAP) {
+            if (tid < nr) s_rf[tid] |= rf_hbm(f);   // (each thread its own row; read after a barrier)
             continue;
         }
-        const uint32_t span = (uint32_t)span64, nw = (span + 3) >> 2;
-        const uint32_t lo_p = bias, hi_p = span;
+        fspan[f] = (uint32_t)span;
+        fst[f] = true;
+    }
+    const bool both = fst[0] && fst[1] && ((fspan[0] + 3) >> 2) + 1 + ((fspan[1] + 3) >> 2) <= MCAPW;
+    const int npass = both ? 1 : (int)fst[0] + (int)fst[1];
+    constexpr int SB = 4;   // words per thread per staging batch
+    for (int pass = 0; pass < npass; pass++) {
+        // the pass's regions (uniform): field, text, bias, image span, first word
+        const uint32_t ng = both ? 2u : 1u;
+        int fg[2];
+        fg[0] = both ? 0 : (pass == 0 ? (fst[0] ? 0 : 1) : 1);
+        fg[1] = 1;
+        const uint8_t *gpg[2];
+        uint32_t biasg[2], spang[2], nwg[2], baseg[2];
+        for (uint32_t g = 0; g < 2; g++) {
+            const int f = fg[g];
+            gpg[g] = (f ? A.auth : A.sum) + gsf[f];
+            biasg[g] = (uint32_t)(reinterpret_cast<uintptr_t>(gpg[g]) & 3u);
+            spang[g] = fspan[f];
+            nwg[g] = (spang[g] + 3) >> 2;
+        }
+        baseg[0] = 0;
+        baseg[1] = nwg[0] + 1;
+        const uint32_t tw = ng == 2 ? baseg[1] + nwg[1] : nwg[0];   // words of the image
+        const uint32_t pb1 = ng == 2 ? 4 * baseg[1] : 0xFFFFFFFFu;   // first byte of region 1
+        uint32_t lo[2], hi[2];
+        for (uint32_t g = 0; g < 2; g++) {
+            lo[g] = 4 * baseg[g] + biasg[g];
+            hi[g] = 4 * baseg[g] + spang[g];
+        }
+        auto reg = [&](uint32_t p) -> uint32_t { return p >= pb1 ? 1u : 0u; };
         if (tid < 4) s_cnt[tid] = 0;
-        __syncthreads();   // the previous field's readers are done with the buffer
-        // stage: aligned words inside [gs, ge) by word loads, the (at most two) edge
-        // words by bytes; ASCII lowered on the way in (SWAR; case classes unchanged,
-        // so Final_Sigma below still sees the original's), lead bytes listed
-        // (wave-aggregated: one LDS atomic per wave and batch)
+        __syncthreads();   // the previous pass's readers are done with the buffer
+        // stage: aligned words inside each field's range by word loads, the edge
+        // words by bytes; ASCII lowered on the way in (SWAR; case classes
+        // unchanged, so Final_Sigma below still sees the original's), lead bytes
+        // listed (wave-aggregated: one LDS atomic per wave and batch)
         {
             uint32_t raw_ff = 0;
-            for (uint32_t k0 = tid - lane; k0 < nw; k0 += SB * MT) {   // wave-uniform trip count
+            for (uint32_t k0 = tid - lane; k0 < tw; k0 += SB * MT) {   // wave-uniform trip count
                 uint32_t v[SB], cnt = 0;
 #pragma unroll
                 for (int u = 0; u < SB; u++) {
                     const uint32_t k = k0 + lane + u * MT;
+                    const uint32_t g = (ng == 2 && k >= baseg[1]) ? 1u : 0u;
+                    const uint32_t kk = k - baseg[g];
                     v[u] = 0;
-                    if (k < nw) v[u] = stage_word(gp, bias, span, k);
+                    if (k < tw && kk < nwg[g]) v[u] = stage_word(gpg[g], biasg[g], spang[g], kk);
                 }
 #pragma unroll
                 for (int u = 0; u < SB; u++) {
                     const uint32_t k = k0 + lane + u * MT;
                     const uint32_t w = v[u];
-                    if (k < nw) s_buf[k] = ascii_lower4(w);
+                    if (k < tw) s_buf[k] = ascii_lower4(w);
                     const uint32_t lead = w & (w << 1) & 0x80808080u;   // bytes >= 0xC0
                     const uint32_t ce = eq_bytes(w, 0xCEu);
                     cnt += (uint32_t)__builtin_popcount(lead & ~ce) + ((uint32_t)__builtin_popcount(ce) << 16);
@@ -321,7 +355,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                         for (uint32_t j = 0; j < 4; j++) {
                             if (!((lead >> (8 * j)) & 0x80u)) continue;
                             if ((ce >> (8 * j)) & 0x80u) {
-                                if (ic < CECAP) s_ce[ic] = (uint16_t)(4 * k + j);
+                                if (ic < LCAP) s_ce[-1 - (int)ic] = (uint16_t)(4 * k + j);
                                 ic++;
                             } else {
                                 if (il < LCAP) s_lead[il] = (uint16_t)(4 * k + j);
@@ -331,30 +365,35 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                     }
                 }
             }
-            if (tid < 4) s_buf[nw + tid] = 0;
-            if (tid < nr) s_rel[tid] = (uint32_t)(orow[f] - gs) + bias;
-            if (tid == 0) s_rel[nr] = span;
+            if (tid < 4) s_buf[tw + tid] = 0;
+            for (uint32_t g = 0; g < ng; g++) {
+                if (tid < nr) s_rel[g][tid] = 4 * baseg[g] + (uint32_t)(orow[fg[g]] - gsf[fg[g]]) + biasg[g];
+                if (tid == 0) s_rel[g][nr] = hi[g];
+            }
             if (raw_ff) atomicOr(&s_cnt[2], 2u);
         }
         __syncthreads();
         const uint32_t nlead = s_cnt[0] & 0xFFFFu, nce = s_cnt[0] >> 16;
-        if (nlead > LCAP || nce > CECAP) {   // uniform: more code points than the lists hold: the stream from HBM
-            if (tid < nr) atomicOr(&s_rf[tid], rf_hbm(f));
+        if (nlead + nce > LCAP) {   // uniform: more code points than the lists hold: the stream from HBM
+            for (uint32_t g = 0; g < ng; g++)
+                if (tid < nr) atomicOr(&s_rf[tid], rf_hbm(fg[g]));
             continue;
         }
-        if (tid < nr && s_rel[tid] < s_rel[tid + 1] && (sb[s_rel[tid]] & 0xC0u) == 0x80u) atomicOr(&s_cnt[2], 1u);
+        for (uint32_t g = 0; g < ng; g++)
+            if (tid < nr && s_rel[g][tid] < s_rel[g][tid + 1] && (sb[s_rel[g][tid]] & 0xC0u) == 0x80u) atomicOr(&s_cnt[2], 1u);
         // Final_Sigma of the U+03A3s, over the original non-ASCII bytes (nothing non-ASCII written yet)
         for (uint32_t i = tid; i < nce; i += MT) {
-            const uint32_t p = s_ce[i];
-            const uint32_t r = row_of(s_rel, nr, p), rs = s_rel[r], n = s_rel[r + 1] - rs;
+            const uint32_t p = s_ce[-1 - (int)i];
+            const uint32_t *rel = s_rel[reg(p)];
+            const uint32_t r = row_of(rel, nr, p), rs = rel[r], n = rel[r + 1] - rs;
             const LdsBytes g{sb + rs};
             uint32_t len;
             if (wg_utf8_decode(g, p - rs, n, &len) == 0x3A3u && wg_final_sigma(T, g, p - rs, n))
-                s_ce[i] = (uint16_t)(p | 0x8000u);
+                s_ce[-1 - (int)i] = (uint16_t)(p | 0x8000u);
         }
         __syncthreads();
         // lower the listed code points in place (a lead's thread writes its whole
-        // sequence).  Decoded against the end of the staged rows unless a row starts
+        // sequence).  Decoded against the end of their region unless a row starts
         // with a continuation byte (then against their row).  A special is marked
         // and its row set to walk — unless its lowered bytes share none with the
         // query: then no match can overlap it; where marks are off it is left
@@ -362,13 +401,14 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         const uint32_t fl = s_cnt[2];
         const bool exact = (fl & 1u) != 0, marks = A.marks && !(fl & 2u);
         for (uint32_t i = tid; i < nlead + nce; i += MT) {
-            const uint32_t e = i < nlead ? s_lead[i] : s_ce[i - nlead];
-            const uint32_t p = e & 0x7FFFu;
-            uint32_t rs = 0, n = hi_p;
+            const uint32_t e = i < nlead ? s_lead[i] : s_ce[-1 - (int)(i - nlead)];
+            const uint32_t p = e & 0x7FFFu, g = reg(p);
+            const uint32_t *rel = s_rel[g];
+            uint32_t rs = 0, n = hi[g];
             if (exact) {
-                const uint32_t r = row_of(s_rel, nr, p);
-                rs = s_rel[r];
-                n = s_rel[r + 1] - rs;
+                const uint32_t r = row_of(rel, nr, p);
+                rs = rel[r];
+                n = rel[r + 1] - rs;
             }
             uint32_t len;
             const uint32_t cp = wg_utf8_decode(LdsBytes{sb + rs}, p - rs, n, &len);
@@ -385,10 +425,10 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                         if ((A.spec_rel >> idx) & 1u) {   // walked locally (windows over it), or the row whole
                             const uint32_t si = m <= 16 ? atomicAdd(&s_cnt[3], 1u) : SPCAP;
                             if (si < SPCAP) s_spos[si] = (uint16_t)p;
-                            else atomicOr(&s_rf[row_of(s_rel, nr, p)], rf_mark(f));
+                            else atomicOr(&s_rf[row_of(rel, nr, p)], rf_mark(fg[g]));
                         }
                     } else {   // raw bytes stay: no window of the row can be trusted
-                        atomicOr(&s_rf[row_of(s_rel, nr, p)], rf_decode(f));
+                        atomicOr(&s_rf[row_of(rel, nr, p)], rf_decode(fg[g]));
                     }
                     continue;
                 }
@@ -396,7 +436,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
             } else {
                 lc = wg_lower_simple(T, cp);
                 if (lc < 0x10000u) {   // none in the tables; walked by decoding if it ever is
-                    atomicOr(&s_rf[row_of(s_rel, nr, p)], rf_decode(f));
+                    atomicOr(&s_rf[row_of(rel, nr, p)], rf_decode(fg[g]));
                     continue;
                 }
             }
@@ -407,9 +447,11 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
             for (uint32_t j = 0; j < len; j++) sb[p + j] = o[j];
         }
         __syncthreads();
-        if (tid < nr && (s_rf[tid] & (rf_mark(f) | rf_decode(f)))) s_wrow[atomicAdd(&s_cnt[1], 1u)] = (uint8_t)tid;
+        for (uint32_t g = 0; g < ng; g++)
+            if (tid < nr && (s_rf[tid] & (rf_mark(fg[g]) | rf_decode(fg[g]))))
+                s_wrow[atomicAdd(&s_cnt[1], 1u)] = (uint16_t)(tid | g << 8);
         // every byte position holding the query's first byte against its first 8 bytes
-        for (uint32_t k = tid + (lo_p >> 2); 4 * k < hi_p; k += MT) {
+        for (uint32_t k = tid + (lo[0] >> 2); k < tw; k += MT) {
             const uint32_t w0 = s_buf[k];
             uint32_t cand = eq_bytes(w0, q0);
             if (!cand) continue;
@@ -419,10 +461,11 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                 cand &= cand - 1;
                 const uint64_t x = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, j) |
                                    ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, j) << 32);
-                const uint32_t p = 4 * k + j;
-                if ((x & qmask) != qv || p < lo_p || p + m > hi_p) continue;
-                const uint32_t r = row_of(s_rel, nr, p);
-                if (p + m > s_rel[r + 1] || (s_rf[r] & rf_decode(f))) continue;
+                const uint32_t p = 4 * k + j, g = reg(p);
+                if ((x & qmask) != qv || p < lo[g] || p + m > hi[g]) continue;
+                const uint32_t *rel = s_rel[g];
+                const uint32_t r = row_of(rel, nr, p);
+                if (p + m > rel[r + 1] || (s_rf[r] & rf_decode(fg[g]))) continue;
                 bool ok = true;
                 for (uint32_t i = 8; i < m && ok; i++) ok = sb[p + i] == A.q[i];
                 if (ok) atomicOr(&s_rf[r], RF_HIT);
@@ -439,16 +482,18 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
             bool dec = false;
             if (i >= nwalk) {
                 const uint32_t p = s_spos[i - nwalk];
-                row = row_of(s_rel, nr, p);
-                const uint32_t rs = s_rel[row], re = s_rel[row + 1], back = 3 * (m - 1);
+                const uint32_t *rel = s_rel[reg(p)];
+                row = row_of(rel, nr, p);
+                const uint32_t rs = rel[row], re = rel[row + 1], back = 3 * (m - 1);
                 a = p - rs > back ? p - back : rs;
                 while (a < p && (sb[a] == 0xFEu || (a > rs && sb[a - 1] == 0xFFu))) a++;
                 b = re - p > 3 + back ? p + 3 + back : re;
             } else {
-                row = s_wrow[i];
-                a = s_rel[row];
-                b = s_rel[row + 1];
-                dec = (s_rf[row] & rf_decode(f)) != 0;
+                const uint32_t e = s_wrow[i], g = e >> 8;
+                row = e & 0xFFu;
+                a = s_rel[g][row];
+                b = s_rel[g][row + 1];
+                dec = (s_rf[row] & rf_decode(fg[g])) != 0;
             }
             if (s_rf[row] & RF_HIT) continue;
             const bool h = i >= nwalk ? walk_marked(sb, a, b, special, sh) : walk_row(T, s_buf, a, b, special, marks, dec, wf);
