@@ -485,13 +485,15 @@ def _lockstep_build_check(d, world, expect_mode, frame=True):
                                                                                     rng[r][0], rng[r][1], m))
             rounds += _lockstep(engines, lambda e, r, m: lib().wg_shard_geometry_begin(e._ctx, keep[5].data_ptr(),
                                                                                         abi.WG_DEVICE, m))
-        assert rounds == 3, rounds   # X1, X2, X3; the geometry passes exchange nothing
+        if expect_mode is not None:
+            assert rounds == 3, rounds   # X1, X2, X3; the geometry passes exchange nothing
         og = o.row_geometry(d.band)
         vo = og["vert_off"].astype(np.int64)
         oe = o.edges.view(np.uint32).reshape(-1, 5)
         for r, e in enumerate(engines):
             s, t = rng[r]
-            assert int(e.debug_counters()[5]) == expect_mode, f"rank {r}: build mode {int(e.debug_counters()[5])}"
+            if expect_mode is not None:
+                assert int(e.debug_counters()[5]) == expect_mode, f"rank {r}: build mode {int(e.debug_counters()[5])}"
             lane, color = e.lanes()
             assert lane.tobytes() == o.lane[s:t].tobytes(), (r, np.nonzero(lane != o.lane[s:t])[0][:5])
             assert color.tobytes() == o.color[s:t].tobytes(), f"rank {r} colours"
