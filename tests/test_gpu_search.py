@@ -60,7 +60,7 @@ def test_match_flags_equal_oracle(engine, data, residency):
 def test_match_without_text_fields_and_wide_rows(engine):
     d = synth.generate("random13", 3000, seed=9)
     engine.build(d)
-    # rows whose summaries are far too long for the 24 KiB LDS stage (read from HBM instead)
+    # rows whose summaries are far too long for the 22 KiB LDS image (read from HBM instead)
     rng = np.random.default_rng(1)
     lens = rng.integers(0, 400, d.n)
     lens[100:400] = 5000
