@@ -19,7 +19,7 @@
 typedef float v4f __attribute__((ext_vector_type(4)));
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
-enum { MAP_DISPATCH = 0, MAP_XCD = 1, MAP_PERSIST_STRIDE = 2, MAP_PERSIST_CONTIG = 3, MAP_XCD_STAGGER = 4, MAP_XCD_DYN = 5 };
+enum { MAP_DISPATCH = 0, MAP_XCD = 1, MAP_PERSIST_STRIDE = 2, MAP_PERSIST_CONTIG = 3, MAP_XCD_STAGGER = 4, MAP_XCD_DYN = 5, MAP_XCD_PERSIST = 6 };
 
 template <bool NT, int R, int TH>
 __device__ __forceinline__ void write_tile(v4f *out, size_t n, size_t t) {
@@ -69,6 +69,13 @@ __global__ void __launch_bounds__(TH) k_tiles(v4f *out, size_t n, size_t ntiles,
         const size_t per = (ntiles + 7) / 8, x = b % 8;
         const size_t t = x * per + (b / 8 + x * per / 8) % per;
         if (b / 8 < per && t < ntiles) write_tile<NT, R, TH>(out, n, t);
+    } else if (MAP == MAP_XCD_PERSIST) {
+        // persistent, XCD-split: XCD x's g / 8 workgroups stride through its
+        // contiguous eighth (the workgroups of one XCD write neighbouring tiles
+        // at any moment, as the one-tile xcd-split does)
+        const size_t per = (ntiles + 7) / 8, x = b % 8, k = g / 8;
+        for (size_t j = b / 8; j < per; j += k)
+            if (x * per + j < ntiles) write_tile<NT, R, TH>(out, n, x * per + j);
     } else if (MAP == MAP_PERSIST_STRIDE) {
         for (size_t t = b; t < ntiles; t += g) write_tile<NT, R, TH>(out, n, t);
     } else {
@@ -123,6 +130,9 @@ int main(int argc, char **argv) {
         });                                                                                                    \
     }
     V(true, 6, 256, MAP_XCD, 0, "24KiB/256 nt xcd-split");
+    V(true, 6, 256, MAP_XCD_PERSIST, 2048, "24KiB/256 nt xcd-persist 2048");
+    V(true, 6, 256, MAP_XCD_PERSIST, 4096, "24KiB/256 nt xcd-persist 4096");
+    V(true, 6, 256, MAP_XCD_PERSIST, 8192, "24KiB/256 nt xcd-persist 8192");
     V(true, 6, 256, MAP_XCD_DYN, 0, "24KiB/256 nt xcd-dynamic");
     V(true, 3, 256, MAP_XCD, 0, "12KiB/256 nt xcd-split");
     V(true, 3, 256, MAP_XCD_DYN, 0, "12KiB/256 nt xcd-dynamic");
