@@ -149,6 +149,38 @@ def test_match_dense_non_ascii_fields(engine):
         engine.match_rows("")
 
 
+@pytest.mark.parametrize("sum_len,auth_len", [(60, 20), (60, 40), (80, 6), (0, 70)])
+def test_match_fields_together_or_apart(engine, sum_len, auth_len):
+    """The kernel stages a workgroup's two fields into one LDS image when they
+    fit together and in two passes when they do not (about 60 + 40 bytes per
+    row is past the image, 60 + 20 is within it, 80 + 6 sits at the edge, an
+    empty summary field leaves the authors alone): the same flags either way."""
+    d = synth.generate("random13", 1500, seed=8)
+    engine.build(d)
+    rng = np.random.default_rng(sum_len * 7 + auth_len)
+    words = ["ΣΟΦΙΑ", "İstanbul", "fix", "Graph", "STRAẞE", "ος", "kelvin", "Åse", "a", "ǅ"]
+
+    def field(mean):
+        rows = []
+        for _ in range(d.n):
+            s = ""
+            target = int(rng.integers(max(0, mean - 8), mean + 9)) if mean else 0
+            while len(s.encode()) < target:
+                s += words[int(rng.integers(0, len(words)))] + " "
+            rows.append(s.encode()[:target] if target else b"")
+        off = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.uint64)
+        return np.frombuffer(b"".join(rows) or b"\0", np.uint8)[:int(off[-1])], off
+
+    summ, auth = field(sum_len), field(auth_len)
+    try:
+        for q in ("fix", "σοφ", "i̇", "ος ", "ss", "å", "ǆ", "a a"):
+            n = engine.match_rows(q, summaries=summ, authors=auth)
+            want, wn = so.match_rows(d, q.encode(), summ, auth)
+            assert n == wn and (engine.match_flags() == want).all(), (q, sum_len, auth_len)
+    finally:
+        engine.match_rows("")
+
+
 def test_empty_query_matches_all_and_build_clears(engine, data):
     d, summ, auth = data
     engine.build(d)
