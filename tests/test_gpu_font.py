@@ -41,3 +41,25 @@ def test_small_atlas_and_errors(engine):
         engine.build_font_atlas(0, width=64, height=64, em_px=96.0)     # does not fit
     with pytest.raises(WgError):
         engine.build_font_atlas(1, ttf=b"not a font")
+
+
+def test_rebuilds_reuse_the_parse_and_follow_changes(engine):
+    """A rebuild of the same font at the same parameters skips the TrueType
+    parse and the uploads (the slot keeps the font's length, hash and
+    parameters) and still gives the golden bytes; a different font or
+    parameter in the same slot is parsed again, and a failed build in between
+    leaves nothing to reuse."""
+    from wgraph import FONTS, WgError
+    z = [np.load(os.path.join(GOLDEN_DIR, f"font_{n}.npz"), allow_pickle=False) for n in ("regular", "bold")]
+    w, h, em, sp, first, last = z[0]["params"]
+    kw = dict(width=int(w), height=int(h), em_px=float(em), spread=int(sp), first=int(first), last=int(last))
+    bold = open(FONTS[1], "rb").read()
+    for ttf, want in ((None, 0), (None, 0), (bold, 1), (bold, 1), (None, 0)):
+        engine.build_font_atlas(0, ttf=ttf, **kw)
+        a = engine.atlas(0)
+        np.testing.assert_array_equal(a["sdf"], z[want]["sdf"])
+        assert a["glyphs"].tobytes() == z[want]["glyphs"].tobytes()
+    with pytest.raises(WgError):
+        engine.build_font_atlas(0, width=64, height=64, em_px=96.0)      # does not fit: the slot's key is dropped
+    engine.build_font_atlas(0, **kw)
+    np.testing.assert_array_equal(engine.atlas(0)["sdf"], z[0]["sdf"])

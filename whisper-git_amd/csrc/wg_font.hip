@@ -418,6 +418,46 @@ void flatten(const std::vector<Font::Pt> &c, float scale, std::vector<float4> &o
 
 }  // namespace
 
+// 64-bit hash of the font's bytes (word-wise multiply-xorshift), for the rebuild check
+static uint64_t font_bytes_hash(const uint8_t *p, uint64_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+    uint64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        std::memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+        h ^= h >> 32;
+    }
+    for (; i < n; i++) h = (h ^ p[i]) * 0x100000001B3ull;
+    return h ^ (h >> 29);
+}
+
+// coverage then the two EDT passes over the slot's uploaded outlines
+static int font_atlas_run(wg_ctx *c, FontSlot &S) {
+    hipStream_t s = c->stream;
+    const uint32_t W = S.W, H = S.H, spread = S.spread;
+    const uint64_t npx = (uint64_t)W * H;
+    wg_stage_begin(c, "font_atlas");
+    wg_stage_begin(c, "font_coverage");
+    WG_HIP(c, hipMemsetAsync(S.cov.p, 0, npx, s));
+    if (S.n_gd)
+        hipLaunchKernelGGL(k_font_coverage, dim3(S.n_gd, (S.max_ch + BAND - 1) / BAND), dim3(COV_T), 0, s,
+                           S.gdesc.as<const GlyphDesc>(), S.edges.as<const float4>(), spread, W, S.cov.as<uint8_t>());
+    wg_stage_end(c);
+    wg_stage_begin(c, "font_edt");
+    hipLaunchKernelGGL(k_edt_cols, dim3((W + EC_TX - 1) / EC_TX, (H + EC_TY - 1) / EC_TY), dim3(EC_TX), 0, s,
+                       S.cov.as<const uint8_t>(), W, H, S.R,
+                       S.gin.as<uint16_t>(), S.gout.as<uint16_t>());
+    hipLaunchKernelGGL(k_edt_rows, dim3(H), dim3(ROW_T), 0, s, S.gin.as<const uint16_t>(), S.gout.as<const uint16_t>(), W,
+                       S.R, (float)spread, S.d2in.as<uint16_t>(), S.d2out.as<uint16_t>(), S.sdf.as<uint8_t>());
+    WG_HIP(c, hipGetLastError());
+    wg_stage_end(c);
+    wg_stage_end(c);
+    WG_HIP(c, hipStreamSynchronize(s));
+    S.built = true;
+    return WG_OK;
+}
+
 extern "C" {
 
 int wg_font_atlas_build(wg_ctx *c, int slot, const uint8_t *ttf, uint64_t len, const wg_atlas_params *prm) {
@@ -427,10 +467,14 @@ int wg_font_atlas_build(wg_ctx *c, int slot, const uint8_t *ttf, uint64_t len, c
         prm->first_char > prm->last_char || prm->last_char > 0xFFFF)
         return wg_fail(c, WG_E_INVALID, "bad atlas parameters");
     (void)hipSetDevice(c->device);
-    Font f;
-    if (!f.open(ttf, len)) return wg_fail(c, WG_E_INVALID, "not a TrueType font with cmap format 4");
     FontSlot &S = c->fonts[slot];
     S.built = false;
+    const uint64_t key = font_bytes_hash(ttf, len);
+    if (S.have_key && S.key_len == len && S.key_hash == key && !std::memcmp(&S.key_prm, prm, sizeof(*prm)))
+        return font_atlas_run(c, S);   // the same font at the same parameters: the device inputs stand
+    S.have_key = false;
+    Font f;
+    if (!f.open(ttf, len)) return wg_fail(c, WG_E_INVALID, "not a TrueType font with cmap format 4");
     const float scale = prm->em_px / (float)f.upem;
     std::vector<float4> edges;
     std::vector<GlyphDesc> gd;
@@ -499,27 +543,17 @@ int wg_font_atlas_build(wg_ctx *c, int slot, const uint8_t *ttf, uint64_t len, c
     if (!edges.empty()) WG_HIP(c, hipMemcpyAsync(S.edges.p, edges.data(), edges.size() * sizeof(float4), hipMemcpyHostToDevice, s));
     if (!gd.empty()) WG_HIP(c, hipMemcpyAsync(S.gdesc.p, gd.data(), gd.size() * sizeof(GlyphDesc), hipMemcpyHostToDevice, s));
     WG_HIP(c, hipMemcpyAsync(S.gtab.p, S.glyphs.data(), S.glyphs.size() * sizeof(wg_glyph), hipMemcpyHostToDevice, s));
-    wg_stage_begin(c, "font_atlas");
-    wg_stage_begin(c, "font_coverage");
-    WG_HIP(c, hipMemsetAsync(S.cov.p, 0, npx, s));
-    uint32_t max_ch = 0;
-    for (const GlyphDesc &d : gd) max_ch = d.ch > max_ch ? d.ch : max_ch;
-    if (!gd.empty())
-        hipLaunchKernelGGL(k_font_coverage, dim3((uint32_t)gd.size(), (max_ch + BAND - 1) / BAND), dim3(COV_T), 0, s,
-                           S.gdesc.as<const GlyphDesc>(), S.edges.as<const float4>(), spread, W, S.cov.as<uint8_t>());
-    wg_stage_end(c);
-    wg_stage_begin(c, "font_edt");
-    hipLaunchKernelGGL(k_edt_cols, dim3((W + EC_TX - 1) / EC_TX, (H + EC_TY - 1) / EC_TY), dim3(EC_TX), 0, s,
-                       S.cov.as<const uint8_t>(), W, H, S.R,
-                       S.gin.as<uint16_t>(), S.gout.as<uint16_t>());
-    hipLaunchKernelGGL(k_edt_rows, dim3(H), dim3(ROW_T), 0, s, S.gin.as<const uint16_t>(), S.gout.as<const uint16_t>(), W,
-                       S.R, (float)spread, S.d2in.as<uint16_t>(), S.d2out.as<uint16_t>(), S.sdf.as<uint8_t>());
-    WG_HIP(c, hipGetLastError());
-    wg_stage_end(c);
-    wg_stage_end(c);
-    WG_HIP(c, hipStreamSynchronize(s));
-    S.built = true;
-    return WG_OK;
+    S.n_gd = (uint32_t)gd.size();
+    S.max_ch = 0;
+    for (const GlyphDesc &d : gd) S.max_ch = d.ch > S.max_ch ? d.ch : S.max_ch;
+    const int rc = font_atlas_run(c, S);
+    if (rc == WG_OK) {
+        S.have_key = true;
+        S.key_len = len;
+        S.key_hash = key;
+        S.key_prm = *prm;
+    }
+    return rc;
 }
 
 int wg_font_atlas_info(wg_ctx *c, int slot, wg_atlas_info *out) {

@@ -182,6 +182,13 @@ struct FontSlot {
     float em_px = 0, ascent = 0, descent = 0, line_gap = 0;
     std::vector<wg_glyph> glyphs;
     DevBuf edges, gdesc, cov, sdf, gin, gout, d2in, d2out, gtab;
+    // the last build's font bytes (length + 64-bit hash) and parameters: a
+    // rebuild of the same font at the same parameters skips the TrueType parse
+    // and the uploads (the outlines and descriptors on the device still hold)
+    bool have_key = false;
+    uint64_t key_len = 0, key_hash = 0;
+    wg_atlas_params key_prm{};
+    uint32_t n_gd = 0, max_ch = 0;
 };
 
 // workspace slots in wg_ctx::lf (wg_lanes_fast.hip; the sharded build reuses LF_EVREC / LF_AUX for the

@@ -436,10 +436,18 @@ class Engine:
         """Rasterise + EDT a TrueType font into atlas slot (0 regular, 1 bold)."""
         if ttf is None:
             ttf = FONTS[slot]
-        data = open(ttf, "rb").read() if isinstance(ttf, str) else bytes(ttf)
-        buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+        if isinstance(ttf, str):   # a font file: read once per path and modification time
+            key = (ttf, os.stat(ttf).st_mtime_ns)
+            cache = self.__dict__.setdefault("_font_files", {})
+            if key not in cache:
+                data = open(ttf, "rb").read()
+                cache[key] = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
+            buf = cache[key]
+        else:
+            data = bytes(ttf)
+            buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data)
         p = abi.AtlasParams(width, height, em_px, spread, first, last)
-        self._check(lib().wg_font_atlas_build(self._ctx, slot, buf, len(data), ctypes.byref(p)))
+        self._check(lib().wg_font_atlas_build(self._ctx, slot, buf, len(buf), ctypes.byref(p)))
 
     def atlas_info(self, slot: int) -> abi.AtlasInfo:
         i = abi.AtlasInfo()
