@@ -10,7 +10,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+sys.path.insert(0, os.environ.get("WG_PKG_DIR") or os.path.join(ROOT, "whisper-git_amd"))   # (WG_PKG_DIR: an A/B copy)
 sys.path.insert(0, ROOT)
 
 

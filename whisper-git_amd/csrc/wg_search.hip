@@ -283,7 +283,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     }
     const bool both = fst[0] && fst[1] && ((fspan[0] + 3) >> 2) + 1 + ((fspan[1] + 3) >> 2) <= MCAPW;
     const int npass = both ? 1 : (int)fst[0] + (int)fst[1];
-    constexpr int SB = 4;   // words per thread per staging batch
+    constexpr int SB = 8;   // words per thread per staging batch
     for (int pass = 0; pass < npass; pass++) {
         // the pass's regions (uniform): field, text, bias, image span, first word
         const uint32_t ng = both ? 2u : 1u;
