@@ -69,6 +69,10 @@ struct MatchArgs {
     uint32_t qhex;                         // the query can match the id's hex (m <= 40, all of [0-9a-f])
     uint32_t marks;                        // the query holds no 0xFE / 0xFF byte: specials can be marked in place
     uint32_t spec_rel;                     // bit i: special i's lowered bytes share a byte with the query
+    // the query's first <= 8 bytes little-endian (as an LDS window holds them) and its mask; its last
+    // <= 16 big-endian in two words with their masks (as the walks' shift registers hold them; m <= 16).
+    // Host-computed: byte loads at the kernel's start wait behind the CU's staging loads.
+    uint64_t qv, qmask, qlo, qhi, mlo, mhi;
     uint8_t *out;                          // [re - rb]
     unsigned long long *count;
 };
@@ -236,23 +240,13 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     const WgCaseTables T{c_lower, c_cased, c_ign, A.flat};
     const uint32_t *special = s_special;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    if (tid < WG_SPECIAL_N) s_special[tid] = A.flat[WG_FLAT_N + tid];
+    const uint32_t spv = tid < WG_SPECIAL_N ? A.flat[WG_FLAT_N + tid] : 0u;   // to LDS after the staging loads
     const uint64_t r0 = A.rb + (uint64_t)blockIdx.x * MT;
     const uint32_t nr = (uint32_t)((A.re - r0) < MT ? (A.re - r0) : MT);
     const uint32_t m = A.m;
-    // the query's first <= 8 bytes little-endian, as an LDS window holds them
-    uint64_t qv = 0, qmask = ~0ull;
-    for (uint32_t i = 0; i < m && i < 8; i++) qv |= (uint64_t)A.q[i] << (8 * i);
-    if (m < 8) qmask = (1ull << (8 * m)) - 1;
+    const uint64_t qv = A.qv, qmask = A.qmask;
     const uint32_t q0 = (uint32_t)(qv & 0xFFu);
-    // ... and its last <= 16 big-endian, as the walk's shift registers hold them
-    FeedShift sh{0, 0, 0, 0, 0, 0, 0, m};
-    if (m <= 16) {
-        for (uint32_t i = 0; i < m; i++) {
-            if (i + 8 < m) { sh.qhi = (sh.qhi << 8) | A.q[i]; sh.mhi = (sh.mhi << 8) | 0xFFu; }
-            else { sh.qlo = (sh.qlo << 8) | A.q[i]; sh.mlo = (sh.mlo << 8) | 0xFFu; }
-        }
-    }
+    const FeedShift sh{0, 0, A.qlo, A.qhi, A.mlo, A.mhi, 0, m};
     const WalkFeed wf{sh, WgKmp{A.q, A.fail, m, 0}, m > 16};
     s_rf[tid] = 0;
     // both fields' row offsets and ranges up front (one round trip)
@@ -366,6 +360,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                 }
             }
             if (tid < 4) s_buf[tw + tid] = 0;
+            if (pass == 0 && tid < WG_SPECIAL_N) s_special[tid] = spv;
             for (uint32_t g = 0; g < ng; g++) {
                 if (tid < nr) s_rel[g][tid] = 4 * baseg[g] + (uint32_t)(orow[fg[g]] - gsf[fg[g]]) + biasg[g];
                 if (tid == 0) s_rel[g][nr] = hi[g];
@@ -678,6 +673,14 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     for (uint8_t b : q) {
         A.qhex &= (b - '0' < 10u) || (b - 'a' < 6u);
         A.marks &= b < 0xFE && b >= WG_SPECIAL_N;   // a mark's bytes never in the query
+    }
+    A.qv = 0;
+    A.qmask = m < 8 ? (1ull << (8 * m)) - 1 : ~0ull;
+    for (uint32_t i = 0; i < m && i < 8; i++) A.qv |= (uint64_t)q[i] << (8 * i);
+    A.qlo = A.qhi = A.mlo = A.mhi = 0;
+    for (uint32_t i = 0; i < m && m <= 16; i++) {
+        if (i + 8 < m) { A.qhi = (A.qhi << 8) | q[i]; A.mhi = (A.mhi << 8) | 0xFFu; }
+        else { A.qlo = (A.qlo << 8) | q[i]; A.mlo = (A.mlo << 8) | 0xFFu; }
     }
     A.spec_rel = 0;
     {
