@@ -22,7 +22,7 @@ CXXFLAGS_HOST := -O2 -std=c++17 -fPIC -Wall -Wextra -Iinclude
 CFLAGS_ORACLE := -O3 -march=x86-64-v3 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function
 
 all: $(PKG)/wgraph/libwgraph.so $(PKG)/wgraph/libwgraph_host.so $(PKG)/wgraph/libwgsynth.so oracle/liboracle.so oracle/libedt_cpu.so oracle/libcpu_mt.so \
-     tests/cpp/test_graph_layout profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost
+     tests/cpp/test_graph_layout profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/store_align profiles/microbench/launch_cost
 
 # one object per source (parallel, incremental); device code is per translation
 # unit (no relocatable device code), host code links into one library
@@ -55,6 +55,9 @@ profiles/microbench/store_ceiling: profiles/microbench/store_ceiling.hip
 profiles/microbench/store_sweep: profiles/microbench/store_sweep.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
+profiles/microbench/store_align: profiles/microbench/store_align.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
 profiles/microbench/launch_cost: profiles/microbench/launch_cost.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Wno-unused-value -Wno-unused-result -o $@ $<
 
@@ -72,6 +75,6 @@ engine: $(PKG)/wgraph/libwgraph.so
 host: $(PKG)/wgraph/libwgraph_host.so tests/cpp/test_graph_layout
 
 clean:
-	rm -rf build/obj; rm -f $(PKG)/wgraph/*.so oracle/*.so profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/launch_cost tests/cpp/test_graph_layout
+	rm -rf build/obj; rm -f $(PKG)/wgraph/*.so oracle/*.so profiles/microbench/store_ceiling profiles/microbench/store_sweep profiles/microbench/store_align profiles/microbench/launch_cost tests/cpp/test_graph_layout
 
 .PHONY: all clean oracle synth engine host

@@ -33,7 +33,7 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "whisper-git_amd"))
+sys.path.insert(0, os.environ.get("WG_PKG_DIR") or os.path.join(ROOT, "whisper-git_amd"))   # (WG_PKG_DIR: an A/B build)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 

@@ -42,11 +42,49 @@ struct Cap {
     // its lists are incomplete and nothing may read them
     const uint32_t *gate;
 };
-__device__ __forceinline__ bool over(Cap a, uint32_t *ovf) {
-    if (a.gate && (a.gate[0] | a.gate[8])) return true;
-    if (a.cap == ~0u || *a.total <= a.cap) return false;
-    if (threadIdx.x == 0) atomicOr(ovf, 1u);
+// A kernel's guards read with every load issued before any is waited on: an
+// absent pointer reads the overflow word instead of branching round its load
+// (a load waited on alone at a kernel's start queues behind the CU's other
+// loads; chained, the guards cost one round trip each).
+template <int K>
+struct CapVals {
+    uint32_t gate, total[K];
+};
+template <int K>
+__device__ __forceinline__ CapVals<K> cap_read(const Cap (&cs)[K], const uint32_t *ovf) {
+    typedef const __attribute__((address_space(1))) uint32_t gword;   // global loads, not flat
+    uint32_t g0[K], g8[K], t[K];
+    for (int k = 0; k < K; k++) {   // every load first
+        const bool hg = cs[k].gate != nullptr, ht = cs[k].total != nullptr;
+        g0[k] = *(const gword *)(hg ? cs[k].gate : ovf);
+        g8[k] = *(const gword *)(hg ? cs[k].gate + 8 : ovf);
+        t[k] = *(const gword *)(ht ? cs[k].total : ovf);
+    }
+    CapVals<K> v;
+    v.gate = 0;
+    for (int k = 0; k < K; k++) {
+        v.gate |= cs[k].gate ? g0[k] | g8[k] : 0u;
+        v.total[k] = cs[k].total ? t[k] : 0u;
+    }
+    return v;
+}
+// (one state word from every load before any branch, so none is sunk past one)
+template <int K>
+__device__ __forceinline__ bool cap_over(const CapVals<K> &v, const Cap (&cs)[K], uint32_t *ovf) {
+    uint32_t o = 0;
+    for (int k = 0; k < K; k++) o |= (uint32_t)(cs[k].cap != ~0u) & (uint32_t)(v.total[k] > cs[k].cap);
+    const uint32_t state = (v.gate ? 2u : 0u) | o;
+    if (state == 0) return false;
+    if (state == 1 && threadIdx.x == 0) atomicOr(ovf, 1u);
     return true;
+}
+template <int K>
+__device__ __forceinline__ bool over_all(const Cap (&cs)[K], uint32_t *ovf) {
+    return cap_over(cap_read(cs, ovf), cs, ovf);
+}
+__device__ __forceinline__ bool over(Cap a, uint32_t *ovf) {
+    const Cap cs[1] = {a};
+    return over_all(cs, ovf);
 }
 
 __device__ __forceinline__ uint32_t pack_vert(uint32_t lane, uint32_t kind, uint32_t color) {
@@ -428,7 +466,8 @@ __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *_
     __shared__ uint32_t s_pre[256 / 64][64], s_k0[256 / 64][64];
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lid = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (over(vc, ovf) || over(cc, ovf)) return;   // (uniform)
+    const Cap gs[2] = {vc, cc};
+    if (over_all(gs, ovf)) return;   // (uniform)
     const bool valid = k < ne && !(ne_dev && k >= *ne_dev);
     wg_edge e{};
     if (valid) e = edges[k];
@@ -642,7 +681,8 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         uint32_t *__restrict__ err, Cap vc, Cap sc, uint32_t *ovf, bool super, const uint32_t *__restrict__ run_if,
         const uint32_t *__restrict__ done) {
     if (super && (*run_if == 0 || *done != 0)) return;   // (uniform over the grid)
-    if (over(vc, ovf) || over(sc, ovf)) return;
+    const Cap gs[2] = {vc, sc};
+    if (over_all(gs, ovf)) return;
     __shared__ uint32_t s_eid[SW_CAP_BLOCK];
     __shared__ uint32_t s_c[SW_CAP_BLOCK];
     __shared__ uint32_t s_p[SW_CAP_BLOCK];
@@ -742,8 +782,13 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[SW_WAVES][SW_STAGE];
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t q = q0 + (uint64_t)blockIdx.x * SW_WAVES + (threadIdx.x >> 6);   // chunks [q0, q1)
-    if (SUPER && (*run_if == 0 || *done != 0)) return;
-    if (over(vc, ovf) || over(sc, ovf) || over(cc, ovf) || q >= q1) return;
+    const Cap gs[3] = {vc, sc, cc};
+    const CapVals<3> gv = cap_read(gs, ovf);
+    if (SUPER) {
+        const uint32_t ri = *run_if, dn = *done;
+        if ((ri == 0) | (dn != 0)) return;
+    }
+    if (cap_over(gv, gs, ovf) || q >= q1) return;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
     // the chunk's top and bottom halves (their entries follow the full ones)
