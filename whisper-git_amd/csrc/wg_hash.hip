@@ -215,7 +215,9 @@ __global__ void __launch_bounds__(WG_BS_THREADS) k_probe_fix(const uint8_t *__re
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t cnt = 0;
     if (i < n) {
-        const uint32_t pa = poff[i], pb = poff[i + 1];
+        // every first load before the first wait (the common row needs only these)
+        const uint32_t pa = poff[i], pb = poff[i + 1], ec = edge_cnt[i], rm = rowmiss[i];
+        asm volatile("" ::"v"(ec), "v"(rm));   // (held here: not sunk past the branch into a second round trip)
         if (*dup != 0xFFFFFFFFu) {
             // duplicate ids (:273-274 last write wins): the table decides every
             // reference; such a list takes the general lane walk
@@ -229,9 +231,9 @@ __global__ void __launch_bounds__(WG_BS_THREADS) k_probe_fix(const uint8_t *__re
             if (L.flags && canon[i] != (uint32_t)i) atomicOr(&L.flags[0], 1u);
         } else {
             canon[i] = (uint32_t)i;
-            cnt = edge_cnt[i];
+            cnt = ec;
             if (L.flags && pb - pa > 0x10000u) atomicOr(&L.flags[0], 1u);   // (lf_refs_row's bound)
-            if (rowmiss[i]) {
+            if (rm) {
                 uint64_t mm = 0;   // the row's misses among its first 64 references
                 for (uint32_t k = pa; k < pb; k++) {
                     if (prow[k] != PROW_MISS) continue;

@@ -345,11 +345,14 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
         if (RI.nev_dev && i < 256) ev[*RI.nev_dev + i] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (j >= R.nl) return;
-    if (gate && *gate) return;   // speculative build: not well formed (the general walk takes over)
     const uint64_t gj = R.s + j;
+    // the row's first loads issued with the gate's, waited on once
     const uint32_t wi = winfo[j], w = wi & 0x3FFFFFFFu;
-    const bool fp_in = wi & 0x40000000u, sec_first = wi & 0x80000000u;
     uint32_t e = ev_off[j];                  // shard-local event index; global id = ev_base + e
+    const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
+    asm volatile("" ::"v"(wi), "v"(e), "v"(pa), "v"(pb));   // (held here: not sunk past the gate's branch)
+    if (gate && *gate) return;   // speculative build: not well formed (the general walk takes over)
+    const bool fp_in = wi & 0x40000000u, sec_first = wi & 0x80000000u;
     if (w == 0) {
         ev[e] = make_uint4(fp_in ? (F_A | F_O) : F_A, 0u, 0u, (uint32_t)gj);
         e++;
@@ -393,7 +396,6 @@ __global__ void k_lf_events(LfRange R, uint32_t ev_base, uint32_t aux_base, cons
         if (death && t0 < ev_off[R.nl]) death[t0] = e + 1u;
         e++;
     }
-    const uint32_t pa = R.poff[gj], pb = R.poff[gj + 1];
     for (uint32_t k = pa + 1; k < pb; k++) {
         const int32_t p = R.prow[k];
         if (p >= 0 && is_first_ref(R, first_ref, gj, k, k - pa, (uint64_t)p)) {
