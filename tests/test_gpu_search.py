@@ -221,3 +221,52 @@ def test_search_dimming_of_vertices_and_glyphs(engine, data):
     finally:
         engine.match_rows("")
         o.close()
+
+
+@pytest.mark.parametrize("dense", ["summary", "author"])
+def test_match_two_passes_with_an_overflowing_pass(engine, dense):
+    """a workgroup whose two fields do not fit one LDS image runs
+    two passes; here one of them lists more non-ASCII leads than the kernel
+    holds (LCAP 2560 per 256 rows: that pass takes the stream from HBM and
+    skips its barriers uniformly) while the other pass walks rows with
+    length-changing code points (U+1E9E, the Kelvin sign, U+0130) — with
+    queries shorter than 8 bytes, between 9 and 16, and past 16 bytes (the KMP
+    whole-row walk) that contain 'ß' / 'k'.  Each pass keeps its own counts
+    (a slower wave of pass 0 must not see pass 1's cleared counters)."""
+    d = synth.generate("random13", 1800, seed=21)
+    engine.build(d)
+    rng = np.random.default_rng(77 if dense == "summary" else 78)
+    cyr = "ДмитрийСтрасБург"
+    mixed = ["STRAẞE ", "straße ", "Kelvin ", "kelvin ", "İ ", "fix ", "Ölçek ", "a "]
+
+    def rows_of(kind, target):
+        rows = []
+        for _ in range(d.n):
+            s = ""
+            if kind == "dense":
+                while len(s.encode()) < target:
+                    s += cyr[int(rng.integers(0, len(cyr)))]
+            else:
+                while len(s.encode()) < target:
+                    s += mixed[int(rng.integers(0, len(mixed)))]
+            b = s.encode()
+            while len(b) > target:      # whole code points only
+                s = s[:-1]
+                b = s.encode()
+            rows.append(b)
+        off = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.uint64)
+        return np.frombuffer(b"".join(rows), np.uint8), off
+
+    dense_f = rows_of("dense", 72)          # ~36 leads per row: 9k per 256 rows
+    other_f = rows_of("mixed", 44)
+    summ, auth = (dense_f, other_f) if dense == "summary" else (other_f, dense_f)
+    qs = ["ß", "k", "дм", "straße kelvin", "strasse", "straße straße straße", "kelvin kelvin kelvin k",
+          "i̇ fix a straße", "KELVIN KELVIN straẞe", "ийстрасбург", "рийстр"]
+    try:
+        for q in qs:
+            n = engine.match_rows(q, summaries=summ, authors=auth)
+            want, wn = so.match_rows(d, q.encode(), summ, auth)
+            got = engine.match_flags()
+            assert n == wn and (got == want).all(), (q, dense, np.flatnonzero(got != want)[:5])
+    finally:
+        engine.match_rows("")

@@ -260,3 +260,39 @@ def test_duplicate_ids_window_row_differs_from_table_row():
             eng.close()
     finally:
         o.close()
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_fused_join_with_deferred_clear_cycle(fused):
+    """with deferred validation, a list of at least slice_min_rows
+    rows leaves the next build's id table to be emptied by the emission, on
+    the side stream beside its tiles.  The next build fills that table — on
+    the main stream when the join is fused — so it must wait for the clear.
+    Build / frame / emit cycles alternating two such lists (different ids in
+    the same table slots), every step bit-exact against the oracle."""
+    import wgraph
+    from oracle import oracle_c
+    lists = [synth.generate("wide16", 300_000, seed=31), synth.generate("random13", 300_000, seed=32)]
+    want = []
+    for d in lists:
+        o = oracle_c.OracleLayout(d)
+        ov, _ = o.emit_vertices(0, d.n, selected=d.n // 2)
+        want.append((o.lane.copy(), o.max_lane, oracle_c.vertex_checksum(ov), len(ov)))
+        o.close()
+    eng = wgraph.Engine(0)
+    try:
+        eng.set_defer_validation(True)
+        eng.set_join_fused(fused)
+        for step in range(6):
+            k = step % 2
+            d = lists[k]
+            eng.build_frame(d, band=d.band)
+            eng.emit_vertices(0, d.n, selected=d.n // 2)
+            vs = eng.vertex_summary()
+            tag = f"fused={fused} step {step}"
+            assert vs.n_vertices == want[k][3] and vs.checksum == want[k][2], tag
+            lane, _ = eng.lanes()
+            assert_bits(tag + " lane", lane, want[k][0])
+            assert eng.layout_summary().max_lane == want[k][1], tag
+    finally:
+        eng.close()

@@ -846,13 +846,6 @@ __global__ void k_band_diff(const uint32_t *__restrict__ a, const uint32_t *__re
         if (a[i] != b[i]) { atomicMin(first, (unsigned long long)i); return; }
 }
 
-// first row whose commit time differs from the built list's (atomicMin)
-__global__ void k_time_diff(const int64_t *__restrict__ a, const int64_t *__restrict__ b, uint64_t n,
-                            unsigned long long *first) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        if (a[i] != b[i]) { atomicMin(first, (unsigned long long)i); return; }
-}
-
 // row_geometry_with_bands(&self, commits, band_heights) (:367-399) with its
 // commits argument: heights from the passed list's times (compute_row_heights
 // (commits), :372), the geometry from the built edges; the built list itself
@@ -879,16 +872,21 @@ int wg_row_geometry_list(wg_ctx *c, const wg_commits *cm, const float *band, int
         return wg_fail(c, WG_E_INVALID, "bad residency %d", cm->residency);
     }
     // The built list's times by pointer only when they are the engine's own
-    // copy: a caller's device buffer may have been rewritten since the build
-    // (then the heights are recomputed from it as it stands).
+    // copy (a host-resident build).  Anything else — a copy, or the caller's
+    // device buffer the build read, which may have been rewritten since — has
+    // its heights recomputed as it stands and compared with the heights the
+    // build computed (a snapshot the caller cannot touch): equal heights give
+    // the same geometry, so the per-frame reuse stands.
     const bool own = c->d_time == c->in_time.as<const int64_t>();
     bool same = !n || (t == c->d_time && own);
-    if (!same && t != c->d_time) {
+    if (!same) {
+        WG_ALLOC(c, c->alt_heights, n * 4 + 4);
+        if (const int rc = wg_heights_run(c, n, n, c->alt_heights.as<float>(), t)) return rc;
         WG_ALLOC(c, c->geom_diff_first, 16);
         WG_HIP(c, hipMemsetAsync(c->geom_diff_first.p, 0xFF, 8, c->stream));
         const uint64_t g = std::min<uint64_t>((n + 255) / 256, 2048);
-        hipLaunchKernelGGL(k_time_diff, dim3((uint32_t)g), dim3(256), 0, c->stream, t, c->d_time, n,
-                           c->geom_diff_first.as<unsigned long long>());
+        hipLaunchKernelGGL(k_band_diff, dim3((uint32_t)g), dim3(256), 0, c->stream, c->alt_heights.as<const uint32_t>(),
+                           c->heights.as<const uint32_t>(), n, c->geom_diff_first.as<unsigned long long>());
         uint64_t first = 0;
         if (const int frc = wg_fetch(c, {{c->geom_diff_first.p, true}}, &first)) return frc;
         same = first == ~0ull;
@@ -896,8 +894,6 @@ int wg_row_geometry_list(wg_ctx *c, const wg_commits *cm, const float *band, int
     if (same) {
         if (c->alt_heights_on) { c->alt_heights_on = false; c->geom_key_gen = ~0ull; }
     } else {
-        WG_ALLOC(c, c->alt_heights, n * 4 + 4);
-        if (const int rc = wg_heights_run(c, n, n, c->alt_heights.as<float>(), t)) return rc;
         c->alt_heights_on = true;
         c->geom_key_gen = ~0ull;   // (no per-frame reuse across height sets)
     }

@@ -470,7 +470,8 @@ int wg_font_atlas_build(wg_ctx *c, int slot, const uint8_t *ttf, uint64_t len, c
     FontSlot &S = c->fonts[slot];
     S.built = false;
     const uint64_t key = font_bytes_hash(ttf, len);
-    if (S.have_key && S.key_len == len && S.key_hash == key && !std::memcmp(&S.key_prm, prm, sizeof(*prm)))
+    if (S.have_key && S.key_len == len && S.key_hash == key && !std::memcmp(&S.key_prm, prm, sizeof(*prm)) &&
+        S.key_bytes.size() == len && !std::memcmp(S.key_bytes.data(), ttf, len))
         return font_atlas_run(c, S);   // the same font at the same parameters: the device inputs stand
     S.have_key = false;
     Font f;
@@ -552,6 +553,7 @@ int wg_font_atlas_build(wg_ctx *c, int slot, const uint8_t *ttf, uint64_t len, c
         S.key_len = len;
         S.key_hash = key;
         S.key_prm = *prm;
+        S.key_bytes.assign(ttf, ttf + len);
     }
     return rc;
 }

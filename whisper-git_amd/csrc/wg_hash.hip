@@ -280,6 +280,9 @@ static int hash_table_prepare(wg_ctx *c, unsigned long long **table, unsigned lo
     }
     *table = c->htab[t].as<unsigned long long>();
     *next = c->htab[o].as<unsigned long long>();
+    // a clear of this table queued on the side stream by the last emission
+    // (wg_hash_clear_next) completes before anything here fills it
+    if (const int rc = wg_side_join(c)) return rc;
     if (c->htab_clean[t] < *words) WG_HIP(c, hipMemsetAsync(*table, 0xFF, *words * 8, c->stream));
     // the next build's table is emptied by this build, unless a long list's
     // emission will (wg_hash_clear_next, beside its tiles: 8 bytes per slot
@@ -321,6 +324,12 @@ int wg_hash_clear_next(wg_ctx *c, hipStream_t s) {
     if (!c->hcap || c->htab_clean[o] >= words || c->htab[o].cap < words * 8) return WG_OK;
     WG_HIP(c, hipMemsetAsync(c->htab[o].p, 0xFF, words * 8, s));
     c->htab_clean[o] = words;
+    if (s == c->side && c->stream != c->side) {
+        // the main stream waits for the clear before the next build fills the
+        // table (wg_side_join at the next fork or in hash_table_prepare)
+        WG_HIP(c, hipEventRecord(c->ev_join, s));
+        c->side_pending = true;
+    }
     return WG_OK;
 }
 

@@ -187,6 +187,7 @@ struct FontSlot {
     // and the uploads (the outlines and descriptors on the device still hold)
     bool have_key = false;
     uint64_t key_len = 0, key_hash = 0;
+    std::vector<uint8_t> key_bytes;   // the last font's bytes: a hash match is confirmed by memcmp
     wg_atlas_params key_prm{};
     uint32_t n_gd = 0, max_ch = 0;
 };

@@ -235,7 +235,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     __shared__ uint16_t s_wrow[2 * MT];       // rows to walk whole: row | region << 8
     __shared__ uint16_t s_spos[SPCAP];        // marked specials the query could overlap: walked locally
     __shared__ uint32_t s_special[WG_SPECIAL_N];
-    __shared__ uint32_t s_cnt[4];             // leads | 0xCE leads << 16, rows to walk, flags (1: a row starts with a continuation byte, 2: a raw 0xFE / 0xFF byte), specials listed
+    __shared__ uint32_t s_cnt[8];             // per pass (4 words each, so a pass never clears counts a slower wave of the previous pass still reads): leads | 0xCE leads << 16, rows to walk, flags (1: a row starts with a continuation byte, 2: a raw 0xFE / 0xFF byte), specials listed
     uint8_t *const sb = reinterpret_cast<uint8_t *>(s_buf);
     const WgCaseTables T{c_lower, c_cased, c_ign, A.flat};
     const uint32_t *special = s_special;
@@ -249,6 +249,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     const FeedShift sh{0, 0, A.qlo, A.qhi, A.mlo, A.mhi, 0, m};
     const WalkFeed wf{sh, WgKmp{A.q, A.fail, m, 0}, m > 16};
     s_rf[tid] = 0;
+    if (tid < 8) s_cnt[tid] = 0;
     // both fields' row offsets and ranges up front (one round trip)
     uint64_t orow[2] = {0, 0}, gsf[2] = {0, 0}, gef[2] = {0, 0};
     for (int f = 0; f < 2; f++) {
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
             hi[g] = 4 * baseg[g] + spang[g];
         }
         auto reg = [&](uint32_t p) -> uint32_t { return p >= pb1 ? 1u : 0u; };
-        if (tid < 4) s_cnt[tid] = 0;
+        uint32_t *const pc = s_cnt + 4 * pass;   // zeroed before the loop
         __syncthreads();   // the previous pass's readers are done with the buffer
         // stage: aligned words inside each field's range by word loads, the edge
         // words by bytes; ASCII lowered on the way in (SWAR; case classes
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                         if (lane >= d) incl += t;
                     }
                     uint32_t base = 0;
-                    if (lane == 63) base = atomicAdd(&s_cnt[0], incl);
+                    if (lane == 63) base = atomicAdd(&pc[0], incl);
                     base = __shfl(base, 63, 64);
                     uint32_t il = (base & 0xFFFFu) + ((incl - cnt) & 0xFFFFu), ic = (base >> 16) + ((incl - cnt) >> 16);
 #pragma unroll
@@ -365,17 +366,17 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                 if (tid < nr) s_rel[g][tid] = 4 * baseg[g] + (uint32_t)(orow[fg[g]] - gsf[fg[g]]) + biasg[g];
                 if (tid == 0) s_rel[g][nr] = hi[g];
             }
-            if (raw_ff) atomicOr(&s_cnt[2], 2u);
+            if (raw_ff) atomicOr(&pc[2], 2u);
         }
         __syncthreads();
-        const uint32_t nlead = s_cnt[0] & 0xFFFFu, nce = s_cnt[0] >> 16;
+        const uint32_t nlead = pc[0] & 0xFFFFu, nce = pc[0] >> 16;
         if (nlead + nce > LCAP) {   // uniform: more code points than the lists hold: the stream from HBM
             for (uint32_t g = 0; g < ng; g++)
                 if (tid < nr) atomicOr(&s_rf[tid], rf_hbm(fg[g]));
             continue;
         }
         for (uint32_t g = 0; g < ng; g++)
-            if (tid < nr && s_rel[g][tid] < s_rel[g][tid + 1] && (sb[s_rel[g][tid]] & 0xC0u) == 0x80u) atomicOr(&s_cnt[2], 1u);
+            if (tid < nr && s_rel[g][tid] < s_rel[g][tid + 1] && (sb[s_rel[g][tid]] & 0xC0u) == 0x80u) atomicOr(&pc[2], 1u);
         // Final_Sigma of the U+03A3s, over the original non-ASCII bytes (nothing non-ASCII written yet)
         for (uint32_t i = tid; i < nce; i += MT) {
             const uint32_t p = s_ce[-1 - (int)i];
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         // and its row set to walk — unless its lowered bytes share none with the
         // query: then no match can overlap it; where marks are off it is left
         // as it was and its row walked by decoding, fast hits void.
-        const uint32_t fl = s_cnt[2];
+        const uint32_t fl = pc[2];
         const bool exact = (fl & 1u) != 0, marks = A.marks && !(fl & 2u);
         for (uint32_t i = tid; i < nlead + nce; i += MT) {
             const uint32_t e = i < nlead ? s_lead[i] : s_ce[-1 - (int)(i - nlead)];
@@ -418,7 +419,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                         sb[p + 1] = (uint8_t)idx;
                         for (uint32_t j = 2; j < len; j++) sb[p + j] = 0xFE;
                         if ((A.spec_rel >> idx) & 1u) {   // walked locally (windows over it), or the row whole
-                            const uint32_t si = m <= 16 ? atomicAdd(&s_cnt[3], 1u) : SPCAP;
+                            const uint32_t si = m <= 16 ? atomicAdd(&pc[3], 1u) : SPCAP;
                             if (si < SPCAP) s_spos[si] = (uint16_t)p;
                             else atomicOr(&s_rf[row_of(rel, nr, p)], rf_mark(fg[g]));
                         }
@@ -444,7 +445,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         __syncthreads();
         for (uint32_t g = 0; g < ng; g++)
             if (tid < nr && (s_rf[tid] & (rf_mark(fg[g]) | rf_decode(fg[g]))))
-                s_wrow[atomicAdd(&s_cnt[1], 1u)] = (uint16_t)(tid | g << 8);
+                s_wrow[atomicAdd(&pc[1], 1u)] = (uint16_t)(tid | g << 8);
         // every byte position holding the query's first byte against its first 8 bytes
         for (uint32_t k = tid + (lo[0] >> 2); k < tw; k += MT) {
             const uint32_t w0 = s_buf[k];
@@ -471,7 +472,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         // ... and the windows over each listed special: the lowered stream from
         // 3 (m - 1) bytes before it to as many after (each 3 bytes of the buffer
         // hold at least one lowered byte), entered at a byte outside a mark
-        const uint32_t nwalk = s_cnt[1], nsp = s_cnt[3] < SPCAP ? s_cnt[3] : SPCAP;
+        const uint32_t nwalk = pc[1], nsp = pc[3] < SPCAP ? pc[3] : SPCAP;
         for (uint32_t i = tid; i < nwalk + nsp; i += MT) {
             uint32_t row, a, b;
             bool dec = false;
@@ -540,33 +541,35 @@ inline uint32_t mblocks(uint64_t n) { return (uint32_t)((n + MT - 1) / MT); }
 // Case_Ignorable, and whether lowering changes its UTF-8 length (the
 // "specials": U+0130 -> "i̇" and the simple mappings across a UTF-8 length,
 // each with its index); then per special its lowered bytes | length << 24.
-void wg_match_flat_table(std::vector<uint32_t> &flat) {
-    static std::vector<uint32_t> cache;
-    if (cache.empty()) {
-        const WgCaseTables HT{h_lower, h_cased, h_ign};
-        std::vector<uint32_t> t(WG_FLAT_N + WG_SPECIAL_N, 0);
-        uint32_t ns = 0;
-        auto entry = [&](uint32_t cp) {
-            const uint32_t lc = wg_lower_simple(HT, cp);
-            uint8_t b0[4], b1[4];
-            const uint32_t n0 = wg_utf8_encode(cp, b0), n1 = wg_utf8_encode(lc, b1);
-            uint32_t e = (lc & 0xFFFFu) | (wg_is_cased(HT, cp) ? WG_FLAT_CASED : 0u) | (wg_is_ignorable(HT, cp) ? WG_FLAT_IGN : 0u);
-            if ((cp == 0x130u || lc >= WG_FLAT_N || n0 != n1) && ns < WG_SPECIAL_N) {   // 25 in the tables
-                const uint32_t x = cp == 0x130u ? ('i' | 0xCCu << 8 | 0x87u << 16 | 3u << 24)
-                                                : ((uint32_t)b1[0] | (n1 > 1 ? (uint32_t)b1[1] << 8 : 0u) |
-                                                   (n1 > 2 ? (uint32_t)b1[2] << 16 : 0u) | n1 << 24);
-                t[WG_FLAT_N + ns] = x;
-                e |= WG_FLAT_LENCHG | ns << WG_FLAT_SPECIAL_SHIFT;
-                ns++;
-            }
-            t[cp] = e;
-        };
-        entry(0x130u);   // special 0
-        for (uint32_t cp = 0; cp < WG_FLAT_N; cp++)
-            if (cp != 0x130u) entry(cp);
-        cache.swap(t);
-    }
-    flat = cache;
+static std::vector<uint32_t> wg_build_flat_table() {
+    const WgCaseTables HT{h_lower, h_cased, h_ign};
+    std::vector<uint32_t> t(WG_FLAT_N + WG_SPECIAL_N, 0);
+    uint32_t ns = 0;
+    auto entry = [&](uint32_t cp) {
+        const uint32_t lc = wg_lower_simple(HT, cp);
+        uint8_t b0[4], b1[4];
+        const uint32_t n0 = wg_utf8_encode(cp, b0), n1 = wg_utf8_encode(lc, b1);
+        uint32_t e = (lc & 0xFFFFu) | (wg_is_cased(HT, cp) ? WG_FLAT_CASED : 0u) | (wg_is_ignorable(HT, cp) ? WG_FLAT_IGN : 0u);
+        if ((cp == 0x130u || lc >= WG_FLAT_N || n0 != n1) && ns < WG_SPECIAL_N) {   // 25 in the tables
+            const uint32_t x = cp == 0x130u ? ('i' | 0xCCu << 8 | 0x87u << 16 | 3u << 24)
+                                            : ((uint32_t)b1[0] | (n1 > 1 ? (uint32_t)b1[1] << 8 : 0u) |
+                                               (n1 > 2 ? (uint32_t)b1[2] << 16 : 0u) | n1 << 24);
+            t[WG_FLAT_N + ns] = x;
+            e |= WG_FLAT_LENCHG | ns << WG_FLAT_SPECIAL_SHIFT;
+            ns++;
+        }
+        t[cp] = e;
+    };
+    entry(0x130u);   // special 0
+    for (uint32_t cp = 0; cp < WG_FLAT_N; cp++)
+        if (cp != 0x130u) entry(cp);
+    return t;
+}
+
+// built once per process (a function-local static: thread-safe initialisation)
+const std::vector<uint32_t> &wg_match_flat_table() {
+    static const std::vector<uint32_t> table = wg_build_flat_table();
+    return table;
 }
 
 // Rust `str::to_lowercase` of a byte string on the host (same tables as the device)
@@ -643,8 +646,7 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
         }
     }
     if (!c->match_flat.p) {   // once per context: the BMP's lowercase and case classes, and the specials
-        std::vector<uint32_t> flat;
-        wg_match_flat_table(flat);
+        const std::vector<uint32_t> &flat = wg_match_flat_table();
         WG_ALLOC(c, c->match_flat, flat.size() * 4 + 16);
         WG_HIP(c, hipMemcpyAsync(c->match_flat.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, s));
         WG_HIP(c, hipStreamSynchronize(s));
@@ -684,8 +686,7 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     }
     A.spec_rel = 0;
     {
-        std::vector<uint32_t> flat;
-        wg_match_flat_table(flat);
+        const std::vector<uint32_t> &flat = wg_match_flat_table();
         for (uint32_t i = 0; i < WG_SPECIAL_N; i++) {
             const uint32_t x = flat[WG_FLAT_N + i];
             for (uint32_t j = 0; j < (x >> 24); j++)
