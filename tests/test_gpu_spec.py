@@ -276,6 +276,7 @@ def test_fused_join_with_deferred_clear_cycle(fused):
     want = []
     for d in lists:
         o = oracle_c.OracleLayout(d)
+        o.row_geometry(d.band)
         ov, _ = o.emit_vertices(0, d.n, selected=d.n // 2)
         want.append((o.lane.copy(), o.max_lane, oracle_c.vertex_checksum(ov), len(ov)))
         o.close()
