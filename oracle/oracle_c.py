@@ -58,6 +58,8 @@ def lib():
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_float]
             getattr(L, f).restype = ctypes.c_float
         L.wgo_cubic_subcurve.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        L.wgo_decompose_edges.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                          ctypes.POINTER(_Geom)]
         _lib = L
     return _lib
 
@@ -188,3 +190,22 @@ def cubic_subcurve(p8, a, b):
     out = np.zeros(8, np.float32)
     lib().wgo_cubic_subcurve(x.ctypes.data, a, b, out.ctypes.data)
     return out
+
+
+def decompose_edges(edges, row_top_y):
+    """decompose_edge_into_rows (commit_graph.rs:525-608) of `edges` (tuples
+    child_row, child_lane, parent_row, parent_lane, color) over
+    RowGeometry::default() rows and the given row_top_y (len = rows + 1), as
+    the reference's known-answer tests call it (:1631-1702).  Returns the
+    flattened geometry dict (vert entries carry their kind in bits 24-25)."""
+    e = np.zeros(len(edges), abi.EDGE_DTYPE)
+    for i, t in enumerate(edges):
+        e[i] = t
+    rt = np.ascontiguousarray(row_top_y, np.float32)
+    g = _Geom()
+    if lib().wgo_decompose_edges(e.ctypes.data, len(e), rt.ctypes.data, len(rt) - 1, ctypes.byref(g)) != 0:
+        raise MemoryError("wgo_decompose_edges failed")
+    try:
+        return _geom_to_dict(g)
+    finally:
+        lib().wgo_geometry_free(ctypes.byref(g))

@@ -294,6 +294,20 @@ static int flatten(rowgeom *rows, uint64_t n, const float *row_top_y, wgo_geomet
     return 0;
 }
 
+/* decompose_edge_into_rows over RowGeometry::default() rows (height
+ * ROW_HEIGHT, node_y NODE_Y, :218-230) and the caller's row_top_y: the
+ * reference's decomposition known-answer tests call it this way
+ * (:1631-1702).  Exported for those tests only. */
+int wgo_decompose_edges(const wg_edge *edges, uint64_t ne, const float *row_top_y, uint64_t nrows, wgo_geometry *out) {
+    rowgeom *rows = (rowgeom *)calloc(nrows ? nrows : 1, sizeof(rowgeom));
+    if (!rows) return -1;
+    for (uint64_t r = 0; r < nrows; r++) { rows[r].height = WG_ROW_HEIGHT; rows[r].node_y = WG_NODE_Y; }
+    for (uint64_t k = 0; k < ne; k++) decompose_edge_into_rows(&edges[k], row_top_y, rows, nrows);
+    int rc = flatten(rows, nrows, row_top_y, out);
+    free(rows);
+    return rc;
+}
+
 void wgo_geometry_free(wgo_geometry *g) {
     if (!g) return;
     free(g->height); free(g->node_y); free(g->row_top); free(g->vert_off); free(g->vert);

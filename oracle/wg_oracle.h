@@ -42,6 +42,8 @@ void wgo_layout_free(wgo_layout *L);
 /* row_geometry_with_bands (:367-399); band NULL = zero bands */
 int  wgo_row_geometry(const wgo_layout *L, const int64_t *time, const float *band, wgo_geometry *out);
 void wgo_geometry_free(wgo_geometry *g);
+/* decompose_edge_into_rows over default rows (the reference KATs, :1631-1702) */
+int  wgo_decompose_edges(const wg_edge *edges, uint64_t ne, const float *row_top_y, uint64_t nrows, wgo_geometry *out);
 /* compute_row_heights (:486-507) */
 void wgo_compute_row_heights(uint64_t n, const int64_t *time, float *heights);
 /* Cubic::{y_at, t_at_y, subcurve} (:614-695) on {p0.x, p0.y, ..., p3.y} */

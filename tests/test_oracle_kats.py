@@ -47,32 +47,65 @@ def test_cubic_subcurve_endpoints_match_y_at(impl):  # :1607-1622
     assert abs(s3 - yb) < 1e-3
 
 
-def _decompose(edge, n):
+def _decompose_py(edge, n):
     rows = [P.RowGeometry() for _ in range(n)]
     P.decompose_edge_into_rows(edge, uniform_offsets(n), rows)
-    return rows
+    return [dict(full=len(r.full), top=len(r.top), bottom=len(r.bottom),
+                 curves=[np.asarray(c[0], np.float32) for c in r.curves]) for r in rows]
 
 
-def test_decompose_same_lane_emits_top_full_bottom_verticals():  # :1631-1651
-    rows = _decompose((0, 1, 3, 1, 0), 4)
-    assert len(rows[0].bottom) == 1 and len(rows[0].full) == 0 and len(rows[0].top) == 0
-    assert len(rows[1].full) == 1 and len(rows[2].full) == 1
-    assert len(rows[3].top) == 1
+def _decompose_c(edge, n):
+    """The C oracle's decompose_edge_into_rows — the restatement the GPU
+    parity tests compare with — over the same default rows and offsets."""
+    from wgraph import abi
+    g = oracle_c.decompose_edges([edge], uniform_offsets(n))
+    out = []
+    for r in range(n):
+        v = (g["vert"][g["vert_off"][r]:g["vert_off"][r + 1]] >> 24) & 3
+        out.append(dict(full=int((v == abi.WG_VERT_FULL).sum()), top=int((v == abi.WG_VERT_TOP).sum()),
+                        bottom=int((v == abi.WG_VERT_BOTTOM).sum()),
+                        curves=list(g["curve"][g["curve_off"][r]:g["curve_off"][r + 1]])))
+    return out
 
 
-def test_decompose_cross_lane_emits_one_curve_per_spanned_row():  # :1653-1674
-    rows = _decompose((0, 0, 3, 2, 0), 4)
-    assert [len(r.curves) for r in rows] == [1, 1, 1, 1]
+def _decompose(impl, edge, n):
+    return _decompose_c(edge, n) if impl == "c" else _decompose_py(edge, n)
+
+
+@pytest.mark.parametrize("impl", ["c", "py"])
+def test_decompose_same_lane_emits_top_full_bottom_verticals(impl):  # :1631-1651
+    rows = _decompose(impl, (0, 1, 3, 1, 0), 4)
+    assert rows[0]["bottom"] == 1 and rows[0]["full"] == 0 and rows[0]["top"] == 0
+    assert rows[1]["full"] == 1 and rows[2]["full"] == 1
+    assert rows[3]["top"] == 1
+
+
+@pytest.mark.parametrize("impl", ["c", "py"])
+def test_decompose_cross_lane_emits_one_curve_per_spanned_row(impl):  # :1653-1674
+    rows = _decompose(impl, (0, 0, 3, 2, 0), 4)
+    assert [len(r["curves"]) for r in rows] == [1, 1, 1, 1]
     for r in rows:
-        assert not r.full and not r.top and not r.bottom
+        assert not r["full"] and not r["top"] and not r["bottom"]
 
 
-def test_decompose_cross_lane_segment_y_spans_row_strip():  # :1676-1702
-    rows = _decompose((0, 0, 2, 1, 0), 3)
-    c0, c1, c2 = rows[0].curves[0][0], rows[1].curves[0][0], rows[2].curves[0][0]
+@pytest.mark.parametrize("impl", ["c", "py"])
+def test_decompose_cross_lane_segment_y_spans_row_strip(impl):  # :1676-1702
+    rows = _decompose(impl, (0, 0, 2, 1, 0), 3)
+    c0, c1, c2 = rows[0]["curves"][0], rows[1]["curves"][0], rows[2]["curves"][0]
     assert abs(c0[1] - NODE_Y) < 0.5 and abs(c0[7] - ROW_HEIGHT) < 0.5
     assert abs(c1[1] - 0.0) < 0.5 and abs(c1[7] - ROW_HEIGHT) < 0.5
     assert abs(c2[1] - 0.0) < 0.5 and abs(c2[7] - NODE_Y) < 0.5
+
+
+def test_decompose_c_and_py_agree_bitwise():
+    """Both restatements give the same curve bits on the KAT edges."""
+    for edge, n in (((0, 0, 3, 2, 0), 4), ((0, 0, 2, 1, 0), 3), ((1, 3, 5, 0, 2), 7)):
+        a, b = _decompose_c(edge, n), _decompose_py(edge, n)
+        for ra, rb in zip(a, b):
+            assert (ra["full"], ra["top"], ra["bottom"]) == (rb["full"], rb["top"], rb["bottom"])
+            assert len(ra["curves"]) == len(rb["curves"])
+            for ca, cb in zip(ra["curves"], rb["curves"]):
+                assert np.asarray(ca, np.float32).tobytes() == np.asarray(cb, np.float32).tobytes(), edge
 
 
 def _heights_c(times):
