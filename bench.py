@@ -209,8 +209,8 @@ def extra_measurements(eng, dag, dev, torch, r0, r1, args, log):
              "edt_ms": round(ev.get("font_edt", 0.0), 4), "coverage_ms": round(ev.get("font_coverage", 0.0), 4),
              "note": ("warm_ms (= gpu_ms): rebuilds of the same font at the same parameters, which skip the TrueType "
                       "parse and uploads (the device inputs stand); cold_ms: the first build at new parameters "
-                      "(parse + flatten + upload + kernels, median of 5). The EDT passes touch ~20 MB per font "
-                      "(1024^2 coverage + u16 distance planes), so they run out of the 256 MB Infinity Cache: "
+                      "(parse + flatten + upload + kernels, median of 5). The EDT passes touch ~10 MB per font "
+                      "(1024^2 u8 coverage and SDF + four u16 distance planes), so they run out of the 256 MB Infinity Cache: "
                       "edt_ms is a cache-resident figure, not an HBM rate.")}
     if not args.no_cpu:
         # C2's CPU leg: an exact Felzenszwalb-Huttenlocher EDT in
