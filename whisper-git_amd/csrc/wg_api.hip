@@ -184,6 +184,12 @@ int wg_side_build_begin(wg_ctx *c, uint64_t m, float *h, float *rt, const float 
     }
     if (rc == WG_OK) rc = wg_heights_run(c, m, c->n_list, h);
     if (rc == WG_OK) rc = wg_rowtop_run(c, m, h, band, rt, 0);
+    if (rc == WG_OK) rc = wg_geom_prezero(c, m);   // (the build's geometry pass joins this stream first)
+    // r06: the next build's table (left to this list's emission by the place
+    // pass, hash_table_prepare's `later`), emptied here instead, beside the
+    // lane stage's latency-bound kernels — the emission saturates HBM and a
+    // clear queued there ran beside the next build's geometry kernels
+    if (rc == WG_OK && c->hash_on_side) rc = wg_hash_clear_next(c, c->stream);
     wg_side_done(c);
     if (rc != WG_OK) c->hash_built = c->hash_on_side = false;
     return rc;

@@ -153,6 +153,12 @@ struct EdgeRowsArgs {
     uint8_t *flags_kept;       // the flags the curve lists are filtered with (rowflags_lists)
     uint32_t *cntB, *diffF, *diffC, *cntCend, *cntPend, *carry_diff, *cntT, *top_fill, *carry_fill, *misc;
 };
+// FUSED (r06): the workspace was zeroed beforehand (wg_geom_prezero, on the
+// side stream beside the hash join), so the parent side of the counts
+// (k_edge_counts) is added here too, per edge, and the child side goes in by
+// atomics as well (a row's entries also collect other rows' parent-side
+// adds): one launch and one pass over the edges fewer.
+template <bool FUSED>
 __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) {
     static_assert(WG_SWEEP_CH == 64, "a wave's rows are one sweep chunk");
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,9 +170,21 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
     do {                                                                                             \
         const uint32_t c = (c_), p = (p_);                                                           \
         if (c < p) {                                                                                 \
-            cd += c / WG_SWEEP_CH + 1 <= p / WG_SWEEP_CH;                                            \
+            const uint32_t k0_ = c / WG_SWEEP_CH + 1, k1_ = p / WG_SWEEP_CH;                          \
+            cd += k0_ <= k1_;                                                                        \
             if (same_) { b++; f += c + 1 < p; }                                                      \
             else { cc += c + 1 < p; ce++; }   /* (the swept lists' flag row is all zero: no child-end filter) */ \
+            if (FUSED) {   /* k_edge_counts' parent side (:526-528) */                               \
+                if (k0_ <= k1_) atomicAdd(&A.carry_diff[k1_ + 1], 0xFFFFFFFFu);                       \
+                if (same_) {                                                                         \
+                    atomicAdd(&A.cntT[p], 1u);                                                       \
+                    if (c + 1 < p) atomicAdd(&A.diffF[p], 0xFFFFFFFFu);                              \
+                } else {                                                                             \
+                    if (c + 1 < p) atomicAdd(&A.diffC[p], 0xFFFFFFFFu);                              \
+                    atomicAdd(&A.cntCend[p], 1u);                                                    \
+                    atomicAdd(&A.cntPend[p], 1u);                                                    \
+                }                                                                                    \
+            }                                                                                        \
         }                                                                                            \
     } while (0)
         if (A.prow) {
@@ -193,13 +211,19 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
         }
 #undef WG_EDGE_COUNT
         A.cntB[r] = b;
-        A.diffF[r + 1] = f;
-        A.diffC[r + 1] = cc;
-        A.cntCend[r] = ce;
-        A.cntPend[r] = 0u;
-        A.cntT[r] = 0u;
-        A.top_fill[r] = 0u;
-        A.zflags[r] = 0;
+        if (FUSED) {   // (zeroed; other rows' parent sides add into these entries)
+            if (f) atomicAdd(&A.diffF[r + 1], f);
+            if (cc) atomicAdd(&A.diffC[r + 1], cc);
+            if (ce) atomicAdd(&A.cntCend[r], ce);
+        } else {
+            A.diffF[r + 1] = f;
+            A.diffC[r + 1] = cc;
+            A.cntCend[r] = ce;
+            A.cntPend[r] = 0u;
+            A.cntT[r] = 0u;
+            A.top_fill[r] = 0u;
+            A.zflags[r] = 0;
+        }
         // RowGeometry (k_row_basic)
         float ht, ny;
         if (A.band) {
@@ -222,12 +246,18 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
         A.rowflags[r] = fl;
         A.flags_kept[r] = fl;
     }
-    if (r == 0) { A.diffF[0] = 0u; A.diffC[0] = 0u; A.carry_diff[0] = 0u; }
-    if (r < 64) A.misc[r] = 0u;
+    if (!FUSED) {
+        if (r == 0) { A.diffF[0] = 0u; A.diffC[0] = 0u; A.carry_diff[0] = 0u; }
+        if (r < 64) A.misc[r] = 0u;
+    }
     const uint32_t tot = wg_wave_scan(cd, 0u, [](uint32_t x, uint32_t y) { return x + y; });
     if ((threadIdx.x & 63) == 63 && r - 63 < n) {
-        A.carry_diff[r / WG_SWEEP_CH + 1] = tot;
-        A.carry_fill[r / WG_SWEEP_CH] = 0u;
+        if (FUSED) {
+            if (tot) atomicAdd(&A.carry_diff[r / WG_SWEEP_CH + 1], tot);
+        } else {
+            A.carry_diff[r / WG_SWEEP_CH + 1] = tot;
+            A.carry_fill[r / WG_SWEEP_CH] = 0u;
+        }
     }
 }
 
@@ -450,17 +480,16 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
     if ((threadIdx.x & 31) == 0 && sub < nbs) { bsV[sub] = tV; bsC[sub] = tC; bsK[sub] = tK; }
 }
 
-// one pass over the edges: same-lane edges' ids into their parent row's
-// top-half slots (sorted and packed by the sweep wave, top_finish_row), and every edge into
-// the carry-in list of each 64-row chunk it is alive across (sorted by
-// k_carry_sort)
+// one pass over the edges: every edge into the carry-in list of each 64-row
+// chunk it is alive across (sorted by k_carry_sort / the sweep's rank).
+// (r06: the top halves are no longer placed here: the sweep wave finds them
+// by ballot in its row loop, already in edge order — every same-lane edge
+// ending at a row of the chunk is in the chunk's edge set.)
 // The (edge, chunk) registrations of a wave's 64 edges are dealt to its
 // lanes in turn: an edge alive across thousands of chunks (a long-lived
 // branch of a wide list) no longer loops alone while its wave waits
 // (linuxwide: 344 us with one lane per edge)
 __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges,
-                            const uint32_t *__restrict__ vert_off,
-                            const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert,
                             const uint32_t *__restrict__ carry_off, uint32_t *carry_fill, uint32_t *carry,
                             const uint32_t *__restrict__ ne_dev, Cap vc, Cap cc, uint32_t *ovf) {
     __shared__ uint32_t s_pre[256 / 64][64], s_k0[256 / 64][64];
@@ -476,6 +505,7 @@ __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *_
     const uint32_t span = (live && k1 >= k0) ? k1 - k0 + 1 : 0u;
     const uint32_t inc = wg_wave_scan(span, 0u, [](uint32_t x, uint32_t y) { return x + y; });
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    if (!tot) return;   // (uniform)
     s_pre[wv][lid] = inc - span;
     s_k0[wv][lid] = k0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -492,39 +522,6 @@ __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *_
         const uint32_t q = s_k0[wv][l] + (t - s_pre[wv][l]);
         const uint32_t pos = atomicAdd(&carry_fill[q], 1u);
         carry[carry_off[q] + pos] = (uint32_t)(kbase + l);
-    }
-    if (!live || e.child_lane != e.parent_lane) return;
-    const uint32_t p = e.parent_row;
-    const uint32_t pos = atomicAdd(&top_fill[p], 1u);
-    vert[vert_off[p] + scanF[p + 1] + pos] = (uint32_t)k;   // edge id, packed below
-}
-
-// per row: the top-half entries (edge ids placed by k_top_carry) sorted by
-// edge id and packed, then the bottom halves (same-lane edges of child r, in
-// parent order) after them
-// (done by the full pass's sweep wave for its 64 rows, one row per lane,
-// before its row loop: one launch fewer)
-__device__ __forceinline__ void top_finish_row(uint64_t r, const uint32_t *__restrict__ edge_off,
-                                               const wg_edge *__restrict__ edges, const uint32_t *__restrict__ vert_off,
-                                               const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT,
-                                               uint32_t *vert) {
-    const uint32_t nt = cntT[r];
-    uint32_t *v = vert + vert_off[r] + scanF[r + 1];
-    for (uint32_t i = 1; i < nt; i++) {   // insertion sort by edge id (in-degree is small)
-        uint32_t x = v[i];
-        uint32_t j = i;
-        while (j > 0 && v[j - 1] > x) { v[j] = v[j - 1]; j--; }
-        v[j] = x;
-    }
-    for (uint32_t i = 0; i < nt; i++) {
-        const wg_edge e = edges[v[i]];
-        v[i] = pack_vert(e.child_lane, WG_VERT_TOP, e.color);
-    }
-    uint32_t o = nt;
-    for (uint32_t k = edge_off[r]; k < edge_off[r + 1]; k++) {
-        const wg_edge e = edges[k];
-        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane)
-            v[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
     }
 }
 
@@ -567,7 +564,7 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ err, uint32_t *E, uint32_t *C, uint32_t *P, uint32_t *I, uint32_t *NC, uint32_t *NP,
-        uint32_t *NI, bool super) {
+        uint32_t *NI, bool super, const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT) {
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
@@ -578,6 +575,9 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
     const uint32_t voff_v = (!super && lid < nr) ? vert_off[rr] : 0u;
     const uint32_t coff_v = (super && lid < nr) ? curve_off[rr] : 0u;
     const uint32_t koff_v = (!super && lid < nr) ? kept_off[rr] : 0u;
+    // (full pass) the row's top halves start after its full verticals, its bottom halves after the tops
+    const uint32_t tof_v = (!super && lid < nr) ? voff_v + scanF[rr + 1] : 0u;
+    const uint32_t bof_v = (!super && lid < nr) ? tof_v + cntT[rr] : 0u;
     const uint32_t E1 = edge_off[R1];
     const uint32_t E0 = (uint32_t)__builtin_amdgcn_readlane((int)eoff_v, 0);
     const bool staged = E1 - E0 <= (uint32_t)SW_NE;
@@ -637,6 +637,8 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
         uint32_t fbase = (uint32_t)__builtin_amdgcn_readlane((int)voff_v, (int)j);
         uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
         uint32_t kbase = (uint32_t)__builtin_amdgcn_readlane((int)koff_v, (int)j);
+        uint32_t tbase = (uint32_t)__builtin_amdgcn_readlane((int)tof_v, (int)j);
+        uint32_t bbase = (uint32_t)__builtin_amdgcn_readlane((int)bof_v, (int)j);
         uint32_t kept = 0;
         for (uint32_t base = 0; base < cnt; base += 64) {
             const uint32_t idx = base + lid;
@@ -645,6 +647,16 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
             if (act) { eid = E[idx]; c = C[idx]; p = P[idx]; info = I[idx]; }
             __builtin_amdgcn_wave_barrier();
             const bool same = (info & 0x10000000u) != 0;
+            // top halves (same-lane edges into row r, edge order) and bottom
+            // halves (same-lane edges of child r, edge order): the list holds
+            // both in edge order (:526-546)
+            const bool top = !super && act && same && p == r && c < p;
+            const bool bot = !super && act && same && c == r && c < p;
+            const uint64_t mt = __ballot(top), mb = __ballot(bot);
+            if (top) vert[tbase + mbcnt(mt)] = pack_vert(info & 0xFFFFFFu, WG_VERT_TOP, (info >> 24) & 0xFu);
+            if (bot) vert[bbase + mbcnt(mb)] = pack_vert(info & 0xFFFFFFu, WG_VERT_BOTTOM, (info >> 24) & 0xFu);
+            tbase += __builtin_popcountll(mt);
+            bbase += __builtin_popcountll(mb);
             const bool full = !super && act && same && c < r && r < p;
             const bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
             const bool seg = act && !same && c <= r && r <= p;
@@ -679,7 +691,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ err, Cap vc, Cap sc, uint32_t *ovf, bool super, const uint32_t *__restrict__ run_if,
-        const uint32_t *__restrict__ done) {
+        const uint32_t *__restrict__ done, const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT) {
     if (super && (*run_if == 0 || *done != 0)) return;   // (uniform over the grid)
     const Cap gs[2] = {vc, sc};
     if (over_all(gs, ovf)) return;
@@ -700,7 +712,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         const bool ok = sweep_chunk_lds(SW_CAP, list[i], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
                                         curve_off, vert, curve_ref, curve_row, kept_off, kept_ref, kept_row, err,
                                         s_eid + o, s_c + o, s_p + o,
-                                        s_info + o, n_c[w], n_p[w], n_info[w], super);
+                                        s_info + o, n_c[w], n_p[w], n_info[w], super, scanF, cntT);
         if (!ok && (threadIdx.x & 63) == 0) {
             const uint32_t at = atomicAdd(&n_wide, 1u);
             if (at < 64u) wide[at] = list[i];
@@ -716,7 +728,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
             if (!sweep_chunk_lds(SW_CAP_BLOCK, wide[j], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
                                  curve_off, vert, curve_ref, curve_row, kept_off, kept_ref, kept_row, err, s_eid, s_c,
                                  s_p, s_info, n_c[0], n_p[0],
-                                 n_info[0], super) &&
+                                 n_info[0], super, scanF, cntT) &&
                 (threadIdx.x & 63) == 0)
                 atomicOr(&err[0], 1u);
 }
@@ -782,6 +794,22 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[SW_WAVES][SW_STAGE];
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t q = q0 + (uint64_t)blockIdx.x * SW_WAVES + (threadIdx.x >> 6);   // chunks [q0, q1)
+    // Every load that depends on nothing else is issued before any is waited
+    // on (r06): the guards, the chunk's carry and edge ranges and the per-row
+    // scalars (a tail wave past q1 reads chunk q1 - 1's and returns below).
+    const uint64_t qc = q < q1 ? q : q1 - 1;
+    const uint64_t R0 = qc * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
+    const uint32_t nr = (uint32_t)(R1 - R0);
+    const uint64_t rr = R0 + lid;
+    const bool inr = lid < nr;
+    const uint32_t a = carry_off[qc], a1 = carry_off[qc + 1];
+    const uint32_t E0 = edge_off[R0], E1 = edge_off[R1];
+    const uint32_t voff_v = (!SUPER && inr) ? vert_off[rr] : 0u;
+    const uint32_t coff_v = (SUPER && inr) ? curve_off[rr] : 0u;
+    const uint32_t koff_v = (!SUPER && inr) ? kept_off[rr] : 0u;
+    const uint32_t rf_v = (!SUPER && inr) ? rowflags[rr] : 0u;
+    const uint32_t nf_v = (!SUPER && inr) ? scanF[rr + 1] : 0u;   // the row's full verticals (its tops follow them)
+    const uint32_t nt_v = (!SUPER && inr) ? cntT[rr] : 0u;        // ... and its top halves (the bottoms follow)
     const Cap gs[3] = {vc, sc, cc};
     const CapVals<3> gv = cap_read(gs, ovf);
     if (SUPER) {
@@ -789,51 +817,54 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         if ((ri == 0) | (dn != 0)) return;
     }
     if (cap_over(gv, gs, ovf) || q >= q1) return;
-    const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
-    const uint32_t nr = (uint32_t)(R1 - R0);
-    // the chunk's top and bottom halves (their entries follow the full ones)
-    if (!SUPER && lid < nr) top_finish_row(R0 + lid, edge_off, edges, vert_off, scanF, cntT, vert);
-    const uint32_t a = carry_off[q], ncar = carry_off[q + 1] - a;
-    const uint32_t E0 = edge_off[R0], E1 = edge_off[R1];
+    const uint32_t ncar = a1 - a;
     const uint32_t total = ncar + (E1 - E0);
     if (total > reg_cap || total > 64u * SW_SLOTS) {   // the LDS sweep (k_sweep_lds) reads the ranked list from HBM
         carry_rank(carry + a, ncar, s_stage[threadIdx.x >> 6], carry_sorted + a);
         if (lid == 0) big[atomicAdd(big_n, 1u)] = (uint32_t)q;
         return;
     }
+    // the chunk's own edges (they follow the carry-in in edge order) load
+    // while the carry-in list is ranked
+    const uint32_t nslots = (total + 63) / 64;
+    wg_edge eo[SW_SLOTS];
+#pragma unroll
+    for (int sl = 0; sl < SW_SLOTS; sl++) {
+        const uint32_t idx = 64u * sl + lid;
+        eo[sl] = wg_edge{0u, 0u, 0u, 0u, 0u};
+        if ((uint32_t)sl < nslots && idx >= ncar && idx < total) eo[sl] = edges[E0 + (idx - ncar)];
+    }
     uint32_t *sorted = s_car[threadIdx.x >> 6];
     carry_rank(carry + a, ncar, s_stage[threadIdx.x >> 6], sorted);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // per-row scalars of the chunk, one row per lane
-    const uint64_t rr = R0 + lid;
-    const uint32_t voff_v = (!SUPER && lid < nr) ? vert_off[rr] : 0u;
-    const uint32_t coff_v = (SUPER && lid < nr) ? curve_off[rr] : 0u;
-    const uint32_t koff_v = (!SUPER && lid < nr) ? kept_off[rr] : 0u;
-    const uint32_t rf_v = (!SUPER && lid < nr) ? rowflags[rr] : 0u;
-    // per slot: the edge id, the packed full-vertical entry and two row windows
-    // as (first row, length - 1) for an unsigned compare: full verticals on
+    // per slot: the edge id, the packed full-vertical entry, two row windows
+    // as (first row, length - 1) for an unsigned compare — full verticals on
     // rows c < r < p of same-lane edges, curve segments on rows c <= r <= p of
-    // cross-lane edges; an empty window has first row ~0.  A full pass writes
-    // the curve list filtered by the row's strip flags (every segment of a row
-    // without flags); the flag-free superset is swept only for a frame pass
-    // whose flags differ (SUPER).
-    uint32_t ek[SW_SLOTS], fb[SW_SLOTS], fl[SW_SLOTS], cb[SW_SLOTS], cl[SW_SLOTS], pv[SW_SLOTS];
-    const uint32_t nslots = (total + 63) / 64;
+    // cross-lane edges; an empty window has first row ~0 — and (full pass) the
+    // chunk rows of a same-lane edge's ends (top half at p, bottom half at c;
+    // 0xFF outside the chunk).  A full pass writes the curve list filtered by
+    // the row's strip flags (every segment of a row without flags); the
+    // flag-free superset is swept only for a frame pass whose flags differ
+    // (SUPER).
+    uint32_t ek[SW_SLOTS], fb[SW_SLOTS], fl[SW_SLOTS], cb[SW_SLOTS], cl[SW_SLOTS], pv[SW_SLOTS], tb[SW_SLOTS];
 #pragma unroll
     for (int sl = 0; sl < SW_SLOTS; sl++) {
         const uint32_t idx = 64u * sl + lid;
-        ek[sl] = 0; fb[sl] = ~0u; fl[sl] = 0; cb[sl] = ~0u; cl[sl] = 0; pv[sl] = 0;
+        ek[sl] = 0; fb[sl] = ~0u; fl[sl] = 0; cb[sl] = ~0u; cl[sl] = 0; pv[sl] = 0; tb[sl] = 0xFFFFu;
         if ((uint32_t)sl < nslots && idx < total) {
             const uint32_t k = idx < ncar ? sorted[idx] : E0 + (idx - ncar);
-            const wg_edge e = edges[k];
+            const wg_edge e = idx < ncar ? edges[k] : eo[sl];
             ek[sl] = k;
             const uint32_t c = e.child_row, p = e.parent_row;
             if (c < p) {
                 if (e.child_lane == e.parent_lane) {
                     if (c + 1 < p) { fb[sl] = c + 1; fl[sl] = p - c - 2; }
                     pv[sl] = pack_vert(e.child_lane & 0xFFFFFFu, WG_VERT_FULL, e.color & 0xFu);
+                    const uint32_t tp = p - (uint32_t)R0 < nr ? p - (uint32_t)R0 : 0xFFu;
+                    const uint32_t bt = c - (uint32_t)R0 < nr ? c - (uint32_t)R0 : 0xFFu;
+                    tb[sl] = tp << 8 | bt;
                 } else {
                     cb[sl] = c;
                     cl[sl] = p - c;
@@ -847,6 +878,10 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
         uint32_t kbase = (uint32_t)__builtin_amdgcn_readlane((int)koff_v, (int)j);
         const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)rf_v, (int)j);
+        // (full pass) the row's top halves after its full verticals, its
+        // bottom halves after the tops; both in edge order = slot order
+        uint32_t tbase = fbase + (uint32_t)__builtin_amdgcn_readlane((int)nf_v, (int)j);
+        uint32_t bbase = tbase + (uint32_t)__builtin_amdgcn_readlane((int)nt_v, (int)j);
 #pragma unroll
         for (int sl = 0; sl < SW_SLOTS; sl++) {
             if ((uint32_t)sl >= nslots) break;
@@ -856,6 +891,16 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
                 if (mf) {
                     if (full) vert[fbase + mbcnt(mf)] = pv[sl];
                     fbase += __builtin_popcountll(mf);
+                }
+                const bool top = (tb[sl] >> 8) == j, bot = (tb[sl] & 0xFFu) == j;
+                const uint64_t mt = __ballot(top), mb = __ballot(bot);
+                if (mt) {
+                    if (top) vert[tbase + mbcnt(mt)] = pv[sl] | (WG_VERT_TOP << 24);
+                    tbase += __builtin_popcountll(mt);
+                }
+                if (mb) {
+                    if (bot) vert[bbase + mbcnt(mb)] = pv[sl] | (WG_VERT_BOTTOM << 24);
+                    bbase += __builtin_popcountll(mb);
                 }
             }
             const bool curv = r - cb[sl] <= cl[sl];
@@ -1226,7 +1271,8 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
                        (const uint32_t *)big_n, E, edge_off, carry_off, (const uint32_t *)carry_sorted,
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), err,
-                       vc, sc, ovf, false, (const uint32_t *)nullptr, (const uint32_t *)nullptr);
+                       vc, sc, ovf, false, (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)L.cntF,
+                       (const uint32_t *)L.cntT);
     // the records of the slice's rows: a grid for its share of the records
     // (+ a quarter), the kernels stride over the rest
     uint64_t grid_recs = L.n_super_grid;
@@ -1262,13 +1308,37 @@ static void launch_superset(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t
                        (const uint32_t *)big_n, E, edge_off, carry_off, (const uint32_t *)c->carry_sorted.as<uint32_t>(),
                        c->rowflags.as<const uint8_t>(), (const uint32_t *)nullptr, soff, (uint32_t *)nullptr,
                        c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(), (const uint32_t *)nullptr,
-                       (uint32_t *)nullptr, (uint32_t *)nullptr, err, g, g, ovf, true, run_if, (const uint32_t *)(err + 5));
+                       (uint32_t *)nullptr, (uint32_t *)nullptr, err, g, g, ovf, true, run_if, (const uint32_t *)(err + 5),
+                       (const uint32_t *)nullptr, (const uint32_t *)nullptr);
 }
 
 int wg_geom_lists_flush(wg_ctx *c) {
     if (!c->glist.deferred) return WG_OK;
     c->glist.deferred = false;
     return wg_geom_lists(c, 0, c->glist.n, 0, c->stream);
+}
+
+// The full pass's zero-initialised workspace (per-row counts and difference
+// arrays, top fill, carry counts and fill, sweep flags, the all-zero flag row)
+// for n rows, in 32-bit words
+static uint64_t geom_zero_words(uint64_t n) {
+    const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
+    const uint64_t rowa = (n + 2 + 63) & ~63ull, cha = (nch + 2 + 63) & ~63ull;
+    return (7 * rowa + 2 * cha + 64 + rowa / 4 + 3) & ~3ull;   // cleared in 16-byte units
+}
+
+// r06: the workspace of the next full pass over n rows, zeroed on the current
+// stream (the build's side stream, beside the hash join and the lanes; the
+// geometry stage joins it first), so the pass counts both edge ends in one
+// kernel (k_edges_rows<true>)
+int wg_geom_prezero(wg_ctx *c, uint64_t n) {
+    c->geom_zero_n = ~0ull;
+    if (!n) return WG_OK;
+    const uint64_t zw = geom_zero_words(n);
+    WG_ALLOC(c, c->geom_zero, zw * 4);
+    WG_HIP(c, hipMemsetAsync(c->geom_zero.p, 0, zw * 4, c->stream));
+    c->geom_zero_n = n;
+    return WG_OK;
 }
 
 int wg_stage_geometry(wg_ctx *c, const float *d_band) {
@@ -1344,7 +1414,10 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     // are swept as a superset.
     const uint64_t nch = (n + WG_SWEEP_CH - 1) / WG_SWEEP_CH;
     const uint64_t rowa = (n + 2 + 63) & ~63ull, cha = (nch + 2 + 63) & ~63ull;
-    const uint64_t zwords = (7 * rowa + 2 * cha + 64 + rowa / 4 + 3) & ~3ull;   // cleared in 16-byte units
+    const uint64_t zwords = geom_zero_words(n);
+    // zeroed beforehand for this pass (wg_geom_prezero): the fused count kernel
+    const bool prezero = c->geom_zero_n == n && c->geom_zero.cap >= zwords * 4;
+    c->geom_zero_n = ~0ull;
     WG_ALLOC(c, c->geom_zero, zwords * 4);
     WG_ALLOC(c, c->rowflags_lists, n + 4);
     uint32_t *cntF = c->geom_zero.as<uint32_t>(), *cntT = cntF + rowa, *cntB = cntT + rowa;
@@ -1373,10 +1446,11 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         A.flags_kept = c->rowflags_lists.as<uint8_t>();
         A.cntB = cntB; A.diffF = cntF; A.diffC = cntC; A.cntCend = cntCend; A.cntPend = cntPend; A.carry_diff = carry_cnt;
         A.cntT = cntT; A.top_fill = top_fill; A.carry_fill = carry_fill; A.misc = sweep_err;
-        hipLaunchKernelGGL(k_edges_rows, dim3(blocks(n)), dim3(256), 0, s, n, A);
+        if (prezero) hipLaunchKernelGGL(k_edges_rows<true>, dim3(blocks(n)), dim3(256), 0, s, n, A);
+        else hipLaunchKernelGGL(k_edges_rows<false>, dim3(blocks(n)), dim3(256), 0, s, n, A);
         c->edges_pending = false;
     }
-    if (ne)
+    if (ne && !prezero)
         hipLaunchKernelGGL(k_edge_counts, dim3(blocks(ne)), dim3(T), 0, s, ne, E, zflags, cntT, cntF, cntC, cntCend,
                            cntPend, carry_cnt, ne_dev);
     // carry-in offsets: the exclusive scan of the chunk difference counts, then
@@ -1449,10 +1523,9 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     wg_stage_end(c);
 
     wg_stage_begin(c, "geom_lists");
-    uint32_t *vert = c->vert.as<uint32_t>();
     if (ne)
-        hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, vert,
-                           (const uint32_t *)carry_off, carry_fill, c->carry.as<uint32_t>(), ne_dev, vc, cc, ovf);
+        hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, (const uint32_t *)carry_off, carry_fill,
+                           c->carry.as<uint32_t>(), ne_dev, vc, cc, ovf);
     WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
     wg_ctx::ListsDef &L = c->glist;
     L = wg_ctx::ListsDef{};

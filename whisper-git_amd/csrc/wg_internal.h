@@ -410,7 +410,7 @@ struct wg_ctx {
             replay_serial = false;
             replay_dc = false;
             dc_warm = dc_warm_fixed ? dc_warm_fixed : WG_DC_WARM0;
-            dc_probe = false;
+            dc_probe = dc_probe_down = false;
             dc_warm_frozen = false;
             dc_blind = 2;
             replay_blind = 4;
@@ -424,7 +424,7 @@ struct wg_ctx {
             replay_serial = false;
             replay_dc = true;
             dc_warm = dc_warm_fixed ? dc_warm_fixed : WG_DC_WARM0;
-            dc_probe = false;
+            dc_probe = dc_probe_down = false;
             dc_blind = 2;
             serial_builds = 0;
         }
@@ -435,27 +435,39 @@ struct wg_ctx {
     // tries a doubled warm-up once (kept only if the model prices it lower:
     // long-lived lanes need more than any affordable warm-up); the blind count.
     bool dc_probe = false;         // the last compacted replay tried a doubled warm-up
-    bool dc_warm_frozen = false;   // ... and it did not pay
+    bool dc_probe_down = false;    // ... or a halved one (r06)
+    bool dc_warm_frozen = false;   // a probe did not pay: the warm-up stays
     double dc_cost_before = 0;     // the modelled cost before that probe
+    static constexpr uint32_t WG_DC_WARM_MIN = 512;
     void dc_adapt(uint32_t fp, uint64_t nev, uint32_t nw, uint32_t warm, uint32_t chunk, uint32_t serial_nw) {
         if (fp == 0) return;
         const double cost = dc_cost_us(nw, warm, chunk, fp);
         if (replay_mode == 0 && fp > 2 && cost > serial_cost_us(nev, serial_nw)) {
             replay_serial = true;
             serial_builds = 0;
-            dc_probe = false;
+            dc_probe = dc_probe_down = false;
             return;
         }
-        if (dc_probe) {
-            dc_probe = false;
-            if (cost >= dc_cost_before) {   // the longer warm-up did not pay: back, and no more probes
-                dc_warm = warm / 2 >= 64 ? warm / 2 : 64;
+        if (dc_probe || dc_probe_down) {
+            // the probe's warm-up stays only if the model prices it lower
+            // with the iterations it actually took; else back, and no more probes
+            if (cost >= dc_cost_before) {
+                dc_warm = dc_probe ? (warm / 2 >= 64 ? warm / 2 : 64) : warm * 2;
                 dc_warm_frozen = true;
             }
+            dc_probe = dc_probe_down = false;
         } else if (fp > 3 && warm < WG_DC_WARM_MAX && !dc_warm_fixed && !dc_warm_frozen) {
             dc_cost_before = cost;
             dc_warm = warm * 2;
             dc_probe = true;
+        } else if (fp <= 3 && warm > WG_DC_WARM_MIN && !dc_warm_fixed && !dc_warm_frozen) {
+            // (r06) iteration 1 is the warm-up's cost: a list whose state
+            // forgets within a shorter window (the Linux shape: fixed point at
+            // iteration 2 with 8192 events of warm-up, 205 of the replay's
+            // 230 us) tries half of it
+            dc_cost_before = cost;
+            dc_warm = warm / 2;
+            dc_probe_down = true;
         }
         dc_blind = fp >= dc_blind ? fp : (dc_blind + fp) / 2;
         if (dc_blind < 2) dc_blind = 2;
@@ -534,6 +546,7 @@ struct wg_ctx {
     DevBuf rt_sup;          // super-chunk tables, binade bases and walk states
     DevBuf rt_flags;        // uint32 [4]
     DevBuf geom_zero;       // zeroed per pass: per-row counts / diff arrays, top fill, carry counts, sweep flags
+    uint64_t geom_zero_n = ~0ull;   // rows the workspace was zeroed for ahead of the pass (wg_geom_prezero), or ~0
     DevBuf vert_off, curve_off;             // uint32 [N+1]
     DevBuf vert, curve, curve_color;
     DevBuf curve_ref;       // uint32 [n_curve] edge id per curve record
@@ -800,8 +813,9 @@ inline uint64_t wg_bs_blocks(uint64_t n) { return (n + WG_BS_THREADS - 1) / WG_B
 
 // stages -------------------------------------------------------------------------
 int wg_stage_hash_join(wg_ctx *c);            // wg_hash.hip
-int wg_hash_table_launch(wg_ctx *c);
-int wg_hash_clear_next(wg_ctx *c, hipStream_t s);   // the next build's table, emptied beside an emission          // wg_hash.hip: place + settle on c->stream
+int wg_hash_table_launch(wg_ctx *c);          // wg_hash.hip: place + settle on c->stream
+int wg_hash_clear_next(wg_ctx *c, hipStream_t s);   // the next build's table, emptied beside an emission
+int wg_geom_prezero(wg_ctx *c, uint64_t n);   // wg_geom.hip: the next full pass's workspace zeroed on c->stream
 // the build's side stream: the hash table (joined by the hash join's fix-up
 // kernel), then the heights and the row_top (joined by the geometry)
 int wg_side_build_begin(wg_ctx *c, uint64_t m, float *h, float *rt, const float *band, const float *band_host,

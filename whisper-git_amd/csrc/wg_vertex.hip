@@ -609,8 +609,10 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         launch(vcap, early_grid, early_grid, 0, 0);
     }
     if (fused_read && !c->sh.on && c->side) {
-        // the next build's empty table, on the side stream beside the tiles
-        // (ordered after the previous builds' use of it by this build's fork)
+        // the next build's empty table, on the side stream (ordered after the
+        // previous builds' use of it by this build's fork); r06: a build with
+        // its table on the side stream has cleared it there already, beside
+        // its lanes (wg_side_build_begin), and this finds it clean
         if (const int rc = wg_hash_clear_next(c, c->side)) return rc;
     }
     uint64_t fv[4 + WG_PENDING_ITEMS] = {0};
