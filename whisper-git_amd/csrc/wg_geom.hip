@@ -480,16 +480,18 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
     if ((threadIdx.x & 31) == 0 && sub < nbs) { bsV[sub] = tV; bsC[sub] = tC; bsK[sub] = tK; }
 }
 
-// one pass over the edges: every edge into the carry-in list of each 64-row
-// chunk it is alive across (sorted by k_carry_sort / the sweep's rank).
-// (r06: the top halves are no longer placed here: the sweep wave finds them
-// by ballot in its row loop, already in edge order — every same-lane edge
-// ending at a row of the chunk is in the chunk's edge set.)
+// one pass over the edges: same-lane edges into their parent row's top-half
+// slots — the packed entry in the vertical list, the edge id (the sort key)
+// beside it in top_key (r06: the sweep wave sorts them by key in registers,
+// top_finish_row, with no gather of the edges) — and every edge into the
+// carry-in list of each 64-row chunk it is alive across (ranked by the sweep)
 // The (edge, chunk) registrations of a wave's 64 edges are dealt to its
 // lanes in turn: an edge alive across thousands of chunks (a long-lived
 // branch of a wide list) no longer loops alone while its wave waits
 // (linuxwide: 344 us with one lane per edge)
 __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges,
+                            const uint32_t *__restrict__ vert_off,
+                            const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert, uint32_t *top_key,
                             const uint32_t *__restrict__ carry_off, uint32_t *carry_fill, uint32_t *carry,
                             const uint32_t *__restrict__ ne_dev, Cap vc, Cap cc, uint32_t *ovf) {
     __shared__ uint32_t s_pre[256 / 64][64], s_k0[256 / 64][64];
@@ -505,6 +507,12 @@ __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *_
     const uint32_t span = (live && k1 >= k0) ? k1 - k0 + 1 : 0u;
     const uint32_t inc = wg_wave_scan(span, 0u, [](uint32_t x, uint32_t y) { return x + y; });
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    if (live && e.child_lane == e.parent_lane) {
+        const uint32_t p = e.parent_row;
+        const uint32_t at = vert_off[p] + scanF[p + 1] + atomicAdd(&top_fill[p], 1u);
+        vert[at] = pack_vert(e.child_lane, WG_VERT_TOP, e.color);
+        top_key[at] = (uint32_t)k;
+    }
     if (!tot) return;   // (uniform)
     s_pre[wv][lid] = inc - span;
     s_k0[wv][lid] = k0;
@@ -564,7 +572,7 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ err, uint32_t *E, uint32_t *C, uint32_t *P, uint32_t *I, uint32_t *NC, uint32_t *NP,
-        uint32_t *NI, bool super, const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT) {
+        uint32_t *NI, bool super) {
     const uint32_t lid = threadIdx.x & 63;
     const uint64_t R0 = q * WG_SWEEP_CH, R1 = (R0 + WG_SWEEP_CH < n) ? R0 + WG_SWEEP_CH : n;
     const uint32_t nr = (uint32_t)(R1 - R0);
@@ -575,9 +583,6 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
     const uint32_t voff_v = (!super && lid < nr) ? vert_off[rr] : 0u;
     const uint32_t coff_v = (super && lid < nr) ? curve_off[rr] : 0u;
     const uint32_t koff_v = (!super && lid < nr) ? kept_off[rr] : 0u;
-    // (full pass) the row's top halves start after its full verticals, its bottom halves after the tops
-    const uint32_t tof_v = (!super && lid < nr) ? voff_v + scanF[rr + 1] : 0u;
-    const uint32_t bof_v = (!super && lid < nr) ? tof_v + cntT[rr] : 0u;
     const uint32_t E1 = edge_off[R1];
     const uint32_t E0 = (uint32_t)__builtin_amdgcn_readlane((int)eoff_v, 0);
     const bool staged = E1 - E0 <= (uint32_t)SW_NE;
@@ -637,8 +642,6 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
         uint32_t fbase = (uint32_t)__builtin_amdgcn_readlane((int)voff_v, (int)j);
         uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
         uint32_t kbase = (uint32_t)__builtin_amdgcn_readlane((int)koff_v, (int)j);
-        uint32_t tbase = (uint32_t)__builtin_amdgcn_readlane((int)tof_v, (int)j);
-        uint32_t bbase = (uint32_t)__builtin_amdgcn_readlane((int)bof_v, (int)j);
         uint32_t kept = 0;
         for (uint32_t base = 0; base < cnt; base += 64) {
             const uint32_t idx = base + lid;
@@ -647,16 +650,6 @@ __device__ bool sweep_chunk_lds(uint32_t cap, uint64_t q, uint64_t n, const wg_e
             if (act) { eid = E[idx]; c = C[idx]; p = P[idx]; info = I[idx]; }
             __builtin_amdgcn_wave_barrier();
             const bool same = (info & 0x10000000u) != 0;
-            // top halves (same-lane edges into row r, edge order) and bottom
-            // halves (same-lane edges of child r, edge order): the list holds
-            // both in edge order (:526-546)
-            const bool top = !super && act && same && p == r && c < p;
-            const bool bot = !super && act && same && c == r && c < p;
-            const uint64_t mt = __ballot(top), mb = __ballot(bot);
-            if (top) vert[tbase + mbcnt(mt)] = pack_vert(info & 0xFFFFFFu, WG_VERT_TOP, (info >> 24) & 0xFu);
-            if (bot) vert[bbase + mbcnt(mb)] = pack_vert(info & 0xFFFFFFu, WG_VERT_BOTTOM, (info >> 24) & 0xFu);
-            tbase += __builtin_popcountll(mt);
-            bbase += __builtin_popcountll(mb);
             const bool full = !super && act && same && c < r && r < p;
             const bool skip = (r == c) ? (rf & RF_CHILD) : (r == p) ? (rf & RF_PARENT) : (rf & RF_ZERO);
             const bool seg = act && !same && c <= r && r <= p;
@@ -691,7 +684,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         uint32_t *__restrict__ vert, uint32_t *__restrict__ curve_ref, uint32_t *__restrict__ curve_row,
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ err, Cap vc, Cap sc, uint32_t *ovf, bool super, const uint32_t *__restrict__ run_if,
-        const uint32_t *__restrict__ done, const uint32_t *__restrict__ scanF, const uint32_t *__restrict__ cntT) {
+        const uint32_t *__restrict__ done) {
     if (super && (*run_if == 0 || *done != 0)) return;   // (uniform over the grid)
     const Cap gs[2] = {vc, sc};
     if (over_all(gs, ovf)) return;
@@ -712,7 +705,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
         const bool ok = sweep_chunk_lds(SW_CAP, list[i], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
                                         curve_off, vert, curve_ref, curve_row, kept_off, kept_ref, kept_row, err,
                                         s_eid + o, s_c + o, s_p + o,
-                                        s_info + o, n_c[w], n_p[w], n_info[w], super, scanF, cntT);
+                                        s_info + o, n_c[w], n_p[w], n_info[w], super);
         if (!ok && (threadIdx.x & 63) == 0) {
             const uint32_t at = atomicAdd(&n_wide, 1u);
             if (at < 64u) wide[at] = list[i];
@@ -728,7 +721,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep_lds(uint64_t n, const u
             if (!sweep_chunk_lds(SW_CAP_BLOCK, wide[j], n, edges, edge_off, carry_off, carry_sorted, rowflags, vert_off,
                                  curve_off, vert, curve_ref, curve_row, kept_off, kept_ref, kept_row, err, s_eid, s_c,
                                  s_p, s_info, n_c[0], n_p[0],
-                                 n_info[0], super, scanF, cntT) &&
+                                 n_info[0], super) &&
                 (threadIdx.x & 63) == 0)
                 atomicOr(&err[0], 1u);
 }
@@ -780,6 +773,60 @@ __device__ __forceinline__ void carry_rank(const uint32_t *__restrict__ carry, u
 // filtered by the rows' strip flags; true (a frame pass whose flags differ
 // from the full pass's, run_if != 0, once per layout: done): the flag-free
 // curve superset the frame filter takes (k_curve_keep / k_curve_compact)
+// per row (one lane each, before the sweep's row loop): the top halves
+// (placed unordered by k_top_carry: packed entries, their edge ids in
+// top_key) sorted by edge id, then the bottom halves (same-lane edges of
+// child r, in parent order) after them.  r06: every load of a row is issued
+// in one round (its offsets came with the sweep's prologue): up to TF_REG
+// tops and parents per row in registers; more go through memory.
+constexpr int TF_REG = 4;
+__device__ __forceinline__ void top_finish_row(uint32_t *__restrict__ vert, uint32_t *__restrict__ top_key,
+                                               const wg_edge *__restrict__ edges, uint32_t tpos, uint32_t nt, uint32_t ea,
+                                               uint32_t eb) {
+    uint32_t tk[TF_REG], tv[TF_REG];
+    wg_edge be[TF_REG];
+#pragma unroll
+    for (int i = 0; i < TF_REG; i++) {
+        tk[i] = ~0u;
+        tv[i] = 0u;
+        if ((uint32_t)i < nt) { tk[i] = top_key[tpos + i]; tv[i] = vert[tpos + i]; }
+        be[i] = wg_edge{1u, 0u, 0u, 1u, 0u};   // (not live)
+        if (ea + (uint32_t)i < eb) be[i] = edges[ea + i];
+    }
+    if (nt <= (uint32_t)TF_REG) {
+        // sorting network over the register pairs (keys distinct; padding ~0 sorts last)
+#define WG_TF_CX(i, j)                                                                   \
+        if (tk[j] < tk[i]) {                                                             \
+            const uint32_t k_ = tk[i], v_ = tv[i];                                       \
+            tk[i] = tk[j]; tv[i] = tv[j]; tk[j] = k_; tv[j] = v_;                        \
+        }
+        WG_TF_CX(0, 1) WG_TF_CX(2, 3) WG_TF_CX(0, 2) WG_TF_CX(1, 3) WG_TF_CX(1, 2)
+#undef WG_TF_CX
+#pragma unroll
+        for (int i = 0; i < TF_REG; i++)
+            if ((uint32_t)i < nt) vert[tpos + i] = tv[i];
+    } else {   // (in-degree past TF_REG: insertion sort of the pairs in memory)
+        uint32_t *v = vert + tpos, *key = top_key + tpos;
+        for (uint32_t i = 1; i < nt; i++) {
+            const uint32_t x = v[i], xk = key[i];
+            uint32_t j = i;
+            while (j > 0 && key[j - 1] > xk) { v[j] = v[j - 1]; key[j] = key[j - 1]; j--; }
+            v[j] = x;
+            key[j] = xk;
+        }
+    }
+    uint32_t o = tpos + nt;
+#pragma unroll
+    for (int i = 0; i < TF_REG; i++) {
+        const wg_edge e = be[i];
+        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane) vert[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
+    }
+    for (uint32_t k = ea + TF_REG; k < eb; k++) {   // (octopus rows)
+        const wg_edge e = edges[k];
+        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane) vert[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
+    }
+}
+
 template <bool SUPER>
 __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0, uint64_t q1, const wg_edge *__restrict__ edges,
         const uint32_t *__restrict__ edge_off, const uint32_t *__restrict__ carry_off,
@@ -789,7 +836,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, Cap cc, uint32_t *ovf,
         const uint32_t *__restrict__ run_if, const uint32_t *__restrict__ done, const uint32_t *__restrict__ scanF,
-        const uint32_t *__restrict__ cntT) {
+        const uint32_t *__restrict__ cntT, uint32_t *__restrict__ top_key) {
     __shared__ uint32_t s_car[SW_WAVES][64 * SW_SLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[SW_WAVES][SW_STAGE];
     const uint32_t lid = threadIdx.x & 63;
@@ -810,6 +857,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
     const uint32_t rf_v = (!SUPER && inr) ? rowflags[rr] : 0u;
     const uint32_t nf_v = (!SUPER && inr) ? scanF[rr + 1] : 0u;   // the row's full verticals (its tops follow them)
     const uint32_t nt_v = (!SUPER && inr) ? cntT[rr] : 0u;        // ... and its top halves (the bottoms follow)
+    const uint32_t ea_v = (!SUPER && inr) ? edge_off[rr] : 0u, eb_v = (!SUPER && inr) ? edge_off[rr + 1] : 0u;
     const Cap gs[3] = {vc, sc, cc};
     const CapVals<3> gv = cap_read(gs, ovf);
     if (SUPER) {
@@ -817,6 +865,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         if ((ri == 0) | (dn != 0)) return;
     }
     if (cap_over(gv, gs, ovf) || q >= q1) return;
+    if (!SUPER && inr) top_finish_row(vert, top_key, edges, voff_v + nf_v, nt_v, ea_v, eb_v);
     const uint32_t ncar = a1 - a;
     const uint32_t total = ncar + (E1 - E0);
     if (total > reg_cap || total > 64u * SW_SLOTS) {   // the LDS sweep (k_sweep_lds) reads the ranked list from HBM
@@ -824,16 +873,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         if (lid == 0) big[atomicAdd(big_n, 1u)] = (uint32_t)q;
         return;
     }
-    // the chunk's own edges (they follow the carry-in in edge order) load
-    // while the carry-in list is ranked
     const uint32_t nslots = (total + 63) / 64;
-    wg_edge eo[SW_SLOTS];
-#pragma unroll
-    for (int sl = 0; sl < SW_SLOTS; sl++) {
-        const uint32_t idx = 64u * sl + lid;
-        eo[sl] = wg_edge{0u, 0u, 0u, 0u, 0u};
-        if ((uint32_t)sl < nslots && idx >= ncar && idx < total) eo[sl] = edges[E0 + (idx - ncar)];
-    }
     uint32_t *sorted = s_car[threadIdx.x >> 6];
     carry_rank(carry + a, ncar, s_stage[threadIdx.x >> 6], sorted);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -842,29 +882,24 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
     // per slot: the edge id, the packed full-vertical entry, two row windows
     // as (first row, length - 1) for an unsigned compare — full verticals on
     // rows c < r < p of same-lane edges, curve segments on rows c <= r <= p of
-    // cross-lane edges; an empty window has first row ~0 — and (full pass) the
-    // chunk rows of a same-lane edge's ends (top half at p, bottom half at c;
-    // 0xFF outside the chunk).  A full pass writes the curve list filtered by
+    // cross-lane edges; an empty window has first row ~0.  A full pass writes the curve list filtered by
     // the row's strip flags (every segment of a row without flags); the
     // flag-free superset is swept only for a frame pass whose flags differ
     // (SUPER).
-    uint32_t ek[SW_SLOTS], fb[SW_SLOTS], fl[SW_SLOTS], cb[SW_SLOTS], cl[SW_SLOTS], pv[SW_SLOTS], tb[SW_SLOTS];
+    uint32_t ek[SW_SLOTS], fb[SW_SLOTS], fl[SW_SLOTS], cb[SW_SLOTS], cl[SW_SLOTS], pv[SW_SLOTS];
 #pragma unroll
     for (int sl = 0; sl < SW_SLOTS; sl++) {
         const uint32_t idx = 64u * sl + lid;
-        ek[sl] = 0; fb[sl] = ~0u; fl[sl] = 0; cb[sl] = ~0u; cl[sl] = 0; pv[sl] = 0; tb[sl] = 0xFFFFu;
+        ek[sl] = 0; fb[sl] = ~0u; fl[sl] = 0; cb[sl] = ~0u; cl[sl] = 0; pv[sl] = 0;
         if ((uint32_t)sl < nslots && idx < total) {
             const uint32_t k = idx < ncar ? sorted[idx] : E0 + (idx - ncar);
-            const wg_edge e = idx < ncar ? edges[k] : eo[sl];
+            const wg_edge e = edges[k];
             ek[sl] = k;
             const uint32_t c = e.child_row, p = e.parent_row;
             if (c < p) {
                 if (e.child_lane == e.parent_lane) {
                     if (c + 1 < p) { fb[sl] = c + 1; fl[sl] = p - c - 2; }
                     pv[sl] = pack_vert(e.child_lane & 0xFFFFFFu, WG_VERT_FULL, e.color & 0xFu);
-                    const uint32_t tp = p - (uint32_t)R0 < nr ? p - (uint32_t)R0 : 0xFFu;
-                    const uint32_t bt = c - (uint32_t)R0 < nr ? c - (uint32_t)R0 : 0xFFu;
-                    tb[sl] = tp << 8 | bt;
                 } else {
                     cb[sl] = c;
                     cl[sl] = p - c;
@@ -878,10 +913,6 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         uint32_t cbase = (uint32_t)__builtin_amdgcn_readlane((int)coff_v, (int)j);
         uint32_t kbase = (uint32_t)__builtin_amdgcn_readlane((int)koff_v, (int)j);
         const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)rf_v, (int)j);
-        // (full pass) the row's top halves after its full verticals, its
-        // bottom halves after the tops; both in edge order = slot order
-        uint32_t tbase = fbase + (uint32_t)__builtin_amdgcn_readlane((int)nf_v, (int)j);
-        uint32_t bbase = tbase + (uint32_t)__builtin_amdgcn_readlane((int)nt_v, (int)j);
 #pragma unroll
         for (int sl = 0; sl < SW_SLOTS; sl++) {
             if ((uint32_t)sl >= nslots) break;
@@ -891,16 +922,6 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
                 if (mf) {
                     if (full) vert[fbase + mbcnt(mf)] = pv[sl];
                     fbase += __builtin_popcountll(mf);
-                }
-                const bool top = (tb[sl] >> 8) == j, bot = (tb[sl] & 0xFFu) == j;
-                const uint64_t mt = __ballot(top), mb = __ballot(bot);
-                if (mt) {
-                    if (top) vert[tbase + mbcnt(mt)] = pv[sl] | (WG_VERT_TOP << 24);
-                    tbase += __builtin_popcountll(mt);
-                }
-                if (mb) {
-                    if (bot) vert[bbase + mbcnt(mb)] = pv[sl] | (WG_VERT_BOTTOM << 24);
-                    bbase += __builtin_popcountll(mb);
                 }
             }
             const bool curv = r - cb[sl] <= cl[sl];
@@ -1258,7 +1279,7 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), big,
                        big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, vc, sc, cc, ovf,
-                       (const uint32_t *)nullptr, (const uint32_t *)nullptr, L.cntF, L.cntT);
+                       (const uint32_t *)nullptr, (const uint32_t *)nullptr, L.cntF, L.cntT, c->top_key.as<uint32_t>());
     // (one wave per wide chunk, ~73 KB of LDS per block: two blocks per CU,
     // the whole chip for lists whose every chunk is wide; sized by the last
     // pass's count of wide chunks; 64 blocks for a list that had none, as
@@ -1271,8 +1292,7 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
                        (const uint32_t *)big_n, E, edge_off, carry_off, (const uint32_t *)carry_sorted,
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), err,
-                       vc, sc, ovf, false, (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)L.cntF,
-                       (const uint32_t *)L.cntT);
+                       vc, sc, ovf, false, (const uint32_t *)nullptr, (const uint32_t *)nullptr);
     // the records of the slice's rows: a grid for its share of the records
     // (+ a quarter), the kernels stride over the rest
     uint64_t grid_recs = L.n_super_grid;
@@ -1301,15 +1321,14 @@ static void launch_superset(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t
                        (uint32_t *)nullptr, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
                        (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, big, big_n,
                        c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, g, g, g, ovf, run_if,
-                       (const uint32_t *)(err + 5), (const uint32_t *)nullptr, (const uint32_t *)nullptr);
+                       (const uint32_t *)(err + 5), (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr);
     const uint64_t lds_grid = std::min<uint64_t>(std::min<uint64_t>(SW_LDS_BLOCKS, 64 + (uint64_t)c->sweep_wide_last / SW_WAVES),
                                                  (nch + SW_WAVES - 1) / SW_WAVES);
     hipLaunchKernelGGL(k_sweep_lds, dim3((uint32_t)lds_grid), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)big,
                        (const uint32_t *)big_n, E, edge_off, carry_off, (const uint32_t *)c->carry_sorted.as<uint32_t>(),
                        c->rowflags.as<const uint8_t>(), (const uint32_t *)nullptr, soff, (uint32_t *)nullptr,
                        c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(), (const uint32_t *)nullptr,
-                       (uint32_t *)nullptr, (uint32_t *)nullptr, err, g, g, ovf, true, run_if, (const uint32_t *)(err + 5),
-                       (const uint32_t *)nullptr, (const uint32_t *)nullptr);
+                       (uint32_t *)nullptr, (uint32_t *)nullptr, err, g, g, ovf, true, run_if, (const uint32_t *)(err + 5));
 }
 
 int wg_geom_lists_flush(wg_ctx *c) {
@@ -1492,6 +1511,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         const uint64_t n_super = tot[1];
         const uint64_t ncarry = tot[2];
         WG_ALLOC(c, c->vert, c->n_vert * 4 + 16);
+        WG_ALLOC(c, c->top_key, c->n_vert * 4 + 16);   // (the top halves' sort keys, at their vertical-list positions)
         WG_ALLOC(c, c->scurve_ref, n_super * 4 + 16);
         WG_ALLOC(c, c->scurve_row, n_super * 4 + 16);
         WG_ALLOC(c, c->curve, n_super * sizeof(wg_curve) + 64);
@@ -1504,7 +1524,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         n_super_grid = n_super;
     } else {
         auto cap_of = [](const DevBuf &b, size_t elem) -> uint64_t { return b.cap / elem; };
-        const uint64_t vcap = cap_of(c->vert, 4);
+        const uint64_t vcap = std::min(cap_of(c->vert, 4), cap_of(c->top_key, 4));
         uint64_t scap = cap_of(c->scurve_ref, 4);
         scap = std::min(scap, cap_of(c->scurve_row, 4));
         scap = std::min(scap, cap_of(c->curve, sizeof(wg_curve)));
@@ -1524,8 +1544,9 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
 
     wg_stage_begin(c, "geom_lists");
     if (ne)
-        hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, (const uint32_t *)carry_off, carry_fill,
-                           c->carry.as<uint32_t>(), ne_dev, vc, cc, ovf);
+        hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, c->vert.as<uint32_t>(),
+                           c->top_key.as<uint32_t>(), (const uint32_t *)carry_off, carry_fill, c->carry.as<uint32_t>(), ne_dev,
+                           vc, cc, ovf);
     WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
     wg_ctx::ListsDef &L = c->glist;
     L = wg_ctx::ListsDef{};
