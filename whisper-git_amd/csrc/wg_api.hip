@@ -446,7 +446,7 @@ void wg_destroy(wg_ctx *c) {
     DevBuf *bufs[] = {&c->in_oid, &c->in_time, &c->in_poff, &c->in_poid, &c->in_flags, &c->hash, &c->canon,
                       &c->prow, &c->lane_asg, &c->lane_out, &c->color_out, &c->lane_scalars, &c->edge_cnt,
                       &c->edges, &c->heights, &c->band, &c->g_height, &c->g_node_y, &c->g_row_top,
-                      &c->rt_chunk, &c->rt_tables, &c->rt_sup, &c->rt_flags, &c->geom_zero, &c->top_key,
+                      &c->rt_chunk, &c->rt_tables, &c->rt_sup, &c->rt_flags, &c->geom_zero,
                       &c->vert_off, &c->curve_off, &c->vert, &c->curve, &c->curve_color,
                       &c->curve_ref, &c->curve_row, &c->carry_off, &c->carry,
                       &c->scan_tmp, &c->scal, &c->rowflags, &c->rowflags_lists, &c->geom_diff, &c->scurve_off,

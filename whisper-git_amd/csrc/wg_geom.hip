@@ -480,18 +480,17 @@ __global__ void __launch_bounds__(GO_T) k_geom_offsets(uint64_t n, uint32_t *F, 
     if ((threadIdx.x & 31) == 0 && sub < nbs) { bsV[sub] = tV; bsC[sub] = tC; bsK[sub] = tK; }
 }
 
-// one pass over the edges: same-lane edges into their parent row's top-half
-// slots — the packed entry in the vertical list, the edge id (the sort key)
-// beside it in top_key (r06: the sweep wave sorts them by key in registers,
-// top_finish_row, with no gather of the edges) — and every edge into the
-// carry-in list of each 64-row chunk it is alive across (ranked by the sweep)
+// one pass over the edges: same-lane edges' ids into their parent row's
+// top-half slots (sorted and packed by the sweep wave, top_finish_row), and every edge into
+// the carry-in list of each 64-row chunk it is alive across (sorted by
+// k_carry_sort)
 // The (edge, chunk) registrations of a wave's 64 edges are dealt to its
 // lanes in turn: an edge alive across thousands of chunks (a long-lived
 // branch of a wide list) no longer loops alone while its wave waits
 // (linuxwide: 344 us with one lane per edge)
 __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *__restrict__ edges,
                             const uint32_t *__restrict__ vert_off,
-                            const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert, uint32_t *top_key,
+                            const uint32_t *__restrict__ scanF, uint32_t *top_fill, uint32_t *vert,
                             const uint32_t *__restrict__ carry_off, uint32_t *carry_fill, uint32_t *carry,
                             const uint32_t *__restrict__ ne_dev, Cap vc, Cap cc, uint32_t *ovf) {
     __shared__ uint32_t s_pre[256 / 64][64], s_k0[256 / 64][64];
@@ -507,13 +506,6 @@ __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *_
     const uint32_t span = (live && k1 >= k0) ? k1 - k0 + 1 : 0u;
     const uint32_t inc = wg_wave_scan(span, 0u, [](uint32_t x, uint32_t y) { return x + y; });
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-    if (live && e.child_lane == e.parent_lane) {
-        const uint32_t p = e.parent_row;
-        const uint32_t at = vert_off[p] + scanF[p + 1] + atomicAdd(&top_fill[p], 1u);
-        vert[at] = pack_vert(e.child_lane, WG_VERT_TOP, e.color);
-        top_key[at] = (uint32_t)k;
-    }
-    if (!tot) return;   // (uniform)
     s_pre[wv][lid] = inc - span;
     s_k0[wv][lid] = k0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -531,6 +523,10 @@ __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *_
         const uint32_t pos = atomicAdd(&carry_fill[q], 1u);
         carry[carry_off[q] + pos] = (uint32_t)(kbase + l);
     }
+    if (!live || e.child_lane != e.parent_lane) return;
+    const uint32_t p = e.parent_row;
+    const uint32_t pos = atomicAdd(&top_fill[p], 1u);
+    vert[vert_off[p] + scanF[p + 1] + pos] = (uint32_t)k;   // edge id, packed below
 }
 
 // ---- carry-in registration for the sweep -------------------------------------
@@ -773,57 +769,59 @@ __device__ __forceinline__ void carry_rank(const uint32_t *__restrict__ carry, u
 // filtered by the rows' strip flags; true (a frame pass whose flags differ
 // from the full pass's, run_if != 0, once per layout: done): the flag-free
 // curve superset the frame filter takes (k_curve_keep / k_curve_compact)
-// per row (one lane each, before the sweep's row loop): the top halves
-// (placed unordered by k_top_carry: packed entries, their edge ids in
-// top_key) sorted by edge id, then the bottom halves (same-lane edges of
-// child r, in parent order) after them.  r06: every load of a row is issued
-// in one round (its offsets came with the sweep's prologue): up to TF_REG
-// tops and parents per row in registers; more go through memory.
+// per row (one lane each, before the sweep's row loop): the top-half entries
+// (edge ids placed by k_top_carry) sorted by edge id and packed, then the
+// bottom halves (same-lane edges of child r, in parent order) after them.
+// r06: the row's offsets come with the sweep's prologue; its ids (up to
+// TF_REG in registers; more are sorted in memory) and its own edges load in
+// one round, the top edges' gather in the next.
 constexpr int TF_REG = 4;
-__device__ __forceinline__ void top_finish_row(uint32_t *__restrict__ vert, uint32_t *__restrict__ top_key,
-                                               const wg_edge *__restrict__ edges, uint32_t tpos, uint32_t nt, uint32_t ea,
-                                               uint32_t eb) {
-    uint32_t tk[TF_REG], tv[TF_REG];
+__device__ __forceinline__ void top_finish_row(uint32_t *__restrict__ vert, const wg_edge *__restrict__ edges, uint32_t tpos,
+                                               uint32_t nt, uint32_t ea, uint32_t eb) {
+    uint32_t tk[TF_REG];
     wg_edge be[TF_REG];
 #pragma unroll
     for (int i = 0; i < TF_REG; i++) {
         tk[i] = ~0u;
-        tv[i] = 0u;
-        if ((uint32_t)i < nt) { tk[i] = top_key[tpos + i]; tv[i] = vert[tpos + i]; }
+        if ((uint32_t)i < nt) tk[i] = vert[tpos + i];
         be[i] = wg_edge{1u, 0u, 0u, 1u, 0u};   // (not live)
         if (ea + (uint32_t)i < eb) be[i] = edges[ea + i];
     }
+    uint32_t *v = vert + tpos;
     if (nt <= (uint32_t)TF_REG) {
-        // sorting network over the register pairs (keys distinct; padding ~0 sorts last)
-#define WG_TF_CX(i, j)                                                                   \
-        if (tk[j] < tk[i]) {                                                             \
-            const uint32_t k_ = tk[i], v_ = tv[i];                                       \
-            tk[i] = tk[j]; tv[i] = tv[j]; tk[j] = k_; tv[j] = v_;                        \
-        }
+        // sorting network (ids distinct; the padding ~0 sorts last)
+#define WG_TF_CX(i, j)                                                  \
+        if (tk[j] < tk[i]) { const uint32_t t_ = tk[i]; tk[i] = tk[j]; tk[j] = t_; }
         WG_TF_CX(0, 1) WG_TF_CX(2, 3) WG_TF_CX(0, 2) WG_TF_CX(1, 3) WG_TF_CX(1, 2)
 #undef WG_TF_CX
+        wg_edge te[TF_REG];
 #pragma unroll
         for (int i = 0; i < TF_REG; i++)
-            if ((uint32_t)i < nt) vert[tpos + i] = tv[i];
-    } else {   // (in-degree past TF_REG: insertion sort of the pairs in memory)
-        uint32_t *v = vert + tpos, *key = top_key + tpos;
+            if ((uint32_t)i < nt) te[i] = edges[tk[i]];
+#pragma unroll
+        for (int i = 0; i < TF_REG; i++)
+            if ((uint32_t)i < nt) v[i] = pack_vert(te[i].child_lane, WG_VERT_TOP, te[i].color);
+    } else {   // (in-degree past TF_REG: insertion sort by edge id in memory)
         for (uint32_t i = 1; i < nt; i++) {
-            const uint32_t x = v[i], xk = key[i];
+            const uint32_t x = v[i];
             uint32_t j = i;
-            while (j > 0 && key[j - 1] > xk) { v[j] = v[j - 1]; key[j] = key[j - 1]; j--; }
+            while (j > 0 && v[j - 1] > x) { v[j] = v[j - 1]; j--; }
             v[j] = x;
-            key[j] = xk;
+        }
+        for (uint32_t i = 0; i < nt; i++) {
+            const wg_edge e = edges[v[i]];
+            v[i] = pack_vert(e.child_lane, WG_VERT_TOP, e.color);
         }
     }
-    uint32_t o = tpos + nt;
+    uint32_t o = nt;
 #pragma unroll
     for (int i = 0; i < TF_REG; i++) {
         const wg_edge e = be[i];
-        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane) vert[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
+        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane) v[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
     }
-    for (uint32_t k = ea + TF_REG; k < eb; k++) {   // (octopus rows)
+    for (uint32_t k = ea + TF_REG; k < eb; k++) {   // (rows with more parents)
         const wg_edge e = edges[k];
-        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane) vert[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
+        if (e.child_row < e.parent_row && e.child_lane == e.parent_lane) v[o++] = pack_vert(e.child_lane, WG_VERT_BOTTOM, e.color);
     }
 }
 
@@ -836,7 +834,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, Cap cc, uint32_t *ovf,
         const uint32_t *__restrict__ run_if, const uint32_t *__restrict__ done, const uint32_t *__restrict__ scanF,
-        const uint32_t *__restrict__ cntT, uint32_t *__restrict__ top_key) {
+        const uint32_t *__restrict__ cntT) {
     __shared__ uint32_t s_car[SW_WAVES][64 * SW_SLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[SW_WAVES][SW_STAGE];
     const uint32_t lid = threadIdx.x & 63;
@@ -865,7 +863,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         if ((ri == 0) | (dn != 0)) return;
     }
     if (cap_over(gv, gs, ovf) || q >= q1) return;
-    if (!SUPER && inr) top_finish_row(vert, top_key, edges, voff_v + nf_v, nt_v, ea_v, eb_v);
+    if (!SUPER && inr) top_finish_row(vert, edges, voff_v + nf_v, nt_v, ea_v, eb_v);
     const uint32_t ncar = a1 - a;
     const uint32_t total = ncar + (E1 - E0);
     if (total > reg_cap || total > 64u * SW_SLOTS) {   // the LDS sweep (k_sweep_lds) reads the ranked list from HBM
@@ -1279,7 +1277,7 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), big,
                        big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, vc, sc, cc, ovf,
-                       (const uint32_t *)nullptr, (const uint32_t *)nullptr, L.cntF, L.cntT, c->top_key.as<uint32_t>());
+                       (const uint32_t *)nullptr, (const uint32_t *)nullptr, L.cntF, L.cntT);
     // (one wave per wide chunk, ~73 KB of LDS per block: two blocks per CU,
     // the whole chip for lists whose every chunk is wide; sized by the last
     // pass's count of wide chunks; 64 blocks for a list that had none, as
@@ -1321,7 +1319,7 @@ static void launch_superset(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t
                        (uint32_t *)nullptr, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
                        (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, big, big_n,
                        c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, g, g, g, ovf, run_if,
-                       (const uint32_t *)(err + 5), (const uint32_t *)nullptr, (const uint32_t *)nullptr, (uint32_t *)nullptr);
+                       (const uint32_t *)(err + 5), (const uint32_t *)nullptr, (const uint32_t *)nullptr);
     const uint64_t lds_grid = std::min<uint64_t>(std::min<uint64_t>(SW_LDS_BLOCKS, 64 + (uint64_t)c->sweep_wide_last / SW_WAVES),
                                                  (nch + SW_WAVES - 1) / SW_WAVES);
     hipLaunchKernelGGL(k_sweep_lds, dim3((uint32_t)lds_grid), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)big,
@@ -1511,7 +1509,6 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         const uint64_t n_super = tot[1];
         const uint64_t ncarry = tot[2];
         WG_ALLOC(c, c->vert, c->n_vert * 4 + 16);
-        WG_ALLOC(c, c->top_key, c->n_vert * 4 + 16);   // (the top halves' sort keys, at their vertical-list positions)
         WG_ALLOC(c, c->scurve_ref, n_super * 4 + 16);
         WG_ALLOC(c, c->scurve_row, n_super * 4 + 16);
         WG_ALLOC(c, c->curve, n_super * sizeof(wg_curve) + 64);
@@ -1524,7 +1521,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         n_super_grid = n_super;
     } else {
         auto cap_of = [](const DevBuf &b, size_t elem) -> uint64_t { return b.cap / elem; };
-        const uint64_t vcap = std::min(cap_of(c->vert, 4), cap_of(c->top_key, 4));
+        const uint64_t vcap = cap_of(c->vert, 4);
         uint64_t scap = cap_of(c->scurve_ref, 4);
         scap = std::min(scap, cap_of(c->scurve_row, 4));
         scap = std::min(scap, cap_of(c->curve, sizeof(wg_curve)));
@@ -1545,8 +1542,7 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
     wg_stage_begin(c, "geom_lists");
     if (ne)
         hipLaunchKernelGGL(k_top_carry, dim3(blocks(ne)), dim3(T), 0, s, ne, E, voff, cntF, top_fill, c->vert.as<uint32_t>(),
-                           c->top_key.as<uint32_t>(), (const uint32_t *)carry_off, carry_fill, c->carry.as<uint32_t>(), ne_dev,
-                           vc, cc, ovf);
+                           (const uint32_t *)carry_off, carry_fill, c->carry.as<uint32_t>(), ne_dev, vc, cc, ovf);
     WG_ALLOC(c, c->sweep_big, nch * 4 + 16);
     wg_ctx::ListsDef &L = c->glist;
     L = wg_ctx::ListsDef{};

@@ -471,6 +471,9 @@ struct wg_ctx {
         }
         dc_blind = fp >= dc_blind ? fp : (dc_blind + fp) / 2;
         if (dc_blind < 2) dc_blind = 2;
+        // a probe's shorter warm-up may need more iterations: blind ones, so
+        // the speculative build that tries it is not redone exactly for that
+        if (dc_probe_down) dc_blind += 2;
     }
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
@@ -545,7 +548,6 @@ struct wg_ctx {
     DevBuf rt_tables;       // per-chunk transducer tables
     DevBuf rt_sup;          // super-chunk tables, binade bases and walk states
     DevBuf rt_flags;        // uint32 [4]
-    DevBuf top_key;         // per vertical-list position of a top half: its edge id (sort key), k_top_carry -> k_sweep
     DevBuf geom_zero;       // zeroed per pass: per-row counts / diff arrays, top fill, carry counts, sweep flags
     uint64_t geom_zero_n = ~0ull;   // rows the workspace was zeroed for ahead of the pass (wg_geom_prezero), or ~0
     DevBuf vert_off, curve_off;             // uint32 [N+1]
