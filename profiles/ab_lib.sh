@@ -2,7 +2,7 @@
 # A/B of two engine builds in one call, alternating (run from the repo root):
 #   profiles/ab_lib.sh <tag> <lib_a> <lib_b> [pairs]
 # per pair and library: the default bench step (wide16 1M), C4 (Linux-shaped
-# 1.3M) and C3 (random13 100k), 30 timed steps each, no CPU legs; then a
+# 1.3M) and C3 (random13 100k) [and skew 1M with AB_SKEW=1], 30 timed steps each, no CPU legs; then a
 # kernel trace of the default step with lib_b -> gpurun_out/<tag>_*
 set -e -o pipefail
 TAG=${1:?tag}; A=${2:?lib a}; B=${3:?lib b}; PAIRS=${4:-3}
@@ -19,6 +19,10 @@ for i in $(seq 1 "$PAIRS"); do
             --rows-per-gpu 1300000 > "$OUT/${TAG}_${v}${i}_c4.json" 2> "$OUT/${TAG}_${v}${i}_c4.err"
         WGRAPH_LIB=$L timeout -k 10 120 python -u bench.py --no-cpu --no-extras --steps 30 --kind random13 \
             --rows-per-gpu 100000 > "$OUT/${TAG}_${v}${i}_c3.json" 2> "$OUT/${TAG}_${v}${i}_c3.err"
+        if [ -n "$AB_SKEW" ]; then
+            WGRAPH_LIB=$L timeout -k 10 120 python -u bench.py --no-cpu --no-extras --steps 30 --warmup 6 --kind skew \
+                > "$OUT/${TAG}_${v}${i}_skew.json" 2> "$OUT/${TAG}_${v}${i}_skew.err"
+        fi
     done
 done
 cd /tmp && export TMPDIR=/tmp

@@ -471,9 +471,14 @@ struct wg_ctx {
         }
         dc_blind = fp >= dc_blind ? fp : (dc_blind + fp) / 2;
         if (dc_blind < 2) dc_blind = 2;
-        // a probe's shorter warm-up may need more iterations: blind ones, so
-        // the speculative build that tries it is not redone exactly for that
-        if (dc_probe_down) dc_blind += 2;
+        // A changed warm-up may need more iterations than this one took: the
+        // next speculative build launches generously many blind (an iteration
+        // after the fixed point exits at once, k_dc_iter), so trying it never
+        // costs an exact redo; the count adapts back down afterwards
+        if (dc_warm != warm) {
+            const uint32_t b = dc_warm < warm ? 4 * fp + 4 : 2 * fp + 2;
+            if (dc_blind < b) dc_blind = b;
+        }
     }
     uint32_t replay_iters = 0;     // iterations the last replay needed
     uint32_t replay_blind = 4;     // iterations launched before the first convergence check (adapts)
