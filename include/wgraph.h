@@ -268,6 +268,9 @@ int         wg_synchronize(wg_ctx *ctx);
  * the kernel that computes the total; 0 = a separate read kernel.  Speed
  * only. */
 #define WG_OPT_FUSED_READ 13
+/* WG_OPT_MATCH_THREADS: threads per 256-row workgroup of the search-match
+ * kernel (wg_match_rows): 512 (default, 0) or 256.  Speed only. */
+#define WG_OPT_MATCH_THREADS 14
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------

@@ -28,7 +28,11 @@ def main():
     dt_ = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (sb, so_.view(np.int64), ab, ao.view(np.int64))]
     devp = ((dt_[0].data_ptr(), dt_[1].data_ptr()), (dt_[2].data_ptr(), dt_[3].data_ptr()))
     alg = int(so_[n] - so_[0]) + int(ao[n] - ao[0]) + n * (16 + 20 + 1 + 1)
-    for query in ("Fix", "refactor parser", "σοφ", "İ"):
+    variants = [int(v) for v in os.environ.get("MATCH_THREADS", "0").split(",")]
+    for rep in range(int(os.environ.get("MATCH_REPS", "1"))):
+      for threads in variants:
+       eng.set_match_threads(threads)
+       for query in ("Fix", "refactor parser", "σοφ", "İ"):
         eng.match_rows(query, 0, n, device=devp)
         torch.cuda.synchronize()
         eng.enable_timing(True, reserve=64)
@@ -41,7 +45,7 @@ def main():
         want, _ = search_oracle.match_rows(dag, query.encode(), (sb, so_), (ab, ao), 0, m)
         ok = bool(np.array_equal(np.asarray(flags[:m], np.uint8), np.asarray(want, np.uint8)))
         k = float(np.mean(ms))
-        print(json.dumps({"query": query, "rows": n, "matches": int(nm), "kernel_ms": round(k, 4),
+        print(json.dumps({"threads": threads, "rep": rep, "query": query, "rows": n, "matches": int(nm), "kernel_ms": round(k, 4),
                           "GBps": round(alg / (k * 1e-3) / 1e9, 1), "first_20k_equal_oracle": ok}), flush=True)
     eng.close()
 

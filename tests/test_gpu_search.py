@@ -31,8 +31,16 @@ def _queries(d):
             "x" * 3000, "remove " * 400]
 
 
+@pytest.fixture(params=[512, 256], ids=["nt512", "nt256"])
+def threads(engine, request):
+    """The kernel's workgroup at 512 threads (default) and at 256: the same flags."""
+    engine.set_match_threads(request.param)
+    yield request.param
+    engine.set_match_threads(0)
+
+
 @pytest.mark.parametrize("residency", ["host", "device"])
-def test_match_flags_equal_oracle(engine, data, residency):
+def test_match_flags_equal_oracle(engine, data, residency, threads):
     import torch
     d, summ, auth = data
     engine.build(d)
@@ -79,7 +87,7 @@ def test_match_without_text_fields_and_wide_rows(engine):
         engine.match_rows("")
 
 
-def test_match_fuzz_bytes_unaligned(engine):
+def test_match_fuzz_bytes_unaligned(engine, threads):
     """Rows of random bytes from an alphabet of ASCII letters, lead and
     continuation bytes of two- to four-byte sequences (valid, truncated,
     overlong, stray), U+03A3 / U+0130 / U+1E9E / U+212A pieces, with the
@@ -121,7 +129,7 @@ def test_match_fuzz_bytes_unaligned(engine):
         engine.match_rows("")
 
 
-def test_match_dense_non_ascii_fields(engine):
+def test_match_dense_non_ascii_fields(engine, threads):
     """Fields with more non-ASCII code points per 256 rows than the kernel's
     lists hold (Cyrillic, Greek with final sigmas) and rows mixing them with
     length-changing code points: every path gives the oracle's flags."""
@@ -150,7 +158,7 @@ def test_match_dense_non_ascii_fields(engine):
 
 
 @pytest.mark.parametrize("sum_len,auth_len", [(60, 20), (60, 40), (80, 6), (0, 70)])
-def test_match_fields_together_or_apart(engine, sum_len, auth_len):
+def test_match_fields_together_or_apart(engine, sum_len, auth_len, threads):
     """The kernel stages a workgroup's two fields into one LDS image when they
     fit together and in two passes when they do not (about 60 + 40 bytes per
     row is past the image, 60 + 20 is within it, 80 + 6 sits at the edge, an
@@ -224,7 +232,7 @@ def test_search_dimming_of_vertices_and_glyphs(engine, data):
 
 
 @pytest.mark.parametrize("dense", ["summary", "author"])
-def test_match_two_passes_with_an_overflowing_pass(engine, dense):
+def test_match_two_passes_with_an_overflowing_pass(engine, dense, threads):
     """a workgroup whose two fields do not fit one LDS image runs
     two passes; here one of them lists more non-ASCII leads than the kernel
     holds (LCAP 2560 per 256 rows: that pass takes the stream from HBM and

@@ -323,6 +323,7 @@ struct wg_ctx {
     // WG_OPT_JOIN_FUSED: the table's place pass in the window probe, settle on the main stream (r05 A/B on
     // wide16 1M: 1.438 / 1.444 ms/step against 1.434 / 1.434 with the table beside the probe: off)
     bool join_fused = false;
+    uint32_t match_threads = 512;   // WG_OPT_MATCH_THREADS
     bool hash_built = false, hash_on_side = false;   // ... launched already (on the side stream)
     DevBuf prow;            // int32  [E]  canonical parent row or -1
     // lanes

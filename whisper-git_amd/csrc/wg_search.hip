@@ -225,7 +225,13 @@ __device__ bool walk_row(const WgCaseTables &T, const uint32_t *buf, uint32_t rs
     return false;
 }
 
-__global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
+// NT threads per workgroup (256 or 512) over its MT rows; SB words per thread
+// per staging batch.  r06: 512 threads give every LDS-bound phase (lowering,
+// Final_Sigma, the first-byte windows, the walks' list) twice the lanes, and
+// a CU twice the waves to hide each phase's round trips with (the workgroup's
+// LDS is unchanged, so the same workgroups fit per CU)
+template <int NT, int SB, int WPS>
+__global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
     __shared__ uint32_t s_buf[MCAPW + 4];
     __shared__ uint32_t s_rel[2][MT + 1];     // per region of the staged image: its rows' byte offsets in it
     __shared__ uint16_t s_lead[LCAP];         // LDS positions of the staged lead bytes (>= 0xC0): others at [0, n), 0xCE
@@ -248,7 +254,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     const uint32_t q0 = (uint32_t)(qv & 0xFFu);
     const FeedShift sh{0, 0, A.qlo, A.qhi, A.mlo, A.mhi, 0, m};
     const WalkFeed wf{sh, WgKmp{A.q, A.fail, m, 0}, m > 16};
-    s_rf[tid] = 0;
+    if (tid < MT) s_rf[tid] = 0;
     if (tid < 8) s_cnt[tid] = 0;
     // both fields' row offsets and ranges up front (one round trip)
     uint64_t orow[2] = {0, 0}, gsf[2] = {0, 0}, gef[2] = {0, 0};
@@ -278,7 +284,6 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
     }
     const bool both = fst[0] && fst[1] && ((fspan[0] + 3) >> 2) + 1 + ((fspan[1] + 3) >> 2) <= MCAPW;
     const int npass = both ? 1 : (int)fst[0] + (int)fst[1];
-    constexpr int SB = 8;   // words per thread per staging batch
     for (int pass = 0; pass < npass; pass++) {
         // the pass's regions (uniform): field, text, bias, image span, first word
         const uint32_t ng = both ? 2u : 1u;
@@ -312,11 +317,11 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         // listed (wave-aggregated: one LDS atomic per wave and batch)
         {
             uint32_t raw_ff = 0;
-            for (uint32_t k0 = tid - lane; k0 < tw; k0 += SB * MT) {   // wave-uniform trip count
+            for (uint32_t k0 = tid - lane; k0 < tw; k0 += SB * NT) {   // wave-uniform trip count
                 uint32_t v[SB], cnt = 0;
 #pragma unroll
                 for (int u = 0; u < SB; u++) {
-                    const uint32_t k = k0 + lane + u * MT;
+                    const uint32_t k = k0 + lane + u * NT;
                     const uint32_t g = (ng == 2 && k >= baseg[1]) ? 1u : 0u;
                     const uint32_t kk = k - baseg[g];
                     v[u] = 0;
@@ -324,7 +329,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                 }
 #pragma unroll
                 for (int u = 0; u < SB; u++) {
-                    const uint32_t k = k0 + lane + u * MT;
+                    const uint32_t k = k0 + lane + u * NT;
                     const uint32_t w = v[u];
                     if (k < tw) s_buf[k] = ascii_lower4(w);
                     const uint32_t lead = w & (w << 1) & 0x80808080u;   // bytes >= 0xC0
@@ -344,7 +349,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
                     uint32_t il = (base & 0xFFFFu) + ((incl - cnt) & 0xFFFFu), ic = (base >> 16) + ((incl - cnt) >> 16);
 #pragma unroll
                     for (int u = 0; u < SB; u++) {
-                        const uint32_t w = v[u], k = k0 + lane + u * MT;
+                        const uint32_t w = v[u], k = k0 + lane + u * NT;
                         const uint32_t lead = w & (w << 1) & 0x80808080u, ce = eq_bytes(w, 0xCEu);
                         if (!lead) continue;
                         for (uint32_t j = 0; j < 4; j++) {
@@ -378,7 +383,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         for (uint32_t g = 0; g < ng; g++)
             if (tid < nr && s_rel[g][tid] < s_rel[g][tid + 1] && (sb[s_rel[g][tid]] & 0xC0u) == 0x80u) atomicOr(&pc[2], 1u);
         // Final_Sigma of the U+03A3s, over the original non-ASCII bytes (nothing non-ASCII written yet)
-        for (uint32_t i = tid; i < nce; i += MT) {
+        for (uint32_t i = tid; i < nce; i += NT) {
             const uint32_t p = s_ce[-1 - (int)i];
             const uint32_t *rel = s_rel[reg(p)];
             const uint32_t r = row_of(rel, nr, p), rs = rel[r], n = rel[r + 1] - rs;
@@ -396,7 +401,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         // as it was and its row walked by decoding, fast hits void.
         const uint32_t fl = pc[2];
         const bool exact = (fl & 1u) != 0, marks = A.marks && !(fl & 2u);
-        for (uint32_t i = tid; i < nlead + nce; i += MT) {
+        for (uint32_t i = tid; i < nlead + nce; i += NT) {
             const uint32_t e = i < nlead ? s_lead[i] : s_ce[-1 - (int)(i - nlead)];
             const uint32_t p = e & 0x7FFFu, g = reg(p);
             const uint32_t *rel = s_rel[g];
@@ -447,7 +452,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
             if (tid < nr && (s_rf[tid] & (rf_mark(fg[g]) | rf_decode(fg[g]))))
                 s_wrow[atomicAdd(&pc[1], 1u)] = (uint16_t)(tid | g << 8);
         // every byte position holding the query's first byte against its first 8 bytes
-        for (uint32_t k = tid + (lo[0] >> 2); k < tw; k += MT) {
+        for (uint32_t k = tid + (lo[0] >> 2); k < tw; k += NT) {
             const uint32_t w0 = s_buf[k];
             uint32_t cand = eq_bytes(w0, q0);
             if (!cand) continue;
@@ -473,7 +478,7 @@ __global__ __launch_bounds__(MT) void k_match(MatchArgs A) {
         // 3 (m - 1) bytes before it to as many after (each 3 bytes of the buffer
         // hold at least one lowered byte), entered at a byte outside a mark
         const uint32_t nwalk = pc[1], nsp = pc[3] < SPCAP ? pc[3] : SPCAP;
-        for (uint32_t i = tid; i < nwalk + nsp; i += MT) {
+        for (uint32_t i = tid; i < nwalk + nsp; i += NT) {
             uint32_t row, a, b;
             bool dec = false;
             if (i >= nwalk) {
@@ -697,7 +702,13 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     A.out = c->match_flags.as<uint8_t>();
     A.count = c->match_q.as<unsigned long long>();
     wg_stage_begin(c, "match");
-    if (rows) hipLaunchKernelGGL(k_match, dim3(mblocks(rows)), dim3(MT), 0, s, A);
+    if (rows) {
+        // (WPS: waves per SIMD the registers must allow — 8: four 512-thread
+        // workgroups per CU, as many as their LDS allows)
+        if (c->match_threads == 512) hipLaunchKernelGGL((k_match<512, 4, 8>), dim3(mblocks(rows)), dim3(512), 0, s, A);
+        else if (c->match_threads == 513) hipLaunchKernelGGL((k_match<512, 4, 6>), dim3(mblocks(rows)), dim3(512), 0, s, A);
+        else hipLaunchKernelGGL((k_match<256, 8, 1>), dim3(mblocks(rows)), dim3(256), 0, s, A);
+    }
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
     uint64_t cnt = 0;

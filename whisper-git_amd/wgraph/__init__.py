@@ -212,6 +212,11 @@ class Engine:
         """WG_OPT_VTX_TILE: vertices per emission tile (1024, 2048; 0 = auto)."""
         self._check(lib().wg_set_option(self._ctx, 12, int(verts)))
 
+    def set_match_threads(self, threads: int):
+        """WG_OPT_MATCH_THREADS: threads per 256-row workgroup of the search
+        kernel: 512 (default, 0) or 256.  Speed only."""
+        self._check(lib().wg_set_option(self._ctx, 14, int(threads)))
+
     def set_fused_read(self, on: bool):
         """WG_OPT_FUSED_READ: the emission's host read written by the kernel
         that computes the vertex total (default) or by a read kernel."""
