@@ -12,8 +12,9 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/pmc_step_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-RX=${PMC_KERNELS:-"k_probe_near|k_probe_fix|k_hash_place|k_hash_settle|k_lf_rows|k_lf_jump_tile|k_lf_replay|k_rt_walk|k_edges_rows|k_edge_counts|k_geom_offsets|k_top_carry|k_top_finish|k_sweep|k_curves_tb|k_curves|k_vtx_prep"}
-BENCH="$ROOT/bench.py --steps 3 --warmup 1 --no-cpu --no-extras"
+RX=${PMC_KERNELS:-"k_probe_near|k_probe_fix|k_hash_place|k_hash_settle|k_lf_rows|k_lf_jump_tile|k_lf_replay|k_dc_iter|k_rt_walk|k_edges_rows|k_edge_counts|k_geom_offsets|k_top_carry|k_top_finish|k_sweep|k_curves_tb|k_curves|k_vtx_prep|k_vtx_tile"}
+# (PMC_BENCH_ARGS: another config, e.g. "--kind linux --rows-per-gpu 1300000" for C4)
+BENCH="$ROOT/bench.py --steps 3 --warmup ${PMC_WARMUP:-1} --no-cpu --no-extras ${PMC_BENCH_ARGS:-}"
 timeout -s KILL 120 rocprofv3 --kernel-include-regex "$RX" --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH > "$OUT/fetch.json" 2> "$OUT/fetch.err"
 timeout -s KILL 120 rocprofv3 --kernel-include-regex "$RX" --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $BENCH > "$OUT/write.json" 2> "$OUT/write.err"
 timeout -s KILL 120 rocprofv3 --kernel-include-regex "$RX" --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/tcc" -o run -- python3 $BENCH > "$OUT/tcc.json" 2> "$OUT/tcc.err"
