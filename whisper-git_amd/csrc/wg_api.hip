@@ -33,7 +33,7 @@ static bool wg_system_events() {
     static const bool sys = [] { const char *v = std::getenv("WG_EVENT_SCOPE"); return v && !std::strcmp(v, "system"); }();
     return sys;
 }
-static unsigned wg_event_scope() { return wg_system_events() ? 0u : hipEventReleaseToDevice; }
+unsigned wg_event_scope() { return wg_system_events() ? 0u : hipEventReleaseToDevice; }
 static hipError_t wg_timing_event(hipEvent_t *e) {
     return hipEventCreateWithFlags(e, wg_system_events() ? hipEventDefault : hipEventReleaseToDevice);
 }

@@ -906,6 +906,7 @@ int wg_heights_run(wg_ctx *c, uint64_t m, uint64_t n, float *out,
 int wg_side_fork(wg_ctx *c);
 void wg_side_done(wg_ctx *c);
 int wg_side_join(wg_ctx *c);
+unsigned wg_event_scope();   // wg_api.hip: the release scope of the engine's stream-order events
 // heights of rows [0, m) of the list + zero-band row_top into (h, rt), on the side stream
 int wg_side_zero_rowtop(wg_ctx *c, uint64_t m, float *h, float *rt, uint64_t row_lo,
                         const float *band = nullptr,   // banded row_top (build_frame)
