@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--replay", default=None, help="CHUNK:WARM: fixed replay chunk / warm-up (options 2 and 6)")
     ap.add_argument("--no-spec-replay", action="store_true", help="WG_OPT_SHARD_SPEC_REPLAY 0: X3 checks its replay")
     ap.add_argument("--replay-mode", type=int, default=None, help="WG_OPT_REPLAY_MODE (0 auto, 1 chunked, 2 serial)")
+    ap.add_argument("--no-isolated", action="store_true", help="skip the isolated per-rank replay")
     ap.add_argument("--two-calls", action="store_true",
                     help="shard_build + shard_geometry (two geometry passes) instead of shard_build_frame (3 exchanges either way)")
     args = ap.parse_args()
@@ -69,6 +70,8 @@ def main():
 
     gpu = threading.Lock()
     bar = threading.Barrier(W)
+    captured = [[] for _ in range(W)]     # per rank: the last step's gathered exchanges (isolated replay)
+    capture_on = [False]
     slots: list = [None] * W
     seg = [[] for _ in range(W)]          # per rank: (label, seconds)
     xlog = []                             # per exchange: (step, bytes per rank)
@@ -145,6 +148,8 @@ def main():
                     self.heads = np.ascontiguousarray(out.view(W, stride)[:, 16:32].cpu().numpy()).view(np.uint32)
                 self.stream.synchronize()
             sizes = [s[1] for s in slots]
+            if capture_on[0]:
+                captured[self.rank].append((out.clone(), stride, list(sizes), self.heads.copy()))
             bar.wait()
             self.start(self.label)
             return out, ShardComm.HDR, stride, sizes
@@ -179,6 +184,11 @@ def main():
             comm = EmuComm(r, eng, streams[r])
             s0, s1 = r * R, min(dag.n, (r + 1) * R)
             for it in range(args.steps + 1):
+                if it == args.steps:
+                    captured[r].clear()
+                    if r == 0:
+                        capture_on[0] = True
+                    bar.wait()
                 if it == 1:
                     # per-stage events only with --stage-events: each costs a few us of
                     # GPU time, which would inflate the segments against the
@@ -221,6 +231,54 @@ def main():
         t.join()
     if errors:
         raise SystemExit(f"emulated rank failed: {errors}")
+
+    capture_on[0] = False
+
+    # Isolated replay (r06): each rank's whole step alone on the GPU — its main
+    # and side streams overlapping each other as on a GPU of its own, no other
+    # rank's work beside it — with every exchange answered from the buffers
+    # the lockstep run gathered for the same step (the exchanges themselves
+    # cost nothing here; the collectives' time is not measured).  The lockstep
+    # segments above run one rank at a time, so a rank's side-stream work
+    # lands under the next rank's segments instead of its own.
+    class IsoComm:
+        def __init__(self, rank, stream):
+            self.rank, self.stream, self.k = rank, stream, 0
+            self.on_device, self.device, self.world = True, dev, W
+            self.heads = None
+            self.held = False
+
+        def allgather(self, nbytes, fill, step=0, pack=None, read_heads=None):
+            out, stride, sizes, heads = captured[self.rank][self.k]
+            with torch.cuda.stream(self.stream):
+                if pack is not None:   # (the rank packs its message as it would; the answer is the recorded one)
+                    cap = stride - ShardComm.HDR
+                    slot = torch.empty(cap + ShardComm.HDR, dtype=torch.uint8, device=dev)
+                    pack(slot.data_ptr(), cap)
+                elif nbytes:
+                    send = torch.zeros(ShardComm.round_cap(nbytes), dtype=torch.uint8, device=dev)
+                    fill(send.data_ptr())
+            self.k += 1
+            self.heads = heads
+            return out, ShardComm.HDR, stride, sizes
+
+    iso_ms = []
+    if not args.no_isolated and all(captured[r] for r in range(W)):
+        for r in range(W):
+            eng, st = engines[r], streams[r]
+            s0, s1 = r * R, min(dag.n, (r + 1) * R)
+            ts = []
+            with torch.cuda.stream(st):
+                for it in range(args.steps + 1):
+                    comm = IsoComm(r, st)
+                    eng.synchronize()
+                    t0 = time.perf_counter()
+                    eng.shard_build_frame(commits, W, r, s0, s1, comm, device_ptr=band_ptr)
+                    eng.emit_vertices(s0, s1, selected=s0 + 7, palette=pal)
+                    eng.synchronize()
+                    if it:
+                        ts.append(time.perf_counter() - t0)
+            iso_ms.append(round(1e3 * float(np.median(ts)), 4))
 
     counters = [int(e.debug_counters()[5]) for e in engines]
     dcs = [e.debug_counters() for e in engines]   # [1] lane slots of the global replay, [10] serial replay
@@ -312,7 +370,14 @@ def main():
            "rank0_reemit_vtx_emit_ms": reemit_ms,
            "max_rank_ms_without_collectives": round(worst, 4),
            "exchanges_per_step": n_x, "exchange_bytes_per_rank": xbytes,
-           "efficiency_without_collectives": round(single_ms / worst, 4), "ranks": per_rank}
+           "efficiency_without_collectives": round(single_ms / worst, 4),
+           "isolated_rank_ms": iso_ms,
+           "max_rank_isolated_ms": max(iso_ms) if iso_ms else None,
+           "efficiency_isolated": round(single_ms / max(iso_ms), 4) if iso_ms else None,
+           "isolated_note": ("each rank's whole step replayed alone on the GPU (main and side streams overlapping "
+                             "as on its own GPU) with the exchanges answered from the gathered buffers the lockstep "
+                             "run recorded; collective time not included"),
+           "ranks": per_rank}
     print(json.dumps(res, indent=1))
     if args.out:
         with open(args.out, "w") as f:

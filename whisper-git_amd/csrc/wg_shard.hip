@@ -1022,6 +1022,10 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
     c->n_list = N;
     WG_ALLOC(c, S.h_g, N * 4 + 4);
     WG_ALLOC(c, S.rt_g, (N + 1) * 4);
+    int rc = wg_side_zero_rowtop(c, N, S.h_g.as<float>(), S.rt_g.as<float>(), 0, S.build_band);
+    if (rc != WG_OK) return rc;
+    S.rt_fresh = true;
+    S.rt_band = S.build_band;
     // ---- local table, probes, global duplicate scan -------------------------------------
     uint64_t cap = 1024;
     while (cap < 2 * nl) cap <<= 1;
@@ -1035,44 +1039,21 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
     WG_ALLOC(c, S.lk, nl + 16);
     WG_ALLOC(c, S.flags, 64);
     { const int _sr = wg_scan_reserve(c, nl + 2); if (_sr != WG_OK) return _sr; }
-    if (!c->ev_hash) WG_HIP(c, hipEventCreateWithFlags(&c->ev_hash, hipEventDisableTiming | wg_event_scope()));
-    WG_HIP(c, hipMemsetAsync(S.flags.p, 0, 64, st));
-    // side stream (r06): the partition's duplicate scan over all N ids — its
-    // flag is read by X1's header, the last kernel of this segment (ev_hash) —
-    // then the heights and the row_top of every row of the list (zero bands,
-    // or build_frame's), overlapping the exchanges; the crossing edges' far
-    // endpoints read their y from it.  The local table and the probes run
-    // here meanwhile.
-    int rc = wg_side_fork(c);
-    if (rc != WG_OK) return rc;
-    {
-        hipStream_t ss = c->stream;
-        const uint32_t nbd = dup_blocks(N);
-        uint32_t *bcnt = reinterpret_cast<uint32_t *>(S.dlist.as<uint4>() + (uint64_t)nbd * T * DUP_R);
-        hipError_t e = hipMemsetAsync(S.ptable.p, 0xFF, pcap * 8, ss);
-        if (e == hipSuccess && N) {
-            hipLaunchKernelGGL(k_sh_dup_place, dim3(nbd), dim3(T), 0, ss, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
-                               S.ptable.as<unsigned long long>(), pcap - 1, S.dlist.as<uint4>(), bcnt);
-            hipLaunchKernelGGL(k_sh_dup_settle, dim3(nbd), dim3(T), 0, ss, c->d_oid, S.ptable.as<unsigned long long>(),
-                               pcap - 1, S.dlist.as<const uint4>(), (const uint32_t *)bcnt, S.flags.as<uint32_t>());
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) e = hipEventRecord(c->ev_hash, ss);
-        if (e != hipSuccess) rc = wg_fail(c, WG_E_HIP, "duplicate scan: %s", hipGetErrorString(e));
-        if (rc == WG_OK) rc = wg_heights_run(c, N, c->n_list, S.h_g.as<float>());
-        if (rc == WG_OK) rc = wg_rowtop_run(c, N, S.h_g.as<const float>(), S.build_band, S.rt_g.as<float>(), 0);
-        wg_side_done(c);
-        if (rc != WG_OK) return rc;
-    }
-    S.rt_fresh = true;
-    S.rt_band = S.build_band;
     wg_stage_begin(c, "hash_join");
     WG_HIP(c, hipMemsetAsync(c->hash.p, 0xFF, cap * 8, st));
+    WG_HIP(c, hipMemsetAsync(S.ptable.p, 0xFF, pcap * 8, st));
+    WG_HIP(c, hipMemsetAsync(S.flags.p, 0, 64, st));
     WG_HIP(c, hipMemsetAsync(S.lk.p, 0, nl + 16, st));
     if (nl) hipLaunchKernelGGL(k_sh_place, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
                                c->hash.as<unsigned long long>(), cap - 1);
+    const uint32_t nbd = dup_blocks(N);
+    uint32_t *bcnt = reinterpret_cast<uint32_t *>(S.dlist.as<uint4>() + (uint64_t)nbd * T * DUP_R);
+    if (N) hipLaunchKernelGGL(k_sh_dup_place, dim3(nbd), dim3(T), 0, st, c->d_oid, N, (uint32_t)world, (uint32_t)rank,
+                              S.ptable.as<unsigned long long>(), pcap - 1, S.dlist.as<uint4>(), bcnt);
     if (nl) hipLaunchKernelGGL(k_sh_settle, dim3(blocks(nl)), dim3(T), 0, st, c->d_oid, row_begin, nl,
                                c->hash.as<unsigned long long>(), cap - 1);
+    if (N) hipLaunchKernelGGL(k_sh_dup_settle, dim3(nbd), dim3(T), 0, st, c->d_oid, S.ptable.as<unsigned long long>(),
+                              pcap - 1, S.dlist.as<const uint4>(), (const uint32_t *)bcnt, S.flags.as<uint32_t>());
     if (nl) {
         hipLaunchKernelGGL(k_sh_probe, dim3(blocks(nl + nl / 2)), dim3(T), 0, st, row_begin, row_end, c->d_poff, c->d_poid,
                            c->d_oid, c->hash.as<const unsigned long long>(), cap - 1, S.prow.as<int32_t>());
@@ -1088,7 +1069,6 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
     // this rank learns its own counts from the gathered heads (X1 exchange).
     rc = sh_send_dev(c, 16 + El * 32, out);
     if (rc != WG_OK) return rc;
-    WG_HIP(c, hipStreamWaitEvent(st, c->ev_hash, 0));   // (the duplicate flag)
     hipLaunchKernelGGL(k_sh_x1_head, dim3(1), dim3(1), 0, st, S.msg.as<uint4>(), S.msg_len.as<unsigned long long>(),
                        (const uint32_t *)S.flags.as<uint32_t>(), (const uint32_t *)S.xcnt.as<uint32_t>(), nl, c->d_poff,
                        row_begin, row_end);
