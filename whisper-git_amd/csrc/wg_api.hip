@@ -543,7 +543,7 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
         c->slice_min_rows = value == 2 ? 4 * WG_SWEEP_CH : 1ull << 18;
         return WG_OK;
     case WG_OPT_MATCH_THREADS:
-        if (value != 0 && value != 256 && value != 512 && value != 513 && value != 1024)   // (513: 512 threads at 6 waves per SIMD, for A/B)
+        if (value != 0 && value != 256 && value != 512 && value != 513)   // (513: 512 threads at 6 waves per SIMD, for A/B)
             return wg_fail(c, WG_E_INVALID, "match threads %lld", (long long)value);
         c->match_threads = value ? (uint32_t)value : 512u;
         return WG_OK;

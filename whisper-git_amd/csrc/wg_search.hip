@@ -707,7 +707,6 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
         // workgroups per CU, as many as their LDS allows)
         if (c->match_threads == 512) hipLaunchKernelGGL((k_match<512, 4, 8>), dim3(mblocks(rows)), dim3(512), 0, s, A);
         else if (c->match_threads == 513) hipLaunchKernelGGL((k_match<512, 4, 6>), dim3(mblocks(rows)), dim3(512), 0, s, A);
-        else if (c->match_threads == 1024) hipLaunchKernelGGL((k_match<1024, 2, 8>), dim3(mblocks(rows)), dim3(1024), 0, s, A);
         else hipLaunchKernelGGL((k_match<256, 8, 1>), dim3(mblocks(rows)), dim3(256), 0, s, A);
     }
     WG_HIP(c, hipGetLastError());
