@@ -263,7 +263,9 @@ def main():
             return out, ShardComm.HDR, stride, sizes
 
     iso_ms = []
-    if not args.no_isolated and all(captured[r] for r in range(W)):
+    iso_err = None
+    try:
+      if not args.no_isolated and all(captured[r] for r in range(W)):
         for r in range(W):
             eng, st = engines[r], streams[r]
             s0, s1 = r * R, min(dag.n, (r + 1) * R)
@@ -279,6 +281,9 @@ def main():
                     if it:
                         ts.append(time.perf_counter() - t0)
             iso_ms.append(round(1e3 * float(np.median(ts)), 4))
+    except Exception as ex:   # (the lockstep figures stand without it)
+        iso_err = repr(ex)
+        iso_ms = []
 
     counters = [int(e.debug_counters()[5]) for e in engines]
     dcs = [e.debug_counters() for e in engines]   # [1] lane slots of the global replay, [10] serial replay
@@ -371,7 +376,7 @@ def main():
            "max_rank_ms_without_collectives": round(worst, 4),
            "exchanges_per_step": n_x, "exchange_bytes_per_rank": xbytes,
            "efficiency_without_collectives": round(single_ms / worst, 4),
-           "isolated_rank_ms": iso_ms,
+           "isolated_rank_ms": iso_ms, "isolated_error": iso_err,
            "max_rank_isolated_ms": max(iso_ms) if iso_ms else None,
            "efficiency_isolated": round(single_ms / max(iso_ms), 4) if iso_ms else None,
            "isolated_note": ("each rank's whole step replayed alone on the GPU (main and side streams overlapping "
