@@ -278,3 +278,34 @@ def test_match_two_passes_with_an_overflowing_pass(engine, dense, threads):
             assert n == wn and (got == want).all(), (q, dense, np.flatnonzero(got != want)[:5])
     finally:
         engine.match_rows("")
+
+
+def test_ascii_queries_across_the_ascii_lowering_code_points(engine, threads):
+    """r06: an ASCII query lists only the leads of U+0130 (-> "i" U+0307) and
+    U+212A (-> "k"), the two code points whose lowering holds an ASCII byte;
+    every other code point is left unlowered in LDS.  Rows mixing both with
+    other specials (U+1E9E, U+2126, U+212B), sigma and plain letters, with and
+    without a raw 0xFF byte in the range (marks off): ASCII queries that match
+    across the Kelvin sign and the dotted I, or must not, give the oracle's
+    flags; non-ASCII queries still take the full lowering."""
+    d = synth.generate("random13", 1300, seed=31)
+    engine.build(d)
+    rng = np.random.default_rng(9)
+    pieces = ["K", "İ", "f", "x", "i", "k", "K", "ẞ", "Ω", "Å", "Σ", "é", "a", " "]
+    qs = ["k", "xk", "kx", "fi", "fix", "i", "ik", "ki", "a k", "fa", "kki", "ix", "x" * 20 + "k", "fik",
+          "σ", "ék", "ẞ"]
+    try:
+        for raw_ff in (False, True):
+            rows = ["".join(pieces[j] for j in rng.integers(0, len(pieces), int(n))).encode()
+                    for n in rng.integers(0, 30, d.n)]
+            if raw_ff:
+                rows[300] = rows[300] + b"\xff"
+            off = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.uint64)
+            body = np.frombuffer(b"".join(rows), np.uint8)
+            for q in qs:
+                n = engine.match_rows(q, summaries=(body, off))
+                want, wn = so.match_rows(d, q.encode(), (body, off), None)
+                got = engine.match_flags()
+                assert n == wn and (got == want).all(), (q, raw_ff, np.flatnonzero(got != want)[:5])
+    finally:
+        engine.match_rows("")

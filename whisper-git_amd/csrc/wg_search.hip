@@ -69,6 +69,7 @@ struct MatchArgs {
     uint32_t qhex;                         // the query can match the id's hex (m <= 40, all of [0-9a-f])
     uint32_t marks;                        // the query holds no 0xFE / 0xFF byte: specials can be marked in place
     uint32_t spec_rel;                     // bit i: special i's lowered bytes share a byte with the query
+    uint32_t ascii;                        // the lowered query is all ASCII (see the lowering pass)
     // the query's first <= 8 bytes little-endian (as an LDS window holds them) and its mask; its last
     // <= 16 big-endian in two words with their masks (as the walks' shift registers hold them; m <= 16).
     // Host-computed: byte loads at the kernel's start wait behind the CU's staging loads.
@@ -230,7 +231,9 @@ __device__ bool walk_row(const WgCaseTables &T, const uint32_t *buf, uint32_t rs
 // Final_Sigma, the first-byte windows, the walks' list) twice the lanes, and
 // a CU twice the waves to hide each phase's round trips with (the workgroup's
 // LDS is unchanged, so the same workgroups fit per CU)
-template <int NT, int SB, int WPS>
+// AQ: the lowered query is all ASCII (A.ascii), a variant of its own so the
+// other queries' code is what it was
+template <int NT, int SB, int WPS, bool AQ>
 __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
     __shared__ uint32_t s_buf[MCAPW + 4];
     __shared__ uint32_t s_rel[2][MT + 1];     // per region of the staged image: its rows' byte offsets in it
@@ -254,6 +257,7 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
     const uint32_t q0 = (uint32_t)(qv & 0xFFu);
     const FeedShift sh{0, 0, A.qlo, A.qhi, A.mlo, A.mhi, 0, m};
     const WalkFeed wf{sh, WgKmp{A.q, A.fail, m, 0}, m > 16};
+    constexpr bool aq = AQ;
     if (tid < MT) s_rf[tid] = 0;
     if (tid < 8) s_cnt[tid] = 0;
     // both fields' row offsets and ranges up front (one round trip)
@@ -332,8 +336,9 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
                     const uint32_t k = k0 + lane + u * NT;
                     const uint32_t w = v[u];
                     if (k < tw) s_buf[k] = ascii_lower4(w);
-                    const uint32_t lead = w & (w << 1) & 0x80808080u;   // bytes >= 0xC0
-                    const uint32_t ce = eq_bytes(w, 0xCEu);
+                    // bytes >= 0xC0; an ASCII query lists only the leads it needs (see the lowering pass)
+                    const uint32_t lead = aq ? eq_bytes(w, 0xC4u) | eq_bytes(w, 0xE2u) : w & (w << 1) & 0x80808080u;
+                    const uint32_t ce = aq ? 0u : eq_bytes(w, 0xCEu);
                     cnt += (uint32_t)__builtin_popcount(lead & ~ce) + ((uint32_t)__builtin_popcount(ce) << 16);
                     raw_ff |= w & (w << 1) & (w << 2) & (w << 3) & (w << 4) & (w << 5) & (w << 6) & 0x80808080u;   // 0xFE / 0xFF
                 }
@@ -350,7 +355,8 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
 #pragma unroll
                     for (int u = 0; u < SB; u++) {
                         const uint32_t w = v[u], k = k0 + lane + u * NT;
-                        const uint32_t lead = w & (w << 1) & 0x80808080u, ce = eq_bytes(w, 0xCEu);
+                        const uint32_t lead = aq ? eq_bytes(w, 0xC4u) | eq_bytes(w, 0xE2u) : w & (w << 1) & 0x80808080u;
+                        const uint32_t ce = aq ? 0u : eq_bytes(w, 0xCEu);
                         if (!lead) continue;
                         for (uint32_t j = 0; j < 4; j++) {
                             if (!((lead >> (8 * j)) & 0x80u)) continue;
@@ -382,8 +388,9 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
         }
         for (uint32_t g = 0; g < ng; g++)
             if (tid < nr && s_rel[g][tid] < s_rel[g][tid + 1] && (sb[s_rel[g][tid]] & 0xC0u) == 0x80u) atomicOr(&pc[2], 1u);
-        // Final_Sigma of the U+03A3s, over the original non-ASCII bytes (nothing non-ASCII written yet)
-        for (uint32_t i = tid; i < nce; i += NT) {
+        // Final_Sigma of the U+03A3s, over the original non-ASCII bytes (nothing non-ASCII written yet);
+        // none for an ASCII query (sigma's lowered forms are not ASCII, and its 0xCE leads are not listed)
+        for (uint32_t i = tid; i < (aq ? 0u : nce); i += NT) {
             const uint32_t p = s_ce[-1 - (int)i];
             const uint32_t *rel = s_rel[reg(p)];
             const uint32_t r = row_of(rel, nr, p), rs = rel[r], n = rel[r + 1] - rs;
@@ -399,11 +406,18 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
         // and its row set to walk — unless its lowered bytes share none with the
         // query: then no match can overlap it; where marks are off it is left
         // as it was and its row walked by decoding, fast hits void.
+        // An ASCII query (r06) needs only the code points whose lowering holds
+        // an ASCII byte: U+0130 -> i + U+0307 (C4 B0) and U+212A -> 'k' (E2 84
+        // AA), no other in the tables.  Every other code point, lowered or not,
+        // is bytes >= 0x80 that no window or walk of the query can match, so
+        // its lead is not listed at all (the staging above), nor any 0xCE lead:
+        // no decode, no table load, and the lists overflow far less often.
         const uint32_t fl = pc[2];
         const bool exact = (fl & 1u) != 0, marks = A.marks && !(fl & 2u);
         for (uint32_t i = tid; i < nlead + nce; i += NT) {
             const uint32_t e = i < nlead ? s_lead[i] : s_ce[-1 - (int)(i - nlead)];
             const uint32_t p = e & 0x7FFFu, g = reg(p);
+            if (aq && sb[p] != 0xC4u && sb[p] != 0xE2u) continue;
             const uint32_t *rel = s_rel[g];
             uint32_t rs = 0, n = hi[g];
             if (exact) {
@@ -677,7 +691,9 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     A.m = m;
     A.qhex = m <= 40;
     A.marks = 1;
+    A.ascii = 1;
     for (uint8_t b : q) {
+        A.ascii &= b < 0x80;
         A.qhex &= (b - '0' < 10u) || (b - 'a' < 6u);
         A.marks &= b < 0xFE && b >= WG_SPECIAL_N;   // a mark's bytes never in the query
     }
@@ -705,9 +721,15 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     if (rows) {
         // (WPS: waves per SIMD the registers must allow — 8: four 512-thread
         // workgroups per CU, as many as their LDS allows)
-        if (c->match_threads == 512) hipLaunchKernelGGL((k_match<512, 4, 8>), dim3(mblocks(rows)), dim3(512), 0, s, A);
-        else if (c->match_threads == 513) hipLaunchKernelGGL((k_match<512, 4, 6>), dim3(mblocks(rows)), dim3(512), 0, s, A);
-        else hipLaunchKernelGGL((k_match<256, 8, 1>), dim3(mblocks(rows)), dim3(256), 0, s, A);
+#define WG_MATCH_LAUNCH(NT_, SB_, WPS_)                                                                  \
+        do {                                                                                             \
+            if (A.ascii) hipLaunchKernelGGL((k_match<NT_, SB_, WPS_, true>), dim3(mblocks(rows)), dim3(NT_), 0, s, A);  \
+            else hipLaunchKernelGGL((k_match<NT_, SB_, WPS_, false>), dim3(mblocks(rows)), dim3(NT_), 0, s, A);         \
+        } while (0)
+        if (c->match_threads == 512) WG_MATCH_LAUNCH(512, 4, 8);
+        else if (c->match_threads == 513) WG_MATCH_LAUNCH(512, 4, 6);
+        else WG_MATCH_LAUNCH(256, 8, 1);
+#undef WG_MATCH_LAUNCH
     }
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
