@@ -70,6 +70,7 @@ struct MatchArgs {
     uint32_t marks;                        // the query holds no 0xFE / 0xFF byte: specials can be marked in place
     uint32_t spec_rel;                     // bit i: special i's lowered bytes share a byte with the query
     uint32_t ascii;                        // the lowered query is all ASCII (see the lowering pass)
+    uint32_t aq_leads;                     // ... and the leads it lists: 1 U+0130's (C4), 2 U+212A's (E2)
     // the query's first <= 8 bytes little-endian (as an LDS window holds them) and its mask; its last
     // <= 16 big-endian in two words with their masks (as the walks' shift registers hold them; m <= 16).
     // Host-computed: byte loads at the kernel's start wait behind the CU's staging loads.
@@ -107,6 +108,12 @@ __device__ __forceinline__ uint32_t ascii_lower4(uint32_t w) {
 __device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t b) {
     const uint32_t x = w ^ (b * 0x01010101u);
     return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+
+// an ASCII query's leads to list (MatchArgs::aq_leads): bit 7 of each byte of
+// w that is 0xC4 (bit 0) or 0xE2 (bit 1)
+__device__ __forceinline__ uint32_t aq_lead_bytes(uint32_t w, uint32_t sel) {
+    return ((sel & 1u) ? eq_bytes(w, 0xC4u) : 0u) | ((sel & 2u) ? eq_bytes(w, 0xE2u) : 0u);
 }
 
 // the largest r < nr with rel[r] <= p (p >= rel[0]): the row holding byte p
@@ -337,7 +344,7 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
                     const uint32_t w = v[u];
                     if (k < tw) s_buf[k] = ascii_lower4(w);
                     // bytes >= 0xC0; an ASCII query lists only the leads it needs (see the lowering pass)
-                    const uint32_t lead = aq ? eq_bytes(w, 0xC4u) | eq_bytes(w, 0xE2u) : w & (w << 1) & 0x80808080u;
+                    const uint32_t lead = aq ? aq_lead_bytes(w, A.aq_leads) : w & (w << 1) & 0x80808080u;
                     const uint32_t ce = aq ? 0u : eq_bytes(w, 0xCEu);
                     cnt += (uint32_t)__builtin_popcount(lead & ~ce) + ((uint32_t)__builtin_popcount(ce) << 16);
                     raw_ff |= w & (w << 1) & (w << 2) & (w << 3) & (w << 4) & (w << 5) & (w << 6) & 0x80808080u;   // 0xFE / 0xFF
@@ -355,7 +362,7 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
 #pragma unroll
                     for (int u = 0; u < SB; u++) {
                         const uint32_t w = v[u], k = k0 + lane + u * NT;
-                        const uint32_t lead = aq ? eq_bytes(w, 0xC4u) | eq_bytes(w, 0xE2u) : w & (w << 1) & 0x80808080u;
+                        const uint32_t lead = aq ? aq_lead_bytes(w, A.aq_leads) : w & (w << 1) & 0x80808080u;
                         const uint32_t ce = aq ? 0u : eq_bytes(w, 0xCEu);
                         if (!lead) continue;
                         for (uint32_t j = 0; j < 4; j++) {
@@ -705,14 +712,33 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
         if (i + 8 < m) { A.qhi = (A.qhi << 8) | q[i]; A.mhi = (A.mhi << 8) | 0xFFu; }
         else { A.qlo = (A.qlo << 8) | q[i]; A.mlo = (A.mlo << 8) | 0xFFu; }
     }
+    // A special can take part in a match only if its lowered bytes L and the
+    // query agree wherever they overlap at some shift (L inside q, q inside L,
+    // or one's prefix the other's suffix): a match holds L contiguously.  r06:
+    // this exact test replaced "shares a byte" — "fix" no longer walks every
+    // U+0130 (L = "i" U+0307 overlaps "fix" at no shift).
     A.spec_rel = 0;
+    A.aq_leads = 0;
     {
         const std::vector<uint32_t> &flat = wg_match_flat_table();
         for (uint32_t i = 0; i < WG_SPECIAL_N; i++) {
-            const uint32_t x = flat[WG_FLAT_N + i];
-            for (uint32_t j = 0; j < (x >> 24); j++)
-                if (std::memchr(q.data(), (int)((x >> (8 * j)) & 0xFFu), q.size())) A.spec_rel |= 1u << i;
+            const uint32_t x = flat[WG_FLAT_N + i], l = x >> 24;
+            bool rel = false;
+            for (int64_t d = -(int64_t)l + 1; d < (int64_t)m && !rel; d++) {   // L starts at q[d]
+                bool ok = true;
+                for (uint32_t j = 0; j < l && ok; j++) {
+                    const int64_t qi = d + (int64_t)j;
+                    if (qi >= 0 && qi < (int64_t)m) ok = q[(size_t)qi] == ((x >> (8 * j)) & 0xFFu);
+                }
+                rel = ok;
+            }
+            if (rel) A.spec_rel |= 1u << i;
         }
+        // an ASCII query: the leads to list, of the two code points whose
+        // lowering holds an ASCII byte (U+0130: special 0; U+212A: C4 / E2)
+        const uint32_t ik = flat[0x212Au];
+        if (A.spec_rel & 1u) A.aq_leads |= 1u;
+        if ((ik & WG_FLAT_LENCHG) && ((A.spec_rel >> ((ik >> WG_FLAT_SPECIAL_SHIFT) & 31u)) & 1u)) A.aq_leads |= 2u;
     }
     A.flat = c->match_flat.as<const uint32_t>();
     A.out = c->match_flags.as<uint8_t>();
