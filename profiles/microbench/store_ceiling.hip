@@ -39,8 +39,8 @@ __global__ void __launch_bounds__(256) k_block(v4f *out, size_t n) {
     }
 }
 
-int main() {
-    const size_t bytes = 5856279118ull & ~(size_t)15;
+int main(int argc, char **argv) {
+    const size_t bytes = (argc > 1 ? strtoull(argv[1], nullptr, 10) : 5856279118ull) & ~(size_t)15;   // (argv[1]: another launch size, e.g. C4's 15.67 GB)
     const size_t n = bytes / 16;
     v4f *out;
     CHECK(hipMalloc(&out, bytes));
