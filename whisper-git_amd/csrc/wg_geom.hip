@@ -163,8 +163,13 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
     static_assert(WG_SWEEP_CH == 64, "a wave's rows are one sweep chunk");
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t cd = 0;
+    // (FUSED) the parent side of the carry counts for the next four chunks,
+    // 16 bits each: edges ending in one chunk all decrement one word, ~20-30
+    // same-address atomics per chunk on the Linux shape (r06, as k_top_carry)
+    uint64_t cdp = 0;
     if (r < n) {
         uint32_t b = 0, f = 0, cc = 0, ce = 0;
+        const bool small = (A.prow ? A.poff[r + 1] - A.poff[r] : A.edge_off[r + 1] - A.edge_off[r]) < 0xFFFFu;
         // (plain accumulation, no by-reference closure: that put the counters in scratch)
 #define WG_EDGE_COUNT(c_, p_, same_)                                                                 \
     do {                                                                                             \
@@ -175,7 +180,11 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
             if (same_) { b++; f += c + 1 < p; }                                                      \
             else { cc += c + 1 < p; ce++; }   /* (the swept lists' flag row is all zero: no child-end filter) */ \
             if (FUSED) {   /* k_edge_counts' parent side (:526-528) */                               \
-                if (k0_ <= k1_) atomicAdd(&A.carry_diff[k1_ + 1], 0xFFFFFFFFu);                       \
+                if (k0_ <= k1_) {   /* near chunks: counted here, one atomic per wave and chunk below */ \
+                    const uint32_t d_ = k1_ - c / WG_SWEEP_CH - 1u;                                   \
+                    if (d_ < 4u && small) cdp += 1ull << (16u * d_);                                  \
+                    else atomicAdd(&A.carry_diff[k1_ + 1], 0xFFFFFFFFu);                              \
+                }                                                                                    \
                 if (same_) {                                                                         \
                     atomicAdd(&A.cntT[p], 1u);                                                       \
                     if (c + 1 < p) atomicAdd(&A.diffF[p], 0xFFFFFFFFu);                              \
@@ -250,11 +259,28 @@ __global__ void __launch_bounds__(256) k_edges_rows(uint64_t n, EdgeRowsArgs A) 
         if (r == 0) { A.diffF[0] = 0u; A.diffC[0] = 0u; A.carry_diff[0] = 0u; }
         if (r < 64) A.misc[r] = 0u;
     }
+    if (FUSED) {
+        struct C5 { uint32_t v[5]; };
+        C5 x{{cd, (uint32_t)cdp & 0xFFFFu, (uint32_t)(cdp >> 16) & 0xFFFFu, (uint32_t)(cdp >> 32) & 0xFFFFu,
+              (uint32_t)(cdp >> 48)}};
+        const C5 zero{{0u, 0u, 0u, 0u, 0u}};
+        x = wg_wave_scan(x, zero, [](C5 a, const C5 &y) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) a.v[i] += y.v[i];
+            return a;
+        });
+        if ((threadIdx.x & 63) == 63 && r - 63 < n) {
+            const uint64_t q = r / WG_SWEEP_CH;
+            if (x.v[0]) atomicAdd(&A.carry_diff[q + 1], x.v[0]);
+#pragma unroll
+            for (int d = 1; d <= 4; d++)
+                if (x.v[d]) atomicAdd(&A.carry_diff[q + d + 1], 0u - x.v[d]);
+        }
+        return;
+    }
     const uint32_t tot = wg_wave_scan(cd, 0u, [](uint32_t x, uint32_t y) { return x + y; });
     if ((threadIdx.x & 63) == 63 && r - 63 < n) {
-        if (FUSED) {
-            if (tot) atomicAdd(&A.carry_diff[r / WG_SWEEP_CH + 1], tot);
-        } else {
+        {
             A.carry_diff[r / WG_SWEEP_CH + 1] = tot;
             A.carry_fill[r / WG_SWEEP_CH] = 0u;
         }
@@ -512,21 +538,46 @@ __global__ void __launch_bounds__(256) k_top_carry(uint64_t ne, const wg_edge *_
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t kbase = k - lid;
-    for (uint32_t t = lid; t < tot; t += 64) {
+    // the top-half slot first: its atomic in flight beside the registrations'
+    const bool top = live && e.child_lane == e.parent_lane;
+    const uint32_t p = e.parent_row;
+    uint32_t tpos = 0;
+    if (top) tpos = atomicAdd(&top_fill[p], 1u);
+    for (uint32_t base = 0; base < tot; base += 64) {   // (uniform)
+        const uint32_t t = base + lid;
+        const bool act = t < tot;
         // the edge: the last lane whose exclusive start is <= t (lanes with
         // no registration share the next lane's start and come before it)
-        uint32_t l = 0;
+        uint32_t l = 0, q = 0;
+        if (act) {
 #pragma unroll
-        for (uint32_t step = 32; step; step >>= 1)
-            if (s_pre[wv][l + step] <= t) l += step;
-        const uint32_t q = s_k0[wv][l] + (t - s_pre[wv][l]);
-        const uint32_t pos = atomicAdd(&carry_fill[q], 1u);
-        carry[carry_off[q] + pos] = (uint32_t)(kbase + l);
+            for (uint32_t step = 32; step; step >>= 1)
+                if (s_pre[wv][l + step] <= t) l += step;
+            q = s_k0[wv][l] + (t - s_pre[wv][l]);
+        }
+        // r06: the batch's registrations into one chunk share one atomic (a
+        // wave's edges start within ~64 rows, so a batch meets a few chunks;
+        // one atomic per registration queued ~27 same-address adds per chunk
+        // on the Linux shape), all of the batch's atomics in flight at once
+        uint64_t pend = __ballot(act);
+        uint32_t mine = 0, leader = 0, rank = 0;
+        while (pend) {   // (uniform: one round per distinct chunk)
+            const uint32_t lead = (uint32_t)__builtin_ctzll(pend);
+            const uint32_t qq = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)lead);
+            const bool in = act && q == qq;
+            const uint64_t m = __ballot(in);
+            if (lid == lead) mine = atomicAdd(&carry_fill[qq], (uint32_t)__builtin_popcountll(m));
+            if (in) {
+                leader = lead;
+                rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            }
+            pend &= ~m;
+        }
+        const uint32_t pos = (uint32_t)__shfl((int)mine, (int)leader, 64) + rank;
+        if (act) carry[carry_off[q] + pos] = (uint32_t)(kbase + l);
     }
-    if (!live || e.child_lane != e.parent_lane) return;
-    const uint32_t p = e.parent_row;
-    const uint32_t pos = atomicAdd(&top_fill[p], 1u);
-    vert[vert_off[p] + scanF[p + 1] + pos] = (uint32_t)k;   // edge id, packed below
+    if (!top) return;
+    vert[vert_off[p] + scanF[p + 1] + tpos] = (uint32_t)k;   // edge id, packed below
 }
 
 // ---- carry-in registration for the sweep -------------------------------------
