@@ -269,8 +269,11 @@ __global__ void __launch_bounds__(WG_BS_THREADS) k_probe_fix(const uint8_t *__re
 // not known empty.
 static int hash_table_prepare(wg_ctx *c, unsigned long long **table, unsigned long long **next, uint64_t *words, bool *later) {
     const uint64_t n = c->n;
+    // load <= 0.25 (r06; was 0.5): a quarter as many rows lose their home slot
+    // to the place pass, and the settle pass's compare-and-swap chains are
+    // what gates the near probe's fix-up (8 bytes per slot: 32 MB at 1M rows)
     uint64_t cap = 1024;
-    while (cap < 2 * n) cap <<= 1;
+    while (cap < 4 * n) cap <<= 1;
     c->hcap = cap;
     *words = cap + 1;   // the table, then the duplicate flag word (all ones = none)
     const int t = c->htab_cur, o = t ^ 1;
