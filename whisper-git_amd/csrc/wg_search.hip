@@ -49,6 +49,7 @@
 namespace {
 
 constexpr int MT = 256;                 // rows per workgroup
+#define WG_MATCH_STRIPES 8              // match-count words (one per 64-byte line)
 
 __constant__ uint32_t c_lower[WG_LOWER_N][3] = WG_LOWER_TABLE_INIT;
 __constant__ uint32_t c_cased[WG_CASED_N][2] = WG_CASED_TABLE_INIT;
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
     }
     if (live) A.out[r - A.rb] = hit ? 1 : 0;
     const int cnt = __syncthreads_count(live && hit);
-    if (tid == 0 && cnt) atomicAdd(A.count, (unsigned long long)cnt);
+    if (tid == 0 && cnt) atomicAdd(A.count + 8 * (blockIdx.x % WG_MATCH_STRIPES), (unsigned long long)cnt);
 }
 
 inline uint32_t mblocks(uint64_t n) { return (uint32_t)((n + MT - 1) / MT); }
@@ -677,13 +678,17 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
         WG_HIP(c, hipMemcpyAsync(c->match_flat.p, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, s));
         WG_HIP(c, hipStreamSynchronize(s));
     }
-    WG_ALLOC(c, c->match_q, 16 + m * 3 + 16);
+    // {the match count in WG_MATCH_STRIPES words, one per 64-byte line} + fail
+    // u16[m] + q u8[m]: a workgroup adds its count to stripe blockIdx % 8 (r06:
+    // ~4k same-address adds on one word queued behind the kernel's end)
+    constexpr size_t QH = 64 * WG_MATCH_STRIPES;
+    WG_ALLOC(c, c->match_q, QH + m * 3 + 16);
     std::vector<uint8_t> &qh = c->match_qhost;
-    qh.assign(16 + (size_t)m * 3, 0);
-    std::memcpy(qh.data() + 16, fail.data(), (size_t)m * 2);
-    std::memcpy(qh.data() + 16 + (size_t)m * 2, q.data(), m);
-    WG_HIP(c, hipMemsetAsync(c->match_q.p, 0, 8, s));
-    WG_HIP(c, hipMemcpyAsync(c->match_q.as<uint8_t>() + 16, qh.data() + 16, (size_t)m * 3, hipMemcpyHostToDevice, s));
+    qh.assign(QH + (size_t)m * 3, 0);
+    std::memcpy(qh.data() + QH, fail.data(), (size_t)m * 2);
+    std::memcpy(qh.data() + QH + (size_t)m * 2, q.data(), m);
+    WG_HIP(c, hipMemsetAsync(c->match_q.p, 0, QH, s));
+    WG_HIP(c, hipMemcpyAsync(c->match_q.as<uint8_t>() + QH, qh.data() + QH, (size_t)m * 3, hipMemcpyHostToDevice, s));
     MatchArgs A;
     A.rb = rb;
     A.re = re;
@@ -693,8 +698,8 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     A.auth_off = d_off[1];
     A.oid = c->d_oid;
     A.flags = c->d_flags;
-    A.fail = reinterpret_cast<const uint16_t *>(c->match_q.as<uint8_t>() + 16);
-    A.q = c->match_q.as<uint8_t>() + 16 + (size_t)m * 2;
+    A.fail = reinterpret_cast<const uint16_t *>(c->match_q.as<uint8_t>() + QH);
+    A.q = c->match_q.as<uint8_t>() + QH + (size_t)m * 2;
     A.m = m;
     A.qhex = m <= 40;
     A.marks = 1;
@@ -759,9 +764,13 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     }
     WG_HIP(c, hipGetLastError());
     wg_stage_end(c);
-    uint64_t cnt = 0;
-    const int frc = wg_fetch(c, {{c->match_q.p, true}}, &cnt);   // also orders the host copies above
+    uint64_t stripes[WG_MATCH_STRIPES] = {0};
+    WgFetch fi[WG_MATCH_STRIPES];
+    for (int k = 0; k < WG_MATCH_STRIPES; k++) fi[k] = WgFetch{c->match_q.as<uint8_t>() + 64 * k, true};
+    const int frc = wg_fetch_n(c, WG_MATCH_STRIPES, fi, stripes);   // also orders the host copies above
     if (frc != WG_OK) return frc;
+    uint64_t cnt = 0;
+    for (uint64_t v : stripes) cnt += v;
     c->match_count = cnt;
     c->match_on = true;
     if (match_count) *match_count = cnt;
