@@ -297,3 +297,35 @@ def test_fused_join_with_deferred_clear_cycle(fused):
             assert eng.layout_summary().max_lane == want[k][1], tag
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("defer", [False, True])
+def test_lds_sweep_skipped_then_needed(defer):
+    """r06: a speculative geometry pass skips the LDS sweep's launch when the
+    context's last exact pass had no chunk past the register sweep; a chunk
+    that then needs it raises the capacity word and the pass is redone exactly
+    (here the register sweep's capacity is cut to 64 edges per chunk after two
+    builds, so every chunk of the next list is wide).  Every build bit-exact,
+    and the next speculative pass launches the LDS sweep again."""
+    import wgraph
+    from oracle import oracle_c
+    from wgraph import lib
+    eng = wgraph.Engine(0)
+    try:
+        eng.set_defer_validation(defer)
+        seq = [("wide16", 3000, 1, 512), ("wide16", 3000, 1, 512), ("wide16", 3000, 2, 64),
+               ("wide16", 3000, 2, 64), ("random13", 5000, 3, 512)]
+        redo = []
+        for i, (kind, n, seed, cap) in enumerate(seq):
+            eng._check(lib().wg_set_option(eng._ctx, 3, cap))   # WG_OPT_SWEEP_REG
+            d = synth.generate(kind, n, seed=seed)
+            o = oracle_c.OracleLayout(d)
+            eng.build(d)
+            full_check(eng, d, o, f"#{i} {kind}/{n} cap {cap}")
+            redo.append(int(eng.debug_counters()[8]))
+            o.close()
+        assert redo[1] == redo[0]          # no wide chunk: the skipped LDS sweep costs nothing
+        assert redo[2] > redo[1]           # every chunk wide: the skipped sweep is redone exactly
+        assert redo[3] == redo[2]          # the next pass launches the LDS sweep: no redo
+    finally:
+        eng.close()

@@ -885,7 +885,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
         const uint32_t *__restrict__ kept_off, uint32_t *__restrict__ kept_ref, uint32_t *__restrict__ kept_row,
         uint32_t *__restrict__ big, uint32_t *__restrict__ big_n, uint32_t reg_cap, Cap vc, Cap sc, Cap cc, uint32_t *ovf,
         const uint32_t *__restrict__ run_if, const uint32_t *__restrict__ done, const uint32_t *__restrict__ scanF,
-        const uint32_t *__restrict__ cntT) {
+        const uint32_t *__restrict__ cntT, uint32_t lds_off) {
     __shared__ uint32_t s_car[SW_WAVES][64 * SW_SLOTS];
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[SW_WAVES][SW_STAGE];
     const uint32_t lid = threadIdx.x & 63;
@@ -918,6 +918,10 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_sweep(uint64_t n, uint64_t q0
     const uint32_t ncar = a1 - a;
     const uint32_t total = ncar + (E1 - E0);
     if (total > reg_cap || total > 64u * SW_SLOTS) {   // the LDS sweep (k_sweep_lds) reads the ranked list from HBM
+        if (lds_off) {   // (not launched: the pass is redone exactly)
+            if (lid == 0) atomicOr(ovf, 1u);
+            return;
+        }
         carry_rank(carry + a, ncar, s_stage[threadIdx.x >> 6], carry_sorted + a);
         if (lid == 0) big[atomicAdd(big_n, 1u)] = (uint32_t)q;
         return;
@@ -1328,7 +1332,7 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), big,
                        big_n, c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, vc, sc, cc, ovf,
-                       (const uint32_t *)nullptr, (const uint32_t *)nullptr, L.cntF, L.cntT);
+                       (const uint32_t *)nullptr, (const uint32_t *)nullptr, L.cntF, L.cntT, L.lds_off ? 1u : 0u);
     // (one wave per wide chunk, ~73 KB of LDS per block: two blocks per CU,
     // the whole chip for lists whose every chunk is wide; sized by the last
     // pass's count of wide chunks; 64 blocks for a list that had none, as
@@ -1337,7 +1341,7 @@ int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s)
     const uint64_t lds_want = 64 + (uint64_t)c->sweep_wide_last / SW_WAVES;
     const uint64_t lds_grid = std::min<uint64_t>(std::min<uint64_t>(SW_LDS_BLOCKS, lds_want),
                                                  (q1 - q0 + SW_WAVES - 1) / SW_WAVES);
-    hipLaunchKernelGGL(k_sweep_lds, dim3((uint32_t)lds_grid), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)big,
+    if (!L.lds_off) hipLaunchKernelGGL(k_sweep_lds, dim3((uint32_t)lds_grid), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)big,
                        (const uint32_t *)big_n, E, edge_off, carry_off, (const uint32_t *)carry_sorted,
                        c->rowflags.as<const uint8_t>(), voff, soff, vert, c->scurve_ref.as<uint32_t>(),
                        c->scurve_row.as<uint32_t>(), koff, c->curve_ref.as<uint32_t>(), c->curve_row.as<uint32_t>(), err,
@@ -1370,7 +1374,7 @@ static void launch_superset(wg_ctx *c, uint64_t n, hipStream_t s, const uint32_t
                        (uint32_t *)nullptr, c->scurve_ref.as<uint32_t>(), c->scurve_row.as<uint32_t>(),
                        (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, big, big_n,
                        c->sweep_reg_cap < 64u * SW_SLOTS ? c->sweep_reg_cap : 64u * SW_SLOTS, g, g, g, ovf, run_if,
-                       (const uint32_t *)(err + 5), (const uint32_t *)nullptr, (const uint32_t *)nullptr);
+                       (const uint32_t *)(err + 5), (const uint32_t *)nullptr, (const uint32_t *)nullptr, 0u);
     const uint64_t lds_grid = std::min<uint64_t>(std::min<uint64_t>(SW_LDS_BLOCKS, 64 + (uint64_t)c->sweep_wide_last / SW_WAVES),
                                                  (nch + SW_WAVES - 1) / SW_WAVES);
     hipLaunchKernelGGL(k_sweep_lds, dim3((uint32_t)lds_grid), dim3(64 * SW_WAVES), 0, s, n, (const uint32_t *)big,
@@ -1615,6 +1619,9 @@ int wg_stage_geometry(wg_ctx *c, const float *d_band) {
         wg_stage_end(c);
         return WG_OK;
     }
+    // r06: a speculative pass skips the LDS sweep's launch (~5 us at its
+    // floor on the critical path) when the last exact pass had no wide chunk
+    L.lds_off = spec && !c->sh.on && c->sweep_wide_last == 0;
     if (const int rc = wg_geom_lists(c, 0, n, 0, s)) return rc;
     wg_stage_end(c);
     if (spec) return WG_OK;   // validated at the end of the build (wg_geom_spec_items / wg_geom_spec_check)

@@ -605,6 +605,10 @@ struct wg_ctx {
         const uint32_t *vtot = nullptr, *stot = nullptr, *ctot = nullptr;   // the lists' scanned totals (capacity checks)
         uint32_t vcap = ~0u, scap = ~0u, ccap = ~0u;
         uint32_t *err = nullptr;   // the pass's flag words (geom_err)
+        // a speculative pass after a list with no chunk past the register
+        // sweep: the LDS sweep is not launched, and a chunk that needs it
+        // raises the capacity-overflow word (the exact pass redoes the lists)
+        bool lds_off = false;
     } glist;
     bool     slice_on = false;     // WG_OPT_SLICE_LISTS (measured slower on wide16 1M: DESIGN §3.2a)
     double   slice_frac = 0.25;
