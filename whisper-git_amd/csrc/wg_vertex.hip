@@ -89,22 +89,36 @@ __global__ void k_vtx_prep(uint64_t rb, uint64_t rows, int64_t sel, const uint32
                            uint4 *__restrict__ info, const uint32_t *__restrict__ gate, WgFusedFetch ff) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j > rows) return;
-    if (gate && (gate[0] | gate[8])) {   // (the host still gets the words: they say the build did not hold)
+    // r06: every load in one round before the first wait (the gate's branch
+    // held the offsets' loads behind it: two dependent round trips).  Row
+    // j + 1 <= rows + 1 is inside vert_off / curve_off (n + 2 entries).
+    typedef const __attribute__((address_space(1))) uint32_t gword;   // global loads, not flat
+    const uint64_t r = rb + j;
+    const uint32_t g0 = gate ? *(gword *)gate : 0u, g8 = gate ? *(gword *)(gate + 8) : 0u;
+    const uint32_t v0 = voff[rb], c0 = coff[rb], vo = voff[r], v1 = voff[r + 1], co = coff[r], c1 = coff[r + 1];
+    const uint32_t vn = voff[rb + rows], cn = coff[rb + rows];
+    asm volatile("" ::"v"(g0), "v"(g8), "v"(v0), "v"(c0), "v"(vo), "v"(v1), "v"(co), "v"(c1), "v"(vn), "v"(cn));
+    if (g0 | g8) {   // (the host still gets the words: they say the build did not hold)
         if (j == rows && ff.seq_word) wg_fused_fetch_store(ff);
         return;
     }
-    const uint32_t v0 = voff[rb], c0 = coff[rb];
-    const uint64_t s = vtx_at(rb, j, sel, voff, coff, v0, c0);
+    // vtx_at's closed form on the loaded words
+    auto at = [&](uint64_t jj, uint32_t vv, uint32_t cc) -> uint64_t {
+        uint64_t v = (uint64_t)WG_VTX_PER_VERTICAL * (vv - v0) + (uint64_t)WG_VTX_PER_CURVE * (cc - c0) +
+                     (uint64_t)WG_VTX_PER_NODE * jj;
+        if (sel >= 0 && (uint64_t)sel >= rb && (uint64_t)sel < rb + jj) v += WG_VTX_PER_RING;
+        return v;
+    };
+    const uint64_t s = at(j, vo, co);
     vtx_off[j] = s;
     if (j == rows) {
         if (ff.seq_word) wg_fused_fetch_store(ff);
         return;
     }
-    const uint64_t e = vtx_at(rb, j + 1, sel, voff, coff, v0, c0);
-    const uint64_t ntiles = (vtx_at(rb, rows, sel, voff, coff, v0, c0) + TILE - 1) / TILE;
+    const uint64_t e = at(j + 1, v1, c1);
+    const uint64_t ntiles = (at(rows, vn, cn) + TILE - 1) / TILE;
     if (ntiles + 1 > tcap) return;
-    const uint64_t r = rb + j;
-    const uint32_t vo = voff[r], nv = voff[r + 1] - vo, co = coff[r], nc = coff[r + 1] - co;
+    const uint32_t nv = v1 - vo, nc = c1 - co;
     const uint64_t cv = s + (uint64_t)WG_VTX_PER_VERTICAL * nv;
     for (uint64_t t = (s + TILE - 1) / TILE; t * TILE < e; t++) {
         const uint64_t vt = t * TILE;
@@ -126,7 +140,7 @@ __global__ void k_vtx_prep(uint64_t rb, uint64_t rows, int64_t sel, const uint32
         }
         info[t] = make_uint4((uint32_t)j, A, K0, fl);
     }
-    if (j == rows - 1) info[ntiles] = make_uint4((uint32_t)rows, voff[r + 1], coff[r + 1], 0u);
+    if (j == rows - 1) info[ntiles] = make_uint4((uint32_t)rows, v1, c1, 0u);
 }
 
 struct RowInfo {
