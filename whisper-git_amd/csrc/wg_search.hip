@@ -44,12 +44,14 @@
 #include "wg_internal.h"
 #include "wg_unicase.h"
 
+#include <algorithm>
 #include <cstring>
 
 namespace {
 
 constexpr int MT = 256;                 // rows per workgroup
 #define WG_MATCH_STRIPES 8              // match-count words (one per 64-byte line)
+#define WG_FILT_LEADS 6                 // lead bytes the lead-filtered variant lists (0xCE apart)
 
 __constant__ uint32_t c_lower[WG_LOWER_N][3] = WG_LOWER_TABLE_INIT;
 __constant__ uint32_t c_cased[WG_CASED_N][2] = WG_CASED_TABLE_INIT;
@@ -70,8 +72,10 @@ struct MatchArgs {
     uint32_t qhex;                         // the query can match the id's hex (m <= 40, all of [0-9a-f])
     uint32_t marks;                        // the query holds no 0xFE / 0xFF byte: specials can be marked in place
     uint32_t spec_rel;                     // bit i: special i's lowered bytes share a byte with the query
-    uint32_t ascii;                        // the lowered query is all ASCII (see the lowering pass)
-    uint32_t aq_leads;                     // ... and the leads it lists: 1 U+0130's (C4), 2 U+212A's (E2)
+    // the lead-filtered variants (k_match<..., MODE 1 / 2>, see the lowering
+    // pass): the lead bytes it lists — up to WG_FILT_LEADS, 0xCE apart (flt_ce)
+    uint32_t flt_n, flt_ce;
+    uint8_t flt_lead[8];
     // the query's first <= 8 bytes little-endian (as an LDS window holds them) and its mask; its last
     // <= 16 big-endian in two words with their masks (as the walks' shift registers hold them; m <= 16).
     // Host-computed: byte loads at the kernel's start wait behind the CU's staging loads.
@@ -111,10 +115,18 @@ __device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t b) {
     return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
 }
 
-// an ASCII query's leads to list (MatchArgs::aq_leads): bit 7 of each byte of
-// w that is 0xC4 (bit 0) or 0xE2 (bit 1)
-__device__ __forceinline__ uint32_t aq_lead_bytes(uint32_t w, uint32_t sel) {
-    return ((sel & 1u) ? eq_bytes(w, 0xC4u) : 0u) | ((sel & 2u) ? eq_bytes(w, 0xE2u) : 0u);
+// the lead-filtered variant's leads to list: bit 7 of each byte of w that is
+// one of the n lead bytes (MatchArgs::flt_lead).  MODE 1 (an ASCII query):
+// the leads are a subset of {0xC4, 0xE2} (U+0130 and U+212A, the only code
+// points whose lowering holds an ASCII byte), selected by bits 0 / 1 of n.
+template <int MODE>
+__device__ __forceinline__ uint32_t filt_lead_bytes(uint32_t w, const uint8_t (&lb)[8], uint32_t n) {
+    if (MODE == 1) return ((n & 1u) ? eq_bytes(w, 0xC4u) : 0u) | ((n & 2u) ? eq_bytes(w, 0xE2u) : 0u);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < WG_FILT_LEADS; i++)
+        if ((uint32_t)i < n) m |= eq_bytes(w, lb[i]);
+    return m;
 }
 
 // the largest r < nr with rel[r] <= p (p >= rel[0]): the row holding byte p
@@ -239,9 +251,11 @@ __device__ bool walk_row(const WgCaseTables &T, const uint32_t *buf, uint32_t rs
 // Final_Sigma, the first-byte windows, the walks' list) twice the lanes, and
 // a CU twice the waves to hide each phase's round trips with (the workgroup's
 // LDS is unchanged, so the same workgroups fit per CU)
-// AQ: the lowered query is all ASCII (A.ascii), a variant of its own so the
-// other queries' code is what it was
-template <int NT, int SB, int WPS, bool AQ>
+// MODE 0: every lead listed; 2: the lead-filtered variant (a query whose
+// matches can hold the lowering of code points under a few lead bytes only;
+// MatchArgs::flt_*); 1: the same for an ASCII query, its leads fixed.  Each a
+// variant of its own so the other queries' code is what it was.
+template <int NT, int SB, int WPS, int MODE>
 __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
     __shared__ uint32_t s_buf[MCAPW + 4];
     __shared__ uint32_t s_rel[2][MT + 1];     // per region of the staged image: its rows' byte offsets in it
@@ -265,7 +279,10 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
     const uint32_t q0 = (uint32_t)(qv & 0xFFu);
     const FeedShift sh{0, 0, A.qlo, A.qhi, A.mlo, A.mhi, 0, m};
     const WalkFeed wf{sh, WgKmp{A.q, A.fail, m, 0}, m > 16};
-    constexpr bool aq = AQ;
+    const uint32_t flt_n = A.flt_n;
+    uint8_t flt_lead[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) flt_lead[i] = A.flt_lead[i];
     if (tid < MT) s_rf[tid] = 0;
     if (tid < 8) s_cnt[tid] = 0;
     // both fields' row offsets and ranges up front (one round trip)
@@ -345,8 +362,8 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
                     const uint32_t w = v[u];
                     if (k < tw) s_buf[k] = ascii_lower4(w);
                     // bytes >= 0xC0; an ASCII query lists only the leads it needs (see the lowering pass)
-                    const uint32_t lead = aq ? aq_lead_bytes(w, A.aq_leads) : w & (w << 1) & 0x80808080u;
-                    const uint32_t ce = aq ? 0u : eq_bytes(w, 0xCEu);
+                    const uint32_t ce = (MODE == 0 || (MODE == 2 && A.flt_ce)) ? eq_bytes(w, 0xCEu) : 0u;   // (a subset of the leads)
+                    const uint32_t lead = MODE ? filt_lead_bytes<MODE>(w, flt_lead, flt_n) | ce : w & (w << 1) & 0x80808080u;
                     cnt += (uint32_t)__builtin_popcount(lead & ~ce) + ((uint32_t)__builtin_popcount(ce) << 16);
                     raw_ff |= w & (w << 1) & (w << 2) & (w << 3) & (w << 4) & (w << 5) & (w << 6) & 0x80808080u;   // 0xFE / 0xFF
                 }
@@ -363,8 +380,8 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
 #pragma unroll
                     for (int u = 0; u < SB; u++) {
                         const uint32_t w = v[u], k = k0 + lane + u * NT;
-                        const uint32_t lead = aq ? aq_lead_bytes(w, A.aq_leads) : w & (w << 1) & 0x80808080u;
-                        const uint32_t ce = aq ? 0u : eq_bytes(w, 0xCEu);
+                        const uint32_t ce = (MODE == 0 || (MODE == 2 && A.flt_ce)) ? eq_bytes(w, 0xCEu) : 0u;   // (a subset of the leads)
+                        const uint32_t lead = MODE ? filt_lead_bytes<MODE>(w, flt_lead, flt_n) | ce : w & (w << 1) & 0x80808080u;
                         if (!lead) continue;
                         for (uint32_t j = 0; j < 4; j++) {
                             if (!((lead >> (8 * j)) & 0x80u)) continue;
@@ -396,9 +413,9 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
         }
         for (uint32_t g = 0; g < ng; g++)
             if (tid < nr && s_rel[g][tid] < s_rel[g][tid + 1] && (sb[s_rel[g][tid]] & 0xC0u) == 0x80u) atomicOr(&pc[2], 1u);
-        // Final_Sigma of the U+03A3s, over the original non-ASCII bytes (nothing non-ASCII written yet);
-        // none for an ASCII query (sigma's lowered forms are not ASCII, and its 0xCE leads are not listed)
-        for (uint32_t i = tid; i < (aq ? 0u : nce); i += NT) {
+        // Final_Sigma of the U+03A3s, over the original non-ASCII bytes (nothing non-ASCII written yet)
+        // (none listed when the lead-filtered variant leaves 0xCE out)
+        for (uint32_t i = tid; i < nce; i += NT) {
             const uint32_t p = s_ce[-1 - (int)i];
             const uint32_t *rel = s_rel[reg(p)];
             const uint32_t r = row_of(rel, nr, p), rs = rel[r], n = rel[r + 1] - rs;
@@ -414,18 +431,16 @@ __global__ __launch_bounds__(NT, WPS) void k_match(MatchArgs A) {
         // and its row set to walk — unless its lowered bytes share none with the
         // query: then no match can overlap it; where marks are off it is left
         // as it was and its row walked by decoding, fast hits void.
-        // An ASCII query (r06) needs only the code points whose lowering holds
-        // an ASCII byte: U+0130 -> i + U+0307 (C4 B0) and U+212A -> 'k' (E2 84
-        // AA), no other in the tables.  Every other code point, lowered or not,
-        // is bytes >= 0x80 that no window or walk of the query can match, so
-        // its lead is not listed at all (the staging above), nor any 0xCE lead:
-        // no decode, no table load, and the lists overflow far less often.
+        // The lead-filtered variant (r06) lists only the leads of code points
+        // whose lowering a match can hold (the host's relevance test, at
+        // wg_match_rows): every other code point stays as it is, bytes that no
+        // window or walk of the query can match lowered or not — no decode, no
+        // table load, and the lists overflow far less often.
         const uint32_t fl = pc[2];
         const bool exact = (fl & 1u) != 0, marks = A.marks && !(fl & 2u);
         for (uint32_t i = tid; i < nlead + nce; i += NT) {
             const uint32_t e = i < nlead ? s_lead[i] : s_ce[-1 - (int)(i - nlead)];
             const uint32_t p = e & 0x7FFFu, g = reg(p);
-            if (aq && sb[p] != 0xC4u && sb[p] != 0xE2u) continue;
             const uint32_t *rel = s_rel[g];
             uint32_t rs = 0, n = hi[g];
             if (exact) {
@@ -599,6 +614,81 @@ const std::vector<uint32_t> &wg_match_flat_table() {
     return table;
 }
 
+// The inverse of the simple lowercase mapping, {lowercase, code point} sorted,
+// without the specials (their relevance is MatchArgs::spec_rel's exact test),
+// and the specials' own code points by index.  Built once per process.
+namespace {
+struct LowerInverse {
+    std::vector<std::pair<uint32_t, uint32_t>> pairs;
+    uint32_t special_cp[WG_SPECIAL_N] = {};
+};
+const LowerInverse &lower_inverse() {
+    static const LowerInverse inv = [] {
+        LowerInverse v;
+        const WgCaseTables HT{h_lower, h_cased, h_ign};
+        const std::vector<uint32_t> &flat = wg_match_flat_table();
+        for (uint32_t cp = 0x80; cp < 0x110000u; cp++) {
+            if (cp >= 0xD800 && cp < 0xE000) continue;
+            if (cp < WG_FLAT_N && (flat[cp] & WG_FLAT_LENCHG)) {
+                v.special_cp[(flat[cp] >> WG_FLAT_SPECIAL_SHIFT) & 31u] = cp;
+                continue;
+            }
+            const uint32_t lc = wg_lower_simple(HT, cp);
+            if (lc != cp) v.pairs.emplace_back(lc, cp);
+        }
+        std::sort(v.pairs.begin(), v.pairs.end());
+        return v;
+    }();
+    return inv;
+}
+}  // namespace
+
+// The lead-filtered variant (r06).  A match holds the lowered text's bytes
+// at the query's code points (for a well-formed query a window can only match
+// at code point boundaries, every byte of the query being a lead or a
+// continuation of one), so only code points whose lowering is one of the
+// query's code points need lowering — those under a few lead bytes — plus
+// U+03A3 when the query holds sigma (Final_Sigma decides between its two
+// forms) and the specials spec_rel found relevant.  Any other code point, left
+// as it is, holds bytes no window of the query can match, and so does its
+// lowering.  Sets A.flt_*; flt_n = ~0 when the query is not well-formed UTF-8
+// or needs more than WG_FILT_LEADS lead bytes besides 0xCE (the full variant).
+static void match_lead_filter(const std::vector<uint8_t> &q, MatchArgs &A) {
+    A.flt_n = 0xFFFFFFFFu;
+    A.flt_ce = 0;
+    for (uint8_t &b : A.flt_lead) b = 0;
+    const LowerInverse &inv = lower_inverse();
+    bool lead[256] = {};
+    const uint32_t m = (uint32_t)q.size();
+    for (uint32_t i = 0; i < m;) {
+        uint32_t len;
+        const uint32_t cp = wg_utf8_decode(q.data(), i, m, &len);
+        if (cp & 0x80000000u) return;   // not well formed: the full variant
+        i += len;
+        auto it = std::lower_bound(inv.pairs.begin(), inv.pairs.end(), std::make_pair(cp, 0u));
+        for (; it != inv.pairs.end() && it->first == cp; ++it) {
+            uint8_t e[4];
+            wg_utf8_encode(it->second, e);
+            lead[e[0]] = true;
+        }
+        if (cp == 0x3C2u || cp == 0x3C3u) lead[0xCE] = true;   // U+03A3 (Final_Sigma)
+    }
+    for (uint32_t i = 0; i < WG_SPECIAL_N; i++)
+        if (((A.spec_rel >> i) & 1u) && inv.special_cp[i]) {
+            uint8_t e[4];
+            wg_utf8_encode(inv.special_cp[i], e);
+            lead[e[0]] = true;
+        }
+    uint32_t n = 0;
+    for (uint32_t b = 0x80; b < 0x100; b++) {
+        if (!lead[b] || b == 0xCE) continue;
+        if (n == WG_FILT_LEADS) return;   // too many: the full variant
+        A.flt_lead[n++] = (uint8_t)b;
+    }
+    A.flt_n = n;
+    A.flt_ce = lead[0xCE] ? 1u : 0u;
+}
+
 // Rust `str::to_lowercase` of a byte string on the host (same tables as the device)
 std::vector<uint8_t> wg_lower_host(const uint8_t *p, uint64_t n) {
     const WgCaseTables T{h_lower, h_cased, h_ign};
@@ -703,9 +793,7 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     A.m = m;
     A.qhex = m <= 40;
     A.marks = 1;
-    A.ascii = 1;
     for (uint8_t b : q) {
-        A.ascii &= b < 0x80;
         A.qhex &= (b - '0' < 10u) || (b - 'a' < 6u);
         A.marks &= b < 0xFE && b >= WG_SPECIAL_N;   // a mark's bytes never in the query
     }
@@ -723,7 +811,6 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
     // this exact test replaced "shares a byte" — "fix" no longer walks every
     // U+0130 (L = "i" U+0307 overlaps "fix" at no shift).
     A.spec_rel = 0;
-    A.aq_leads = 0;
     {
         const std::vector<uint32_t> &flat = wg_match_flat_table();
         for (uint32_t i = 0; i < WG_SPECIAL_N; i++) {
@@ -739,12 +826,27 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
             }
             if (rel) A.spec_rel |= 1u << i;
         }
-        // an ASCII query: the leads to list, of the two code points whose
-        // lowering holds an ASCII byte (U+0130: special 0; U+212A: C4 / E2)
-        const uint32_t ik = flat[0x212Au];
-        if (A.spec_rel & 1u) A.aq_leads |= 1u;
-        if ((ik & WG_FLAT_LENCHG) && ((A.spec_rel >> ((ik >> WG_FLAT_SPECIAL_SHIFT) & 31u)) & 1u)) A.aq_leads |= 2u;
     }
+    match_lead_filter(q, A);
+    // the variant: 1 an ASCII query (its leads a subset of {C4, E2}: flt_n
+    // becomes the selection bits), 2 other filtered queries, 0 the rest
+    int mode = A.flt_n == 0xFFFFFFFFu ? 0 : 2;
+    if (mode == 2 && !A.flt_ce) {
+        uint32_t sel = 0;
+        bool only = true;
+        for (uint32_t i = 0; i < A.flt_n; i++) {
+            if (A.flt_lead[i] == 0xC4u) sel |= 1u;
+            else if (A.flt_lead[i] == 0xE2u) sel |= 2u;
+            else only = false;
+        }
+        bool ascii = true;
+        for (uint8_t b : q) ascii &= b < 0x80;
+        if (only && ascii) {
+            mode = 1;
+            A.flt_n = sel;
+        }
+    }
+    if (mode == 0) A.flt_n = 0;
     A.flat = c->match_flat.as<const uint32_t>();
     A.out = c->match_flags.as<uint8_t>();
     A.count = c->match_q.as<unsigned long long>();
@@ -754,8 +856,9 @@ int wg_match_rows(wg_ctx *c, const uint8_t *query, uint64_t query_len, uint64_t 
         // workgroups per CU, as many as their LDS allows)
 #define WG_MATCH_LAUNCH(NT_, SB_, WPS_)                                                                  \
         do {                                                                                             \
-            if (A.ascii) hipLaunchKernelGGL((k_match<NT_, SB_, WPS_, true>), dim3(mblocks(rows)), dim3(NT_), 0, s, A);  \
-            else hipLaunchKernelGGL((k_match<NT_, SB_, WPS_, false>), dim3(mblocks(rows)), dim3(NT_), 0, s, A);         \
+            if (mode == 1) hipLaunchKernelGGL((k_match<NT_, SB_, WPS_, 1>), dim3(mblocks(rows)), dim3(NT_), 0, s, A);  \
+            else if (mode == 2) hipLaunchKernelGGL((k_match<NT_, SB_, WPS_, 2>), dim3(mblocks(rows)), dim3(NT_), 0, s, A); \
+            else hipLaunchKernelGGL((k_match<NT_, SB_, WPS_, 0>), dim3(mblocks(rows)), dim3(NT_), 0, s, A);            \
         } while (0)
         if (c->match_threads == 512) WG_MATCH_LAUNCH(512, 4, 8);
         else if (c->match_threads == 513) WG_MATCH_LAUNCH(512, 4, 6);
