@@ -1027,10 +1027,12 @@ static int shard_build_impl(wg_ctx *c, const wg_commits *in, int world, int rank
     S.rt_fresh = true;
     S.rt_band = S.build_band;
     // ---- local table, probes, global duplicate scan -------------------------------------
+    // (load <= 0.25, as the single-GPU table since r06: fewer rows lose their
+    // home slot to the place passes, shorter compare-and-swap chains in settle)
     uint64_t cap = 1024;
-    while (cap < 2 * nl) cap <<= 1;
+    while (cap < 4 * nl) cap <<= 1;
     uint64_t pcap = 1024;
-    while (pcap < 2 * (N / world + 1) + 1024) pcap <<= 1;
+    while (pcap < 4 * (N / world + 1) + 1024) pcap <<= 1;
     WG_ALLOC(c, c->hash, cap * 8);
     WG_ALLOC(c, S.ptable, pcap * 8);
     WG_ALLOC(c, S.dlist, (uint64_t)dup_blocks(N) * (T * DUP_R * 16 + 4) + 16);
