@@ -342,7 +342,12 @@ int wg_stage_hash_join(wg_ctx *c) {
     WG_ALLOC(c, c->prow, e * 4 + 4);
     WG_ALLOC(c, c->edge_cnt, (n + 1) * 4);
     WG_ALLOC(c, c->rowmiss, n + 4);
-    WG_ALLOC(c, c->bsum, 3 * (wg_bs_blocks(n) + 64) * 4);
+    // block sums: the edge counts' at [3 (nbs + 64), 4 (nbs + 64)), apart from
+    // the lane stage's three arrays (its scan may take this one along)
+    const uint64_t nbs = wg_bs_blocks(n);
+    WG_ALLOC(c, c->bsum, 4 * (nbs + 64) * 4);
+    uint32_t *ebs = c->bsum.as<uint32_t>() + 3 * (nbs + 64);
+    c->edge_scan_pending = false;
     { const int _sr = wg_scan_reserve(c, n + 1); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "hash_join");
     // the table: built on the side stream already (joined below), or here —
@@ -399,14 +404,20 @@ int wg_stage_hash_join(wg_ctx *c) {
         if (side) WG_HIP(c, hipStreamWaitEvent(c->stream, c->ev_hash, 0));
         hipLaunchKernelGGL(k_probe_fix, dim3(g), dim3(T), 0, c->stream, c->d_oid, n, c->d_poff, c->d_poid,
                            (const unsigned long long *)table, cap - 1, dup, c->canon.as<uint32_t>(), c->prow.as<int32_t>(),
-                           c->edge_cnt.as<uint32_t>(), (const uint8_t *)c->rowmiss.as<uint8_t>(), c->bsum.as<uint32_t>(), L);
+                           c->edge_cnt.as<uint32_t>(), (const uint8_t *)c->rowmiss.as<uint8_t>(), ebs, L);
         c->lf_refs_done = lanes;
-        WgScanBs S;
-        S.na = 1;
-        S.in[0] = c->edge_cnt.as<const uint32_t>();
-        S.out[0] = c->edge_cnt.as<uint32_t>();
-        S.bsum[0] = c->bsum.as<const uint32_t>();
-        WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, c->stream));
+        if (c->spec && lanes) {
+            // r06: a speculative build's lane stage runs its offsets scan next
+            // (wg_lf_refs, no kernel between): this scan joins that launch
+            c->edge_scan_pending = true;
+        } else {
+            WgScanBs S;
+            S.na = 1;
+            S.in[0] = c->edge_cnt.as<const uint32_t>();
+            S.out[0] = c->edge_cnt.as<uint32_t>();
+            S.bsum[0] = ebs;
+            WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, c->stream));
+        }
         // read by wg_stage_edges after the lane stage's own synchronisation (a
         // speculative build reads it with its end-of-build validation)
         if (!c->spec)

@@ -516,6 +516,7 @@ struct wg_ctx {
     const uint32_t *replay_death = nullptr;    // the exact single-GPU replay's consumption times (replay_setup)
     bool lane_out_fused = false;
     bool lf_refs_done = false;     // the hash join's kernels did the lane stage's clear + reference pass (single GPU)
+    bool edge_scan_pending = false;   // (r06) a speculative build's edge-count scan rides on the lane stage's (wg_lf_refs)
     bool edges_pending = false;    // the edge list is written by the next full geometry pass (k_edges_rows)   // the lane kernel wrote lane_out / color_out (speculative fast path)
     bool force_general_lanes = false;   // WG_LANES=general (testing the general walk)
     ReplayRun spec_run;     // the speculative build's replay (its iteration count and flag words)

@@ -497,7 +497,7 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back, uint32_t *scal) {
     DevBuf &ch_fill = c->lf[LF_CHFILL];
     WG_ALLOC(c, ch_fill, (n + 2) * 4);
     const uint64_t nbs = wg_bs_blocks(n);
-    WG_ALLOC(c, c->bsum, 3 * (nbs + 64) * 4);
+    WG_ALLOC(c, c->bsum, 4 * (nbs + 64) * 4);   // (the edge counts' block sums at [3 (nbs + 64), ...), wg_stage_hash_join)
     { const int _sr = wg_scan_reserve(c, n + 2); if (_sr != WG_OK) return _sr; }
     wg_stage_begin(c, "lf_refs");
     if (c->lf_refs_done) {   // cleared by the hash join's place pass, references taken by its per-row probe
@@ -531,6 +531,11 @@ int wg_lf_refs(wg_ctx *c, const LfRange &R, bool read_back, uint32_t *scal) {
     S.in[0] = ev_off.as<const uint32_t>(); S.out[0] = ev_off.as<uint32_t>(); S.bsum[0] = bs;
     S.in[1] = aux_off.as<const uint32_t>(); S.out[1] = aux_off.as<uint32_t>(); S.bsum[1] = bs + nbs;
     S.in[2] = fpc.as<const uint32_t>(); S.out[2] = ch_off.as<uint32_t>(); S.bsum[2] = bs + 2 * nbs;
+    if (c->edge_scan_pending) {   // the hash join's edge-count scan, in the same launch (speculative build)
+        c->edge_scan_pending = false;
+        S.na = 4;
+        S.in[3] = c->edge_cnt.as<const uint32_t>(); S.out[3] = c->edge_cnt.as<uint32_t>(); S.bsum[3] = bs + 3 * (nbs + 64);
+    }
     WG_HIP(c, wg_scan_bs_u32(S, n, c->scan_tmp.p, s));
     // read back while the chain phase runs (wg_lf_refs_end); a speculative
     // build reads the same words with its end-of-build validation instead
