@@ -271,6 +271,13 @@ int         wg_synchronize(wg_ctx *ctx);
 /* WG_OPT_MATCH_THREADS: threads per 256-row workgroup of the search-match
  * kernel (wg_match_rows): 512 (default, 0) or 256.  Speed only. */
 #define WG_OPT_MATCH_THREADS 14
+/* WG_OPT_VTX_PLACE: when the vertex buffer grows to 1 GiB or more, this
+ * many candidate allocations (1..8, default 4; 0 or 1 = one; fewer when
+ * device memory is short) are timed with a store probe and the fastest kept
+ * (wg_vertex.hip vtx_alloc_placed: the emission's store rate follows the
+ * buffer's physical pages).  Setting it frees the vertex buffer (the last
+ * emission is dropped; the next one allocates afresh).  Speed only. */
+#define WG_OPT_VTX_PLACE 15
 int         wg_set_option(wg_ctx *ctx, int option, int64_t value);
 
 /* ---- layout (GraphLayout::build, :265-355) -------------------------------
@@ -314,6 +321,10 @@ int wg_copy_geometry(wg_ctx *ctx, const wg_geometry_host *dst);
 int wg_emit_vertices(wg_ctx *ctx, uint64_t row_begin, uint64_t row_end,
                      int64_t selected_row, const float *palette);
 int wg_vertex_summary_get(wg_ctx *ctx, wg_vertex_summary *out);
+/* The vertex buffer's last placement (WG_OPT_VTX_PLACE): candidates probed
+ * (0: plain allocation), the index kept, and each candidate's store-probe
+ * time in ms (probe_ms: 8 floats, may be NULL). */
+int wg_vertex_placement_get(wg_ctx *ctx, uint32_t *n_probed, uint32_t *kept, float *probe_ms);
 /* Copy vertices [first, first+count) of the last emission to host memory. */
 int wg_copy_vertices(wg_ctx *ctx, uint64_t first, uint64_t count, wg_vertex *dst);
 /* Per-row vertex offsets (row_end-row_begin+1 entries) to host memory. */

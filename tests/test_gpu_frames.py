@@ -181,3 +181,41 @@ def test_row_geometry_list_device_times_rewritten_in_place(engine):
         assert engine.geometry()["row_top"].tobytes() == o.row_geometry(d.band)["row_top"].tobytes()
     finally:
         o.close()
+
+
+def test_vertex_buffer_placement_probes_and_keeps_the_vertices(engine):
+    """WG_OPT_VTX_PLACE (wg_vertex.hip vtx_alloc_placed): a vertex buffer of
+    1 GiB or more is chosen from K probed candidates; the emission written
+    into it is the same, byte for byte, as into a plain allocation, and a
+    later emission that fits reuses the buffer without probing again."""
+    import ctypes
+    from wgraph import lib
+
+    def placement():
+        n, kept, ms = ctypes.c_uint32(), ctypes.c_uint32(), (ctypes.c_float * 8)()
+        engine._check(lib().wg_vertex_placement_get(engine._ctx, ctypes.byref(n), ctypes.byref(kept), ms))
+        return n.value, kept.value, list(ms)
+
+    d = synth.generate("wide16", 250000, seed=12)
+    engine.build(d)
+    engine.row_geometry(d.band)
+    try:
+        engine._check(lib().wg_set_option(engine._ctx, 15, 1))   # one plain allocation
+        engine.emit_vertices(0, d.n, selected=7)
+        s1 = engine.vertex_summary()
+        assert s1.n_vertices * 24 >= 1 << 30                      # past the placement threshold
+        assert placement()[0] == 0
+        engine._check(lib().wg_set_option(engine._ctx, 15, 3))   # frees the buffer: the next emission places it
+        engine.emit_vertices(0, d.n, selected=7)
+        s3 = engine.vertex_summary()
+        n, kept, ms = placement()
+        assert n == 3
+        assert kept < n and all(x > 0 for x in ms[:n]) and ms[kept] == min(ms[:n])
+        assert (s3.n_vertices, s3.checksum) == (s1.n_vertices, s1.checksum)
+        engine.emit_vertices(0, d.n, selected=7)                  # fits: no new placement
+        assert placement() == (n, kept, ms)
+        assert engine.vertex_summary().checksum == s1.checksum
+        with pytest.raises(Exception):
+            engine._check(lib().wg_set_option(engine._ctx, 15, 9))
+    finally:
+        engine._check(lib().wg_set_option(engine._ctx, 15, 4))   # the default

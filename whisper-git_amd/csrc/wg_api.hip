@@ -509,6 +509,14 @@ int wg_set_stream(wg_ctx *c, void *s) {
     return WG_OK;
 }
 
+int wg_vertex_placement_get(wg_ctx *c, uint32_t *n_probed, uint32_t *kept, float *probe_ms) {
+    if (!c) return WG_E_INVALID;
+    if (n_probed) *n_probed = c->vtx_place_n;
+    if (kept) *kept = c->vtx_place_pick;
+    if (probe_ms) for (int k = 0; k < 8; k++) probe_ms[k] = c->vtx_place_ms[k];
+    return WG_OK;
+}
+
 int wg_set_option(wg_ctx *c, int option, int64_t value) {
     if (!c) return WG_E_INVALID;
     switch (option) {
@@ -567,6 +575,14 @@ int wg_set_option(wg_ctx *c, int option, int64_t value) {
     case WG_OPT_SWEEP_REG:
         if (value < 0 || value > 512) return wg_fail(c, WG_E_INVALID, "sweep register capacity must be 0..512");
         c->sweep_reg_cap = (uint32_t)value;
+        return WG_OK;
+    case WG_OPT_VTX_PLACE:
+        if (value < 0 || value > 8) return wg_fail(c, WG_E_INVALID, "vertex placement candidates must be 0..8");
+        WG_SETTLE(c);
+        WG_HIP(c, hipStreamSynchronize(c->stream));
+        c->vtx.release();   // placed afresh by the next emission
+        c->have_vtx = false;
+        c->vtx_place = value ? (uint32_t)value : 1u;   // (0: one allocation, as 1)
         return WG_OK;
     default: return wg_fail(c, WG_E_INVALID, "unknown option %d", option);
     }

@@ -624,6 +624,9 @@ struct wg_ctx {
     uint64_t vtx_tiles_last = 0;   // tiles of the last emission (bounds the next one's early grid)
     uint32_t vtx_tile_last = 1024; // ... of this many vertices (wg_vertex.hip)
     uint32_t vtx_tile_opt = 0;     // WG_OPT_VTX_TILE: 0 auto, 1024 or 2048
+    uint32_t vtx_place = 4;        // WG_OPT_VTX_PLACE: vertex buffer candidates (wg_vertex.hip vtx_alloc_placed)
+    uint32_t vtx_place_n = 0, vtx_place_pick = 0;   // the last placement: candidates probed, the one kept
+    float    vtx_place_ms[8] = {};
     static constexpr uint64_t WG_VTX_BIG_VERTICES = 400000000ull;   // auto: 2048-vertex tiles past this many
     int64_t  selected = -1;
     DevBuf vtx_off;         // uint64 [rows+1]

@@ -461,6 +461,7 @@ __global__ void k_checksum(const uint32_t *__restrict__ w, uint64_t nwords, unsi
 }
 
 }  // namespace
+static int vtx_alloc_placed(wg_ctx *c, size_t bytes);   // the vertex buffer (WG_OPT_VTX_PLACE), below
 
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const uint64_t rows = re - rb;
@@ -642,7 +643,7 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     c->vtx_tiles_last = ntiles;
     if (!early || total > vcap || ntiles + 1 > tcap || ntiles > early_grid) {   // did not fit: size the buffers and launch again
         if (early) wg_stage_begin(c, "vtx_counts");
-        WG_ALLOC(c, c->vtx, total * sizeof(wg_vertex) + 64);
+        if (const int rc = vtx_alloc_placed(c, total * sizeof(wg_vertex) + 64)) return rc;
         WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
         prep(ntiles + 1, no_fetch);
         launch(total, ntiles, ntiles, 0, 0);
@@ -654,6 +655,89 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
         if (need2 > (g2 + 7) / 8 * 8) launch(vcap, need2, early_grid, 2, g1);   // part 2 short of tiles: again, whole
     }
     WG_HIP(c, hipGetLastError());
+    return WG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Vertex buffer placement (WG_OPT_VTX_PLACE).  The emission's store rate is a
+// property of the physical pages behind the vertex buffer: one 5.75 GB buffer
+// takes 0.81-0.83 ms or 0.92-0.94 ms per wide16 1M emission (7.0 or 6.1 TB/s),
+// fixed for the buffer's lifetime and changed only by reallocating it with
+// the same inputs (profiles/r06/r06ax_*; not clocks or power: r06at_*).  A buffer
+// of 1 GiB or more is therefore chosen from up to vtx_place candidates, each timed
+// with the emission's own store pattern (non-temporal 16-byte stores, one
+// contiguous block per workgroup), and the fastest is kept, the others freed
+// (r06ay: the probe's best of 4 picked buffers emitting in 0.819-0.855 ms where
+// plain allocations in the same process took 0.82-0.94).  Once per growth of
+// the buffer (1/16 headroom; ~20 ms for 6 GB), never per frame.
+// ---------------------------------------------------------------------------
+#define WG_PLACE_MIN_BYTES (1ull << 30)
+
+__global__ void __launch_bounds__(256) k_store_probe(v4f *__restrict__ out, uint64_t n4) {
+    const uint64_t per = (n4 + gridDim.x - 1) / gridDim.x;
+    const uint64_t b = (uint64_t)blockIdx.x * per, e = b + per < n4 ? b + per : n4;
+    const v4f z = {0.f, 0.f, 0.f, 0.f};
+    for (uint64_t i = b + threadIdx.x; i < e; i += blockDim.x) __builtin_nontemporal_store(z, out + i);
+}
+
+static int vtx_probe_ms(wg_ctx *c, void *p, size_t bytes, float *ms) {
+    hipEvent_t e0, e1;
+    WG_HIP(c, hipEventCreate(&e0));
+    WG_HIP(c, hipEventCreate(&e1));
+    const uint64_t n4 = bytes / sizeof(v4f);
+    *ms = 1e30f;
+    int rc = WG_OK;
+    for (int rep = 0; rep < 3 && rc == WG_OK; rep++) {   // best of 3 (the first also warms the pages' translations)
+        float t = 0.f;
+        hipError_t e = hipEventRecord(e0, c->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_store_probe, dim3(8192), dim3(256), 0, c->stream, reinterpret_cast<v4f *>(p), n4);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+        if (e != hipSuccess) rc = wg_fail(c, WG_E_HIP, "vertex placement probe: %s", hipGetErrorString(e));
+        else if (t < *ms) *ms = t;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
+}
+
+static int vtx_alloc_placed(wg_ctx *c, size_t bytes) {
+    const uint32_t k_max = std::min<uint32_t>(c->vtx_place, 8);
+    if (bytes <= c->vtx.cap && c->vtx.p) return WG_OK;
+    c->vtx_place_n = 0;
+    if (k_max <= 1 || bytes < WG_PLACE_MIN_BYTES) {
+        WG_ALLOC(c, c->vtx, bytes);
+        return WG_OK;
+    }
+    WG_HIP(c, hipStreamSynchronize(c->stream));
+    c->vtx.release();
+    DevBuf cand[8];
+    float best = 1e30f;
+    int ib = -1, rc = WG_OK;
+    for (uint32_t k = 0; k < k_max && rc == WG_OK; k++) {
+        if (k) {   // another candidate only with room for it beside the ones held
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes + bytes / 16 + (4ull << 30)) break;
+        }
+        if (cand[k].ensure(bytes) != hipSuccess) { (void)hipGetLastError(); break; }
+        float ms = 0.f;
+        rc = vtx_probe_ms(c, cand[k].p, cand[k].cap, &ms);
+        if (rc == WG_OK) {
+            c->vtx_place_ms[k] = ms;
+            c->vtx_place_n = k + 1;
+            if (ms < best) { best = ms; ib = (int)k; }
+        }
+    }
+    for (int k = 0; k < 8; k++) if (k != ib) cand[k].release();
+    if (rc != WG_OK) { if (ib >= 0) cand[ib].release(); return rc; }
+    if (ib < 0) { WG_ALLOC(c, c->vtx, bytes); return WG_OK; }
+    c->vtx.p = cand[ib].p;
+    c->vtx.cap = cand[ib].cap;
+    c->vtx_place_pick = (uint32_t)ib;
     return WG_OK;
 }
 

@@ -71,6 +71,7 @@ def lib():
             "wg_copy_geometry": ([vp, ctypes.POINTER(abi.GeometryHost)], ctypes.c_int),
             "wg_emit_vertices": ([vp, u64, u64, i64, vp], ctypes.c_int),
             "wg_vertex_summary_get": ([vp, ctypes.POINTER(abi.VertexSummary)], ctypes.c_int),
+            "wg_vertex_placement_get": ([vp, vp, vp, vp], ctypes.c_int),
             "wg_copy_vertices": ([vp, u64, u64, vp], ctypes.c_int),
             "wg_copy_vertex_offsets": ([vp, vp], ctypes.c_int),
             "wg_device_views_get": ([vp, ctypes.POINTER(abi.DeviceViews)], ctypes.c_int),
@@ -116,7 +117,7 @@ EXPORTED_SYMBOLS = (
     "wg_abi_version", "wg_create", "wg_destroy", "wg_last_error", "wg_set_stream", "wg_synchronize", "wg_set_option",
     "wg_layout_build", "wg_layout_summary_get", "wg_copy_lanes", "wg_copy_edges", "wg_copy_row_heights",
     "wg_compute_row_heights", "wg_row_geometry", "wg_row_geometry_list", "wg_layout_build_frame", "wg_geometry_summary_get", "wg_copy_geometry", "wg_emit_vertices",
-    "wg_vertex_summary_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
+    "wg_vertex_summary_get", "wg_vertex_placement_get", "wg_copy_vertices", "wg_copy_vertex_offsets", "wg_device_views_get",
     "wg_enable_timing", "wg_stage_timings", "wg_debug_counters", "wg_shard_build_begin", "wg_shard_build_frame_begin", "wg_shard_geometry_begin",
     "wg_shard_copy_msg", "wg_shard_msg_bytes", "wg_shard_pack_slot", "wg_shard_slot_heads", "wg_shard_exchange", "wg_font_atlas_build", "wg_font_atlas_info", "wg_copy_font_atlas",
     "wg_emit_glyphs", "wg_glyph_summary_get", "wg_copy_glyph_vertices", "wg_copy_glyph_offsets",
