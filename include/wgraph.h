@@ -274,7 +274,7 @@ int         wg_synchronize(wg_ctx *ctx);
 /* WG_OPT_VTX_PLACE: when the vertex buffer grows to 1 GiB or more, this
  * many candidate allocations (1..8, default 4; 0 or 1 = one; fewer when
  * device memory is short) are timed with a store probe and the fastest kept
- * (wg_vertex.hip vtx_alloc_placed: the emission's store rate follows the
+ * (wg_vertex.hip wg_alloc_placed: the emission's store rate follows the
  * buffer's physical pages).  Setting it frees the vertex buffer (the last
  * emission is dropped; the next one allocates afresh).  Speed only. */
 #define WG_OPT_VTX_PLACE 15

@@ -184,7 +184,7 @@ def test_row_geometry_list_device_times_rewritten_in_place(engine):
 
 
 def test_vertex_buffer_placement_probes_and_keeps_the_vertices(engine):
-    """WG_OPT_VTX_PLACE (wg_vertex.hip vtx_alloc_placed): a vertex buffer of
+    """WG_OPT_VTX_PLACE (wg_vertex.hip wg_alloc_placed): a vertex buffer of
     1 GiB or more is chosen from K probed candidates; the emission written
     into it is the same, byte for byte, as into a plain allocation, and a
     later emission that fits reuses the buffer without probing again."""

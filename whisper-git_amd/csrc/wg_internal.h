@@ -624,7 +624,7 @@ struct wg_ctx {
     uint64_t vtx_tiles_last = 0;   // tiles of the last emission (bounds the next one's early grid)
     uint32_t vtx_tile_last = 1024; // ... of this many vertices (wg_vertex.hip)
     uint32_t vtx_tile_opt = 0;     // WG_OPT_VTX_TILE: 0 auto, 1024 or 2048
-    uint32_t vtx_place = 4;        // WG_OPT_VTX_PLACE: vertex buffer candidates (wg_vertex.hip vtx_alloc_placed)
+    uint32_t vtx_place = 4;        // WG_OPT_VTX_PLACE: vertex buffer candidates (wg_vertex.hip wg_alloc_placed)
     uint32_t vtx_place_n = 0, vtx_place_pick = 0;   // the last placement: candidates probed, the one kept
     float    vtx_place_ms[8] = {};
     static constexpr uint64_t WG_VTX_BIG_VERTICES = 400000000ull;   // auto: 2048-vertex tiles past this many
@@ -933,5 +933,8 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel);  // wg_
 int wg_geom_lists(wg_ctx *c, uint64_t r0, uint64_t r1, int slice, hipStream_t s);
 int wg_geom_lists_flush(wg_ctx *c);
 int wg_vertex_checksum_run(wg_ctx *c, uint64_t *out);  // wg_vertex.hip
+// an output buffer of >= 1 GiB chosen from WG_OPT_VTX_PLACE probed candidates
+// (wg_vertex.hip); record: the vertex buffer's (wg_vertex_placement_get)
+int wg_alloc_placed(wg_ctx *c, DevBuf &buf, size_t bytes, bool record);
 int wg_words_checksum(wg_ctx *c, const uint32_t *w, uint64_t nwords, uint64_t *out);  // wg_vertex.hip
 void wg_init_height_thresholds(uint32_t *th);  // wg_rowtop.hip

@@ -461,7 +461,6 @@ __global__ void k_checksum(const uint32_t *__restrict__ w, uint64_t nwords, unsi
 }
 
 }  // namespace
-static int vtx_alloc_placed(wg_ctx *c, size_t bytes);   // the vertex buffer (WG_OPT_VTX_PLACE), below
 
 int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     const uint64_t rows = re - rb;
@@ -643,7 +642,7 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
     c->vtx_tiles_last = ntiles;
     if (!early || total > vcap || ntiles + 1 > tcap || ntiles > early_grid) {   // did not fit: size the buffers and launch again
         if (early) wg_stage_begin(c, "vtx_counts");
-        if (const int rc = vtx_alloc_placed(c, total * sizeof(wg_vertex) + 64)) return rc;
+        if (const int rc = wg_alloc_placed(c, c->vtx, total * sizeof(wg_vertex) + 64, true)) return rc;
         WG_ALLOC(c, c->tile_first, (ntiles + 1) * sizeof(uint4));
         prep(ntiles + 1, no_fetch);
         launch(total, ntiles, ntiles, 0, 0);
@@ -659,17 +658,21 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
 }
 
 // ---------------------------------------------------------------------------
-// Vertex buffer placement (WG_OPT_VTX_PLACE).  The emission's store rate is a
+// Output buffer placement (WG_OPT_VTX_PLACE): the vertex buffer (the glyph
+// quads' buffer measured no gain, r06bd: 1.253 against 1.248 ms).  The emission's store rate is a
 // property of the physical pages behind the vertex buffer: one 5.75 GB buffer
 // takes 0.81-0.83 ms or 0.92-0.94 ms per wide16 1M emission (7.0 or 6.1 TB/s),
 // fixed for the buffer's lifetime and changed only by reallocating it with
 // the same inputs (profiles/r06/r06ax_*; not clocks or power: r06at_*).  A buffer
 // of 1 GiB or more is therefore chosen from up to vtx_place candidates, each timed
 // with the emission's own store pattern (non-temporal 16-byte stores, one
-// contiguous block per workgroup), and the fastest is kept, the others freed
-// (r06ay: the probe's best of 4 picked buffers emitting in 0.819-0.855 ms where
-// plain allocations in the same process took 0.82-0.94).  Once per growth of
-// the buffer (1/16 headroom; ~20 ms for 6 GB), never per frame.
+// contiguous block per workgroup, one pass), and the fastest is kept, the
+// others freed (r06ay: the probe's best of 4 picked buffers emitting in
+// 0.819-0.855 ms where plain allocations in the same process took 0.82-0.94;
+// the first large allocation of a process landed on the slow pages on 5 of 6
+// boxes, r06at-bb).  The probe ranks candidates within a process only: its
+// absolute rate differs from box to box.  Once per growth of the buffer (1/16
+// headroom; ~5 ms for 4 x 6 GB on the first emission), never per frame.
 // ---------------------------------------------------------------------------
 #define WG_PLACE_MIN_BYTES (1ull << 30)
 
@@ -687,7 +690,7 @@ static int vtx_probe_ms(wg_ctx *c, void *p, size_t bytes, float *ms) {
     const uint64_t n4 = bytes / sizeof(v4f);
     *ms = 1e30f;
     int rc = WG_OK;
-    for (int rep = 0; rep < 3 && rc == WG_OK; rep++) {   // best of 3 (the first also warms the pages' translations)
+    for (int rep = 0; rep < 1 && rc == WG_OK; rep++) {   // one pass (r06ba: 3 passes cost the first emission 14 ms for 4 candidates)
         float t = 0.f;
         hipError_t e = hipEventRecord(e0, c->stream);
         if (e == hipSuccess) {
@@ -705,16 +708,16 @@ static int vtx_probe_ms(wg_ctx *c, void *p, size_t bytes, float *ms) {
     return rc;
 }
 
-static int vtx_alloc_placed(wg_ctx *c, size_t bytes) {
+int wg_alloc_placed(wg_ctx *c, DevBuf &buf, size_t bytes, bool record) {
     const uint32_t k_max = std::min<uint32_t>(c->vtx_place, 8);
-    if (bytes <= c->vtx.cap && c->vtx.p) return WG_OK;
-    c->vtx_place_n = 0;
+    if (bytes <= buf.cap && buf.p) return WG_OK;
+    if (record) c->vtx_place_n = 0;
     if (k_max <= 1 || bytes < WG_PLACE_MIN_BYTES) {
-        WG_ALLOC(c, c->vtx, bytes);
+        WG_ALLOC(c, buf, bytes);
         return WG_OK;
     }
     WG_HIP(c, hipStreamSynchronize(c->stream));
-    c->vtx.release();
+    buf.release();
     DevBuf cand[8];
     float best = 1e30f;
     int ib = -1, rc = WG_OK;
@@ -727,17 +730,19 @@ static int vtx_alloc_placed(wg_ctx *c, size_t bytes) {
         float ms = 0.f;
         rc = vtx_probe_ms(c, cand[k].p, cand[k].cap, &ms);
         if (rc == WG_OK) {
-            c->vtx_place_ms[k] = ms;
-            c->vtx_place_n = k + 1;
+            if (record) {
+                c->vtx_place_ms[k] = ms;
+                c->vtx_place_n = k + 1;
+            }
             if (ms < best) { best = ms; ib = (int)k; }
         }
     }
     for (int k = 0; k < 8; k++) if (k != ib) cand[k].release();
     if (rc != WG_OK) { if (ib >= 0) cand[ib].release(); return rc; }
-    if (ib < 0) { WG_ALLOC(c, c->vtx, bytes); return WG_OK; }
-    c->vtx.p = cand[ib].p;
-    c->vtx.cap = cand[ib].cap;
-    c->vtx_place_pick = (uint32_t)ib;
+    if (ib < 0) { WG_ALLOC(c, buf, bytes); return WG_OK; }
+    buf.p = cand[ib].p;
+    buf.cap = cand[ib].cap;
+    if (record) c->vtx_place_pick = (uint32_t)ib;
     return WG_OK;
 }
 
