@@ -490,10 +490,18 @@ def build_lifecycle(dag, dev, torch, args, pal):
 
 
 def pmc_traffic(args, workload):
-    """Latest profiles/<tag>_pmc.json collected on this exact workload (or None)."""
+    """Latest profiles/<tag>_pmc.json collected on this exact workload (or None).
+    Tags run r<round><a..z, aa..az, ba..>: ordered by round, then suffix length,
+    then suffix (so r06o < r06af < r06bf)."""
     import glob
+    import re
+
+    def order(f):
+        m = re.match(r"r(\d+)([a-z]*)_pmc\.json$", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, os.path.basename(f))
+
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=order):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
