@@ -724,6 +724,13 @@ def main():
         torch.cuda.synchronize()
         host_rate = rows_total * 3 / (time.perf_counter() - t1)
 
+    # the vertex buffer's placement (WG_OPT_VTX_PLACE): read
+    # before the side measurements, which emit other lists into the buffer
+    import ctypes
+    pn, pk, pms = ctypes.c_uint32(), ctypes.c_uint32(), (ctypes.c_float * 8)()
+    eng._check(wgraph.lib().wg_vertex_placement_get(eng._ctx, ctypes.byref(pn), ctypes.byref(pk), pms))
+    placement = {"candidates_probed": pn.value, "kept": pk.value, "probe_ms": [round(x, 4) for x in pms[:pn.value]]}
+
     extras = {}
     if rank == 0 and world == 1 and not args.no_extras:
         extras = extra_measurements(eng, dag, dev, torch, shard0, shard1, args, log)
@@ -749,7 +756,8 @@ def main():
                           "rows_total": rows_total, "rows_per_gpu": args.rows_per_gpu,
                           "vertices_per_gpu": int(vs.n_vertices), "parallelism": f"row-shard x{world}"},
                "stages_ms": stages, "host_input_rows_per_s": None if host_rate is None else round(host_rate, 1),
-               "roofline": roofline, "cpu_baseline": cpu, "cpu_baseline_threads": cpu_mt, "host_cpu": host_cpu(),
+               "roofline": roofline, "vtx_placement": placement,
+               "cpu_baseline": cpu, "cpu_baseline_threads": cpu_mt, "host_cpu": host_cpu(),
                **extras}
         if exchange is not None:
             out["seam_exchange"] = exchange

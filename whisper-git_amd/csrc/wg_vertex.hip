@@ -665,8 +665,10 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
 // fixed for the buffer's lifetime and changed only by reallocating it with
 // the same inputs (profiles/r06/r06ax_*; not clocks or power: r06at_*).  A buffer
 // of 1 GiB or more is therefore chosen from up to vtx_place candidates, each timed
-// with the emission's own store pattern (non-temporal 16-byte stores, one
-// contiguous block per workgroup, one pass), and the fastest is kept, the
+// with the emission's own store pattern (non-temporal 16-byte stores in 24 KiB
+// tiles taken grid-stride, one pass; r06bk-bm: fast candidates 0.90-0.96 ms,
+// slow 1.09-1.18 for 6.1 GB — twice the separation of a first probe that gave
+// each workgroup one contiguous block), and the fastest is kept, the
 // others freed (r06ay: the probe's best of 4 picked buffers emitting in
 // 0.819-0.855 ms where plain allocations in the same process took 0.82-0.94;
 // the first large allocation of a process landed on the slow pages on 5 of 6
@@ -676,11 +678,16 @@ int wg_stage_vertices(wg_ctx *c, uint64_t rb, uint64_t re, int64_t sel) {
 // ---------------------------------------------------------------------------
 #define WG_PLACE_MIN_BYTES (1ull << 30)
 
+// 24 KiB tiles (the emission's tile of 1024 vertices), taken grid-stride by
+// the workgroups, 16-byte non-temporal stores
+constexpr uint32_t PROBE_TILE4 = 1536;
 __global__ void __launch_bounds__(256) k_store_probe(v4f *__restrict__ out, uint64_t n4) {
-    const uint64_t per = (n4 + gridDim.x - 1) / gridDim.x;
-    const uint64_t b = (uint64_t)blockIdx.x * per, e = b + per < n4 ? b + per : n4;
     const v4f z = {0.f, 0.f, 0.f, 0.f};
-    for (uint64_t i = b + threadIdx.x; i < e; i += blockDim.x) __builtin_nontemporal_store(z, out + i);
+    const uint64_t ntile = (n4 + PROBE_TILE4 - 1) / PROBE_TILE4;
+    for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+        const uint64_t b = t * PROBE_TILE4, e = b + PROBE_TILE4 < n4 ? b + PROBE_TILE4 : n4;
+        for (uint64_t i = b + threadIdx.x; i < e; i += 256) __builtin_nontemporal_store(z, out + i);
+    }
 }
 
 static int vtx_probe_ms(wg_ctx *c, void *p, size_t bytes, float *ms) {
@@ -694,7 +701,7 @@ static int vtx_probe_ms(wg_ctx *c, void *p, size_t bytes, float *ms) {
         float t = 0.f;
         hipError_t e = hipEventRecord(e0, c->stream);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_store_probe, dim3(8192), dim3(256), 0, c->stream, reinterpret_cast<v4f *>(p), n4);
+            hipLaunchKernelGGL(k_store_probe, dim3(4096), dim3(256), 0, c->stream, reinterpret_cast<v4f *>(p), n4);
             e = hipGetLastError();
         }
         if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
